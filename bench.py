@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Episodes/s of the CWT inference episode (BASELINE.json metric, config #2: PASCAL-shaped
+split-0 1-shot ResNet-50, 473x473, batch_size_val = 1, adapt_iter 200, heads 4) on MI355X.
+
+A step = one full episode (test.py:138-219): feature extraction of support + query, the
+200-step inner loop, normalize + CWT + classifier, upsample/argmax/IoU/CE for pred_q and
+pred_q0.  Inputs (images, labels, W0) are resident in HBM before the timed region.
+N GPUs = N independent replicas, episodes sharded by rank (weak scaling, no data-path
+collective).
+
+    python bench.py [--gpus N --steps K --warmup W] [--shot 5] [--layers 101 --size 641]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+PEAK_HBM_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cfg, sd, tsd, budget_s: float = 25.0, max_eps: int = 4):
+    """The oracle (CPU restatement of the reference path) on the host cores, bounded sample."""
+    from few_shot_seg_cwt_amd import synthetic as syn
+    from oracle import cwt_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sdt, tsdt = O.to_torch_state(sd), O.to_torch_state(tsd)
+    eps = [syn.make_episode(2021, 100 + i, cfg["image_size"], cfg["shot"]) for i in range(max_eps + 1)]
+    W0 = torch.from_numpy(syn.normal(2021, "cpuW0", (2, 512, 1, 1), 0.04))
+    O.run_inference_episode(eps[0], sdt, tsdt, W0, cfg)   # warm-up
+    t0 = time.time()
+    n = 0
+    for ep in eps[1:]:
+        O.run_inference_episode(ep, sdt, tsdt, W0, cfg)
+        n += 1
+        if time.time() - t0 > budget_s:
+            break
+    dt = time.time() - t0
+    return {"value": n / dt, "unit": "episodes/s", "cores": threads, "kind": "port",
+            "sample": f"{n} episodes (after 1 warm-up) of the same workload through oracle/cwt_oracle.py "
+                      f"run_inference_episode (torch CPU fp32, {threads} threads); s/episode {dt / n:.2f}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--shot", type=int, default=1)
+    ap.add_argument("--layers", type=int, default=50)
+    ap.add_argument("--size", type=int, default=473)
+    ap.add_argument("--pool", type=int, default=4, help="distinct resident episodes cycled through")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-json", default=None, help="write per-launch records here (rank 0)")
+    args = ap.parse_args()
+
+    from few_shot_seg_cwt_amd import dist as cdist
+    rank, local, world = cdist.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib, get_model
+    from few_shot_seg_cwt_amd import synthetic as syn
+    from few_shot_seg_cwt_amd.episode import EpisodeEngine
+
+    _lib.load_library()
+    S, shot, layers = args.size, args.shot, args.layers
+    cfg = syn.cfg_defaults(image_size=S, shot=shot, layers=layers)
+    seed = 2021
+    sd = syn.make_pspnet_state(layers, seed)
+    tsd = syn.make_transformer_state(4, 512, seed)
+    model = get_model(cfg)
+    model.load_state_dict(sd)
+    trans = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    trans.load_state_dict(tsd)
+    engine = EpisodeEngine(model, trans, cfg)
+
+    # resident inputs: a pool of distinct episodes per rank + one W0 buffer per step
+    classes = syn.coco_val_classes(0) if layers == 101 else None
+    pool = []
+    for i in range(args.pool):
+        ep = syn.make_episode(seed, rank * 1000 + i, S, shot, classes)
+        imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
+        pool.append((imgs, torch.from_numpy(ep["s_label"][0]).to(dev), torch.from_numpy(ep["q_label"]).to(dev)))
+    g = torch.Generator().manual_seed(seed + rank)
+    nW = args.warmup + args.steps
+    bound = 1.0 / np.sqrt(512)
+    W0 = ((torch.rand((nW, 2, 512), generator=g) * 2 - 1) * bound).to(dev)
+    torch.cuda.synchronize()
+
+    for s in range(args.warmup):
+        imgs, sl, ql = pool[s % len(pool)]
+        engine.run(imgs, sl, ql, W0[s])
+    torch.cuda.synchronize()
+
+    _lib.profile_enable(True)
+    cdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    iu = torch.zeros((3, 2), device=dev)
+    for s in range(args.steps):
+        imgs, sl, ql = pool[s % len(pool)]
+        r = engine.run(imgs, sl, ql, W0[args.warmup + s])
+        iu += r["iut"][0]
+    torch.cuda.synchronize()
+    cdist.barrier()
+    t1 = time.perf_counter()
+    _lib.profile_enable(False)
+    dt = cdist.all_reduce_max_scalar(t1 - t0)
+    value = world * args.steps / dt
+
+    recs = _lib.profile_records()
+    # per-launch records -> per-kernel aggregates
+    agg = {}
+    for name, fl, by, ms in recs:
+        key = name.split(" ")[0]
+        a = agg.setdefault(key, [0, 0.0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += fl
+        a[2] += by
+        a[3] += ms
+    conv = [(n, fl, by, ms) for n, fl, by, ms in recs if n.startswith("conv_igemm")]
+    conv_fl = sum(r[1] for r in conv)
+    conv_ms = sum(r[3] for r in conv)
+    extract_ms = sum(r[3] for r in recs if not (r[0].startswith("inner_adapt") or r[0].startswith("attention")))
+    adapt_ms = sum(r[3] for r in recs if r[0].startswith("inner_adapt"))
+    attn_ms = sum(r[3] for r in recs if r[0].startswith("attention"))
+    # dominant kernel = the kernel symbol with the largest total time among the conv launches
+    conv_keys = {k: v for k, v in agg.items() if k.startswith("conv_igemm")}
+    dom = max(conv_keys, key=lambda k: conv_keys[k][3])
+    dn, dfl, dby, dms = conv_keys[dom]
+    achieved = (dfl / dn) / (dms / dn * 1e-3) / 1e12
+
+    out = {
+        "metric": "episodes/sec (473x473, 1-shot, R50) at 1/2/4/8 MI355X; mIoU vs ref"
+        if (S, shot, layers) == (473, 1, 50) else f"episodes/sec ({S}x{S}, {shot}-shot, R{layers})",
+        "value": round(value, 3),
+        "unit": "episodes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (PRNG weights + PASCAL-shaped episodes, few_shot_seg_cwt_amd/synthetic.py)",
+        "config": {"workload": f"CWT inference episode (validate_transformer, batch_size_val=1): "
+                               f"{'PASCAL split-0' if layers == 50 else 'COCO-20i split-0'} {shot}-shot "
+                               f"ResNet-{layers} PSPNet {S}x{S}, adapt_iter 200, heads 4",
+                   "image_size": S, "shot": shot, "layers": layers, "episodes_per_step_per_gpu": 1,
+                   "parallelism": f"{world} episode-sharded replicas"},
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                     "launches_per_step": dn // args.steps, "flops_per_launch": dfl / dn,
+                     "avg_launch_ms": round(dms / dn, 4)},
+        "conv_stack": {"tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2),
+                       "frac": round(conv_fl / (conv_ms * 1e-3) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4),
+                       "gflop_per_step": round(conv_fl / args.steps / 1e9, 1),
+                       "ms_per_step": round(conv_ms / args.steps, 3)},
+        "phases_ms_per_step": {"extract": round(extract_ms / args.steps, 3), "inner_adapt": round(adapt_ms / args.steps, 3),
+                               "attention": round(attn_ms / args.steps, 3)},
+        "iou_fg_timed": round(float((iu[0, 1] / iu[1, 1].clamp_min(1)).item()), 4),
+    }
+    if rank == 0 and args.profile_json:
+        with open(args.profile_json, "w") as f:
+            json.dump({"records": recs, "aggregate": agg}, f, indent=1)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, sd, tsd)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,134 @@
+"""ctypes binding of libcwt.so (include/cwt.h).
+
+The product path has no CPU fallback: if the library is missing or no GPU is visible,
+every call raises.  cffi is not installed in this image, so the binding uses ctypes;
+the ABI is plain C and equally bindable from cffi.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcwt.so")
+
+_P = C.c_void_p
+_I = C.c_int
+_F = C.c_float
+_I64 = C.c_int64
+
+# name -> (restype, argtypes); must match include/cwt.h exactly (tests check every symbol)
+SIGNATURES = {
+    "cwt_version": (C.c_char_p, []),
+    "cwt_last_error": (C.c_char_p, []),
+    "cwt_ctx_create": (_I, [_I, C.POINTER(_P)]),
+    "cwt_ctx_destroy": (_I, [_P]),
+    "cwt_backbone_load": (_I, [_P, _I, _I, C.POINTER(C.c_char_p), C.POINTER(_P), C.POINTER(_I64), _F]),
+    "cwt_extract_features": (_I, [_P, _P, _I, _I, _P, _P]),
+    "cwt_workspace_bytes": (C.c_size_t, [_P]),
+    "cwt_inner_adapt": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
+    "cwt_normalize": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
+    "cwt_attention_fwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cwt_attention_saved_floats": (C.c_size_t, [_I, _I, _I, _I]),
+    "cwt_attention_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cwt_classify": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
+    "cwt_seg_metrics": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "cwt_seg_ce_fwd_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "cwt_classify_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
+    "cwt_iou_preds": (_I, [_P, _P, _P, _I64, _I, _I, _P, _P]),
+    "cwt_sgd_step": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _I, _I, _P]),
+    "cwt_profile_enable": (_I, [_P, _I]),
+    "cwt_profile_count": (_I, [_P]),
+    "cwt_profile_record": (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                C.POINTER(_F)]),
+}
+
+_lib = None
+_lock = threading.Lock()
+_ctx = {}
+
+
+class CwtError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libcwt.so and declare every prototype (works without a GPU)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise CwtError(f"{path} not built: run `python -m few_shot_seg_cwt_amd.build` "
+                               "(the product path has no CPU fallback)")
+            lib = C.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def lib():
+    return load_library()
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().cwt_last_error().decode(errors="replace")
+        raise CwtError(f"{what} failed (code {rc}): {msg}")
+
+
+def ctx(device: int | None = None):
+    """Per-device context (one per process per device)."""
+    if not torch.cuda.is_available():
+        raise CwtError("libcwt needs a HIP device (torch.cuda.is_available() is False); no CPU fallback")
+    if device is None:
+        device = torch.cuda.current_device()
+    with _lock:
+        if device not in _ctx:
+            p = C.c_void_p()
+            rc = load_library().cwt_ctx_create(device, C.byref(p))
+            if rc != 0:
+                raise CwtError(f"cwt_ctx_create failed: {_lib.cwt_last_error().decode()}")
+            _ctx[device] = p
+        return _ctx[device]
+
+
+def stream_ptr(device=None) -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t: torch.Tensor | None) -> C.c_void_p | None:
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def require(t: torch.Tensor, name: str, dtype=torch.float32, device=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise CwtError(f"{name} must be a device tensor (no CPU fallback)")
+    return t
+
+
+def profile_enable(on: bool, device=None):
+    check(lib().cwt_profile_enable(ctx(device), int(on)), "cwt_profile_enable")
+
+
+def profile_records(device=None):
+    """[(name, flops, bytes, ms)] of the launches recorded since profile_enable(True)."""
+    c = ctx(device)
+    out = []
+    buf = C.create_string_buffer(256)
+    fl, by, ms = C.c_double(), C.c_double(), C.c_float()
+    for i in range(lib().cwt_profile_count(c)):
+        check(lib().cwt_profile_record(c, i, buf, 256, C.byref(fl), C.byref(by), C.byref(ms)), "cwt_profile_record")
+        out.append((buf.value.decode(), fl.value, by.value, ms.value))
+    return out

@@ -1,0 +1,374 @@
+// Support-set inner loop (reference test.py:164-187, train.py:206-231).
+//
+// Per SGD step the reference launches ~10 kernels (1x1 conv, bilinear upsample to S x S,
+// log-softmax, weighted NLL, and the three backwards) and materialises four S x S x 2
+// fp32 tensors.  Here one kernel does the whole step:
+//   z      = W . f_s                       at low resolution, per tile (+1-pixel halo)
+//   z_hi   = bilinear(align_corners) (z)   per high-res pixel, never stored
+//   g_hi   = w_y (softmax(z_hi) - onehot)  weighted CE gradient (the 1/sum(w) is folded
+//                                          into the learning rate)
+//   g_lo   = U^T g_hi                      adjoint of the upsample, accumulated in LDS
+//   dW    += g_lo . f_s^T                  f_s tile already in registers from the z pass
+// Workgroup = (lo-res row pair r, 16-column block, shot).  With two classes the gradient
+// of class 0 is exactly minus that of class 1 (softmax sums to one, so does the one-hot),
+// so only dW[1] is reduced: one 2 KB fp32 atomic add per workgroup into acc[s % 3].
+// The next step's kernel applies W <- W - lr/sum(w) * dW on the fly, so a step is one
+// launch; three accumulator slots let step s zero slot s+1 without a race.
+// f_s (7.4 MB per shot at 60x60x512) is re-read every step from L2 / Infinity Cache.
+#include "common.h"
+#include "kernels.h"
+
+namespace cwt {
+
+struct AdaptScalars {
+  unsigned long long nbg, nfg;  // label counts (class 0 / class 1)
+  float wfg;                    // CE class weight of class 1
+  float lr_eff;                 // lr / sum_p w_{y_p}
+};
+
+__global__ void adapt_prep_kernel(const int64_t* __restrict__ lbl, long total, uint8_t* __restrict__ out,
+                                  AdaptScalars* sc) {
+  unsigned long long nb = 0, nf = 0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int64_t v = lbl[i];
+    out[i] = (uint8_t)(v == 0 ? 0 : (v == 1 ? 1 : 255));
+    nb += (v == 0);
+    nf += (v == 1);
+  }
+  // wave reduce then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) {
+    nb += __shfl_xor(nb, o, 64);
+    nf += __shfl_xor(nf, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&sc->nbg, nb);
+    atomicAdd(&sc->nfg, nf);
+  }
+}
+
+// mode 0: weight = [1, nbg/nfg]        (test.py:169-175, train.py:211-217)
+// mode 1: weight = [1, nbg/(nfg+1e-12)] (train.py:237-243, query loss)
+__global__ void adapt_scalars_kernel(AdaptScalars* sc, float lr, int mode) {
+  double nb = (double)sc->nbg, nf = (double)sc->nfg;
+  double r = (mode == 0) ? nb / nf : nb / (nf + 1e-12);
+  float wfg = (float)r;  // torch.tensor([1.0, r]) -> float32
+  sc->wfg = wfg;
+  double sumw = nb + nf * (double)wfg;
+  sc->lr_eff = (float)((double)lr / sumw);
+}
+
+constexpr int ADAPT_CB = 16;           // lo-res columns per workgroup
+constexpr int ADAPT_NP = 2 * (ADAPT_CB + 1);
+constexpr int ADAPT_PPW = (ADAPT_NP + 3) / 4;  // lo pixels per wave
+
+struct AdaptStepArgs {
+  const float* f;        // NHWC [n][h][w][512]
+  const uint8_t* lbl;    // [n][S][S]
+  const AdaptScalars* sc;
+  const float* w_src;    // W before the previous update ([2][512]); for step 0 the initial W
+  const float* acc_prev; // dW[1] of the previous step, or null at step 0
+  float* w_dst;          // block (0,0,0) stores the current W here (may be null)
+  float* acc_cur;        // dW[1] accumulator of this step (zeroed)
+  float* acc_zero;       // slot to zero for the next step (may be null)
+  int h, w, S;
+  float sy, sx;          // align_corners scales (h-1)/(S-1), (w-1)/(S-1)
+};
+
+// Accumulate the weighted-CE gradient of high-res pixels of this tile into gs[ri][xi]
+// (class-1 component; class 0 is its negative).  z[ri][xi][2] low-res logits in LDS.
+// Returns this thread's sum of w_y * nll (used by the query loss).
+template <bool WITH_LOSS>
+__device__ __forceinline__ float hires_tile_grad(const float (*z)[ADAPT_CB + 1][2], float (*gs)[ADAPT_CB + 1],
+                                                 const uint8_t* __restrict__ lbl, int S, int h, int w, int r,
+                                                 int cb, int ncb, float sy, float sx, float wfg) {
+  const int t = threadIdx.x;
+  const int rg = t >> 7;
+  const int x_begin = cb * 8 * ADAPT_CB;
+  const int x_end = (cb == ncb - 1) ? S : min(S - 1, x_begin + 8 * ADAPT_CB);
+  const int ylo = 8 * r + 4 * rg;
+  const int yhi = (r == h - 2 && rg == 1) ? S : ylo + 4;  // last pair also owns row S-1
+  float loss = 0.f;
+  for (int X = x_begin + (t & 127); X < x_end; X += 128) {
+    Lerp lx = lerp_coord(X, w, sx);
+    const int xi0 = lx.i0 - cb * ADAPT_CB, xi1 = lx.i1 - cb * ADAPT_CB;
+    float a00 = 0.f, a01 = 0.f, a10 = 0.f, a11 = 0.f;  // [row of i0/i1][x0/x1]
+    float b0 = 0.f, b1 = 0.f;                          // contributions when i0 == i1 == r+1
+    for (int Y = ylo; Y < yhi; ++Y) {
+      const int y = lbl[(long)Y * S + X];
+      if (y == 255) continue;
+      Lerp ly = lerp_coord(Y, h, sy);
+      const int ri0 = ly.i0 - r, ri1 = ly.i1 - r;
+      float l0 = ly.l0 * (lx.l0 * z[ri0][xi0][0] + lx.l1 * z[ri0][xi1][0]) +
+                 ly.l1 * (lx.l0 * z[ri1][xi0][0] + lx.l1 * z[ri1][xi1][0]);
+      float l1 = ly.l0 * (lx.l0 * z[ri0][xi0][1] + lx.l1 * z[ri0][xi1][1]) +
+                 ly.l1 * (lx.l0 * z[ri1][xi0][1] + lx.l1 * z[ri1][xi1][1]);
+      const float d = l1 - l0;
+      const float p1 = 1.f / (1.f + __expf(-d));
+      const float wy = (y == 1) ? wfg : 1.f;
+      const float g = wy * (p1 - (float)y);
+      if (WITH_LOSS) {
+        // nll = logsumexp(l) - l_y, computed stably
+        const float m = fmaxf(l0, l1);
+        const float lse = m + __logf(__expf(l0 - m) + __expf(l1 - m));
+        loss += wy * (lse - (y == 1 ? l1 : l0));
+      }
+      if (ri0 == 0) {
+        a00 += ly.l0 * lx.l0 * g;
+        a01 += ly.l0 * lx.l1 * g;
+        a10 += ly.l1 * lx.l0 * g;
+        a11 += ly.l1 * lx.l1 * g;
+      } else {  // Y = S-1: only row r+1 with weight 1
+        b0 += lx.l0 * g;
+        b1 += lx.l1 * g;
+      }
+    }
+    atomicAdd(&gs[0][xi0], a00);
+    atomicAdd(&gs[0][xi1], a01);
+    atomicAdd(&gs[1][xi0], a10 + b0);
+    atomicAdd(&gs[1][xi1], a11 + b1);
+  }
+  return loss;
+}
+
+__global__ __launch_bounds__(256) void adapt_step_kernel(AdaptStepArgs a) {
+  constexpr int C = 512;
+  __shared__ float z[2][ADAPT_CB + 1][2];
+  __shared__ float gs[2][ADAPT_CB + 1];
+  __shared__ float red[4][C];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int cb = blockIdx.x, r = blockIdx.y, n = blockIdx.z;
+  const int ncb = gridDim.x;
+  const AdaptScalars sc = *a.sc;
+
+  // current weights for this lane's 8 channels
+  float w0[8], w1[8];
+  {
+    const float* s0 = a.w_src + lane * 8;
+    const float* s1 = a.w_src + C + lane * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      w0[q] = s0[q];
+      w1[q] = s1[q];
+    }
+    if (a.acc_prev) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float d = a.acc_prev[lane * 8 + q];
+        w1[q] -= sc.lr_eff * d;
+        w0[q] += sc.lr_eff * d;
+      }
+    }
+  }
+  const bool leader = (cb | r | n) == 0;
+  if (leader && wv == 0 && a.w_dst) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      a.w_dst[lane * 8 + q] = w0[q];
+      a.w_dst[C + lane * 8 + q] = w1[q];
+    }
+  }
+  if (leader && a.acc_zero) {
+    for (int i = t; i < C; i += 256) a.acc_zero[i] = 0.f;
+  }
+  if (t < 2 * (ADAPT_CB + 1)) (&gs[0][0])[t] = 0.f;
+
+  // ---- z = W . f for the tile's low-res pixels (rows r, r+1; cols cb*16 .. +16) ----
+  const int x0 = cb * ADAPT_CB;
+  const int ncol = min(ADAPT_CB + 1, a.w - x0);
+  const float* fimg = a.f + (long)n * a.h * a.w * C;
+  float fv[ADAPT_PPW][8];
+#pragma unroll
+  for (int j = 0; j < ADAPT_PPW; ++j) {
+    const int p = wv + 4 * j;
+    const int ri = p / (ADAPT_CB + 1), xi = p % (ADAPT_CB + 1);
+    const bool valid = p < ADAPT_NP && xi < ncol;
+    if (valid) {
+      const float* src = fimg + ((long)(r + ri) * a.w + x0 + xi) * C + lane * 8;
+      f32x4 u = *(const f32x4*)src, v = *(const f32x4*)(src + 4);
+      fv[j][0] = u[0]; fv[j][1] = u[1]; fv[j][2] = u[2]; fv[j][3] = u[3];
+      fv[j][4] = v[0]; fv[j][5] = v[1]; fv[j][6] = v[2]; fv[j][7] = v[3];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) fv[j][q] = 0.f;
+    }
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      s0 = fmaf(w0[q], fv[j][q], s0);
+      s1 = fmaf(w1[q], fv[j][q], s1);
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (valid && lane == 0) {
+      z[ri][xi][0] = s0;
+      z[ri][xi][1] = s1;
+    }
+  }
+  __syncthreads();
+
+  hires_tile_grad<false>(z, gs, a.lbl + (long)n * a.S * a.S, a.S, a.h, a.w, r, cb, ncb, a.sy, a.sx, sc.wfg);
+  __syncthreads();
+
+  // ---- dW[1] partial = sum_p g[p] f[p] over the tile, reduced over waves, one atomic set ----
+  float d[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) d[q] = 0.f;
+#pragma unroll
+  for (int j = 0; j < ADAPT_PPW; ++j) {
+    const int p = wv + 4 * j;
+    if (p < ADAPT_NP) {
+      const float g = gs[p / (ADAPT_CB + 1)][p % (ADAPT_CB + 1)];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) d[q] = fmaf(g, fv[j][q], d[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[wv][lane * 8 + q] = d[q];
+  __syncthreads();
+  for (int k = t; k < C; k += 256) {
+    const float s = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+    atomicAdd(&a.acc_cur[k], s);
+  }
+}
+
+__global__ void adapt_final_kernel(const float* w_src, const float* acc, const AdaptScalars* sc, float* w_out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= 512) return;
+  const float lr = sc->lr_eff;
+  float d = acc ? acc[k] : 0.f;
+  w_out[k] = w_src[k] + lr * d;
+  w_out[512 + k] = w_src[512 + k] - lr * d;
+}
+
+int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int S, float lr, int iters, float* W,
+                 uint8_t* lbl_ws, AdaptScalars* sc, float* acc3 /*[3][512]*/, float* wbuf /*[2][2][512]*/,
+                 hipStream_t st) {
+  const long total = (long)n * S * S;
+  CWT_HIP(hipMemsetAsync(sc, 0, sizeof(AdaptScalars), st));
+  int pblocks = (int)std::min<long>(1024, cdiv(total, 256));
+  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(256), 0, st, lbl64, total, lbl_ws, sc);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(adapt_scalars_kernel, dim3(1), dim3(1), 0, st, sc, lr, 0);
+  CWT_LAUNCH_CHECK();
+  if (iters <= 0) return 0;
+  CWT_HIP(hipMemsetAsync(acc3, 0, sizeof(float) * 512, st));
+  AdaptStepArgs a;
+  a.f = f;
+  a.lbl = lbl_ws;
+  a.sc = sc;
+  a.h = h;
+  a.w = w;
+  a.S = S;
+  a.sy = align_corners_scale(h, S);
+  a.sx = align_corners_scale(w, S);
+  const int ncb = cdiv(S - 1, 8 * ADAPT_CB);
+  dim3 grid(ncb, h - 1, n);
+  for (int s = 0; s < iters; ++s) {
+    a.w_src = (s == 0) ? W : wbuf + ((s - 1) & 1) * 1024;
+    a.acc_prev = (s == 0) ? nullptr : acc3 + ((s - 1) % 3) * 512;
+    a.w_dst = wbuf + (s & 1) * 1024;
+    a.acc_cur = acc3 + (s % 3) * 512;
+    a.acc_zero = acc3 + ((s + 1) % 3) * 512;
+    hipLaunchKernelGGL(adapt_step_kernel, grid, dim3(256), 0, st, a);
+    CWT_LAUNCH_CHECK();
+  }
+  const int last = iters - 1;
+  hipLaunchKernelGGL(adapt_final_kernel, dim3(2), dim3(256), 0, st, (const float*)(wbuf + (last & 1) * 1024),
+                     (const float*)(acc3 + (last % 3) * 512), (const AdaptScalars*)sc, W);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Outer-loop query CE (train.py:237-243,261-265) on precomputed low-res logits:
+// loss = sum w_y nll / sum w_y, dlogits = U^T (w_y (p - onehot)) / sum w_y.
+// Same tiling as the inner-loop step; logits read from memory instead of W . f.
+// ---------------------------------------------------------------------------------------
+struct SegCEArgs {
+  const float* logits;  // [B][2][h][w]
+  const uint8_t* lbl;   // [B][S][S]
+  const AdaptScalars* sc;
+  float* dlogits;       // [B][2][h][w], zeroed; accumulates U^T g (unscaled)
+  double* loss_num;     // [1] sum w nll
+  int h, w, S;
+  float sy, sx;
+};
+
+__global__ __launch_bounds__(256) void seg_ce_kernel(SegCEArgs a) {
+  __shared__ float z[2][ADAPT_CB + 1][2];
+  __shared__ float gs[2][ADAPT_CB + 1];
+  __shared__ float lsum[4];
+  const int t = threadIdx.x;
+  const int cb = blockIdx.x, r = blockIdx.y, b = blockIdx.z;
+  const int ncb = gridDim.x;
+  const int x0 = cb * ADAPT_CB;
+  const int ncol = min(ADAPT_CB + 1, a.w - x0);
+  const long plane = (long)a.h * a.w;
+  if (t < 2 * (ADAPT_CB + 1)) {
+    const int ri = t / (ADAPT_CB + 1), xi = t % (ADAPT_CB + 1);
+    gs[ri][xi] = 0.f;
+    if (xi < ncol) {
+      z[ri][xi][0] = a.logits[(long)b * 2 * plane + (long)(r + ri) * a.w + x0 + xi];
+      z[ri][xi][1] = a.logits[(long)b * 2 * plane + plane + (long)(r + ri) * a.w + x0 + xi];
+    }
+  }
+  __syncthreads();
+  float l = hires_tile_grad<true>(z, gs, a.lbl + (long)b * a.S * a.S, a.S, a.h, a.w, r, cb, ncb, a.sy, a.sx,
+                                  a.sc->wfg);
+  l = wave_sum(l);
+  if ((t & 63) == 0) lsum[t >> 6] = l;
+  __syncthreads();
+  if (t == 0) atomicAdd(a.loss_num, (double)((lsum[0] + lsum[1]) + (lsum[2] + lsum[3])));
+  if (t < 2 * (ADAPT_CB + 1)) {
+    const int ri = t / (ADAPT_CB + 1), xi = t % (ADAPT_CB + 1);
+    if (xi < ncol) {
+      const float g = gs[ri][xi];
+      const long off = (long)b * 2 * plane + (long)(r + ri) * a.w + x0 + xi;
+      atomicAdd(&a.dlogits[off + plane], g);
+      atomicAdd(&a.dlogits[off], -g);
+    }
+  }
+}
+
+__global__ void seg_ce_final_kernel(const AdaptScalars* sc, const double* loss_num, float* loss_out, float* dlogits,
+                                    long n) {
+  const double sumw = (double)sc->nbg + (double)sc->nfg * (double)sc->wfg;
+  const float inv = (float)(1.0 / sumw);
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) loss_out[0] = (float)(loss_num[0] / sumw);
+  for (; i < n; i += (long)gridDim.x * blockDim.x) dlogits[i] *= inv;
+}
+
+int launch_seg_ce(const float* logits, const int64_t* target, int B, int h, int w, int S, float* loss_out,
+                  float* dlogits, uint8_t* lbl_ws, AdaptScalars* sc, double* loss_num, hipStream_t st) {
+  const long total = (long)B * S * S;
+  CWT_HIP(hipMemsetAsync(sc, 0, sizeof(AdaptScalars), st));
+  CWT_HIP(hipMemsetAsync(loss_num, 0, sizeof(double), st));
+  CWT_HIP(hipMemsetAsync(dlogits, 0, sizeof(float) * (size_t)B * 2 * h * w, st));
+  int pblocks = (int)std::min<long>(1024, cdiv(total, 256));
+  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(256), 0, st, target, total, lbl_ws, sc);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(adapt_scalars_kernel, dim3(1), dim3(1), 0, st, sc, 1.0f, 1);
+  CWT_LAUNCH_CHECK();
+  SegCEArgs a;
+  a.logits = logits;
+  a.lbl = lbl_ws;
+  a.sc = sc;
+  a.dlogits = dlogits;
+  a.loss_num = loss_num;
+  a.h = h;
+  a.w = w;
+  a.S = S;
+  a.sy = align_corners_scale(h, S);
+  a.sx = align_corners_scale(w, S);
+  dim3 grid(cdiv(S - 1, 8 * ADAPT_CB), h - 1, B);
+  hipLaunchKernelGGL(seg_ce_kernel, grid, dim3(256), 0, st, a);
+  CWT_LAUNCH_CHECK();
+  long n = (long)B * 2 * h * w;
+  hipLaunchKernelGGL(seg_ce_final_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, (const AdaptScalars*)sc,
+                     (const double*)loss_num, loss_out, dlogits, n);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace cwt

@@ -1,0 +1,698 @@
+// C ABI of libcwt.so (declared in include/cwt.h): context, weight loading, workspace pool
+// and the frozen-extractor orchestration.  See include/cwt.h for the contract of each
+// entry point and the reference call site it replaces.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/cwt.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace cwt {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+// launchers defined in the other units
+struct AdaptScalars;
+int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int S, float lr, int iters, float* W,
+                 uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf, hipStream_t st);
+int launch_seg_ce(const float* logits, const int64_t* target, int B, int h, int w, int S, float* loss_out,
+                  float* dlogits, uint8_t* lbl_ws, AdaptScalars* sc, double* loss_num, hipStream_t st);
+int launch_normalize(const float* f, int B, int Pb, float* out, const float* W0, float* logits0, hipStream_t st);
+int launch_classify(const float* W, const float* f, int B, int Pb, float* logits, hipStream_t st);
+int launch_classify_bwd(const float* dl, const float* f, int B, int Pb, float* dW, hipStream_t st);
+int launch_seg_metrics(const float* logits, const int64_t* target, int B, int h, int w, int S, float* iut,
+                       double* ce, unsigned* counts_ws, hipStream_t st);
+int launch_iou_preds(const int64_t* preds, const int64_t* target, long n, int K, int ignore, float* iut,
+                     unsigned* counts_ws, hipStream_t st);
+int launch_sgd(float* p, const float* g, float* buf, long n, float lr, float mom, float wd, int nesterov, int first,
+               hipStream_t st);
+size_t attention_saved_floats(int B, int hw, int C, int H);
+size_t attention_ws_floats(int B, int hw, int C, int H);
+int attention_fwd(const float* q, const float* f, int B, int hw, int C, int H, const float* w_qkvs,
+                  const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b, float* out,
+                  float* saved, float* ws, hipStream_t st);
+int attention_bwd(const float* q, const float* f, int B, int hw, int C, int H, const float* w_qkvs,
+                  const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b, const float* saved,
+                  const float* d_out, float* g_w_qkvs, float* g_fc_w, float* g_fc_b, float* g_ln_w, float* g_ln_b,
+                  float* ws, hipStream_t st);
+size_t attention_bwd_ws_floats(int B, int hw, int C, int H);
+
+// ------------------------------------------------------------------------------------------
+struct ConvLayer {
+  int Ci = 0, Co = 0, k = 1, stride = 1, pad = 0, dil = 1;
+  float* w = nullptr;  // device, packed [Co][k][k][Ci] (stem conv1: [ci][ky][kx][co])
+  float* scale = nullptr;
+  float* shift = nullptr;
+};
+
+struct Block {
+  ConvLayer c1, c2, c3, down;
+  bool has_down = false;
+};
+
+struct Backbone {
+  int layers = 0;
+  ConvLayer stem[3];
+  std::vector<Block> blocks[4];
+  ConvLayer ppm[4];
+  ConvLayer bott;
+  std::vector<void*> allocs;
+};
+
+struct WsBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace cwt
+
+struct cwt_ctx {
+  int device = 0;
+  cwt::Backbone* bb = nullptr;
+  std::map<std::string, cwt::WsBuf> ws;
+  size_t ws_total = 0;
+  // optional per-launch profiling: events recorded on the caller's stream around each
+  // instrumented launch (cwt_profile_enable); read back after a sync
+  bool prof_on = false;
+  struct Rec {
+    std::string name;
+    double flops, bytes;
+    hipEvent_t e0, e1;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> evpool;
+  size_t ev_used = 0;
+};
+
+namespace cwt {
+
+// Profiling bracket: Prof p(ctx, st, name, flops, bytes); ... launches ...; p.end();
+struct Prof {
+  cwt_ctx* c;
+  hipStream_t st;
+  int idx = -1;
+  Prof(cwt_ctx* ctx, hipStream_t s, const std::string& name, double flops, double bytes) : c(ctx), st(s) {
+    if (!c->prof_on) return;
+    hipEvent_t ev[2];
+    for (int k = 0; k < 2; ++k) {
+      if (c->ev_used == c->evpool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        c->evpool.push_back(e);
+      }
+      ev[k] = c->evpool[c->ev_used++];
+    }
+    c->recs.push_back({name, flops, bytes, ev[0], ev[1]});
+    idx = (int)c->recs.size() - 1;
+    (void)hipEventRecord(ev[0], st);
+  }
+  void end() {
+    if (idx >= 0) (void)hipEventRecord(c->recs[idx].e1, st);
+    idx = -1;
+  }
+};
+
+static int ensure_ws(cwt_ctx* ctx, const std::string& name, size_t bytes, void** out) {
+  WsBuf& b = ctx->ws[name];
+  if (b.bytes < bytes) {
+    if (b.p) {
+      CWT_HIP(hipDeviceSynchronize());  // the old buffer may still be in use by queued work
+      CWT_HIP(hipFree(b.p));
+      ctx->ws_total -= b.bytes;
+      b.p = nullptr;
+      b.bytes = 0;
+    }
+    size_t nb = (bytes + 255) & ~(size_t)255;
+    CWT_HIP(hipMalloc(&b.p, nb));
+    b.bytes = nb;
+    ctx->ws_total += nb;
+  }
+  *out = b.p;
+  return 0;
+}
+
+struct HostParams {
+  std::map<std::string, std::pair<const float*, int64_t>> m;
+  const float* get(const std::string& k, int64_t numel, std::string* err) const {
+    auto it = m.find(k);
+    if (it == m.end() || it->second.first == nullptr) {
+      *err = "missing tensor '" + k + "'";
+      return nullptr;
+    }
+    if (it->second.second != numel) {
+      *err = "tensor '" + k + "' has " + std::to_string(it->second.second) + " elements, expected " +
+             std::to_string(numel);
+      return nullptr;
+    }
+    return it->second.first;
+  }
+};
+
+static int upload(Backbone* bb, const std::vector<float>& v, float** out) {
+  void* p = nullptr;
+  CWT_HIP(hipMalloc(&p, v.size() * sizeof(float)));
+  CWT_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice));
+  bb->allocs.push_back(p);
+  *out = (float*)p;
+  return 0;
+}
+
+// BN eval folding as PyTorch's CPU inference kernel: alpha = w / sqrt(var + eps), beta = b - mean * alpha.
+static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wname, const std::string& bnp, int Ci,
+                     int Co, int k, int stride, int pad, int dil, float eps, bool stem1, ConvLayer* L) {
+  std::string err;
+  const float* w = hp.get(wname, (int64_t)Co * Ci * k * k, &err);
+  if (!w) return fail(CWT_EARG, err);
+  const float* g = hp.get(bnp + ".weight", Co, &err);
+  const float* b = g ? hp.get(bnp + ".bias", Co, &err) : nullptr;
+  const float* rm = b ? hp.get(bnp + ".running_mean", Co, &err) : nullptr;
+  const float* rv = rm ? hp.get(bnp + ".running_var", Co, &err) : nullptr;
+  if (!rv) return fail(CWT_EARG, err);
+  L->Ci = Ci;
+  L->Co = Co;
+  L->k = k;
+  L->stride = stride;
+  L->pad = pad;
+  L->dil = dil;
+  const int K = k * k * Ci;
+  std::vector<float> packed((size_t)Co * K);
+  for (int co = 0; co < Co; ++co)
+    for (int ci = 0; ci < Ci; ++ci)
+      for (int ky = 0; ky < k; ++ky)
+        for (int kx = 0; kx < k; ++kx) {
+          const float v = w[(((size_t)co * Ci + ci) * k + ky) * k + kx];
+          if (stem1)
+            packed[((size_t)(ci * 9 + ky * 3 + kx)) * Co + co] = v;
+          else
+            packed[(size_t)co * K + (ky * k + kx) * Ci + ci] = v;
+        }
+  std::vector<float> sc(Co), sh(Co);
+  for (int c = 0; c < Co; ++c) {
+    const float invstd = 1.0f / std::sqrt(rv[c] + eps);
+    sc[c] = g[c] * invstd;
+    sh[c] = b[c] - rm[c] * sc[c];
+  }
+  int rc;
+  if ((rc = upload(bb, packed, &L->w))) return rc;
+  if ((rc = upload(bb, sc, &L->scale))) return rc;
+  if ((rc = upload(bb, sh, &L->shift))) return rc;
+  return 0;
+}
+
+static const int kBlocks50[4] = {3, 4, 6, 3};
+static const int kBlocks101[4] = {3, 4, 23, 3};
+static const int kBins[4] = {1, 2, 3, 6};
+
+static int load_backbone(cwt_ctx* ctx, int layers, const HostParams& hp, float eps) {
+  if (layers != 50 && layers != 101) return fail(CWT_EARG, "layers must be 50 or 101");
+  Backbone* bb = new Backbone();
+  bb->layers = layers;
+  int rc = 0;
+  auto cleanup = [&]() {
+    for (void* p : bb->allocs) (void)hipFree(p);
+    delete bb;
+  };
+  // layer0: deep-base stem (resnet.py:110-118)
+  if ((rc = load_conv(bb, hp, "layer0.0.weight", "layer0.1", 3, 64, 3, 2, 1, 1, eps, true, &bb->stem[0])) ||
+      (rc = load_conv(bb, hp, "layer0.3.weight", "layer0.4", 64, 64, 3, 1, 1, 1, eps, false, &bb->stem[1])) ||
+      (rc = load_conv(bb, hp, "layer0.6.weight", "layer0.7", 64, 128, 3, 1, 1, 1, eps, false, &bb->stem[2]))) {
+    cleanup();
+    return rc;
+  }
+  const int* nb = (layers == 50) ? kBlocks50 : kBlocks101;
+  int inplanes = 128;
+  const int planes_of[4] = {64, 128, 256, 512};
+  for (int li = 0; li < 4; ++li) {
+    const int planes = planes_of[li];
+    for (int bi = 0; bi < nb[li]; ++bi) {
+      Block B;
+      // dilation surgery (pspnet.py:103-112): layer3 conv2 d2 s1, layer4 conv2 d4 s1, downsample s1
+      int s2 = 1, d2 = 1, sd = 1;
+      if (li == 1 && bi == 0) {
+        s2 = 2;
+        sd = 2;
+      }
+      if (li == 2) d2 = 2;
+      if (li == 3) d2 = 4;
+      const std::string p = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+      if ((rc = load_conv(bb, hp, p + ".conv1.weight", p + ".bn1", inplanes, planes, 1, 1, 0, 1, eps, false, &B.c1)) ||
+          (rc = load_conv(bb, hp, p + ".conv2.weight", p + ".bn2", planes, planes, 3, s2, d2, d2, eps, false, &B.c2)) ||
+          (rc = load_conv(bb, hp, p + ".conv3.weight", p + ".bn3", planes, planes * 4, 1, 1, 0, 1, eps, false,
+                          &B.c3))) {
+        cleanup();
+        return rc;
+      }
+      if (bi == 0) {
+        B.has_down = true;
+        if ((rc = load_conv(bb, hp, p + ".downsample.0.weight", p + ".downsample.1", inplanes, planes * 4, 1, sd, 0, 1,
+                            eps, false, &B.down))) {
+          cleanup();
+          return rc;
+        }
+      }
+      inplanes = planes * 4;
+      bb->blocks[li].push_back(B);
+    }
+  }
+  for (int i = 0; i < 4; ++i) {
+    const std::string p = "ppm.features." + std::to_string(i);
+    if ((rc = load_conv(bb, hp, p + ".1.weight", p + ".2", 2048, 512, 1, 1, 0, 1, eps, false, &bb->ppm[i]))) {
+      cleanup();
+      return rc;
+    }
+  }
+  if ((rc = load_conv(bb, hp, "bottleneck.0.weight", "bottleneck.1", 4096, 512, 3, 1, 1, 1, eps, false, &bb->bott))) {
+    cleanup();
+    return rc;
+  }
+  if (ctx->bb) {
+    for (void* p : ctx->bb->allocs) (void)hipFree(p);
+    delete ctx->bb;
+  }
+  ctx->bb = bb;
+  return 0;
+}
+
+static inline int down2(int x) { return (x - 1) / 2 + 1; }  // 3x3 s2 p1 conv / maxpool output size
+
+struct ConvCall {
+  int stage;  // 0 stem, 1-4 layer1-4, 5 PPM, 6 bottleneck (kernel symbol tag)
+  const ConvLayer* L;
+  const float* x;
+  int N, Hi, Wi, x_ld;
+  float* y;
+  int y_ld, y_off;
+  const float* res;
+  int res_ld;
+  int relu;
+};
+
+static ConvArgs make_args(const ConvCall& c) {
+  ConvArgs a;
+  memset(&a, 0, sizeof(a));
+  const ConvLayer& L = *c.L;
+  a.x = c.x;
+  a.w = L.w;
+  a.scale = L.scale;
+  a.shift = L.shift;
+  a.res = c.res;
+  a.y = c.y;
+  a.N = c.N;
+  a.Hi = c.Hi;
+  a.Wi = c.Wi;
+  a.Ci = L.Ci;
+  a.x_ld = c.x_ld;
+  a.Ho = (c.Hi + 2 * L.pad - L.dil * (L.k - 1) - 1) / L.stride + 1;
+  a.Wo = (c.Wi + 2 * L.pad - L.dil * (L.k - 1) - 1) / L.stride + 1;
+  a.Co = L.Co;
+  a.kh = a.kw = L.k;
+  a.stride = L.stride;
+  a.pad = L.pad;
+  a.dil = L.dil;
+  a.M = c.N * a.Ho * a.Wo;
+  a.K = L.k * L.k * L.Ci;
+  a.y_ld = c.y_ld;
+  a.y_off = c.y_off;
+  a.res_ld = c.res_ld;
+  a.relu = c.relu;
+  return a;
+}
+
+// The whole extractor as a list of conv calls + byte kernels.  dry_run sizes the split-K workspace.
+static int run_extract(cwt_ctx* ctx, const float* img, int N, int S, float* feat, hipStream_t st) {
+  Backbone* bb = ctx->bb;
+  const int Hs = down2(S), H1 = down2(Hs), h = down2(H1);
+  const long sA = std::max({(long)N * Hs * Hs * 128, (long)N * H1 * H1 * 256, (long)N * h * h * 2048});
+  const long sT1 = std::max((long)N * H1 * H1 * 128, (long)N * h * h * 512);
+  const long sT2 = std::max((long)N * H1 * H1 * 64, (long)N * h * h * 512);
+  const long sD = std::max((long)N * H1 * H1 * 256, (long)N * h * h * 2048);
+  const long sCat = (long)N * h * h * 4096;
+  const long sCol = (long)N * h * 12 * 2048;
+  const long sPool = (long)N * 50 * 2048;
+  const long sPpm = (long)N * 50 * 512;
+
+  // collect every conv call first (to size split-K scratch), then run
+  float *A, *B, *T1, *T2, *D, *CAT, *COL, *POOL, *PPM;
+  void* p;
+  int rc;
+  if ((rc = ensure_ws(ctx, "bb.A", sA * 4, &p))) return rc;
+  A = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.B", sA * 4, &p))) return rc;
+  B = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.T1", sT1 * 4, &p))) return rc;
+  T1 = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.T2", sT2 * 4, &p))) return rc;
+  T2 = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.D", sD * 4, &p))) return rc;
+  D = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.CAT", sCat * 4, &p))) return rc;
+  CAT = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.COL", sCol * 4, &p))) return rc;
+  COL = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.POOL", sPool * 4, &p))) return rc;
+  POOL = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.PPM", sPpm * 4, &p))) return rc;
+  PPM = (float*)p;
+
+  std::vector<ConvCall> calls;
+  int stage = 0;
+  auto cc = [&](const ConvLayer* L, const float* x, int n, int Hi, int Wi, int x_ld, float* y, int y_ld, int y_off,
+                const float* res, int res_ld, int relu) {
+    ConvCall c{stage, L, x, n, Hi, Wi, x_ld, y, y_ld, y_off, res, res_ld, relu};
+    calls.push_back(c);
+  };
+  // stem conv2/conv3 (conv1 and maxpool are separate kernels, ordered below by index)
+  cc(&bb->stem[1], A, N, Hs, Hs, 64, B, 64, 0, nullptr, 0, 1);
+  cc(&bb->stem[2], B, N, Hs, Hs, 64, A, 128, 0, nullptr, 0, 1);
+  const size_t n_stem_calls = calls.size();
+  float* cur = B;  // maxpool output
+  float* other = A;
+  int H = H1;
+  for (int li = 0; li < 4; ++li) {
+    stage = li + 1;
+    const int nbk = (int)bb->blocks[li].size();
+    for (int bi = 0; bi < nbk; ++bi) {
+      const Block& blk = bb->blocks[li][bi];
+      const int Cin = blk.c1.Ci;
+      const int Ho = (blk.c2.stride == 2) ? down2(H) : H;
+      const bool last = (li == 3 && bi == nbk - 1);
+      cc(&blk.c1, cur, N, H, H, Cin, T1, blk.c1.Co, 0, nullptr, 0, 1);
+      cc(&blk.c2, T1, N, H, H, blk.c2.Ci, T2, blk.c2.Co, 0, nullptr, 0, 1);
+      const float* res = cur;
+      int res_ld = Cin;
+      if (blk.has_down) {
+        cc(&blk.down, cur, N, H, H, Cin, D, blk.down.Co, 0, nullptr, 0, 0);
+        res = D;
+        res_ld = blk.down.Co;
+      }
+      float* out = last ? CAT : other;
+      const int out_ld = last ? 4096 : blk.c3.Co;
+      cc(&blk.c3, T2, N, Ho, Ho, blk.c3.Ci, out, out_ld, 0, res, res_ld, 1);
+      std::swap(cur, other);
+      H = Ho;
+    }
+  }
+  const size_t n_backbone_calls = calls.size();
+  // PPM 1x1 convs over the pooled cells (bin-major rows), then the bottleneck conv
+  stage = 5;
+  {
+    long off_in = 0, off_out = 0;
+    for (int i = 0; i < 4; ++i) {
+      const int cells = N * kBins[i] * kBins[i];
+      cc(&bb->ppm[i], POOL + off_in * 2048, 1, 1, cells, 2048, PPM + off_out * 512, 512, 0, nullptr, 0, 1);
+      off_in += cells;
+      off_out += cells;
+    }
+  }
+  stage = 6;
+  cc(&bb->bott, CAT, N, h, h, 4096, feat, 512, 0, nullptr, 0, 1);
+
+  // split-K scratch
+  size_t part_floats = 0;
+  std::vector<ConvPlan> plans;
+  for (auto& c : calls) {
+    ConvArgs a = make_args(c);
+    ConvPlan pl = plan_conv(a.M, a.Co, a.K);
+    plans.push_back(pl);
+    if (pl.nsplit > 1) part_floats = std::max(part_floats, (size_t)pl.nsplit * a.M * a.Co);
+  }
+  float* PART = nullptr;
+  if (part_floats) {
+    if ((rc = ensure_ws(ctx, "bb.PART", part_floats * 4, &p))) return rc;
+    PART = (float*)p;
+  }
+  auto run_call = [&](size_t i) -> int {
+    ConvArgs a = make_args(calls[i]);
+    const ConvPlan& pl = plans[i];
+    const double flops = 2.0 * a.M * a.Co * a.K;
+    const double bytes = 4.0 * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K + (double)a.M * a.Co +
+                                (a.res ? (double)a.M * a.Co : 0.0));
+    Prof p(ctx, st,
+           "conv_igemm_f32<" + std::to_string(pl.bm) + "," + std::to_string(pl.bn) + "," +
+               std::to_string(calls[i].stage) + ">" +
+               (pl.nsplit > 1 ? "+splitk" + std::to_string(pl.nsplit) : std::string()) + " " +
+               std::to_string(a.Ci) + "x" + std::to_string(a.Co) + "k" + std::to_string(a.kh) + "s" +
+               std::to_string(a.stride) + "d" + std::to_string(a.dil) + "@" + std::to_string(a.Ho),
+           flops, bytes);
+    int r = launch_conv(a, pl, calls[i].stage, PART, part_floats, st);
+    p.end();
+    return r;
+  };
+
+  {
+    Prof p(ctx, st, "stem_conv1 3x64k3s2", 2.0 * N * Hs * Hs * 64 * 27, 4.0 * ((double)N * 3 * S * S + (double)N * Hs * Hs * 64));
+    if ((rc = launch_stem_conv1(img, N, S, bb->stem[0].w, bb->stem[0].scale, bb->stem[0].shift, A, Hs, st))) return rc;
+    p.end();
+  }
+  for (size_t i = 0; i < n_stem_calls; ++i)
+    if ((rc = run_call(i))) return rc;
+  {
+    Prof p(ctx, st, "maxpool3s2", 0.0, 4.0 * ((double)N * Hs * Hs * 128 + (double)N * H1 * H1 * 128));
+    if ((rc = launch_maxpool3s2(A, N, Hs, Hs, 128, B, H1, H1, st))) return rc;
+    p.end();
+  }
+  for (size_t i = n_stem_calls; i < n_backbone_calls; ++i)
+    if ((rc = run_call(i))) return rc;
+  {
+    Prof p(ctx, st, "ppm_pool", 0.0, 4.0 * ((double)N * h * h * 2048 + (double)N * 50 * 2048));
+    if ((rc = launch_ppm(CAT, N, h, h, 4096, kBins, 4, COL, POOL, st))) return rc;
+    p.end();
+  }
+  for (size_t i = n_backbone_calls; i < n_backbone_calls + 4; ++i)
+    if ((rc = run_call(i))) return rc;
+  {
+    Prof p(ctx, st, "ppm_upsample", 0.0, 4.0 * ((double)N * h * h * 2048 + (double)N * 50 * 512));
+    if ((rc = launch_ppm_upsample(PPM, N, h, h, kBins, 4, 512, CAT, 4096, 2048, st))) return rc;
+    p.end();
+  }
+  return run_call(n_backbone_calls + 4);
+}
+
+}  // namespace cwt
+
+using namespace cwt;
+
+extern "C" {
+
+const char* cwt_version(void) { return "libcwt 0.1 (gfx950, fp32 MFMA)"; }
+
+const char* cwt_last_error(void) { return g_err.c_str(); }
+
+int cwt_ctx_create(int device, cwt_ctx** out) {
+  if (!out) return fail(CWT_EARG, "out is NULL");
+  int n = 0;
+  CWT_HIP(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(CWT_EARG, "no such device");
+  CWT_HIP(hipSetDevice(device));
+  cwt_ctx* c = new cwt_ctx();
+  c->device = device;
+  *out = c;
+  return 0;
+}
+
+int cwt_ctx_destroy(cwt_ctx* ctx) {
+  if (!ctx) return 0;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  if (ctx->bb) {
+    for (void* p : ctx->bb->allocs) (void)hipFree(p);
+    delete ctx->bb;
+  }
+  for (auto& kv : ctx->ws)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  delete ctx;
+  return 0;
+}
+
+int cwt_backbone_load(cwt_ctx* ctx, int layers, int n_tensors, const char* const* names,
+                      const float* const* host_data, const int64_t* numel, float bn_eps) {
+  if (!ctx || !names || !host_data || !numel || n_tensors <= 0) return fail(CWT_EARG, "null argument");
+  CWT_HIP(hipSetDevice(ctx->device));
+  HostParams hp;
+  for (int i = 0; i < n_tensors; ++i) hp.m[names[i]] = {host_data[i], numel[i]};
+  return load_backbone(ctx, layers, hp, bn_eps);
+}
+
+int cwt_extract_features(cwt_ctx* ctx, const float* img, int N, int S, float* feat, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  if (!ctx->bb) return fail(CWT_ESTATE, "backbone weights not loaded (cwt_backbone_load)");
+  CWT_CHECK(img && feat, "null buffer");
+  CWT_CHECK(N >= 1 && S >= 9 && (S - 1) % 8 == 0, "need N >= 1 and (S-1) % 8 == 0 (pspnet.py:150)");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return run_extract(ctx, img, N, S, feat, (hipStream_t)stream);
+}
+
+size_t cwt_workspace_bytes(cwt_ctx* ctx) { return ctx ? ctx->ws_total : 0; }
+
+int cwt_inner_adapt(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int n, int h, int w, int C, int S,
+                    float lr, int iters, float* W_inout, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(f_s && s_label && W_inout, "null buffer");
+  CWT_CHECK(C == 512, "C must be 512");
+  CWT_CHECK(n >= 1 && h >= 2 && w >= 2 && iters >= 0, "bad sizes");
+  CWT_CHECK(S - 1 == 8 * (h - 1) && S - 1 == 8 * (w - 1), "need S-1 == 8*(h-1) == 8*(w-1)");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void *lbl, *sc, *acc, *wb;
+  int rc;
+  if ((rc = ensure_ws(ctx, "adapt.lbl", (size_t)n * S * S, &lbl))) return rc;
+  if ((rc = ensure_ws(ctx, "adapt.sc", 64, &sc))) return rc;
+  if ((rc = ensure_ws(ctx, "adapt.acc", 3 * 512 * 4, &acc))) return rc;
+  if ((rc = ensure_ws(ctx, "adapt.wbuf", 2 * 1024 * 4, &wb))) return rc;
+  // algorithmic work: per step 2 x (2*2*C*h*w*n) FLOPs; minimal bytes = f_s + labels once per step
+  Prof p(ctx, (hipStream_t)stream, "inner_adapt x" + std::to_string(iters), (double)iters * 2.0 * (4.0 * C * h * w * n),
+         (double)iters * ((double)n * h * w * C * 4 + (double)n * S * S));
+  rc = launch_adapt(f_s, s_label, n, h, w, S, lr, iters, W_inout, (uint8_t*)lbl, (AdaptScalars*)sc, (float*)acc,
+                    (float*)wb, (hipStream_t)stream);
+  p.end();
+  return rc;
+}
+
+int cwt_normalize(cwt_ctx* ctx, const float* f, int B, int P_per_b, int C, float* out, const float* W0,
+                  float* logits0, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(f && out && C == 512 && B >= 1 && P_per_b >= 1, "bad arguments");
+  CWT_CHECK((W0 == nullptr) == (logits0 == nullptr), "W0 and logits0 go together");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_normalize(f, B, P_per_b, out, W0, logits0, (hipStream_t)stream);
+}
+
+size_t cwt_attention_saved_floats(int B, int hw, int C, int H) { return attention_saved_floats(B, hw, C, H); }
+
+int cwt_attention_fwd(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                      const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b,
+                      float* out, float* saved, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(q && f && w_qkvs && fc_w && fc_b && ln_w && ln_b && out, "null buffer");
+  CWT_CHECK(B >= 1 && B <= 4 && hw >= 1 && C == 512, "need 1 <= B <= 4, C == 512");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void* ws;
+  int rc;
+  if ((rc = ensure_ws(ctx, "attn.ws", attention_ws_floats(B, hw, C, H) * 4, &ws))) return rc;
+  // reference-formulation FLOPs: k/v projections 2 x 2*hw*C*C*H + QK^T/AV 2 x 2*H*2*hw*C
+  Prof p(ctx, (hipStream_t)stream, "attention_fwd",
+         (double)B * (2.0 * 2.0 * hw * C * C * H + 2.0 * 2.0 * H * 2.0 * hw * C),
+         4.0 * ((double)B * hw * C + 2.0 * H * C * C + 2.0 * C));
+  rc = attention_fwd(q, f, B, hw, C, H, w_qkvs, fc_w, fc_b, ln_w, ln_b, out, saved, (float*)ws, (hipStream_t)stream);
+  p.end();
+  return rc;
+}
+
+int cwt_attention_bwd(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                      const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b,
+                      const float* saved, const float* d_out, float* g_w_qkvs, float* g_fc_w, float* g_fc_b,
+                      float* g_ln_w, float* g_ln_b, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(q && f && w_qkvs && fc_w && fc_b && ln_w && ln_b && saved && d_out, "null buffer");
+  CWT_CHECK(g_w_qkvs && g_fc_w && g_fc_b && g_ln_w && g_ln_b, "null gradient buffer");
+  CWT_CHECK(B >= 1 && B <= 4 && hw >= 1 && C == 512, "need 1 <= B <= 4, C == 512");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void* ws;
+  int rc;
+  if ((rc = ensure_ws(ctx, "attn.bws", attention_bwd_ws_floats(B, hw, C, H) * 4, &ws))) return rc;
+  return attention_bwd(q, f, B, hw, C, H, w_qkvs, fc_w, fc_b, ln_w, ln_b, saved, d_out, g_w_qkvs, g_fc_w, g_fc_b,
+                       g_ln_w, g_ln_b, (float*)ws, (hipStream_t)stream);
+}
+
+int cwt_classify(cwt_ctx* ctx, const float* W, const float* f, int B, int P, int C, float* logits, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(W && f && logits && C == 512 && B >= 1 && P >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_classify(W, f, B, P, logits, (hipStream_t)stream);
+}
+
+int cwt_classify_bwd(cwt_ctx* ctx, const float* dlogits, const float* f, int B, int P, int C, float* dW,
+                     void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(dlogits && f && dW && C == 512 && B >= 1 && P >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_classify_bwd(dlogits, f, B, P, dW, (hipStream_t)stream);
+}
+
+int cwt_seg_metrics(cwt_ctx* ctx, const float* logits, const int64_t* target, int B, int h, int w, int S,
+                    float* iut_out, double* ce_out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(logits && target && iut_out && B >= 1 && B <= 64 && h >= 1 && w >= 1 && S >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void* cnt;
+  int rc;
+  if ((rc = ensure_ws(ctx, "metrics.cnt", (size_t)B * 6 * 4, &cnt))) return rc;
+  return launch_seg_metrics(logits, target, B, h, w, S, iut_out, ce_out, (unsigned*)cnt, (hipStream_t)stream);
+}
+
+int cwt_seg_ce_fwd_bwd(cwt_ctx* ctx, const float* logits, const int64_t* target, int B, int h, int w, int S,
+                       float* loss_out, float* dlogits, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(logits && target && loss_out && dlogits && B >= 1, "bad arguments");
+  CWT_CHECK(S - 1 == 8 * (h - 1) && S - 1 == 8 * (w - 1), "need S-1 == 8*(h-1) == 8*(w-1)");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void *lbl, *sc, *num;
+  int rc;
+  if ((rc = ensure_ws(ctx, "ce.lbl", (size_t)B * S * S, &lbl))) return rc;
+  if ((rc = ensure_ws(ctx, "ce.sc", 64, &sc))) return rc;
+  if ((rc = ensure_ws(ctx, "ce.num", 64, &num))) return rc;
+  return launch_seg_ce(logits, target, B, h, w, S, loss_out, dlogits, (uint8_t*)lbl, (AdaptScalars*)sc,
+                       (double*)num, (hipStream_t)stream);
+}
+
+int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int64_t n, int num_classes,
+                  int ignore_index, float* iut_out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(preds && target && iut_out && n >= 0 && num_classes >= 1 && num_classes <= 16, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void* cnt;
+  int rc;
+  if ((rc = ensure_ws(ctx, "iou.cnt", 3 * 16 * 4, &cnt))) return rc;
+  return launch_iou_preds(preds, target, n, num_classes, ignore_index, iut_out, (unsigned*)cnt, (hipStream_t)stream);
+}
+
+int cwt_profile_enable(cwt_ctx* ctx, int on) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  ctx->prof_on = on != 0;
+  if (on) {
+    ctx->recs.clear();
+    ctx->ev_used = 0;
+  }
+  return 0;
+}
+
+int cwt_profile_count(cwt_ctx* ctx) { return ctx ? (int)ctx->recs.size() : 0; }
+
+int cwt_profile_record(cwt_ctx* ctx, int i, char* name, int name_len, double* flops, double* bytes, float* ms) {
+  if (!ctx || i < 0 || i >= (int)ctx->recs.size()) return fail(CWT_EARG, "no such profile record");
+  auto& r = ctx->recs[i];
+  if (name && name_len > 0) {
+    strncpy(name, r.name.c_str(), name_len - 1);
+    name[name_len - 1] = 0;
+  }
+  if (flops) *flops = r.flops;
+  if (bytes) *bytes = r.bytes;
+  if (ms) {
+    CWT_HIP(hipEventSynchronize(r.e1));
+    CWT_HIP(hipEventElapsedTime(ms, r.e0, r.e1));
+  }
+  return 0;
+}
+
+int cwt_sgd_step(cwt_ctx* ctx, float* param, const float* grad, float* momentum_buf, int64_t n, float lr,
+                 float momentum, float weight_decay, int nesterov, int first_step, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(param && grad && n >= 0, "bad arguments");
+  CWT_CHECK(momentum == 0.f || momentum_buf, "momentum needs a buffer");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_sgd(param, grad, momentum_buf, n, lr, momentum, weight_decay, nesterov, first_step,
+                    (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,74 @@
+// Shared device/host helpers for libcwt (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace cwt {
+
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define CWT_HIP(expr)                                                                         \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      return ::cwt::fail((int)e_, std::string(#expr " -> ") + hipGetErrorString(e_));         \
+  } while (0)
+
+#define CWT_CHECK(cond, msg)                                                                  \
+  do {                                                                                        \
+    if (!(cond)) return ::cwt::fail(CWT_EARG, std::string("bad argument: ") + (msg));         \
+  } while (0)
+
+#define CWT_LAUNCH_CHECK()                                                                    \
+  do {                                                                                        \
+    hipError_t e_ = hipGetLastError();                                                        \
+    if (e_ != hipSuccess)                                                                     \
+      return ::cwt::fail((int)e_, std::string("kernel launch: ") + hipGetErrorString(e_));    \
+  } while (0)
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bilinear source coordinate, PyTorch upsample_bilinear2d(align_corners=True) CPU semantics
+// (aten/src/ATen/native/UpSample.h area_pixel_compute_scale / source index): scale is a float
+// (in-1)/(out-1), src = scale*dst, i0 = (int)src, i1 = i0 + (i0 < in-1), l1 = src - i0.
+struct Lerp {
+  int i0, i1;
+  float l0, l1;
+};
+__device__ __forceinline__ Lerp lerp_coord(int dst, int in_size, float scale) {
+  Lerp r;
+  float src = scale * (float)dst;
+  r.i0 = (int)src;
+  r.i1 = r.i0 + ((r.i0 < in_size - 1) ? 1 : 0);
+  r.l1 = src - (float)r.i0;
+  r.l0 = 1.0f - r.l1;
+  return r;
+}
+static inline float align_corners_scale(int in_size, int out_size) {
+  return out_size > 1 ? (float)(in_size - 1) / (float)(out_size - 1) : 0.0f;
+}
+
+}  // namespace cwt
+
+#ifndef CWT_EARG
+#define CWT_EARG 1001
+#define CWT_ESTATE 1002
+#define CWT_ENOFG 1003
+#endif

@@ -1,0 +1,39 @@
+// Kernel-side argument structs and launcher declarations shared by the .hip units.
+#pragma once
+#include "common.h"
+
+namespace cwt {
+
+struct ConvArgs {
+  const float* x;      // NHWC input, pixel stride x_ld floats
+  const float* w;      // packed [Co][K], K = kh*kw*Ci (tap-major)
+  const float* scale;  // [Co] folded BN scale
+  const float* shift;  // [Co] folded BN shift
+  const float* res;    // optional residual, NHWC, pixel stride res_ld
+  float* y;            // output NHWC, pixel stride y_ld, channel offset y_off
+  float* part;         // split-K partials [nsplit][M][Co] (set by launch_conv)
+  int N, Hi, Wi, Ci, x_ld;
+  int Ho, Wo, Co, kh, kw, stride, pad, dil;
+  int M, K, ktiles, kt_per_split;
+  int y_ld, y_off, res_ld;
+  int relu;
+};
+
+struct ConvPlan {
+  int bm = 128, bn = 128, kt_per_split = 1, nsplit = 1;
+};
+
+ConvPlan plan_conv(int M, int Co, int K);
+int launch_conv(ConvArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats, hipStream_t st);
+
+// backbone helpers (backbone.hip)
+int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const float* scale,
+                      const float* shift, float* out, int Ho, hipStream_t st);
+int launch_maxpool3s2(const float* in, int N, int H, int W, int C, float* out, int Ho, int Wo,
+                      hipStream_t st);
+int launch_ppm(const float* cat, int N, int h, int w, int ld, const int* bins, int nbins,
+               float* colsum, float* pooled, hipStream_t st);
+int launch_ppm_upsample(const float* ppm_out, int N, int h, int w, const int* bins, int nbins,
+                        int red, float* cat, int ld, int off, hipStream_t st);
+
+}  // namespace cwt

@@ -1,0 +1,103 @@
+"""Multi-GPU plumbing: one process per GPU, torch.distributed over RCCL ("nccl" backend on
+ROCm) on the GPU box, gloo in the CPU tests.
+
+The CWT path has exactly two exchange points:
+  * training: the mean of the CWT gradients, ONE all-reduce of the flat 2,098,688-float
+    (H=4) bucket per step, before the identical SGD step on every rank;
+  * inference: one sum all-reduce of the per-class intersection/union table at the end of
+    a run (episodes are sharded round-robin, no data-path collective).
+The reference's own DDP code (src/train_ddp.py:106-119) wraps a different model (MMN) and
+is not runnable; this is the CWT's equivalent, not a translation of it.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def rank_world() -> Tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def init_from_env(backend: str | None = None) -> Tuple[int, int, int]:
+    """Initialise from torchrun's env (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*).  Returns
+    (rank, local_rank, world)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+    return rank, local, world
+
+
+def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:
+    """In-place mean over ranks of one flat bucket (the CWT gradient)."""
+    _, world = rank_world()
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t.div_(world)
+    return t
+
+
+def _reduce_device() -> torch.device:
+    if dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def all_reduce_sum_np(a: np.ndarray) -> np.ndarray:
+    _, world = rank_world()
+    if world == 1:
+        return a
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(_reduce_device())
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+def all_reduce_mean_scalar(x: float) -> float:
+    _, world = rank_world()
+    if world == 1:
+        return x
+    return float(all_reduce_sum_np(np.array([x]))[0] / world)
+
+
+def all_reduce_max_scalar(x: float) -> float:
+    _, world = rank_world()
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=_reduce_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def union_keys(keys: List[int], max_keys: int = 128) -> List[int]:
+    """Union of integer class ids over ranks (fixed-size all-reduce of a presence mask)."""
+    _, world = rank_world()
+    if world == 1:
+        return sorted(keys)
+    mask = np.zeros(max_keys)
+    for k in keys:
+        mask[int(k)] = 1
+    mask = all_reduce_sum_np(mask)
+    return [i for i in range(max_keys) if mask[i] > 0]
+
+
+def barrier():
+    if rank_world()[1] > 1:
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()

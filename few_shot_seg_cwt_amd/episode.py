@@ -1,0 +1,328 @@
+"""Episode drivers: the build's counterparts of the reference's ``validate_transformer``
+(src/test.py:103-254) and ``do_epoch`` (src/train.py:166-288), plus the device-resident
+single-episode pipeline they (and bench.py) are built from.
+
+Order of operations per inference episode (test.py:138-219):
+  extract_features(support ++ query)   one backbone pass over shot+1 images (batching the
+                                       query with the support is exact: eval-mode BN)
+  inner_adapt(f_s, s_label, W0)        200 fused SGD steps            (test.py:180-187)
+  normalize(f_q) + pred_q0 = W . f_q   one pass                        (test.py:190-194)
+  W' = CWT(W, f_hat, f_hat)                                            (test.py:195-197)
+  pred_q = W' . f_hat                                                  (test.py:200-204)
+  upsample + argmax + IoU + CE         for pred_q and pred_q0          (test.py:214-224)
+Everything stays on the device; the host reads back per-episode IoU counts only.
+"""
+from __future__ import annotations
+
+import time
+from collections import defaultdict
+from typing import Iterable, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import dist as cdist
+from .synthetic import feature_side, make_episode, pascal_val_classes
+from .util import AverageMeter, seg_metrics
+
+
+def _a(args, k, default=None):
+    if isinstance(args, dict):
+        return args.get(k, default)
+    return getattr(args, k, default)
+
+
+# --------------------------------------------------------------------------------------
+# device primitives
+# --------------------------------------------------------------------------------------
+
+def inner_adapt(f_s: torch.Tensor, s_label: torch.Tensor, W: torch.Tensor, lr: float, iters: int) -> torch.Tensor:
+    """Support-set inner loop, in place on W [2,512] (test.py:164-187; train.py:206-231).
+    f_s [n,512,h,w] channels_last; s_label [n,S,S] int64."""
+    _lib.require(f_s, "f_s")
+    _lib.require(s_label, "s_label", torch.int64)
+    _lib.require(W, "W")
+    n, Cc, h, w = f_s.shape
+    if not f_s.is_contiguous(memory_format=torch.channels_last):
+        f_s = f_s.contiguous(memory_format=torch.channels_last)
+    S = s_label.shape[-1]
+    lbl = s_label.reshape(n, S, S).contiguous()
+    assert W.is_contiguous() and W.numel() == 2 * Cc
+    _lib.check(_lib.lib().cwt_inner_adapt(_lib.ctx(W.device.index), _lib.ptr(f_s), _lib.ptr(lbl), n, h, w, Cc, S,
+                                          float(lr), int(iters), _lib.ptr(W), _lib.stream_ptr(W.device)),
+               "cwt_inner_adapt")
+    return W
+
+
+def normalize(f: torch.Tensor, W0: torch.Tensor | None = None):
+    """F.normalize(f, dim=1) (+ baseline logits W0 . f). f [B,512,h,w] channels_last."""
+    B, Cc, h, w = f.shape
+    out = torch.empty_like(f, memory_format=torch.channels_last)
+    logits0 = torch.empty((B, 2, h, w), device=f.device, dtype=torch.float32) if W0 is not None else None
+    _lib.check(_lib.lib().cwt_normalize(_lib.ctx(f.device.index), _lib.ptr(f), B, h * w, Cc, _lib.ptr(out),
+                                        _lib.ptr(W0), _lib.ptr(logits0), _lib.stream_ptr(f.device)), "cwt_normalize")
+    return out, logits0
+
+
+def classify(W: torch.Tensor, f: torch.Tensor) -> torch.Tensor:
+    """W [B,2,512] . f [B,512,h,w] (channels_last) -> logits [B,2,h,w]."""
+    B, Cc, h, w = f.shape
+    logits = torch.empty((B, 2, h, w), device=f.device, dtype=torch.float32)
+    _lib.check(_lib.lib().cwt_classify(_lib.ctx(f.device.index), _lib.ptr(W.contiguous()), _lib.ptr(f), B, h * w, Cc,
+                                       _lib.ptr(logits), _lib.stream_ptr(f.device)), "cwt_classify")
+    return logits
+
+
+def classify_bwd(dlogits: torch.Tensor, f: torch.Tensor, dW: torch.Tensor):
+    B, Cc, h, w = f.shape
+    _lib.check(_lib.lib().cwt_classify_bwd(_lib.ctx(f.device.index), _lib.ptr(dlogits.contiguous()), _lib.ptr(f), B,
+                                           h * w, Cc, _lib.ptr(dW), _lib.stream_ptr(f.device)), "cwt_classify_bwd")
+    return dW
+
+
+def seg_ce_fwd_bwd(logits: torch.Tensor, target: torch.Tensor):
+    """Query CE with class weight [1, #bg/(#fg+1e-12)] (train.py:237-243,261-265):
+    returns (loss [1] device, dlogits [B,2,h,w])."""
+    B, _, h, w = logits.shape
+    S = target.shape[-1]
+    loss = torch.empty(1, device=logits.device, dtype=torch.float32)
+    dl = torch.empty_like(logits)
+    _lib.check(_lib.lib().cwt_seg_ce_fwd_bwd(_lib.ctx(logits.device.index), _lib.ptr(logits.contiguous()),
+                                             _lib.ptr(target.contiguous()), B, h, w, S, _lib.ptr(loss), _lib.ptr(dl),
+                                             _lib.stream_ptr(logits.device)), "cwt_seg_ce_fwd_bwd")
+    return loss, dl
+
+
+class EpisodeEngine:
+    """Device-resident CWT inference episode (batch_size_val = 1), no host syncs."""
+
+    def __init__(self, model, transformer, args):
+        self.model, self.transformer = model, transformer
+        self.S = int(_a(args, "image_size", 473))
+        self.h = feature_side(self.S)
+        self.shot = int(_a(args, "shot", 1))
+        self.lr = float(_a(args, "cls_lr", 0.1))
+        self.iters = int(_a(args, "adapt_iter", 200))
+
+    @torch.no_grad()
+    def run(self, imgs: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor, W0: torch.Tensor) -> dict:
+        """imgs [shot+1,3,S,S] (supports then query), s_label [shot,S,S], q_label [1,S,S] int64,
+        W0 [2,512] (consumed: adapted in place)."""
+        shot = imgs.shape[0] - 1
+        f_all, _ = self.model.extract_features(imgs)
+        f_s, f_q = f_all[:shot], f_all[shot:]
+        W = inner_adapt(f_s, s_label, W0, self.lr, self.iters)
+        Wb = W.view(1, 2, -1)
+        fqn, pred_q0 = normalize(f_q, Wb)
+        W2 = self.transformer(Wb, fqn, fqn)
+        pred_q = classify(W2, fqn)
+        iut, ce = seg_metrics(pred_q, q_label)
+        iut0, _ = seg_metrics(pred_q0, q_label, with_ce=False)
+        return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, f_s=f_s, f_q=f_q)
+
+
+def new_binary_classifier_weight(bottleneck_dim: int = 512, num_classes: int = 2) -> torch.Tensor:
+    """W0 exactly as the reference draws it: nn.Conv2d(512, 2, 1, bias=False) constructed on the
+    host from the global torch RNG (test.py:164; train.py:206), returned as [2,512]."""
+    conv = torch.nn.Conv2d(bottleneck_dim, num_classes, kernel_size=1, bias=False)
+    return conv.weight.detach().reshape(num_classes, bottleneck_dim).clone()
+
+
+def _class_weight_check(s_label_cpu: torch.Tensor):
+    # test.py:169-175: len(back_pix) / len(target_pix) raises ZeroDivisionError without FG
+    arr = s_label_cpu.numpy()
+    nf = int(np.count_nonzero(arr == 1))
+    nb = int(np.count_nonzero(arr == 0))
+    return nb / nf
+
+
+# --------------------------------------------------------------------------------------
+# loaders
+# --------------------------------------------------------------------------------------
+
+class SyntheticEpisodes:
+    """Episode loader yielding the reference 7-tuple (dataset.py:326-327) as CPU tensors;
+    its iterator has ``.next()`` like the torch-1.6 DataLoader iterators the reference uses."""
+
+    def __init__(self, n: int, S: int = 473, shot: int = 1, seed: int = 2021, start: int = 0, classes=None,
+                 stride: int = 1):
+        self.n, self.S, self.shot, self.seed, self.start, self.classes, self.stride = n, S, shot, seed, start, \
+            classes or pascal_val_classes(0), stride
+
+    def __len__(self):
+        return self.n
+
+    def episode(self, i: int):
+        ep = make_episode(self.seed, self.start + i * self.stride, self.S, self.shot, self.classes)
+        t = torch.from_numpy
+        return (t(ep["qry_img"]), t(ep["q_label"]), t(ep["spprt_imgs"]), t(ep["s_label"]),
+                [torch.tensor([c]) for c in ep["subcls"]], "", "")
+
+    def __iter__(self):
+        outer = self
+
+        class _It:
+            def __init__(self):
+                self.i = 0
+
+            def next(self):
+                r = outer.episode(self.i % outer.n)
+                self.i += 1
+                return r
+
+            __next__ = next
+
+        return _It()
+
+
+# --------------------------------------------------------------------------------------
+# validate_transformer (test.py:103-254)
+# --------------------------------------------------------------------------------------
+
+def validate_transformer(args, val_loader, model, transformer, episodes_out: list | None = None) -> Tuple[float, float]:
+    """Mirror of the reference's validate_transformer for batch_size_val = 1.  Returns
+    (mean mIoU over runs, mean loss).  With torch.distributed initialised, rank r runs the
+    episodes e with e % world == r and the per-class intersection/union sums are all-reduced
+    once at the end of each run."""
+    if int(_a(args, "batch_size_val", 1)) != 1:
+        raise NotImplementedError("batch_size_val must be 1 (scripts/test.sh)")
+    model.eval()
+    transformer.eval()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    engine = EpisodeEngine(model, transformer, args)
+    nb_episodes = int(_a(args, "test_num", 1000))
+    n_runs = int(_a(args, "n_runs", 1))
+    rank, world = cdist.rank_world()
+    runtimes = np.zeros(n_runs)
+    val_IoUs = np.zeros(n_runs)
+    val_losses = np.zeros(n_runs)
+    it = iter(val_loader)
+    for run in range(n_runs):
+        loss_meter = AverageMeter()
+        runtime = 0.0
+        cls_iu = defaultdict(lambda: np.zeros(2))
+        cls_iu0 = defaultdict(lambda: np.zeros(2))
+        for e in range(nb_episodes):
+            qry_img, q_label, spprt_imgs, s_label, subcls, _, _ = it.next() if hasattr(it, "next") else next(it)
+            W0 = new_binary_classifier_weight()          # consumes the torch RNG like test.py:164
+            new_binary_classifier_weight()               # ... and like Pseudo_cls (test.py:200)
+            if e % world != rank:
+                continue
+            t0 = time.time()
+            _class_weight_check(s_label)
+            imgs = torch.cat([spprt_imgs[0], qry_img], 0).to(dev, non_blocking=True)
+            sl = s_label[0].to(dev, non_blocking=True)
+            ql = q_label.to(dev, non_blocking=True)
+            r = engine.run(imgs, sl, ql, W0.to(dev))
+            iut = r["iut"].cpu().numpy()[0]
+            iut0 = r["iut0"].cpu().numpy()[0]
+            ce = r["ce"].cpu().numpy()[0]
+            runtime += time.time() - t0
+            loss_meter.update(float(ce[0] / max(ce[1], 1.0)))
+            for c in [int(x.item()) for x in subcls]:
+                cls_iu[c] += (iut[0, 1], iut[1, 1])       # FG only (test.py:227-228)
+                cls_iu0[c] += (iut0[0, 1], iut0[1, 1])
+            if episodes_out is not None:
+                episodes_out.append({k: (v.detach().cpu() if isinstance(v, torch.Tensor) else v)
+                                     for k, v in r.items() if k not in ("f_s", "f_q")})
+        classes = sorted(set(cls_iu) | set(cls_iu0))
+        if world > 1:
+            classes = cdist.union_keys(classes)
+            table = np.array([[*cls_iu[c], *cls_iu0[c]] for c in classes], dtype=np.float64)
+            table = cdist.all_reduce_sum_np(table)
+            for c, row in zip(classes, table):
+                cls_iu[c] = row[:2]
+                cls_iu0[c] = row[2:]
+            loss_meter.avg = cdist.all_reduce_mean_scalar(loss_meter.avg)
+        IoU = {c: cls_iu[c][0] / (cls_iu[c][1] + 1e-10) for c in classes}
+        mIoU = float(np.mean(list(IoU.values()))) if IoU else 0.0
+        if rank == 0:
+            print("mIoU---Val result: mIoU {:.4f}.".format(mIoU))
+            for c in classes:
+                print("Class {} : {:.4f}".format(c, IoU[c]))
+        runtimes[run] = runtime
+        val_IoUs[run] = mIoU
+        val_losses[run] = loss_meter.avg
+    if rank == 0:
+        print("Average mIoU over {} runs --- {:.4f}.".format(n_runs, val_IoUs.mean()))
+        print("Average runtime / run --- {:.4f}.".format(runtimes.mean()))
+    return float(val_IoUs.mean()), float(val_losses.mean())
+
+
+# --------------------------------------------------------------------------------------
+# do_epoch (train.py:166-288)
+# --------------------------------------------------------------------------------------
+
+def train_episode(model, transformer, args, batch, W0: torch.Tensor, dev) -> dict:
+    """Forward/backward of one training episode (train.py:188-267) without the optimiser
+    step; gradients are ACCUMULATED into transformer.flat.grad.  Backbone eval (frozen),
+    CWT dropout off.  The 1-shot support is not duplicated: the reference's two identical
+    copies (train.py:199-201) give exactly the same inner-loop loss and gradient as one."""
+    qry_img, q_label, spprt_imgs, s_label, subcls = batch[:5]
+    S = int(_a(args, "image_size", 473))
+    shot = spprt_imgs.shape[1]
+    _class_weight_check(s_label)
+    imgs = torch.cat([spprt_imgs[0], qry_img], 0).to(dev, non_blocking=True)
+    sl = s_label[0].to(dev, non_blocking=True).long()
+    ql = q_label.to(dev, non_blocking=True).long()
+    f_all, _ = model.extract_features(imgs)
+    f_s, f_q = f_all[:shot], f_all[shot:]
+    W = inner_adapt(f_s, sl, W0.to(dev), float(_a(args, "cls_lr", 0.1)), int(_a(args, "adapt_iter", 200)))
+    Wb = W.view(1, 2, -1)
+    fqn, pred_q0 = normalize(f_q, Wb)
+    W2, state = transformer.forward_train(Wb, fqn)
+    pred_q = classify(W2, fqn)
+    loss, dl = seg_ce_fwd_bwd(pred_q, ql)
+    dW2 = torch.zeros_like(W2)
+    classify_bwd(dl, fqn, dW2)
+    transformer.backward_into(state, dW2)
+    iut, _ = seg_metrics(pred_q, ql, with_ce=False)
+    iut0, _ = seg_metrics(pred_q0, ql, with_ce=False)
+    return dict(loss=loss, W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0)
+
+
+def do_epoch(args, train_loader, model, transformer, optimizer_trans, epoch: int, iter_per_epoch: int,
+             log_iter: int, records: list | None = None):
+    """Mirror of train.py:166-288 (batch_size 1).  With torch.distributed initialised each
+    rank runs its own episode per iteration and the CWT gradient bucket is all-reduced
+    (mean) before the identical SGD step on every rank."""
+    if int(_a(args, "batch_size", 1)) != 1:
+        raise NotImplementedError("batch_size must be 1 (scripts/train.sh)")
+    dev = torch.device("cuda", torch.cuda.current_device())
+    loss_meter = AverageMeter()
+    train_losses = torch.zeros(log_iter)
+    train_Ious = torch.zeros(log_iter)
+    train_Ious0 = torch.zeros(log_iter)
+    it = iter(train_loader)
+    model.train()
+    transformer.train()
+    rank, world = cdist.rank_world()
+    for i in range(iter_per_epoch):
+        batch = it.next() if hasattr(it, "next") else next(it)
+        W0 = new_binary_classifier_weight()              # train.py:206
+        if transformer.flat.grad is None:
+            transformer.flat.grad = torch.zeros_like(transformer.flat)
+        optimizer_trans.zero_grad()
+        r = train_episode(model, transformer, args, batch, W0, dev)
+        if world > 1:
+            cdist.all_reduce_mean_(transformer.flat.grad)
+        optimizer_trans.step()
+        loss = float(r["loss"].item())
+        iut = r["iut"].cpu().numpy()[0]
+        iut0 = r["iut0"].cpu().numpy()[0]
+        IoUb, IoUf = iut[0] / (iut[1] + 1e-10)
+        IoUb0, IoUf0 = iut0[0] / (iut0[1] + 1e-10)
+        loss_meter.update(loss / 1)
+        train_losses[i] = loss_meter.avg
+        train_Ious[i] = float((IoUb + IoUf) / 2)
+        train_Ious0[i] = float((IoUb0 + IoUf0) / 2)
+        if records is not None:
+            records.append(dict(loss=loss, W=r["W"].detach().cpu(), W2=r["W2"].detach().cpu(),
+                                grad=transformer.flat.grad.detach().cpu().clone()))
+        if ((epoch == 0 and i % 100 == 0) or i % 500 == 0) and rank == 0:
+            print("iter {} IoUf {:.2f}, IoUb {:.2f}, IoUf0 {:.2f}, IoUb0 {:.2f}".format(i, IoUf, IoUb, IoUf0, IoUb0))
+    if rank == 0:
+        print("Epoch {}: The mIoU {:.2f}, loss {:.2f}, mIoU0 {:.2f}".format(
+            epoch + 1, train_Ious.mean(), train_losses.mean(), train_Ious0.mean()))
+    return train_Ious, train_losses

@@ -1,0 +1,135 @@
+"""Drop-in for the reference's frozen feature extractor (src/model/pspnet.py).
+
+``get_model(args)`` returns a :class:`PSPNet` whose ``extract_features(x)`` has the
+reference signature (pspnet.py:172-181): ``x`` [N,3,S,S] fp32 -> ``(f [N,512,h,w], [])``.
+The whole extractor (stem, 16/33 dilated bottlenecks, PPM, 3x3 bottleneck conv) runs as
+HIP kernels in libcwt.so; ``f`` is returned as an [N,512,h,w] tensor in channels_last
+memory format (NHWC), which is what every downstream kernel reads.
+
+Weights are loaded with ``load_state_dict`` using the reference key names (the
+reference's ``PSPNet.state_dict()``, `gamma` first, pspnet.py:141).  Only eval semantics
+are implemented: the backbone is frozen in every CWT driver (train.py:77-91); the
+reference's first-episode train-mode BN quirk (train.py:184) is out of scope.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+from .synthetic import BN_EPS, feature_side, pspnet_param_specs
+
+
+def get_model(args) -> "PSPNet":
+    """pspnet.py:15 get_model(args) -> PSPNet(args, zoom_factor=8, use_ppm=True)."""
+    return PSPNet(args)
+
+
+def _arg(args, k, default=None):
+    if isinstance(args, dict):
+        return args.get(k, default)
+    return getattr(args, k, default)
+
+
+class PSPNet:
+    """Frozen ResNet-50/101 + PPM extractor on MI355X (pspnet.py:70-141)."""
+
+    def __init__(self, args, device=None):
+        self.layers = int(_arg(args, "layers", 50))
+        if self.layers not in (50, 101):
+            raise ValueError("layers must be 50 or 101")
+        if _arg(args, "arch", "resnet") != "resnet":
+            raise NotImplementedError("only arch=resnet is on the CWT path (vgg is out of scope)")
+        if list(_arg(args, "bins", [1, 2, 3, 6])) != [1, 2, 3, 6]:
+            raise NotImplementedError("PPM bins must be [1, 2, 3, 6] (pascal.yaml:48)")
+        if int(_arg(args, "bottleneck_dim", 512)) != 512:
+            raise NotImplementedError("bottleneck_dim must be 512")
+        if _arg(args, "m_scale", False):
+            raise NotImplementedError("m_scale is not on the CWT path")
+        self.bottleneck_dim = 512
+        self.device = torch.device("cuda", device if device is not None else torch.cuda.current_device()) \
+            if torch.cuda.is_available() else None
+        self._state = None
+        self.training = False
+
+    # -- nn.Module-like surface used by the drivers --------------------------------------
+    def eval(self):
+        self.training = False
+        return self
+
+    def train(self, mode: bool = True):
+        # Eval semantics only (frozen backbone); see module docstring.
+        self.training = False
+        return self
+
+    def cuda(self, *a, **k):
+        return self
+
+    def parameters(self):
+        return iter(())
+
+    def state_dict(self):
+        if self._state is None:
+            raise RuntimeError("no weights loaded")
+        return OrderedDict((k, torch.from_numpy(np.array(v))) for k, v in self._state.items())
+
+    def load_state_dict(self, state_dict, strict: bool = True):
+        """Accepts the reference PSPNet.state_dict() (torch tensors or numpy arrays).
+        Keys may carry the DDP 'module.' prefix (train.py:67-68, convert_pth.py:9-14)."""
+        sd = OrderedDict()
+        for k, v in state_dict.items():
+            k = k[7:] if k.startswith("module.") else k
+            sd[k] = v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v)
+        specs = pspnet_param_specs(self.layers, self.bottleneck_dim)
+        if strict:
+            want = {n for n, _, _ in specs}
+            missing = [n for n in want if n not in sd]
+            if missing:
+                raise KeyError(f"missing keys in state_dict: {missing[:5]}{'...' if len(missing) > 5 else ''}")
+        names, ptrs, numels, keep = [], [], [], []
+        for n, shape, kind in specs:
+            if n not in sd or kind in ("bn_nbt", "gamma", "cls"):
+                continue
+            a = np.ascontiguousarray(sd[n], dtype=np.float32)
+            if tuple(a.shape) != tuple(shape):
+                raise ValueError(f"{n}: shape {a.shape} != {shape}")
+            keep.append(a)
+            names.append(n.encode())
+            ptrs.append(a.ctypes.data)
+            numels.append(a.size)
+        lib = _lib.lib()
+        arr_n = (C.c_char_p * len(names))(*names)
+        arr_p = (C.c_void_p * len(ptrs))(*ptrs)
+        arr_e = (C.c_int64 * len(numels))(*numels)
+        _lib.check(lib.cwt_backbone_load(_lib.ctx(), self.layers, len(names), arr_n, arr_p, arr_e, BN_EPS),
+                   "cwt_backbone_load")
+        self._state = sd
+        return self
+
+    def feature_res(self, S: int):
+        h = feature_side(S)
+        return (h, h)
+
+    # -- hot path ------------------------------------------------------------------------
+    def extract_features(self, x: torch.Tensor, out: torch.Tensor | None = None):
+        """pspnet.py:172-181: returns (f [N,512,h,w] channels_last, [])."""
+        if self._state is None:
+            raise RuntimeError("load_state_dict first")
+        _lib.require(x, "x")
+        if x.dim() != 4 or x.shape[1] != 3 or x.shape[2] != x.shape[3]:
+            raise ValueError(f"x must be [N,3,S,S], got {tuple(x.shape)}")
+        N, _, S, _ = x.shape
+        assert (S - 1) % 8 == 0, "pspnet.py:150: (S-1) % 8 == 0"
+        h = feature_side(S)
+        x = x.contiguous()
+        if out is None:
+            out = torch.empty((N, 512, h, h), device=x.device, dtype=torch.float32,
+                              memory_format=torch.channels_last)
+        _lib.check(_lib.lib().cwt_extract_features(_lib.ctx(x.device.index), _lib.ptr(x), N, S, _lib.ptr(out),
+                                                   _lib.stream_ptr(x.device)), "cwt_extract_features")
+        return out, []
+
+    __call__ = extract_features

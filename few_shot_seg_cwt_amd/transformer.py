@@ -1,0 +1,187 @@
+"""Drop-in for the reference's Classifier Weight Transformer (src/model/transformer.py:33-83).
+
+``MultiHeadAttentionOne(n_head, d_model, d_k, d_v, dropout)`` keeps the reference
+constructor, ``forward(q, k, v) -> [B, 2, d_model]`` signature and state_dict keys
+(``w_qkvs.weight``, ``layer_norm.{weight,bias}``, ``fc.{weight,bias}``).  The forward and
+the parameter backward run as HIP kernels (libcwt.so, cwt_attention_fwd/bwd) in the
+re-associated form described in cwt_attn.hip / DESIGN.md.
+
+All parameters live in ONE flat fp32 device buffer (``self.flat``); the named tensors are
+views of it.  That makes the 8-GPU gradient all-reduce one RCCL call on one bucket and the
+outer SGD step one kernel.
+
+Differences from the reference, by design: k and v must be the same tensor
+(the only way the CWT drivers call it, test.py:197 / train.py:257); dropout layers are
+not applied (the parity runs of the training path use p = 0).
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _layout(heads: int, C: int):
+    names = [("w_qkvs.weight", (heads * C, C)), ("layer_norm.weight", (C,)), ("layer_norm.bias", (C,)),
+             ("fc.weight", (C, heads * C)), ("fc.bias", (C,))]
+    out, off = [], 0
+    for n, shp in names:
+        k = int(np.prod(shp))
+        out.append((n, shp, off, k))
+        off += k
+    return out, off
+
+
+def as_tokens(k: torch.Tensor) -> torch.Tensor:
+    """[B,C,h,w] (any memory format) -> NHWC-contiguous [B,h,w,C] storage, returned as [B,C,h,w]
+    channels_last so its data_ptr is the token-major [B, hw, C] map the kernels read."""
+    if k.dim() == 3:  # [B, hw, C] tokens already
+        return k.contiguous()
+    return k.contiguous(memory_format=torch.channels_last)
+
+
+class _CWTFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, f, flat, mod):
+        out, saved = mod._fwd(q, f, need_saved=True)
+        ctx.mod = mod
+        ctx.save_for_backward(q, f, flat)
+        ctx.saved_buf = saved
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        q, f, flat = ctx.saved_tensors
+        g = torch.zeros_like(flat)
+        ctx.mod._bwd(q, f, ctx.saved_buf, d_out.contiguous(), g)
+        return None, None, g, None
+
+
+class MultiHeadAttentionOne(torch.nn.Module):
+    """transformer.py:33-83 (shared projection, d_k = d_v = d_model per head)."""
+
+    def __init__(self, n_head: int, d_model: int, d_k: int, d_v: int, dropout: float = 0.1, device=None):
+        super().__init__()
+        if not (d_model == d_k == d_v == 512):
+            raise NotImplementedError("the CWT path uses d_model = d_k = d_v = 512 (test.py:57)")
+        if n_head not in (1, 2, 4):
+            raise NotImplementedError("n_head must be 1, 2 or 4 (heads 1 in the yaml, 4 in scripts/*.sh)")
+        self.n_head, self.d_model = n_head, d_model
+        self.dropout_p = dropout  # recorded, not applied (module docstring)
+        self._layout, total = _layout(n_head, d_model)
+        dev = torch.device("cuda", device if device is not None else torch.cuda.current_device()) \
+            if torch.cuda.is_available() else torch.device("cpu")
+        self.flat = torch.nn.Parameter(torch.zeros(total, dtype=torch.float32, device=dev))
+        self._init_reference_like()
+
+    # -- parameters -----------------------------------------------------------------------
+    def _init_reference_like(self):
+        """transformer.py:45,51 init: w_qkvs ~ N(0, sqrt(2/(d_model+d_k))), fc xavier_normal,
+        LayerNorm (1, 0), fc.bias U(+-1/sqrt(fan_in)) (nn.Linear default)."""
+        C, H = self.d_model, self.n_head
+        with torch.no_grad():
+            self.view("w_qkvs.weight").normal_(0, math.sqrt(2.0 / (2 * C)))
+            self.view("layer_norm.weight").fill_(1.0)
+            self.view("layer_norm.bias").zero_()
+            self.view("fc.weight").normal_(0, math.sqrt(2.0 / (H * C + C)))
+            b = 1.0 / math.sqrt(H * C)
+            self.view("fc.bias").uniform_(-b, b)
+
+    def view(self, name: str, t: torch.Tensor | None = None) -> torch.Tensor:
+        t = self.flat if t is None else t
+        for n, shp, off, k in self._layout:
+            if n == name:
+                return t.data[off:off + k].view(shp) if t is self.flat else t[off:off + k].view(shp)
+        raise KeyError(name)
+
+    def state_dict(self, *a, **k):
+        return OrderedDict((n, self.flat.data[off:off + kk].view(shp).clone()) for n, shp, off, kk in self._layout)
+
+    def load_state_dict(self, sd, strict: bool = True):
+        for n, shp, off, k in self._layout:
+            if n not in sd:
+                if strict:
+                    raise KeyError(n)
+                continue
+            v = sd[n]
+            v = torch.as_tensor(np.asarray(v)) if not isinstance(v, torch.Tensor) else v
+            if tuple(v.shape) != tuple(shp):
+                raise ValueError(f"{n}: {tuple(v.shape)} != {shp}")
+            with torch.no_grad():
+                self.flat.data[off:off + k].copy_(v.reshape(-1).to(self.flat.device, torch.float32))
+        return self
+
+    def named_views(self):
+        return [(n, self.flat.data[off:off + k].view(shp)) for n, shp, off, k in self._layout]
+
+    # -- kernels --------------------------------------------------------------------------
+    def _ptrs(self, t: torch.Tensor):
+        return [_lib.ptr(self.view(n, t)) for n in ("w_qkvs.weight", "fc.weight", "fc.bias", "layer_norm.weight",
+                                                    "layer_norm.bias")]
+
+    def _check(self, q, f):
+        _lib.require(q, "q")
+        _lib.require(f, "k")
+        if q.dim() != 3 or q.shape[1] != 2 or q.shape[2] != self.d_model:
+            raise ValueError(f"q must be [B,2,{self.d_model}], got {tuple(q.shape)}")
+        B = q.shape[0]
+        if f.dim() == 4:
+            if f.shape[0] != B or f.shape[1] != self.d_model:
+                raise ValueError(f"k must be [B,{self.d_model},h,w], got {tuple(f.shape)}")
+            hw = f.shape[2] * f.shape[3]
+        else:
+            hw = f.shape[1]
+        return B, hw
+
+    def _fwd(self, q, f, need_saved: bool):
+        q = q.contiguous()
+        B, hw = self._check(q, f)
+        out = torch.empty((B, 2, self.d_model), device=q.device, dtype=torch.float32)
+        saved = None
+        if need_saved:
+            n = _lib.lib().cwt_attention_saved_floats(B, hw, self.d_model, self.n_head)
+            saved = torch.empty(n, device=q.device, dtype=torch.float32)
+        w, fw, fb, lw, lb = self._ptrs(self.flat)
+        _lib.check(_lib.lib().cwt_attention_fwd(_lib.ctx(q.device.index), _lib.ptr(q), _lib.ptr(f), B, hw,
+                                                self.d_model, self.n_head, w, fw, fb, lw, lb, _lib.ptr(out),
+                                                _lib.ptr(saved), _lib.stream_ptr(q.device)), "cwt_attention_fwd")
+        return out, saved
+
+    def _bwd(self, q, f, saved, d_out, grad_flat):
+        B, hw = self._check(q, f)
+        w, fw, fb, lw, lb = self._ptrs(self.flat)
+        gw, gfw, gfb, glw, glb = self._ptrs(grad_flat)
+        _lib.check(_lib.lib().cwt_attention_bwd(_lib.ctx(q.device.index), _lib.ptr(q), _lib.ptr(f), B, hw,
+                                                self.d_model, self.n_head, w, fw, fb, lw, lb, _lib.ptr(saved),
+                                                _lib.ptr(d_out), gw, gfw, gfb, glw, glb,
+                                                _lib.stream_ptr(q.device)), "cwt_attention_bwd")
+
+    # -- reference API --------------------------------------------------------------------
+    def forward(self, q, k, v, query_input=False):
+        """transformer.py:54: q [B,2,512]; k = v = normalised query features [B,512,h,w]."""
+        if k is not v and k.data_ptr() != v.data_ptr():
+            raise NotImplementedError("CWT kernels attend with k == v (test.py:197, train.py:257)")
+        f = as_tokens(k)
+        if torch.is_grad_enabled() and self.flat.requires_grad:
+            return _CWTFunction.apply(q, f, self.flat, self)
+        out, _ = self._fwd(q, f, need_saved=False)
+        return out
+
+    # explicit training API (no autograd graph; used by the episode drivers)
+    def forward_train(self, q, f):
+        f = as_tokens(f)
+        out, saved = self._fwd(q, f, need_saved=True)
+        return out, (q.contiguous(), f, saved)
+
+    def backward_into(self, state, d_out, grad_flat=None):
+        q, f, saved = state
+        if grad_flat is None:
+            if self.flat.grad is None:
+                self.flat.grad = torch.zeros_like(self.flat)
+            grad_flat = self.flat.grad
+        self._bwd(q, f, saved, d_out.contiguous(), grad_flat)
+        return grad_flat

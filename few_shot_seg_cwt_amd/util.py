@@ -1,0 +1,78 @@
+"""Metrics of the CWT drivers (reference src/util.py:199-308), on the device.
+
+``intersectionAndUnionGPU`` / ``batch_intersectionAndUnionGPU`` keep the reference
+signatures and return float tensors like ``torch.histc`` does, but the upsample, argmax
+and histogram run as one HIP kernel (cwt_seg_metrics / cwt_iou_preds) instead of
+materialising S x S logits.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from . import _lib
+
+
+class AverageMeter:
+    """util.py:199-214."""
+
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.val = 0
+        self.avg = 0
+        self.sum = 0
+        self.count = 0
+
+    def update(self, val, n=1):
+        self.val = val
+        self.sum += val * n
+        self.count += n
+        self.avg = self.sum / self.count
+
+
+def intersectionAndUnionGPU(preds: torch.Tensor, target: torch.Tensor, num_classes: int,
+                            ignore_index: int = 255) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """util.py:280-308 on argmax maps: returns (intersection, union, target) [num_classes] float."""
+    assert preds.dim() in (1, 2, 3)
+    assert preds.shape == target.shape
+    _lib.require(preds, "preds", torch.int64)
+    _lib.require(target, "target", torch.int64)
+    p, t = preds.contiguous(), target.contiguous()
+    out = torch.empty((3, num_classes), device=p.device, dtype=torch.float32)
+    _lib.check(_lib.lib().cwt_iou_preds(_lib.ctx(p.device.index), _lib.ptr(p), _lib.ptr(t), p.numel(), num_classes,
+                                        ignore_index, _lib.ptr(out), _lib.stream_ptr(p.device)), "cwt_iou_preds")
+    return out[0], out[1], out[2]
+
+
+def seg_metrics(logits: torch.Tensor, target: torch.Tensor, with_ce: bool = True):
+    """Upsample [B,2,h,w] logits to the [B,S,S] target (bilinear, align_corners), argmax,
+    histc (util.py:237-277) and the CE(ignore 255) sum (test.py:222-224).
+    Returns iut [B,3,2] float32 and ce [B,2] float64 (sum nll, count) on the device."""
+    _lib.require(logits, "logits")
+    _lib.require(target, "target", torch.int64)
+    B, nc, h, w = logits.shape
+    if nc != 2:
+        raise NotImplementedError("2-way episodes only (num_classes_tr = 2)")
+    S = target.shape[-1]
+    lg, tg = logits.contiguous(), target.contiguous()
+    iut = torch.empty((B, 3, 2), device=lg.device, dtype=torch.float32)
+    ce = torch.empty((B, 2), device=lg.device, dtype=torch.float64) if with_ce else None
+    _lib.check(_lib.lib().cwt_seg_metrics(_lib.ctx(lg.device.index), _lib.ptr(lg), _lib.ptr(tg), B, h, w, S,
+                                          _lib.ptr(iut), _lib.ptr(ce), _lib.stream_ptr(lg.device)),
+               "cwt_seg_metrics")
+    return iut, ce
+
+
+def batch_intersectionAndUnionGPU(logits: torch.Tensor, target: torch.Tensor, num_classes: int,
+                                  ignore_index: int = 255):
+    """util.py:237-277: logits [n_task, shot, C, h, w], target [n_task, shot, H, W] ->
+    (intersection, union, target) each [n_task, shot, C]."""
+    assert ignore_index == 255
+    n_task, shots, nc, h, w = logits.shape
+    iut, _ = seg_metrics(logits.reshape(n_task * shots, nc, h, w), target.reshape(n_task * shots, *target.shape[-2:]),
+                         with_ce=False)
+    iut = iut.view(n_task, shots, 3, nc)
+    return iut[:, :, 0], iut[:, :, 1], iut[:, :, 2]

@@ -1,0 +1,185 @@
+/*
+ * cwt.h — C ABI of libcwt.so, the MI355X-native CWT episode engine.
+ *
+ * The reference (TeamOfProfGuo/Few_Shot_Seg_CWT) has no FFI layer: its "boundary" is
+ * the PyTorch nn.Module API the episode drivers call.  Each entry
+ * point below replaces one of those call sites; the reference interface is cited above
+ * each declaration.  The ctypes shim in few_shot_seg_cwt_amd/_lib.py binds exactly these.
+ *
+ * Conventions
+ *  - Plain C types only; no C++ types or exceptions cross the boundary.
+ *  - Every device buffer is CALLER-OWNED (e.g. torch tensors via data_ptr()).  The
+ *    library owns only packed weights and an internal workspace pool per context.
+ *  - Every call is asynchronous on the given stream (a hipStream_t passed as void*;
+ *    NULL = the legacy default stream).  Nothing here synchronises the host.
+ *  - Return value: 0 on success, a hipError_t value, or a CWT_E* code below.  The
+ *    message of the last failure on the calling thread: cwt_last_error().
+ *  - One context per device; calls on one context must be externally serialised.
+ *  - Activations are fp32.  Feature maps are NHWC ([N][h][w][C], C contiguous), which
+ *    is torch's channels_last memory format of an [N,C,h,w] tensor.
+ */
+#ifndef CWT_H_
+#define CWT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CWT_OK 0
+#define CWT_EARG 1001      /* invalid argument / shape (reference: shape asserts, pspnet.py:74-76,150) */
+#define CWT_ESTATE 1002    /* weights not loaded / wrong call order */
+#define CWT_ENOFG 1003     /* support mask has no foreground (reference: ZeroDivisionError, test.py:174) */
+
+typedef struct cwt_ctx cwt_ctx;
+
+/* Version string of the library build. */
+const char* cwt_version(void);
+
+/* Thread-local message of the last failing call on this thread ("" if none). */
+const char* cwt_last_error(void);
+
+/* Create / destroy a context bound to HIP device `device`. */
+int cwt_ctx_create(int device, cwt_ctx** out);
+int cwt_ctx_destroy(cwt_ctx* ctx);
+
+/*
+ * Load the frozen PSPNet feature extractor from a state dict given by name.
+ * Replaces: get_model(args) (pspnet.py:15) + PSPNet.__init__ (pspnet.py:70-141) +
+ *           model.load_state_dict(...) (test.py:61-81; train.py:57-75).
+ * names/host_data/numel: n_tensors entries of the reference's PSPNet.state_dict()
+ * (keys as in the reference, e.g. "layer1.0.conv1.weight", "ppm.features.0.2.running_var",
+ * "bottleneck.0.weight"); host_data are host fp32 pointers (integer entries such as
+ * num_batches_tracked may be passed with host_data == NULL and are ignored).
+ * layers: 50 or 101.  BatchNorm (eval mode, eps bn_eps) is folded to per-channel
+ * scale/shift and conv weights are repacked [Co][kh][kw][Ci] on the device.
+ */
+int cwt_backbone_load(cwt_ctx* ctx, int layers, int n_tensors, const char* const* names,
+                      const float* const* host_data, const int64_t* numel, float bn_eps);
+
+/*
+ * Frozen feature extractor forward (eval mode).
+ * Replaces: PSPNet.extract_features(x) -> (f, []) (pspnet.py:172-181; get_feat_list
+ *           pspnet.py:272-287; PPM pspnet.py:33-38; bottleneck pspnet.py:124-129).
+ * img:  device fp32 NCHW [N,3,S,S] (S-1 divisible by 8).
+ * feat: device fp32 NHWC [N,h,w,512] with h = (S-1)/8+1.
+ */
+int cwt_extract_features(cwt_ctx* ctx, const float* img, int N, int S, float* feat, void* stream);
+
+/* Bytes of device workspace the context holds for the last extract shape (for reporting). */
+size_t cwt_workspace_bytes(cwt_ctx* ctx);
+
+/*
+ * Support-set inner loop: `iters` SGD steps of a bias-free 2-way 1x1 classifier on f_s,
+ * loss = weighted CrossEntropy(ignore 255, mean) of the bilinear(align_corners=True)
+ * upsampled logits vs s_label; class weight [1, #bg/#fg] counted on the device.
+ * Replaces: test.py:164-187 and train.py:206-231 (nn.Conv2d(512,2,1) + F.interpolate +
+ *           nn.CrossEntropyLoss(weight, ignore_index=255) + backward + optim.SGD(lr)).
+ * f_s:     device fp32 NHWC [n,h,w,C];  s_label: device int64 [n,S,S] (0, 1, 255).
+ * W_inout: device fp32 [2,C] — W0 on entry, adapted weights on return.
+ * Returns CWT_EARG on bad shapes. A mask without foreground yields an infinite class
+ * weight exactly like the reference; the caller checks counts if it needs to raise.
+ */
+int cwt_inner_adapt(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int n, int h, int w,
+                    int C, int S, float lr, int iters, float* W_inout, void* stream);
+
+/* Per-pixel L2 normalisation over channels, F.normalize(f, dim=1) (test.py:194,
+ * train.py:250): out[p,:] = f[p,:] / max(||f[p,:]||_2, 1e-12).  NHWC [P,C] -> [P,C].
+ * If W0 (device [B,2,C]) and logits0 (device [B,2,P/B]) are non-NULL, also writes the
+ * un-normalised baseline logits W0 . f (test.py:192 pred_q0) in the same pass. */
+int cwt_normalize(cwt_ctx* ctx, const float* f, int B, int P_per_b, int C, float* out,
+                  const float* W0, float* logits0, void* stream);
+
+/*
+ * Classifier Weight Transformer forward: MultiHeadAttentionOne(H, C, C, C).forward(q, k, v)
+ * with k = v = f (transformer.py:54-83, ScaledDotProductAttention transformer.py:23-30),
+ * eval mode (dropouts identity).  Computed in the re-associated form
+ * scores_h = (W_h^T W_h q) . f / sqrt(C), out_h = W_h (softmax . f)  (DESIGN.md §CWT).
+ * q:       device fp32 [B,2,C]         (classifier weights, transformer.py:66 residual)
+ * f:       device fp32 NHWC [B,hw,C]   (normalised query features = keys = values)
+ * w_qkvs:  device fp32 [H*C, C]; fc_w [C, H*C]; fc_b [C]; ln_w [C]; ln_b [C]
+ * out:     device fp32 [B,2,C]
+ * saved:   device fp32 buffer of cwt_attention_saved_floats(B,hw,C,H) floats kept for the
+ *          backward pass, or NULL for inference.
+ */
+int cwt_attention_fwd(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                      const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
+                      const float* ln_b, float* out, float* saved, void* stream);
+size_t cwt_attention_saved_floats(int B, int hw, int C, int H);
+
+/*
+ * Backward of cwt_attention_fwd w.r.t. the transformer parameters (q and f carry no
+ * gradient in the reference: train.py:252-257 passes .data weights and no_grad features).
+ * d_out: device [B,2,C].  Gradients are ACCUMULATED (+=) into g_* (device, same shapes as
+ * the parameters), like autograd's .grad.
+ */
+int cwt_attention_bwd(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                      const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
+                      const float* ln_b, const float* saved, const float* d_out,
+                      float* g_w_qkvs, float* g_fc_w, float* g_fc_b, float* g_ln_w, float* g_ln_b,
+                      void* stream);
+
+/* Per-pixel classifier logits = W . f (test.py:200-204 Pseudo_cls; train.py:259-261 matmul).
+ * W: device [B,2,C]; f: NHWC [B,P,C]; logits: device [B,2,P] (NCHW [B,2,h,w]). */
+int cwt_classify(cwt_ctx* ctx, const float* W, const float* f, int B, int P, int C, float* logits,
+                 void* stream);
+
+/*
+ * Segmentation metrics of low-res logits against a full-res label:
+ * bilinear(align_corners=True) upsample [B,2,h,w] -> [B,2,S,S], argmax over classes,
+ * preds[target==255] = 255, histc intersection / union / target over 2 classes
+ * (util.py:237-308 batch_intersectionAndUnionGPU / intersectionAndUnionGPU), plus the
+ * CrossEntropy(ignore 255) sum and valid-pixel count of the upsampled logits
+ * (test.py:222-224 criterion_standard).
+ * iut_out: device fp32 [B,3,2] (intersection, union, target per class);
+ * ce_out:  device fp64 [B,2] (sum of -log p_y, count) or NULL.
+ */
+int cwt_seg_metrics(cwt_ctx* ctx, const float* logits, const int64_t* target, int B, int h, int w,
+                    int S, float* iut_out, double* ce_out, void* stream);
+
+/*
+ * Weighted CE of upsampled logits and its gradient w.r.t. the low-res logits, for the
+ * outer loop (train.py:237-243,261-265): class weight [1, #bg/(#fg+1e-12)] from target,
+ * loss = sum_p w_y * nll_p / sum_p w_y over non-ignored p.
+ * logits: device [B,2,h,w]; target int64 [B,S,S]; loss_out device fp32 [1];
+ * dlogits: device [B,2,h,w] (overwritten).
+ */
+int cwt_seg_ce_fwd_bwd(cwt_ctx* ctx, const float* logits, const int64_t* target, int B, int h,
+                       int w, int S, float* loss_out, float* dlogits, void* stream);
+
+/* intersectionAndUnionGPU on argmax maps (util.py:280-308): preds/target device int64 [n];
+ * preds[target==ignore] are ignored; histc over classes 0..num_classes-1 (num_classes <= 16).
+ * iut_out: device fp32 [3, num_classes] (intersection, union, target). */
+int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int64_t n, int num_classes,
+                  int ignore_index, float* iut_out, void* stream);
+
+/* dW[b,c,:] += sum_p dlogits[b,c,p] * f[b,p,:]  (backward of cwt_classify w.r.t. W). */
+int cwt_classify_bwd(cwt_ctx* ctx, const float* dlogits, const float* f, int B, int P, int C,
+                     float* dW, void* stream);
+
+/* torch.optim.SGD(momentum, dampening 0, weight_decay, nesterov) step over one flat
+ * fp32 parameter buffer (optimizer.py:8-15): buf = m*buf + (g + wd*p) (buf = g+wd*p on
+ * the first step, first_step != 0); p -= lr * (nesterov ? g + wd*p + m*buf : buf). */
+int cwt_sgd_step(cwt_ctx* ctx, float* param, const float* grad, float* momentum_buf, int64_t n,
+                 float lr, float momentum, float weight_decay, int nesterov, int first_step,
+                 void* stream);
+
+/*
+ * Per-launch profiling (no reference counterpart; measurement support for bench.py).
+ * While enabled, the context records a hipEvent pair on the call's stream around every
+ * conv launch of cwt_extract_features (plus the stem, maxpool and PPM kernels), around the
+ * whole cwt_inner_adapt loop and around cwt_attention_fwd, with the algorithmic FLOPs and
+ * minimal HBM bytes of that launch.  Enabling clears the records.
+ * cwt_profile_record waits for record i's stop event and returns its elapsed time.
+ */
+int cwt_profile_enable(cwt_ctx* ctx, int on);
+int cwt_profile_count(cwt_ctx* ctx);
+int cwt_profile_record(cwt_ctx* ctx, int i, char* name, int name_len, double* flops, double* bytes,
+                       float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CWT_H_ */

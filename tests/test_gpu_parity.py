@@ -1,0 +1,257 @@
+"""HIP path (libcwt.so through the C ABI) vs the oracle and the reference's golden vectors.
+
+Tolerances (BASELINE.json north_star): fp32 logits within 1e-3 relative
+(max|d| / max|ref|), W and W' within 1e-3; argmax identical except on pixels whose
+reference logit margin is below 1e-3 * max|logit| (IoU counts compared within the
+count of such pixels)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from few_shot_seg_cwt_amd import synthetic as syn  # noqa: E402
+
+SEED = 2021
+TOL = 1e-3
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
+    b = b.detach().double().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+_models = {}
+
+
+def model(layers):
+    from few_shot_seg_cwt_amd import get_model
+    if layers not in _models:
+        m = get_model(syn.cfg_defaults(layers=layers))
+        m.load_state_dict(syn.make_pspnet_state(layers, SEED))
+        _models[layers] = m
+    return _models[layers]
+
+
+def transformer(heads=4):
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne
+    t = MultiHeadAttentionOne(heads, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(heads, 512, SEED))
+    return t
+
+
+@pytest.fixture(scope="module")
+def small(golden_dir):
+    return dict(np.load(os.path.join(golden_dir, "modules_small.npz")))
+
+
+# ---------------------------------------------------------------- feature extractor
+@pytest.mark.parametrize("layers", [50, 101])
+def test_extract_features_small_vs_reference(dev, small, layers):
+    ep = syn.make_episode(SEED, 7, 33, 2)
+    x = torch.from_numpy(ep["spprt_imgs"][0]).to(dev)
+    f, lst = model(layers).extract_features(x)
+    torch.cuda.synchronize()
+    assert lst == [] and tuple(f.shape) == (2, 512, 5, 5)
+    assert rel(f, small[f"feat_r{layers}_S33"]) < 1e-4
+
+
+def test_extract_features_full_vs_oracle(dev):
+    from oracle import cwt_oracle as O
+    ep = syn.make_episode(SEED, 0, 473, 1)
+    x = torch.from_numpy(ep["qry_img"])
+    f, _ = model(50).extract_features(x.to(dev))
+    ref = O.extract_features(x, O.to_torch_state(syn.make_pspnet_state(50, SEED)))
+    assert rel(f, ref) < TOL
+
+
+def test_extract_batch_independent(dev):
+    # batching support + query in one pass must equal separate passes (eval-mode BN)
+    ep = syn.make_episode(SEED, 3, 129, 2)
+    x = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
+    fa, _ = model(50).extract_features(x)
+    fb, _ = model(50).extract_features(x[2:].contiguous())
+    assert rel(fa[2:], fb) < 1e-6
+
+
+# ---------------------------------------------------------------- inner loop
+def test_inner_loop_small_vs_reference(dev, small):
+    from few_shot_seg_cwt_amd.episode import inner_adapt
+    ep = syn.make_episode(SEED, 7, 33, 2)
+    f_s = torch.from_numpy(small["feat_r50_S33"]).to(dev).contiguous(memory_format=torch.channels_last)
+    W = torch.from_numpy(small["inner_W0"]).reshape(2, 512).to(dev).contiguous()
+    inner_adapt(f_s, torch.from_numpy(ep["s_label"][0]).to(dev), W, 0.1, 200)
+    assert rel(W, small["inner_W200"].reshape(2, 512)) < TOL
+
+
+@pytest.mark.parametrize("iters", [0, 1, 5])
+def test_inner_loop_few_steps_vs_oracle(dev, iters):
+    from few_shot_seg_cwt_amd.episode import inner_adapt
+    from oracle import cwt_oracle as O
+    ep = syn.make_episode(SEED, 11, 65, 1)
+    f_s = torch.from_numpy(syn.normal(SEED, "fs", (1, 512, 9, 9), 0.1))
+    W0 = torch.from_numpy(syn.normal(SEED, "w0", (2, 512), 0.05))
+    ref = O.inner_adapt(f_s, torch.from_numpy(ep["s_label"][0]), W0.reshape(2, 512, 1, 1), 0.1, iters,
+                        O.class_weight(ep["s_label"]))
+    W = W0.clone().to(dev)
+    inner_adapt(f_s.to(dev).contiguous(memory_format=torch.channels_last), torch.from_numpy(ep["s_label"][0]).to(dev),
+                W, 0.1, iters)
+    assert rel(W, ref.reshape(2, 512)) < 1e-4
+
+
+# ---------------------------------------------------------------- CWT
+@pytest.mark.parametrize("heads", [1, 4])
+def test_cwt_forward_vs_reference(dev, small, heads):
+    t = transformer(heads)
+    k = torch.nn.functional.normalize(torch.from_numpy(small["feat_r50_S33"][:1]), dim=1).to(dev)
+    q = torch.from_numpy(small[f"mha_h{heads}_q"]).to(dev)
+    with torch.no_grad():
+        out = t(q, k, k)
+    assert rel(out, small[f"mha_h{heads}_out"]) < 1e-4
+
+
+def test_cwt_forward_full_vs_oracle(dev):
+    from oracle import cwt_oracle as O
+    k = torch.nn.functional.normalize(torch.from_numpy(syn.normal(SEED, "fq", (1, 512, 60, 60))), dim=1)
+    q = torch.from_numpy(syn.normal(SEED, "q", (1, 2, 512), 0.3))
+    tsd = O.to_torch_state(syn.make_transformer_state(4, 512, SEED))
+    ref = O.cwt_forward(q, k, k, tsd, 4)
+    kd = k.to(dev)
+    with torch.no_grad():
+        out = transformer(4)(q.to(dev), kd, kd)
+    assert rel(out, ref) < 1e-4
+
+
+@pytest.mark.parametrize("heads", [1, 4])
+def test_cwt_backward_vs_oracle_autograd(dev, heads):
+    from oracle import cwt_oracle as O
+    k = torch.nn.functional.normalize(torch.from_numpy(syn.normal(SEED, "fk", (1, 512, 7, 9))), dim=1)
+    q = torch.from_numpy(syn.normal(SEED, "qb", (1, 2, 512), 0.3))
+    gout = torch.from_numpy(syn.normal(SEED, "go", (1, 2, 512), 1.0))
+    tsd = {n: v.clone().requires_grad_(True) for n, v in
+           O.to_torch_state(syn.make_transformer_state(heads, 512, SEED)).items()}
+    ref_out = O.cwt_forward(q, k, k, tsd, heads)
+    ref_g = torch.autograd.grad(ref_out, list(tsd.values()), gout)
+    t = transformer(heads)
+    kd = k.to(dev)
+    out = t(q.to(dev), kd, kd)
+    out.backward(gout.to(dev))
+    g = t.flat.grad
+    for (n, _), rg in zip(t.named_views(), ref_g):
+        assert rel(t.view(n, g), rg) < 1e-4, n
+
+
+# ---------------------------------------------------------------- metrics
+def test_seg_metrics_vs_oracle(dev):
+    from few_shot_seg_cwt_amd.util import seg_metrics
+    from oracle import cwt_oracle as O
+    logits = torch.from_numpy(syn.normal(SEED, "lg", (2, 2, 60, 60), 1.0))
+    ep = syn.make_episode(SEED, 5, 473, 2)
+    tgt = torch.from_numpy(ep["s_label"][0])
+    iut, ce = seg_metrics(logits.to(dev), tgt.to(dev))
+    up = O.upsample(logits, 473)
+    for b in range(2):
+        i, u, t = O.intersection_union(up.argmax(1)[b], tgt[b])
+        np.testing.assert_array_equal(iut[b].cpu().numpy(), np.stack([i.numpy(), u.numpy(), t.numpy()]))
+        l = torch.nn.functional.cross_entropy(up[b:b + 1], tgt[b:b + 1], ignore_index=255).item()
+        c = ce[b].cpu().numpy()
+        assert abs(c[0] / c[1] - l) < 1e-4 * abs(l)
+
+
+def test_iou_preds_vs_reference(dev, small):
+    from few_shot_seg_cwt_amd.util import intersectionAndUnionGPU
+    i, u, t = intersectionAndUnionGPU(torch.from_numpy(small["iou_preds"]).to(dev),
+                                      torch.from_numpy(small["iou_target"]).to(dev), 2, 255)
+    np.testing.assert_array_equal(torch.stack([i, u, t]).cpu().numpy(), small["iou_out"])
+
+
+def test_sgd_nesterov_vs_torch(dev):
+    from few_shot_seg_cwt_amd.optimizer import HipSGD
+    p0 = torch.from_numpy(syn.normal(SEED, "p", (1000,), 1.0))
+    grads = [torch.from_numpy(syn.normal(SEED, f"g{i}", (1000,), 1.0)) for i in range(3)]
+    pr = p0.clone().requires_grad_(True)
+    opt_r = torch.optim.SGD([pr], lr=0.01, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    pd = torch.nn.Parameter(p0.clone().to(dev))
+    opt = HipSGD([pd], lr=0.01, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    for g in grads:
+        pr.grad = g.clone()
+        opt_r.step()
+        pd.grad = g.clone().to(dev)
+        opt.step()
+    assert rel(pd.data, pr.detach()) < 1e-6
+
+
+# ---------------------------------------------------------------- full episodes vs golden
+def _low_margin(pred_ref, S):
+    up = torch.nn.functional.interpolate(torch.from_numpy(pred_ref)[None], size=(S, S), mode="bilinear",
+                                         align_corners=True)[0]
+    m = (up[1] - up[0]).abs()
+    return int((m < 1e-3 * up.abs().max()).sum())
+
+
+@pytest.mark.parametrize("name,layers,S,shot,n_ep", [
+    ("episode_pascal_r50_1shot.npz", 50, 473, 1, 3),
+    ("episode_pascal_r50_5shot.npz", 50, 473, 5, 1),
+    ("episode_coco_r101_1shot.npz", 101, 641, 1, 1),
+])
+def test_episode_vs_reference(dev, golden_dir, name, layers, S, shot, n_ep):
+    from few_shot_seg_cwt_amd.episode import EpisodeEngine
+    g = dict(np.load(os.path.join(golden_dir, name)))
+    cfg = syn.cfg_defaults(layers=layers, image_size=S, shot=shot)
+    eng = EpisodeEngine(model(layers), transformer(4), cfg)
+    classes = syn.coco_val_classes(0) if layers == 101 else None
+    for e in range(n_ep):
+        ep = syn.make_episode(SEED, e, S, shot, classes)
+        imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
+        W0 = torch.from_numpy(g[f"e{e}_W0"]).to(dev).contiguous()
+        r = eng.run(imgs, torch.from_numpy(ep["s_label"][0]).to(dev), torch.from_numpy(ep["q_label"]).to(dev), W0)
+        torch.cuda.synchronize()
+        assert rel(r["W"], g[f"e{e}_W"]) < TOL
+        assert rel(r["W2"][0], g[f"e{e}_W2"]) < TOL
+        assert rel(r["pred_q"][0], g[f"e{e}_pred_q"]) < TOL
+        assert rel(r["pred_q0"][0], g[f"e{e}_pred_q0"]) < TOL
+        flips = _low_margin(g[f"e{e}_pred_q"], S)
+        iu = r["iut"][0].cpu().numpy()
+        assert np.abs(iu - g[f"e{e}_iu"]).max() <= flips, (iu, g[f"e{e}_iu"], flips)
+
+
+def test_validate_transformer_vs_reference(dev, golden_dir):
+    from few_shot_seg_cwt_amd.episode import SyntheticEpisodes, validate_transformer
+    g = dict(np.load(os.path.join(golden_dir, "episode_pascal_r50_1shot.npz")))
+    cfg = syn.cfg_defaults(test_num=3, n_runs=1)
+    torch.manual_seed(SEED)
+    eps = []
+    miou, loss = validate_transformer(cfg, SyntheticEpisodes(3), model(50), transformer(4), episodes_out=eps)
+    assert abs(miou - float(g["mIoU"])) < 2e-3
+    assert abs(loss - float(g["loss"])) < 1e-3 * abs(float(g["loss"]))
+    for e in range(3):   # W0 drawn from the torch RNG exactly as the reference draws it
+        assert rel(eps[e]["W"], g[f"e{e}_W"]) < TOL
+
+
+def test_do_epoch_vs_reference(dev, golden_dir):
+    from few_shot_seg_cwt_amd.episode import SyntheticEpisodes, do_epoch
+    from few_shot_seg_cwt_amd.optimizer import get_optimizer
+    g = dict(np.load(os.path.join(golden_dir, "train_pascal_r50_1shot.npz")))
+    cfg = syn.cfg_defaults()
+    t = transformer(4)
+    opt = get_optimizer(cfg, [dict(params=[t.flat], lr=cfg["trans_lr"] * cfg["scale_lr"])])
+    torch.manual_seed(SEED)
+    recs = []
+    ious, losses = do_epoch(cfg, SyntheticEpisodes(2, start=int(g["start"])), model(50), t, opt, epoch=1,
+                            iter_per_epoch=2, log_iter=2, records=recs)
+    np.testing.assert_allclose(losses.numpy(), g["train_losses"], rtol=1e-3)
+    assert rel(recs[0]["W"], g["e0_W"]) < TOL
+    for n, v in t.named_views():
+        gv = t.view(n, recs[0]["grad"])
+        assert rel(gv.reshape(-1)[::101], g[f"e0_grad_{n}_sample"]) < 5e-3, n
+        assert rel(v.reshape(-1)[::101], g[f"final_{n}_sample"]) < 1e-4, n
