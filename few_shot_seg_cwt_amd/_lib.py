@@ -26,8 +26,10 @@ SIGNATURES = {
     "cwt_last_error": (C.c_char_p, []),
     "cwt_ctx_create": (_I, [_I, C.POINTER(_P)]),
     "cwt_ctx_destroy": (_I, [_P]),
-    "cwt_backbone_load": (_I, [_P, _I, _I, C.POINTER(C.c_char_p), C.POINTER(_P), C.POINTER(_I64), _F]),
-    "cwt_extract_features": (_I, [_P, _P, _I, _I, _P, _P]),
+    "cwt_backbone_load": (_I, [_P, _I, _I, C.POINTER(C.c_char_p), C.POINTER(_P), C.POINTER(_I64), _F,
+                               C.POINTER(_P)]),
+    "cwt_backbone_destroy": (_I, [_P]),
+    "cwt_extract_features": (_I, [_P, _P, _P, _I, _I, _P, _P]),
     "cwt_workspace_bytes": (C.c_size_t, [_P]),
     "cwt_inner_adapt": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
     "cwt_normalize": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
@@ -40,6 +42,8 @@ SIGNATURES = {
     "cwt_classify_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_iou_preds": (_I, [_P, _P, _P, _I64, _I, _I, _P, _P]),
     "cwt_sgd_step": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _I, _I, _P]),
+    "cwt_debug_conv": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I,
+                            _I, _I, _I, _P]),
     "cwt_profile_enable": (_I, [_P, _I]),
     "cwt_profile_count": (_I, [_P]),
     "cwt_profile_record": (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -47,7 +51,7 @@ SIGNATURES = {
 }
 
 _lib = None
-_lock = threading.Lock()
+_lock = threading.RLock()
 _ctx = {}
 
 

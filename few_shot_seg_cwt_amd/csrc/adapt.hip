@@ -61,11 +61,25 @@ constexpr int ADAPT_CB = 16;           // lo-res columns per workgroup
 constexpr int ADAPT_NP = 2 * (ADAPT_CB + 1);
 constexpr int ADAPT_PPW = (ADAPT_NP + 3) / 4;  // lo pixels per wave
 
+// Per-call pointers, read by the kernels from device memory so that one captured graph of
+// the 200 step launches serves every call with the same geometry.
+struct AdaptDevArgs {
+  const float* f;     // NHWC [n][h][w][512]
+  const float* w_in;  // initial W [2][512]
+  float* w_out;       // adapted W [2][512]
+};
+
+__global__ void adapt_setargs_kernel(AdaptDevArgs* d, const float* f, const float* w_in, float* w_out) {
+  d->f = f;
+  d->w_in = w_in;
+  d->w_out = w_out;
+}
+
 struct AdaptStepArgs {
-  const float* f;        // NHWC [n][h][w][512]
+  const AdaptDevArgs* dargs;
   const uint8_t* lbl;    // [n][S][S]
   const AdaptScalars* sc;
-  const float* w_src;    // W before the previous update ([2][512]); for step 0 the initial W
+  const float* w_src;    // W before the previous update ([2][512]); null at step 0 (dargs->w_in)
   const float* acc_prev; // dW[1] of the previous step, or null at step 0
   float* w_dst;          // block (0,0,0) stores the current W here (may be null)
   float* acc_cur;        // dW[1] accumulator of this step (zeroed)
@@ -143,8 +157,9 @@ __global__ __launch_bounds__(256) void adapt_step_kernel(AdaptStepArgs a) {
   // current weights for this lane's 8 channels
   float w0[8], w1[8];
   {
-    const float* s0 = a.w_src + lane * 8;
-    const float* s1 = a.w_src + C + lane * 8;
+    const float* wsrc = a.w_src ? a.w_src : a.dargs->w_in;
+    const float* s0 = wsrc + lane * 8;
+    const float* s1 = wsrc + C + lane * 8;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       w0[q] = s0[q];
@@ -175,7 +190,7 @@ __global__ __launch_bounds__(256) void adapt_step_kernel(AdaptStepArgs a) {
   // ---- z = W . f for the tile's low-res pixels (rows r, r+1; cols cb*16 .. +16) ----
   const int x0 = cb * ADAPT_CB;
   const int ncol = min(ADAPT_CB + 1, a.w - x0);
-  const float* fimg = a.f + (long)n * a.h * a.w * C;
+  const float* fimg = a.dargs->f + (long)n * a.h * a.w * C;
   float fv[ADAPT_PPW][8];
 #pragma unroll
   for (int j = 0; j < ADAPT_PPW; ++j) {
@@ -231,29 +246,22 @@ __global__ __launch_bounds__(256) void adapt_step_kernel(AdaptStepArgs a) {
   }
 }
 
-__global__ void adapt_final_kernel(const float* w_src, const float* acc, const AdaptScalars* sc, float* w_out) {
+__global__ void adapt_final_kernel(const float* w_src, const float* acc, const AdaptScalars* sc,
+                                   const AdaptDevArgs* dargs) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= 512) return;
+  float* w_out = dargs->w_out;
   const float lr = sc->lr_eff;
   float d = acc ? acc[k] : 0.f;
   w_out[k] = w_src[k] + lr * d;
   w_out[512 + k] = w_src[512 + k] - lr * d;
 }
 
-int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int S, float lr, int iters, float* W,
-                 uint8_t* lbl_ws, AdaptScalars* sc, float* acc3 /*[3][512]*/, float* wbuf /*[2][2][512]*/,
-                 hipStream_t st) {
-  const long total = (long)n * S * S;
-  CWT_HIP(hipMemsetAsync(sc, 0, sizeof(AdaptScalars), st));
-  int pblocks = (int)std::min<long>(1024, cdiv(total, 256));
-  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(256), 0, st, lbl64, total, lbl_ws, sc);
-  CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(adapt_scalars_kernel, dim3(1), dim3(1), 0, st, sc, lr, 0);
-  CWT_LAUNCH_CHECK();
-  if (iters <= 0) return 0;
-  CWT_HIP(hipMemsetAsync(acc3, 0, sizeof(float) * 512, st));
+// The 200 step launches + the final update, enqueued on `st` (directly or while capturing).
+static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws, const AdaptScalars* sc, float* acc3,
+                               float* wbuf, int n, int h, int w, int S, int iters, hipStream_t st) {
   AdaptStepArgs a;
-  a.f = f;
+  a.dargs = dargs;
   a.lbl = lbl_ws;
   a.sc = sc;
   a.h = h;
@@ -264,7 +272,7 @@ int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int 
   const int ncb = cdiv(S - 1, 8 * ADAPT_CB);
   dim3 grid(ncb, h - 1, n);
   for (int s = 0; s < iters; ++s) {
-    a.w_src = (s == 0) ? W : wbuf + ((s - 1) & 1) * 1024;
+    a.w_src = (s == 0) ? nullptr : wbuf + ((s - 1) & 1) * 1024;
     a.acc_prev = (s == 0) ? nullptr : acc3 + ((s - 1) % 3) * 512;
     a.w_dst = wbuf + (s & 1) * 1024;
     a.acc_cur = acc3 + (s % 3) * 512;
@@ -274,8 +282,52 @@ int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int 
   }
   const int last = iters - 1;
   hipLaunchKernelGGL(adapt_final_kernel, dim3(2), dim3(256), 0, st, (const float*)(wbuf + (last & 1) * 1024),
-                     (const float*)(acc3 + (last % 3) * 512), (const AdaptScalars*)sc, W);
+                     (const float*)(acc3 + (last % 3) * 512), sc, dargs);
   CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+AdaptGraphCache::~AdaptGraphCache() {
+  for (auto& e : entries) (void)hipGraphExecDestroy(e.exec);
+  if (cap_stream) (void)hipStreamDestroy(cap_stream);
+}
+
+int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int S, float lr, int iters, float* W,
+                 uint8_t* lbl_ws, AdaptScalars* sc, float* acc3 /*[3][512]*/, float* wbuf /*[2][2][512]*/,
+                 AdaptDevArgs* dargs, AdaptGraphCache* cache, hipStream_t st) {
+  const long total = (long)n * S * S;
+  CWT_HIP(hipMemsetAsync(sc, 0, sizeof(AdaptScalars), st));
+  int pblocks = (int)std::min<long>(1024, cdiv(total, 256));
+  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(256), 0, st, lbl64, total, lbl_ws, sc);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(adapt_scalars_kernel, dim3(1), dim3(1), 0, st, sc, lr, 0);
+  CWT_LAUNCH_CHECK();
+  if (iters <= 0) return 0;
+  hipLaunchKernelGGL(adapt_setargs_kernel, dim3(1), dim3(1), 0, st, dargs, f, (const float*)W, W);
+  CWT_LAUNCH_CHECK();
+  CWT_HIP(hipMemsetAsync(acc3, 0, sizeof(float) * 512, st));
+  if (!cache) return enqueue_adapt_steps(dargs, lbl_ws, sc, acc3, wbuf, n, h, w, S, iters, st);
+  // graph path: one instantiated graph per (geometry, workspace pointers)
+  AdaptGraphCache::Entry key{n, h, w, S, iters, (const void*)lbl_ws, (const void*)sc, (const void*)acc3,
+                             (const void*)wbuf, (const void*)dargs, nullptr};
+  hipGraphExec_t exec = nullptr;
+  for (auto& e : cache->entries)
+    if (e.same(key)) exec = e.exec;
+  if (!exec) {
+    if (!cache->cap_stream) CWT_HIP(hipStreamCreateWithFlags(&cache->cap_stream, hipStreamNonBlocking));
+    hipGraph_t g;
+    CWT_HIP(hipStreamBeginCapture(cache->cap_stream, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_adapt_steps(dargs, lbl_ws, sc, acc3, wbuf, n, h, w, S, iters, cache->cap_stream);
+    hipError_t e2 = hipStreamEndCapture(cache->cap_stream, &g);
+    if (rc) return rc;
+    if (e2 != hipSuccess) return fail((int)e2, std::string("adapt graph capture: ") + hipGetErrorString(e2));
+    hipError_t e3 = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e3 != hipSuccess) return fail((int)e3, std::string("adapt graph instantiate: ") + hipGetErrorString(e3));
+    key.exec = exec;
+    cache->entries.push_back(key);
+  }
+  CWT_HIP(hipGraphLaunch(exec, st));
   return 0;
 }
 

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -25,8 +26,10 @@ int fail(int code, const std::string& msg) {
 
 // launchers defined in the other units
 struct AdaptScalars;
+struct AdaptDevArgs;
 int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int S, float lr, int iters, float* W,
-                 uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf, hipStream_t st);
+                 uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf, AdaptDevArgs* dargs,
+                 AdaptGraphCache* cache, hipStream_t st);
 int launch_seg_ce(const float* logits, const int64_t* target, int B, int h, int w, int S, float* loss_out,
                   float* dlogits, uint8_t* lbl_ws, AdaptScalars* sc, double* loss_num, hipStream_t st);
 int launch_normalize(const float* f, int B, int Pb, float* out, const float* W0, float* logits0, hipStream_t st);
@@ -62,8 +65,9 @@ struct Block {
   bool has_down = false;
 };
 
-struct Backbone {
+struct Backbone {  // the opaque cwt_backbone of the C ABI
   int layers = 0;
+  int device = 0;
   ConvLayer stem[3];
   std::vector<Block> blocks[4];
   ConvLayer ppm[4];
@@ -80,7 +84,6 @@ struct WsBuf {
 
 struct cwt_ctx {
   int device = 0;
-  cwt::Backbone* bb = nullptr;
   std::map<std::string, cwt::WsBuf> ws;
   size_t ws_total = 0;
   // optional per-launch profiling: events recorded on the caller's stream around each
@@ -94,6 +97,9 @@ struct cwt_ctx {
   std::vector<Rec> recs;
   std::vector<hipEvent_t> evpool;
   size_t ev_used = 0;
+  // inner loop: captured graphs of the step sequence (disable with CWT_ADAPT_GRAPH=0)
+  cwt::AdaptGraphCache adapt_graphs;
+  bool use_graph = true;
 };
 
 namespace cwt {
@@ -215,7 +221,7 @@ static const int kBlocks50[4] = {3, 4, 6, 3};
 static const int kBlocks101[4] = {3, 4, 23, 3};
 static const int kBins[4] = {1, 2, 3, 6};
 
-static int load_backbone(cwt_ctx* ctx, int layers, const HostParams& hp, float eps) {
+static int load_backbone(int layers, const HostParams& hp, float eps, Backbone** out) {
   if (layers != 50 && layers != 101) return fail(CWT_EARG, "layers must be 50 or 101");
   Backbone* bb = new Backbone();
   bb->layers = layers;
@@ -277,11 +283,7 @@ static int load_backbone(cwt_ctx* ctx, int layers, const HostParams& hp, float e
     cleanup();
     return rc;
   }
-  if (ctx->bb) {
-    for (void* p : ctx->bb->allocs) (void)hipFree(p);
-    delete ctx->bb;
-  }
-  ctx->bb = bb;
+  *out = bb;
   return 0;
 }
 
@@ -331,8 +333,8 @@ static ConvArgs make_args(const ConvCall& c) {
 }
 
 // The whole extractor as a list of conv calls + byte kernels.  dry_run sizes the split-K workspace.
-static int run_extract(cwt_ctx* ctx, const float* img, int N, int S, float* feat, hipStream_t st) {
-  Backbone* bb = ctx->bb;
+static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N, int S, float* feat,
+                       hipStream_t st) {
   const int Hs = down2(S), H1 = down2(Hs), h = down2(H1);
   const long sA = std::max({(long)N * Hs * Hs * 128, (long)N * H1 * H1 * 256, (long)N * h * h * 2048});
   const long sT1 = std::max((long)N * H1 * H1 * 128, (long)N * h * h * 512);
@@ -498,6 +500,8 @@ int cwt_ctx_create(int device, cwt_ctx** out) {
   CWT_HIP(hipSetDevice(device));
   cwt_ctx* c = new cwt_ctx();
   c->device = device;
+  const char* g = getenv("CWT_ADAPT_GRAPH");
+  c->use_graph = !(g && g[0] == '0');
   *out = c;
   return 0;
 }
@@ -506,10 +510,6 @@ int cwt_ctx_destroy(cwt_ctx* ctx) {
   if (!ctx) return 0;
   (void)hipSetDevice(ctx->device);
   (void)hipDeviceSynchronize();
-  if (ctx->bb) {
-    for (void* p : ctx->bb->allocs) (void)hipFree(p);
-    delete ctx->bb;
-  }
   for (auto& kv : ctx->ws)
     if (kv.second.p) (void)hipFree(kv.second.p);
   delete ctx;
@@ -517,21 +517,39 @@ int cwt_ctx_destroy(cwt_ctx* ctx) {
 }
 
 int cwt_backbone_load(cwt_ctx* ctx, int layers, int n_tensors, const char* const* names,
-                      const float* const* host_data, const int64_t* numel, float bn_eps) {
-  if (!ctx || !names || !host_data || !numel || n_tensors <= 0) return fail(CWT_EARG, "null argument");
+                      const float* const* host_data, const int64_t* numel, float bn_eps, cwt_backbone** out) {
+  if (!ctx || !names || !host_data || !numel || n_tensors <= 0 || !out) return fail(CWT_EARG, "null argument");
   CWT_HIP(hipSetDevice(ctx->device));
   HostParams hp;
   for (int i = 0; i < n_tensors; ++i) hp.m[names[i]] = {host_data[i], numel[i]};
-  return load_backbone(ctx, layers, hp, bn_eps);
+  Backbone* bb = nullptr;
+  int rc = load_backbone(layers, hp, bn_eps, &bb);
+  if (rc) return rc;
+  bb->device = ctx->device;
+  *out = reinterpret_cast<cwt_backbone*>(bb);
+  return 0;
 }
 
-int cwt_extract_features(cwt_ctx* ctx, const float* img, int N, int S, float* feat, void* stream) {
+int cwt_backbone_destroy(cwt_backbone* handle) {
+  Backbone* bb = reinterpret_cast<Backbone*>(handle);
+  if (!bb) return 0;
+  (void)hipSetDevice(bb->device);
+  (void)hipDeviceSynchronize();
+  for (void* p : bb->allocs) (void)hipFree(p);
+  delete bb;
+  return 0;
+}
+
+int cwt_extract_features(cwt_ctx* ctx, const cwt_backbone* handle, const float* img, int N, int S, float* feat,
+                         void* stream) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
-  if (!ctx->bb) return fail(CWT_ESTATE, "backbone weights not loaded (cwt_backbone_load)");
+  const Backbone* bb = reinterpret_cast<const Backbone*>(handle);
+  if (!bb) return fail(CWT_ESTATE, "backbone is NULL (cwt_backbone_load)");
+  if (bb->device != ctx->device) return fail(CWT_EARG, "backbone and context are on different devices");
   CWT_CHECK(img && feat, "null buffer");
   CWT_CHECK(N >= 1 && S >= 9 && (S - 1) % 8 == 0, "need N >= 1 and (S-1) % 8 == 0 (pspnet.py:150)");
   CWT_HIP(hipSetDevice(ctx->device));
-  return run_extract(ctx, img, N, S, feat, (hipStream_t)stream);
+  return run_extract(ctx, bb, img, N, S, feat, (hipStream_t)stream);
 }
 
 size_t cwt_workspace_bytes(cwt_ctx* ctx) { return ctx ? ctx->ws_total : 0; }
@@ -544,8 +562,9 @@ int cwt_inner_adapt(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int 
   CWT_CHECK(n >= 1 && h >= 2 && w >= 2 && iters >= 0, "bad sizes");
   CWT_CHECK(S - 1 == 8 * (h - 1) && S - 1 == 8 * (w - 1), "need S-1 == 8*(h-1) == 8*(w-1)");
   CWT_HIP(hipSetDevice(ctx->device));
-  void *lbl, *sc, *acc, *wb;
+  void *lbl, *sc, *acc, *wb, *dargs;
   int rc;
+  if ((rc = ensure_ws(ctx, "adapt.args", 64, &dargs))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.lbl", (size_t)n * S * S, &lbl))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.sc", 64, &sc))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.acc", 3 * 512 * 4, &acc))) return rc;
@@ -554,7 +573,8 @@ int cwt_inner_adapt(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int 
   Prof p(ctx, (hipStream_t)stream, "inner_adapt x" + std::to_string(iters), (double)iters * 2.0 * (4.0 * C * h * w * n),
          (double)iters * ((double)n * h * w * C * 4 + (double)n * S * S));
   rc = launch_adapt(f_s, s_label, n, h, w, S, lr, iters, W_inout, (uint8_t*)lbl, (AdaptScalars*)sc, (float*)acc,
-                    (float*)wb, (hipStream_t)stream);
+                    (float*)wb, (AdaptDevArgs*)dargs, ctx->use_graph ? &ctx->adapt_graphs : nullptr,
+                    (hipStream_t)stream);
   p.end();
   return rc;
 }
@@ -644,6 +664,45 @@ int cwt_seg_ce_fwd_bwd(cwt_ctx* ctx, const float* logits, const int64_t* target,
   if ((rc = ensure_ws(ctx, "ce.num", 64, &num))) return rc;
   return launch_seg_ce(logits, target, B, h, w, S, loss_out, dlogits, (uint8_t*)lbl, (AdaptScalars*)sc,
                        (double*)num, (hipStream_t)stream);
+}
+
+int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, int x_ld, const float* w_packed,
+                   const float* scale, const float* shift, int Co, int k, int stride, int pad, int dil,
+                   const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
+                   int nsplit, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && w_packed && scale && shift && y, "null buffer");
+  CWT_CHECK(Ci % 32 == 0 && Co % 64 == 0 && x_ld >= Ci && y_ld >= y_off + Co, "need Ci%32==0, Co%64==0");
+  CWT_HIP(hipSetDevice(ctx->device));
+  ConvLayer L;
+  L.Ci = Ci;
+  L.Co = Co;
+  L.k = k;
+  L.stride = stride;
+  L.pad = pad;
+  L.dil = dil;
+  L.w = (float*)w_packed;
+  L.scale = (float*)scale;
+  L.shift = (float*)shift;
+  ConvCall c{0, &L, x, N, Hi, Wi, x_ld, y, y_ld, y_off, res, res_ld, relu};
+  ConvArgs a = make_args(c);
+  ConvPlan p = plan_conv(a.M, a.Co, a.K);
+  if (bm > 0) {
+    CWT_CHECK((bm == 128 && (bn == 128 || bn == 64)) || (bm == 64 && bn == 64), "tile must be 128x128, 128x64, 64x64");
+    CWT_CHECK(Co % bn == 0, "Co % bn");
+    p.bm = bm;
+    p.bn = bn;
+  }
+  if (nsplit > 0) {
+    const int kt = a.K / 32;
+    p.kt_per_split = cdiv(kt, nsplit);
+    p.nsplit = cdiv(kt, p.kt_per_split);
+  }
+  void* part = nullptr;
+  size_t pf = (size_t)p.nsplit * a.M * a.Co;
+  int rc;
+  if (p.nsplit > 1 && (rc = ensure_ws(ctx, "dbg.PART", pf * 4, &part))) return rc;
+  return launch_conv(a, p, 0, (float*)part, pf, (hipStream_t)stream);
 }
 
 int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int64_t n, int num_classes,

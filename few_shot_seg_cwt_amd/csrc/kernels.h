@@ -1,5 +1,7 @@
 // Kernel-side argument structs and launcher declarations shared by the .hip units.
 #pragma once
+#include <vector>
+
 #include "common.h"
 
 namespace cwt {
@@ -25,6 +27,22 @@ struct ConvPlan {
 
 ConvPlan plan_conv(int M, int Co, int K);
 int launch_conv(ConvArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats, hipStream_t st);
+
+// inner loop (adapt.hip): cache of instantiated graphs of the 200-step launch sequence
+struct AdaptGraphCache {
+  struct Entry {
+    int n, h, w, S, iters;
+    const void *lbl, *sc, *acc, *wbuf, *dargs;
+    hipGraphExec_t exec;
+    bool same(const Entry& o) const {
+      return n == o.n && h == o.h && w == o.w && S == o.S && iters == o.iters && lbl == o.lbl && sc == o.sc &&
+             acc == o.acc && wbuf == o.wbuf && dargs == o.dargs;
+    }
+  };
+  std::vector<Entry> entries;
+  hipStream_t cap_stream = nullptr;
+  ~AdaptGraphCache();
+};
 
 // backbone helpers (backbone.hip)
 int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const float* scale,

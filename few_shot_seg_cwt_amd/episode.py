@@ -69,14 +69,16 @@ def classify(W: torch.Tensor, f: torch.Tensor) -> torch.Tensor:
     """W [B,2,512] . f [B,512,h,w] (channels_last) -> logits [B,2,h,w]."""
     B, Cc, h, w = f.shape
     logits = torch.empty((B, 2, h, w), device=f.device, dtype=torch.float32)
-    _lib.check(_lib.lib().cwt_classify(_lib.ctx(f.device.index), _lib.ptr(W.contiguous()), _lib.ptr(f), B, h * w, Cc,
+    W = W.contiguous()  # keep the (possible) copy alive until the call has been enqueued
+    _lib.check(_lib.lib().cwt_classify(_lib.ctx(f.device.index), _lib.ptr(W), _lib.ptr(f), B, h * w, Cc,
                                        _lib.ptr(logits), _lib.stream_ptr(f.device)), "cwt_classify")
     return logits
 
 
 def classify_bwd(dlogits: torch.Tensor, f: torch.Tensor, dW: torch.Tensor):
     B, Cc, h, w = f.shape
-    _lib.check(_lib.lib().cwt_classify_bwd(_lib.ctx(f.device.index), _lib.ptr(dlogits.contiguous()), _lib.ptr(f), B,
+    dlogits = dlogits.contiguous()
+    _lib.check(_lib.lib().cwt_classify_bwd(_lib.ctx(f.device.index), _lib.ptr(dlogits), _lib.ptr(f), B,
                                            h * w, Cc, _lib.ptr(dW), _lib.stream_ptr(f.device)), "cwt_classify_bwd")
     return dW
 
@@ -87,9 +89,10 @@ def seg_ce_fwd_bwd(logits: torch.Tensor, target: torch.Tensor):
     B, _, h, w = logits.shape
     S = target.shape[-1]
     loss = torch.empty(1, device=logits.device, dtype=torch.float32)
+    logits, target = logits.contiguous(), target.contiguous()
     dl = torch.empty_like(logits)
-    _lib.check(_lib.lib().cwt_seg_ce_fwd_bwd(_lib.ctx(logits.device.index), _lib.ptr(logits.contiguous()),
-                                             _lib.ptr(target.contiguous()), B, h, w, S, _lib.ptr(loss), _lib.ptr(dl),
+    _lib.check(_lib.lib().cwt_seg_ce_fwd_bwd(_lib.ctx(logits.device.index), _lib.ptr(logits),
+                                             _lib.ptr(target), B, h, w, S, _lib.ptr(loss), _lib.ptr(dl),
                                              _lib.stream_ptr(logits.device)), "cwt_seg_ce_fwd_bwd")
     return loss, dl
 

@@ -53,7 +53,19 @@ class PSPNet:
         self.device = torch.device("cuda", device if device is not None else torch.cuda.current_device()) \
             if torch.cuda.is_available() else None
         self._state = None
+        self._handle = None
         self.training = False
+
+    def _release(self):
+        if getattr(self, "_handle", None) is not None and _lib._lib is not None:
+            _lib.lib().cwt_backbone_destroy(self._handle)
+        self._handle = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
 
     # -- nn.Module-like surface used by the drivers --------------------------------------
     def eval(self):
@@ -104,8 +116,11 @@ class PSPNet:
         arr_n = (C.c_char_p * len(names))(*names)
         arr_p = (C.c_void_p * len(ptrs))(*ptrs)
         arr_e = (C.c_int64 * len(numels))(*numels)
-        _lib.check(lib.cwt_backbone_load(_lib.ctx(), self.layers, len(names), arr_n, arr_p, arr_e, BN_EPS),
-                   "cwt_backbone_load")
+        handle = C.c_void_p()
+        _lib.check(lib.cwt_backbone_load(_lib.ctx(self.device.index), self.layers, len(names), arr_n, arr_p, arr_e,
+                                         BN_EPS, C.byref(handle)), "cwt_backbone_load")
+        self._release()
+        self._handle = handle
         self._state = sd
         return self
 
@@ -128,7 +143,10 @@ class PSPNet:
         if out is None:
             out = torch.empty((N, 512, h, h), device=x.device, dtype=torch.float32,
                               memory_format=torch.channels_last)
-        _lib.check(_lib.lib().cwt_extract_features(_lib.ctx(x.device.index), _lib.ptr(x), N, S, _lib.ptr(out),
+        if x.device != self.device:
+            raise ValueError(f"x is on {x.device}, the backbone on {self.device}")
+        _lib.check(_lib.lib().cwt_extract_features(_lib.ctx(x.device.index), self._handle, _lib.ptr(x), N, S,
+                                                   _lib.ptr(out),
                                                    _lib.stream_ptr(x.device)), "cwt_extract_features")
         return out, []
 

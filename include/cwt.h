@@ -34,6 +34,7 @@ extern "C" {
 #define CWT_ENOFG 1003     /* support mask has no foreground (reference: ZeroDivisionError, test.py:174) */
 
 typedef struct cwt_ctx cwt_ctx;
+typedef struct cwt_backbone cwt_backbone;  /* one loaded (frozen) PSPNet extractor */
 
 /* Version string of the library build. */
 const char* cwt_version(void);
@@ -54,10 +55,14 @@ int cwt_ctx_destroy(cwt_ctx* ctx);
  * "bottleneck.0.weight"); host_data are host fp32 pointers (integer entries such as
  * num_batches_tracked may be passed with host_data == NULL and are ignored).
  * layers: 50 or 101.  BatchNorm (eval mode, eps bn_eps) is folded to per-channel
- * scale/shift and conv weights are repacked [Co][kh][kw][Ci] on the device.
+ * scale/shift and conv weights are repacked [Co][kh][kw][Ci] on the device of ctx.
+ * *out receives an independent handle (several backbones may coexist on one context);
+ * release it with cwt_backbone_destroy.
  */
 int cwt_backbone_load(cwt_ctx* ctx, int layers, int n_tensors, const char* const* names,
-                      const float* const* host_data, const int64_t* numel, float bn_eps);
+                      const float* const* host_data, const int64_t* numel, float bn_eps,
+                      cwt_backbone** out);
+int cwt_backbone_destroy(cwt_backbone* bb);
 
 /*
  * Frozen feature extractor forward (eval mode).
@@ -66,9 +71,10 @@ int cwt_backbone_load(cwt_ctx* ctx, int layers, int n_tensors, const char* const
  * img:  device fp32 NCHW [N,3,S,S] (S-1 divisible by 8).
  * feat: device fp32 NHWC [N,h,w,512] with h = (S-1)/8+1.
  */
-int cwt_extract_features(cwt_ctx* ctx, const float* img, int N, int S, float* feat, void* stream);
+int cwt_extract_features(cwt_ctx* ctx, const cwt_backbone* bb, const float* img, int N, int S,
+                         float* feat, void* stream);
 
-/* Bytes of device workspace the context holds for the last extract shape (for reporting). */
+/* Bytes of device workspace the context holds (activations etc.; shared by all backbones). */
 size_t cwt_workspace_bytes(cwt_ctx* ctx);
 
 /*
@@ -174,6 +180,17 @@ int cwt_sgd_step(cwt_ctx* ctx, float* param, const float* grad, float* momentum_
  * minimal HBM bytes of that launch.  Enabling clears the records.
  * cwt_profile_record waits for record i's stop event and returns its elapsed time.
  */
+/*
+ * Test hook: one implicit-GEMM conv + folded BN (+residual) (+ReLU), NHWC, with the tile
+ * (bm x bn in {128x128, 128x64, 64x64}; 0 = automatic) and split-K count (0 = automatic)
+ * forced, so every plan can be checked against a reference conv.  w_packed: device
+ * [Co][k][k][Ci]; scale/shift: device [Co]; res: NHWC (pixel stride res_ld) or NULL.
+ */
+int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, int x_ld,
+                   const float* w_packed, const float* scale, const float* shift, int Co, int k,
+                   int stride, int pad, int dil, const float* res, int res_ld, int relu, float* y,
+                   int y_ld, int y_off, int bm, int bn, int nsplit, void* stream);
+
 int cwt_profile_enable(cwt_ctx* ctx, int on);
 int cwt_profile_count(cwt_ctx* ctx);
 int cwt_profile_record(cwt_ctx* ctx, int i, char* name, int name_len, double* flops, double* bytes,

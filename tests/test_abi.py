@@ -41,7 +41,7 @@ def test_version_and_error_calls_without_gpu(lib):
     assert b"gfx950" in lib.cwt_version()
     assert lib.cwt_last_error() is not None
     # argument validation happens before any device call
-    assert lib.cwt_extract_features(None, None, 1, 473, None, None) == 1001
+    assert lib.cwt_extract_features(None, None, None, 1, 473, None, None) == 1001
     assert b"ctx" in lib.cwt_last_error()
     assert lib.cwt_attention_saved_floats(1, 3600, 512, 4) > 0
 

@@ -1,0 +1,90 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the two exchange points of the CWT path
+(DESIGN.md §6): the mean all-reduce of the flat CWT gradient bucket before the identical SGD
+step, and the sum all-reduce of the per-class intersection/union table of sharded inference."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _flat_grads(seed_ep: int):
+    """Oracle CWT gradients of one small training episode, flattened in the layout of
+    few_shot_seg_cwt_amd.transformer (w_qkvs, layer_norm.w/b, fc.w/b)."""
+    from few_shot_seg_cwt_amd import synthetic as syn
+    from few_shot_seg_cwt_amd.transformer import _layout
+    from oracle import cwt_oracle as O
+    heads = 2
+    tsd = O.to_torch_state(syn.make_transformer_state(heads, 512, 2021))
+    f_q = torch.from_numpy(syn.normal(seed_ep, "fq", (1, 512, 5, 5), 0.1))
+    W = torch.from_numpy(syn.normal(seed_ep, "W", (2, 512), 0.05))
+    ep = syn.make_episode(seed_ep, 0, 33, 1)
+    _, grads, _ = O.cwt_train_step_grads(W, f_q, torch.from_numpy(ep["q_label"]), tsd, heads)
+    lay, total = _layout(heads, 512)
+    flat = torch.zeros(total)
+    for n, shp, off, k in lay:
+        flat[off:off + k] = grads[n].reshape(-1)
+    return flat, tsd, lay
+
+
+def _worker(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from few_shot_seg_cwt_amd import dist as cdist
+    from oracle import cwt_oracle as O
+    r, _, w = cdist.init_from_env(backend="gloo")
+    assert (r, w) == (rank, WORLD)
+    # --- training: rank r runs episode base + r (train_ddp.py:62-66 seeding idiom) ---
+    mine, tsd, lay = _flat_grads(100 + rank)
+    bucket = mine.clone()
+    cdist.all_reduce_mean_(bucket)
+    g0, _, _ = _flat_grads(100)
+    g1, _, _ = _flat_grads(101)
+    expect = (g0 + g1) / 2
+    assert torch.allclose(bucket, expect, rtol=1e-6, atol=1e-9)
+    # identical SGD step everywhere -> identical parameters on every rank
+    params = {n: tsd[n].clone() for n, _, _, _ in lay}
+    grads = {n: bucket[off:off + k].view(shp) for n, shp, off, k in lay}
+    newp, _ = O.sgd_nesterov(params, grads, {}, lr=1e-3, momentum=0.9, wd=1e-4)
+    flatp = torch.cat([newp[n].reshape(-1) for n, _, _, _ in lay])
+    allp = [torch.zeros_like(flatp) for _ in range(WORLD)]
+    torch.distributed.all_gather(allp, flatp)
+    assert torch.equal(allp[0], allp[1])
+    # --- inference: episodes sharded round-robin, per-class table summed once ---
+    n_ep, classes = 10, [1, 2, 3, 4, 5]
+    mine_eps = [e for e in range(n_ep) if e % WORLD == rank]
+    table = {}
+    for e in mine_eps:
+        c = classes[e % len(classes)]
+        t = table.setdefault(c, np.zeros(2))
+        t += (e + 1, 2 * e + 3)      # stand-in (intersection, union) per episode
+    keys = cdist.union_keys(sorted(table))
+    assert keys == classes
+    tab = np.array([table.get(c, np.zeros(2)) for c in keys])
+    tab = cdist.all_reduce_sum_np(tab)
+    ref = {c: np.zeros(2) for c in classes}
+    for e in range(n_ep):
+        ref[classes[e % len(classes)]] += (e + 1, 2 * e + 3)
+    np.testing.assert_array_equal(tab, np.array([ref[c] for c in classes]))
+    assert cdist.all_reduce_max_scalar(float(rank)) == WORLD - 1
+    torch.distributed.destroy_process_group()
+    open(os.path.join(out_dir, f"ok{rank}"), "w").write("ok")
+
+
+def test_gloo_world2_exchange_points(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(port, str(tmp_path)), nprocs=WORLD, join=True)
+    assert all((tmp_path / f"ok{r}").exists() for r in range(WORLD))
