@@ -43,7 +43,7 @@ SIGNATURES = {
     "cwt_iou_preds": (_I, [_P, _P, _P, _I64, _I, _I, _P, _P]),
     "cwt_sgd_step": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _I, _I, _P]),
     "cwt_debug_conv": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I,
-                            _I, _I, _I, _P]),
+                            _I, _I, _I, _I, _P]),
     "cwt_profile_enable": (_I, [_P, _I]),
     "cwt_profile_count": (_I, [_P]),
     "cwt_profile_record": (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -122,8 +122,9 @@ def require(t: torch.Tensor, name: str, dtype=torch.float32, device=None):
     return t
 
 
-def profile_enable(on: bool, device=None):
-    check(lib().cwt_profile_enable(ctx(device), int(on)), "cwt_profile_enable")
+def profile_enable(level: int, device=None):
+    """0 off; 1 phases + bottleneck conv (cheap, for timed regions); 2 every launch."""
+    check(lib().cwt_profile_enable(ctx(device), int(level)), "cwt_profile_enable")
 
 
 def profile_records(device=None):

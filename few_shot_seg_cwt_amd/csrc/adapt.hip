@@ -35,14 +35,25 @@ __global__ void adapt_prep_kernel(const int64_t* __restrict__ lbl, long total, u
     nb += (v == 0);
     nf += (v == 1);
   }
-  // wave reduce then one atomic per wave
+  // wave reduce, block reduce, then one pair of atomics per block
+  __shared__ unsigned long long red[2][16];
   for (int o = 32; o > 0; o >>= 1) {
     nb += __shfl_xor(nb, o, 64);
     nf += __shfl_xor(nf, o, 64);
   }
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&sc->nbg, nb);
-    atomicAdd(&sc->nfg, nf);
+    red[0][threadIdx.x >> 6] = nb;
+    red[1][threadIdx.x >> 6] = nf;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = 0, f = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+      b += red[0][i];
+      f += red[1][i];
+    }
+    atomicAdd(&sc->nbg, b);
+    atomicAdd(&sc->nfg, f);
   }
 }
 
@@ -58,6 +69,12 @@ __global__ void adapt_scalars_kernel(AdaptScalars* sc, float lr, int mode) {
 }
 
 constexpr int ADAPT_CB = 16;           // lo-res columns per workgroup
+// dW[1] accumulator replicas: ~240 workgroups adding 2 KB each into ONE 2 KB row run at the
+// contended atomic rate (~0.09 TB/s, ~5 us per step; MI355X_MICROARCH.md Global float
+// atomics); spreading them over R rows (workgroup id % R) removes the contention and the
+// next step sums the R rows when it loads W.
+constexpr int ADAPT_R = 16;
+constexpr int ADAPT_SLOT = ADAPT_R * 512;  // floats per accumulator slot
 constexpr int ADAPT_NP = 2 * (ADAPT_CB + 1);
 constexpr int ADAPT_PPW = (ADAPT_NP + 3) / 4;  // lo pixels per wave
 
@@ -80,10 +97,10 @@ struct AdaptStepArgs {
   const uint8_t* lbl;    // [n][S][S]
   const AdaptScalars* sc;
   const float* w_src;    // W before the previous update ([2][512]); null at step 0 (dargs->w_in)
-  const float* acc_prev; // dW[1] of the previous step, or null at step 0
+  const float* acc_prev; // dW[1] replicas [R][512] of the previous step, or null at step 0
   float* w_dst;          // block (0,0,0) stores the current W here (may be null)
-  float* acc_cur;        // dW[1] accumulator of this step (zeroed)
-  float* acc_zero;       // slot to zero for the next step (may be null)
+  float* acc_cur;        // dW[1] replicas [R][512] of this step (zeroed)
+  float* acc_zero;       // slot [R][512] to zero for the next step (may be null)
   int h, w, S;
   float sy, sx;          // align_corners scales (h-1)/(S-1), (w-1)/(S-1)
 };
@@ -166,11 +183,18 @@ __global__ __launch_bounds__(256) void adapt_step_kernel(AdaptStepArgs a) {
       w1[q] = s1[q];
     }
     if (a.acc_prev) {
+      f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float d = a.acc_prev[lane * 8 + q];
-        w1[q] -= sc.lr_eff * d;
-        w0[q] += sc.lr_eff * d;
+      for (int rr = 0; rr < ADAPT_R; ++rr) {
+        d0 += *(const f32x4*)(a.acc_prev + rr * 512 + lane * 8);
+        d1 += *(const f32x4*)(a.acc_prev + rr * 512 + lane * 8 + 4);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w1[q] -= sc.lr_eff * d0[q];
+        w0[q] += sc.lr_eff * d0[q];
+        w1[4 + q] -= sc.lr_eff * d1[q];
+        w0[4 + q] += sc.lr_eff * d1[q];
       }
     }
   }
@@ -183,7 +207,7 @@ __global__ __launch_bounds__(256) void adapt_step_kernel(AdaptStepArgs a) {
     }
   }
   if (leader && a.acc_zero) {
-    for (int i = t; i < C; i += 256) a.acc_zero[i] = 0.f;
+    for (int i = t; i < ADAPT_SLOT / 4; i += 256) ((f32x4*)a.acc_zero)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   if (t < 2 * (ADAPT_CB + 1)) (&gs[0][0])[t] = 0.f;
 
@@ -242,7 +266,7 @@ __global__ __launch_bounds__(256) void adapt_step_kernel(AdaptStepArgs a) {
   __syncthreads();
   for (int k = t; k < C; k += 256) {
     const float s = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
-    atomicAdd(&a.acc_cur[k], s);
+    atomicAdd(&a.acc_cur[((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) % ADAPT_R) * 512 + k], s);
   }
 }
 
@@ -252,7 +276,9 @@ __global__ void adapt_final_kernel(const float* w_src, const float* acc, const A
   if (k >= 512) return;
   float* w_out = dargs->w_out;
   const float lr = sc->lr_eff;
-  float d = acc ? acc[k] : 0.f;
+  float d = 0.f;
+  if (acc)
+    for (int rr = 0; rr < ADAPT_R; ++rr) d += acc[rr * 512 + k];
   w_out[k] = w_src[k] + lr * d;
   w_out[512 + k] = w_src[512 + k] - lr * d;
 }
@@ -273,16 +299,16 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws,
   dim3 grid(ncb, h - 1, n);
   for (int s = 0; s < iters; ++s) {
     a.w_src = (s == 0) ? nullptr : wbuf + ((s - 1) & 1) * 1024;
-    a.acc_prev = (s == 0) ? nullptr : acc3 + ((s - 1) % 3) * 512;
+    a.acc_prev = (s == 0) ? nullptr : acc3 + ((s - 1) % 3) * ADAPT_SLOT;
     a.w_dst = wbuf + (s & 1) * 1024;
-    a.acc_cur = acc3 + (s % 3) * 512;
-    a.acc_zero = acc3 + ((s + 1) % 3) * 512;
+    a.acc_cur = acc3 + (s % 3) * ADAPT_SLOT;
+    a.acc_zero = acc3 + ((s + 1) % 3) * ADAPT_SLOT;
     hipLaunchKernelGGL(adapt_step_kernel, grid, dim3(256), 0, st, a);
     CWT_LAUNCH_CHECK();
   }
   const int last = iters - 1;
   hipLaunchKernelGGL(adapt_final_kernel, dim3(2), dim3(256), 0, st, (const float*)(wbuf + (last & 1) * 1024),
-                     (const float*)(acc3 + (last % 3) * 512), sc, dargs);
+                     (const float*)(acc3 + (last % 3) * ADAPT_SLOT), sc, dargs);
   CWT_LAUNCH_CHECK();
   return 0;
 }
@@ -293,19 +319,19 @@ AdaptGraphCache::~AdaptGraphCache() {
 }
 
 int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int S, float lr, int iters, float* W,
-                 uint8_t* lbl_ws, AdaptScalars* sc, float* acc3 /*[3][512]*/, float* wbuf /*[2][2][512]*/,
+                 uint8_t* lbl_ws, AdaptScalars* sc, float* acc3 /*[3][R][512]*/, float* wbuf /*[2][2][512]*/,
                  AdaptDevArgs* dargs, AdaptGraphCache* cache, hipStream_t st) {
   const long total = (long)n * S * S;
   CWT_HIP(hipMemsetAsync(sc, 0, sizeof(AdaptScalars), st));
-  int pblocks = (int)std::min<long>(1024, cdiv(total, 256));
-  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(256), 0, st, lbl64, total, lbl_ws, sc);
+  int pblocks = (int)std::min<long>(256, cdiv(total, 1024));
+  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(1024), 0, st, lbl64, total, lbl_ws, sc);
   CWT_LAUNCH_CHECK();
   hipLaunchKernelGGL(adapt_scalars_kernel, dim3(1), dim3(1), 0, st, sc, lr, 0);
   CWT_LAUNCH_CHECK();
   if (iters <= 0) return 0;
   hipLaunchKernelGGL(adapt_setargs_kernel, dim3(1), dim3(1), 0, st, dargs, f, (const float*)W, W);
   CWT_LAUNCH_CHECK();
-  CWT_HIP(hipMemsetAsync(acc3, 0, sizeof(float) * 512, st));
+  CWT_HIP(hipMemsetAsync(acc3, 0, sizeof(float) * ADAPT_SLOT, st));
   if (!cache) return enqueue_adapt_steps(dargs, lbl_ws, sc, acc3, wbuf, n, h, w, S, iters, st);
   // graph path: one instantiated graph per (geometry, workspace pointers)
   AdaptGraphCache::Entry key{n, h, w, S, iters, (const void*)lbl_ws, (const void*)sc, (const void*)acc3,
@@ -397,8 +423,8 @@ int launch_seg_ce(const float* logits, const int64_t* target, int B, int h, int 
   CWT_HIP(hipMemsetAsync(sc, 0, sizeof(AdaptScalars), st));
   CWT_HIP(hipMemsetAsync(loss_num, 0, sizeof(double), st));
   CWT_HIP(hipMemsetAsync(dlogits, 0, sizeof(float) * (size_t)B * 2 * h * w, st));
-  int pblocks = (int)std::min<long>(1024, cdiv(total, 256));
-  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(256), 0, st, target, total, lbl_ws, sc);
+  int pblocks = (int)std::min<long>(256, cdiv(total, 1024));
+  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(1024), 0, st, target, total, lbl_ws, sc);
   CWT_LAUNCH_CHECK();
   hipLaunchKernelGGL(adapt_scalars_kernel, dim3(1), dim3(1), 0, st, sc, 1.0f, 1);
   CWT_LAUNCH_CHECK();

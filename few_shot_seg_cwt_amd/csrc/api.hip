@@ -56,6 +56,8 @@ size_t attention_bwd_ws_floats(int B, int hw, int C, int H);
 struct ConvLayer {
   int Ci = 0, Co = 0, k = 1, stride = 1, pad = 0, dil = 1;
   float* w = nullptr;  // device, packed [Co][k][k][Ci] (stem conv1: [ci][ky][kx][co])
+  __bf16* w_hi = nullptr;  // bf16x3 split of w (same layout); null for the stem conv1
+  __bf16* w_lo = nullptr;
   float* scale = nullptr;
   float* shift = nullptr;
 };
@@ -88,7 +90,7 @@ struct cwt_ctx {
   size_t ws_total = 0;
   // optional per-launch profiling: events recorded on the caller's stream around each
   // instrumented launch (cwt_profile_enable); read back after a sync
-  bool prof_on = false;
+  int prof_level = 0;  // 0 off, 1 phases + the bottleneck conv, 2 every launch
   struct Rec {
     std::string name;
     double flops, bytes;
@@ -100,6 +102,8 @@ struct cwt_ctx {
   // inner loop: captured graphs of the step sequence (disable with CWT_ADAPT_GRAPH=0)
   cwt::AdaptGraphCache adapt_graphs;
   bool use_graph = true;
+  // conv arithmetic: bf16x3 on the bf16 matrix cores (default) or exact fp32 MFMA (CWT_CONV=f32)
+  bool conv_x3 = true;
 };
 
 namespace cwt {
@@ -109,8 +113,9 @@ struct Prof {
   cwt_ctx* c;
   hipStream_t st;
   int idx = -1;
-  Prof(cwt_ctx* ctx, hipStream_t s, const std::string& name, double flops, double bytes) : c(ctx), st(s) {
-    if (!c->prof_on) return;
+  Prof(cwt_ctx* ctx, hipStream_t s, const std::string& name, double flops, double bytes, int level = 2)
+      : c(ctx), st(s) {
+    if (c->prof_level < level) return;
     hipEvent_t ev[2];
     for (int k = 0; k < 2; ++k) {
       if (c->ev_used == c->evpool.size()) {
@@ -175,6 +180,30 @@ static int upload(Backbone* bb, const std::vector<float>& v, float** out) {
   return 0;
 }
 
+static uint16_t bf16_rne(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7F800000u) == 0x7F800000u) return (uint16_t)(u >> 16);  // inf / nan pass through
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+static float bf16_to_float(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+static int upload_u16(Backbone* bb, const std::vector<uint16_t>& v, __bf16** out) {
+  void* p = nullptr;
+  CWT_HIP(hipMalloc(&p, v.size() * sizeof(uint16_t)));
+  CWT_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  bb->allocs.push_back(p);
+  *out = (__bf16*)p;
+  return 0;
+}
+
 // BN eval folding as PyTorch's CPU inference kernel: alpha = w / sqrt(var + eps), beta = b - mean * alpha.
 static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wname, const std::string& bnp, int Ci,
                      int Co, int k, int stride, int pad, int dil, float eps, bool stem1, ConvLayer* L) {
@@ -212,6 +241,15 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
   }
   int rc;
   if ((rc = upload(bb, packed, &L->w))) return rc;
+  if (!stem1) {  // bf16x3 operands: hi = bf16_rne(w), lo = bf16_rne(w - hi)
+    std::vector<uint16_t> hi(packed.size()), lo(packed.size());
+    for (size_t i = 0; i < packed.size(); ++i) {
+      const float v = packed[i];
+      hi[i] = bf16_rne(v);
+      lo[i] = bf16_rne(v - bf16_to_float(hi[i]));
+    }
+    if ((rc = upload_u16(bb, hi, &L->w_hi)) || (rc = upload_u16(bb, lo, &L->w_lo))) return rc;
+  }
   if ((rc = upload(bb, sc, &L->scale))) return rc;
   if ((rc = upload(bb, sh, &L->shift))) return rc;
   return 0;
@@ -307,6 +345,8 @@ static ConvArgs make_args(const ConvCall& c) {
   const ConvLayer& L = *c.L;
   a.x = c.x;
   a.w = L.w;
+  a.w_hi = L.w_hi;
+  a.w_lo = L.w_lo;
   a.scale = L.scale;
   a.shift = L.shift;
   a.res = c.res;
@@ -426,7 +466,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   std::vector<ConvPlan> plans;
   for (auto& c : calls) {
     ConvArgs a = make_args(c);
-    ConvPlan pl = plan_conv(a.M, a.Co, a.K);
+    ConvPlan pl = ctx->conv_x3 ? plan_conv_x3(a.M, a.Co, a.K) : plan_conv(a.M, a.Co, a.K);
     plans.push_back(pl);
     if (pl.nsplit > 1) part_floats = std::max(part_floats, (size_t)pl.nsplit * a.M * a.Co);
   }
@@ -442,17 +482,26 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     const double bytes = 4.0 * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K + (double)a.M * a.Co +
                                 (a.res ? (double)a.M * a.Co : 0.0));
     Prof p(ctx, st,
-           "conv_igemm_f32<" + std::to_string(pl.bm) + "," + std::to_string(pl.bn) + "," +
+           std::string(ctx->conv_x3 ? "conv_igemm_bf16x3<" : "conv_igemm_f32<") + std::to_string(pl.bm) + "," +
+               std::to_string(pl.bn) + "," +
                std::to_string(calls[i].stage) + ">" +
                (pl.nsplit > 1 ? "+splitk" + std::to_string(pl.nsplit) : std::string()) + " " +
                std::to_string(a.Ci) + "x" + std::to_string(a.Co) + "k" + std::to_string(a.kh) + "s" +
                std::to_string(a.stride) + "d" + std::to_string(a.dil) + "@" + std::to_string(a.Ho),
-           flops, bytes);
-    int r = launch_conv(a, pl, calls[i].stage, PART, part_floats, st);
+           flops, bytes, calls[i].stage == 6 ? 1 : 2);
+    int r = ctx->conv_x3 ? launch_conv_x3(a, pl, calls[i].stage, PART, part_floats, st)
+                         : launch_conv(a, pl, calls[i].stage, PART, part_floats, st);
     p.end();
     return r;
   };
 
+  double all_flops = 2.0 * N * Hs * Hs * 64 * 27, all_bytes = 0.0;
+  for (auto& c : calls) {
+    ConvArgs a = make_args(c);
+    all_flops += 2.0 * a.M * a.Co * a.K;
+    all_bytes += 4.0 * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K + (double)a.M * a.Co);
+  }
+  Prof whole(ctx, st, "extract_features N=" + std::to_string(N) + " S=" + std::to_string(S), all_flops, all_bytes, 1);
   {
     Prof p(ctx, st, "stem_conv1 3x64k3s2", 2.0 * N * Hs * Hs * 64 * 27, 4.0 * ((double)N * 3 * S * S + (double)N * Hs * Hs * 64));
     if ((rc = launch_stem_conv1(img, N, S, bb->stem[0].w, bb->stem[0].scale, bb->stem[0].shift, A, Hs, st))) return rc;
@@ -479,7 +528,9 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     if ((rc = launch_ppm_upsample(PPM, N, h, h, kBins, 4, 512, CAT, 4096, 2048, st))) return rc;
     p.end();
   }
-  return run_call(n_backbone_calls + 4);
+  rc = run_call(n_backbone_calls + 4);
+  whole.end();
+  return rc;
 }
 
 }  // namespace cwt
@@ -502,6 +553,8 @@ int cwt_ctx_create(int device, cwt_ctx** out) {
   c->device = device;
   const char* g = getenv("CWT_ADAPT_GRAPH");
   c->use_graph = !(g && g[0] == '0');
+  const char* cv = getenv("CWT_CONV");
+  c->conv_x3 = !(cv && std::string(cv) == "f32");
   *out = c;
   return 0;
 }
@@ -567,11 +620,11 @@ int cwt_inner_adapt(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int 
   if ((rc = ensure_ws(ctx, "adapt.args", 64, &dargs))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.lbl", (size_t)n * S * S, &lbl))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.sc", 64, &sc))) return rc;
-  if ((rc = ensure_ws(ctx, "adapt.acc", 3 * 512 * 4, &acc))) return rc;
+  if ((rc = ensure_ws(ctx, "adapt.acc", 3 * 16 * 512 * 4, &acc))) return rc;  // [3][ADAPT_R][512]
   if ((rc = ensure_ws(ctx, "adapt.wbuf", 2 * 1024 * 4, &wb))) return rc;
   // algorithmic work: per step 2 x (2*2*C*h*w*n) FLOPs; minimal bytes = f_s + labels once per step
   Prof p(ctx, (hipStream_t)stream, "inner_adapt x" + std::to_string(iters), (double)iters * 2.0 * (4.0 * C * h * w * n),
-         (double)iters * ((double)n * h * w * C * 4 + (double)n * S * S));
+         (double)iters * ((double)n * h * w * C * 4 + (double)n * S * S), 1);
   rc = launch_adapt(f_s, s_label, n, h, w, S, lr, iters, W_inout, (uint8_t*)lbl, (AdaptScalars*)sc, (float*)acc,
                     (float*)wb, (AdaptDevArgs*)dargs, ctx->use_graph ? &ctx->adapt_graphs : nullptr,
                     (hipStream_t)stream);
@@ -603,7 +656,7 @@ int cwt_attention_fwd(cwt_ctx* ctx, const float* q, const float* f, int B, int h
   // reference-formulation FLOPs: k/v projections 2 x 2*hw*C*C*H + QK^T/AV 2 x 2*H*2*hw*C
   Prof p(ctx, (hipStream_t)stream, "attention_fwd",
          (double)B * (2.0 * 2.0 * hw * C * C * H + 2.0 * 2.0 * H * 2.0 * hw * C),
-         4.0 * ((double)B * hw * C + 2.0 * H * C * C + 2.0 * C));
+         4.0 * ((double)B * hw * C + 2.0 * H * C * C + 2.0 * C), 1);
   rc = attention_fwd(q, f, B, hw, C, H, w_qkvs, fc_w, fc_b, ln_w, ln_b, out, saved, (float*)ws, (hipStream_t)stream);
   p.end();
   return rc;
@@ -669,7 +722,7 @@ int cwt_seg_ce_fwd_bwd(cwt_ctx* ctx, const float* logits, const int64_t* target,
 int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, int x_ld, const float* w_packed,
                    const float* scale, const float* shift, int Co, int k, int stride, int pad, int dil,
                    const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
-                   int nsplit, void* stream) {
+                   int nsplit, int precision, void* stream) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
   CWT_CHECK(x && w_packed && scale && shift && y, "null buffer");
   CWT_CHECK(Ci % 32 == 0 && Co % 64 == 0 && x_ld >= Ci && y_ld >= y_off + Co, "need Ci%32==0, Co%64==0");
@@ -686,9 +739,11 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
   L.shift = (float*)shift;
   ConvCall c{0, &L, x, N, Hi, Wi, x_ld, y, y_ld, y_off, res, res_ld, relu};
   ConvArgs a = make_args(c);
-  ConvPlan p = plan_conv(a.M, a.Co, a.K);
+  const bool x3 = precision == 1;
+  ConvPlan p = x3 ? plan_conv_x3(a.M, a.Co, a.K) : plan_conv(a.M, a.Co, a.K);
   if (bm > 0) {
-    CWT_CHECK((bm == 128 && (bn == 128 || bn == 64)) || (bm == 64 && bn == 64), "tile must be 128x128, 128x64, 64x64");
+    CWT_CHECK((bm == 128 && (bn == 128 || bn == 64)) || (bm == 64 && bn == 64) || (x3 && bm == 64 && bn == 128),
+              "tile must be 128x128, 128x64, 64x64 (or 64x128 for bf16x3)");
     CWT_CHECK(Co % bn == 0, "Co % bn");
     p.bm = bm;
     p.bn = bn;
@@ -702,7 +757,14 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
   size_t pf = (size_t)p.nsplit * a.M * a.Co;
   int rc;
   if (p.nsplit > 1 && (rc = ensure_ws(ctx, "dbg.PART", pf * 4, &part))) return rc;
-  return launch_conv(a, p, 0, (float*)part, pf, (hipStream_t)stream);
+  if (!x3) return launch_conv(a, p, 0, (float*)part, pf, (hipStream_t)stream);
+  void *hi, *lo;
+  const long nw = (long)Co * a.K;
+  if ((rc = ensure_ws(ctx, "dbg.whi", nw * 2, &hi)) || (rc = ensure_ws(ctx, "dbg.wlo", nw * 2, &lo))) return rc;
+  if ((rc = launch_split_bf16(w_packed, (__bf16*)hi, (__bf16*)lo, nw, (hipStream_t)stream))) return rc;
+  a.w_hi = (const __bf16*)hi;
+  a.w_lo = (const __bf16*)lo;
+  return launch_conv_x3(a, p, 0, (float*)part, pf, (hipStream_t)stream);
 }
 
 int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int64_t n, int num_classes,
@@ -718,7 +780,7 @@ int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int
 
 int cwt_profile_enable(cwt_ctx* ctx, int on) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
-  ctx->prof_on = on != 0;
+  ctx->prof_level = on;
   if (on) {
     ctx->recs.clear();
     ctx->ev_used = 0;

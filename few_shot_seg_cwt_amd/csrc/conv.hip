@@ -254,11 +254,31 @@ int launch_conv(ConvArgs a, const ConvPlan& p, int stage, float* part_ws, size_t
     default: launch_tiles<6>(a, p, grid, st); break;
   }
   CWT_LAUNCH_CHECK();
-  if (nsplit > 1) {
-    long total = (long)a.M * (a.Co / 4);
-    hipLaunchKernelGGL(conv_splitk_epilogue, dim3(cdiv(total, 256)), dim3(256), 0, st, a, nsplit);
-    CWT_LAUNCH_CHECK();
+  if (nsplit > 1) return launch_splitk_epilogue(a, nsplit, st);
+  return 0;
+}
+
+int launch_splitk_epilogue(const ConvArgs& a, int nsplit, hipStream_t st) {
+  long total = (long)a.M * (a.Co / 4);
+  hipLaunchKernelGGL(conv_splitk_epilogue, dim3(cdiv(total, 256)), dim3(256), 0, st, a, nsplit);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void split_bf16_kernel(const float* __restrict__ w, __bf16* __restrict__ hi, __bf16* __restrict__ lo,
+                                  long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = w[i];
+    const __bf16 h = (__bf16)v;
+    hi[i] = h;
+    lo[i] = (__bf16)(v - (float)h);
   }
+}
+
+int launch_split_bf16(const float* w, __bf16* hi, __bf16* lo, long n, hipStream_t st) {
+  hipLaunchKernelGGL(split_bf16_kernel, dim3((unsigned)std::min<long>(4096, cdiv(n, 256))), dim3(256), 0, st, w, hi,
+                     lo, n);
+  CWT_LAUNCH_CHECK();
   return 0;
 }
 

@@ -222,29 +222,42 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(const float* __restri
 }
 
 // g[h][b*2+i][k] = sum_c e^{m_c-M} part_g_c / sum_c e^{m_c-M} l_c; also stores (M, L) per row.
+// Block = (64 channels, row rho, batch b); its 4 waves take every 4th chunk, then combine in LDS.
 template <int NR>
-__global__ void attn_combine_kernel(const float* __restrict__ part_g, const float* __restrict__ part_ml, int nchunk,
-                                    int nv, float* __restrict__ g, float* __restrict__ ml_out) {
+__global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part_g,
+                                                           const float* __restrict__ part_ml, int nchunk, int nv,
+                                                           float* __restrict__ g, float* __restrict__ ml_out) {
   constexpr int C = 512;
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float sm[4], sg[4][64], sl[4];
+  const int t = threadIdx.x, kk = t & 63, cg = t >> 6;
+  const int k = blockIdx.x * 64 + kk;
   const int rho = blockIdx.y, b = blockIdx.z;
-  if (k >= C) return;
   const float* ml = part_ml + ((long)b * nchunk * NR + rho) * 2;
   float M = -INFINITY;
-  for (int c = 0; c < nchunk; ++c) M = fmaxf(M, ml[(long)c * NR * 2]);
+  for (int c = cg; c < nchunk; c += 4) M = fmaxf(M, ml[(long)c * NR * 2]);
+  if (kk == 0) sm[cg] = M;
+  __syncthreads();
+  M = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
   float G = 0.f, L = 0.f;
   const float* pg = part_g + ((long)b * nchunk * NR + rho) * C + k;
-  for (int c = 0; c < nchunk; ++c) {
+  for (int c = cg; c < nchunk; c += 4) {
     const float mc = ml[(long)c * NR * 2];
     const float sc = (mc == -INFINITY) ? 0.f : __expf(mc - M);
     G = fmaf(sc, pg[(long)c * NR * C], G);
     L = fmaf(sc, ml[(long)c * NR * 2 + 1], L);
   }
-  const int h = rho >> 1, qi = rho & 1;
-  g[((long)h * nv + b * 2 + qi) * C + k] = G / L;
-  if (ml_out && k == 0) {
-    ml_out[((long)b * NR + rho) * 2] = M;
-    ml_out[((long)b * NR + rho) * 2 + 1] = L;
+  sg[cg][kk] = G;
+  if (kk == 0) sl[cg] = L;
+  __syncthreads();
+  if (cg == 0) {
+    const float Gs = (sg[0][kk] + sg[1][kk]) + (sg[2][kk] + sg[3][kk]);
+    const float Ls = (sl[0] + sl[1]) + (sl[2] + sl[3]);
+    const int h = rho >> 1, qi = rho & 1;
+    g[((long)h * nv + b * 2 + qi) * C + k] = Gs / Ls;
+    if (ml_out && k == 0) {
+      ml_out[((long)b * NR + rho) * 2] = M;
+      ml_out[((long)b * NR + rho) * 2 + 1] = Ls;
+    }
   }
 }
 
@@ -345,7 +358,7 @@ int attention_fwd(const float* q, const float* f, int B, int hw, int C, int H, c
     hipLaunchKernelGGL((attn_partial_kernel<8>), g3, dim3(256), 0, st, sv + L.r, f, hw, nv, part_g, part_ml, sc_out);
   CWT_LAUNCH_CHECK();
   // 4. combine -> g[h][v][C]
-  dim3 g4(C / 256, NR, B);
+  dim3 g4(C / 64, NR, B);
   if (H == 1)
     hipLaunchKernelGGL((attn_combine_kernel<2>), g4, dim3(256), 0, st, part_g, part_ml, nchunk, nv, sv + L.g, sv + L.ml);
   else if (H == 2)

@@ -15,7 +15,9 @@
  *  - Return value: 0 on success, a hipError_t value, or a CWT_E* code below.  The
  *    message of the last failure on the calling thread: cwt_last_error().
  *  - One context per device; calls on one context must be externally serialised.
- *  - Activations are fp32.  Feature maps are NHWC ([N][h][w][C], C contiguous), which
+ *  - Activations are fp32 in HBM.  The convs compute in "bf16x3" by default (fp32 operands
+ *    split into bf16 hi + lo, three bf16 MFMA products, fp32 accumulation; ~1e-5 relative
+ *    per conv); CWT_CONV=f32 selects exact fp32 MFMA.  Feature maps are NHWC ([N][h][w][C], C contiguous), which
  *    is torch's channels_last memory format of an [N,C,h,w] tensor.
  */
 #ifndef CWT_H_
@@ -174,24 +176,28 @@ int cwt_sgd_step(cwt_ctx* ctx, float* param, const float* grad, float* momentum_
 
 /*
  * Per-launch profiling (no reference counterpart; measurement support for bench.py).
- * While enabled, the context records a hipEvent pair on the call's stream around every
- * conv launch of cwt_extract_features (plus the stem, maxpool and PPM kernels), around the
- * whole cwt_inner_adapt loop and around cwt_attention_fwd, with the algorithmic FLOPs and
- * minimal HBM bytes of that launch.  Enabling clears the records.
+ * level 1: the context records a hipEvent pair on the call's stream around each whole
+ *          cwt_extract_features, its bottleneck conv (the largest single launch), the whole
+ *          cwt_inner_adapt loop and cwt_attention_fwd;
+ * level 2: additionally around every conv / stem / maxpool / PPM launch (adds ~10 us of
+ *          event overhead per launch: use for per-layer tables, not for timing);
+ * each record carries the algorithmic FLOPs and minimal HBM bytes of the bracket
+ * (SURVEY.md §8(d)).  Enabling (level > 0) clears the records; 0 stops recording.
  * cwt_profile_record waits for record i's stop event and returns its elapsed time.
  */
 /*
  * Test hook: one implicit-GEMM conv + folded BN (+residual) (+ReLU), NHWC, with the tile
- * (bm x bn in {128x128, 128x64, 64x64}; 0 = automatic) and split-K count (0 = automatic)
- * forced, so every plan can be checked against a reference conv.  w_packed: device
+ * (bm x bn in {128x128, 128x64, 64x64}, plus 64x128 for bf16x3; 0 = automatic) and split-K
+ * count (0 = automatic) forced, so every plan can be checked against a reference conv.
+ * precision: 0 = fp32 MFMA, 1 = bf16x3 (hi/lo split, 3 bf16 MFMAs per product).  w_packed: device
  * [Co][k][k][Ci]; scale/shift: device [Co]; res: NHWC (pixel stride res_ld) or NULL.
  */
 int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, int x_ld,
                    const float* w_packed, const float* scale, const float* shift, int Co, int k,
                    int stride, int pad, int dil, const float* res, int res_ld, int relu, float* y,
-                   int y_ld, int y_off, int bm, int bn, int nsplit, void* stream);
+                   int y_ld, int y_off, int bm, int bn, int nsplit, int precision, void* stream);
 
-int cwt_profile_enable(cwt_ctx* ctx, int on);
+int cwt_profile_enable(cwt_ctx* ctx, int level);
 int cwt_profile_count(cwt_ctx* ctx);
 int cwt_profile_record(cwt_ctx* ctx, int i, char* name, int name_len, double* flops, double* bytes,
                        float* ms);

@@ -43,14 +43,14 @@ ep = syn.make_episode(2021, 0, S, 1)
 imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
 torch.cuda.synchronize()
 say("inputs on device")
-_lib.profile_enable(True)
+_lib.profile_enable(2)
 f, _ = m.extract_features(imgs)
 say("extract launched")
 torch.cuda.synchronize()
 say("extract done", tuple(f.shape), float(f.abs().sum()))
 for name, fl, by, ms in _lib.profile_records():
     say(f"   {name:60s} {ms:8.3f} ms  {fl / max(ms, 1e-9) / 1e9:8.1f} TFLOP/s")
-_lib.profile_enable(False)
+_lib.profile_enable(0)
 W = torch.from_numpy(syn.normal(2021, "w", (2, 512), 0.04)).to(dev)
 inner_adapt(f[:1], torch.from_numpy(ep["s_label"][0]).to(dev), W, 0.1, 1)
 torch.cuda.synchronize()
