@@ -15,6 +15,8 @@
 // The next step's kernel applies W <- W - lr/sum(w) * dW on the fly, so a step is one
 // launch; three accumulator slots let step s zero slot s+1 without a race.
 // f_s (7.4 MB per shot at 60x60x512) is re-read every step from L2 / Infinity Cache.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -103,6 +105,9 @@ struct AdaptStepArgs {
   float* acc_zero;       // slot [R][512] to zero for the next step (may be null)
   int h, w, S;
   float sy, sx;          // align_corners scales (h-1)/(S-1), (w-1)/(S-1)
+  int dbg;               // ablation flags for timing studies only (CWT_ADAPT_DBG): 1 skip replica
+                         // reads, 2 skip the high-res pass, 4 skip the global atomics, 8 skip f loads,
+                         // 16 return at entry
 };
 
 // Accumulate the weighted-CE gradient of high-res pixels of this tile into gs[ri][xi]
@@ -161,112 +166,213 @@ __device__ __forceinline__ float hires_tile_grad(const float (*z)[ADAPT_CB + 1][
   return loss;
 }
 
-__global__ __launch_bounds__(256) void adapt_step_kernel(AdaptStepArgs a) {
+// DPP lane exchanges (VALU modifiers, no LDS round trip): quad_perm xor 1 / xor 2, and the
+// 8- / 16-lane mirrors.  After xor1, xor2, half-mirror every lane of an aligned octet holds
+// the octet's sum; a further row-mirror gives the 16-lane row sum.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float octet_sum(float v) {
+  return dpp_add<0x141>(dpp_add<0x4E>(dpp_add<0xB1>(v)));
+}
+// Full 64-lane sum, wave-uniform result: row sums by DPP, then four readlanes.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = dpp_add<0x140>(octet_sum(v));
+  const int i = __float_as_int(v);
+  return (__int_as_float(__builtin_amdgcn_readlane(i, 0)) + __int_as_float(__builtin_amdgcn_readlane(i, 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(i, 32)) + __int_as_float(__builtin_amdgcn_readlane(i, 48)));
+}
+
+constexpr int ADAPT_T = 1024;                          // threads per step workgroup
+constexpr int ADAPT_NW = ADAPT_T / 64;                 // waves
+constexpr int ADAPT_PPW16 = (ADAPT_NP + ADAPT_NW - 1) / ADAPT_NW;  // lo pixels per wave (3)
+
+// One SGD step over one tile (lo-res rows r, r+1; columns cb*16 .. cb*16+16; shot n).
+// 16 waves: wave v owns hi-res row 8r + v/2 and 64 of the tile's 128 hi-res columns (one
+// pixel per lane; with S-1 == 8(h-1) the interpolation weights are exact multiples of 1/8,
+// so an aligned lane octet shares its two lo-res columns and is pre-reduced by DPP before
+// one lane adds it into LDS).  Wave 0 alone reads W and the R gradient replicas and
+// publishes the current W through LDS.  f for the tile stays in registers between the z
+// pass and the dW pass.
+__global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
   constexpr int C = 512;
+  __shared__ float wl[2][C];
   __shared__ float z[2][ADAPT_CB + 1][2];
   __shared__ float gs[2][ADAPT_CB + 1];
-  __shared__ float red[4][C];
+  __shared__ float red[ADAPT_NW][C];
+  if (a.dbg & 16) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int cb = blockIdx.x, r = blockIdx.y, n = blockIdx.z;
   const int ncb = gridDim.x;
-  const AdaptScalars sc = *a.sc;
+  const int S = a.S;
 
-  // current weights for this lane's 8 channels
-  float w0[8], w1[8];
-  {
-    const float* wsrc = a.w_src ? a.w_src : a.dargs->w_in;
-    const float* s0 = wsrc + lane * 8;
-    const float* s1 = wsrc + C + lane * 8;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      w0[q] = s0[q];
-      w1[q] = s1[q];
-    }
-    if (a.acc_prev) {
-      f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int rr = 0; rr < ADAPT_R; ++rr) {
-        d0 += *(const f32x4*)(a.acc_prev + rr * 512 + lane * 8);
-        d1 += *(const f32x4*)(a.acc_prev + rr * 512 + lane * 8 + 4);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        w1[q] -= sc.lr_eff * d0[q];
-        w0[q] += sc.lr_eff * d0[q];
-        w1[4 + q] -= sc.lr_eff * d1[q];
-        w0[4 + q] += sc.lr_eff * d1[q];
-      }
-    }
-  }
-  const bool leader = (cb | r | n) == 0;
-  if (leader && wv == 0 && a.w_dst) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      a.w_dst[lane * 8 + q] = w0[q];
-      a.w_dst[C + lane * 8 + q] = w1[q];
-    }
-  }
-  if (leader && a.acc_zero) {
-    for (int i = t; i < ADAPT_SLOT / 4; i += 256) ((f32x4*)a.acc_zero)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  if (t < 2 * (ADAPT_CB + 1)) (&gs[0][0])[t] = 0.f;
-
-  // ---- z = W . f for the tile's low-res pixels (rows r, r+1; cols cb*16 .. +16) ----
+  // ---- loads that do not depend on W: the tile's f pixels and this lane's labels ----
   const int x0 = cb * ADAPT_CB;
   const int ncol = min(ADAPT_CB + 1, a.w - x0);
   const float* fimg = a.dargs->f + (long)n * a.h * a.w * C;
-  float fv[ADAPT_PPW][8];
+  float fv[ADAPT_PPW16][8];
 #pragma unroll
-  for (int j = 0; j < ADAPT_PPW; ++j) {
-    const int p = wv + 4 * j;
+  for (int j = 0; j < ADAPT_PPW16; ++j) {
+    const int p = wv + ADAPT_NW * j;
     const int ri = p / (ADAPT_CB + 1), xi = p % (ADAPT_CB + 1);
-    const bool valid = p < ADAPT_NP && xi < ncol;
-    if (valid) {
+    if (p < ADAPT_NP && xi < ncol && !(a.dbg & 8)) {
       const float* src = fimg + ((long)(r + ri) * a.w + x0 + xi) * C + lane * 8;
-      f32x4 u = *(const f32x4*)src, v = *(const f32x4*)(src + 4);
+      const f32x4 u = *(const f32x4*)src, v = *(const f32x4*)(src + 4);
       fv[j][0] = u[0]; fv[j][1] = u[1]; fv[j][2] = u[2]; fv[j][3] = u[3];
       fv[j][4] = v[0]; fv[j][5] = v[1]; fv[j][6] = v[2]; fv[j][7] = v[3];
     } else {
 #pragma unroll
       for (int q = 0; q < 8; ++q) fv[j][q] = 0.f;
     }
-    float s0 = 0.f, s1 = 0.f;
+  }
+  const uint8_t* lbl = a.lbl + (long)n * S * S;
+  const int x_begin = cb * 8 * ADAPT_CB;
+  const int x_end = (cb == ncb - 1) ? S : x_begin + 8 * ADAPT_CB;
+  const int Y = 8 * r + (wv >> 1);
+  // rows 8r .. 8r+7 belong to this pair; the last pair also owns row S-1 (waves 0, 1)
+  const bool extra = (r == a.h - 2) && (wv >> 1) == 0;
+  const int xw = x_begin + 64 * (wv & 1);   // wave-uniform column base (+128 per round)
+  const int nrounds = (x_end - xw + 127) / 128;  // 1, or 2 when the last block has 129 columns
+  int y_main[2], y_extra[2];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      s0 = fmaf(w0[q], fv[j][q], s0);
-      s1 = fmaf(w1[q], fv[j][q], s1);
+  for (int k = 0; k < 2; ++k) {
+    const int X = xw + 128 * k + lane;
+    const bool in = k < nrounds && X < x_end;
+    y_main[k] = in ? lbl[(long)Y * S + X] : 255;
+    y_extra[k] = (in && extra) ? lbl[(long)(S - 1) * S + X] : 255;
+  }
+  const float wfg = a.sc->wfg;
+
+  // ---- current W (wave 0): W_src - lr_eff * sum of the previous step's replicas ----
+  if (wv == 0) {
+    const float lr = a.sc->lr_eff;
+    const float* wsrc = a.w_src ? a.w_src : a.dargs->w_in;
+    f32x4 w0a = *(const f32x4*)(wsrc + lane * 8), w0b = *(const f32x4*)(wsrc + lane * 8 + 4);
+    f32x4 w1a = *(const f32x4*)(wsrc + C + lane * 8), w1b = *(const f32x4*)(wsrc + C + lane * 8 + 4);
+    if (a.acc_prev && !(a.dbg & 1)) {
+      f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int rr = 0; rr < ADAPT_R; ++rr) {
+        d0 += *(const f32x4*)(a.acc_prev + rr * 512 + lane * 8);
+        d1 += *(const f32x4*)(a.acc_prev + rr * 512 + lane * 8 + 4);
+      }
+      w1a -= lr * d0;
+      w0a += lr * d0;
+      w1b -= lr * d1;
+      w0b += lr * d1;
     }
-    s0 = wave_sum(s0);
-    s1 = wave_sum(s1);
-    if (valid && lane == 0) {
-      z[ri][xi][0] = s0;
-      z[ri][xi][1] = s1;
+    *(f32x4*)&wl[0][lane * 8] = w0a;
+    *(f32x4*)&wl[0][lane * 8 + 4] = w0b;
+    *(f32x4*)&wl[1][lane * 8] = w1a;
+    *(f32x4*)&wl[1][lane * 8 + 4] = w1b;
+    if ((cb | r | n) == 0 && a.w_dst) {
+      *(f32x4*)(a.w_dst + lane * 8) = w0a;
+      *(f32x4*)(a.w_dst + lane * 8 + 4) = w0b;
+      *(f32x4*)(a.w_dst + C + lane * 8) = w1a;
+      *(f32x4*)(a.w_dst + C + lane * 8 + 4) = w1b;
+    }
+  }
+  if ((cb | r | n) == 0 && a.acc_zero)
+    for (int i = t; i < ADAPT_SLOT / 4; i += ADAPT_T) ((f32x4*)a.acc_zero)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (t < ADAPT_NP) (&gs[0][0])[t] = 0.f;
+  __syncthreads();
+
+  // ---- z = W . f for the tile's low-res pixels ----
+  {
+    float w0[8], w1[8];
+    const f32x4 a0 = *(const f32x4*)&wl[0][lane * 8], b0 = *(const f32x4*)&wl[0][lane * 8 + 4];
+    const f32x4 a1 = *(const f32x4*)&wl[1][lane * 8], b1 = *(const f32x4*)&wl[1][lane * 8 + 4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      w0[q] = a0[q]; w0[4 + q] = b0[q];
+      w1[q] = a1[q]; w1[4 + q] = b1[q];
+    }
+#pragma unroll
+    for (int j = 0; j < ADAPT_PPW16; ++j) {
+      const int p = wv + ADAPT_NW * j;
+      if (p >= ADAPT_NP) break;  // wave-uniform
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        s0 = fmaf(w0[q], fv[j][q], s0);
+        s1 = fmaf(w1[q], fv[j][q], s1);
+      }
+      s0 = wave_sum_dpp(s0);
+      s1 = wave_sum_dpp(s1);
+      if (lane == 0) {
+        (&z[0][0][0])[2 * p] = s0;
+        (&z[0][0][0])[2 * p + 1] = s1;
+      }
     }
   }
   __syncthreads();
 
-  hires_tile_grad<false>(z, gs, a.lbl + (long)n * a.S * a.S, a.S, a.h, a.w, r, cb, ncb, a.sy, a.sx, sc.wfg);
-  __syncthreads();
-
-  // ---- dW[1] partial = sum_p g[p] f[p] over the tile, reduced over waves, one atomic set ----
-  float d[8];
+  // ---- hi-res pass: weighted-CE gradient, bilinear adjoint into gs (class-1 component) ----
+  if (!(a.dbg & 2)) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) d[q] = 0.f;
+    for (int k = 0; k < 2; ++k) {
+      if (k >= nrounds) break;  // wave-uniform
+      const int X = xw + 128 * k + lane;
+      const bool xin = X < x_end;
+      // x interpolation, exact: S-1 == 8(w-1) so src = X/8
+      const int ix = min(X >> 3, a.w - 1);
+      const int xi0 = ix - x0, xi1 = (ix < a.w - 1) ? xi0 + 1 : xi0;
+      const float lx1 = (float)(X & 7) * 0.125f, lx0 = 1.f - lx1;
 #pragma unroll
-  for (int j = 0; j < ADAPT_PPW; ++j) {
-    const int p = wv + 4 * j;
-    if (p < ADAPT_NP) {
-      const float g = gs[p / (ADAPT_CB + 1)][p % (ADAPT_CB + 1)];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) d[q] = fmaf(g, fv[j][q], d[q]);
+      for (int e = 0; e < 2; ++e) {
+        if (e == 1 && !extra) break;  // wave-uniform
+        const int y = e ? y_extra[k] : y_main[k];
+        // row S-1 reads lo row r+1 with weight 1; rows 8r+i read rows r, r+1 with (1-i/8, i/8)
+        const int ri0 = e, ri1 = 1;
+        const float ly1 = e ? 0.f : (float)(Y & 7) * 0.125f, ly0 = 1.f - ly1;
+        float g = 0.f;
+        if (xin && y != 255) {
+          const float2 z00 = *(const float2*)z[ri0][xi0], z01 = *(const float2*)z[ri0][xi1];
+          const float2 z10 = *(const float2*)z[ri1][xi0], z11 = *(const float2*)z[ri1][xi1];
+          const float l0 = ly0 * (lx0 * z00.x + lx1 * z01.x) + ly1 * (lx0 * z10.x + lx1 * z11.x);
+          const float l1 = ly0 * (lx0 * z00.y + lx1 * z01.y) + ly1 * (lx0 * z10.y + lx1 * z11.y);
+          const float p1 = 1.f / (1.f + __expf(l0 - l1));
+          g = ((y == 1) ? wfg : 1.f) * (p1 - (float)y);
+        }
+        float v00 = octet_sum(ly0 * lx0 * g), v01 = octet_sum(ly0 * lx1 * g);
+        float v10 = octet_sum(ly1 * lx0 * g), v11 = octet_sum(ly1 * lx1 * g);
+        if ((lane & 7) == 0 && xin) {
+          if (e == 0) {
+            atomicAdd(&gs[0][xi0], v00);
+            atomicAdd(&gs[0][xi1], v01);
+          }
+          atomicAdd(&gs[1][xi0], v10 + (e ? v00 : 0.f));
+          atomicAdd(&gs[1][xi1], v11 + (e ? v01 : 0.f));
+        }
+      }
     }
   }
-#pragma unroll
-  for (int q = 0; q < 8; ++q) red[wv][lane * 8 + q] = d[q];
   __syncthreads();
-  for (int k = t; k < C; k += 256) {
-    const float s = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
-    atomicAdd(&a.acc_cur[((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) % ADAPT_R) * 512 + k], s);
+
+  // ---- dW[1] partial = sum_p g[p] f[p] over the tile ----
+  {
+    float d[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) d[q] = 0.f;
+#pragma unroll
+    for (int j = 0; j < ADAPT_PPW16; ++j) {
+      const int p = wv + ADAPT_NW * j;
+      if (p < ADAPT_NP) {
+        const float g = (&gs[0][0])[p];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) d[q] = fmaf(g, fv[j][q], d[q]);
+      }
+    }
+    *(f32x4*)&red[wv][lane * 8] = f32x4{d[0], d[1], d[2], d[3]};
+    *(f32x4*)&red[wv][lane * 8 + 4] = f32x4{d[4], d[5], d[6], d[7]};
+  }
+  __syncthreads();
+  if (t < C && !(a.dbg & 4)) {
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < ADAPT_NW; ++v) s += red[v][t];
+    atomicAdd(&a.acc_cur[((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) % ADAPT_R) * 512 + t], s);
   }
 }
 
@@ -295,6 +401,8 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws,
   a.S = S;
   a.sy = align_corners_scale(h, S);
   a.sx = align_corners_scale(w, S);
+  const char* dbg = getenv("CWT_ADAPT_DBG");
+  a.dbg = dbg ? atoi(dbg) : 0;
   const int ncb = cdiv(S - 1, 8 * ADAPT_CB);
   dim3 grid(ncb, h - 1, n);
   for (int s = 0; s < iters; ++s) {
@@ -303,7 +411,7 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws,
     a.w_dst = wbuf + (s & 1) * 1024;
     a.acc_cur = acc3 + (s % 3) * ADAPT_SLOT;
     a.acc_zero = acc3 + ((s + 1) % 3) * ADAPT_SLOT;
-    hipLaunchKernelGGL(adapt_step_kernel, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(adapt_step_kernel, grid, dim3(ADAPT_T), 0, st, a);
     CWT_LAUNCH_CHECK();
   }
   const int last = iters - 1;
