@@ -207,23 +207,7 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16x3(ConvArgs a) {
       sh = a.shift[co];
     }
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < a.M) {
-          float v = acc[i][j][r];
-          if (a.part) {
-            a.part[((long)ks * a.M + m) * a.Co + co] = v;
-          } else {
-            v = fmaf(v, sc, sh);
-            if (a.res) v += a.res[(long)m * a.res_ld + co];
-            if (a.relu) v = fmaxf(v, 0.f);
-            a.y[(long)m * a.y_ld + a.y_off + co] = v;
-          }
-        }
-      }
-    }
+    for (int i = 0; i < TM; ++i) conv_store_fragment(a, acc[i][j], m0 + wm * WM + i * 32, co, h, ks, sc, sh);
   }
 }
 

@@ -23,6 +23,41 @@ struct ConvArgs {
   int relu;
 };
 
+// Epilogue of one 32x32 MFMA accumulator fragment of the implicit-GEMM conv (C/D layout:
+// col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)): BN scale/shift, residual, ReLU, or
+// the raw split-K partial.  All 16 residual loads are issued (at clamped, always-valid
+// addresses) before the first store: res and y are not known not to alias, so loads
+// interleaved with stores would each wait a full memory round trip.
+__device__ __forceinline__ void conv_store_fragment(const ConvArgs& a, const f32x16& acc, int mbase, int co, int h,
+                                                    int ks, float sc, float sh) {
+  if (a.part) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = mbase + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m < a.M) a.part[((long)ks * a.M + m) * a.Co + co] = acc[r];
+    }
+    return;
+  }
+  float rv[16];
+  if (a.res) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = min(mbase + (r & 3) + 8 * (r >> 2) + 4 * h, a.M - 1);
+      rv[r] = a.res[(long)m * a.res_ld + co];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rv[r] = 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = mbase + (r & 3) + 8 * (r >> 2) + 4 * h;
+    float v = fmaf(acc[r], sc, sh) + rv[r];
+    if (a.relu) v = fmaxf(v, 0.f);
+    if (m < a.M) a.y[(long)m * a.y_ld + a.y_off + co] = v;
+  }
+}
+
 struct ConvPlan {
   int bm = 128, bn = 128, kt_per_split = 1, nsplit = 1;
 };

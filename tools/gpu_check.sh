@@ -11,7 +11,7 @@ rc=${PIPESTATUS[0]}
 echo "smoke rc=$rc"
 if [ $rc -ne 0 ]; then exit $rc; fi
 echo "== pytest $(date +%T)"
-timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider -rf --timeout 300 --durations=0 ${PYTEST_ARGS:-} 2>&1 | tee gpurun_out/pytest_gpu.log
+timeout -k 10 900 python -u -m pytest ${PYTEST_PATHS:-tests} -m gpu -v -p no:cacheprovider -rf --timeout 300 --durations=0 ${PYTEST_ARGS:-} 2>&1 | tee gpurun_out/pytest_gpu.log
 rc=${PIPESTATUS[0]}
 echo "pytest rc=$rc"
 if [ $rc -gt 1 ]; then exit $rc; fi
