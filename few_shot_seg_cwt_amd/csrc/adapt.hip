@@ -166,24 +166,6 @@ __device__ __forceinline__ float hires_tile_grad(const float (*z)[ADAPT_CB + 1][
   return loss;
 }
 
-// DPP lane exchanges (VALU modifiers, no LDS round trip): quad_perm xor 1 / xor 2, and the
-// 8- / 16-lane mirrors.  After xor1, xor2, half-mirror every lane of an aligned octet holds
-// the octet's sum; a further row-mirror gives the 16-lane row sum.
-template <int CTRL>
-__device__ __forceinline__ float dpp_add(float v) {
-  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float octet_sum(float v) {
-  return dpp_add<0x141>(dpp_add<0x4E>(dpp_add<0xB1>(v)));
-}
-// Full 64-lane sum, wave-uniform result: row sums by DPP, then four readlanes.
-__device__ __forceinline__ float wave_sum_dpp(float v) {
-  v = dpp_add<0x140>(octet_sum(v));
-  const int i = __float_as_int(v);
-  return (__int_as_float(__builtin_amdgcn_readlane(i, 0)) + __int_as_float(__builtin_amdgcn_readlane(i, 16))) +
-         (__int_as_float(__builtin_amdgcn_readlane(i, 32)) + __int_as_float(__builtin_amdgcn_readlane(i, 48)));
-}
-
 constexpr int ADAPT_T = 1024;                          // threads per step workgroup
 constexpr int ADAPT_NW = ADAPT_T / 64;                 // waves
 constexpr int ADAPT_PPW16 = (ADAPT_NP + ADAPT_NW - 1) / ADAPT_NW;  // lo pixels per wave (3)

@@ -72,8 +72,10 @@ struct Backbone {  // the opaque cwt_backbone of the C ABI
   int device = 0;
   ConvLayer stem[3];
   std::vector<Block> blocks[4];
-  ConvLayer ppm[4];
-  ConvLayer bott;
+  ConvLayer ppm[4];     // PPM 1x1 convs (scale/shift used; weights below)
+  float* ppm_wt[4] = {};  // their weights K-major [2048][512] for the small-M GEMM
+  ConvLayer bott;       // bottleneck conv over the 2048 layer4 channels only
+  float* ppm_q[4] = {};   // bottleneck weights of PPM bin b, K-major [512][9 * 512], BN scale folded in
   std::vector<void*> allocs;
 };
 
@@ -205,10 +207,14 @@ static int upload_u16(Backbone* bb, const std::vector<uint16_t>& v, __bf16** out
 }
 
 // BN eval folding as PyTorch's CPU inference kernel: alpha = w / sqrt(var + eps), beta = b - mean * alpha.
+// ci_total / ci_off: the stored weight has ci_total input channels; this layer takes
+// [ci_off, ci_off + Ci) of them (the bottleneck's layer4 half).
 static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wname, const std::string& bnp, int Ci,
-                     int Co, int k, int stride, int pad, int dil, float eps, bool stem1, ConvLayer* L) {
+                     int Co, int k, int stride, int pad, int dil, float eps, bool stem1, ConvLayer* L,
+                     int ci_total = -1, int ci_off = 0) {
+  if (ci_total < 0) ci_total = Ci;
   std::string err;
-  const float* w = hp.get(wname, (int64_t)Co * Ci * k * k, &err);
+  const float* w = hp.get(wname, (int64_t)Co * ci_total * k * k, &err);
   if (!w) return fail(CWT_EARG, err);
   const float* g = hp.get(bnp + ".weight", Co, &err);
   const float* b = g ? hp.get(bnp + ".bias", Co, &err) : nullptr;
@@ -227,11 +233,11 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
     for (int ci = 0; ci < Ci; ++ci)
       for (int ky = 0; ky < k; ++ky)
         for (int kx = 0; kx < k; ++kx) {
-          const float v = w[(((size_t)co * Ci + ci) * k + ky) * k + kx];
+          const float v = w[(((size_t)co * ci_total + ci_off + ci) * k + ky) * k + kx];
           if (stem1)
             packed[((size_t)(ci * 9 + ky * 3 + kx)) * Co + co] = v;
           else
-            packed[(size_t)co * K + (ky * k + kx) * Ci + ci] = v;
+            packed[(size_t)co * K + packed_k(ci, ky * k + kx, k * k)] = v;
         }
   std::vector<float> sc(Co), sh(Co);
   for (int c = 0; c < Co; ++c) {
@@ -252,6 +258,38 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
   }
   if ((rc = upload(bb, sc, &L->scale))) return rc;
   if ((rc = upload(bb, sh, &L->shift))) return rc;
+  return 0;
+}
+
+// Weights of the folded PPM branch (backbone.hip, PPM section): the PPM 1x1 conv weights
+// transposed to [2048][512], and per bin b the bottleneck taps over that bin's 512 concat
+// channels as Wq_b[ci][tap * 512 + co] = W[co][2048 + 512 b + ci][tap] * bn_scale[co].
+static int load_ppm_fold(Backbone* bb, const HostParams& hp, float eps) {
+  std::string err;
+  for (int b = 0; b < 4; ++b) {
+    const float* w = hp.get("ppm.features." + std::to_string(b) + ".1.weight", (int64_t)512 * 2048, &err);
+    if (!w) return fail(CWT_EARG, err);
+    std::vector<float> t((size_t)2048 * 512);
+    for (int co = 0; co < 512; ++co)
+      for (int ci = 0; ci < 2048; ++ci) t[(size_t)ci * 512 + co] = w[(size_t)co * 2048 + ci];
+    int rc;
+    if ((rc = upload(bb, t, &bb->ppm_wt[b]))) return rc;
+  }
+  const float* w = hp.get("bottleneck.0.weight", (int64_t)512 * 4096 * 9, &err);
+  const float* g = w ? hp.get("bottleneck.1.weight", 512, &err) : nullptr;
+  const float* rv = g ? hp.get("bottleneck.1.running_var", 512, &err) : nullptr;
+  if (!rv) return fail(CWT_EARG, err);
+  for (int b = 0; b < 4; ++b) {
+    std::vector<float> q((size_t)512 * 4608);
+    for (int co = 0; co < 512; ++co) {
+      const float sc = g[co] * (1.0f / std::sqrt(rv[co] + eps));  // as load_conv's BN fold
+      for (int ci = 0; ci < 512; ++ci)
+        for (int tap = 0; tap < 9; ++tap)
+          q[(size_t)ci * 4608 + tap * 512 + co] = w[((size_t)co * 4096 + 2048 + 512 * b + ci) * 9 + tap] * sc;
+    }
+    int rc;
+    if ((rc = upload(bb, q, &bb->ppm_q[b]))) return rc;
+  }
   return 0;
 }
 
@@ -317,7 +355,9 @@ static int load_backbone(int layers, const HostParams& hp, float eps, Backbone**
       return rc;
     }
   }
-  if ((rc = load_conv(bb, hp, "bottleneck.0.weight", "bottleneck.1", 4096, 512, 3, 1, 1, 1, eps, false, &bb->bott))) {
+  if ((rc = load_conv(bb, hp, "bottleneck.0.weight", "bottleneck.1", 2048, 512, 3, 1, 1, 1, eps, false, &bb->bott,
+                      4096, 0)) ||
+      (rc = load_ppm_fold(bb, hp, eps))) {
     cleanup();
     return rc;
   }
@@ -380,13 +420,17 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   const long sT1 = std::max((long)N * H1 * H1 * 128, (long)N * h * h * 512);
   const long sT2 = std::max((long)N * H1 * H1 * 64, (long)N * h * h * 512);
   const long sD = std::max((long)N * H1 * H1 * 256, (long)N * h * h * 2048);
-  const long sCat = (long)N * h * h * 4096;
   const long sCol = (long)N * h * 12 * 2048;
   const long sPool = (long)N * 50 * 2048;
   const long sPpm = (long)N * 50 * 512;
+  const long sQ = (long)N * 50 * 4608;
+  const long sR = (long)N * 12 * h * 3 * 512;
+  const long sF = (long)N * h * h * 512;
+  constexpr int kKcPpm = 32, kKcQ = 64;  // K chunk of the two small-M GEMMs
+  const long sPartS = std::max((long)(2048 / kKcPpm) * N * 50 * 512, (long)(512 / kKcQ) * N * 50 * 4608);
 
   // collect every conv call first (to size split-K scratch), then run
-  float *A, *B, *T1, *T2, *D, *CAT, *COL, *POOL, *PPM;
+  float *A, *B, *T1, *T2, *D, *COL, *POOL, *PPM, *QB, *RB, *FB, *PARTS;
   void* p;
   int rc;
   if ((rc = ensure_ws(ctx, "bb.A", sA * 4, &p))) return rc;
@@ -399,14 +443,20 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   T2 = (float*)p;
   if ((rc = ensure_ws(ctx, "bb.D", sD * 4, &p))) return rc;
   D = (float*)p;
-  if ((rc = ensure_ws(ctx, "bb.CAT", sCat * 4, &p))) return rc;
-  CAT = (float*)p;
   if ((rc = ensure_ws(ctx, "bb.COL", sCol * 4, &p))) return rc;
   COL = (float*)p;
   if ((rc = ensure_ws(ctx, "bb.POOL", sPool * 4, &p))) return rc;
   POOL = (float*)p;
   if ((rc = ensure_ws(ctx, "bb.PPM", sPpm * 4, &p))) return rc;
   PPM = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.Q", sQ * 4, &p))) return rc;
+  QB = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.R", sR * 4, &p))) return rc;
+  RB = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.F", sF * 4, &p))) return rc;
+  FB = (float*)p;
+  if ((rc = ensure_ws(ctx, "bb.PARTS", sPartS * 4, &p))) return rc;
+  PARTS = (float*)p;
 
   std::vector<ConvCall> calls;
   int stage = 0;
@@ -429,7 +479,6 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
       const Block& blk = bb->blocks[li][bi];
       const int Cin = blk.c1.Ci;
       const int Ho = (blk.c2.stride == 2) ? down2(H) : H;
-      const bool last = (li == 3 && bi == nbk - 1);
       cc(&blk.c1, cur, N, H, H, Cin, T1, blk.c1.Co, 0, nullptr, 0, 1);
       cc(&blk.c2, T1, N, H, H, blk.c2.Ci, T2, blk.c2.Co, 0, nullptr, 0, 1);
       const float* res = cur;
@@ -439,27 +488,16 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
         res = D;
         res_ld = blk.down.Co;
       }
-      float* out = last ? CAT : other;
-      const int out_ld = last ? 4096 : blk.c3.Co;
-      cc(&blk.c3, T2, N, Ho, Ho, blk.c3.Ci, out, out_ld, 0, res, res_ld, 1);
+      cc(&blk.c3, T2, N, Ho, Ho, blk.c3.Ci, other, blk.c3.Co, 0, res, res_ld, 1);
       std::swap(cur, other);
       H = Ho;
     }
   }
   const size_t n_backbone_calls = calls.size();
-  // PPM 1x1 convs over the pooled cells (bin-major rows), then the bottleneck conv
-  stage = 5;
-  {
-    long off_in = 0, off_out = 0;
-    for (int i = 0; i < 4; ++i) {
-      const int cells = N * kBins[i] * kBins[i];
-      cc(&bb->ppm[i], POOL + off_in * 2048, 1, 1, cells, 2048, PPM + off_out * 512, 512, 0, nullptr, 0, 1);
-      off_in += cells;
-      off_out += cells;
-    }
-  }
+  const float* L4 = cur;  // layer4 output [N][h][h][2048]
+  // the bottleneck conv over the layer4 channels; the folded PPM field FB enters as residual
   stage = 6;
-  cc(&bb->bott, CAT, N, h, h, 4096, feat, 512, 0, nullptr, 0, 1);
+  cc(&bb->bott, L4, N, h, h, 2048, feat, 512, 0, FB, 512, 1);
 
   // split-K scratch
   size_t part_floats = 0;
@@ -495,7 +533,10 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     return r;
   };
 
-  double all_flops = 2.0 * N * Hs * Hs * 64 * 27, all_bytes = 0.0;
+  const long cells = (long)N * 50;
+  const double ppm_flops = 2.0 * cells * 512 * 2048 + 2.0 * cells * 4608 * 512 +
+                           2.0 * N * 12 * h * 3 * 512 * 3 * 6 + 2.0 * N * h * h * 512 * 36;
+  double all_flops = 2.0 * N * Hs * Hs * 64 * 27 + ppm_flops, all_bytes = 0.0;
   for (auto& c : calls) {
     ConvArgs a = make_args(c);
     all_flops += 2.0 * a.M * a.Co * a.K;
@@ -518,17 +559,38 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     if ((rc = run_call(i))) return rc;
   {
     Prof p(ctx, st, "ppm_pool", 0.0, 4.0 * ((double)N * h * h * 2048 + (double)N * 50 * 2048));
-    if ((rc = launch_ppm(CAT, N, h, h, 4096, kBins, 4, COL, POOL, st))) return rc;
+    if ((rc = launch_ppm(L4, N, h, h, 2048, kBins, 4, COL, POOL, st))) return rc;
     p.end();
   }
-  for (size_t i = n_backbone_calls; i < n_backbone_calls + 4; ++i)
-    if ((rc = run_call(i))) return rc;
-  {
-    Prof p(ctx, st, "ppm_upsample", 0.0, 4.0 * ((double)N * h * h * 2048 + (double)N * 50 * 512));
-    if ((rc = launch_ppm_upsample(PPM, N, h, h, kBins, 4, 512, CAT, 4096, 2048, st))) return rc;
+  int Mb[4];
+  const float *Wp[4], *Wq[4], *Sc[4], *Sh[4];
+  for (int i = 0; i < 4; ++i) {
+    Mb[i] = N * kBins[i] * kBins[i];
+    Wp[i] = bb->ppm_wt[i];
+    Wq[i] = bb->ppm_q[i];
+    Sc[i] = bb->ppm[i].scale;
+    Sh[i] = bb->ppm[i].shift;
+  }
+  {  // PPM 1x1 conv + BN + ReLU over the pooled cells (pspnet.py:27-29)
+    Prof p(ctx, st, "ppm_conv smallm 2048x512", 2.0 * cells * 512 * 2048, 4.0 * (4.0 * 2048 * 512 + cells * 2560.0));
+    if ((rc = launch_smallm_gemm(POOL, 2048, Wp, Mb, 4, 512, 2048, kKcPpm, PARTS, (size_t)sPartS, Sc, Sh, PPM, st)))
+      return rc;
     p.end();
   }
-  rc = run_call(n_backbone_calls + 4);
+  {  // per-tap products of the bottleneck's PPM channels with the cells
+    Prof p(ctx, st, "ppm_fold_q smallm 512x4608", 2.0 * cells * 4608 * 512, 4.0 * (4.0 * 512 * 4608 + cells * 5120.0));
+    if ((rc = launch_smallm_gemm(PPM, 512, Wq, Mb, 4, 4608, 512, kKcQ, PARTS, (size_t)sPartS, nullptr, nullptr, QB,
+                                 st)))
+      return rc;
+    p.end();
+  }
+  {  // separable interpolation of the per-tap products: the PPM half of the bottleneck conv
+    Prof p(ctx, st, "ppm_field", 2.0 * N * 12 * h * 3 * 512 * 3 * 6 + 2.0 * N * h * h * 512 * 36,
+           4.0 * ((double)cells * 4608 + 2.0 * sR + sF));
+    if ((rc = launch_ppm_field(QB, N, h, h, kBins, RB, FB, st))) return rc;
+    p.end();
+  }
+  rc = run_call(n_backbone_calls);
   whole.end();
   return rc;
 }
@@ -735,15 +797,24 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
   L.pad = pad;
   L.dil = dil;
   L.w = (float*)w_packed;
+  int rc;
+  if (k > 1 && precision != 2) {  // caller layout [Co][k][k][Ci] -> packed_k order
+    void* wp;
+    if ((rc = ensure_ws(ctx, "dbg.wpack", (size_t)Co * k * k * Ci * 4, &wp))) return rc;
+    if ((rc = launch_repack_cblock(w_packed, (float*)wp, Co, k * k, Ci, (hipStream_t)stream))) return rc;
+    L.w = (float*)wp;
+    w_packed = L.w;
+  }
   L.scale = (float*)scale;
   L.shift = (float*)shift;
   ConvCall c{0, &L, x, N, Hi, Wi, x_ld, y, y_ld, y_off, res, res_ld, relu};
   ConvArgs a = make_args(c);
-  const bool x3 = precision == 1;
+  const bool x3 = precision == 1 || precision == 2;
   ConvPlan p = x3 ? plan_conv_x3(a.M, a.Co, a.K) : plan_conv(a.M, a.Co, a.K);
   if (bm > 0) {
-    CWT_CHECK((bm == 128 && (bn == 128 || bn == 64)) || (bm == 64 && bn == 64) || (x3 && bm == 64 && bn == 128),
-              "tile must be 128x128, 128x64, 64x64 (or 64x128 for bf16x3)");
+    CWT_CHECK((bm == 128 && (bn == 128 || bn == 64)) || (bm == 64 && bn == 64) ||
+                  (x3 && ((bm == 64 && bn == 128) || (bm == 256 && (bn == 256 || bn == 128)))),
+              "tile must be 128x128, 128x64, 64x64 (or 64x128, 256x256, 256x128 for bf16x3)");
     CWT_CHECK(Co % bn == 0, "Co % bn");
     p.bm = bm;
     p.bn = bn;
@@ -755,11 +826,15 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
   }
   void* part = nullptr;
   size_t pf = (size_t)p.nsplit * a.M * a.Co;
-  int rc;
   if (p.nsplit > 1 && (rc = ensure_ws(ctx, "dbg.PART", pf * 4, &part))) return rc;
   if (!x3) return launch_conv(a, p, 0, (float*)part, pf, (hipStream_t)stream);
   void *hi, *lo;
   const long nw = (long)Co * a.K;
+  if (precision == 2) {  // w_packed already holds bf16 hi [Co][K] followed by lo [Co][K]
+    a.w_hi = (const __bf16*)w_packed;
+    a.w_lo = (const __bf16*)w_packed + nw;
+    return launch_conv_x3(a, p, 0, (float*)part, pf, (hipStream_t)stream);
+  }
   if ((rc = ensure_ws(ctx, "dbg.whi", nw * 2, &hi)) || (rc = ensure_ws(ctx, "dbg.wlo", nw * 2, &lo))) return rc;
   if ((rc = launch_split_bf16(w_packed, (__bf16*)hi, (__bf16*)lo, nw, (hipStream_t)stream))) return rc;
   a.w_hi = (const __bf16*)hi;

@@ -3,8 +3,11 @@
 //    reading the caller's NCHW image and writing NHWC            (resnet.py:111-112,147)
 //  * maxpool 3x3 s2 p1 (-inf padding)                           (resnet.py:118)
 //  * PPM adaptive average pooling for all bins in one sweep     (pspnet.py:26)
-//  * PPM bilinear(align_corners) upsample written straight into the concat buffer
-//    channel slices, so torch.cat never materialises a copy  (pspnet.py:37-38)
+//  * the PPM branch of the bottleneck conv, folded: small-M GEMMs over the pooled cells and
+//    a separable interpolation of their per-tap products   (pspnet.py:19-38,124-128); the
+//    concat buffer of the reference (torch.cat) is never materialised
+#include <cstring>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -123,45 +126,52 @@ static PPMWindows make_windows(int in, const int* bins, int nbins) {
   return wd;
 }
 
-// colsum[n][y][win][c] = sum_{x in window} cat[n][y][x][c]; one thread per (n, y, c4).
+// colsum[n][y][win][c] = sum_{x in window} x[n][y][x][c]; one thread per (n, y, c): four
+// threads per 16-B chunk keep ~4x the waves of a float4 mapping in flight (the sweep is
+// latency-bound), 8 loads outstanding per thread.
 __global__ void ppm_colsum_kernel(const float* __restrict__ cat, int N, int h, int w, int ld, int C,
                                   PPMWindows wd, float* __restrict__ colsum) {
-  const int c4n = C >> 2;
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * h * c4n;
+  long total = (long)N * h * C;
   if (idx >= total) return;
-  int c4 = (int)(idx % c4n);
-  long ny = idx / c4n;  // n*h + y
-  f32x4 acc[16];
+  const int c = (int)(idx % C);
+  const long ny = idx / C;  // n*h + y
+  float acc[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* row = cat + ny * w * (long)ld + c4 * 4;
-  for (int x = 0; x < w; ++x) {
-    f32x4 v = *(const f32x4*)(row + (long)x * ld);
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  const float* row = cat + ny * w * (long)ld + c;
+  for (int x0 = 0; x0 < w; x0 += 8) {
+    float v[8];  // unconditional loads at clamped addresses: no branch joins between them
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i < wd.nwin && x >= wd.st[i] && x < wd.en[i]) acc[i] += v;
+    for (int u = 0; u < 8; ++u) v[u] = row[(long)min(x0 + u, w - 1) * ld];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int x = x0 + u;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (i < wd.nwin && x >= wd.st[i] && x < wd.en[i]) acc[i] += v[u];
+    }
   }
-  float* o = colsum + ny * (long)wd.nwin * C + c4 * 4;
+  float* o = colsum + ny * (long)wd.nwin * C + c;
 #pragma unroll
   for (int i = 0; i < 16; ++i)
-    if (i < wd.nwin) *(f32x4*)(o + (long)i * C) = acc[i];
+    if (i < wd.nwin) o[(long)i * C] = acc[i];
 }
 
-// pooled (bin-major, [sum_b N*b*b][C]) = ((sum over window rows of colsum) / kh) / kw
+// pooled (bin-major, [sum_b N*b*b][C]) = ((sum over window rows of colsum) / kh) / kw;
+// one thread per (n, cell, c).
 __global__ void ppm_pool_kernel(const float* __restrict__ colsum, int N, int h, int C, PPMWindows wr,
                                 PPMWindows wc, int nbins, int b0, int b1, int b2, int b3,
                                 float* __restrict__ pooled) {
   const int bins[4] = {b0, b1, b2, b3};
   int ncells = 0;
   for (int k = 0; k < nbins; ++k) ncells += bins[k] * bins[k];
-  const int c4n = C >> 2;
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * ncells * c4n;
+  long total = (long)N * ncells * C;
   if (idx >= total) return;
-  int c4 = (int)(idx % c4n);
-  int cell = (int)((idx / c4n) % ncells);
-  int n = (int)(idx / ((long)c4n * ncells));
+  const int c = (int)(idx % C);
+  const int cell = (int)((idx / C) % ncells);
+  const int n = (int)(idx / ((long)C * ncells));
   int base = 0, woff = 0, k = 0;
   while (cell >= base + bins[k] * bins[k]) {
     base += bins[k] * bins[k];
@@ -171,17 +181,22 @@ __global__ void ppm_pool_kernel(const float* __restrict__ colsum, int N, int h, 
   const int b = bins[k];
   const int i = (cell - base) / b, j = (cell - base) % b;
   const int wrow = woff + i, wcol = woff + j;
-  int ys = wr.st[wrow], ye = wr.en[wrow];
-  int xs = wc.st[wcol], xe = wc.en[wcol];
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  for (int y = ys; y < ye; ++y)
-    s += *(const f32x4*)(colsum + (((long)n * h + y) * wc.nwin + wcol) * C + c4 * 4);
-  const float kh = (float)(ye - ys), kw = (float)(xe - xs);
-  f32x4 r;
+  const int ys = wr.st[wrow], ye = wr.en[wrow];
+  const int xs = wc.st[wcol], xe = wc.en[wcol];
+  const float* src = colsum + ((long)n * h * wc.nwin + wcol) * C + c;
+  const long ystride = (long)wc.nwin * C;
+  float s = 0.f;
+  for (int y0 = ys; y0 < ye; y0 += 8) {
+    float v[8];  // unconditional loads at clamped addresses
 #pragma unroll
-  for (int q = 0; q < 4; ++q) r[q] = (s[q] / kh) / kw;
-  long out_row = (long)base * N + (long)n * b * b + i * b + j;
-  *(f32x4*)(pooled + out_row * C + c4 * 4) = r;
+    for (int u = 0; u < 8; ++u) v[u] = src[min(y0 + u, ye - 1) * ystride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (y0 + u < ye) s += v[u];
+  }
+  const float kh = (float)(ye - ys), kw = (float)(xe - xs);
+  const long out_row = (long)base * N + (long)n * b * b + i * b + j;
+  pooled[out_row * C + c] = (s / kh) / kw;
 }
 
 int launch_ppm(const float* cat, int N, int h, int w, int ld, const int* bins, int nbins, float* colsum,
@@ -193,56 +208,268 @@ int launch_ppm(const float* cat, int N, int h, int w, int ld, const int* bins, i
   const int C = 2048;
   int ncells = 0;
   for (int b = 0; b < nbins; ++b) ncells += bins[b] * bins[b];
-  long t1 = (long)N * h * (C / 4);
+  long t1 = (long)N * h * C;
   hipLaunchKernelGGL(ppm_colsum_kernel, dim3(cdiv(t1, 256)), dim3(256), 0, st, cat, N, h, w, ld, C, wc, colsum);
   CWT_LAUNCH_CHECK();
-  long t2 = (long)N * ncells * (C / 4);
+  long t2 = (long)N * ncells * C;
   hipLaunchKernelGGL(ppm_pool_kernel, dim3(cdiv(t2, 256)), dim3(256), 0, st, colsum, N, h, C, wr, wc, nbins,
                      bins[0], bins[1], bins[2], bins[3], pooled);
   CWT_LAUNCH_CHECK();
   return 0;
 }
 
-// cat[n][y][x][off + bin*red + c] = bilinear(ppm_out_bin[n][b][b][red]) (align_corners=True)
-__global__ void ppm_upsample_kernel(const float* __restrict__ ppm_out, int N, int h, int w, int nbins,
-                                    int b0, int b1, int b2, int b3, int red, float* __restrict__ cat, int ld,
-                                    int off) {
-  const int c4n = nbins * red / 4;
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * h * w * c4n;
-  if (idx >= total) return;
-  int c4 = (int)(idx % c4n);
-  long pix = idx / c4n;
-  int x = (int)(pix % w);
-  int y = (int)((pix / w) % h);
-  int n = (int)(pix / ((long)w * h));
-  int bin = (c4 * 4) / red;
-  int c = c4 * 4 - bin * red;
-  int bins[4] = {b0, b1, b2, b3};
-  int base = 0;
-  for (int k = 0; k < bin; ++k) base += bins[k] * bins[k];
-  int b = bins[bin];
-  const float sy = (h > 1) ? (float)(b - 1) / (float)(h - 1) : 0.f;
-  const float sx = (w > 1) ? (float)(b - 1) / (float)(w - 1) : 0.f;
-  Lerp ly = lerp_coord(y, b, sy), lx = lerp_coord(x, b, sx);
-  const float* src = ppm_out + ((long)base * N + (long)n * b * b) * red + c;
-  f32x4 v00 = *(const f32x4*)(src + ((long)ly.i0 * b + lx.i0) * red);
-  f32x4 v01 = *(const f32x4*)(src + ((long)ly.i0 * b + lx.i1) * red);
-  f32x4 v10 = *(const f32x4*)(src + ((long)ly.i1 * b + lx.i0) * red);
-  f32x4 v11 = *(const f32x4*)(src + ((long)ly.i1 * b + lx.i1) * red);
-  f32x4 r;
+// ---------------------------------------------------------------------------------------
+// PPM branch of the bottleneck conv, folded (pspnet.py:19-38,124-128).
+//
+// The bottleneck conv reads concat[layer4 (2048 ch), up_b(P_b) (4 x 512 ch)], where
+// P_b = relu(BN(conv1x1(pool_b(x)))) lives on a b x b grid (b = 1, 2, 3, 6) and up_b is the
+// bilinear align_corners upsample to h x w.  Both the upsample and the conv are linear, so
+//   conv3x3(W_b, up_b(P_b))(y, x) = sum_{ky,kx} sum_{i,j} u_b(y+ky-1, i) u_b(x+kx-1, j) Q_b[i][j][ky][kx]
+// with Q_b[i][j][tap] = W_b[tap] . P_b[i][j] (a 512 x 4608 GEMM over the b*b cells) and
+// u_b the 1-D interpolation weights (zero outside [0, h): the conv's zero padding).  The
+// bottleneck conv then only runs over the 2048 layer4 channels (half its FLOPs) with the
+// PPM field F added in its epilogue as a residual (BN scale pre-folded into Q's weights).
+// ---------------------------------------------------------------------------------------
+
+// Small-M fp32 GEMM, block-diagonal over up to 4 problems sharing N and K:
+//   part[ks][m][n] = sum_{k in chunk ks} A[m][k] Bt_p[k][n]   for rows m of problem p.
+// Weights are stored K-major so a wave streams 64 consecutive n of one k row (coalesced);
+// the A block (SG_MB rows x kc) sits in LDS and is read as broadcasts.  Each wave owns 64
+// columns over the whole chunk, so no cross-wave reduction; chunks are summed in fixed
+// order by smallm_finish_kernel (deterministic).
+constexpr int SG_MB = 24;  // rows per workgroup: the A block (24 x 64 fp32) fits the scalar cache
+typedef const float __attribute__((address_space(4))) const_f32;
+struct SmallGemmArgs {
+  const float* A;      // [Mtot][lda]
+  const float* Bt[4];  // [K][N] per problem
+  float* part;         // [nks][Mtot][N]
+  int row0[4], M[4], wg0[5];
+  int np, Mtot, N, K, lda, nks;
+};
+
+// Each lane first issues the loads of its whole B column chunk (KC values in flight), then
+// runs rows x KC FMAs whose A operand is wave-uniform: read with scalar loads (SGPR operands
+// of v_fma), so the broadcast costs neither LDS bandwidth nor VGPRs.
+template <int KC>
+__global__ __launch_bounds__(256) void smallm_gemm_kernel(SmallGemmArgs g) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  int p = 0;
+  while (p + 1 < g.np && (int)blockIdx.x >= g.wg0[p + 1]) ++p;
+  int w = (int)blockIdx.x - g.wg0[p];
+  const int nnb = g.N / 256;
+  const int nb = w % nnb;
+  w /= nnb;
+  const int ks = w % g.nks;
+  const int mb = w / g.nks;
+  const int m0 = g.row0[p] + mb * SG_MB;
+  const int rows = min(SG_MB, g.row0[p] + g.M[p] - m0);
+  const int k0 = ks * KC;
+  const int n = nb * 256 + wv * 64 + lane;
+  const float* b = g.Bt[p] + (long)k0 * g.N + n;
+  float bv[KC];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    r[q] = ly.l0 * (lx.l0 * v00[q] + lx.l1 * v01[q]) + ly.l1 * (lx.l0 * v10[q] + lx.l1 * v11[q]);
-  *(f32x4*)(cat + pix * ld + off + bin * red + c) = r;
+  for (int k = 0; k < KC; ++k) bv[k] = b[(long)k * g.N];
+  float* o = g.part + ((long)ks * g.Mtot + m0) * g.N + n;
+  for (int r0 = 0; r0 < rows; r0 += 4) {
+    float acc[4];
+    const_f32* ar[4];  // constant address space: uniform reads become s_load
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      acc[r] = 0.f;
+      ar[r] = (const_f32*)(g.A + (long)min(m0 + r0 + r, g.Mtot - 1) * g.lda + k0);  // clamped: a valid row
+    }
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = fmaf(ar[r][k], bv[k], acc[r]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r0 + r < rows) o[(long)(r0 + r) * g.N] = acc[r];
+  }
 }
 
-int launch_ppm_upsample(const float* ppm_out, int N, int h, int w, const int* bins, int nbins, int red, float* cat,
-                        int ld, int off, hipStream_t st) {
-  if (nbins != 4) return fail(CWT_EARG, "PPM expects 4 bins");
-  long total = (long)N * h * w * (nbins * red / 4);
-  hipLaunchKernelGGL(ppm_upsample_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, ppm_out, N, h, w, nbins,
-                     bins[0], bins[1], bins[2], bins[3], red, cat, ld, off);
+// out[m][n] = sum_ks part[ks][m][n] (fixed order), then for problems with a BN:
+// relu(scale[n] * s + shift[n]).
+struct SmallFinishArgs {
+  const float* scale[4];
+  const float* shift[4];
+  int row0[5];
+  int np;
+};
+__global__ void smallm_finish_kernel(const float* __restrict__ part, int nks, int Mtot, int N, SmallFinishArgs f,
+                                     float* __restrict__ out) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)Mtot * (N >> 2);
+  if (idx >= total) return;
+  const long e = idx * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  const long cs = (long)Mtot * N;
+  for (int k0 = 0; k0 < nks; k0 += 8) {  // 8 loads in flight, summed in chunk order
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(part + min(k0 + u, nks - 1) * cs + e);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (k0 + u < nks) s += v[u];
+  }
+  const int m = (int)(e / N), n = (int)(e % N);
+  int p = 0;
+  while (p + 1 < f.np && m >= f.row0[p + 1]) ++p;
+  if (f.scale[p]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] = fmaxf(fmaf(s[q], f.scale[p][n + q], f.shift[p][n + q]), 0.f);
+  }
+  *(f32x4*)(out + e) = s;
+}
+
+int launch_smallm_gemm(const float* A, int lda, const float* const* Bt, const int* M, int np, int N, int K, int kc,
+                       float* part, size_t part_floats, const float* const* scale, const float* const* shift,
+                       float* out, hipStream_t st) {
+  if (np < 1 || np > 4 || N % 256 != 0 || (kc != 32 && kc != 64) || K % kc != 0)
+    return fail(CWT_EARG, "smallm_gemm: need 1..4 problems, N % 256 == 0, kc in {32, 64}, K % kc == 0");
+  SmallGemmArgs g;
+  memset(&g, 0, sizeof(g));
+  SmallFinishArgs f;
+  memset(&f, 0, sizeof(f));
+  g.A = A;
+  g.part = part;
+  g.np = f.np = np;
+  g.N = N;
+  g.K = K;
+  g.lda = lda;
+  g.nks = K / kc;
+  int row = 0, wg = 0;
+  for (int q = 0; q < np; ++q) {
+    g.Bt[q] = Bt[q];
+    g.row0[q] = f.row0[q] = row;
+    g.M[q] = M[q];
+    g.wg0[q] = wg;
+    f.scale[q] = scale ? scale[q] : nullptr;
+    f.shift[q] = shift ? shift[q] : nullptr;
+    row += M[q];
+    wg += cdiv(M[q], SG_MB) * g.nks * (N / 256);
+  }
+  g.wg0[np] = wg;
+  f.row0[np] = row;
+  g.Mtot = row;
+  if ((size_t)g.nks * row * N > part_floats) return fail(CWT_ESTATE, "smallm_gemm: partial workspace too small");
+  if (kc == 32)
+    hipLaunchKernelGGL(smallm_gemm_kernel<32>, dim3(wg), dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL(smallm_gemm_kernel<64>, dim3(wg), dim3(256), 0, st, g);
+  CWT_LAUNCH_CHECK();
+  const long total = (long)row * (N / 4);
+  hipLaunchKernelGGL(smallm_finish_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)part, g.nks, row,
+                     N, f, out);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+// Interpolation table for destination p in [-1, out] (the 3x3 conv's zero padding outside
+// [0, out)): source cells i0, i1 with weights l0, l1 of the align_corners upsample in -> out.
+struct LerpEntry {
+  int i0, i1;
+  float l0, l1;
+};
+__device__ __forceinline__ LerpEntry lerp_entry(int p, int out, int in) {
+  LerpEntry e{0, 0, 0.f, 0.f};
+  if (p < 0 || p >= out) return e;
+  const float sc = (out > 1) ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  const Lerp l = lerp_coord(p, in, sc);
+  e.i0 = l.i0;
+  e.i1 = l.i1;
+  e.l0 = l.l0;
+  e.l1 = l.l1;
+  return e;
+}
+
+struct PPMBins {
+  int b[4];
+  int cell0[4];  // first cell (per image) of bin k in the bin-major cell order: 0, 1, 5, 14
+  int row0[4];   // first grid row of bin k among the 12 rows (1 + 2 + 3 + 6): 0, 1, 3, 6
+};
+
+constexpr int PPM_MAXS = 160;  // largest feature side the field kernels take (641 -> 81)
+
+// Pass 1 (columns): R[n][row][x][ky][c] = sum_{kx} sum_{j in {i0, i1}(x+kx-1)} u Q[cell(row, j)][ky*3+kx][c].
+// Workgroup = (n, grid row, 64 channels); Q for the row's cells staged in LDS.
+__global__ __launch_bounds__(256) void ppm_field_cols_kernel(const float* __restrict__ Q, int N, int w, PPMBins bn,
+                                                             float* __restrict__ R) {
+  __shared__ f32x4 qs[6 * 9 * 16];
+  __shared__ LerpEntry tab[PPM_MAXS + 2];
+  const int t = threadIdx.x;
+  const int n = blockIdx.x / 12, row = blockIdx.x % 12, c0 = blockIdx.y * 64;
+  int k = 3;
+  while (row < bn.row0[k]) --k;
+  const int b = bn.b[k], i = row - bn.row0[k];
+  const long cell0 = (long)bn.cell0[k] * N + (long)n * b * b + (long)i * b;  // first cell of this grid row
+  for (int e = t; e < b * 9 * 16; e += 256) {
+    const int c4 = e & 15, jt = e >> 4;  // jt = j * 9 + tap
+    qs[e] = *(const f32x4*)(Q + (cell0 + jt / 9) * 4608 + (jt % 9) * 512 + c0 + 4 * c4);
+  }
+  for (int p = t; p < w + 2; p += 256) tab[p] = lerp_entry(p - 1, w, b);
+  __syncthreads();
+  for (int e = t; e < w * 3 * 16; e += 256) {
+    const int c4 = e & 15, xk = e >> 4;
+    const int x = xk / 3, ky = xk - 3 * (xk / 3);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const LerpEntry l = tab[x + kx];  // destination x + kx - 1
+      acc += l.l0 * qs[(l.i0 * 9 + ky * 3 + kx) * 16 + c4];
+      acc += l.l1 * qs[(l.i1 * 9 + ky * 3 + kx) * 16 + c4];
+    }
+    *(f32x4*)(R + ((((long)n * 12 + row) * w + x) * 3 + ky) * 512 + c0 + 4 * c4) = acc;
+  }
+}
+
+// Pass 2 (rows): F[n][y][x][c] = sum_{k, ky} sum_{i in {i0, i1}(y+ky-1)} u_k R[n][row(k, i)][x][ky][c].
+// Workgroup = (n, x, 64 channels); the 12 x 3 R vectors of this column staged in LDS.
+__global__ __launch_bounds__(256) void ppm_field_rows_kernel(const float* __restrict__ R, int N, int h, int w,
+                                                             PPMBins bn, float* __restrict__ F) {
+  __shared__ f32x4 rs[12 * 3 * 16];
+  __shared__ LerpEntry tab[4][PPM_MAXS + 2];
+  const int t = threadIdx.x;
+  const int n = blockIdx.x / w, x = blockIdx.x % w, c0 = blockIdx.y * 64;
+  for (int e = t; e < 12 * 3 * 16; e += 256) {
+    const int c4 = e & 15, rk = e >> 4;  // rk = row * 3 + ky
+    rs[e] = *(const f32x4*)(R + ((((long)n * 12 + rk / 3) * w + x) * 3 + rk % 3) * 512 + c0 + 4 * c4);
+  }
+  for (int e = t; e < 4 * (h + 2); e += 256) {
+    const int k = e / (h + 2), p = e - k * (h + 2);
+    tab[k][p] = lerp_entry(p - 1, h, bn.b[k]);
+  }
+  __syncthreads();
+  for (int e = t; e < h * 16; e += 256) {
+    const int c4 = e & 15, y = e >> 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const LerpEntry l = tab[k][y + ky];  // destination y + ky - 1
+        acc += l.l0 * rs[((bn.row0[k] + l.i0) * 3 + ky) * 16 + c4];
+        acc += l.l1 * rs[((bn.row0[k] + l.i1) * 3 + ky) * 16 + c4];
+      }
+    *(f32x4*)(F + (((long)n * h + y) * w + x) * 512 + c0 + 4 * c4) = acc;
+  }
+}
+
+int launch_ppm_field(const float* Q, int N, int h, int w, const int* bins, float* R, float* F, hipStream_t st) {
+  PPMBins bn;
+  int cell = 0, row = 0;
+  for (int k = 0; k < 4; ++k) {
+    bn.b[k] = bins[k];
+    bn.cell0[k] = cell;
+    bn.row0[k] = row;
+    cell += bins[k] * bins[k];
+    row += bins[k];
+  }
+  if (row != 12 || bins[3] > 6 || h > PPM_MAXS || w > PPM_MAXS)
+    return fail(CWT_EARG, "PPM field expects bins {1,2,3,6} and a feature side <= 160");
+  hipLaunchKernelGGL(ppm_field_cols_kernel, dim3(N * 12, 8), dim3(256), 0, st, Q, N, w, bn, R);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ppm_field_rows_kernel, dim3(N * w, 8), dim3(256), 0, st, (const float*)R, N, h, w, bn, F);
   CWT_LAUNCH_CHECK();
   return 0;
 }

@@ -39,6 +39,24 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// DPP lane exchanges (VALU modifiers, no LDS round trip): quad_perm xor 1 / xor 2, and the
+// 8- / 16-lane mirrors.  After xor1, xor2, half-mirror every lane of an aligned octet holds
+// the octet's sum; a further row-mirror gives the 16-lane row sum.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float octet_sum(float v) {
+  return dpp_add<0x141>(dpp_add<0x4E>(dpp_add<0xB1>(v)));
+}
+// Full 64-lane sum, wave-uniform result: row sums by DPP, then four readlanes.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = dpp_add<0x140>(octet_sum(v));
+  const int i = __float_as_int(v);
+  return (__int_as_float(__builtin_amdgcn_readlane(i, 0)) + __int_as_float(__builtin_amdgcn_readlane(i, 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(i, 32)) + __int_as_float(__builtin_amdgcn_readlane(i, 48)));
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -20,6 +20,8 @@
 // Epilogue: y = acc*scale[co] + shift[co] (+ residual) (ReLU), written NHWC at a channel
 // offset/stride so layer4 can write straight into the PPM concat buffer.  With split-K
 // the raw partial sums go to a workspace and conv_splitk_epilogue applies the same math.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -41,9 +43,10 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(ConvArgs a) {
   const int lane = tid & 63;
   const int wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int ks = blockIdx.z;
+  int mt, nt, ks;
+  conv_tile_coords(mt, nt, ks);
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
   const int kt_begin = ks * a.kt_per_split;
   const int kt_end = min(a.ktiles, kt_begin + a.kt_per_split);
 
@@ -74,8 +77,10 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(ConvArgs a) {
   f32x4 ra[A_LD], rb[B_LD];
   auto load_slice = [&](int kt) {
     const int k0 = kt * BK;
-    const int tap = k0 / a.Ci;
-    const int ci0 = k0 - tap * a.Ci;
+    const int taps = a.kh * a.kw;  // packed_k order: 32-channel block major, taps inner
+    const int cb = kt / taps;
+    const int tap = kt - cb * taps;
+    const int ci0 = cb * BK;
     const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
     const int dy = ky * a.dil, dx = kx * a.dil;
 #pragma unroll
@@ -165,6 +170,9 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(ConvArgs a) {
 }
 
 // Sum split-K partials in fixed order (deterministic), then BN / residual / ReLU.
+// NS = compile-time split count (0: runtime nsplit): every partial and the residual are
+// loaded before the first add, then summed in split order (deterministic).
+template <int NS>
 __global__ void conv_splitk_epilogue(ConvArgs a, int nsplit) {
   const int c4n = a.Co >> 2;
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -172,14 +180,28 @@ __global__ void conv_splitk_epilogue(ConvArgs a, int nsplit) {
   if (idx >= total) return;
   int m = (int)(idx / c4n);
   int co = (int)(idx - (long)m * c4n) * 4;
-  f32x4 s = *(const f32x4*)(a.part + (long)m * a.Co + co);
-  for (int k = 1; k < nsplit; ++k) s += *(const f32x4*)(a.part + ((long)k * a.M + m) * a.Co + co);
+  const long ps = (long)a.M * a.Co;
+  const float* pp = a.part + (long)m * a.Co + co;
+  f32x4 s;
+  f32x4 r = {0.f, 0.f, 0.f, 0.f};
+  if (a.res) r = *(const f32x4*)(a.res + (long)m * a.res_ld + co);
+  if (NS > 0) {
+    f32x4 pv[NS > 0 ? NS : 1];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) pv[k] = *(const f32x4*)(pp + k * ps);
+    s = pv[0];
+#pragma unroll
+    for (int k = 1; k < NS; ++k) s += pv[k];
+  } else {
+    s = *(const f32x4*)pp;
+    for (int k = 1; k < nsplit; ++k) s += *(const f32x4*)(pp + k * ps);
+  }
   f32x4 sc = *(const f32x4*)(a.scale + co);
   f32x4 sh = *(const f32x4*)(a.shift + co);
   f32x4 v;
 #pragma unroll
   for (int q = 0; q < 4; ++q) v[q] = fmaf(s[q], sc[q], sh[q]);
-  if (a.res) v += *(const f32x4*)(a.res + (long)m * a.res_ld + co);
+  v += r;
   if (a.relu) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
@@ -244,7 +266,34 @@ int launch_conv(ConvArgs a, const ConvPlan& p, int stage, float* part_ws, size_t
 
 int launch_splitk_epilogue(const ConvArgs& a, int nsplit, hipStream_t st) {
   long total = (long)a.M * (a.Co / 4);
-  hipLaunchKernelGGL(conv_splitk_epilogue, dim3(cdiv(total, 256)), dim3(256), 0, st, a, nsplit);
+  const dim3 grid(cdiv(total, 256));
+  switch (nsplit) {
+    case 2: hipLaunchKernelGGL(conv_splitk_epilogue<2>, grid, dim3(256), 0, st, a, nsplit); break;
+    case 4: hipLaunchKernelGGL(conv_splitk_epilogue<4>, grid, dim3(256), 0, st, a, nsplit); break;
+    case 8: hipLaunchKernelGGL(conv_splitk_epilogue<8>, grid, dim3(256), 0, st, a, nsplit); break;
+    default: hipLaunchKernelGGL(conv_splitk_epilogue<0>, grid, dim3(256), 0, st, a, nsplit); break;
+  }
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+// [Co][taps][Ci] (tap-major) -> [Co][packed_k] (32-channel block major, taps inner).
+__global__ void repack_cblock_kernel(const float* __restrict__ src, float* __restrict__ dst, int Co, int taps,
+                                     int Ci) {
+  const long K = (long)taps * Ci;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < (long)Co * K; i += (long)gridDim.x * blockDim.x) {
+    const long co = i / K;
+    const int r = (int)(i - co * K);
+    const int tap = r / Ci, ci = r - tap * Ci;
+    dst[co * K + packed_k(ci, tap, taps)] = src[i];
+  }
+}
+
+int launch_repack_cblock(const float* src, float* dst, int Co, int taps, int Ci, hipStream_t st) {
+  if (Ci % 32) return fail(CWT_EARG, "repack: Ci % 32 != 0");
+  const long n = (long)Co * taps * Ci;
+  hipLaunchKernelGGL(repack_cblock_kernel, dim3((unsigned)std::min<long>(4096, cdiv(n, 256))), dim3(256), 0, st, src,
+                     dst, Co, taps, Ci);
   CWT_LAUNCH_CHECK();
   return 0;
 }

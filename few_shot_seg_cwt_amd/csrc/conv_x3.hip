@@ -24,13 +24,21 @@ namespace cwt {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-template <int BM, int BN, int STAGE>
-__global__ __launch_bounds__(256) void conv_igemm_bf16x3(ConvArgs a) {
+// Tile BM x BN, WAVES_M x WAVES_N waves (each WM x WN = TM x TN fragments of 32x32).
+// 4-wave tiles (up to 128x128) keep one workgroup per SIMD quad; the 8-wave 256-row tiles
+// halve the operand bytes per FLOP (a 128x128 tile asks ~42 B/clk/CU of L2->CU traffic at
+// the bf16 MFMA rate, close to the per-CU load bandwidth).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int STAGE>
+__global__ __launch_bounds__(WAVES_M * WAVES_N * 64) void conv_igemm_bf16x3(ConvArgs a) {
+  constexpr int NT = WAVES_M * WAVES_N * 64;
   constexpr int BK = 32;
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int A_LD = BM * 8 / 256;  // fp32 float4 per thread per A slice
-  constexpr int B_LD = BN * 4 / 256;  // 16-B bf16 chunks per thread per B slice (each of hi, lo)
+  constexpr int A_LD = BM * 8 / NT;  // fp32 float4 per thread per A slice
+  constexpr int B_LD = BN * 4 / NT;  // 16-B bf16 chunks per thread per B slice (each of hi, lo)
+  constexpr int A_PASS = NT / 8;     // A rows covered per load pass
+  constexpr int B_PASS = NT / 4;     // B rows covered per load pass
+  static_assert(A_LD >= 1 && B_LD >= 1 && TM >= 1 && TN >= 1, "tile too small for the thread count");
   // chunk (16 B) offsets of the four regions inside one stage
   constexpr int AHI = 0, ALO = BM * 4, BHI = BM * 8, BLO = BM * 8 + BN * 4;
   constexpr int STAGE_CHUNKS = BM * 8 + BN * 8;
@@ -39,21 +47,23 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16x3(ConvArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int ks = blockIdx.z;
+  const int wm = wv / WAVES_N, wn = wv % WAVES_N;
+  int mt, nt, ks;
+  conv_tile_coords(mt, nt, ks);
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
   const int kt_begin = ks * a.kt_per_split;
   const int kt_end = min(a.ktiles, kt_begin + a.kt_per_split);
 
-  // A gather geometry (constant over K): thread -> (row lr + 32j, float4 lc)
+  // A gather geometry (constant over K): thread -> (row lr + A_PASS j, float4 lc).  Element
+  // offsets are 32-bit (activations stay far below 2^31 floats); the per-tap shift is uniform.
   const int lc = tid & 7;
   const int lr = tid >> 3;
-  int a_ih0[A_LD], a_iw0[A_LD], a_pix[A_LD];
+  int a_ih0[A_LD], a_iw0[A_LD], a_off0[A_LD];
   const int HoWo = a.Ho * a.Wo;
 #pragma unroll
   for (int j = 0; j < A_LD; ++j) {
-    int m = m0 + lr + 32 * j;
+    int m = m0 + lr + A_PASS * j;
     if (m < a.M) {
       int n = m / HoWo;
       int rem = m - n * HoWo;
@@ -61,14 +71,14 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16x3(ConvArgs a) {
       int ow = rem - oh * a.Wo;
       a_ih0[j] = oh * a.stride - a.pad;
       a_iw0[j] = ow * a.stride - a.pad;
-      a_pix[j] = n * a.Hi * a.Wi;
+      a_off0[j] = ((n * a.Hi + a_ih0[j]) * a.Wi + a_iw0[j]) * a.x_ld + lc * 4;
     } else {
       a_ih0[j] = -(1 << 28);
       a_iw0[j] = 0;
-      a_pix[j] = 0;
+      a_off0[j] = 0;
     }
   }
-  // B geometry: thread -> (row br + 64j, chunk bc)
+  // B geometry: thread -> (row br + B_PASS j, chunk bc)
   const int bc = tid & 3;
   const int br = tid >> 2;
   const __bf16* whi = a.w_hi + (long)(n0 + br) * a.K + bc * 8;
@@ -76,42 +86,43 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16x3(ConvArgs a) {
 
   f32x4 ra[A_LD];
   bf16x8 rbh[B_LD], rbl[B_LD];
-  // incremental tap / channel position of the K slice (avoids per-slice integer division)
+  // incremental tap / channel position of the K slice (packed_k order: 32-channel block
+  // major, taps inner; avoids per-slice integer division)
   int cur_ci0 = 0, cur_ky = 0, cur_kx = 0;
+  const int taps = a.kh * a.kw;
   auto seek = [&](int kt) {
-    const int k0 = kt * BK;
-    const int tap = k0 / a.Ci;
-    cur_ci0 = k0 - tap * a.Ci;
+    const int cb = kt / taps;
+    const int tap = kt - cb * taps;
+    cur_ci0 = cb * BK;
     cur_ky = tap / a.kw;
     cur_kx = tap - cur_ky * a.kw;
   };
   auto advance = [&]() {
-    cur_ci0 += BK;
-    if (cur_ci0 == a.Ci) {
-      cur_ci0 = 0;
-      if (++cur_kx == a.kw) {
-        cur_kx = 0;
-        ++cur_ky;
+    if (++cur_kx == a.kw) {
+      cur_kx = 0;
+      if (++cur_ky == a.kh) {
+        cur_ky = 0;
+        cur_ci0 += BK;
       }
     }
   };
+  bool a_in[A_LD];
   auto load_slice = [&](int kt) {
     const int dy = cur_ky * a.dil, dx = cur_kx * a.dil;
+    const int shift = (dy * a.Wi + dx) * a.x_ld + cur_ci0;  // uniform
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
+      // unconditional load at a clamped (always valid) offset; out-of-image rows are zeroed
+      // when staged, so no branch (and no wait) sits between the loads
       const int ih = a_ih0[j] + dy, iw = a_iw0[j] + dx;
-      if ((unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi) {
-        const float* p = a.x + (long)(a_pix[j] + ih * a.Wi + iw) * a.x_ld + cur_ci0 + lc * 4;
-        ra[j] = *(const f32x4*)p;
-      } else {
-        ra[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      a_in[j] = (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+      ra[j] = *(const f32x4*)(a.x + (a_in[j] ? a_off0[j] + shift : lc * 4));
     }
     const int k0 = kt * BK;
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
-      rbh[j] = *(const bf16x8*)(whi + (long)(64 * j) * a.K + k0);
-      rbl[j] = *(const bf16x8*)(wlo + (long)(64 * j) * a.K + k0);
+      rbh[j] = *(const bf16x8*)(whi + (long)(B_PASS * j) * a.K + k0);
+      rbl[j] = *(const bf16x8*)(wlo + (long)(B_PASS * j) * a.K + k0);
     }
   };
   auto store_slice = [&](int buf) {
@@ -119,22 +130,23 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16x3(ConvArgs a) {
     bf16x4* sb4 = (bf16x4*)sb;
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
-      const int row = lr + 32 * j;
+      const int row = lr + A_PASS * j;
       const int c = lc >> 1, half = lc & 1;
       const int pos = row * 4 + (c ^ ((row >> 2) & 3));
       bf16x4 hi, lo;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const __bf16 hb = (__bf16)ra[j][q];
+        const float v = a_in[j] ? ra[j][q] : 0.f;
+        const __bf16 hb = (__bf16)v;
         hi[q] = hb;
-        lo[q] = (__bf16)(ra[j][q] - (float)hb);
+        lo[q] = (__bf16)(v - (float)hb);
       }
       sb4[(AHI + pos) * 2 + half] = hi;
       sb4[(ALO + pos) * 2 + half] = lo;
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
-      const int row = br + 64 * j;
+      const int row = br + B_PASS * j;
       const int pos = row * 4 + (bc ^ ((row >> 2) & 3));
       sb[BHI + pos] = rbh[j];
       sb[BLO + pos] = rbl[j];
@@ -213,29 +225,41 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16x3(ConvArgs a) {
 
 template <int STAGE>
 static void launch_tiles_x3(const ConvArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
-  if (p.bm == 128 && p.bn == 128)
-    hipLaunchKernelGGL((conv_igemm_bf16x3<128, 128, STAGE>), grid, dim3(256), 0, st, a);
+  if (p.bm == 256 && p.bn == 256)
+    hipLaunchKernelGGL((conv_igemm_bf16x3<256, 256, 2, 4, STAGE>), grid, dim3(512), 0, st, a);
+  else if (p.bm == 256 && p.bn == 128)
+    hipLaunchKernelGGL((conv_igemm_bf16x3<256, 128, 4, 2, STAGE>), grid, dim3(512), 0, st, a);
+  else if (p.bm == 128 && p.bn == 128)
+    hipLaunchKernelGGL((conv_igemm_bf16x3<128, 128, 2, 2, STAGE>), grid, dim3(256), 0, st, a);
   else if (p.bm == 128 && p.bn == 64)
-    hipLaunchKernelGGL((conv_igemm_bf16x3<128, 64, STAGE>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_igemm_bf16x3<128, 64, 2, 2, STAGE>), grid, dim3(256), 0, st, a);
   else if (p.bm == 64 && p.bn == 128)
-    hipLaunchKernelGGL((conv_igemm_bf16x3<64, 128, STAGE>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_igemm_bf16x3<64, 128, 2, 2, STAGE>), grid, dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((conv_igemm_bf16x3<64, 64, STAGE>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_igemm_bf16x3<64, 64, 2, 2, STAGE>), grid, dim3(256), 0, st, a);
 }
 
+// Largest tile that still yields >= kMinWG workgroups, splitting K (powers of two, at
+// least 8 k-tiles of 32 per split) where the output alone is too small a grid.
 ConvPlan plan_conv_x3(int M, int Co, int K) {
-  ConvPlan p;
+  constexpr long kMinWG = 200;
   const int ktiles = K / 32;
-  p.bn = (Co % 128 == 0) ? 128 : 64;
-  p.bm = 128;
-  auto tiles = [&]() { return (long)cdiv(M, p.bm) * (Co / p.bn); };
-  if (tiles() < 256) p.bm = 64;
-  if (tiles() < 256 && p.bn == 128) p.bn = 64;
-  int ks = 1;
-  while (tiles() * ks < 256 && ktiles / (ks * 2) >= 8) ks *= 2;
-  p.kt_per_split = cdiv(ktiles, ks);
-  p.nsplit = cdiv(ktiles, p.kt_per_split);
-  return p;
+  static const int cand[6][2] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  ConvPlan best;  // if no tile reaches kMinWG: the smallest one that divides Co, most splits
+  for (auto& c : cand) {
+    if (Co % c[1] != 0) continue;
+    const long tiles = (long)cdiv(M, c[0]) * (Co / c[1]);
+    int ks = 1;
+    while (tiles * ks < kMinWG && ktiles / (ks * 2) >= 8) ks *= 2;
+    ConvPlan p;
+    p.bm = c[0];
+    p.bn = c[1];
+    p.kt_per_split = cdiv(ktiles, ks);
+    p.nsplit = cdiv(ktiles, p.kt_per_split);
+    if (tiles * p.nsplit >= kMinWG) return p;
+    best = p;
+  }
+  return best;
 }
 
 int launch_conv_x3(ConvArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,

@@ -78,24 +78,30 @@ int launch_rowdot(const float* A, int R, int K, const float* X, int nv, long xvs
 }
 
 // out[g][v][k] += alpha * sum_{d in chunk} A[g*Dg + d][k] * X[v*xvs + g*Dg + d]
-// (transposed GEMV per group g).  Block = (k block of 256, group, d chunk of 64).
+// (transposed GEMV per group g).  Block = (k block of 256, group, d chunk of 16); the
+// chunk's 16 rows are loaded before any FMA (16 loads in flight per lane).
+constexpr int COLDOT_D = 16;
 __global__ __launch_bounds__(64) void coldot_kernel(const float* __restrict__ A, int K, int Dg,
                                                     const float* __restrict__ X, int nv, long xvs,
                                                     float* __restrict__ out, float alpha) {
   const int k = blockIdx.x * 256 + threadIdx.x * 4;
   const int g = blockIdx.y;
-  const int d0 = blockIdx.z * 64;
+  const int d0 = blockIdx.z * COLDOT_D;
   if (k >= K) return;
+  const int dn = min(COLDOT_D, Dg - d0);
+  f32x4 av[COLDOT_D];
+#pragma unroll
+  for (int d = 0; d < COLDOT_D; ++d) av[d] = *(const f32x4*)(A + ((long)g * Dg + d0 + min(d, dn - 1)) * K + k);
   f32x4 acc[8];
 #pragma unroll
   for (int v = 0; v < 8; ++v) acc[v] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int dn = min(64, Dg - d0);
-  for (int d = 0; d < dn; ++d) {
+#pragma unroll
+  for (int d = 0; d < COLDOT_D; ++d) {
+    if (d >= dn) break;
     const long row = (long)g * Dg + d0 + d;
-    const f32x4 av = *(const f32x4*)(A + row * K + k);
 #pragma unroll
     for (int v = 0; v < 8; ++v)
-      if (v < nv) acc[v] += X[v * xvs + row] * av;
+      if (v < nv) acc[v] += X[v * xvs + row] * av[d];
   }
 #pragma unroll
   for (int v = 0; v < 8; ++v)
@@ -109,7 +115,7 @@ __global__ __launch_bounds__(64) void coldot_kernel(const float* __restrict__ A,
 int launch_coldot(const float* A, int G, int Dg, int K, const float* X, int nv, long xvs, float* out, float alpha,
                   hipStream_t st) {
   if (nv > 8) return fail(CWT_EARG, "coldot: at most 8 vectors");
-  dim3 grid(cdiv(K, 256), G, cdiv(Dg, 64));
+  dim3 grid(cdiv(K, 256), G, cdiv(Dg, COLDOT_D));
   hipLaunchKernelGGL(coldot_kernel, grid, dim3(64), 0, st, A, K, Dg, X, nv, xvs, out, alpha);
   CWT_LAUNCH_CHECK();
   return 0;
@@ -164,7 +170,7 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(const float* __restri
       float d = 0.f;
 #pragma unroll
       for (int q = 0; q < 8; ++q) d = fmaf(rv[q], fv[tt][q], d);
-      s[tt][rho] = wave_sum(d);
+      s[tt][rho] = wave_sum_dpp(d);
     }
   }
   if (scores && lane < ATT_TPW) {
@@ -233,18 +239,36 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
   const int k = blockIdx.x * 64 + kk;
   const int rho = blockIdx.y, b = blockIdx.z;
   const float* ml = part_ml + ((long)b * nchunk * NR + rho) * 2;
+  // 8 chunks per round in flight (unconditional loads at clamped chunk indices)
   float M = -INFINITY;
-  for (int c = cg; c < nchunk; c += 4) M = fmaxf(M, ml[(long)c * NR * 2]);
+  for (int c0 = cg; c0 < nchunk; c0 += 32) {
+    float mv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mv[u] = ml[(long)min(c0 + 4 * u, nchunk - 1) * NR * 2];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) M = fmaxf(M, mv[u]);  // clamped duplicates do not change a max
+  }
   if (kk == 0) sm[cg] = M;
   __syncthreads();
   M = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
   float G = 0.f, L = 0.f;
   const float* pg = part_g + ((long)b * nchunk * NR + rho) * C + k;
-  for (int c = cg; c < nchunk; c += 4) {
-    const float mc = ml[(long)c * NR * 2];
-    const float sc = (mc == -INFINITY) ? 0.f : __expf(mc - M);
-    G = fmaf(sc, pg[(long)c * NR * C], G);
-    L = fmaf(sc, ml[(long)c * NR * 2 + 1], L);
+  for (int c0 = cg; c0 < nchunk; c0 += 32) {
+    float mc[8], lc[8], gc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long c = min(c0 + 4 * u, nchunk - 1);
+      mc[u] = ml[c * NR * 2];
+      lc[u] = ml[c * NR * 2 + 1];
+      gc[u] = pg[c * NR * C];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (c0 + 4 * u >= nchunk) break;
+      const float sc = (mc[u] == -INFINITY) ? 0.f : __expf(mc[u] - M);
+      G = fmaf(sc, gc[u], G);
+      L = fmaf(sc, lc[u], L);
+    }
   }
   sg[cg][kk] = G;
   if (kk == 0) sl[cg] = L;

@@ -23,6 +23,31 @@ struct ConvArgs {
   int relu;
 };
 
+// Conv weights are packed [Co][K] with K ordered (32-channel block, tap, channel in block):
+// a 3x3 conv's workgroup walks its 9 taps over one 32-channel slab of its input window
+// before the next slab, so the slab (~40 KB for 256 output pixels) is re-read from L1/L2
+// 9 times back to back instead of once per pass over all channels (an L2-missing
+// 9-fold re-stream of the window).  For 1x1 convs this is the plain channel order.
+__host__ __device__ __forceinline__ long packed_k(int ci, int tap, int taps) {
+  return (long)(ci >> 5) * (taps * 32) + tap * 32 + (ci & 31);
+}
+
+// Tile of this workgroup.  Blocks b and b+8 are observed to land on the same XCD (speed
+// only, MI355X_MICROARCH.md §Workgroup dispatch); the linear block id is remapped so that
+// each XCD gets one contiguous run of (split, m-tile, n-tile) with n fastest: its
+// workgroups share A rows across n-tiles and B columns across m-tiles in their L2.
+__device__ __forceinline__ void conv_tile_coords(int& mt, int& nt, int& ks) {
+  const int T = gridDim.x * gridDim.y * gridDim.z;
+  const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int q = T >> 3, r = T & 7;
+  const int xcd = lin & 7, slot = lin >> 3;
+  const int L = (xcd < r) ? xcd * (q + 1) + slot : r * (q + 1) + (xcd - r) * q + slot;
+  nt = L % gridDim.y;
+  const int rest = L / gridDim.y;
+  mt = rest % gridDim.x;
+  ks = rest / gridDim.x;
+}
+
 // Epilogue of one 32x32 MFMA accumulator fragment of the implicit-GEMM conv (C/D layout:
 // col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)): BN scale/shift, residual, ReLU, or
 // the raw split-K partial.  All 16 residual loads are issued (at clamped, always-valid
@@ -94,7 +119,10 @@ int launch_maxpool3s2(const float* in, int N, int H, int W, int C, float* out, i
                       hipStream_t st);
 int launch_ppm(const float* cat, int N, int h, int w, int ld, const int* bins, int nbins,
                float* colsum, float* pooled, hipStream_t st);
-int launch_ppm_upsample(const float* ppm_out, int N, int h, int w, const int* bins, int nbins,
-                        int red, float* cat, int ld, int off, hipStream_t st);
+int launch_repack_cblock(const float* src, float* dst, int Co, int taps, int Ci, hipStream_t st);
+int launch_smallm_gemm(const float* A, int lda, const float* const* Bt, const int* M, int np, int N, int K, int kc,
+                       float* part, size_t part_floats, const float* const* scale, const float* const* shift,
+                       float* out, hipStream_t st);
+int launch_ppm_field(const float* Q, int N, int h, int w, const int* bins, float* R, float* F, hipStream_t st);
 
 }  // namespace cwt

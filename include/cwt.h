@@ -187,10 +187,12 @@ int cwt_sgd_step(cwt_ctx* ctx, float* param, const float* grad, float* momentum_
  */
 /*
  * Test hook: one implicit-GEMM conv + folded BN (+residual) (+ReLU), NHWC, with the tile
- * (bm x bn in {128x128, 128x64, 64x64}, plus 64x128 for bf16x3; 0 = automatic) and split-K
- * count (0 = automatic) forced, so every plan can be checked against a reference conv.
- * precision: 0 = fp32 MFMA, 1 = bf16x3 (hi/lo split, 3 bf16 MFMAs per product).  w_packed: device
- * [Co][k][k][Ci]; scale/shift: device [Co]; res: NHWC (pixel stride res_ld) or NULL.
+ * (bm x bn in {128x128, 128x64, 64x64}, plus 64x128, 256x256, 256x128 for bf16x3; 0 =
+ * automatic) and split-K count (0 = automatic) forced, so every plan can be checked against a
+ * reference conv.  precision: 0 = fp32 MFMA, 1 = bf16x3 (hi/lo split, 3 bf16 MFMAs per
+ * product), 2 = bf16x3 with w_packed already split and packed (bf16 hi [Co][K] then lo
+ * [Co][K] in the library's K order, for timing the conv alone).  w_packed: device [Co][k][k][Ci]; scale/shift: device [Co]; res:
+ * NHWC (pixel stride res_ld) or NULL.
  */
 int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, int x_ld,
                    const float* w_packed, const float* scale, const float* shift, int Co, int k,

@@ -57,8 +57,10 @@ CASES = [  # N, Ci, Co, Hi, k, stride, dil, residual
     (2, 256, 256, 15, 3, 1, 2, True),
     (1, 512, 128, 13, 3, 1, 4, False),
     (3, 96, 64, 9, 1, 1, 1, True),
+    (1, 64, 512, 19, 3, 1, 1, True),
 ]
-PLANS = [(0, 0, 0), (128, 128, 1), (128, 64, 1), (64, 64, 1), (64, 128, 1), (64, 64, 3), (128, 128, 2)]
+PLANS = [(0, 0, 0), (128, 128, 1), (128, 64, 1), (64, 64, 1), (64, 128, 1), (64, 64, 3), (128, 128, 2),
+         (256, 256, 1), (256, 128, 1), (256, 256, 3)]
 # fp32 MFMA is exact-fp32 arithmetic; bf16x3 drops the lo*lo term (~2^-16 relative per product)
 TOLS = {0: 1e-5, 1: 1e-4}
 
@@ -71,10 +73,10 @@ def test_conv_plans(case, plan, precision):
         pytest.skip("no HIP device")
     N, Ci, Co, Hi, k, stride, dil, has_res = case
     bm, bn, ns = plan
-    if bn == 128 and Co % 128:
+    if bn and Co % bn:
         pytest.skip("Co not a multiple of the tile")
-    if (bm, bn) == (64, 128) and precision == 0:
-        pytest.skip("64x128 tile exists for bf16x3 only")
+    if ((bm, bn) == (64, 128) or bm == 256) and precision == 0:
+        pytest.skip("64x128 and 256-row tiles exist for bf16x3 only")
     tag = f"{N}_{Ci}_{Co}_{Hi}_{k}"
     x = torch.from_numpy(syn.normal(1, "x" + tag, (N, Ci, Hi, Hi), 1.0))
     w = torch.from_numpy(syn.normal(1, "w" + tag, (Co, Ci, k, k), (2.0 / (Ci * k * k)) ** 0.5))
