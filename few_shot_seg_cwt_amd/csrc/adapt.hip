@@ -28,8 +28,11 @@ struct AdaptScalars {
   float lr_eff;                 // lr / sum_p w_{y_p}
 };
 
+// int64 labels -> u8 (0, 1, 255 for anything else) plus per-block label counts (no atomics,
+// so nothing has to be zeroed first; adapt_setup_kernel sums the blocks in fixed order).
+constexpr int PREP_MAXBLK = 256;
 __global__ void adapt_prep_kernel(const int64_t* __restrict__ lbl, long total, uint8_t* __restrict__ out,
-                                  AdaptScalars* sc) {
+                                  unsigned long long* __restrict__ part /*[gridDim][2]*/) {
   unsigned long long nb = 0, nf = 0;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int64_t v = lbl[i];
@@ -37,7 +40,6 @@ __global__ void adapt_prep_kernel(const int64_t* __restrict__ lbl, long total, u
     nb += (v == 0);
     nf += (v == 1);
   }
-  // wave reduce, block reduce, then one pair of atomics per block
   __shared__ unsigned long long red[2][16];
   for (int o = 32; o > 0; o >>= 1) {
     nb += __shfl_xor(nb, o, 64);
@@ -54,21 +56,20 @@ __global__ void adapt_prep_kernel(const int64_t* __restrict__ lbl, long total, u
       b += red[0][i];
       f += red[1][i];
     }
-    atomicAdd(&sc->nbg, b);
-    atomicAdd(&sc->nfg, f);
+    part[2 * blockIdx.x] = b;
+    part[2 * blockIdx.x + 1] = f;
   }
 }
 
+// One block: label counts -> class weight and effective learning rate, the per-call pointers
+// of the captured step graph, and the zeroing of the first accumulator slot (or of the CE
+// loss numerator) -- one launch where there were two memsets and three kernels.
 // mode 0: weight = [1, nbg/nfg]        (test.py:169-175, train.py:211-217)
 // mode 1: weight = [1, nbg/(nfg+1e-12)] (train.py:237-243, query loss)
-__global__ void adapt_scalars_kernel(AdaptScalars* sc, float lr, int mode) {
-  double nb = (double)sc->nbg, nf = (double)sc->nfg;
-  double r = (mode == 0) ? nb / nf : nb / (nf + 1e-12);
-  float wfg = (float)r;  // torch.tensor([1.0, r]) -> float32
-  sc->wfg = wfg;
-  double sumw = nb + nf * (double)wfg;
-  sc->lr_eff = (float)((double)lr / sumw);
-}
+struct AdaptDevArgs;
+__global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, int nblk, AdaptScalars* sc, float lr,
+                                   int mode, AdaptDevArgs* dargs, const float* f, const float* w_in, float* w_out,
+                                   float* zero, int nzero, double* zero_d);
 
 constexpr int ADAPT_CB = 16;           // lo-res columns per workgroup
 // dW[1] accumulator replicas: ~240 workgroups adding 2 KB each into ONE 2 KB row run at the
@@ -88,10 +89,39 @@ struct AdaptDevArgs {
   float* w_out;       // adapted W [2][512]
 };
 
-__global__ void adapt_setargs_kernel(AdaptDevArgs* d, const float* f, const float* w_in, float* w_out) {
-  d->f = f;
-  d->w_in = w_in;
-  d->w_out = w_out;
+__global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, int nblk, AdaptScalars* sc, float lr,
+                                   int mode, AdaptDevArgs* dargs, const float* f, const float* w_in, float* w_out,
+                                   float* zero, int nzero, double* zero_d) {
+  __shared__ unsigned long long red[2][PREP_MAXBLK];
+  const int t = threadIdx.x;
+  red[0][t] = t < nblk ? part[2 * t] : 0ull;
+  red[1][t] = t < nblk ? part[2 * t + 1] : 0ull;
+  __syncthreads();
+  for (int o = PREP_MAXBLK / 2; o > 0; o >>= 1) {  // integer sums: order-independent
+    if (t < o) {
+      red[0][t] += red[0][t + o];
+      red[1][t] += red[1][t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const unsigned long long nbg = red[0][0], nfg = red[1][0];
+    sc->nbg = nbg;
+    sc->nfg = nfg;
+    const double nb = (double)nbg, nf = (double)nfg;
+    const double r = (mode == 0) ? nb / nf : nb / (nf + 1e-12);
+    const float wfg = (float)r;  // torch.tensor([1.0, r]) -> float32
+    sc->wfg = wfg;
+    const double sumw = nb + nf * (double)wfg;
+    sc->lr_eff = (float)((double)lr / sumw);
+    if (dargs) {
+      dargs->f = f;
+      dargs->w_in = w_in;
+      dargs->w_out = w_out;
+    }
+    if (zero_d) *zero_d = 0.0;
+  }
+  for (int i = t; i < nzero; i += blockDim.x) zero[i] = 0.f;
 }
 
 struct AdaptStepArgs {
@@ -412,16 +442,14 @@ int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int 
                  uint8_t* lbl_ws, AdaptScalars* sc, float* acc3 /*[3][R][512]*/, float* wbuf /*[2][2][512]*/,
                  AdaptDevArgs* dargs, AdaptGraphCache* cache, hipStream_t st) {
   const long total = (long)n * S * S;
-  CWT_HIP(hipMemsetAsync(sc, 0, sizeof(AdaptScalars), st));
-  int pblocks = (int)std::min<long>(256, cdiv(total, 1024));
-  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(1024), 0, st, lbl64, total, lbl_ws, sc);
+  unsigned long long* part = (unsigned long long*)(sc + 1);  // [PREP_MAXBLK][2] after the scalars
+  const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
+  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(1024), 0, st, lbl64, total, lbl_ws, part);
   CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(adapt_scalars_kernel, dim3(1), dim3(1), 0, st, sc, lr, 0);
+  hipLaunchKernelGGL(adapt_setup_kernel, dim3(1), dim3(PREP_MAXBLK), 0, st, (const unsigned long long*)part, pblocks,
+                     sc, lr, 0, dargs, f, (const float*)W, W, acc3, iters > 0 ? ADAPT_SLOT : 0, (double*)nullptr);
   CWT_LAUNCH_CHECK();
   if (iters <= 0) return 0;
-  hipLaunchKernelGGL(adapt_setargs_kernel, dim3(1), dim3(1), 0, st, dargs, f, (const float*)W, W);
-  CWT_LAUNCH_CHECK();
-  CWT_HIP(hipMemsetAsync(acc3, 0, sizeof(float) * ADAPT_SLOT, st));
   if (!cache) return enqueue_adapt_steps(dargs, lbl_ws, sc, acc3, wbuf, n, h, w, S, iters, st);
   // graph path: one instantiated graph per (geometry, workspace pointers)
   AdaptGraphCache::Entry key{n, h, w, S, iters, (const void*)lbl_ws, (const void*)sc, (const void*)acc3,
@@ -510,13 +538,13 @@ __global__ void seg_ce_final_kernel(const AdaptScalars* sc, const double* loss_n
 int launch_seg_ce(const float* logits, const int64_t* target, int B, int h, int w, int S, float* loss_out,
                   float* dlogits, uint8_t* lbl_ws, AdaptScalars* sc, double* loss_num, hipStream_t st) {
   const long total = (long)B * S * S;
-  CWT_HIP(hipMemsetAsync(sc, 0, sizeof(AdaptScalars), st));
-  CWT_HIP(hipMemsetAsync(loss_num, 0, sizeof(double), st));
-  CWT_HIP(hipMemsetAsync(dlogits, 0, sizeof(float) * (size_t)B * 2 * h * w, st));
-  int pblocks = (int)std::min<long>(256, cdiv(total, 1024));
-  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(1024), 0, st, target, total, lbl_ws, sc);
+  unsigned long long* part = (unsigned long long*)(sc + 1);
+  const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
+  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(1024), 0, st, target, total, lbl_ws, part);
   CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(adapt_scalars_kernel, dim3(1), dim3(1), 0, st, sc, 1.0f, 1);
+  hipLaunchKernelGGL(adapt_setup_kernel, dim3(1), dim3(PREP_MAXBLK), 0, st, (const unsigned long long*)part, pblocks,
+                     sc, 1.0f, 1, (AdaptDevArgs*)nullptr, (const float*)nullptr, (const float*)nullptr,
+                     (float*)nullptr, dlogits, B * 2 * h * w, loss_num);
   CWT_LAUNCH_CHECK();
   SegCEArgs a;
   a.logits = logits;

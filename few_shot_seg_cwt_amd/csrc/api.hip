@@ -420,7 +420,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   const long sT1 = std::max((long)N * H1 * H1 * 128, (long)N * h * h * 512);
   const long sT2 = std::max((long)N * H1 * H1 * 64, (long)N * h * h * 512);
   const long sD = std::max((long)N * H1 * H1 * 256, (long)N * h * h * 2048);
-  const long sCol = (long)N * h * 12 * 2048;
+  const long sCol = (long)N * h * 16 * 2048 + (long)N * 16 * 16 * 2048;  // PPM row-segment + block sums
   const long sPool = (long)N * 50 * 2048;
   const long sPpm = (long)N * 50 * 512;
   const long sQ = (long)N * 50 * 4608;
@@ -681,7 +681,7 @@ int cwt_inner_adapt(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int 
   int rc;
   if ((rc = ensure_ws(ctx, "adapt.args", 64, &dargs))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.lbl", (size_t)n * S * S, &lbl))) return rc;
-  if ((rc = ensure_ws(ctx, "adapt.sc", 64, &sc))) return rc;
+  if ((rc = ensure_ws(ctx, "adapt.sc", 8192, &sc))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.acc", 3 * 16 * 512 * 4, &acc))) return rc;  // [3][ADAPT_R][512]
   if ((rc = ensure_ws(ctx, "adapt.wbuf", 2 * 1024 * 4, &wb))) return rc;
   // algorithmic work: per step 2 x (2*2*C*h*w*n) FLOPs; minimal bytes = f_s + labels once per step
@@ -762,7 +762,7 @@ int cwt_seg_metrics(cwt_ctx* ctx, const float* logits, const int64_t* target, in
   CWT_HIP(hipSetDevice(ctx->device));
   void* cnt;
   int rc;
-  if ((rc = ensure_ws(ctx, "metrics.cnt", (size_t)B * 6 * 4, &cnt))) return rc;
+  if ((rc = ensure_ws(ctx, "metrics.cnt", (size_t)B * 256 * (6 * 4 + 2 * 8) + 16, &cnt))) return rc;
   return launch_seg_metrics(logits, target, B, h, w, S, iut_out, ce_out, (unsigned*)cnt, (hipStream_t)stream);
 }
 
@@ -775,7 +775,7 @@ int cwt_seg_ce_fwd_bwd(cwt_ctx* ctx, const float* logits, const int64_t* target,
   void *lbl, *sc, *num;
   int rc;
   if ((rc = ensure_ws(ctx, "ce.lbl", (size_t)B * S * S, &lbl))) return rc;
-  if ((rc = ensure_ws(ctx, "ce.sc", 64, &sc))) return rc;
+  if ((rc = ensure_ws(ctx, "ce.sc", 8192, &sc))) return rc;
   if ((rc = ensure_ws(ctx, "ce.num", 64, &num))) return rc;
   return launch_seg_ce(logits, target, B, h, w, S, loss_out, dlogits, (uint8_t*)lbl, (AdaptScalars*)sc,
                        (double*)num, (hipStream_t)stream);

@@ -6,6 +6,7 @@
 //  * the PPM branch of the bottleneck conv, folded: small-M GEMMs over the pooled cells and
 //    a separable interpolation of their per-tap products   (pspnet.py:19-38,124-128); the
 //    concat buffer of the reference (torch.cat) is never materialised
+#include <algorithm>
 #include <cstring>
 
 #include "common.h"
@@ -107,67 +108,105 @@ int launch_maxpool3s2(const float* in, int N, int H, int W, int C, float* out, i
   return 0;
 }
 
-// Adaptive-pool windows: start = floor(i*in/b), end = ceil((i+1)*in/b)
-// (aten adaptive_avg_pool2d start_index/end_index).
-struct PPMWindows {
+// Adaptive average pooling for all bins (pspnet.py:26), in three passes that each issue at
+// most ~14 independent loads per thread:
+//   segment boundaries = every window start / end along an axis (the windows of all bins
+//   are unions of consecutive "elementary segments");
+//   (1) rowseg[n][y][xs][c]  = sum of x[n][y][x][c] over x in x-segment xs
+//   (2) blk[n][ys][xs][c]    = sum of rowseg over y in y-segment ys
+//   (3) pooled[cell][c]      = ((sum of blk over the cell's segments) / kh) / kw
+// (The summation order differs from aten's window loop at fp32 rounding level.)
+struct PPMSegs {
+  int nseg;
+  int b[17];   // boundaries b[0] = 0 < ... < b[nseg] = in
+  int w0[16];  // window k covers segments [w0[k], w1[k])
+  int w1[16];
+  int wst[16], wen[16];
   int nwin;
-  int st[16], en[16];
 };
 
-static PPMWindows make_windows(int in, const int* bins, int nbins) {
-  PPMWindows wd;
-  wd.nwin = 0;
-  for (int b = 0; b < nbins; ++b)
-    for (int i = 0; i < bins[b]; ++i) {
-      wd.st[wd.nwin] = (i * in) / bins[b];
-      wd.en[wd.nwin] = ((i + 1) * in + bins[b] - 1) / bins[b];
-      ++wd.nwin;
+static PPMSegs make_segs(int in, const int* bins, int nbins) {
+  PPMSegs sg;
+  memset(&sg, 0, sizeof(sg));
+  int bnd[40], nb = 0;
+  for (int k = 0; k < nbins; ++k)
+    for (int i = 0; i < bins[k]; ++i) {
+      const int st = (i * in) / bins[k], en = ((i + 1) * in + bins[k] - 1) / bins[k];
+      sg.wst[sg.nwin] = st;
+      sg.wen[sg.nwin] = en;
+      ++sg.nwin;
+      bnd[nb++] = st;
+      bnd[nb++] = en;
     }
-  return wd;
+  std::sort(bnd, bnd + nb);
+  nb = (int)(std::unique(bnd, bnd + nb) - bnd);
+  sg.nseg = nb - 1;
+  for (int q = 0; q < nb; ++q) sg.b[q] = bnd[q];
+  for (int k = 0; k < sg.nwin; ++k) {
+    sg.w0[k] = (int)(std::lower_bound(bnd, bnd + nb, sg.wst[k]) - bnd);
+    sg.w1[k] = (int)(std::lower_bound(bnd, bnd + nb, sg.wen[k]) - bnd);
+  }
+  return sg;
 }
 
-// colsum[n][y][win][c] = sum_{x in window} x[n][y][x][c]; one thread per (n, y, c): four
-// threads per 16-B chunk keep ~4x the waves of a float4 mapping in flight (the sweep is
-// latency-bound), 8 loads outstanding per thread.
-__global__ void ppm_colsum_kernel(const float* __restrict__ cat, int N, int h, int w, int ld, int C,
-                                  PPMWindows wd, float* __restrict__ colsum) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * h * C;
+constexpr int PPM_MAXSEG = 16;  // longest elementary segment handled without a loop
+
+__global__ void ppm_rowseg_kernel(const float* __restrict__ x, int N, int h, int w, int ld, int C, PPMSegs sx,
+                                  float* __restrict__ rowseg) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)N * h * sx.nseg * C;
   if (idx >= total) return;
   const int c = (int)(idx % C);
-  const long ny = idx / C;  // n*h + y
-  float acc[16];
+  const long r = idx / C;
+  const int xs = (int)(r % sx.nseg);
+  const long ny = r / sx.nseg;
+  const int x0 = sx.b[xs], len = sx.b[xs + 1] - x0;
+  const float* src = x + (ny * w + x0) * (long)ld + c;
+  float s = 0.f;
+  for (int u0 = 0; u0 < len; u0 += PPM_MAXSEG) {
+    float v[PPM_MAXSEG];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  const float* row = cat + ny * w * (long)ld + c;
-  for (int x0 = 0; x0 < w; x0 += 8) {
-    float v[8];  // unconditional loads at clamped addresses: no branch joins between them
+    for (int u = 0; u < PPM_MAXSEG; ++u) v[u] = src[(long)min(u0 + u, len - 1) * ld];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = row[(long)min(x0 + u, w - 1) * ld];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int x = x0 + u;
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (i < wd.nwin && x >= wd.st[i] && x < wd.en[i]) acc[i] += v[u];
-    }
+    for (int u = 0; u < PPM_MAXSEG; ++u)
+      if (u0 + u < len) s += v[u];
   }
-  float* o = colsum + ny * (long)wd.nwin * C + c;
-#pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (i < wd.nwin) o[(long)i * C] = acc[i];
+  rowseg[idx] = s;
 }
 
-// pooled (bin-major, [sum_b N*b*b][C]) = ((sum over window rows of colsum) / kh) / kw;
-// one thread per (n, cell, c).
-__global__ void ppm_pool_kernel(const float* __restrict__ colsum, int N, int h, int C, PPMWindows wr,
-                                PPMWindows wc, int nbins, int b0, int b1, int b2, int b3,
-                                float* __restrict__ pooled) {
+__global__ void ppm_blk_kernel(const float* __restrict__ rowseg, int N, int h, int C, PPMSegs sx, PPMSegs sy,
+                               float* __restrict__ blk) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)N * sy.nseg * sx.nseg * C;
+  if (idx >= total) return;
+  const int c = (int)(idx % C);
+  long r = idx / C;
+  const int xs = (int)(r % sx.nseg);
+  r /= sx.nseg;
+  const int ys = (int)(r % sy.nseg);
+  const int n = (int)(r / sy.nseg);
+  const int y0 = sy.b[ys], len = sy.b[ys + 1] - y0;
+  const long rstride = (long)sx.nseg * C;
+  const float* src = rowseg + (((long)n * h + y0) * sx.nseg + xs) * C + c;
+  float s = 0.f;
+  for (int u0 = 0; u0 < len; u0 += PPM_MAXSEG) {
+    float v[PPM_MAXSEG];
+#pragma unroll
+    for (int u = 0; u < PPM_MAXSEG; ++u) v[u] = src[min(u0 + u, len - 1) * rstride];
+#pragma unroll
+    for (int u = 0; u < PPM_MAXSEG; ++u)
+      if (u0 + u < len) s += v[u];
+  }
+  blk[idx] = s;
+}
+
+// pooled (bin-major, [sum_b N*b*b][C]); one thread per (n, cell, c)
+__global__ void ppm_cell_kernel(const float* __restrict__ blk, int N, int C, PPMSegs sx, PPMSegs sy, int b0, int b1,
+                                int b2, int b3, float* __restrict__ pooled) {
   const int bins[4] = {b0, b1, b2, b3};
-  int ncells = 0;
-  for (int k = 0; k < nbins; ++k) ncells += bins[k] * bins[k];
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * ncells * C;
+  const int ncells = b0 * b0 + b1 * b1 + b2 * b2 + b3 * b3;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)N * ncells * C;
   if (idx >= total) return;
   const int c = (int)(idx % C);
   const int cell = (int)((idx / C) % ncells);
@@ -180,40 +219,43 @@ __global__ void ppm_pool_kernel(const float* __restrict__ colsum, int N, int h, 
   }
   const int b = bins[k];
   const int i = (cell - base) / b, j = (cell - base) % b;
-  const int wrow = woff + i, wcol = woff + j;
-  const int ys = wr.st[wrow], ye = wr.en[wrow];
-  const int xs = wc.st[wcol], xe = wc.en[wcol];
-  const float* src = colsum + ((long)n * h * wc.nwin + wcol) * C + c;
-  const long ystride = (long)wc.nwin * C;
+  const int ya = sy.w0[woff + i], yb = sy.w1[woff + i];
+  const int xa = sx.w0[woff + j], xb = sx.w1[woff + j];
   float s = 0.f;
-  for (int y0 = ys; y0 < ye; y0 += 8) {
-    float v[8];  // unconditional loads at clamped addresses
+  for (int ys = ya; ys < yb; ++ys) {
+    float v[PPM_MAXSEG];
+    const float* src = blk + (((long)n * sy.nseg + ys) * sx.nseg) * C + c;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = src[min(y0 + u, ye - 1) * ystride];
+    for (int u = 0; u < PPM_MAXSEG; ++u) v[u] = src[(long)min(xa + u, xb - 1) * C];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (y0 + u < ye) s += v[u];
+    for (int u = 0; u < PPM_MAXSEG; ++u)
+      if (xa + u < xb) s += v[u];
   }
-  const float kh = (float)(ye - ys), kw = (float)(xe - xs);
-  const long out_row = (long)base * N + (long)n * b * b + i * b + j;
-  pooled[out_row * C + c] = (s / kh) / kw;
+  const float kh = (float)(sy.wen[woff + i] - sy.wst[woff + i]), kw = (float)(sx.wen[woff + j] - sx.wst[woff + j]);
+  pooled[((long)base * N + (long)n * b * b + i * b + j) * C + c] = (s / kh) / kw;
 }
 
-int launch_ppm(const float* cat, int N, int h, int w, int ld, const int* bins, int nbins, float* colsum,
+// ws: rowseg [N][h][nseg_x][C] followed by blk [N][nseg_y][nseg_x][C]
+int launch_ppm(const float* x, int N, int h, int w, int ld, const int* bins, int nbins, float* ws,
                float* pooled, hipStream_t st) {
   if (nbins != 4) return fail(CWT_EARG, "PPM expects 4 bins");
-  PPMWindows wc = make_windows(w, bins, nbins);
-  PPMWindows wr = make_windows(h, bins, nbins);
-  if (wc.nwin > 16) return fail(CWT_EARG, "PPM: too many windows");
+  const PPMSegs sx = make_segs(w, bins, nbins), sy = make_segs(h, bins, nbins);
+  if (sx.nwin > 16 || sx.nseg > 16 || sy.nseg > 16) return fail(CWT_EARG, "PPM: too many windows");
   const int C = 2048;
-  int ncells = 0;
-  for (int b = 0; b < nbins; ++b) ncells += bins[b] * bins[b];
-  long t1 = (long)N * h * C;
-  hipLaunchKernelGGL(ppm_colsum_kernel, dim3(cdiv(t1, 256)), dim3(256), 0, st, cat, N, h, w, ld, C, wc, colsum);
+  float* rowseg = ws;
+  float* blk = ws + (long)N * h * sx.nseg * C;
+  const long t1 = (long)N * h * sx.nseg * C;
+  hipLaunchKernelGGL(ppm_rowseg_kernel, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx, rowseg);
   CWT_LAUNCH_CHECK();
-  long t2 = (long)N * ncells * C;
-  hipLaunchKernelGGL(ppm_pool_kernel, dim3(cdiv(t2, 256)), dim3(256), 0, st, colsum, N, h, C, wr, wc, nbins,
-                     bins[0], bins[1], bins[2], bins[3], pooled);
+  const long t2 = (long)N * sy.nseg * sx.nseg * C;
+  hipLaunchKernelGGL(ppm_blk_kernel, dim3(cdiv(t2, 256)), dim3(256), 0, st, (const float*)rowseg, N, h, C, sx, sy,
+                     blk);
+  CWT_LAUNCH_CHECK();
+  int ncells = 0;
+  for (int k = 0; k < nbins; ++k) ncells += bins[k] * bins[k];
+  const long t3 = (long)N * ncells * C;
+  hipLaunchKernelGGL(ppm_cell_kernel, dim3(cdiv(t3, 256)), dim3(256), 0, st, (const float*)blk, N, C, sx, sy, bins[0],
+                     bins[1], bins[2], bins[3], pooled);
   CWT_LAUNCH_CHECK();
   return 0;
 }

@@ -239,11 +239,28 @@ static void launch_tiles_x3(const ConvArgs& a, const ConvPlan& p, dim3 grid, hip
     hipLaunchKernelGGL((conv_igemm_bf16x3<64, 64, 2, 2, STAGE>), grid, dim3(256), 0, st, a);
 }
 
-// Largest tile that still yields >= kMinWG workgroups, splitting K (powers of two, at
+struct MeasuredPlan {
+  int M, Co, K, bm, bn, nsplit;
+};
+static const MeasuredPlan kMeasuredPlans[] = {
+#include "conv_plans.inc"
+};
+
+// The measured plan for this GEMM shape if the sweep found one (conv_plans.inc), else the
+// largest tile that still yields >= kMinWG workgroups, splitting K (powers of two, at
 // least 8 k-tiles of 32 per split) where the output alone is too small a grid.
 ConvPlan plan_conv_x3(int M, int Co, int K) {
   constexpr long kMinWG = 200;
   const int ktiles = K / 32;
+  for (const MeasuredPlan& e : kMeasuredPlans)
+    if (e.M == M && e.Co == Co && e.K == K && Co % e.bn == 0) {
+      ConvPlan p;
+      p.bm = e.bm;
+      p.bn = e.bn;
+      p.kt_per_split = cdiv(ktiles, e.nsplit);
+      p.nsplit = cdiv(ktiles, p.kt_per_split);
+      return p;
+    }
   static const int cand[6][2] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
   ConvPlan best;  // if no tile reaches kMinWG: the smallest one that divides Co, most splits
   for (auto& c : cand) {

@@ -117,8 +117,8 @@ int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const
                       const float* shift, float* out, int Ho, hipStream_t st);
 int launch_maxpool3s2(const float* in, int N, int H, int W, int C, float* out, int Ho, int Wo,
                       hipStream_t st);
-int launch_ppm(const float* cat, int N, int h, int w, int ld, const int* bins, int nbins,
-               float* colsum, float* pooled, hipStream_t st);
+int launch_ppm(const float* x, int N, int h, int w, int ld, const int* bins, int nbins, float* ws,
+               float* pooled, hipStream_t st);
 int launch_repack_cblock(const float* src, float* dst, int Co, int taps, int Ci, hipStream_t st);
 int launch_smallm_gemm(const float* A, int lda, const float* const* Bt, const int* M, int np, int N, int K, int kc,
                        float* part, size_t part_floats, const float* const* scale, const float* const* shift,

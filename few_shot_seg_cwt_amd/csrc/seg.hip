@@ -184,31 +184,60 @@ __global__ __launch_bounds__(256) void seg_metrics_kernel(const float* __restric
     cel[wv][1] = (double)nvalid;
   }
   __syncthreads();
-  if (t < 6) atomicAdd(&counts[b * 6 + t], cnt[0][t] + cnt[1][t] + cnt[2][t] + cnt[3][t]);
-  if (ce && t < 2) atomicAdd(&ce[b * 2 + t], (cel[0][t] + cel[1][t]) + (cel[2][t] + cel[3][t]));
+  // per-block partials (no atomics, nothing to zero first); seg_metrics_final sums them in
+  // block order, so the double CE sum is deterministic
+  const long pb = (long)b * gridDim.x + blockIdx.x;
+  if (t < 6) counts[pb * 6 + t] = cnt[0][t] + cnt[1][t] + cnt[2][t] + cnt[3][t];
+  if (ce && t < 2) ce[pb * 2 + t] = (cel[0][t] + cel[1][t]) + (cel[2][t] + cel[3][t]);
 }
 
-__global__ void seg_metrics_final_kernel(const unsigned* counts, int B, float* iut) {
-  const int b = threadIdx.x;
-  if (b >= B) return;
-  const unsigned* c = counts + b * 6;
-  for (int k = 0; k < 2; ++k) {
-    iut[b * 6 + k] = (float)c[k];                       // intersection
-    iut[b * 6 + 2 + k] = (float)(c[2 + k] + c[4 + k] - c[k]);  // union = output + target - intersection
-    iut[b * 6 + 4 + k] = (float)c[4 + k];               // target
+// one 256-thread block per batch item: thread k takes block k's partials, then a fixed-shape
+// LDS tree (deterministic) gives [inter, union, target] x 2 classes and (nll sum, valid count)
+__global__ __launch_bounds__(256) void seg_metrics_final_kernel(const unsigned* __restrict__ counts,
+                                                                const double* __restrict__ ce_part, int nblk,
+                                                                float* __restrict__ iut, double* __restrict__ ce) {
+  __shared__ unsigned c[6][256];
+  __shared__ double d[2][256];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const bool have = t < nblk;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) c[q][t] = have ? counts[((long)b * nblk + t) * 6 + q] : 0u;
+  if (ce) {
+    d[0][t] = have ? ce_part[((long)b * nblk + t) * 2] : 0.0;
+    d[1][t] = have ? ce_part[((long)b * nblk + t) * 2 + 1] : 0.0;
+  }
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q) c[q][t] += c[q][t + o];
+      if (ce) {
+        d[0][t] += d[0][t + o];
+        d[1][t] += d[1][t + o];
+      }
+    }
+    __syncthreads();
+  }
+  if (t < 2) {
+    iut[b * 6 + t] = (float)c[t][0];                                 // intersection
+    iut[b * 6 + 2 + t] = (float)(c[2 + t][0] + c[4 + t][0] - c[t][0]);  // union = output + target - intersection
+    iut[b * 6 + 4 + t] = (float)c[4 + t][0];                         // target
+    if (ce) ce[b * 2 + t] = d[t][0];
   }
 }
 
+// counts_ws: [B][nblk][6] unsigned, then (8-B aligned) [B][nblk][2] double partials
 int launch_seg_metrics(const float* logits, const int64_t* target, int B, int h, int w, int S, float* iut,
                        double* ce, unsigned* counts_ws, hipStream_t st) {
-  CWT_HIP(hipMemsetAsync(counts_ws, 0, sizeof(unsigned) * 6 * B, st));
-  if (ce) CWT_HIP(hipMemsetAsync(ce, 0, sizeof(double) * 2 * B, st));
   const long npix = (long)S * S;
-  dim3 grid((unsigned)std::min<long>(256, cdiv(npix, 256)), B);
+  const int nblk = (int)std::min<long>(256, cdiv(npix, 256));
+  double* ce_part = ce ? (double*)(counts_ws + (((long)B * nblk * 6 + 1) & ~1L)) : nullptr;
+  dim3 grid(nblk, B);
   hipLaunchKernelGGL(seg_metrics_kernel, grid, dim3(256), 0, st, logits, target, h, w, S,
-                     align_corners_scale(h, S), align_corners_scale(w, S), counts_ws, ce);
+                     align_corners_scale(h, S), align_corners_scale(w, S), counts_ws, ce_part);
   CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(seg_metrics_final_kernel, dim3(1), dim3(64), 0, st, (const unsigned*)counts_ws, B, iut);
+  hipLaunchKernelGGL(seg_metrics_final_kernel, dim3(B), dim3(256), 0, st, (const unsigned*)counts_ws,
+                     (const double*)ce_part, nblk, iut, ce);
   CWT_LAUNCH_CHECK();
   return 0;
 }
