@@ -56,6 +56,24 @@ def cpu_baseline(cfg, sd, tsd, budget_s: float = 25.0, max_eps: int = 4):
                       f"run_inference_episode (torch CPU fp32, {threads} threads); s/episode {dt / n:.2f}"}
 
 
+def pmc_traffic(dom_name: str):
+    """HBM-side bytes per launch of the dominant kernel from the newest committed PMC summary
+    (profiles/r*/pmc_summary.json, made by tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x 2 +
+    WRITE_SIZE, gfx950-corrected).  None if no summary covers this kernel."""
+    import glob
+    import re
+    mt = re.match(r"conv_igemm_(\w+)<(\d+),(\d+),(\d+)>", dom_name)
+    if not mt:
+        return None, None
+    kind, bm, bn, stage = mt.group(1), mt.group(2), mt.group(3), mt.group(4)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), reverse=True):
+        for k, e in json.load(open(path)).items():
+            if f"conv_igemm_{kind}<{bm}, {bn}, " in k and k.split(">(")[0].endswith(f", {stage}") \
+                    and "traffic_bytes" in e:
+                return int(e["traffic_bytes"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -143,6 +161,8 @@ def main():
     else:
         peak, peak_basis = PEAK_FP32_MFMA_TFLOPS, "fp32 MFMA 157.3 TF"
 
+    traffic, traffic_src = pmc_traffic(dom_name)
+
     # per-launch table from one extra (untimed) episode at profile level 2
     _lib.profile_enable(2)
     step(0, W0[0].clone())
@@ -171,7 +191,8 @@ def main():
                    "parallelism": f"{world} episode-sharded replicas"},
         "roofline": {"bound": "mfma", "kernel": dom_name + " (bottleneck conv 4096->512 3x3, pspnet.py:125)",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "traffic_source": traffic_src,
                      "peak_basis": peak_basis, "launches_per_step": dn // args.steps,
                      "flops_per_launch": dfl / dn, "avg_launch_ms": round(dms / dn, 4)},
         "conv_stack": {"tflops": round(ex_fl / (ex_ms * 1e-3) / 1e12, 2),

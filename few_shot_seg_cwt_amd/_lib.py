@@ -42,6 +42,9 @@ SIGNATURES = {
     "cwt_classify_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_iou_preds": (_I, [_P, _P, _P, _I64, _I, _I, _P, _P]),
     "cwt_sgd_step": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _I, _I, _P]),
+    "cwt_cu_count": (_I, [_P, _P]),
+    "cwt_stream_create_masked": (_I, [_P, _P, _I, _P]),
+    "cwt_stream_destroy": (_I, [_P]),
     "cwt_debug_conv": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I,
                             _I, _I, _I, _I, _P]),
     "cwt_profile_enable": (_I, [_P, _I]),
@@ -137,3 +140,43 @@ def profile_records(device=None):
         check(lib().cwt_profile_record(c, i, buf, 256, C.byref(fl), C.byref(by), C.byref(ms)), "cwt_profile_record")
         out.append((buf.value.decode(), fl.value, by.value, ms.value))
     return out
+
+
+def cu_count(device: int | None = None) -> int:
+    """Number of compute units of the device (cwt_cu_count)."""
+    import ctypes
+    n = ctypes.c_int(0)
+    check(lib().cwt_cu_count(ctx(device), ctypes.byref(n)), "cwt_cu_count")
+    return n.value
+
+
+class MaskedStream:
+    """A HIP stream restricted to a set of CUs (cwt_stream_create_masked), usable as a torch
+    stream through ``.torch`` (torch.cuda.ExternalStream).  Destroyed with the object."""
+
+    def __init__(self, cus, device: int | None = None):
+        import ctypes
+        import torch
+        self.device = torch.cuda.current_device() if device is None else device
+        ncu = cu_count(self.device)
+        words = (ncu + 31) // 32
+        mask = (ctypes.c_uint32 * words)()
+        self.cus = sorted(set(int(c) for c in cus))
+        if not self.cus or self.cus[0] < 0 or self.cus[-1] >= ncu:
+            raise ValueError(f"CU ids must lie in [0, {ncu})")
+        for c in self.cus:
+            mask[c // 32] |= 1 << (c % 32)
+        ptr = ctypes.c_void_p()
+        check(lib().cwt_stream_create_masked(ctx(self.device), mask, words, ctypes.byref(ptr)),
+              "cwt_stream_create_masked")
+        self.ptr = ptr.value
+        self.torch = torch.cuda.ExternalStream(self.ptr, device=torch.device("cuda", self.device))
+
+    def __del__(self):
+        p = getattr(self, "ptr", None)
+        if p:
+            try:
+                lib().cwt_stream_destroy(p)
+            except Exception:
+                pass
+            self.ptr = None

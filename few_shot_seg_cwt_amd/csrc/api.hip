@@ -881,6 +881,29 @@ int cwt_profile_record(cwt_ctx* ctx, int i, char* name, int name_len, double* fl
   return 0;
 }
 
+int cwt_cu_count(cwt_ctx* ctx, int* count) {
+  if (!ctx || !count) return fail(CWT_EARG, "null argument");
+  hipDeviceProp_t prop;
+  CWT_HIP(hipGetDeviceProperties(&prop, ctx->device));
+  *count = prop.multiProcessorCount;
+  return 0;
+}
+
+int cwt_stream_create_masked(cwt_ctx* ctx, const uint32_t* mask, int mask_words, void** stream) {
+  if (!ctx || !mask || !stream || mask_words < 1) return fail(CWT_EARG, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t s;
+  CWT_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask_words, mask));
+  *stream = (void*)s;
+  return 0;
+}
+
+int cwt_stream_destroy(void* stream) {
+  if (!stream) return fail(CWT_EARG, "stream is NULL");
+  CWT_HIP(hipStreamDestroy((hipStream_t)stream));
+  return 0;
+}
+
 int cwt_sgd_step(cwt_ctx* ctx, float* param, const float* grad, float* momentum_buf, int64_t n, float lr,
                  float momentum, float weight_decay, int nesterov, int first_step, void* stream) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");

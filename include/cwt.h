@@ -199,6 +199,17 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
                    int stride, int pad, int dil, const float* res, int res_ld, int relu, float* y,
                    int y_ld, int y_off, int bm, int bn, int nsplit, int precision, void* stream);
 
+/*
+ * CU-partitioned streams (MI355X-native episode pipelining): a HIP stream
+ * whose kernels (including replays of graphs launched on it) only run on the CUs whose bits
+ * are set in mask (mask_words 32-bit words, bit i = CU i of the device).  Used to run one
+ * episode's latency-bound inner loop on a small partition while the next episode's conv
+ * stack runs on the rest.  cwt_cu_count returns the device's CU count.
+ */
+int cwt_cu_count(cwt_ctx* ctx, int* count);
+int cwt_stream_create_masked(cwt_ctx* ctx, const uint32_t* mask, int mask_words, void** stream);
+int cwt_stream_destroy(void* stream);
+
 int cwt_profile_enable(cwt_ctx* ctx, int level);
 int cwt_profile_count(cwt_ctx* ctx);
 int cwt_profile_record(cwt_ctx* ctx, int i, char* name, int name_len, double* flops, double* bytes,
