@@ -154,7 +154,7 @@ def main():
     dom = [r for r in recs if r[0].startswith("conv_igemm")]     # the bottleneck conv (level 1 records only it)
     dom_name = dom[0][0].split(" ")[0] if dom else "n/a"
     dn, dfl, dms = len(dom), sum(r[1] for r in dom), sum(r[3] for r in dom)
-    conv_x3 = dom_name.startswith("conv_igemm_bf16x3")
+    conv_x3 = dom_name.startswith("conv_igemm_bf16x3") or dom_name.startswith("conv_igemm_x3s")
     achieved = (dfl / dn) / (dms / dn * 1e-3) / 1e12
     if conv_x3:   # fp32 GEMM done as 3 bf16 MFMA products: the roof is the dense bf16 rate / 3
         peak, peak_basis = round(PEAK_BF16_MFMA_TFLOPS / 3, 1), "bf16x3: 2516.6 TF dense bf16 MFMA / 3 products"

@@ -58,6 +58,7 @@ struct ConvLayer {
   float* w = nullptr;  // device, packed [Co][k][k][Ci] (stem conv1: [ci][ky][kx][co])
   __bf16* w_hi = nullptr;  // bf16x3 split of w (same layout); null for the stem conv1
   __bf16* w_lo = nullptr;
+  __bf16* w_s = nullptr;   // S-layout [Co][K/32][hi 32 | lo 32] of the same split (conv_x3s.hip)
   float* scale = nullptr;
   float* shift = nullptr;
 };
@@ -104,8 +105,10 @@ struct cwt_ctx {
   // inner loop: captured graphs of the step sequence (disable with CWT_ADAPT_GRAPH=0)
   cwt::AdaptGraphCache adapt_graphs;
   bool use_graph = true;
-  // conv arithmetic: bf16x3 on the bf16 matrix cores (default) or exact fp32 MFMA (CWT_CONV=f32)
+  // conv arithmetic: bf16x3 on the bf16 matrix cores over S-layout activations (default,
+  // CWT_CONV=x3s), bf16x3 over fp32 activations (CWT_CONV=x3) or exact fp32 MFMA (CWT_CONV=f32)
   bool conv_x3 = true;
+  bool conv_split = true;
 };
 
 namespace cwt {
@@ -153,6 +156,17 @@ static int ensure_ws(cwt_ctx* ctx, const std::string& name, size_t bytes, void**
     ctx->ws_total += nb;
   }
   *out = b.p;
+  return 0;
+}
+
+// 256 B of zeros on the device (the LDS-DMA source of zero-padding taps in conv_x3s)
+static int zero_line(cwt_ctx* ctx, const __bf16** out) {
+  const bool fresh = ctx->ws.find("zero") == ctx->ws.end();
+  void* p;
+  int rc;
+  if ((rc = ensure_ws(ctx, "zero", 256, &p))) return rc;
+  if (fresh) CWT_HIP(hipMemset(p, 0, 256));
+  *out = (const __bf16*)p;
   return 0;
 }
 
@@ -255,6 +269,15 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
       lo[i] = bf16_rne(v - bf16_to_float(hi[i]));
     }
     if ((rc = upload_u16(bb, hi, &L->w_hi)) || (rc = upload_u16(bb, lo, &L->w_lo))) return rc;
+    std::vector<uint16_t> sl(2 * packed.size());
+    for (size_t r = 0; r < (size_t)Co; ++r)
+      for (int kb = 0; kb < K / 32; ++kb)
+        for (int i = 0; i < 32; ++i) {
+          const size_t src = r * K + kb * 32 + i, dst = (r * (K / 32) + kb) * 64 + i;
+          sl[dst] = hi[src];
+          sl[dst + 32] = lo[src];
+        }
+    if ((rc = upload_u16(bb, sl, &L->w_s))) return rc;
   }
   if ((rc = upload(bb, sc, &L->scale))) return rc;
   if ((rc = upload(bb, sh, &L->shift))) return rc;
@@ -377,6 +400,7 @@ struct ConvCall {
   const float* res;
   int res_ld;
   int relu;
+  bool out_f32;  // S-layout mode: this call writes fp32 (and takes an fp32 residual)
 };
 
 static ConvArgs make_args(const ConvCall& c) {
@@ -462,7 +486,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   int stage = 0;
   auto cc = [&](const ConvLayer* L, const float* x, int n, int Hi, int Wi, int x_ld, float* y, int y_ld, int y_off,
                 const float* res, int res_ld, int relu) {
-    ConvCall c{stage, L, x, n, Hi, Wi, x_ld, y, y_ld, y_off, res, res_ld, relu};
+    ConvCall c{stage, L, x, n, Hi, Wi, x_ld, y, y_ld, y_off, res, res_ld, relu, stage == 6};
     calls.push_back(c);
   };
   // stem conv2/conv3 (conv1 and maxpool are separate kernels, ordered below by index)
@@ -504,10 +528,14 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   std::vector<ConvPlan> plans;
   for (auto& c : calls) {
     ConvArgs a = make_args(c);
-    ConvPlan pl = ctx->conv_x3 ? plan_conv_x3(a.M, a.Co, a.K) : plan_conv(a.M, a.Co, a.K);
+    ConvPlan pl = ctx->conv_split ? plan_conv_x3s(a.M, a.Co, a.K)
+                  : ctx->conv_x3  ? plan_conv_x3(a.M, a.Co, a.K)
+                                  : plan_conv(a.M, a.Co, a.K);
     plans.push_back(pl);
     if (pl.nsplit > 1) part_floats = std::max(part_floats, (size_t)pl.nsplit * a.M * a.Co);
   }
+  const __bf16* zero = nullptr;
+  if (ctx->conv_split && (rc = zero_line(ctx, &zero))) return rc;
   float* PART = nullptr;
   if (part_floats) {
     if ((rc = ensure_ws(ctx, "bb.PART", part_floats * 4, &p))) return rc;
@@ -520,15 +548,54 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     const double bytes = 4.0 * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K + (double)a.M * a.Co +
                                 (a.res ? (double)a.M * a.Co : 0.0));
     Prof p(ctx, st,
-           std::string(ctx->conv_x3 ? "conv_igemm_bf16x3<" : "conv_igemm_f32<") + std::to_string(pl.bm) + "," +
+           std::string(ctx->conv_split ? "conv_igemm_x3s<" : ctx->conv_x3 ? "conv_igemm_bf16x3<" : "conv_igemm_f32<") +
+               std::to_string(pl.bm) + "," +
                std::to_string(pl.bn) + "," +
                std::to_string(calls[i].stage) + ">" +
                (pl.nsplit > 1 ? "+splitk" + std::to_string(pl.nsplit) : std::string()) + " " +
                std::to_string(a.Ci) + "x" + std::to_string(a.Co) + "k" + std::to_string(a.kh) + "s" +
                std::to_string(a.stride) + "d" + std::to_string(a.dil) + "@" + std::to_string(a.Ho),
            flops, bytes, calls[i].stage == 6 ? 1 : 2);
-    int r = ctx->conv_x3 ? launch_conv_x3(a, pl, calls[i].stage, PART, part_floats, st)
-                         : launch_conv(a, pl, calls[i].stage, PART, part_floats, st);
+    int r;
+    if (ctx->conv_split) {
+      ConvSArgs sa;
+      memset(&sa, 0, sizeof(sa));
+      const ConvCall& c = calls[i];
+      sa.xs = (const __bf16*)c.x;
+      sa.ws = c.L->w_s;
+      sa.zero = zero;
+      sa.scale = a.scale;
+      sa.shift = a.shift;
+      if (c.out_f32) {
+        sa.y = c.y;
+        sa.y_ld = c.y_ld;
+        sa.y_off = c.y_off;
+        sa.res = c.res;
+        sa.res_ld = c.res_ld;
+      } else {
+        sa.ys = (__bf16*)c.y;
+        sa.res_s = (const __bf16*)c.res;
+      }
+      sa.relu = c.relu;
+      sa.N = a.N;
+      sa.Hi = a.Hi;
+      sa.Wi = a.Wi;
+      sa.Ci = a.Ci;
+      sa.Ho = a.Ho;
+      sa.Wo = a.Wo;
+      sa.Co = a.Co;
+      sa.kh = a.kh;
+      sa.kw = a.kw;
+      sa.stride = a.stride;
+      sa.pad = a.pad;
+      sa.dil = a.dil;
+      sa.M = a.M;
+      sa.K = a.K;
+      r = launch_conv_x3s(sa, pl, c.stage, PART, part_floats, st);
+    } else {
+      r = ctx->conv_x3 ? launch_conv_x3(a, pl, calls[i].stage, PART, part_floats, st)
+                       : launch_conv(a, pl, calls[i].stage, PART, part_floats, st);
+    }
     p.end();
     return r;
   };
@@ -545,21 +612,25 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   Prof whole(ctx, st, "extract_features N=" + std::to_string(N) + " S=" + std::to_string(S), all_flops, all_bytes, 1);
   {
     Prof p(ctx, st, "stem_conv1 3x64k3s2", 2.0 * N * Hs * Hs * 64 * 27, 4.0 * ((double)N * 3 * S * S + (double)N * Hs * Hs * 64));
-    if ((rc = launch_stem_conv1(img, N, S, bb->stem[0].w, bb->stem[0].scale, bb->stem[0].shift, A, Hs, st))) return rc;
+    if ((rc = launch_stem_conv1(img, N, S, bb->stem[0].w, bb->stem[0].scale, bb->stem[0].shift, A, Hs, st,
+                                ctx->conv_split)))
+      return rc;
     p.end();
   }
   for (size_t i = 0; i < n_stem_calls; ++i)
     if ((rc = run_call(i))) return rc;
   {
     Prof p(ctx, st, "maxpool3s2", 0.0, 4.0 * ((double)N * Hs * Hs * 128 + (double)N * H1 * H1 * 128));
-    if ((rc = launch_maxpool3s2(A, N, Hs, Hs, 128, B, H1, H1, st))) return rc;
+    if ((rc = ctx->conv_split ? launch_maxpool3s2_s((const __bf16*)A, N, Hs, Hs, 128, (__bf16*)B, H1, H1, st)
+                              : launch_maxpool3s2(A, N, Hs, Hs, 128, B, H1, H1, st)))
+      return rc;
     p.end();
   }
   for (size_t i = n_stem_calls; i < n_backbone_calls; ++i)
     if ((rc = run_call(i))) return rc;
   {
     Prof p(ctx, st, "ppm_pool", 0.0, 4.0 * ((double)N * h * h * 2048 + (double)N * 50 * 2048));
-    if ((rc = launch_ppm(L4, N, h, h, 2048, kBins, 4, COL, POOL, st))) return rc;
+    if ((rc = launch_ppm(L4, N, h, h, 2048, kBins, 4, COL, POOL, st, ctx->conv_split))) return rc;
     p.end();
   }
   int Mb[4];
@@ -616,7 +687,9 @@ int cwt_ctx_create(int device, cwt_ctx** out) {
   const char* g = getenv("CWT_ADAPT_GRAPH");
   c->use_graph = !(g && g[0] == '0');
   const char* cv = getenv("CWT_CONV");
-  c->conv_x3 = !(cv && std::string(cv) == "f32");
+  const std::string mode = cv ? std::string(cv) : std::string("x3s");
+  c->conv_x3 = mode != "f32";
+  c->conv_split = mode == "x3s";
   *out = c;
   return 0;
 }
@@ -807,7 +880,7 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
   }
   L.scale = (float*)scale;
   L.shift = (float*)shift;
-  ConvCall c{0, &L, x, N, Hi, Wi, x_ld, y, y_ld, y_off, res, res_ld, relu};
+  ConvCall c{0, &L, x, N, Hi, Wi, x_ld, y, y_ld, y_off, res, res_ld, relu, true};
   ConvArgs a = make_args(c);
   const bool x3 = precision == 1 || precision == 2;
   ConvPlan p = x3 ? plan_conv_x3(a.M, a.Co, a.K) : plan_conv(a.M, a.Co, a.K);
@@ -840,6 +913,90 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
   a.w_hi = (const __bf16*)hi;
   a.w_lo = (const __bf16*)lo;
   return launch_conv_x3(a, p, 0, (float*)part, pf, (hipStream_t)stream);
+}
+
+int cwt_debug_split_act(cwt_ctx* ctx, const float* x, int64_t P, int C, int ld, void* out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && out && P >= 0 && C % 32 == 0 && ld >= C && ld % 4 == 0, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_split_act(x, P, C, ld, (__bf16*)out, (hipStream_t)stream);
+}
+
+int cwt_debug_unsplit_act(cwt_ctx* ctx, const void* s, int64_t P, int C, float* out, int ld, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(s && out && P >= 0 && C % 32 == 0 && ld >= C && ld % 4 == 0, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_unsplit_act((const __bf16*)s, P, C, out, ld, (hipStream_t)stream);
+}
+
+int cwt_debug_pack_wsplit(cwt_ctx* ctx, const float* w, int Co, int k, int Ci, void* out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(w && out && Co > 0 && Ci % 32 == 0 && (k == 1 || k == 3), "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void* wp;
+  int rc;
+  const long K = (long)k * k * Ci;
+  if ((rc = ensure_ws(ctx, "dbg.wpack", (size_t)Co * K * 4, &wp))) return rc;
+  if ((rc = launch_repack_cblock(w, (float*)wp, Co, k * k, Ci, (hipStream_t)stream))) return rc;
+  return launch_split_act((const float*)wp, Co, (int)K, (int)K, (__bf16*)out, (hipStream_t)stream);
+}
+
+int cwt_debug_conv_s(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws, const float* scale,
+                     const float* shift, int Co, int k, int stride, int pad, int dil, const float* res, int res_ld,
+                     const void* res_s, int relu, float* y, int y_ld, int y_off, void* ys, int bm, int bn, int nsplit,
+                     void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(xs && ws && scale && shift && (y || ys), "null buffer");
+  CWT_CHECK(Ci % 32 == 0 && Co % 64 == 0, "need Ci%32==0, Co%64==0");
+  CWT_CHECK(!y || (y_ld >= y_off + Co && y_ld % 4 == 0 && y_off % 4 == 0), "bad y stride");
+  CWT_HIP(hipSetDevice(ctx->device));
+  ConvSArgs a;
+  memset(&a, 0, sizeof(a));
+  int rc;
+  if ((rc = zero_line(ctx, &a.zero))) return rc;
+  a.xs = (const __bf16*)xs;
+  a.ws = (const __bf16*)ws;
+  a.scale = scale;
+  a.shift = shift;
+  a.res = res;
+  a.res_ld = res_ld;
+  a.res_s = (const __bf16*)res_s;
+  a.relu = relu;
+  a.y = y;
+  a.y_ld = y_ld;
+  a.y_off = y_off;
+  a.ys = (__bf16*)ys;
+  a.N = N;
+  a.Hi = Hi;
+  a.Wi = Wi;
+  a.Ci = Ci;
+  a.Co = Co;
+  a.kh = a.kw = k;
+  a.stride = stride;
+  a.pad = pad;
+  a.dil = dil;
+  a.Ho = (Hi + 2 * pad - dil * (k - 1) - 1) / stride + 1;
+  a.Wo = (Wi + 2 * pad - dil * (k - 1) - 1) / stride + 1;
+  a.M = N * a.Ho * a.Wo;
+  a.K = k * k * Ci;
+  ConvPlan p = plan_conv_x3s(a.M, a.Co, a.K);
+  if (bm > 0) {
+    CWT_CHECK((bm == 256 && (bn == 256 || bn == 128)) || (bm == 128 && (bn == 128 || bn == 64)) ||
+                  (bm == 64 && (bn == 128 || bn == 64)),
+              "tile must be one of 256x256, 256x128, 128x128, 128x64, 64x128, 64x64");
+    CWT_CHECK(Co % bn == 0, "Co % bn");
+    p.bm = bm;
+    p.bn = bn;
+  }
+  if (nsplit > 0) {
+    const int kt = a.K / 32;
+    p.kt_per_split = cdiv(kt, nsplit);
+    p.nsplit = cdiv(kt, p.kt_per_split);
+  }
+  void* part = nullptr;
+  const size_t pf = (size_t)p.nsplit * a.M * a.Co;
+  if (p.nsplit > 1 && (rc = ensure_ws(ctx, "dbg.PART", pf * 4, &part))) return rc;
+  return launch_conv_x3s(a, p, 0, (float*)part, pf, (hipStream_t)stream);
 }
 
 int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int64_t n, int num_classes,

@@ -14,7 +14,11 @@
 
 namespace cwt {
 
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
 // One thread per output pixel, all 64 output channels; weights [ci][ky][kx][co] in LDS.
+// SPLIT: write the S-layout [pix][2][hi 32 | lo 32] bf16 (conv_x3s.hip) instead of fp32 NHWC.
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void stem_conv1_kernel(const float* __restrict__ img, int N, int S,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ scale,
@@ -49,25 +53,46 @@ __global__ __launch_bounds__(256) void stem_conv1_kernel(const float* __restrict
       }
   float* o = out + pix * 64;
 #pragma unroll
-  for (int c4 = 0; c4 < 16; ++c4) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c8 = 0; c8 < 8; ++c8) {
+    float r[8];
 #pragma unroll
-    for (int k = 0; k < 27; ++k) {
-      f32x4 wv = *(const f32x4*)&ws[k * 64 + c4 * 4];
-      acc += in[k] * wv;
+    for (int h = 0; h < 2; ++h) {
+      const int c4 = c8 * 2 + h;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 27; ++k) {
+        f32x4 wv = *(const f32x4*)&ws[k * 64 + c4 * 4];
+        acc += in[k] * wv;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) r[h * 4 + q] = fmaxf(fmaf(acc[q], ss[c4 * 4 + q], bs[c4 * 4 + q]), 0.f);
     }
-    f32x4 r;
+    if (SPLIT) {
+      bf16x8 hi, lo;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) r[q] = fmaxf(fmaf(acc[q], ss[c4 * 4 + q], bs[c4 * 4 + q]), 0.f);
-    *(f32x4*)(o + c4 * 4) = r;
+      for (int q = 0; q < 8; ++q) {
+        hi[q] = (__bf16)r[q];
+        lo[q] = (__bf16)(r[q] - (float)hi[q]);
+      }
+      __bf16* sp = (__bf16*)out + pix * 128 + (c8 >> 2) * 64 + (c8 & 3) * 8;
+      *(bf16x8*)sp = hi;
+      *(bf16x8*)(sp + 32) = lo;
+    } else {
+      *(f32x4*)(o + c8 * 8) = f32x4{r[0], r[1], r[2], r[3]};
+      *(f32x4*)(o + c8 * 8 + 4) = f32x4{r[4], r[5], r[6], r[7]};
+    }
   }
 }
 
 int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const float* scale,
-                      const float* shift, float* out, int Ho, hipStream_t st) {
+                      const float* shift, float* out, int Ho, hipStream_t st, bool split) {
   long total = (long)N * Ho * Ho;
-  hipLaunchKernelGGL(stem_conv1_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, img, N, S, w27x64, scale,
-                     shift, out, Ho);
+  if (split)
+    hipLaunchKernelGGL(stem_conv1_kernel<true>, dim3(cdiv(total, 256)), dim3(256), 0, st, img, N, S, w27x64, scale,
+                       shift, out, Ho);
+  else
+    hipLaunchKernelGGL(stem_conv1_kernel<false>, dim3(cdiv(total, 256)), dim3(256), 0, st, img, N, S, w27x64, scale,
+                       shift, out, Ho);
   CWT_LAUNCH_CHECK();
   return 0;
 }
@@ -104,6 +129,56 @@ int launch_maxpool3s2(const float* in, int N, int H, int W, int C, float* out, i
                       hipStream_t st) {
   long total = (long)N * Ho * Wo * (C / 4);
   hipLaunchKernelGGL(maxpool3s2_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, in, N, H, W, C, out, Ho, Wo);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+// maxpool 3x3 s2 p1 on the S-layout: one thread per (pixel, 8 channels); max of hi + lo
+// (exact in fp32), re-split (same sum).
+__global__ void maxpool3s2_s_kernel(const __bf16* __restrict__ in, int N, int H, int W, int C,
+                                    __bf16* __restrict__ out, int Ho, int Wo) {
+  const int g8 = C >> 3;
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)N * Ho * Wo * g8;
+  if (idx >= total) return;
+  const int g = (int)(idx % g8);
+  const long pix = idx / g8;
+  const int ow = (int)(pix % Wo);
+  const int oh = (int)((pix / Wo) % Ho);
+  const int n = (int)(pix / ((long)Wo * Ho));
+  const int coff = (g >> 2) * 64 + (g & 3) * 8;  // within a pixel's C*2 bf16
+  float m[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) m[q] = -INFINITY;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    int ih = oh * 2 - 1 + ky;
+    if ((unsigned)ih >= (unsigned)H) continue;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      int iw = ow * 2 - 1 + kx;
+      if ((unsigned)iw >= (unsigned)W) continue;
+      const __bf16* sp = in + (((long)n * H + ih) * W + iw) * (2L * C) + coff;
+      const bf16x8 hi = *(const bf16x8*)sp, lo = *(const bf16x8*)(sp + 32);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], (float)hi[q] + (float)lo[q]);
+    }
+  }
+  bf16x8 hi, lo;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    hi[q] = (__bf16)m[q];
+    lo[q] = (__bf16)(m[q] - (float)hi[q]);
+  }
+  __bf16* dp = out + pix * (2L * C) + coff;
+  *(bf16x8*)dp = hi;
+  *(bf16x8*)(dp + 32) = lo;
+}
+
+int launch_maxpool3s2_s(const __bf16* in, int N, int H, int W, int C, __bf16* out, int Ho, int Wo, hipStream_t st) {
+  if (C % 32) return fail(CWT_EARG, "maxpool_s: C % 32");
+  long total = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool3s2_s_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, in, N, H, W, C, out, Ho, Wo);
   CWT_LAUNCH_CHECK();
   return 0;
 }
@@ -151,6 +226,8 @@ static PPMSegs make_segs(int in, const int* bins, int nbins) {
 
 constexpr int PPM_MAXSEG = 16;  // longest elementary segment handled without a loop
 
+// SPLIT: x is the S-layout (pixel stride 2*C bf16; value = hi + lo), else fp32 (stride ld).
+template <bool SPLIT>
 __global__ void ppm_rowseg_kernel(const float* __restrict__ x, int N, int h, int w, int ld, int C, PPMSegs sx,
                                   float* __restrict__ rowseg) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -162,11 +239,18 @@ __global__ void ppm_rowseg_kernel(const float* __restrict__ x, int N, int h, int
   const long ny = r / sx.nseg;
   const int x0 = sx.b[xs], len = sx.b[xs + 1] - x0;
   const float* src = x + (ny * w + x0) * (long)ld + c;
+  const __bf16* ssrc = (const __bf16*)x + (ny * w + x0) * (2L * C) + (c >> 5) * 64 + (c & 31);
   float s = 0.f;
   for (int u0 = 0; u0 < len; u0 += PPM_MAXSEG) {
     float v[PPM_MAXSEG];
 #pragma unroll
-    for (int u = 0; u < PPM_MAXSEG; ++u) v[u] = src[(long)min(u0 + u, len - 1) * ld];
+    for (int u = 0; u < PPM_MAXSEG; ++u) {
+      const long o = (long)min(u0 + u, len - 1);
+      if (SPLIT)
+        v[u] = (float)ssrc[o * 2 * C] + (float)ssrc[o * 2 * C + 32];
+      else
+        v[u] = src[o * ld];
+    }
 #pragma unroll
     for (int u = 0; u < PPM_MAXSEG; ++u)
       if (u0 + u < len) s += v[u];
@@ -237,7 +321,7 @@ __global__ void ppm_cell_kernel(const float* __restrict__ blk, int N, int C, PPM
 
 // ws: rowseg [N][h][nseg_x][C] followed by blk [N][nseg_y][nseg_x][C]
 int launch_ppm(const float* x, int N, int h, int w, int ld, const int* bins, int nbins, float* ws,
-               float* pooled, hipStream_t st) {
+               float* pooled, hipStream_t st, bool split) {
   if (nbins != 4) return fail(CWT_EARG, "PPM expects 4 bins");
   const PPMSegs sx = make_segs(w, bins, nbins), sy = make_segs(h, bins, nbins);
   if (sx.nwin > 16 || sx.nseg > 16 || sy.nseg > 16) return fail(CWT_EARG, "PPM: too many windows");
@@ -245,7 +329,11 @@ int launch_ppm(const float* x, int N, int h, int w, int ld, const int* bins, int
   float* rowseg = ws;
   float* blk = ws + (long)N * h * sx.nseg * C;
   const long t1 = (long)N * h * sx.nseg * C;
-  hipLaunchKernelGGL(ppm_rowseg_kernel, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx, rowseg);
+  if (split)
+    hipLaunchKernelGGL(ppm_rowseg_kernel<true>, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx, rowseg);
+  else
+    hipLaunchKernelGGL(ppm_rowseg_kernel<false>, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx,
+                       rowseg);
   CWT_LAUNCH_CHECK();
   const long t2 = (long)N * sy.nseg * sx.nseg * C;
   hipLaunchKernelGGL(ppm_blk_kernel, dim3(cdiv(t2, 256)), dim3(256), 0, st, (const float*)rowseg, N, h, C, sx, sy,

@@ -1,0 +1,480 @@
+// Implicit-GEMM convolution on split activations ("x3s"): bf16x3 arithmetic (see
+// conv_x3.hip) with BOTH operands stored pre-split in HBM, so the main loop moves bytes
+// HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4) and never touches them in VGPRs.
+//
+// Split layout ("S-layout") of an activation map with C channels, and of the packed weights:
+//   [row][C/32][64 bf16]: per 32-channel block, 32 x hi = bf16_rne(v) then 32 x lo =
+//   bf16_rne(v - hi).  One 128-B line holds one block of one pixel (or of one output
+//   channel's K-slice for the weights, rows = Co, blocks in packed_k order).
+// hi + lo carries 16 significant bits; the bf16x3 conv of conv_x3.hip splits its fp32
+// input the same way while staging, so the MFMA inputs are bit-identical: storing the split
+// instead of fp32 changes only what residual adds and the byte kernels see (hi + lo, a
+// 2^-17 relative rounding of the fp32 value).  Same bytes as fp32 (4 B per element).
+//
+// Main loop (one barrier per 32-deep K-tile, NSTG-deep LDS ring):
+//   wait own LDS-DMA of tile t (counted vmcnt, later tiles stay in flight) -> barrier ->
+//   issue LDS-DMA of tile t+NSTG-1 into the slot tile t-1 just vacated -> fragments of
+//   tile t by ds_read_b128 -> 3 x v_mfma_f32_16x16x32_bf16 per 16x16 fragment pair.
+// LDS image: rows of 128 B (A rows then B rows per stage), 16-B chunk c of row r stored in
+// slot c ^ ((r >> 1) & 7) (the swizzle goes on the LDS-DMA SOURCE address, the image
+// itself is lane-linear): conflict-free for the 16x16x32 fragment reads (4 lane groups of
+// 16 hit 16 distinct 16-B bank slots; checked exhaustively).
+// Out-of-image taps (zero padding) and rows past M load from a zero line.
+// Epilogue: fragments -> per-wave LDS tile -> row-contiguous 8-channel groups per lane:
+// BN scale/shift, residual (fp32 or S-layout), ReLU, stored as fp32 NHWC (channel
+// offset/stride) and/or S-layout, or the raw split-K partials (fp32 [ks][M][Co]).
+#include "common.h"
+#include "kernels.h"
+
+namespace cwt {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+#define CWT_LDS __attribute__((address_space(3)))
+#define CWT_GLB __attribute__((address_space(1)))
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const CWT_GLB void*)src, (CWT_LDS void*)lds_dst, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// vmcnt(n * LPT) for a runtime n in [0, 3]
+template <int LPT>
+__device__ __forceinline__ void wait_tiles(int n) {
+  if (n <= 0)
+    wait_vmcnt<0>();
+  else if (n == 1)
+    wait_vmcnt<LPT>();
+  else if (n == 2)
+    wait_vmcnt<2 * LPT>();
+  else
+    wait_vmcnt<3 * LPT>();
+}
+
+__device__ __forceinline__ void block_sync_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// 8 consecutive channels [co, co + 8) of output row m: BN, residual, ReLU, stores.
+__device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, const float* v, const float* sc,
+                                           const float* sh) {
+  float o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = fmaf(v[i], sc[i], sh[i]);
+  if (a.res) {
+    const f32x4* rp = (const f32x4*)(a.res + (long)m * a.res_ld + co);
+    const f32x4 r0 = rp[0], r1 = rp[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[i] += r0[i];
+      o[4 + i] += r1[i];
+    }
+  } else if (a.res_s) {
+    const __bf16* rp = a.res_s + ((long)m * (a.Co >> 5) + (co >> 5)) * 64 + (co & 31);
+    const bf16x8 rh = *(const bf16x8*)rp, rl = *(const bf16x8*)(rp + 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] += (float)rh[i] + (float)rl[i];
+  }
+  if (a.relu) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = fmaxf(o[i], 0.f);
+  }
+  if (a.y) {
+    f32x4* yp = (f32x4*)(a.y + (long)m * a.y_ld + a.y_off + co);
+    yp[0] = f32x4{o[0], o[1], o[2], o[3]};
+    yp[1] = f32x4{o[4], o[5], o[6], o[7]};
+  }
+  if (a.ys) {
+    bf16x8 hi, lo;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      hi[i] = (__bf16)o[i];
+      lo[i] = (__bf16)(o[i] - (float)hi[i]);
+    }
+    __bf16* sp = a.ys + ((long)m * (a.Co >> 5) + (co >> 5)) * 64 + (co & 31);
+    *(bf16x8*)sp = hi;
+    *(bf16x8*)(sp + 32) = lo;
+  }
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArgs a) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  constexpr int LA = BM / (8 * NW), LB = BN / (8 * NW);  // LDS-DMA pieces (8 rows x 128 B) per wave per tile
+  constexpr int LPT = LA + LB;
+  constexpr int STG_BYTES = (BM + BN) * 128;
+  static_assert(LA * 8 * NW == BM && LB * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
+  static_assert(NSTG >= 2 && NSTG <= 5, "ring depth");
+  constexpr int EP_ROWS = WM < 32 ? WM : 32;
+  constexpr int EP_LD = WN + 4;  // floats per row of a wave's epilogue tile
+  constexpr int EP_BYTES = NW * EP_ROWS * EP_LD * 4;
+  constexpr int SMEM = NSTG * STG_BYTES > EP_BYTES ? NSTG * STG_BYTES : EP_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];  // the one LDS object (ring + epilogue)
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv / WAVES_N, wn = wv % WAVES_N;
+  int mt, nt, ks;
+  conv_tile_coords(mt, nt, ks);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kt_begin = ks * a.kt_per_split;
+  const int kt_end = min(a.ktiles, kt_begin + a.kt_per_split);
+  const int T = kt_end - kt_begin;
+
+  // ---- LDS-DMA source geometry (constant over K) ----
+  const int lrow = lane >> 3, lslot = lane & 7;
+  const int cblocks = a.Ci >> 5;
+  int a_ih0[LA], a_iw0[LA], a_pix0[LA], a_ch[LA];
+  const int HoWo = a.Ho * a.Wo;
+#pragma unroll
+  for (int j = 0; j < LA; ++j) {
+    const int r = (wv * LA + j) * 8 + lrow;
+    a_ch[j] = (lslot ^ ((r >> 1) & 7)) * 8;
+    const int m = m0 + r;
+    if (m < a.M) {
+      const int n = m / HoWo;
+      const int rem = m - n * HoWo;
+      const int oh = rem / a.Wo;
+      const int ow = rem - oh * a.Wo;
+      a_ih0[j] = oh * a.stride - a.pad;
+      a_iw0[j] = ow * a.stride - a.pad;
+      a_pix0[j] = (n * a.Hi + a_ih0[j]) * a.Wi + a_iw0[j];
+    } else {
+      a_ih0[j] = -(1 << 28);
+      a_iw0[j] = 0;
+      a_pix0[j] = 0;
+    }
+  }
+  const int b_rowlen = a.ktiles_total * 64;  // bf16 per packed weight row
+  int b_off[LB];
+#pragma unroll
+  for (int j = 0; j < LB; ++j) {
+    const int r = (wv * LB + j) * 8 + lrow;
+    b_off[j] = (n0 + r) * b_rowlen + (lslot ^ ((r >> 1) & 7)) * 8;
+  }
+
+  // next tile to issue: (channel block, ky, kx) walked incrementally (packed_k order)
+  int i_cb, i_ky, i_kx;
+  {
+    const int taps = a.kh * a.kw;
+    i_cb = kt_begin / taps;
+    const int tap = kt_begin - i_cb * taps;
+    i_ky = tap / a.kw;
+    i_kx = tap - i_ky * a.kw;
+  }
+  int i_kt = kt_begin;
+  auto issue = [&](int stg) {
+    char* sb = smem + stg * STG_BYTES;
+    const int dy = i_ky * a.dil, dx = i_kx * a.dil;
+    const int shift = dy * a.Wi + dx;
+#pragma unroll
+    for (int j = 0; j < LA; ++j) {
+      const int ih = a_ih0[j] + dy, iw = a_iw0[j] + dx;
+      const bool in = (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+      const __bf16* src = in ? a.xs + ((a_pix0[j] + shift) * cblocks + i_cb) * 64 + a_ch[j] : a.zero;
+      glds16(src, sb + (wv * LA + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < LB; ++j) glds16(a.ws + b_off[j] + i_kt * 64, sb + BM * 128 + (wv * LB + j) * 1024);
+    ++i_kt;
+    if (++i_kx == a.kw) {
+      i_kx = 0;
+      if (++i_ky == a.kh) {
+        i_ky = 0;
+        ++i_cb;
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read geometry: lane -> row (lane & 15) of a 16-row block, k-chunk (lane >> 4)
+  const int fr = lane & 15, fk = lane >> 4;
+  const int swz = (fr >> 1) & 7;
+  const int off_hi = fr * 128 + ((fk ^ swz) << 4);
+  const int off_lo = fr * 128 + (((4 + fk) ^ swz) << 4);
+  const int a_row0 = wm * WM, b_row0 = BM + wn * WN;
+
+#pragma unroll
+  for (int s = 0; s < NSTG - 1; ++s)
+    if (s < T) issue(s);
+
+  for (int t = 0; t < T; ++t) {
+    wait_tiles<LPT>(min(NSTG - 2, T - 1 - t));
+    block_sync_lds();
+    if (t + NSTG - 1 < T) issue((t + NSTG - 1) % NSTG);
+    const char* sb = smem + (t % NSTG) * STG_BYTES;
+    bf16x8 bh[FN], bl[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const char* p = sb + (b_row0 + j * 16) * 128;
+      bh[j] = *(const bf16x8*)(p + off_hi);
+      bl[j] = *(const bf16x8*)(p + off_lo);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const char* p = sb + (a_row0 + i * 16) * 128;
+      const bf16x8 ah = *(const bf16x8*)(p + off_hi);
+      const bf16x8 al = *(const bf16x8*)(p + off_lo);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue through a per-wave LDS tile ----
+  wait_vmcnt<0>();
+  block_sync_lds();
+  float* ep = (float*)smem + wv * (EP_ROWS * EP_LD);
+  constexpr int LPR = WN / 8;    // lanes per output row (8 channels each)
+  constexpr int RPR = 64 / LPR;  // rows per round
+  static_assert(LPR * 8 == WN && RPR * LPR == 64 && EP_ROWS % RPR == 0, "epilogue geometry");
+  const int er = lane / LPR, eg = lane - er * LPR;
+  const int co = n0 + wn * WN + eg * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = a.part ? 1.f : a.scale[co + i];
+    sh[i] = a.part ? 0.f : a.shift[co + i];
+  }
+  const int fq = lane >> 4;
+#pragma unroll
+  for (int pass = 0; pass < WM / EP_ROWS; ++pass) {
+#pragma unroll
+    for (int fi = 0; fi < EP_ROWS / 16; ++fi)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ep[(fi * 16 + fq * 4 + q) * EP_LD + j * 16 + fr] = acc[pass * (EP_ROWS / 16) + fi][j][q];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int rr = 0; rr < EP_ROWS / RPR; ++rr) {
+      const int r = rr * RPR + er;
+      const int m = m0 + wm * WM + pass * EP_ROWS + r;
+      const f32x4 v0 = *(const f32x4*)(ep + r * EP_LD + eg * 8);
+      const f32x4 v1 = *(const f32x4*)(ep + r * EP_LD + eg * 8 + 4);
+      if (m < a.M) {
+        if (a.part) {
+          f32x4* pp = (f32x4*)(a.part + ((long)ks * a.M + m) * a.Co + co);
+          pp[0] = v0;
+          pp[1] = v1;
+        } else {
+          const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          store_out8(a, m, co, v, sc, sh);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+// Split-K reduction (fixed order, deterministic) + the same epilogue math.
+template <int NS>
+__global__ void conv_s_splitk_epilogue(ConvSArgs a, int nsplit) {
+  const int g8 = a.Co >> 3;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)a.M * g8) return;
+  const int m = (int)(idx / g8);
+  const int co = (int)(idx - (long)m * g8) * 8;
+  const long ps = (long)a.M * a.Co;
+  const float* pp = a.part + (long)m * a.Co + co;
+  float v[8];
+  {
+    const f32x4 p0 = *(const f32x4*)pp, p1 = *(const f32x4*)(pp + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = p0[i];
+      v[4 + i] = p1[i];
+    }
+  }
+  const int ns = NS > 0 ? NS : nsplit;
+#pragma unroll
+  for (int k = 1; k < (NS > 0 ? NS : 64); ++k) {
+    if (k >= ns) break;
+    const f32x4 p0 = *(const f32x4*)(pp + k * ps), p1 = *(const f32x4*)(pp + k * ps + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] += p0[i];
+      v[4 + i] += p1[i];
+    }
+  }
+  float sc[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = a.scale[co + i];
+    sh[i] = a.shift[co + i];
+  }
+  store_out8(a, m, co, v, sc, sh);
+}
+
+// fp32 [P][C] (pixel stride ld) -> S-layout [P][C/32][64]
+__global__ void split_act_kernel(const float* x, long P, int C, int ld, __bf16* out) {
+  const int g8 = C >> 3;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= P * g8) return;
+  const long p = idx / g8;
+  const int c = (int)(idx - p * g8) * 8;
+  const f32x4 v0 = *(const f32x4*)(x + p * ld + c), v1 = *(const f32x4*)(x + p * ld + c + 4);
+  const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  bf16x8 hi, lo;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    hi[i] = (__bf16)v[i];
+    lo[i] = (__bf16)(v[i] - (float)hi[i]);
+  }
+  __bf16* sp = out + (p * (C >> 5) + (c >> 5)) * 64 + (c & 31);
+  *(bf16x8*)sp = hi;
+  *(bf16x8*)(sp + 32) = lo;
+}
+
+// S-layout -> fp32 (hi + lo), pixel stride ld
+__global__ void unsplit_act_kernel(const __bf16* s, long P, int C, float* out, int ld) {
+  const int g8 = C >> 3;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= P * g8) return;
+  const long p = idx / g8;
+  const int c = (int)(idx - p * g8) * 8;
+  const __bf16* sp = s + (p * (C >> 5) + (c >> 5)) * 64 + (c & 31);
+  const bf16x8 hi = *(const bf16x8*)sp, lo = *(const bf16x8*)(sp + 32);
+  f32x4 v0, v1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v0[i] = (float)hi[i] + (float)lo[i];
+    v1[i] = (float)hi[4 + i] + (float)lo[4 + i];
+  }
+  *(f32x4*)(out + p * ld + c) = v0;
+  *(f32x4*)(out + p * ld + c + 4) = v1;
+}
+
+int launch_split_act(const float* x, long P, int C, int ld, __bf16* out, hipStream_t st) {
+  if (C % 32) return fail(CWT_EARG, "split_act: C % 32");
+  const long n = P * (C / 8);
+  hipLaunchKernelGGL(split_act_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, P, C, ld, out);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipStream_t st) {
+  if (C % 32) return fail(CWT_EARG, "unsplit_act: C % 32");
+  const long n = P * (C / 8);
+  hipLaunchKernelGGL(unsplit_act_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, s, P, C, out, ld);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int STAGE>
+static void launch_tiles_x3s(const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
+  if (p.bm == 256 && p.bn == 256)
+    hipLaunchKernelGGL((conv_igemm_x3s<256, 256, 2, 4, 2, STAGE>), grid, dim3(512), 0, st, a);
+  else if (p.bm == 256 && p.bn == 128)
+    hipLaunchKernelGGL((conv_igemm_x3s<256, 128, 4, 2, 3, STAGE>), grid, dim3(512), 0, st, a);
+  else if (p.bm == 128 && p.bn == 128)
+    hipLaunchKernelGGL((conv_igemm_x3s<128, 128, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
+  else if (p.bm == 128 && p.bn == 64)
+    hipLaunchKernelGGL((conv_igemm_x3s<128, 64, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
+  else if (p.bm == 64 && p.bn == 128)
+    hipLaunchKernelGGL((conv_igemm_x3s<64, 128, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_igemm_x3s<64, 64, 2, 2, 4, STAGE>), grid, dim3(256), 0, st, a);
+}
+
+struct MeasuredPlanS {
+  int M, Co, K, bm, bn, nsplit;
+};
+static const MeasuredPlanS kMeasuredPlansS[] = {
+#include "conv_plans_x3s.inc"
+};
+
+// The measured plan for this GEMM shape if the sweep found one (conv_plans_x3s.inc, made by
+// tools/gen_plan_table.py --x3s from tools/conv_s_sweep.py on the MI355X), else the largest
+// tile giving >= kMinWG workgroups, splitting K by powers of two (>= 8 K-tiles per split)
+// where the output grid is too small.
+ConvPlan plan_conv_x3s(int M, int Co, int K) {
+  constexpr long kMinWG = 200;
+  const int ktiles = K / 32;
+  for (const MeasuredPlanS& e : kMeasuredPlansS)
+    if (e.M == M && e.Co == Co && e.K == K && Co % e.bn == 0) {
+      ConvPlan p;
+      p.bm = e.bm;
+      p.bn = e.bn;
+      p.kt_per_split = cdiv(ktiles, e.nsplit);
+      p.nsplit = cdiv(ktiles, p.kt_per_split);
+      return p;
+    }
+  static const int cand[6][2] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  ConvPlan best;
+  for (auto& c : cand) {
+    if (Co % c[1] != 0) continue;
+    const long tiles = (long)cdiv(M, c[0]) * (Co / c[1]);
+    int ks = 1;
+    while (tiles * ks < kMinWG && ktiles / (ks * 2) >= 8) ks *= 2;
+    ConvPlan p;
+    p.bm = c[0];
+    p.bn = c[1];
+    p.kt_per_split = cdiv(ktiles, ks);
+    p.nsplit = cdiv(ktiles, p.kt_per_split);
+    if (tiles * p.nsplit >= kMinWG) return p;
+    best = p;
+  }
+  return best;
+}
+
+int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,
+                    hipStream_t st) {
+  if (!a.xs || !a.ws || !a.zero) return fail(CWT_ESTATE, "x3s conv needs split input, split weights and a zero line");
+  if (a.Ci % 32 || a.Co % 64 || a.Co % p.bn) return fail(CWT_EARG, "x3s conv: need Ci % 32 == 0, Co % 64 == 0");
+  a.ktiles = a.K / 32;
+  a.ktiles_total = a.ktiles;
+  a.kt_per_split = p.kt_per_split;
+  const int nsplit = p.nsplit;
+  ConvSArgs main = a;
+  if (nsplit > 1) {
+    if ((size_t)nsplit * a.M * a.Co > part_ws_floats) return fail(CWT_ESTATE, "split-K workspace too small");
+    main.part = part_ws;
+  } else {
+    main.part = nullptr;
+  }
+  dim3 grid(cdiv(a.M, p.bm), a.Co / p.bn, nsplit);
+  switch (stage) {
+    case 0: launch_tiles_x3s<0>(main, p, grid, st); break;
+    case 1: launch_tiles_x3s<1>(main, p, grid, st); break;
+    case 2: launch_tiles_x3s<2>(main, p, grid, st); break;
+    case 3: launch_tiles_x3s<3>(main, p, grid, st); break;
+    case 4: launch_tiles_x3s<4>(main, p, grid, st); break;
+    case 5: launch_tiles_x3s<5>(main, p, grid, st); break;
+    default: launch_tiles_x3s<6>(main, p, grid, st); break;
+  }
+  CWT_LAUNCH_CHECK();
+  if (nsplit > 1) {
+    main.part = part_ws;
+    const long n = (long)a.M * (a.Co / 8);
+    const dim3 g((unsigned)((n + 255) / 256)), b(256);
+    switch (nsplit) {
+      case 2: hipLaunchKernelGGL(conv_s_splitk_epilogue<2>, g, b, 0, st, main, nsplit); break;
+      case 3: hipLaunchKernelGGL(conv_s_splitk_epilogue<3>, g, b, 0, st, main, nsplit); break;
+      case 4: hipLaunchKernelGGL(conv_s_splitk_epilogue<4>, g, b, 0, st, main, nsplit); break;
+      case 8: hipLaunchKernelGGL(conv_s_splitk_epilogue<8>, g, b, 0, st, main, nsplit); break;
+      default: hipLaunchKernelGGL(conv_s_splitk_epilogue<0>, g, b, 0, st, main, nsplit); break;
+    }
+    CWT_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+}  // namespace cwt

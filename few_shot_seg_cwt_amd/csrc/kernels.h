@@ -23,6 +23,26 @@ struct ConvArgs {
   int relu;
 };
 
+// Conv on split activations (conv_x3s.hip): input and weights in the S-layout
+// [row][C/32][hi 32 | lo 32] bf16; output fp32 NHWC and/or S-layout.
+struct ConvSArgs {
+  const __bf16* xs;     // input, S-layout [N*Hi*Wi][Ci/32][64]
+  const __bf16* ws;     // weights, S-layout [Co][K/32][64] (K in packed_k order)
+  const __bf16* zero;   // >= 128 B of zeros (padding taps, rows past M)
+  const float* scale;   // [Co] folded BN scale
+  const float* shift;   // [Co] folded BN shift
+  const float* res;     // optional fp32 residual NHWC, pixel stride res_ld
+  const __bf16* res_s;  // optional S-layout residual [M][Co/32][64]
+  float* y;             // optional fp32 output NHWC, pixel stride y_ld, channel offset y_off
+  __bf16* ys;           // optional S-layout output [M][Co/32][64]
+  float* part;          // split-K partials [nsplit][M][Co] (set by launch_conv_x3s)
+  int N, Hi, Wi, Ci;
+  int Ho, Wo, Co, kh, kw, stride, pad, dil;
+  int M, K, ktiles, ktiles_total, kt_per_split;
+  int y_ld, y_off, res_ld;
+  int relu;
+};
+
 // Conv weights are packed [Co][K] with K ordered (32-channel block, tap, channel in block):
 // a 3x3 conv's workgroup walks its 9 taps over one 32-channel slab of its input window
 // before the next slab, so the slab (~40 KB for 256 output pixels) is re-read from L1/L2
@@ -95,6 +115,12 @@ ConvPlan plan_conv_x3(int M, int Co, int K);
 int launch_conv_x3(ConvArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,
                    hipStream_t st);
 int launch_split_bf16(const float* w, __bf16* hi, __bf16* lo, long n, hipStream_t st);
+// split-activation variant (conv_x3s.hip)
+ConvPlan plan_conv_x3s(int M, int Co, int K);
+int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,
+                    hipStream_t st);
+int launch_split_act(const float* x, long P, int C, int ld, __bf16* out, hipStream_t st);
+int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipStream_t st);
 
 // inner loop (adapt.hip): cache of instantiated graphs of the 200-step launch sequence
 struct AdaptGraphCache {
@@ -114,11 +140,12 @@ struct AdaptGraphCache {
 
 // backbone helpers (backbone.hip)
 int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const float* scale,
-                      const float* shift, float* out, int Ho, hipStream_t st);
+                      const float* shift, float* out, int Ho, hipStream_t st, bool split = false);
+int launch_maxpool3s2_s(const __bf16* in, int N, int H, int W, int C, __bf16* out, int Ho, int Wo, hipStream_t st);
 int launch_maxpool3s2(const float* in, int N, int H, int W, int C, float* out, int Ho, int Wo,
                       hipStream_t st);
 int launch_ppm(const float* x, int N, int h, int w, int ld, const int* bins, int nbins, float* ws,
-               float* pooled, hipStream_t st);
+               float* pooled, hipStream_t st, bool split = false);
 int launch_repack_cblock(const float* src, float* dst, int Co, int taps, int Ci, hipStream_t st);
 int launch_smallm_gemm(const float* A, int lda, const float* const* Bt, const int* M, int np, int N, int K, int kc,
                        float* part, size_t part_floats, const float* const* scale, const float* const* shift,

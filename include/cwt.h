@@ -200,6 +200,24 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
                    int y_ld, int y_off, int bm, int bn, int nsplit, int precision, void* stream);
 
 /*
+ * Test hooks of the split-activation conv (conv_x3s.hip).  S-layout = [rows][C/32][64 bf16]:
+ * per 32-channel block 32 x hi = bf16_rne(v) then 32 x lo = bf16_rne(v - hi).
+ * cwt_debug_split_act: fp32 [P][C] (pixel stride ld) -> S-layout; cwt_debug_unsplit_act the
+ * inverse (hi + lo).  cwt_debug_pack_wsplit: weights [Co][k][k][Ci] fp32 -> S-layout rows of
+ * K = k*k*Ci in the library's K order.  cwt_debug_conv_s: one conv on S-layout input and
+ * weights, folded BN, optional fp32 (res) or S-layout (res_s) residual, ReLU; writes fp32 NHWC
+ * y (pixel stride y_ld, channel offset y_off) and/or S-layout ys; bm/bn/nsplit force the plan
+ * (0 = automatic).
+ */
+int cwt_debug_split_act(cwt_ctx* ctx, const float* x, int64_t P, int C, int ld, void* out, void* stream);
+int cwt_debug_unsplit_act(cwt_ctx* ctx, const void* s, int64_t P, int C, float* out, int ld, void* stream);
+int cwt_debug_pack_wsplit(cwt_ctx* ctx, const float* w, int Co, int k, int Ci, void* out, void* stream);
+int cwt_debug_conv_s(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws,
+                     const float* scale, const float* shift, int Co, int k, int stride, int pad,
+                     int dil, const float* res, int res_ld, const void* res_s, int relu, float* y,
+                     int y_ld, int y_off, void* ys, int bm, int bn, int nsplit, void* stream);
+
+/*
  * CU-partitioned streams (MI355X-native episode pipelining): a HIP stream
  * whose kernels (including replays of graphs launched on it) only run on the CUs whose bits
  * are set in mask (mask_words 32-bit words, bit i = CU i of the device).  Used to run one

@@ -1,0 +1,139 @@
+"""Every tile / split-K plan of the split-activation conv (cwt_debug_conv_s, conv_x3s.hip)
+against a float64 torch conv + folded BN (+ fp32 or S-layout residual) (+ ReLU), with both
+output forms (fp32 NHWC at a channel offset/stride, and S-layout), plus the S-layout
+split/unsplit round trip."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from few_shot_seg_cwt_amd import synthetic as syn  # noqa: E402
+
+# bf16x3 drops the lo*lo term (~2^-16 relative per product); the S-layout input is hi+lo
+# (16 significant bits), which is exactly what the bf16x3 MFMAs see anyway
+TOL = 1e-4
+
+
+def _lib():
+    from few_shot_seg_cwt_amd import _lib as L
+    return L
+
+
+def split(t_nhwc):
+    """fp32 [..., C] (device) -> S-layout bf16 [..., C/32, 64]"""
+    L = _lib()
+    C = t_nhwc.shape[-1]
+    P = t_nhwc.numel() // C
+    out = torch.empty(P * C * 2, dtype=torch.bfloat16, device=t_nhwc.device)
+    L.check(L.lib().cwt_debug_split_act(L.ctx(0), L.ptr(t_nhwc), P, C, C, L.ptr(out), L.stream_ptr()), "split")
+    return out
+
+
+def unsplit(s, P, C):
+    L = _lib()
+    out = torch.empty(P, C, device=s.device)
+    L.check(L.lib().cwt_debug_unsplit_act(L.ctx(0), L.ptr(s), P, C, L.ptr(out), C, L.stream_ptr()), "unsplit")
+    return out
+
+
+def run_conv_s(x, w, scale, shift, stride, pad, dil, res=None, res_split=False, relu=True, bm=0, bn=0, nsplit=0,
+               y_pad=0, y_off=0):
+    L = _lib()
+    dev = torch.device("cuda", 0)
+    N, Ci, Hi, Wi = x.shape
+    Co, _, k, _ = w.shape
+    xs = split(x.permute(0, 2, 3, 1).contiguous().to(dev))
+    wd = w.permute(0, 2, 3, 1).contiguous().to(dev)
+    ws = torch.empty(Co * k * k * Ci * 2, dtype=torch.bfloat16, device=dev)
+    L.check(L.lib().cwt_debug_pack_wsplit(L.ctx(0), L.ptr(wd), Co, k, Ci, L.ptr(ws), L.stream_ptr()), "pack")
+    Ho = (Hi + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    y_ld = Co + y_pad
+    y = torch.full((N, Ho, Ho, y_ld), float("nan"), device=dev)
+    ys = torch.zeros(N * Ho * Ho * Co * 2, dtype=torch.bfloat16, device=dev)
+    rd = res.permute(0, 2, 3, 1).contiguous().to(dev) if res is not None else None
+    rs = split(rd) if (rd is not None and res_split) else None
+    sc, sh = scale.to(dev), shift.to(dev)
+    rc = L.lib().cwt_debug_conv_s(L.ctx(0), L.ptr(xs), N, Hi, Wi, Ci, L.ptr(ws), L.ptr(sc), L.ptr(sh), Co, k,
+                                  stride, pad, dil, None if res_split else L.ptr(rd), Co, L.ptr(rs), int(relu),
+                                  L.ptr(y), y_ld, y_off, L.ptr(ys), bm, bn, nsplit, L.stream_ptr())
+    L.check(rc, "cwt_debug_conv_s")
+    torch.cuda.synchronize()
+    yc = y.cpu()
+    if y_pad:
+        untouched = torch.cat([yc[..., :y_off], yc[..., y_off + Co:]], -1)
+        assert torch.isnan(untouched).all(), "wrote outside its channel slice"
+    yf = yc[..., y_off:y_off + Co]
+    yu = unsplit(ys, N * Ho * Ho, Co).cpu().reshape(N, Ho, Ho, Co)
+    return yf.permute(0, 3, 1, 2), yu.permute(0, 3, 1, 2)
+
+
+def ref_conv(x, w, scale, shift, stride, pad, dil, res=None, relu=True):
+    y = F.conv2d(x.double(), w.double(), None, stride, pad, dil)
+    y = y * scale.double()[None, :, None, None] + shift.double()[None, :, None, None]
+    if res is not None:
+        y = y + res.double()
+    return F.relu(y) if relu else y
+
+
+CASES = [  # N, Ci, Co, Hi, k, stride, dil, residual
+    (2, 64, 64, 37, 3, 1, 1, False),
+    (2, 64, 128, 37, 3, 1, 1, False),
+    (1, 128, 256, 23, 1, 1, 1, True),
+    (2, 256, 128, 21, 1, 2, 1, False),
+    (1, 128, 128, 21, 3, 2, 1, False),
+    (2, 256, 256, 15, 3, 1, 2, True),
+    (1, 512, 128, 13, 3, 1, 4, False),
+    (3, 96, 64, 9, 1, 1, 1, True),
+    (1, 64, 512, 19, 3, 1, 1, True),
+]
+PLANS = [(0, 0, 0), (256, 256, 1), (256, 128, 1), (128, 128, 1), (128, 64, 1), (64, 128, 1), (64, 64, 1),
+         (64, 64, 3), (128, 128, 2), (256, 256, 4)]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("plan", PLANS, ids=lambda p: f"{p[0]}x{p[1]}s{p[2]}")
+def test_conv_s_plans(case, plan):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    N, Ci, Co, Hi, k, stride, dil, has_res = case
+    bm, bn, ns = plan
+    if bn and Co % bn:
+        pytest.skip("Co not a multiple of the tile")
+    tag = f"{N}_{Ci}_{Co}_{Hi}_{k}"
+    x = torch.from_numpy(syn.normal(1, "x" + tag, (N, Ci, Hi, Hi), 1.0))
+    w = torch.from_numpy(syn.normal(1, "w" + tag, (Co, Ci, k, k), (2.0 / (Ci * k * k)) ** 0.5))
+    scale = torch.from_numpy(syn.uniform(1, "s" + tag, (Co,), 0.5, 1.5))
+    shift = torch.from_numpy(syn.normal(1, "b" + tag, (Co,), 0.1))
+    pad = dil if k == 3 else 0
+    Ho = (Hi + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    res = torch.from_numpy(syn.normal(1, "r" + tag, (N, Co, Ho, Ho), 1.0)) if has_res else None
+    yf, yu = run_conv_s(x, w, scale, shift, stride, pad, dil, res, res_split=(ns % 2 == 1), bm=bm, bn=bn,
+                        nsplit=ns)
+    ref = ref_conv(x, w, scale, shift, stride, pad, dil, res, True)
+    err = float((yf.double() - ref).abs().max() / ref.abs().max())
+    assert err < TOL, err
+    # the S-layout output is the split of the fp32 output (hi + lo = 16 significant bits)
+    assert float((yu.double() - yf.double()).abs().max() / ref.abs().max()) < 2.0 ** -15
+
+
+def test_conv_s_channel_strided_out():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    x = torch.from_numpy(syn.normal(2, "x", (2, 64, 11, 11), 1.0))
+    w = torch.from_numpy(syn.normal(2, "w", (128, 64, 3, 3), 0.06))
+    scale, shift = torch.ones(128), torch.zeros(128)
+    yf, _ = run_conv_s(x, w, scale, shift, 1, 1, 1, None, relu=False, y_pad=256, y_off=128)
+    ref = ref_conv(x, w, scale, shift, 1, 1, 1, None, False)
+    assert float((yf.double() - ref).abs().max() / ref.abs().max()) < TOL
+
+
+def test_split_roundtrip():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    x = torch.from_numpy(syn.normal(3, "rt", (1000, 96), 10.0)).cuda()
+    s = split(x)
+    hi = s.view(1000, 3, 2, 32)[:, :, 0].reshape(1000, 96)
+    assert torch.equal(hi, x.to(torch.bfloat16))          # hi = bf16_rne(x)
+    back = unsplit(s, 1000, 96)
+    assert float(((back - x).abs() / x.abs().clamp_min(1e-30)).max()) < 2.0 ** -16
