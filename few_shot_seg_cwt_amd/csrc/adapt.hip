@@ -76,8 +76,9 @@ constexpr int ADAPT_CB = 16;           // lo-res columns per workgroup
 // contended atomic rate (~0.09 TB/s, ~5 us per step; MI355X_MICROARCH.md Global float
 // atomics); spreading them over R rows (workgroup id % R) removes the contention and the
 // next step sums the R rows when it loads W.
-constexpr int ADAPT_R = 16;
-constexpr int ADAPT_SLOT = ADAPT_R * 512;  // floats per accumulator slot
+constexpr int ADAPT_RMAX = 32;                 // replica rows allocated per slot
+constexpr int ADAPT_R_DEFAULT = 8;             // replica rows used (CWT_ADAPT_R overrides: 4, 8, 16 or 32)
+constexpr int ADAPT_SLOT = ADAPT_RMAX * 512;   // floats per accumulator slot
 constexpr int ADAPT_NP = 2 * (ADAPT_CB + 1);
 constexpr int ADAPT_PPW = (ADAPT_NP + 3) / 4;  // lo pixels per wave
 
@@ -135,6 +136,7 @@ struct AdaptStepArgs {
   float* acc_zero;       // slot [R][512] to zero for the next step (may be null)
   int h, w, S;
   float sy, sx;          // align_corners scales (h-1)/(S-1), (w-1)/(S-1)
+  int nrep;              // replica rows in use
   int dbg;               // ablation flags for timing studies only (CWT_ADAPT_DBG): 1 skip replica
                          // reads, 2 skip the high-res pass, 4 skip the global atomics, 8 skip f loads,
                          // 16 return at entry
@@ -210,7 +212,7 @@ constexpr int ADAPT_PPW16 = (ADAPT_NP + ADAPT_NW - 1) / ADAPT_NW;  // lo pixels 
 __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
   constexpr int C = 512;
   __shared__ float wl[2][C];
-  __shared__ float z[2][ADAPT_CB + 1][2];
+  __shared__ float zd[2][ADAPT_CB + 1];  // z1 - z0: the softmax over two classes needs only the difference
   __shared__ float gs[2][ADAPT_CB + 1];
   __shared__ float red[ADAPT_NW][C];
   if (a.dbg & 16) return;
@@ -264,8 +266,8 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
     f32x4 w1a = *(const f32x4*)(wsrc + C + lane * 8), w1b = *(const f32x4*)(wsrc + C + lane * 8 + 4);
     if (a.acc_prev && !(a.dbg & 1)) {
       f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int rr = 0; rr < ADAPT_R; ++rr) {
+#pragma unroll 4
+      for (int rr = 0; rr < a.nrep; ++rr) {
         d0 += *(const f32x4*)(a.acc_prev + rr * 512 + lane * 8);
         d1 += *(const f32x4*)(a.acc_prev + rr * 512 + lane * 8 + 4);
       }
@@ -286,36 +288,34 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
     }
   }
   if ((cb | r | n) == 0 && a.acc_zero)
-    for (int i = t; i < ADAPT_SLOT / 4; i += ADAPT_T) ((f32x4*)a.acc_zero)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = t; i < a.nrep * 128; i += ADAPT_T) ((f32x4*)a.acc_zero)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (t < ADAPT_NP) (&gs[0][0])[t] = 0.f;
   __syncthreads();
 
-  // ---- z = W . f for the tile's low-res pixels ----
+  // ---- zd = (W1 - W0) . f for the tile's low-res pixels ----
   {
-    float w0[8], w1[8];
+    float dw[8];
     const f32x4 a0 = *(const f32x4*)&wl[0][lane * 8], b0 = *(const f32x4*)&wl[0][lane * 8 + 4];
     const f32x4 a1 = *(const f32x4*)&wl[1][lane * 8], b1 = *(const f32x4*)&wl[1][lane * 8 + 4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      w0[q] = a0[q]; w0[4 + q] = b0[q];
-      w1[q] = a1[q]; w1[4 + q] = b1[q];
+      dw[q] = a1[q] - a0[q];
+      dw[4 + q] = b1[q] - b0[q];
     }
+    float sd[ADAPT_PPW16];
+#pragma unroll
+    for (int j = 0; j < ADAPT_PPW16; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s = fmaf(dw[q], fv[j][q], s);
+      sd[j] = s;
+    }
+#pragma unroll
+    for (int j = 0; j < ADAPT_PPW16; ++j) sd[j] = wave_sum_dpp(sd[j]);  // independent chains interleave
 #pragma unroll
     for (int j = 0; j < ADAPT_PPW16; ++j) {
       const int p = wv + ADAPT_NW * j;
-      if (p >= ADAPT_NP) break;  // wave-uniform
-      float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        s0 = fmaf(w0[q], fv[j][q], s0);
-        s1 = fmaf(w1[q], fv[j][q], s1);
-      }
-      s0 = wave_sum_dpp(s0);
-      s1 = wave_sum_dpp(s1);
-      if (lane == 0) {
-        (&z[0][0][0])[2 * p] = s0;
-        (&z[0][0][0])[2 * p + 1] = s1;
-      }
+      if (p < ADAPT_NP && lane == 0) (&zd[0][0])[p] = sd[j];
     }
   }
   __syncthreads();
@@ -340,15 +340,13 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
         const float ly1 = e ? 0.f : (float)(Y & 7) * 0.125f, ly0 = 1.f - ly1;
         float g = 0.f;
         if (xin && y != 255) {
-          const float2 z00 = *(const float2*)z[ri0][xi0], z01 = *(const float2*)z[ri0][xi1];
-          const float2 z10 = *(const float2*)z[ri1][xi0], z11 = *(const float2*)z[ri1][xi1];
-          const float l0 = ly0 * (lx0 * z00.x + lx1 * z01.x) + ly1 * (lx0 * z10.x + lx1 * z11.x);
-          const float l1 = ly0 * (lx0 * z00.y + lx1 * z01.y) + ly1 * (lx0 * z10.y + lx1 * z11.y);
-          const float p1 = 1.f / (1.f + __expf(l0 - l1));
+          const float d = ly0 * (lx0 * zd[ri0][xi0] + lx1 * zd[ri0][xi1]) + ly1 * (lx0 * zd[ri1][xi0] + lx1 * zd[ri1][xi1]);
+          const float p1 = 1.f / (1.f + __expf(-d));
           g = ((y == 1) ? wfg : 1.f) * (p1 - (float)y);
         }
-        float v00 = octet_sum(ly0 * lx0 * g), v01 = octet_sum(ly0 * lx1 * g);
-        float v10 = octet_sum(ly1 * lx0 * g), v11 = octet_sum(ly1 * lx1 * g);
+        // ly0 / ly1 are wave-uniform: reduce lx * g over the octet once, scale per row after
+        const float sa = octet_sum(lx0 * g), sb = octet_sum(lx1 * g);
+        const float v00 = ly0 * sa, v01 = ly0 * sb, v10 = ly1 * sa, v11 = ly1 * sb;
         if ((lane & 7) == 0 && xin) {
           if (e == 0) {
             atomicAdd(&gs[0][xi0], v00);
@@ -384,19 +382,19 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
     float s = 0.f;
 #pragma unroll
     for (int v = 0; v < ADAPT_NW; ++v) s += red[v][t];
-    atomicAdd(&a.acc_cur[((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) % ADAPT_R) * 512 + t], s);
+    atomicAdd(&a.acc_cur[((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) % a.nrep) * 512 + t], s);
   }
 }
 
 __global__ void adapt_final_kernel(const float* w_src, const float* acc, const AdaptScalars* sc,
-                                   const AdaptDevArgs* dargs) {
+                                   const AdaptDevArgs* dargs, int nrep) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= 512) return;
   float* w_out = dargs->w_out;
   const float lr = sc->lr_eff;
   float d = 0.f;
   if (acc)
-    for (int rr = 0; rr < ADAPT_R; ++rr) d += acc[rr * 512 + k];
+    for (int rr = 0; rr < nrep; ++rr) d += acc[rr * 512 + k];
   w_out[k] = w_src[k] + lr * d;
   w_out[512 + k] = w_src[512 + k] - lr * d;
 }
@@ -415,6 +413,9 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws,
   a.sx = align_corners_scale(w, S);
   const char* dbg = getenv("CWT_ADAPT_DBG");
   a.dbg = dbg ? atoi(dbg) : 0;
+  const char* nr = getenv("CWT_ADAPT_R");
+  a.nrep = nr ? atoi(nr) : ADAPT_R_DEFAULT;
+  if (a.nrep != 4 && a.nrep != 8 && a.nrep != 16 && a.nrep != 32) a.nrep = ADAPT_R_DEFAULT;
   const int ncb = cdiv(S - 1, 8 * ADAPT_CB);
   dim3 grid(ncb, h - 1, n);
   for (int s = 0; s < iters; ++s) {
@@ -428,7 +429,7 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws,
   }
   const int last = iters - 1;
   hipLaunchKernelGGL(adapt_final_kernel, dim3(2), dim3(256), 0, st, (const float*)(wbuf + (last & 1) * 1024),
-                     (const float*)(acc3 + (last % 3) * ADAPT_SLOT), sc, dargs);
+                     (const float*)(acc3 + (last % 3) * ADAPT_SLOT), sc, dargs, a.nrep);
   CWT_LAUNCH_CHECK();
   return 0;
 }

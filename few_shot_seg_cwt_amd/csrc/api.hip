@@ -755,7 +755,7 @@ int cwt_inner_adapt(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int 
   if ((rc = ensure_ws(ctx, "adapt.args", 64, &dargs))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.lbl", (size_t)n * S * S, &lbl))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.sc", 8192, &sc))) return rc;
-  if ((rc = ensure_ws(ctx, "adapt.acc", 3 * 16 * 512 * 4, &acc))) return rc;  // [3][ADAPT_R][512]
+  if ((rc = ensure_ws(ctx, "adapt.acc", 3 * 32 * 512 * 4, &acc))) return rc;  // [3][ADAPT_RMAX][512]
   if ((rc = ensure_ws(ctx, "adapt.wbuf", 2 * 1024 * 4, &wb))) return rc;
   // algorithmic work: per step 2 x (2*2*C*h*w*n) FLOPs; minimal bytes = f_s + labels once per step
   Prof p(ctx, (hipStream_t)stream, "inner_adapt x" + std::to_string(iters), (double)iters * 2.0 * (4.0 * C * h * w * n),
@@ -913,6 +913,32 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
   a.w_hi = (const __bf16*)hi;
   a.w_lo = (const __bf16*)lo;
   return launch_conv_x3(a, p, 0, (float*)part, pf, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+namespace cwt {
+// HW_REG_HW_ID (wave, SIMD, CU, SH, SE fields) and HW_REG_XCC_ID of each workgroup's first wave
+__global__ void census_kernel(unsigned* out) {
+  unsigned hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = hw;
+    out[2 * blockIdx.x + 1] = xcc;
+  }
+}
+}  // namespace cwt
+
+extern "C" {
+
+int cwt_debug_census(cwt_ctx* ctx, int nblocks, unsigned* out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(out && nblocks > 0, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(census_kernel, dim3(nblocks), dim3(64), 0, (hipStream_t)stream, out);
+  CWT_LAUNCH_CHECK();
+  return 0;
 }
 
 int cwt_debug_split_act(cwt_ctx* ctx, const float* x, int64_t P, int C, int ld, void* out, void* stream) {

@@ -84,12 +84,57 @@ __global__ __launch_bounds__(256) void stem_conv1_kernel(const float* __restrict
   }
 }
 
+// S-layout output: one thread per (pixel, 8 output channels); a wave covers 8 pixels and
+// writes them as 2 KB of contiguous lines (hi and lo chunks of each 32-channel block).
+__global__ __launch_bounds__(256) void stem_conv1_s_kernel(const float* __restrict__ img, int N, int S,
+                                                           const float* __restrict__ w,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           __bf16* __restrict__ out, int Ho) {
+  __shared__ float ws[27 * 64];
+  for (int i = threadIdx.x; i < 27 * 64; i += blockDim.x) ws[i] = w[i];
+  __syncthreads();
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)N * Ho * Ho * 8;
+  if (idx >= total) return;
+  const int g = (int)(idx & 7);
+  const long pix = idx >> 3;
+  const int n = (int)(pix / ((long)Ho * Ho));
+  const int rem = (int)(pix - (long)n * Ho * Ho);
+  const int oh = rem / Ho, ow = rem - (rem / Ho) * Ho;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ih = oh * 2 - 1 + ky, iw = ow * 2 - 1 + kx;
+        float v = 0.f;
+        if ((unsigned)ih < (unsigned)S && (unsigned)iw < (unsigned)S) v = img[(((long)n * 3 + ci) * S + ih) * S + iw];
+        const int k = ci * 9 + ky * 3 + kx;
+        a0 += v * *(const f32x4*)&ws[k * 64 + g * 8];
+        a1 += v * *(const f32x4*)&ws[k * 64 + g * 8 + 4];
+      }
+  bf16x8 hi, lo;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int c = g * 8 + q;
+    const float r = fmaxf(fmaf(q < 4 ? a0[q & 3] : a1[q & 3], scale[c], shift[c]), 0.f);
+    hi[q] = (__bf16)r;
+    lo[q] = (__bf16)(r - (float)hi[q]);
+  }
+  __bf16* sp = out + pix * 128 + (g >> 2) * 64 + (g & 3) * 8;
+  *(bf16x8*)sp = hi;
+  *(bf16x8*)(sp + 32) = lo;
+}
+
 int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const float* scale,
                       const float* shift, float* out, int Ho, hipStream_t st, bool split) {
   long total = (long)N * Ho * Ho;
   if (split)
-    hipLaunchKernelGGL(stem_conv1_kernel<true>, dim3(cdiv(total, 256)), dim3(256), 0, st, img, N, S, w27x64, scale,
-                       shift, out, Ho);
+    hipLaunchKernelGGL(stem_conv1_s_kernel, dim3(cdiv(total * 8, 256)), dim3(256), 0, st, img, N, S, w27x64, scale,
+                       shift, (__bf16*)out, Ho);
   else
     hipLaunchKernelGGL(stem_conv1_kernel<false>, dim3(cdiv(total, 256)), dim3(256), 0, st, img, N, S, w27x64, scale,
                        shift, out, Ho);

@@ -61,23 +61,40 @@ __device__ __forceinline__ void block_sync_lds() {
   asm volatile("" ::: "memory");
 }
 
+// Residual of 8 consecutive channels [co, co + 8) of output row m (0 without a residual).
+struct Res8 {
+  f32x4 a, b;  // fp32 residual, or the S-layout hi / lo halves reinterpreted
+};
+__device__ __forceinline__ Res8 load_res8(const ConvSArgs& a, int m, int co) {
+  Res8 r;
+  if (a.res) {
+    const f32x4* rp = (const f32x4*)(a.res + (long)m * a.res_ld + co);
+    r.a = rp[0];
+    r.b = rp[1];
+  } else if (a.res_s) {
+    const __bf16* rp = a.res_s + ((long)m * (a.Co >> 5) + (co >> 5)) * 64 + (co & 31);
+    r.a = *(const f32x4*)rp;
+    r.b = *(const f32x4*)(rp + 32);
+  } else {
+    r.a = r.b = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  return r;
+}
+
 // 8 consecutive channels [co, co + 8) of output row m: BN, residual, ReLU, stores.
 __device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, const float* v, const float* sc,
-                                           const float* sh) {
+                                           const float* sh, const Res8& rs) {
   float o[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) o[i] = fmaf(v[i], sc[i], sh[i]);
   if (a.res) {
-    const f32x4* rp = (const f32x4*)(a.res + (long)m * a.res_ld + co);
-    const f32x4 r0 = rp[0], r1 = rp[1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      o[i] += r0[i];
-      o[4 + i] += r1[i];
+      o[i] += rs.a[i];
+      o[4 + i] += rs.b[i];
     }
   } else if (a.res_s) {
-    const __bf16* rp = a.res_s + ((long)m * (a.Co >> 5) + (co >> 5)) * 64 + (co & 31);
-    const bf16x8 rh = *(const bf16x8*)rp, rl = *(const bf16x8*)(rp + 32);
+    const bf16x8 rh = __builtin_bit_cast(bf16x8, rs.a), rl = __builtin_bit_cast(bf16x8, rs.b);
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] += (float)rh[i] + (float)rl[i];
   }
@@ -254,8 +271,16 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
     sh[i] = a.part ? 0.f : a.shift[co + i];
   }
   const int fq = lane >> 4;
+  constexpr int NPASS = WM / EP_ROWS, RR = EP_ROWS / RPR;
+  const int mrow = m0 + wm * WM + er;  // output row of round rr of pass p: mrow + p*EP_ROWS + rr*RPR
+  // residuals of pass p+1 are loaded while pass p is stored (double buffer; rows past M clamp)
+  Res8 resb[2][RR];
+  const bool fused = !a.part;
 #pragma unroll
-  for (int pass = 0; pass < WM / EP_ROWS; ++pass) {
+  for (int rr = 0; rr < RR; ++rr)
+    if (fused) resb[0][rr] = load_res8(a, min(mrow + rr * RPR, a.M - 1), co);
+#pragma unroll
+  for (int pass = 0; pass < NPASS; ++pass) {
 #pragma unroll
     for (int fi = 0; fi < EP_ROWS / 16; ++fi)
 #pragma unroll
@@ -263,20 +288,29 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
 #pragma unroll
         for (int q = 0; q < 4; ++q) ep[(fi * 16 + fq * 4 + q) * EP_LD + j * 16 + fr] = acc[pass * (EP_ROWS / 16) + fi][j][q];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    f32x4 v0[RR], v1[RR];
 #pragma unroll
-    for (int rr = 0; rr < EP_ROWS / RPR; ++rr) {
+    for (int rr = 0; rr < RR; ++rr) {
       const int r = rr * RPR + er;
-      const int m = m0 + wm * WM + pass * EP_ROWS + r;
-      const f32x4 v0 = *(const f32x4*)(ep + r * EP_LD + eg * 8);
-      const f32x4 v1 = *(const f32x4*)(ep + r * EP_LD + eg * 8 + 4);
+      v0[rr] = *(const f32x4*)(ep + r * EP_LD + eg * 8);
+      v1[rr] = *(const f32x4*)(ep + r * EP_LD + eg * 8 + 4);
+    }
+    if (pass + 1 < NPASS && fused) {
+#pragma unroll
+      for (int rr = 0; rr < RR; ++rr)
+        resb[(pass + 1) & 1][rr] = load_res8(a, min(mrow + (pass + 1) * EP_ROWS + rr * RPR, a.M - 1), co);
+    }
+#pragma unroll
+    for (int rr = 0; rr < RR; ++rr) {
+      const int m = mrow + pass * EP_ROWS + rr * RPR;
       if (m < a.M) {
-        if (a.part) {
+        if (!fused) {
           f32x4* pp = (f32x4*)(a.part + ((long)ks * a.M + m) * a.Co + co);
-          pp[0] = v0;
-          pp[1] = v1;
+          pp[0] = v0[rr];
+          pp[1] = v1[rr];
         } else {
-          const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          store_out8(a, m, co, v, sc, sh);
+          const float v[8] = {v0[rr][0], v0[rr][1], v0[rr][2], v0[rr][3], v1[rr][0], v1[rr][1], v1[rr][2], v1[rr][3]};
+          store_out8(a, m, co, v, sc, sh, resb[pass & 1][rr]);
         }
       }
     }
@@ -320,7 +354,7 @@ __global__ void conv_s_splitk_epilogue(ConvSArgs a, int nsplit) {
     sc[i] = a.scale[co + i];
     sh[i] = a.shift[co + i];
   }
-  store_out8(a, m, co, v, sc, sh);
+  store_out8(a, m, co, v, sc, sh, load_res8(a, m, co));
 }
 
 // fp32 [P][C] (pixel stride ld) -> S-layout [P][C/32][64]

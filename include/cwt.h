@@ -217,6 +217,10 @@ int cwt_debug_conv_s(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci
                      int dil, const float* res, int res_ld, const void* res_s, int relu, float* y,
                      int y_ld, int y_off, void* ys, int bm, int bn, int nsplit, void* stream);
 
+/* Test hook: per workgroup of a 64-thread grid, the raw HW_REG_HW_ID and HW_REG_XCC_ID of the
+ * CU it ran on (out[2*b], out[2*b+1]); with a CU-masked stream this maps mask bits to CUs. */
+int cwt_debug_census(cwt_ctx* ctx, int nblocks, unsigned* out, void* stream);
+
 /*
  * CU-partitioned streams (MI355X-native episode pipelining): a HIP stream
  * whose kernels (including replays of graphs launched on it) only run on the CUs whose bits

@@ -22,8 +22,8 @@ e1.record(); torch.cuda.synchronize()
 print(e0.elapsed_time(e1) / 10 / 200 * 1e3)
 ''' % ROOT
 out = {}
-for n in (1, 5):
-    for flags in (0, 1, 2, 4, 8, 15, 16):
+for n in [int(x) for x in os.environ.get("SHOTS", "1,5").split(",")]:
+    for flags in [int(x) for x in os.environ.get("FLAGS", "0,1,2,4,8,15,16").split(",")]:
         env = dict(os.environ, CWT_ADAPT_DBG=str(flags))
         r = subprocess.run([sys.executable, "-c", CODE, str(n)], env=env, capture_output=True, text=True, timeout=300)
         us = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else "ERR " + r.stderr[-300:]
