@@ -225,6 +225,35 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
   const int off_lo = fr * 128 + (((4 + fk) ^ swz) << 4);
   const int a_row0 = wm * WM, b_row0 = BM + wn * WN;
 
+  struct Frags {
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+  };
+  auto read_frags = [&](Frags& F, int stg) {
+    const char* sb = smem + stg * STG_BYTES;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const char* p = sb + (b_row0 + j * 16) * 128;
+      F.bh[j] = *(const bf16x8*)(p + off_hi);
+      F.bl[j] = *(const bf16x8*)(p + off_lo);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const char* p = sb + (a_row0 + i * 16) * 128;
+      F.ah[i] = *(const bf16x8*)(p + off_hi);
+      F.al[i] = *(const bf16x8*)(p + off_lo);
+    }
+  };
+  auto mfmas = [&](const Frags& F) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.al[i], F.bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.ah[i], F.bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.ah[i], F.bh[j], acc[i][j], 0, 0, 0);
+      }
+  };
+
 #pragma unroll
   for (int s = 0; s < NSTG - 1; ++s)
     if (s < T) issue(s);
@@ -233,26 +262,9 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
     wait_tiles<LPT>(min(NSTG - 2, T - 1 - t));
     block_sync_lds();
     if (t + NSTG - 1 < T) issue((t + NSTG - 1) % NSTG);
-    const char* sb = smem + (t % NSTG) * STG_BYTES;
-    bf16x8 bh[FN], bl[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const char* p = sb + (b_row0 + j * 16) * 128;
-      bh[j] = *(const bf16x8*)(p + off_hi);
-      bl[j] = *(const bf16x8*)(p + off_lo);
-    }
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const char* p = sb + (a_row0 + i * 16) * 128;
-      const bf16x8 ah = *(const bf16x8*)(p + off_hi);
-      const bf16x8 al = *(const bf16x8*)(p + off_lo);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
-      }
-    }
+    Frags F;
+    read_frags(F, t % NSTG);
+    mfmas(F);
   }
 
   // ---- epilogue through a per-wave LDS tile ----
