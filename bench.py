@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--layers", type=int, default=50)
     ap.add_argument("--size", type=int, default=473)
     ap.add_argument("--pool", type=int, default=4, help="distinct resident episodes cycled through")
+    ap.add_argument("--conv-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="conv-stack arithmetic: fp32 (reference numerics) or bf16 (config #5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-json", default=None, help="write per-launch records here (rank 0)")
     args = ap.parse_args()
@@ -98,7 +100,7 @@ def main():
 
     _lib.load_library()
     S, shot, layers = args.size, args.shot, args.layers
-    cfg = syn.cfg_defaults(image_size=S, shot=shot, layers=layers)
+    cfg = syn.cfg_defaults(image_size=S, shot=shot, layers=layers, conv_dtype=args.conv_dtype)
     seed = 2021
     sd = syn.make_pspnet_state(layers, seed)
     tsd = syn.make_transformer_state(4, 512, seed)
@@ -155,9 +157,12 @@ def main():
     dom_name = dom[0][0].split(" ")[0] if dom else "n/a"
     dn, dfl, dms = len(dom), sum(r[1] for r in dom), sum(r[3] for r in dom)
     conv_x3 = dom_name.startswith("conv_igemm_bf16x3") or dom_name.startswith("conv_igemm_x3s")
+    conv_b16 = dom_name.startswith("conv_igemm_b16")
     achieved = (dfl / dn) / (dms / dn * 1e-3) / 1e12
     if conv_x3:   # fp32 GEMM done as 3 bf16 MFMA products: the roof is the dense bf16 rate / 3
         peak, peak_basis = round(PEAK_BF16_MFMA_TFLOPS / 3, 1), "bf16x3: 2516.6 TF dense bf16 MFMA / 3 products"
+    elif conv_b16:
+        peak, peak_basis = PEAK_BF16_MFMA_TFLOPS, "dense bf16 MFMA 2516.6 TF"
     else:
         peak, peak_basis = PEAK_FP32_MFMA_TFLOPS, "fp32 MFMA 157.3 TF"
 
@@ -171,8 +176,9 @@ def main():
     _lib.profile_enable(0)
 
     out = {
-        "metric": "episodes/sec (473x473, 1-shot, R50) at 1/2/4/8 MI355X; mIoU vs ref"
-        if (S, shot, layers) == (473, 1, 50) else f"episodes/sec ({S}x{S}, {shot}-shot, R{layers})",
+        "metric": ("episodes/sec (473x473, 1-shot, R50) at 1/2/4/8 MI355X; mIoU vs ref"
+                   if (S, shot, layers) == (473, 1, 50) else f"episodes/sec ({S}x{S}, {shot}-shot, R{layers})")
+        + (" [bf16 conv stack]" if args.conv_dtype == "bf16" else ""),
         "value": round(value, 3),
         "unit": "episodes/s",
         "n_gpus": world,
@@ -182,7 +188,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32 (conv stack: bf16x3 split-fp32 on bf16 MFMA)" if conv_x3 else "fp32",
+        "dtype": "fp32 (conv stack: bf16x3 split-fp32 on bf16 MFMA)" if conv_x3
+        else "bf16 conv stack (fp32 accumulate) + fp32 inner loop / CWT / classifier" if conv_b16 else "fp32",
         "data": "synthetic (PRNG weights + PASCAL-shaped episodes, few_shot_seg_cwt_amd/synthetic.py)",
         "config": {"workload": f"CWT inference episode (validate_transformer, batch_size_val=1): "
                                f"{'PASCAL split-0' if layers == 50 else 'COCO-20i split-0'} {shot}-shot "

@@ -29,6 +29,7 @@ SIGNATURES = {
     "cwt_backbone_load": (_I, [_P, _I, _I, C.POINTER(C.c_char_p), C.POINTER(_P), C.POINTER(_I64), _F,
                                C.POINTER(_P)]),
     "cwt_backbone_destroy": (_I, [_P]),
+    "cwt_backbone_set_precision": (_I, [_P, _I]),
     "cwt_extract_features": (_I, [_P, _P, _P, _I, _I, _P, _P]),
     "cwt_workspace_bytes": (C.c_size_t, [_P]),
     "cwt_inner_adapt": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
@@ -52,6 +53,8 @@ SIGNATURES = {
     "cwt_debug_pack_wsplit": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "cwt_debug_conv_s": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _I,
                               _P, _I, _I, _I, _P]),
+    "cwt_debug_conv_b16": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _I,
+                                _P, _I, _I, _I, _P]),
     "cwt_debug_census": (_I, [_P, _I, _P, _P]),
     "cwt_profile_enable": (_I, [_P, _I]),
     "cwt_profile_count": (_I, [_P]),

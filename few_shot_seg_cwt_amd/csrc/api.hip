@@ -59,6 +59,7 @@ struct ConvLayer {
   __bf16* w_hi = nullptr;  // bf16x3 split of w (same layout); null for the stem conv1
   __bf16* w_lo = nullptr;
   __bf16* w_s = nullptr;   // S-layout [Co][K/32][hi 32 | lo 32] of the same split (conv_x3s.hip)
+  __bf16* w_b = nullptr;   // plain bf16 [Co][K], K in packed_k64 order (bf16 conv stack; Ci % 64 == 0)
   float* scale = nullptr;
   float* shift = nullptr;
 };
@@ -71,6 +72,7 @@ struct Block {
 struct Backbone {  // the opaque cwt_backbone of the C ABI
   int layers = 0;
   int device = 0;
+  int precision = CWT_CONV_FP32;  // cwt_backbone_set_precision
   ConvLayer stem[3];
   std::vector<Block> blocks[4];
   ConvLayer ppm[4];     // PPM 1x1 convs (scale/shift used; weights below)
@@ -278,6 +280,14 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
           sl[dst + 32] = lo[src];
         }
     if ((rc = upload_u16(bb, sl, &L->w_s))) return rc;
+    if (Ci % 64 == 0) {  // plain bf16 operand of the bf16 conv stack, K in packed_k64 order
+      std::vector<uint16_t> b16(packed.size());
+      for (int co = 0; co < Co; ++co)
+        for (int ci = 0; ci < Ci; ++ci)
+          for (int tap = 0; tap < k * k; ++tap)
+            b16[(size_t)co * K + packed_k64(ci, tap, k * k)] = hi[(size_t)co * K + packed_k(ci, tap, k * k)];
+      if ((rc = upload_u16(bb, b16, &L->w_b))) return rc;
+    }
   }
   if ((rc = upload(bb, sc, &L->scale))) return rc;
   if ((rc = upload(bb, sh, &L->shift))) return rc;
@@ -439,6 +449,12 @@ static ConvArgs make_args(const ConvCall& c) {
 // The whole extractor as a list of conv calls + byte kernels.  dry_run sizes the split-K workspace.
 static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N, int S, float* feat,
                        hipStream_t st) {
+  // conv arithmetic / activation storage: plain bf16 (cwt_backbone_set_precision), else the
+  // context's fp32-accurate mode (S-layout bf16x3 by default)
+  const bool b16 = bb->precision == CWT_CONV_BF16;
+  const bool s_path = b16 || ctx->conv_split;  // conv_x3s.hip kernels
+  const int layout = b16 ? ACT_BF16 : ctx->conv_split ? ACT_SPLIT : ACT_F32;
+  const int prec = b16 ? 1 : 3;
   const int Hs = down2(S), H1 = down2(Hs), h = down2(H1);
   const long sA = std::max({(long)N * Hs * Hs * 128, (long)N * H1 * H1 * 256, (long)N * h * h * 2048});
   const long sT1 = std::max((long)N * H1 * H1 * 128, (long)N * h * h * 512);
@@ -528,14 +544,16 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   std::vector<ConvPlan> plans;
   for (auto& c : calls) {
     ConvArgs a = make_args(c);
-    ConvPlan pl = ctx->conv_split ? plan_conv_x3s(a.M, a.Co, a.K)
-                  : ctx->conv_x3  ? plan_conv_x3(a.M, a.Co, a.K)
-                                  : plan_conv(a.M, a.Co, a.K);
+    if (b16 && !c.L->w_b) return fail(CWT_ESTATE, "bf16 conv weights missing (Ci % 64 != 0)");
+    ConvPlan pl = b16              ? plan_conv_b16(a.M, a.Co, a.K)
+                  : ctx->conv_split ? plan_conv_x3s(a.M, a.Co, a.K)
+                  : ctx->conv_x3    ? plan_conv_x3(a.M, a.Co, a.K)
+                                    : plan_conv(a.M, a.Co, a.K);
     plans.push_back(pl);
     if (pl.nsplit > 1) part_floats = std::max(part_floats, (size_t)pl.nsplit * a.M * a.Co);
   }
   const __bf16* zero = nullptr;
-  if (ctx->conv_split && (rc = zero_line(ctx, &zero))) return rc;
+  if (s_path && (rc = zero_line(ctx, &zero))) return rc;
   float* PART = nullptr;
   if (part_floats) {
     if ((rc = ensure_ws(ctx, "bb.PART", part_floats * 4, &p))) return rc;
@@ -548,7 +566,8 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     const double bytes = 4.0 * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K + (double)a.M * a.Co +
                                 (a.res ? (double)a.M * a.Co : 0.0));
     Prof p(ctx, st,
-           std::string(ctx->conv_split ? "conv_igemm_x3s<" : ctx->conv_x3 ? "conv_igemm_bf16x3<" : "conv_igemm_f32<") +
+           std::string(b16 ? "conv_igemm_b16<" : ctx->conv_split ? "conv_igemm_x3s<" : ctx->conv_x3 ? "conv_igemm_bf16x3<"
+                                                                                                     : "conv_igemm_f32<") +
                std::to_string(pl.bm) + "," +
                std::to_string(pl.bn) + "," +
                std::to_string(calls[i].stage) + ">" +
@@ -557,12 +576,12 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
                std::to_string(a.stride) + "d" + std::to_string(a.dil) + "@" + std::to_string(a.Ho),
            flops, bytes, calls[i].stage == 6 ? 1 : 2);
     int r;
-    if (ctx->conv_split) {
+    if (s_path) {
       ConvSArgs sa;
       memset(&sa, 0, sizeof(sa));
       const ConvCall& c = calls[i];
       sa.xs = (const __bf16*)c.x;
-      sa.ws = c.L->w_s;
+      sa.ws = b16 ? c.L->w_b : c.L->w_s;
       sa.zero = zero;
       sa.scale = a.scale;
       sa.shift = a.shift;
@@ -591,7 +610,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
       sa.dil = a.dil;
       sa.M = a.M;
       sa.K = a.K;
-      r = launch_conv_x3s(sa, pl, c.stage, PART, part_floats, st);
+      r = launch_conv_x3s(sa, pl, c.stage, PART, part_floats, st, prec);
     } else {
       r = ctx->conv_x3 ? launch_conv_x3(a, pl, calls[i].stage, PART, part_floats, st)
                        : launch_conv(a, pl, calls[i].stage, PART, part_floats, st);
@@ -613,7 +632,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   {
     Prof p(ctx, st, "stem_conv1 3x64k3s2", 2.0 * N * Hs * Hs * 64 * 27, 4.0 * ((double)N * 3 * S * S + (double)N * Hs * Hs * 64));
     if ((rc = launch_stem_conv1(img, N, S, bb->stem[0].w, bb->stem[0].scale, bb->stem[0].shift, A, Hs, st,
-                                ctx->conv_split)))
+                                layout)))
       return rc;
     p.end();
   }
@@ -621,8 +640,9 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     if ((rc = run_call(i))) return rc;
   {
     Prof p(ctx, st, "maxpool3s2", 0.0, 4.0 * ((double)N * Hs * Hs * 128 + (double)N * H1 * H1 * 128));
-    if ((rc = ctx->conv_split ? launch_maxpool3s2_s((const __bf16*)A, N, Hs, Hs, 128, (__bf16*)B, H1, H1, st)
-                              : launch_maxpool3s2(A, N, Hs, Hs, 128, B, H1, H1, st)))
+    if ((rc = layout == ACT_BF16    ? launch_maxpool3s2_b16((const __bf16*)A, N, Hs, Hs, 128, (__bf16*)B, H1, H1, st)
+              : layout == ACT_SPLIT ? launch_maxpool3s2_s((const __bf16*)A, N, Hs, Hs, 128, (__bf16*)B, H1, H1, st)
+                                    : launch_maxpool3s2(A, N, Hs, Hs, 128, B, H1, H1, st)))
       return rc;
     p.end();
   }
@@ -630,7 +650,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     if ((rc = run_call(i))) return rc;
   {
     Prof p(ctx, st, "ppm_pool", 0.0, 4.0 * ((double)N * h * h * 2048 + (double)N * 50 * 2048));
-    if ((rc = launch_ppm(L4, N, h, h, 2048, kBins, 4, COL, POOL, st, ctx->conv_split))) return rc;
+    if ((rc = launch_ppm(L4, N, h, h, 2048, kBins, 4, COL, POOL, st, layout))) return rc;
     p.end();
   }
   int Mb[4];
@@ -725,6 +745,15 @@ int cwt_backbone_destroy(cwt_backbone* handle) {
   (void)hipDeviceSynchronize();
   for (void* p : bb->allocs) (void)hipFree(p);
   delete bb;
+  return 0;
+}
+
+int cwt_backbone_set_precision(cwt_backbone* handle, int precision) {
+  Backbone* bb = reinterpret_cast<Backbone*>(handle);
+  if (!bb) return fail(CWT_EARG, "backbone is NULL");
+  if (precision != CWT_CONV_FP32 && precision != CWT_CONV_BF16)
+    return fail(CWT_EARG, "precision must be CWT_CONV_FP32 (0) or CWT_CONV_BF16 (1)");
+  bb->precision = precision;
   return 0;
 }
 
@@ -967,13 +996,16 @@ int cwt_debug_pack_wsplit(cwt_ctx* ctx, const float* w, int Co, int k, int Ci, v
   return launch_split_act((const float*)wp, Co, (int)K, (int)K, (__bf16*)out, (hipStream_t)stream);
 }
 
-int cwt_debug_conv_s(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws, const float* scale,
-                     const float* shift, int Co, int k, int stride, int pad, int dil, const float* res, int res_ld,
-                     const void* res_s, int relu, float* y, int y_ld, int y_off, void* ys, int bm, int bn, int nsplit,
-                     void* stream) {
+}  // extern "C"
+
+static int debug_conv_s(cwt_ctx* ctx, int prec, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws,
+                        const float* scale, const float* shift, int Co, int k, int stride, int pad, int dil,
+                        const float* res, int res_ld, const void* res_s, int relu, float* y, int y_ld, int y_off,
+                        void* ys, int bm, int bn, int nsplit, void* stream) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
   CWT_CHECK(xs && ws && scale && shift && (y || ys), "null buffer");
-  CWT_CHECK(Ci % 32 == 0 && Co % 64 == 0, "need Ci%32==0, Co%64==0");
+  const int kb = prec == 1 ? 64 : 32;
+  CWT_CHECK(Ci % kb == 0 && Co % 64 == 0, prec == 1 ? "need Ci%64==0, Co%64==0" : "need Ci%32==0, Co%64==0");
   CWT_CHECK(!y || (y_ld >= y_off + Co && y_ld % 4 == 0 && y_off % 4 == 0), "bad y stride");
   CWT_HIP(hipSetDevice(ctx->device));
   ConvSArgs a;
@@ -1005,7 +1037,7 @@ int cwt_debug_conv_s(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci
   a.Wo = (Wi + 2 * pad - dil * (k - 1) - 1) / stride + 1;
   a.M = N * a.Ho * a.Wo;
   a.K = k * k * Ci;
-  ConvPlan p = plan_conv_x3s(a.M, a.Co, a.K);
+  ConvPlan p = prec == 1 ? plan_conv_b16(a.M, a.Co, a.K) : plan_conv_x3s(a.M, a.Co, a.K);
   if (bm > 0) {
     CWT_CHECK((bm == 256 && (bn == 256 || bn == 128)) || (bm == 128 && (bn == 128 || bn == 64)) ||
                   (bm == 64 && (bn == 128 || bn == 64)),
@@ -1015,14 +1047,32 @@ int cwt_debug_conv_s(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci
     p.bn = bn;
   }
   if (nsplit > 0) {
-    const int kt = a.K / 32;
+    const int kt = a.K / kb;
     p.kt_per_split = cdiv(kt, nsplit);
     p.nsplit = cdiv(kt, p.kt_per_split);
   }
   void* part = nullptr;
   const size_t pf = (size_t)p.nsplit * a.M * a.Co;
   if (p.nsplit > 1 && (rc = ensure_ws(ctx, "dbg.PART", pf * 4, &part))) return rc;
-  return launch_conv_x3s(a, p, 0, (float*)part, pf, (hipStream_t)stream);
+  return launch_conv_x3s(a, p, 0, (float*)part, pf, (hipStream_t)stream, prec);
+}
+
+extern "C" {
+
+int cwt_debug_conv_s(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws, const float* scale,
+                     const float* shift, int Co, int k, int stride, int pad, int dil, const float* res, int res_ld,
+                     const void* res_s, int relu, float* y, int y_ld, int y_off, void* ys, int bm, int bn, int nsplit,
+                     void* stream) {
+  return debug_conv_s(ctx, 3, xs, N, Hi, Wi, Ci, ws, scale, shift, Co, k, stride, pad, dil, res, res_ld, res_s, relu, y,
+                      y_ld, y_off, ys, bm, bn, nsplit, stream);
+}
+
+int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws, const float* scale,
+                       const float* shift, int Co, int k, int stride, int pad, int dil, const float* res, int res_ld,
+                       const void* res_s, int relu, float* y, int y_ld, int y_off, void* ys, int bm, int bn,
+                       int nsplit, void* stream) {
+  return debug_conv_s(ctx, 1, xs, N, Hi, Wi, Ci, ws, scale, shift, Co, k, stride, pad, dil, res, res_ld, res_s, relu, y,
+                      y_ld, y_off, ys, bm, bn, nsplit, stream);
 }
 
 int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int64_t n, int num_classes,

@@ -86,6 +86,8 @@ __global__ __launch_bounds__(256) void stem_conv1_kernel(const float* __restrict
 
 // S-layout output: one thread per (pixel, 8 output channels); a wave covers 8 pixels and
 // writes them as 2 KB of contiguous lines (hi and lo chunks of each 32-channel block).
+// BF16: the same with plain bf16 NHWC output (1 KB of contiguous lines per wave).
+template <bool BF16>
 __global__ __launch_bounds__(256) void stem_conv1_s_kernel(const float* __restrict__ img, int N, int S,
                                                            const float* __restrict__ w,
                                                            const float* __restrict__ scale,
@@ -124,17 +126,24 @@ __global__ __launch_bounds__(256) void stem_conv1_s_kernel(const float* __restri
     hi[q] = (__bf16)r;
     lo[q] = (__bf16)(r - (float)hi[q]);
   }
-  __bf16* sp = out + pix * 128 + (g >> 2) * 64 + (g & 3) * 8;
-  *(bf16x8*)sp = hi;
-  *(bf16x8*)(sp + 32) = lo;
+  if (BF16) {
+    *(bf16x8*)(out + pix * 64 + g * 8) = hi;
+  } else {
+    __bf16* sp = out + pix * 128 + (g >> 2) * 64 + (g & 3) * 8;
+    *(bf16x8*)sp = hi;
+    *(bf16x8*)(sp + 32) = lo;
+  }
 }
 
 int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const float* scale,
-                      const float* shift, float* out, int Ho, hipStream_t st, bool split) {
+                      const float* shift, float* out, int Ho, hipStream_t st, int layout) {
   long total = (long)N * Ho * Ho;
-  if (split)
-    hipLaunchKernelGGL(stem_conv1_s_kernel, dim3(cdiv(total * 8, 256)), dim3(256), 0, st, img, N, S, w27x64, scale,
-                       shift, (__bf16*)out, Ho);
+  if (layout == ACT_SPLIT)
+    hipLaunchKernelGGL(stem_conv1_s_kernel<false>, dim3(cdiv(total * 8, 256)), dim3(256), 0, st, img, N, S, w27x64,
+                       scale, shift, (__bf16*)out, Ho);
+  else if (layout == ACT_BF16)
+    hipLaunchKernelGGL(stem_conv1_s_kernel<true>, dim3(cdiv(total * 8, 256)), dim3(256), 0, st, img, N, S, w27x64,
+                       scale, shift, (__bf16*)out, Ho);
   else
     hipLaunchKernelGGL(stem_conv1_kernel<false>, dim3(cdiv(total, 256)), dim3(256), 0, st, img, N, S, w27x64, scale,
                        shift, out, Ho);
@@ -228,6 +237,49 @@ int launch_maxpool3s2_s(const __bf16* in, int N, int H, int W, int C, __bf16* ou
   return 0;
 }
 
+// maxpool 3x3 s2 p1 on bf16 NHWC: one thread per (pixel, 8 channels); max is exact in bf16.
+__global__ void maxpool3s2_b16_kernel(const __bf16* __restrict__ in, int N, int H, int W, int C,
+                                      __bf16* __restrict__ out, int Ho, int Wo) {
+  const int g8 = C >> 3;
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)N * Ho * Wo * g8;
+  if (idx >= total) return;
+  const int g = (int)(idx % g8);
+  const long pix = idx / g8;
+  const int ow = (int)(pix % Wo);
+  const int oh = (int)((pix / Wo) % Ho);
+  const int n = (int)(pix / ((long)Wo * Ho));
+  float m[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) m[q] = -INFINITY;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    int ih = oh * 2 - 1 + ky;
+    if ((unsigned)ih >= (unsigned)H) continue;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      int iw = ow * 2 - 1 + kx;
+      if ((unsigned)iw >= (unsigned)W) continue;
+      const bf16x8 v = *(const bf16x8*)(in + (((long)n * H + ih) * W + iw) * C + g * 8);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], (float)v[q]);
+    }
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = (__bf16)m[q];
+  *(bf16x8*)(out + pix * C + g * 8) = o;
+}
+
+int launch_maxpool3s2_b16(const __bf16* in, int N, int H, int W, int C, __bf16* out, int Ho, int Wo,
+                          hipStream_t st) {
+  if (C % 8) return fail(CWT_EARG, "maxpool_b16: C % 8");
+  long total = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool3s2_b16_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, in, N, H, W, C, out, Ho, Wo);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 // Adaptive average pooling for all bins (pspnet.py:26), in three passes that each issue at
 // most ~14 independent loads per thread:
 //   segment boundaries = every window start / end along an axis (the windows of all bins
@@ -271,10 +323,12 @@ static PPMSegs make_segs(int in, const int* bins, int nbins) {
 
 constexpr int PPM_MAXSEG = 16;  // longest elementary segment handled without a loop
 
-// SPLIT: x is the S-layout (pixel stride 2*C bf16; value = hi + lo), else fp32 (stride ld).
-template <bool SPLIT>
+// LAYOUT: ACT_SPLIT = x is the S-layout (pixel stride 2*C bf16; value = hi + lo), ACT_BF16 =
+// bf16 NHWC (pixel stride C), ACT_F32 = fp32 (pixel stride ld).
+template <int LAYOUT>
 __global__ void ppm_rowseg_kernel(const float* __restrict__ x, int N, int h, int w, int ld, int C, PPMSegs sx,
                                   float* __restrict__ rowseg) {
+  constexpr bool SPLIT = LAYOUT == ACT_SPLIT;
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)N * h * sx.nseg * C;
   if (idx >= total) return;
@@ -285,6 +339,7 @@ __global__ void ppm_rowseg_kernel(const float* __restrict__ x, int N, int h, int
   const int x0 = sx.b[xs], len = sx.b[xs + 1] - x0;
   const float* src = x + (ny * w + x0) * (long)ld + c;
   const __bf16* ssrc = (const __bf16*)x + (ny * w + x0) * (2L * C) + (c >> 5) * 64 + (c & 31);
+  const __bf16* bsrc = (const __bf16*)x + (ny * w + x0) * (long)C + c;
   float s = 0.f;
   for (int u0 = 0; u0 < len; u0 += PPM_MAXSEG) {
     float v[PPM_MAXSEG];
@@ -293,6 +348,8 @@ __global__ void ppm_rowseg_kernel(const float* __restrict__ x, int N, int h, int
       const long o = (long)min(u0 + u, len - 1);
       if (SPLIT)
         v[u] = (float)ssrc[o * 2 * C] + (float)ssrc[o * 2 * C + 32];
+      else if (LAYOUT == ACT_BF16)
+        v[u] = (float)bsrc[o * C];
       else
         v[u] = src[o * ld];
     }
@@ -366,7 +423,7 @@ __global__ void ppm_cell_kernel(const float* __restrict__ blk, int N, int C, PPM
 
 // ws: rowseg [N][h][nseg_x][C] followed by blk [N][nseg_y][nseg_x][C]
 int launch_ppm(const float* x, int N, int h, int w, int ld, const int* bins, int nbins, float* ws,
-               float* pooled, hipStream_t st, bool split) {
+               float* pooled, hipStream_t st, int layout) {
   if (nbins != 4) return fail(CWT_EARG, "PPM expects 4 bins");
   const PPMSegs sx = make_segs(w, bins, nbins), sy = make_segs(h, bins, nbins);
   if (sx.nwin > 16 || sx.nseg > 16 || sy.nseg > 16) return fail(CWT_EARG, "PPM: too many windows");
@@ -374,10 +431,14 @@ int launch_ppm(const float* x, int N, int h, int w, int ld, const int* bins, int
   float* rowseg = ws;
   float* blk = ws + (long)N * h * sx.nseg * C;
   const long t1 = (long)N * h * sx.nseg * C;
-  if (split)
-    hipLaunchKernelGGL(ppm_rowseg_kernel<true>, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx, rowseg);
+  if (layout == ACT_SPLIT)
+    hipLaunchKernelGGL(ppm_rowseg_kernel<ACT_SPLIT>, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx,
+                       rowseg);
+  else if (layout == ACT_BF16)
+    hipLaunchKernelGGL(ppm_rowseg_kernel<ACT_BF16>, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx,
+                       rowseg);
   else
-    hipLaunchKernelGGL(ppm_rowseg_kernel<false>, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx,
+    hipLaunchKernelGGL(ppm_rowseg_kernel<ACT_F32>, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx,
                        rowseg);
   CWT_LAUNCH_CHECK();
   const long t2 = (long)N * sy.nseg * sx.nseg * C;

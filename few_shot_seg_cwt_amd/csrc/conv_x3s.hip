@@ -23,6 +23,14 @@
 // Epilogue: fragments -> per-wave LDS tile -> row-contiguous 8-channel groups per lane:
 // BN scale/shift, residual (fp32 or S-layout), ReLU, stored as fp32 NHWC (channel
 // offset/stride) and/or S-layout, or the raw split-K partials (fp32 [ks][M][Co]).
+//
+// PREC = 1 (conv_igemm_b16, the bf16 conv stack of BASELINE config #5): the same kernel over
+// PLAIN bf16 operands.  Activations are NHWC bf16 ([row][C], i.e. the S-layout with
+// 64-channel blocks and no lo half) and the weights [Co][K] bf16 with K ordered
+// (64-channel block, tap, channel): a 128-B LDS row holds 64 consecutive k of one pixel/tap,
+// so a K-tile is 64 deep and its two 32-deep halves (chunks 0-3 and 4-7 of the row, where
+// PREC 3 keeps hi and lo) take one MFMA each.  fp32 accumulation; BN, residual and ReLU in
+// fp32; outputs rounded to bf16 (fp32 for the last conv, whose output is the feature map).
 #include "common.h"
 #include "kernels.h"
 
@@ -63,8 +71,9 @@ __device__ __forceinline__ void block_sync_lds() {
 
 // Residual of 8 consecutive channels [co, co + 8) of output row m (0 without a residual).
 struct Res8 {
-  f32x4 a, b;  // fp32 residual, or the S-layout hi / lo halves reinterpreted
+  f32x4 a, b;  // fp32 residual, or the S-layout hi / lo halves (PREC 1: a = 8 bf16) reinterpreted
 };
+template <int PREC>
 __device__ __forceinline__ Res8 load_res8(const ConvSArgs& a, int m, int co) {
   Res8 r;
   if (a.res) {
@@ -72,9 +81,14 @@ __device__ __forceinline__ Res8 load_res8(const ConvSArgs& a, int m, int co) {
     r.a = rp[0];
     r.b = rp[1];
   } else if (a.res_s) {
-    const __bf16* rp = a.res_s + ((long)m * (a.Co >> 5) + (co >> 5)) * 64 + (co & 31);
-    r.a = *(const f32x4*)rp;
-    r.b = *(const f32x4*)(rp + 32);
+    if (PREC == 1) {
+      r.a = *(const f32x4*)(a.res_s + (long)m * a.Co + co);
+      r.b = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      const __bf16* rp = a.res_s + ((long)m * (a.Co >> 5) + (co >> 5)) * 64 + (co & 31);
+      r.a = *(const f32x4*)rp;
+      r.b = *(const f32x4*)(rp + 32);
+    }
   } else {
     r.a = r.b = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -82,6 +96,7 @@ __device__ __forceinline__ Res8 load_res8(const ConvSArgs& a, int m, int co) {
 }
 
 // 8 consecutive channels [co, co + 8) of output row m: BN, residual, ReLU, stores.
+template <int PREC>
 __device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, const float* v, const float* sc,
                                            const float* sh, const Res8& rs) {
   float o[8];
@@ -96,7 +111,7 @@ __device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, co
   } else if (a.res_s) {
     const bf16x8 rh = __builtin_bit_cast(bf16x8, rs.a), rl = __builtin_bit_cast(bf16x8, rs.b);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] += (float)rh[i] + (float)rl[i];
+    for (int i = 0; i < 8; ++i) o[i] += PREC == 1 ? (float)rh[i] : (float)rh[i] + (float)rl[i];
   }
   if (a.relu) {
 #pragma unroll
@@ -114,14 +129,19 @@ __device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, co
       hi[i] = (__bf16)o[i];
       lo[i] = (__bf16)(o[i] - (float)hi[i]);
     }
-    __bf16* sp = a.ys + ((long)m * (a.Co >> 5) + (co >> 5)) * 64 + (co & 31);
-    *(bf16x8*)sp = hi;
-    *(bf16x8*)(sp + 32) = lo;
+    if (PREC == 1) {
+      *(bf16x8*)(a.ys + (long)m * a.Co + co) = hi;
+    } else {
+      __bf16* sp = a.ys + ((long)m * (a.Co >> 5) + (co >> 5)) * 64 + (co & 31);
+      *(bf16x8*)sp = hi;
+      *(bf16x8*)(sp + 32) = lo;
+    }
   }
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE>
-__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArgs a) {
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC>
+__device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
+  static_assert(PREC == 1 || PREC == 3, "PREC: 3 = bf16x3 over the S-layout, 1 = plain bf16");
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int FM = WM / 16, FN = WN / 16;
@@ -149,7 +169,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
 
   // ---- LDS-DMA source geometry (constant over K) ----
   const int lrow = lane >> 3, lslot = lane & 7;
-  const int cblocks = a.Ci >> 5;
+  const int cblocks = a.Ci >> (PREC == 1 ? 6 : 5);  // 128-B lines per pixel
   int a_ih0[LA], a_iw0[LA], a_pix0[LA], a_ch[LA];
   const int HoWo = a.Ho * a.Wo;
 #pragma unroll
@@ -248,9 +268,14 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.al[i], F.bh[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.ah[i], F.bl[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.ah[i], F.bh[j], acc[i][j], 0, 0, 0);
+        if (PREC == 1) {  // "hi" / "lo" = first / second 32 k of the 64-deep tile
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.ah[i], F.bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.al[i], F.bl[j], acc[i][j], 0, 0, 0);
+        } else {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.al[i], F.bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.ah[i], F.bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.ah[i], F.bh[j], acc[i][j], 0, 0, 0);
+        }
       }
   };
 
@@ -290,7 +315,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
   const bool fused = !a.part;
 #pragma unroll
   for (int rr = 0; rr < RR; ++rr)
-    if (fused) resb[0][rr] = load_res8(a, min(mrow + rr * RPR, a.M - 1), co);
+    if (fused) resb[0][rr] = load_res8<PREC>(a, min(mrow + rr * RPR, a.M - 1), co);
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
 #pragma unroll
@@ -310,7 +335,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
     if (pass + 1 < NPASS && fused) {
 #pragma unroll
       for (int rr = 0; rr < RR; ++rr)
-        resb[(pass + 1) & 1][rr] = load_res8(a, min(mrow + (pass + 1) * EP_ROWS + rr * RPR, a.M - 1), co);
+        resb[(pass + 1) & 1][rr] = load_res8<PREC>(a, min(mrow + (pass + 1) * EP_ROWS + rr * RPR, a.M - 1), co);
     }
 #pragma unroll
     for (int rr = 0; rr < RR; ++rr) {
@@ -322,7 +347,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
           pp[1] = v1[rr];
         } else {
           const float v[8] = {v0[rr][0], v0[rr][1], v0[rr][2], v0[rr][3], v1[rr][0], v1[rr][1], v1[rr][2], v1[rr][3]};
-          store_out8(a, m, co, v, sc, sh, resb[pass & 1][rr]);
+          store_out8<PREC>(a, m, co, v, sc, sh, resb[pass & 1][rr]);
         }
       }
     }
@@ -330,8 +355,18 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
   }
 }
 
+// STAGE only names the instantiation (rocprofv3 reports the conv stack by stage).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArgs a) {
+  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 3>(a);
+}
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_b16(ConvSArgs a) {
+  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 1>(a);
+}
+
 // Split-K reduction (fixed order, deterministic) + the same epilogue math.
-template <int NS>
+template <int NS, int PREC>
 __global__ void conv_s_splitk_epilogue(ConvSArgs a, int nsplit) {
   const int g8 = a.Co >> 3;
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -366,7 +401,7 @@ __global__ void conv_s_splitk_epilogue(ConvSArgs a, int nsplit) {
     sc[i] = a.scale[co + i];
     sh[i] = a.shift[co + i];
   }
-  store_out8(a, m, co, v, sc, sh, load_res8(a, m, co));
+  store_out8<PREC>(a, m, co, v, sc, sh, load_res8<PREC>(a, m, co));
 }
 
 // fp32 [P][C] (pixel stride ld) -> S-layout [P][C/32][64]
@@ -440,6 +475,22 @@ static void launch_tiles_x3s(const ConvSArgs& a, const ConvPlan& p, dim3 grid, h
     hipLaunchKernelGGL((conv_igemm_x3s<64, 64, 2, 2, 4, STAGE>), grid, dim3(256), 0, st, a);
 }
 
+template <int STAGE>
+static void launch_tiles_b16(const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
+  if (p.bm == 256 && p.bn == 256)
+    hipLaunchKernelGGL((conv_igemm_b16<256, 256, 2, 4, 2, STAGE>), grid, dim3(512), 0, st, a);
+  else if (p.bm == 256 && p.bn == 128)
+    hipLaunchKernelGGL((conv_igemm_b16<256, 128, 4, 2, 3, STAGE>), grid, dim3(512), 0, st, a);
+  else if (p.bm == 128 && p.bn == 128)
+    hipLaunchKernelGGL((conv_igemm_b16<128, 128, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
+  else if (p.bm == 128 && p.bn == 64)
+    hipLaunchKernelGGL((conv_igemm_b16<128, 64, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
+  else if (p.bm == 64 && p.bn == 128)
+    hipLaunchKernelGGL((conv_igemm_b16<64, 128, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_igemm_b16<64, 64, 2, 2, 4, STAGE>), grid, dim3(256), 0, st, a);
+}
+
 struct MeasuredPlanS {
   int M, Co, K, bm, bn, nsplit;
 };
@@ -451,18 +502,8 @@ static const MeasuredPlanS kMeasuredPlansS[] = {
 // tools/gen_plan_table.py --x3s from tools/conv_s_sweep.py on the MI355X), else the largest
 // tile giving >= kMinWG workgroups, splitting K by powers of two (>= 8 K-tiles per split)
 // where the output grid is too small.
-ConvPlan plan_conv_x3s(int M, int Co, int K) {
+static ConvPlan plan_heuristic_s(int M, int Co, int ktiles) {
   constexpr long kMinWG = 200;
-  const int ktiles = K / 32;
-  for (const MeasuredPlanS& e : kMeasuredPlansS)
-    if (e.M == M && e.Co == Co && e.K == K && Co % e.bn == 0) {
-      ConvPlan p;
-      p.bm = e.bm;
-      p.bn = e.bn;
-      p.kt_per_split = cdiv(ktiles, e.nsplit);
-      p.nsplit = cdiv(ktiles, p.kt_per_split);
-      return p;
-    }
   static const int cand[6][2] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
   ConvPlan best;
   for (auto& c : cand) {
@@ -481,14 +522,51 @@ ConvPlan plan_conv_x3s(int M, int Co, int K) {
   return best;
 }
 
+ConvPlan plan_conv_x3s(int M, int Co, int K) {
+  const int ktiles = K / 32;
+  for (const MeasuredPlanS& e : kMeasuredPlansS)
+    if (e.M == M && e.Co == Co && e.K == K && Co % e.bn == 0) {
+      ConvPlan p;
+      p.bm = e.bm;
+      p.bn = e.bn;
+      p.kt_per_split = cdiv(ktiles, e.nsplit);
+      p.nsplit = cdiv(ktiles, p.kt_per_split);
+      return p;
+    }
+  return plan_heuristic_s(M, Co, ktiles);
+}
+
+// Plain bf16: 64-deep K-tiles (the sweep table is for bf16x3 and is not reused).
+ConvPlan plan_conv_b16(int M, int Co, int K) { return plan_heuristic_s(M, Co, K / 64); }
+
+template <int PREC>
+static void launch_splitk_s(const ConvSArgs& a, int nsplit, hipStream_t st) {
+  const long n = (long)a.M * (a.Co / 8);
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+  switch (nsplit) {
+    case 2: hipLaunchKernelGGL((conv_s_splitk_epilogue<2, PREC>), g, b, 0, st, a, nsplit); break;
+    case 3: hipLaunchKernelGGL((conv_s_splitk_epilogue<3, PREC>), g, b, 0, st, a, nsplit); break;
+    case 4: hipLaunchKernelGGL((conv_s_splitk_epilogue<4, PREC>), g, b, 0, st, a, nsplit); break;
+    case 8: hipLaunchKernelGGL((conv_s_splitk_epilogue<8, PREC>), g, b, 0, st, a, nsplit); break;
+    default: hipLaunchKernelGGL((conv_s_splitk_epilogue<0, PREC>), g, b, 0, st, a, nsplit); break;
+  }
+}
+
+// prec 3: bf16x3 over S-layout operands; prec 1: plain bf16 (NHWC bf16 activations, weights in
+// 64-channel-block order, plan_conv_b16)
 int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,
-                    hipStream_t st) {
-  if (!a.xs || !a.ws || !a.zero) return fail(CWT_ESTATE, "x3s conv needs split input, split weights and a zero line");
-  if (a.Ci % 32 || a.Co % 64 || a.Co % p.bn) return fail(CWT_EARG, "x3s conv: need Ci % 32 == 0, Co % 64 == 0");
-  a.ktiles = a.K / 32;
+                    hipStream_t st, int prec) {
+  if (prec != 1 && prec != 3) return fail(CWT_EARG, "conv precision must be 3 (bf16x3) or 1 (bf16)");
+  if (!a.xs || !a.ws || !a.zero) return fail(CWT_ESTATE, "S-layout conv needs its input, weights and a zero line");
+  const int kb = prec == 1 ? 64 : 32;
+  if (a.Ci % kb || a.Co % 64 || a.Co % p.bn)
+    return fail(CWT_EARG, prec == 1 ? "bf16 conv: need Ci % 64 == 0, Co % 64 == 0"
+                                    : "x3s conv: need Ci % 32 == 0, Co % 64 == 0");
+  a.ktiles = a.K / kb;
   a.ktiles_total = a.ktiles;
   a.kt_per_split = p.kt_per_split;
   const int nsplit = p.nsplit;
+  if (nsplit < 1 || (long)p.kt_per_split * nsplit < a.ktiles) return fail(CWT_EARG, "conv plan does not cover K");
   ConvSArgs main = a;
   if (nsplit > 1) {
     if ((size_t)nsplit * a.M * a.Co > part_ws_floats) return fail(CWT_ESTATE, "split-K workspace too small");
@@ -497,27 +575,34 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
     main.part = nullptr;
   }
   dim3 grid(cdiv(a.M, p.bm), a.Co / p.bn, nsplit);
-  switch (stage) {
-    case 0: launch_tiles_x3s<0>(main, p, grid, st); break;
-    case 1: launch_tiles_x3s<1>(main, p, grid, st); break;
-    case 2: launch_tiles_x3s<2>(main, p, grid, st); break;
-    case 3: launch_tiles_x3s<3>(main, p, grid, st); break;
-    case 4: launch_tiles_x3s<4>(main, p, grid, st); break;
-    case 5: launch_tiles_x3s<5>(main, p, grid, st); break;
-    default: launch_tiles_x3s<6>(main, p, grid, st); break;
+  if (prec == 1) {
+    switch (stage) {
+      case 0: launch_tiles_b16<0>(main, p, grid, st); break;
+      case 1: launch_tiles_b16<1>(main, p, grid, st); break;
+      case 2: launch_tiles_b16<2>(main, p, grid, st); break;
+      case 3: launch_tiles_b16<3>(main, p, grid, st); break;
+      case 4: launch_tiles_b16<4>(main, p, grid, st); break;
+      case 5: launch_tiles_b16<5>(main, p, grid, st); break;
+      default: launch_tiles_b16<6>(main, p, grid, st); break;
+    }
+  } else {
+    switch (stage) {
+      case 0: launch_tiles_x3s<0>(main, p, grid, st); break;
+      case 1: launch_tiles_x3s<1>(main, p, grid, st); break;
+      case 2: launch_tiles_x3s<2>(main, p, grid, st); break;
+      case 3: launch_tiles_x3s<3>(main, p, grid, st); break;
+      case 4: launch_tiles_x3s<4>(main, p, grid, st); break;
+      case 5: launch_tiles_x3s<5>(main, p, grid, st); break;
+      default: launch_tiles_x3s<6>(main, p, grid, st); break;
+    }
   }
   CWT_LAUNCH_CHECK();
   if (nsplit > 1) {
     main.part = part_ws;
-    const long n = (long)a.M * (a.Co / 8);
-    const dim3 g((unsigned)((n + 255) / 256)), b(256);
-    switch (nsplit) {
-      case 2: hipLaunchKernelGGL(conv_s_splitk_epilogue<2>, g, b, 0, st, main, nsplit); break;
-      case 3: hipLaunchKernelGGL(conv_s_splitk_epilogue<3>, g, b, 0, st, main, nsplit); break;
-      case 4: hipLaunchKernelGGL(conv_s_splitk_epilogue<4>, g, b, 0, st, main, nsplit); break;
-      case 8: hipLaunchKernelGGL(conv_s_splitk_epilogue<8>, g, b, 0, st, main, nsplit); break;
-      default: hipLaunchKernelGGL(conv_s_splitk_epilogue<0>, g, b, 0, st, main, nsplit); break;
-    }
+    if (prec == 1)
+      launch_splitk_s<1>(main, nsplit, st);
+    else
+      launch_splitk_s<3>(main, nsplit, st);
     CWT_LAUNCH_CHECK();
   }
   return 0;

@@ -51,6 +51,10 @@ struct ConvSArgs {
 __host__ __device__ __forceinline__ long packed_k(int ci, int tap, int taps) {
   return (long)(ci >> 5) * (taps * 32) + tap * 32 + (ci & 31);
 }
+// The same with 64-channel blocks: the K order of the plain-bf16 conv (one 128-B line = 64 k).
+__host__ __device__ __forceinline__ long packed_k64(int ci, int tap, int taps) {
+  return (long)(ci >> 6) * (taps * 64) + tap * 64 + (ci & 63);
+}
 
 // Tile of this workgroup.  Blocks b and b+8 are observed to land on the same XCD (speed
 // only, MI355X_MICROARCH.md §Workgroup dispatch); the linear block id is remapped so that
@@ -117,8 +121,11 @@ int launch_conv_x3(ConvArgs a, const ConvPlan& p, int stage, float* part_ws, siz
 int launch_split_bf16(const float* w, __bf16* hi, __bf16* lo, long n, hipStream_t st);
 // split-activation variant (conv_x3s.hip)
 ConvPlan plan_conv_x3s(int M, int Co, int K);
+ConvPlan plan_conv_b16(int M, int Co, int K);
+// prec 3: bf16x3 (S-layout operands); prec 1: plain bf16 (NHWC bf16 activations, [Co][K]
+// bf16 weights with K ordered (64-channel block, tap, channel): packed_k64)
 int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,
-                    hipStream_t st);
+                    hipStream_t st, int prec = 3);
 int launch_split_act(const float* x, long P, int C, int ld, __bf16* out, hipStream_t st);
 int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipStream_t st);
 
@@ -138,14 +145,16 @@ struct AdaptGraphCache {
   ~AdaptGraphCache();
 };
 
-// backbone helpers (backbone.hip)
+// backbone helpers (backbone.hip).  Activation storage of the conv stack:
+enum ActLayout { ACT_F32 = 0, ACT_SPLIT = 1, ACT_BF16 = 2 };  // fp32 NHWC, S-layout, bf16 NHWC
 int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const float* scale,
-                      const float* shift, float* out, int Ho, hipStream_t st, bool split = false);
+                      const float* shift, float* out, int Ho, hipStream_t st, int layout = ACT_F32);
 int launch_maxpool3s2_s(const __bf16* in, int N, int H, int W, int C, __bf16* out, int Ho, int Wo, hipStream_t st);
+int launch_maxpool3s2_b16(const __bf16* in, int N, int H, int W, int C, __bf16* out, int Ho, int Wo, hipStream_t st);
 int launch_maxpool3s2(const float* in, int N, int H, int W, int C, float* out, int Ho, int Wo,
                       hipStream_t st);
 int launch_ppm(const float* x, int N, int h, int w, int ld, const int* bins, int nbins, float* ws,
-               float* pooled, hipStream_t st, bool split = false);
+               float* pooled, hipStream_t st, int layout = ACT_F32);
 int launch_repack_cblock(const float* src, float* dst, int Co, int taps, int Ci, hipStream_t st);
 int launch_smallm_gemm(const float* A, int lda, const float* const* Bt, const int* M, int np, int N, int K, int kc,
                        float* part, size_t part_floats, const float* const* scale, const float* const* shift,

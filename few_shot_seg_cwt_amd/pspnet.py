@@ -55,6 +55,23 @@ class PSPNet:
         self._state = None
         self._handle = None
         self.training = False
+        # conv-stack arithmetic (BASELINE config #5): "fp32" (reference numerics, default) or
+        # "bf16" (bf16 MFMA convs, bf16 activations between convs, fp32 feature map out)
+        self.conv_dtype = str(_arg(args, "conv_dtype", "fp32"))
+        if self.conv_dtype not in self._PRECISION:
+            raise ValueError(f"conv_dtype must be one of {sorted(self._PRECISION)}")
+
+    _PRECISION = {"fp32": 0, "bf16": 1}  # CWT_CONV_FP32 / CWT_CONV_BF16 (include/cwt.h)
+
+    def set_conv_dtype(self, dtype: str):
+        """Switch the conv-stack arithmetic of the loaded extractor ("fp32" or "bf16")."""
+        if dtype not in self._PRECISION:
+            raise ValueError(f"conv_dtype must be one of {sorted(self._PRECISION)}")
+        self.conv_dtype = dtype
+        if self._handle is not None:
+            _lib.check(_lib.lib().cwt_backbone_set_precision(self._handle, self._PRECISION[dtype]),
+                       "cwt_backbone_set_precision")
+        return self
 
     def _release(self):
         if getattr(self, "_handle", None) is not None and _lib._lib is not None:
@@ -122,6 +139,7 @@ class PSPNet:
         self._release()
         self._handle = handle
         self._state = sd
+        self.set_conv_dtype(self.conv_dtype)
         return self
 
     def feature_res(self, S: int):

@@ -67,6 +67,20 @@ int cwt_backbone_load(cwt_ctx* ctx, int layers, int n_tensors, const char* const
 int cwt_backbone_destroy(cwt_backbone* bb);
 
 /*
+ * Arithmetic of the extractor's conv stack (SURVEY.md §8(b) `dtype` of cwt_backbone_load;
+ * BASELINE.json config #5 "mixed-precision bf16 conv + fp32 CWT").  The reference computes
+ * in fp32 only; CWT_CONV_FP32 (the default) matches it to ~1e-5 per conv (bf16x3, see the
+ * header comment).  CWT_CONV_BF16 runs every MFMA conv on plain bf16 operands with fp32
+ * accumulation and stores the activations between convs as bf16 (the stem conv1, pooling and
+ * the PPM branch stay fp32 arithmetic); the returned feature map is fp32 as before, so the
+ * inner loop, the CWT and the classifier are unchanged fp32.  Applies to subsequent
+ * cwt_extract_features calls with this backbone.  Returns CWT_EARG for an unknown value.
+ */
+#define CWT_CONV_FP32 0
+#define CWT_CONV_BF16 1
+int cwt_backbone_set_precision(cwt_backbone* bb, int precision);
+
+/*
  * Frozen feature extractor forward (eval mode).
  * Replaces: PSPNet.extract_features(x) -> (f, []) (pspnet.py:172-181; get_feat_list
  *           pspnet.py:272-287; PPM pspnet.py:33-38; bottleneck pspnet.py:124-129).
@@ -216,6 +230,13 @@ int cwt_debug_conv_s(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci
                      const float* scale, const float* shift, int Co, int k, int stride, int pad,
                      int dil, const float* res, int res_ld, const void* res_s, int relu, float* y,
                      int y_ld, int y_off, void* ys, int bm, int bn, int nsplit, void* stream);
+/* The same conv on plain bf16 operands (the CWT_CONV_BF16 kernel): xs bf16 NHWC [N*Hi*Wi][Ci]
+ * (Ci % 64 == 0), ws bf16 [Co][K] with K ordered (64-channel block, tap, channel in block),
+ * res_s / ys bf16 NHWC [M][Co]. */
+int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws,
+                       const float* scale, const float* shift, int Co, int k, int stride, int pad,
+                       int dil, const float* res, int res_ld, const void* res_s, int relu, float* y,
+                       int y_ld, int y_off, void* ys, int bm, int bn, int nsplit, void* stream);
 
 /* Test hook: per workgroup of a 64-thread grid, the raw HW_REG_HW_ID and HW_REG_XCC_ID of the
  * CU it ran on (out[2*b], out[2*b+1]); with a CU-masked stream this maps mask bits to CUs. */

@@ -137,3 +137,72 @@ def test_split_roundtrip():
     assert torch.equal(hi, x.to(torch.bfloat16))          # hi = bf16_rne(x)
     back = unsplit(s, 1000, 96)
     assert float(((back - x).abs() / x.abs().clamp_min(1e-30)).max()) < 2.0 ** -16
+
+
+# ---------------------------------------------------------------- plain bf16 (CWT_CONV_BF16)
+# fp32 accumulation of exact bf16 x bf16 products: against a float64 conv of the SAME
+# bf16-rounded operands only the summation order differs (~K * 2^-24 relative).
+TOL_B16 = 2e-5
+
+
+def bf16_nhwc(t_nchw):
+    return t_nchw.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+
+
+def pack_w_b16(w):
+    """[Co,Ci,k,k] fp32 -> bf16 [Co][K], K ordered (64-channel block, tap, channel)."""
+    Co, Ci, k, _ = w.shape
+    return w.reshape(Co, Ci // 64, 64, k * k).permute(0, 1, 3, 2).contiguous().to(torch.bfloat16)
+
+
+def run_conv_b16(x, w, scale, shift, stride, pad, dil, res=None, res_bf16=False, relu=True, bm=0, bn=0, nsplit=0):
+    L = _lib()
+    dev = torch.device("cuda", 0)
+    N, Ci, Hi, Wi = x.shape
+    Co, _, k, _ = w.shape
+    xs = bf16_nhwc(x).to(dev)
+    ws = pack_w_b16(w).to(dev)
+    Ho = (Hi + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    y = torch.full((N, Ho, Ho, Co), float("nan"), device=dev)
+    ys = torch.zeros((N, Ho, Ho, Co), dtype=torch.bfloat16, device=dev)
+    rd = res.permute(0, 2, 3, 1).contiguous().to(dev) if res is not None else None
+    rs = rd.to(torch.bfloat16) if (rd is not None and res_bf16) else None
+    sc, sh = scale.to(dev), shift.to(dev)
+    rc = L.lib().cwt_debug_conv_b16(L.ctx(0), L.ptr(xs), N, Hi, Wi, Ci, L.ptr(ws), L.ptr(sc), L.ptr(sh), Co, k,
+                                    stride, pad, dil, None if res_bf16 else L.ptr(rd), Co, L.ptr(rs), int(relu),
+                                    L.ptr(y), Co, 0, L.ptr(ys), bm, bn, nsplit, L.stream_ptr())
+    L.check(rc, "cwt_debug_conv_b16")
+    torch.cuda.synchronize()
+    return y.cpu().permute(0, 3, 1, 2), ys.cpu().float().permute(0, 3, 1, 2)
+
+
+CASES_B16 = [c for c in CASES if c[1] % 64 == 0]
+
+
+@pytest.mark.parametrize("case", CASES_B16, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("plan", PLANS, ids=lambda p: f"{p[0]}x{p[1]}s{p[2]}")
+def test_conv_b16_plans(case, plan):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    N, Ci, Co, Hi, k, stride, dil, has_res = case
+    bm, bn, ns = plan
+    if bn and Co % bn:
+        pytest.skip("Co not a multiple of the tile")
+    tag = f"{N}_{Ci}_{Co}_{Hi}_{k}"
+    x = torch.from_numpy(syn.normal(1, "x" + tag, (N, Ci, Hi, Hi), 1.0))
+    w = torch.from_numpy(syn.normal(1, "w" + tag, (Co, Ci, k, k), (2.0 / (Ci * k * k)) ** 0.5))
+    scale = torch.from_numpy(syn.uniform(1, "s" + tag, (Co,), 0.5, 1.5))
+    shift = torch.from_numpy(syn.normal(1, "b" + tag, (Co,), 0.1))
+    pad = dil if k == 3 else 0
+    Ho = (Hi + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    res = torch.from_numpy(syn.normal(1, "r" + tag, (N, Co, Ho, Ho), 1.0)) if has_res else None
+    res_bf16 = ns % 2 == 1
+    yf, yb = run_conv_b16(x, w, scale, shift, stride, pad, dil, res, res_bf16=res_bf16, bm=bm, bn=bn, nsplit=ns)
+    xr = x.to(torch.bfloat16).float()
+    wr = w.to(torch.bfloat16).float()
+    rr = res.to(torch.bfloat16).float() if (res is not None and res_bf16) else res
+    ref = ref_conv(xr, wr, scale, shift, stride, pad, dil, rr, True)
+    err = float((yf.double() - ref).abs().max() / ref.abs().max())
+    assert err < TOL_B16, err
+    # the bf16 output is the round-to-nearest bf16 of the fp32 output
+    assert torch.equal(yb, yf.to(torch.bfloat16).float())
