@@ -33,6 +33,7 @@ SIGNATURES = {
     "cwt_extract_features": (_I, [_P, _P, _P, _I, _I, _P, _P]),
     "cwt_workspace_bytes": (C.c_size_t, [_P]),
     "cwt_inner_adapt": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
+    "cwt_inner_adapt_batch": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
     "cwt_normalize": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "cwt_attention_fwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cwt_attention_saved_floats": (C.c_size_t, [_I, _I, _I, _I]),

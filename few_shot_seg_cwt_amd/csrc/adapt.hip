@@ -15,6 +15,10 @@
 // The next step's kernel applies W <- W - lr/sum(w) * dW on the fly, so a step is one
 // launch; three accumulator slots let step s zero slot s+1 without a race.
 // f_s (7.4 MB per shot at 60x60x512) is re-read every step from L2 / Infinity Cache.
+//
+// Several independent episodes (E, each with its own W, labels, class weight and replica
+// accumulators) run in the same launches: grid.z = E * shots.  A step is latency-bound (one
+// dependent launch per SGD step), so E episodes share the ~200 launch boundaries of one.
 #include <cstdlib>
 
 #include "common.h"
@@ -31,8 +35,12 @@ struct AdaptScalars {
 // int64 labels -> u8 (0, 1, 255 for anything else) plus per-block label counts (no atomics,
 // so nothing has to be zeroed first; adapt_setup_kernel sums the blocks in fixed order).
 constexpr int PREP_MAXBLK = 256;
+// Episode e = blockIdx.y owns lbl[e*total, (e+1)*total) and part[e][PREP_MAXBLK][2].
 __global__ void adapt_prep_kernel(const int64_t* __restrict__ lbl, long total, uint8_t* __restrict__ out,
-                                  unsigned long long* __restrict__ part /*[gridDim][2]*/) {
+                                  unsigned long long* __restrict__ part) {
+  lbl += (long)blockIdx.y * total;
+  out += (long)blockIdx.y * total;
+  part += (long)blockIdx.y * 2 * PREP_MAXBLK;
   unsigned long long nb = 0, nf = 0;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int64_t v = lbl[i];
@@ -67,9 +75,6 @@ __global__ void adapt_prep_kernel(const int64_t* __restrict__ lbl, long total, u
 // mode 0: weight = [1, nbg/nfg]        (test.py:169-175, train.py:211-217)
 // mode 1: weight = [1, nbg/(nfg+1e-12)] (train.py:237-243, query loss)
 struct AdaptDevArgs;
-__global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, int nblk, AdaptScalars* sc, float lr,
-                                   int mode, AdaptDevArgs* dargs, const float* f, const float* w_in, float* w_out,
-                                   float* zero, int nzero, double* zero_d);
 
 constexpr int ADAPT_CB = 16;           // lo-res columns per workgroup
 // dW[1] accumulator replicas: ~240 workgroups adding 2 KB each into ONE 2 KB row run at the
@@ -80,6 +85,8 @@ constexpr int ADAPT_RMAX = 32;                 // replica rows allocated per slo
 constexpr int ADAPT_R_DEFAULT = 8;             // replica rows used (CWT_ADAPT_R overrides: 4, 8, 16 or 32)
 constexpr int ADAPT_SLOT = ADAPT_RMAX * 512;   // floats per accumulator slot
 constexpr int ADAPT_NP = 2 * (ADAPT_CB + 1);
+constexpr long ADAPT_ESTRIDE = 3L * ADAPT_SLOT;  // accumulator floats per episode (3 slots)
+constexpr int ADAPT_WSTRIDE = 2 * 1024;          // W ping-pong floats per episode
 constexpr int ADAPT_PPW = (ADAPT_NP + 3) / 4;  // lo pixels per wave
 
 // Per-call pointers, read by the kernels from device memory so that one captured graph of
@@ -90,11 +97,18 @@ struct AdaptDevArgs {
   float* w_out;       // adapted W [2][512]
 };
 
+// One block per episode e = blockIdx.x: its scalars sc[e], its pointers dargs[e] (f + e *
+// f_stride, w_in / w_out + e * w_stride) and the zeroing of zero[e * zero_stride + [0, nzero)).
 __global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, int nblk, AdaptScalars* sc, float lr,
-                                   int mode, AdaptDevArgs* dargs, const float* f, const float* w_in, float* w_out,
-                                   float* zero, int nzero, double* zero_d) {
+                                   int mode, AdaptDevArgs* dargs, const float* f, long f_stride, const float* w_in,
+                                   float* w_out, int w_stride, float* zero, long zero_stride, int nzero,
+                                   double* zero_d) {
   __shared__ unsigned long long red[2][PREP_MAXBLK];
   const int t = threadIdx.x;
+  const int e = blockIdx.x;
+  part += (long)e * 2 * PREP_MAXBLK;
+  sc += e;
+  if (zero) zero += (long)e * zero_stride;
   red[0][t] = t < nblk ? part[2 * t] : 0ull;
   red[1][t] = t < nblk ? part[2 * t + 1] : 0ull;
   __syncthreads();
@@ -116,25 +130,28 @@ __global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, 
     const double sumw = nb + nf * (double)wfg;
     sc->lr_eff = (float)((double)lr / sumw);
     if (dargs) {
-      dargs->f = f;
-      dargs->w_in = w_in;
-      dargs->w_out = w_out;
+      dargs[e].f = f + e * f_stride;
+      dargs[e].w_in = w_in + (long)e * w_stride;
+      dargs[e].w_out = w_out + (long)e * w_stride;
     }
     if (zero_d) *zero_d = 0.0;
   }
-  for (int i = t; i < nzero; i += blockDim.x) zero[i] = 0.f;
+  if (zero)
+    for (int i = t; i < nzero; i += blockDim.x) zero[i] = 0.f;
 }
 
+// Per-episode state e = blockIdx.z / nshot: dargs[e], sc[e], and the W / accumulator buffers
+// below offset by e * ADAPT_WSTRIDE / e * ADAPT_ESTRIDE floats.
 struct AdaptStepArgs {
   const AdaptDevArgs* dargs;
-  const uint8_t* lbl;    // [n][S][S]
+  const uint8_t* lbl;    // [E][n][S][S]
   const AdaptScalars* sc;
   const float* w_src;    // W before the previous update ([2][512]); null at step 0 (dargs->w_in)
   const float* acc_prev; // dW[1] replicas [R][512] of the previous step, or null at step 0
   float* w_dst;          // block (0,0,0) stores the current W here (may be null)
   float* acc_cur;        // dW[1] replicas [R][512] of this step (zeroed)
   float* acc_zero;       // slot [R][512] to zero for the next step (may be null)
-  int h, w, S;
+  int h, w, S, nshot;
   float sy, sx;          // align_corners scales (h-1)/(S-1), (w-1)/(S-1)
   int nrep;              // replica rows in use
   int dbg;               // ablation flags for timing studies only (CWT_ADAPT_DBG): 1 skip replica
@@ -217,14 +234,18 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
   __shared__ float red[ADAPT_NW][C];
   if (a.dbg & 16) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int cb = blockIdx.x, r = blockIdx.y, n = blockIdx.z;
+  const int cb = blockIdx.x, r = blockIdx.y;
+  const int ep = blockIdx.z / a.nshot, n = blockIdx.z - ep * a.nshot;
   const int ncb = gridDim.x;
   const int S = a.S;
+  const AdaptDevArgs* dargs = a.dargs + ep;
+  const AdaptScalars* scal = a.sc + ep;
+  const long eacc = ep * ADAPT_ESTRIDE, ew = (long)ep * ADAPT_WSTRIDE;
 
   // ---- loads that do not depend on W: the tile's f pixels and this lane's labels ----
   const int x0 = cb * ADAPT_CB;
   const int ncol = min(ADAPT_CB + 1, a.w - x0);
-  const float* fimg = a.dargs->f + (long)n * a.h * a.w * C;
+  const float* fimg = dargs->f + (long)n * a.h * a.w * C;
   float fv[ADAPT_PPW16][8];
 #pragma unroll
   for (int j = 0; j < ADAPT_PPW16; ++j) {
@@ -240,7 +261,7 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
       for (int q = 0; q < 8; ++q) fv[j][q] = 0.f;
     }
   }
-  const uint8_t* lbl = a.lbl + (long)n * S * S;
+  const uint8_t* lbl = a.lbl + (long)blockIdx.z * S * S;
   const int x_begin = cb * 8 * ADAPT_CB;
   const int x_end = (cb == ncb - 1) ? S : x_begin + 8 * ADAPT_CB;
   const int Y = 8 * r + (wv >> 1);
@@ -256,20 +277,20 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
     y_main[k] = in ? lbl[(long)Y * S + X] : 255;
     y_extra[k] = (in && extra) ? lbl[(long)(S - 1) * S + X] : 255;
   }
-  const float wfg = a.sc->wfg;
+  const float wfg = scal->wfg;
 
   // ---- current W (wave 0): W_src - lr_eff * sum of the previous step's replicas ----
   if (wv == 0) {
-    const float lr = a.sc->lr_eff;
-    const float* wsrc = a.w_src ? a.w_src : a.dargs->w_in;
+    const float lr = scal->lr_eff;
+    const float* wsrc = a.w_src ? a.w_src + ew : dargs->w_in;
     f32x4 w0a = *(const f32x4*)(wsrc + lane * 8), w0b = *(const f32x4*)(wsrc + lane * 8 + 4);
     f32x4 w1a = *(const f32x4*)(wsrc + C + lane * 8), w1b = *(const f32x4*)(wsrc + C + lane * 8 + 4);
     if (a.acc_prev && !(a.dbg & 1)) {
       f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
       for (int rr = 0; rr < a.nrep; ++rr) {
-        d0 += *(const f32x4*)(a.acc_prev + rr * 512 + lane * 8);
-        d1 += *(const f32x4*)(a.acc_prev + rr * 512 + lane * 8 + 4);
+        d0 += *(const f32x4*)(a.acc_prev + eacc + rr * 512 + lane * 8);
+        d1 += *(const f32x4*)(a.acc_prev + eacc + rr * 512 + lane * 8 + 4);
       }
       w1a -= lr * d0;
       w0a += lr * d0;
@@ -281,14 +302,15 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
     *(f32x4*)&wl[1][lane * 8] = w1a;
     *(f32x4*)&wl[1][lane * 8 + 4] = w1b;
     if ((cb | r | n) == 0 && a.w_dst) {
-      *(f32x4*)(a.w_dst + lane * 8) = w0a;
-      *(f32x4*)(a.w_dst + lane * 8 + 4) = w0b;
-      *(f32x4*)(a.w_dst + C + lane * 8) = w1a;
-      *(f32x4*)(a.w_dst + C + lane * 8 + 4) = w1b;
+      float* wd = a.w_dst + ew;
+      *(f32x4*)(wd + lane * 8) = w0a;
+      *(f32x4*)(wd + lane * 8 + 4) = w0b;
+      *(f32x4*)(wd + C + lane * 8) = w1a;
+      *(f32x4*)(wd + C + lane * 8 + 4) = w1b;
     }
   }
   if ((cb | r | n) == 0 && a.acc_zero)
-    for (int i = t; i < a.nrep * 128; i += ADAPT_T) ((f32x4*)a.acc_zero)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = t; i < a.nrep * 128; i += ADAPT_T) ((f32x4*)(a.acc_zero + eacc))[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (t < ADAPT_NP) (&gs[0][0])[t] = 0.f;
   __syncthreads();
 
@@ -382,7 +404,7 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
     float s = 0.f;
 #pragma unroll
     for (int v = 0; v < ADAPT_NW; ++v) s += red[v][t];
-    atomicAdd(&a.acc_cur[((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) % a.nrep) * 512 + t], s);
+    atomicAdd(&a.acc_cur[eacc + ((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * n)) % a.nrep) * 512 + t], s);
   }
 }
 
@@ -390,6 +412,11 @@ __global__ void adapt_final_kernel(const float* w_src, const float* acc, const A
                                    const AdaptDevArgs* dargs, int nrep) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= 512) return;
+  const int ep = blockIdx.y;
+  w_src += (long)ep * ADAPT_WSTRIDE;
+  if (acc) acc += ep * ADAPT_ESTRIDE;
+  sc += ep;
+  dargs += ep;
   float* w_out = dargs->w_out;
   const float lr = sc->lr_eff;
   float d = 0.f;
@@ -401,7 +428,7 @@ __global__ void adapt_final_kernel(const float* w_src, const float* acc, const A
 
 // The 200 step launches + the final update, enqueued on `st` (directly or while capturing).
 static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws, const AdaptScalars* sc, float* acc3,
-                               float* wbuf, int n, int h, int w, int S, int iters, hipStream_t st) {
+                               float* wbuf, int E, int n, int h, int w, int S, int iters, hipStream_t st) {
   AdaptStepArgs a;
   a.dargs = dargs;
   a.lbl = lbl_ws;
@@ -409,6 +436,7 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws,
   a.h = h;
   a.w = w;
   a.S = S;
+  a.nshot = n;
   a.sy = align_corners_scale(h, S);
   a.sx = align_corners_scale(w, S);
   const char* dbg = getenv("CWT_ADAPT_DBG");
@@ -417,7 +445,7 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws,
   a.nrep = nr ? atoi(nr) : ADAPT_R_DEFAULT;
   if (a.nrep != 4 && a.nrep != 8 && a.nrep != 16 && a.nrep != 32) a.nrep = ADAPT_R_DEFAULT;
   const int ncb = cdiv(S - 1, 8 * ADAPT_CB);
-  dim3 grid(ncb, h - 1, n);
+  dim3 grid(ncb, h - 1, E * n);
   for (int s = 0; s < iters; ++s) {
     a.w_src = (s == 0) ? nullptr : wbuf + ((s - 1) & 1) * 1024;
     a.acc_prev = (s == 0) ? nullptr : acc3 + ((s - 1) % 3) * ADAPT_SLOT;
@@ -428,7 +456,7 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws,
     CWT_LAUNCH_CHECK();
   }
   const int last = iters - 1;
-  hipLaunchKernelGGL(adapt_final_kernel, dim3(2), dim3(256), 0, st, (const float*)(wbuf + (last & 1) * 1024),
+  hipLaunchKernelGGL(adapt_final_kernel, dim3(2, E), dim3(256), 0, st, (const float*)(wbuf + (last & 1) * 1024),
                      (const float*)(acc3 + (last % 3) * ADAPT_SLOT), sc, dargs, a.nrep);
   CWT_LAUNCH_CHECK();
   return 0;
@@ -439,21 +467,33 @@ AdaptGraphCache::~AdaptGraphCache() {
   if (cap_stream) (void)hipStreamDestroy(cap_stream);
 }
 
-int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int S, float lr, int iters, float* W,
-                 uint8_t* lbl_ws, AdaptScalars* sc, float* acc3 /*[3][R][512]*/, float* wbuf /*[2][2][512]*/,
-                 AdaptDevArgs* dargs, AdaptGraphCache* cache, hipStream_t st) {
-  const long total = (long)n * S * S;
-  unsigned long long* part = (unsigned long long*)(sc + 1);  // [PREP_MAXBLK][2] after the scalars
+size_t adapt_ws_sizes(int E, int n, int S, size_t* lbl, size_t* sc, size_t* acc, size_t* wbuf, size_t* dargs) {
+  *lbl = (size_t)E * n * S * S;
+  *sc = (size_t)E * (sizeof(AdaptScalars) + 2 * PREP_MAXBLK * sizeof(unsigned long long)) + 64;
+  *acc = (size_t)E * ADAPT_ESTRIDE * sizeof(float);
+  *wbuf = (size_t)E * ADAPT_WSTRIDE * sizeof(float);
+  *dargs = (size_t)E * sizeof(AdaptDevArgs);
+  return 0;
+}
+
+// E episodes of n shots each: f [E][n][h][w][512], lbl64 [E][n][S][S], W [E][2][512].
+int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
+                 float* W, uint8_t* lbl_ws, AdaptScalars* sc /*[E] + partial counts*/,
+                 float* acc3 /*[E][3][R][512]*/, float* wbuf /*[E][2][2][512]*/, AdaptDevArgs* dargs /*[E]*/,
+                 AdaptGraphCache* cache, hipStream_t st) {
+  const long total = (long)n * S * S;  // labels per episode
+  unsigned long long* part = (unsigned long long*)(sc + E);  // [E][PREP_MAXBLK][2] after the scalars
   const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
-  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(1024), 0, st, lbl64, total, lbl_ws, part);
+  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks, E), dim3(1024), 0, st, lbl64, total, lbl_ws, part);
   CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(adapt_setup_kernel, dim3(1), dim3(PREP_MAXBLK), 0, st, (const unsigned long long*)part, pblocks,
-                     sc, lr, 0, dargs, f, (const float*)W, W, acc3, iters > 0 ? ADAPT_SLOT : 0, (double*)nullptr);
+  hipLaunchKernelGGL(adapt_setup_kernel, dim3(E), dim3(PREP_MAXBLK), 0, st, (const unsigned long long*)part, pblocks,
+                     sc, lr, 0, dargs, f, (long)n * h * w * 512, (const float*)W, W, 1024,
+                     iters > 0 ? acc3 : (float*)nullptr, ADAPT_ESTRIDE, ADAPT_SLOT, (double*)nullptr);
   CWT_LAUNCH_CHECK();
   if (iters <= 0) return 0;
-  if (!cache) return enqueue_adapt_steps(dargs, lbl_ws, sc, acc3, wbuf, n, h, w, S, iters, st);
+  if (!cache) return enqueue_adapt_steps(dargs, lbl_ws, sc, acc3, wbuf, E, n, h, w, S, iters, st);
   // graph path: one instantiated graph per (geometry, workspace pointers)
-  AdaptGraphCache::Entry key{n, h, w, S, iters, (const void*)lbl_ws, (const void*)sc, (const void*)acc3,
+  AdaptGraphCache::Entry key{E, n, h, w, S, iters, (const void*)lbl_ws, (const void*)sc, (const void*)acc3,
                              (const void*)wbuf, (const void*)dargs, nullptr};
   hipGraphExec_t exec = nullptr;
   for (auto& e : cache->entries)
@@ -462,7 +502,7 @@ int launch_adapt(const float* f, const int64_t* lbl64, int n, int h, int w, int 
     if (!cache->cap_stream) CWT_HIP(hipStreamCreateWithFlags(&cache->cap_stream, hipStreamNonBlocking));
     hipGraph_t g;
     CWT_HIP(hipStreamBeginCapture(cache->cap_stream, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_adapt_steps(dargs, lbl_ws, sc, acc3, wbuf, n, h, w, S, iters, cache->cap_stream);
+    int rc = enqueue_adapt_steps(dargs, lbl_ws, sc, acc3, wbuf, E, n, h, w, S, iters, cache->cap_stream);
     hipError_t e2 = hipStreamEndCapture(cache->cap_stream, &g);
     if (rc) return rc;
     if (e2 != hipSuccess) return fail((int)e2, std::string("adapt graph capture: ") + hipGetErrorString(e2));
@@ -541,11 +581,11 @@ int launch_seg_ce(const float* logits, const int64_t* target, int B, int h, int 
   const long total = (long)B * S * S;
   unsigned long long* part = (unsigned long long*)(sc + 1);
   const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
-  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks), dim3(1024), 0, st, target, total, lbl_ws, part);
+  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks, 1), dim3(1024), 0, st, target, total, lbl_ws, part);
   CWT_LAUNCH_CHECK();
   hipLaunchKernelGGL(adapt_setup_kernel, dim3(1), dim3(PREP_MAXBLK), 0, st, (const unsigned long long*)part, pblocks,
-                     sc, 1.0f, 1, (AdaptDevArgs*)nullptr, (const float*)nullptr, (const float*)nullptr,
-                     (float*)nullptr, dlogits, B * 2 * h * w, loss_num);
+                     sc, 1.0f, 1, (AdaptDevArgs*)nullptr, (const float*)nullptr, 0L, (const float*)nullptr,
+                     (float*)nullptr, 0, dlogits, 0L, B * 2 * h * w, loss_num);
   CWT_LAUNCH_CHECK();
   SegCEArgs a;
   a.logits = logits;

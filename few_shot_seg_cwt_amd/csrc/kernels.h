@@ -132,12 +132,12 @@ int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipSt
 // inner loop (adapt.hip): cache of instantiated graphs of the 200-step launch sequence
 struct AdaptGraphCache {
   struct Entry {
-    int n, h, w, S, iters;
+    int E, n, h, w, S, iters;
     const void *lbl, *sc, *acc, *wbuf, *dargs;
     hipGraphExec_t exec;
     bool same(const Entry& o) const {
-      return n == o.n && h == o.h && w == o.w && S == o.S && iters == o.iters && lbl == o.lbl && sc == o.sc &&
-             acc == o.acc && wbuf == o.wbuf && dargs == o.dargs;
+      return E == o.E && n == o.n && h == o.h && w == o.w && S == o.S && iters == o.iters && lbl == o.lbl &&
+             sc == o.sc && acc == o.acc && wbuf == o.wbuf && dargs == o.dargs;
     }
   };
   std::vector<Entry> entries;

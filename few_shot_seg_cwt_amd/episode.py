@@ -55,6 +55,28 @@ def inner_adapt(f_s: torch.Tensor, s_label: torch.Tensor, W: torch.Tensor, lr: f
     return W
 
 
+def inner_adapt_batch(f_s: torch.Tensor, s_label: torch.Tensor, W: torch.Tensor, lr: float, iters: int) -> torch.Tensor:
+    """E independent inner loops in the same launches (cwt_inner_adapt_batch), in place on
+    W [E,2,512].  f_s [E*n,512,h,w] channels_last (episode-major), s_label [E,n,S,S] or
+    [E*n,S,S] int64.  Episode e gets exactly inner_adapt(f_s[e*n:(e+1)*n], s_label[e], W[e])."""
+    _lib.require(f_s, "f_s")
+    _lib.require(s_label, "s_label", torch.int64)
+    _lib.require(W, "W")
+    E = W.shape[0]
+    En, Cc, h, w = f_s.shape
+    if W.shape != (E, 2, Cc) or not W.is_contiguous() or En % E:
+        raise ValueError(f"W must be a contiguous [E,2,{Cc}] tensor and f_s hold E*n images")
+    n = En // E
+    if not f_s.is_contiguous(memory_format=torch.channels_last):
+        f_s = f_s.contiguous(memory_format=torch.channels_last)
+    S = s_label.shape[-1]
+    lbl = s_label.reshape(E * n, S, S).contiguous()
+    _lib.check(_lib.lib().cwt_inner_adapt_batch(_lib.ctx(W.device.index), _lib.ptr(f_s), _lib.ptr(lbl), E, n, h, w,
+                                                Cc, S, float(lr), int(iters), _lib.ptr(W),
+                                                _lib.stream_ptr(W.device)), "cwt_inner_adapt_batch")
+    return W
+
+
 def normalize(f: torch.Tensor, W0: torch.Tensor | None = None):
     """F.normalize(f, dim=1) (+ baseline logits W0 . f). f [B,512,h,w] channels_last."""
     B, Cc, h, w = f.shape
@@ -119,6 +141,28 @@ class EpisodeEngine:
         Wb = W.view(1, 2, -1)
         fqn, pred_q0 = normalize(f_q, Wb)
         W2 = self.transformer(Wb, fqn, fqn)
+        pred_q = classify(W2, fqn)
+        iut, ce = seg_metrics(pred_q, q_label)
+        iut0, _ = seg_metrics(pred_q0, q_label, with_ce=False)
+        return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, f_s=f_s, f_q=f_q)
+
+    @torch.no_grad()
+    def run_batch(self, imgs: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor, W0: torch.Tensor) -> dict:
+        """E independent episodes in flight at once (throughput form of ``run``; each
+        episode's outputs are those ``run`` gives it alone: eval-mode BN makes the shared
+        backbone pass exact, and the inner loops keep per-episode W, class weights and
+        accumulators).  imgs [E*shot + E,3,S,S] = the E*shot supports (episode-major) then the
+        E queries; s_label [E,shot,S,S]; q_label [E,S,S] int64; W0 [E,2,512] (adapted in
+        place).  E <= 4 (the CWT kernel's batch limit)."""
+        E = W0.shape[0]
+        shot = s_label.shape[1]
+        if imgs.shape[0] != E * (shot + 1) or E > 4:
+            raise ValueError("imgs must hold E*shot supports then E queries, E <= 4")
+        f_all, _ = self.model.extract_features(imgs)
+        f_s, f_q = f_all[:E * shot], f_all[E * shot:]
+        W = inner_adapt_batch(f_s, s_label, W0, self.lr, self.iters)
+        fqn, pred_q0 = normalize(f_q, W)
+        W2 = self.transformer(W, fqn, fqn)
         pred_q = classify(W2, fqn)
         iut, ce = seg_metrics(pred_q, q_label)
         iut0, _ = seg_metrics(pred_q0, q_label, with_ce=False)

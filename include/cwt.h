@@ -107,6 +107,16 @@ size_t cwt_workspace_bytes(cwt_ctx* ctx);
 int cwt_inner_adapt(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int n, int h, int w,
                     int C, int S, float lr, int iters, float* W_inout, void* stream);
 
+/*
+ * E independent inner loops (E episodes of n shots each) in the same launches: f_s NHWC
+ * [E*n,h,w,C] (episode-major), s_label int64 [E*n,S,S], W_inout [E,2,C].  Episode e's result
+ * is exactly what cwt_inner_adapt gives for its slices alone (its own class weight, W and
+ * gradient accumulators).  Throughput form of test.py:164-187 for several episodes in flight
+ * per GPU (the 200 dependent step launches are shared).  1 <= E <= 64.
+ */
+int cwt_inner_adapt_batch(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int E, int n, int h,
+                          int w, int C, int S, float lr, int iters, float* W_inout, void* stream);
+
 /* Per-pixel L2 normalisation over channels, F.normalize(f, dim=1) (test.py:194,
  * train.py:250): out[p,:] = f[p,:] / max(||f[p,:]||_2, 1e-12).  NHWC [P,C] -> [P,C].
  * If W0 (device [B,2,C]) and logits0 (device [B,2,P/B]) are non-NULL, also writes the

@@ -1,0 +1,66 @@
+"""Episodes in flight (cwt_inner_adapt_batch, EpisodeEngine.run_batch): E independent
+episodes sharing the backbone pass and the inner loop's step launches give each episode the
+result it gets alone.  Only the inner loop's fp32 atomic accumulation order differs between
+the two runs, so the bar is 1e-5 relative, and IoU counts may differ only on pixels whose
+logit margin is at that rounding level."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from few_shot_seg_cwt_amd import synthetic as syn  # noqa: E402
+
+SEED = 2021
+TOL = 1e-5
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("E,n,S,iters", [(3, 2, 65, 20), (2, 1, 129, 200), (4, 1, 33, 5)])
+def test_inner_adapt_batch_equals_single(dev, E, n, S, iters):
+    from few_shot_seg_cwt_amd.episode import inner_adapt, inner_adapt_batch
+    h = (S - 1) // 8 + 1
+    f = torch.from_numpy(syn.normal(5, f"fb{E}{n}{S}", (E * n, 512, h, h), 0.5)).abs().to(dev)
+    f = f.contiguous(memory_format=torch.channels_last)
+    lbl = torch.stack([torch.from_numpy(syn.make_episode(SEED, 40 + e, S, n)["s_label"][0]) for e in range(E)]).to(dev)
+    W0 = torch.from_numpy(syn.normal(6, f"wb{E}{n}{S}", (E, 2, 512), 0.04)).to(dev)
+    Wb = inner_adapt_batch(f, lbl, W0.clone(), 0.1, iters)
+    for e in range(E):
+        We = inner_adapt(f[e * n:(e + 1) * n], lbl[e], W0[e].clone(), 0.1, iters)
+        assert rel(Wb[e], We) < TOL, e
+
+
+def test_run_batch_equals_run(dev):
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, get_model
+    from few_shot_seg_cwt_amd.episode import EpisodeEngine
+    S, E, shot = 129, 3, 1
+    cfg = syn.cfg_defaults(image_size=S)
+    m = get_model(cfg).load_state_dict(syn.make_pspnet_state(50, SEED))
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    eng = EpisodeEngine(m, t, cfg)
+    eps = [syn.make_episode(SEED, 60 + e, S, shot) for e in range(E)]
+    W0 = torch.from_numpy(syn.normal(7, "wrb", (E, 2, 512), 0.04)).to(dev)
+    imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0] for ep in eps] + [ep["qry_img"] for ep in eps])).to(dev)
+    sl = torch.from_numpy(np.stack([ep["s_label"][0] for ep in eps])).to(dev)
+    ql = torch.from_numpy(np.concatenate([ep["q_label"] for ep in eps])).to(dev)
+    rb = eng.run_batch(imgs, sl, ql, W0.clone())
+    for e, ep in enumerate(eps):
+        x = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
+        r = eng.run(x, sl[e], ql[e:e + 1], W0[e].clone())
+        assert rel(rb["W"][e], r["W"]) < TOL
+        assert rel(rb["W2"][e], r["W2"][0]) < TOL
+        assert rel(rb["pred_q"][e], r["pred_q"][0]) < TOL
+        assert rel(rb["pred_q0"][e], r["pred_q0"][0]) < TOL
+        assert float((rb["iut"][e] - r["iut"][0]).abs().max()) <= 2
