@@ -56,6 +56,37 @@ def cpu_baseline(cfg, sd, tsd, budget_s: float = 25.0, max_eps: int = 4):
                       f"run_inference_episode (torch CPU fp32, {threads} threads); s/episode {dt / n:.2f}"}
 
 
+def cpu_baseline_train(cfg, sd, tsd, budget_s: float = 25.0, max_eps: int = 3):
+    """The oracle's training episode (inference pieces + CWT loss/gradients + SGD) on the
+    host cores, bounded sample."""
+    from few_shot_seg_cwt_amd import synthetic as syn
+    from oracle import cwt_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sdt, tsdt = O.to_torch_state(sd), O.to_torch_state(tsd)
+    classes = syn.coco_val_classes(0) if cfg["layers"] == 101 else None
+    eps = [syn.make_episode(2021, 100 + i, cfg["image_size"], cfg["shot"], classes) for i in range(max_eps + 1)]
+    W0 = torch.from_numpy(syn.normal(2021, "cpuW0", (2, 512, 1, 1), 0.04))
+
+    def one(ep):
+        r = O.run_inference_episode(ep, sdt, tsdt, W0, cfg)
+        _, grads, _ = O.cwt_train_step_grads(r["W"], r["f_q"], torch.from_numpy(ep["q_label"]), tsdt, cfg["heads"])
+        O.sgd_nesterov(tsdt, grads, {}, 0.001, 0.9, 1e-4)
+
+    one(eps[0])
+    t0 = time.time()
+    n = 0
+    for ep in eps[1:]:
+        one(ep)
+        n += 1
+        if time.time() - t0 > budget_s:
+            break
+    dt = time.time() - t0
+    return {"value": n / dt, "unit": "training episodes/s", "cores": threads, "kind": "port",
+            "sample": f"{n} training episodes (after 1 warm-up) through oracle/cwt_oracle.py (inference episode + "
+                      f"cwt_train_step_grads + sgd_nesterov, torch CPU fp32, {threads} threads); s/episode {dt / n:.2f}"}
+
+
 def pmc_traffic(dom_name: str):
     """HBM-side bytes per launch of the dominant kernel from the newest committed PMC summary
     (profiles/r*/pmc_summary.json, made by tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x 2 +
@@ -87,6 +118,9 @@ def main():
                     help="independent episodes processed together per step (EpisodeEngine.run_batch, <= 4)")
     ap.add_argument("--conv-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="conv-stack arithmetic: fp32 (reference numerics) or bf16 (config #5)")
+    ap.add_argument("--train", action="store_true",
+                    help="training episodes (do_epoch step: inner loop, CWT fwd/bwd, RCCL gradient all-reduce, SGD); "
+                         "BASELINE config #4 is --train --layers 101 --size 641")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-json", default=None, help="write per-launch records here (rank 0)")
     args = ap.parse_args()
@@ -98,7 +132,8 @@ def main():
 
     from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib, get_model
     from few_shot_seg_cwt_amd import synthetic as syn
-    from few_shot_seg_cwt_amd.episode import EpisodeEngine
+    from few_shot_seg_cwt_amd.episode import EpisodeEngine, TrainEngine
+    from few_shot_seg_cwt_amd.optimizer import get_optimizer
 
     _lib.load_library()
     S, shot, layers = args.size, args.shot, args.layers
@@ -111,6 +146,11 @@ def main():
     trans = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
     trans.load_state_dict(tsd)
     engine = EpisodeEngine(model, trans, cfg)
+    if args.train and args.inflight != 1:
+        raise SystemExit("--train runs one episode per rank per step (train.py batch_size 1)")
+    if args.train:
+        tengine = TrainEngine(model, trans, cfg)
+        opt = get_optimizer(cfg, [dict(params=[trans.flat], lr=cfg["trans_lr"] * cfg["scale_lr"])])
 
     # resident inputs: a pool of distinct episodes per rank + one W0 buffer per step
     classes = syn.coco_val_classes(0) if layers == 101 else None
@@ -130,6 +170,12 @@ def main():
 
     def step(i: int, Wbuf):
         imgs, sl, ql = pool[i % len(pool)]
+        if args.train:   # do_epoch iteration (train.py:188-267 + the all-reduce point of SURVEY §8(e))
+            trans.flat.grad.zero_() if trans.flat.grad is not None else None
+            r = tengine.step(imgs, sl[0], ql, Wbuf[0])
+            cdist.all_reduce_mean_(trans.flat.grad)
+            opt.step()
+            return r["loss"].view(1, 1, 1).expand(1, 2, 2)
         if E == 1:
             return engine.run(imgs, sl[0], ql, Wbuf[0])["iut"]
         return engine.run_batch(imgs, sl, ql, Wbuf)["iut"]
@@ -183,11 +229,12 @@ def main():
     _lib.profile_enable(0)
 
     out = {
-        "metric": ("episodes/sec (473x473, 1-shot, R50) at 1/2/4/8 MI355X; mIoU vs ref"
+        "metric": (f"training episodes/sec ({S}x{S}, {shot}-shot, R{layers})" if args.train else
+                   "episodes/sec (473x473, 1-shot, R50) at 1/2/4/8 MI355X; mIoU vs ref"
                    if (S, shot, layers) == (473, 1, 50) else f"episodes/sec ({S}x{S}, {shot}-shot, R{layers})")
         + (" [bf16 conv stack]" if args.conv_dtype == "bf16" else ""),
         "value": round(value, 3),
-        "unit": "episodes/s",
+        "unit": "training episodes/s" if args.train else "episodes/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -198,7 +245,9 @@ def main():
         "dtype": "fp32 (conv stack: bf16x3 split-fp32 on bf16 MFMA)" if conv_x3
         else "bf16 conv stack (fp32 accumulate) + fp32 inner loop / CWT / classifier" if conv_b16 else "fp32",
         "data": "synthetic (PRNG weights + PASCAL-shaped episodes, few_shot_seg_cwt_amd/synthetic.py)",
-        "config": {"workload": f"CWT inference episode (validate_transformer, batch_size_val=1): "
+        "config": {"workload": (f"CWT training episode (do_epoch, batch_size=1, RCCL mean all-reduce of the "
+                                f"8.39 MB gradient bucket + nesterov SGD per step): " if args.train else
+                                f"CWT inference episode (validate_transformer, batch_size_val=1): ") +
                                f"{'PASCAL split-0' if layers == 50 else 'COCO-20i split-0'} {shot}-shot "
                                f"ResNet-{layers} PSPNet {S}x{S}, adapt_iter 200, heads 4",
                    "image_size": S, "shot": shot, "layers": layers, "episodes_per_step_per_gpu": E,
@@ -216,13 +265,13 @@ def main():
                        "note": "whole extract_features bracket (convs + stem/maxpool/PPM byte kernels + gaps)"},
         "phases_ms_per_step": {"extract": round(ex_ms / args.steps, 3), "inner_adapt": round(ad_ms / args.steps, 3),
                                "attention": round(at_ms / args.steps, 3)},
-        "iou_fg_timed": round(float((iu[0, 1] / iu[1, 1].clamp_min(1)).item()), 4),
+        "iou_fg_timed": None if args.train else round(float((iu[0, 1] / iu[1, 1].clamp_min(1)).item()), 4),
     }
     if rank == 0 and args.profile_json:
         with open(args.profile_json, "w") as f:
             json.dump({"timed_records": recs, "per_launch_one_episode": fine}, f, indent=1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, sd, tsd)
+        out["cpu_baseline"] = cpu_baseline_train(cfg, sd, tsd) if args.train else cpu_baseline(cfg, sd, tsd)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -144,6 +144,8 @@ __global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, 
 // below offset by e * ADAPT_WSTRIDE / e * ADAPT_ESTRIDE floats.
 struct AdaptStepArgs {
   const AdaptDevArgs* dargs;
+  const float* f;        // the library's copy of f_s, NHWC [E][n][h][w][512] (a direct global pointer:
+                         // no per-step pointer chase, and global_load rather than flat_load)
   const uint8_t* lbl;    // [E][n][S][S]
   const AdaptScalars* sc;
   const float* w_src;    // W before the previous update ([2][512]); null at step 0 (dargs->w_in)
@@ -151,7 +153,7 @@ struct AdaptStepArgs {
   float* w_dst;          // block (0,0,0) stores the current W here (may be null)
   float* acc_cur;        // dW[1] replicas [R][512] of this step (zeroed)
   float* acc_zero;       // slot [R][512] to zero for the next step (may be null)
-  int h, w, S, nshot;
+  int h, w, S, nshot, nep;  // shots per episode, episodes
   float sy, sx;          // align_corners scales (h-1)/(S-1), (w-1)/(S-1)
   int nrep;              // replica rows in use
   int dbg;               // ablation flags for timing studies only (CWT_ADAPT_DBG): 1 skip replica
@@ -219,89 +221,131 @@ constexpr int ADAPT_T = 1024;                          // threads per step workg
 constexpr int ADAPT_NW = ADAPT_T / 64;                 // waves
 constexpr int ADAPT_PPW16 = (ADAPT_NP + ADAPT_NW - 1) / ADAPT_NW;  // lo pixels per wave (3)
 
-// One SGD step over one tile (lo-res rows r, r+1; columns cb*16 .. cb*16+16; shot n).
-// 16 waves: wave v owns hi-res row 8r + v/2 and 64 of the tile's 128 hi-res columns (one
-// pixel per lane; with S-1 == 8(h-1) the interpolation weights are exact multiples of 1/8,
-// so an aligned lane octet shares its two lo-res columns and is pre-reduced by DPP before
-// one lane adds it into LDS).  Wave 0 alone reads W and the R gradient replicas and
-// publishes the current W through LDS.  f for the tile stays in registers between the z
+// One SGD step over one spatial tile (lo-res rows r, r+1; columns cb*16 .. cb*16+16) of
+// every shot of G episodes (episode group blockIdx.z): the workgroup walks its T = G * shots
+// tiles in turn, prefetching tile k+1's f and labels while it computes tile k, and adds one
+// 2-KB dW row per episode.  (One workgroup per tile and shot would take ceil(T) rounds of
+// the whole grid; the walk shares the launch, the W publish and the reduction.)
+// Per tile, 16 waves: wave v owns hi-res row 8r + v/2 and 64 of the tile's 128 hi-res columns
+// (one pixel per lane; with S-1 == 8(h-1) the interpolation weights are exact multiples of
+// 1/8, so an aligned lane octet shares its two lo-res columns and is pre-reduced by DPP
+// before one lane adds it into LDS).  Wave g < G reads episode g's W and R gradient replicas
+// and publishes its current W through LDS.  f of the tile stays in registers between the z
 // pass and the dW pass.
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global loads (__syncthreads() would also drain vmcnt, i.e. wait for the next
+// tile's prefetch).  Every cross-wave exchange in the step kernel goes through LDS.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// The loads of a tile are branch-free (clamped addresses, validity applied at use) so that
+// they stay in flight across the previous tile's passes: a load under a divergent branch makes
+// the compiler drain vmcnt at the join.
+struct AdaptTile {
+  float fv[ADAPT_PPW16][8];  // pixels past the tile / image hold a clamped (finite) pixel: their
+                             // zd is never read and their gs stays 0
+  int y_main[2], y_extra[2];  // raw label bytes; y_in / y_ex_in below say which are real
+};
+
+template <int G>
 __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
   constexpr int C = 512;
-  __shared__ float wl[2][C];
+  __shared__ float wl[G][2][C];
   __shared__ float zd[2][ADAPT_CB + 1];  // z1 - z0: the softmax over two classes needs only the difference
-  __shared__ float gs[2][ADAPT_CB + 1];
+  __shared__ float gs[2][2][ADAPT_CB + 1];  // double-buffered over tiles
   __shared__ float red[ADAPT_NW][C];
   if (a.dbg & 16) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int cb = blockIdx.x, r = blockIdx.y;
-  const int ep = blockIdx.z / a.nshot, n = blockIdx.z - ep * a.nshot;
+  const int ep0 = blockIdx.z * G;
+  const int ng = min(G, a.nep - ep0);  // episodes of this group
+  const int T = ng * a.nshot;           // tiles walked
   const int ncb = gridDim.x;
   const int S = a.S;
-  const AdaptDevArgs* dargs = a.dargs + ep;
-  const AdaptScalars* scal = a.sc + ep;
-  const long eacc = ep * ADAPT_ESTRIDE, ew = (long)ep * ADAPT_WSTRIDE;
-
-  // ---- loads that do not depend on W: the tile's f pixels and this lane's labels ----
   const int x0 = cb * ADAPT_CB;
   const int ncol = min(ADAPT_CB + 1, a.w - x0);
-  const float* fimg = dargs->f + (long)n * a.h * a.w * C;
-  float fv[ADAPT_PPW16][8];
-#pragma unroll
-  for (int j = 0; j < ADAPT_PPW16; ++j) {
-    const int p = wv + ADAPT_NW * j;
-    const int ri = p / (ADAPT_CB + 1), xi = p % (ADAPT_CB + 1);
-    if (p < ADAPT_NP && xi < ncol && !(a.dbg & 8)) {
-      const float* src = fimg + ((long)(r + ri) * a.w + x0 + xi) * C + lane * 8;
-      const f32x4 u = *(const f32x4*)src, v = *(const f32x4*)(src + 4);
-      fv[j][0] = u[0]; fv[j][1] = u[1]; fv[j][2] = u[2]; fv[j][3] = u[3];
-      fv[j][4] = v[0]; fv[j][5] = v[1]; fv[j][6] = v[2]; fv[j][7] = v[3];
-    } else {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) fv[j][q] = 0.f;
-    }
-  }
-  const uint8_t* lbl = a.lbl + (long)blockIdx.z * S * S;
   const int x_begin = cb * 8 * ADAPT_CB;
   const int x_end = (cb == ncb - 1) ? S : x_begin + 8 * ADAPT_CB;
   const int Y = 8 * r + (wv >> 1);
   // rows 8r .. 8r+7 belong to this pair; the last pair also owns row S-1 (waves 0, 1)
   const bool extra = (r == a.h - 2) && (wv >> 1) == 0;
-  const int xw = x_begin + 64 * (wv & 1);   // wave-uniform column base (+128 per round)
+  const int xw = x_begin + 64 * (wv & 1);        // wave-uniform column base (+128 per round)
   const int nrounds = (x_end - xw + 127) / 128;  // 1, or 2 when the last block has 129 columns
-  int y_main[2], y_extra[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int X = xw + 128 * k + lane;
-    const bool in = k < nrounds && X < x_end;
-    y_main[k] = in ? lbl[(long)Y * S + X] : 255;
-    y_extra[k] = (in && extra) ? lbl[(long)(S - 1) * S + X] : 255;
-  }
-  const float wfg = scal->wfg;
+  const bool first_blk = (cb | r) == 0;          // the tile (0, 0) workgroup also keeps the episode's W history
 
-  // ---- current W (wave 0): W_src - lr_eff * sum of the previous step's replicas ----
-  if (wv == 0) {
-    const float lr = scal->lr_eff;
-    const float* wsrc = a.w_src ? a.w_src + ew : dargs->w_in;
+  // ---- loads that do not depend on W: the tile's f pixels and this lane's labels ----
+  bool y_in[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) y_in[kk] = kk < nrounds && xw + 128 * kk + lane < x_end;
+  auto load_tile = [&](AdaptTile& tl, int k) {
+    const float* fimg = a.f + (long)(ep0 * a.nshot + k) * a.h * a.w * C;
+#pragma unroll
+    for (int j = 0; j < ADAPT_PPW16; ++j) {
+      const int p = min(wv + ADAPT_NW * j, ADAPT_NP - 1);
+      const int ri = p / (ADAPT_CB + 1), xi = min(p % (ADAPT_CB + 1), ncol - 1);
+      const float* src = fimg + ((long)(r + ri) * a.w + x0 + xi) * C + lane * 8;
+      const f32x4 u = *(const f32x4*)src, v = *(const f32x4*)(src + 4);
+      tl.fv[j][0] = u[0]; tl.fv[j][1] = u[1]; tl.fv[j][2] = u[2]; tl.fv[j][3] = u[3];
+      tl.fv[j][4] = v[0]; tl.fv[j][5] = v[1]; tl.fv[j][6] = v[2]; tl.fv[j][7] = v[3];
+    }
+    const uint8_t* lbl = a.lbl + (long)(ep0 * a.nshot + k) * S * S;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int X = min(xw + 128 * kk + lane, S - 1);
+      tl.y_main[kk] = lbl[(long)Y * S + X];
+      tl.y_extra[kk] = lbl[(long)(S - 1) * S + X];
+    }
+  };
+  AdaptTile cur;
+  load_tile(cur, 0);
+  float wfg_g[G];  // class-1 CE weight per episode, read once (a load inside the tile loop would
+                   // drain the prefetch)
+#pragma unroll
+  for (int g = 0; g < G; ++g) wfg_g[g] = a.sc[ep0 + min(g, ng - 1)].wfg;
+
+  // ---- current W (wave g < ng, episode ep0 + g): W_src - lr_eff * sum of the previous step's replicas ----
+  if (wv < ng) {
+    const int ep = ep0 + wv;
+    const long eacc = ep * ADAPT_ESTRIDE, ew = (long)ep * ADAPT_WSTRIDE;
+    const float lr = a.sc[ep].lr_eff;
+    const float* wsrc = a.w_src ? a.w_src + ew : a.dargs[ep].w_in;
     f32x4 w0a = *(const f32x4*)(wsrc + lane * 8), w0b = *(const f32x4*)(wsrc + lane * 8 + 4);
     f32x4 w1a = *(const f32x4*)(wsrc + C + lane * 8), w1b = *(const f32x4*)(wsrc + C + lane * 8 + 4);
     if (a.acc_prev && !(a.dbg & 1)) {
       f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+      const float* ap = a.acc_prev + eacc + lane * 8;
+      if (a.nrep == ADAPT_R_DEFAULT) {  // all replica loads in flight together
+        f32x4 v0[ADAPT_R_DEFAULT], v1[ADAPT_R_DEFAULT];
+#pragma unroll
+        for (int rr = 0; rr < ADAPT_R_DEFAULT; ++rr) {
+          v0[rr] = *(const f32x4*)(ap + rr * 512);
+          v1[rr] = *(const f32x4*)(ap + rr * 512 + 4);
+        }
+#pragma unroll
+        for (int rr = 0; rr < ADAPT_R_DEFAULT; ++rr) {
+          d0 += v0[rr];
+          d1 += v1[rr];
+        }
+      } else {
 #pragma unroll 4
-      for (int rr = 0; rr < a.nrep; ++rr) {
-        d0 += *(const f32x4*)(a.acc_prev + eacc + rr * 512 + lane * 8);
-        d1 += *(const f32x4*)(a.acc_prev + eacc + rr * 512 + lane * 8 + 4);
+        for (int rr = 0; rr < a.nrep; ++rr) {
+          d0 += *(const f32x4*)(ap + rr * 512);
+          d1 += *(const f32x4*)(ap + rr * 512 + 4);
+        }
       }
       w1a -= lr * d0;
       w0a += lr * d0;
       w1b -= lr * d1;
       w0b += lr * d1;
     }
-    *(f32x4*)&wl[0][lane * 8] = w0a;
-    *(f32x4*)&wl[0][lane * 8 + 4] = w0b;
-    *(f32x4*)&wl[1][lane * 8] = w1a;
-    *(f32x4*)&wl[1][lane * 8 + 4] = w1b;
-    if ((cb | r | n) == 0 && a.w_dst) {
+    *(f32x4*)&wl[wv][0][lane * 8] = w0a;
+    *(f32x4*)&wl[wv][0][lane * 8 + 4] = w0b;
+    *(f32x4*)&wl[wv][1][lane * 8] = w1a;
+    *(f32x4*)&wl[wv][1][lane * 8 + 4] = w1b;
+    if (first_blk && a.w_dst) {
       float* wd = a.w_dst + ew;
       *(f32x4*)(wd + lane * 8) = w0a;
       *(f32x4*)(wd + lane * 8 + 4) = w0b;
@@ -309,102 +353,121 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
       *(f32x4*)(wd + C + lane * 8 + 4) = w1b;
     }
   }
-  if ((cb | r | n) == 0 && a.acc_zero)
-    for (int i = t; i < a.nrep * 128; i += ADAPT_T) ((f32x4*)(a.acc_zero + eacc))[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (t < ADAPT_NP) (&gs[0][0])[t] = 0.f;
-  __syncthreads();
+  if (first_blk && a.acc_zero)
+    for (int g = 0; g < ng; ++g)
+      for (int i = t; i < a.nrep * 128; i += ADAPT_T)
+        ((f32x4*)(a.acc_zero + (ep0 + g) * ADAPT_ESTRIDE))[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (t < ADAPT_NP) (&gs[0][0][0])[t] = 0.f;
+  lds_barrier();
 
-  // ---- zd = (W1 - W0) . f for the tile's low-res pixels ----
-  {
-    float dw[8];
-    const f32x4 a0 = *(const f32x4*)&wl[0][lane * 8], b0 = *(const f32x4*)&wl[0][lane * 8 + 4];
-    const f32x4 a1 = *(const f32x4*)&wl[1][lane * 8], b1 = *(const f32x4*)&wl[1][lane * 8 + 4];
+  const float inv8 = 0.125f;
+  float d[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      dw[q] = a1[q] - a0[q];
-      dw[4 + q] = b1[q] - b0[q];
-    }
-    float sd[ADAPT_PPW16];
-#pragma unroll
-    for (int j = 0; j < ADAPT_PPW16; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) s = fmaf(dw[q], fv[j][q], s);
-      sd[j] = s;
-    }
-#pragma unroll
-    for (int j = 0; j < ADAPT_PPW16; ++j) sd[j] = wave_sum_dpp(sd[j]);  // independent chains interleave
-#pragma unroll
-    for (int j = 0; j < ADAPT_PPW16; ++j) {
-      const int p = wv + ADAPT_NW * j;
-      if (p < ADAPT_NP && lane == 0) (&zd[0][0])[p] = sd[j];
-    }
-  }
-  __syncthreads();
+  for (int q = 0; q < 8; ++q) d[q] = 0.f;
+  for (int k = 0; k < T; ++k) {
+    const int g = k / a.nshot, n = k - g * a.nshot;
+    const int buf = k & 1;
+    AdaptTile nxt;
+    if (k + 1 < T) load_tile(nxt, k + 1);  // in flight during this tile's passes
 
-  // ---- hi-res pass: weighted-CE gradient, bilinear adjoint into gs (class-1 component) ----
-  if (!(a.dbg & 2)) {
+    // ---- zd = (W1 - W0) . f for the tile's low-res pixels ----
+    {
+      float dw[8];
+      const f32x4 a0 = *(const f32x4*)&wl[g][0][lane * 8], b0 = *(const f32x4*)&wl[g][0][lane * 8 + 4];
+      const f32x4 a1 = *(const f32x4*)&wl[g][1][lane * 8], b1 = *(const f32x4*)&wl[g][1][lane * 8 + 4];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (k >= nrounds) break;  // wave-uniform
-      const int X = xw + 128 * k + lane;
-      const bool xin = X < x_end;
-      // x interpolation, exact: S-1 == 8(w-1) so src = X/8
-      const int ix = min(X >> 3, a.w - 1);
-      const int xi0 = ix - x0, xi1 = (ix < a.w - 1) ? xi0 + 1 : xi0;
-      const float lx1 = (float)(X & 7) * 0.125f, lx0 = 1.f - lx1;
+      for (int q = 0; q < 4; ++q) {
+        dw[q] = a1[q] - a0[q];
+        dw[4 + q] = b1[q] - b0[q];
+      }
+      float sd[ADAPT_PPW16];
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        if (e == 1 && !extra) break;  // wave-uniform
-        const int y = e ? y_extra[k] : y_main[k];
-        // row S-1 reads lo row r+1 with weight 1; rows 8r+i read rows r, r+1 with (1-i/8, i/8)
-        const int ri0 = e, ri1 = 1;
-        const float ly1 = e ? 0.f : (float)(Y & 7) * 0.125f, ly0 = 1.f - ly1;
-        float g = 0.f;
-        if (xin && y != 255) {
-          const float d = ly0 * (lx0 * zd[ri0][xi0] + lx1 * zd[ri0][xi1]) + ly1 * (lx0 * zd[ri1][xi0] + lx1 * zd[ri1][xi1]);
-          const float p1 = 1.f / (1.f + __expf(-d));
-          g = ((y == 1) ? wfg : 1.f) * (p1 - (float)y);
-        }
-        // ly0 / ly1 are wave-uniform: reduce lx * g over the octet once, scale per row after
-        const float sa = octet_sum(lx0 * g), sb = octet_sum(lx1 * g);
-        const float v00 = ly0 * sa, v01 = ly0 * sb, v10 = ly1 * sa, v11 = ly1 * sb;
-        if ((lane & 7) == 0 && xin) {
-          if (e == 0) {
-            atomicAdd(&gs[0][xi0], v00);
-            atomicAdd(&gs[0][xi1], v01);
+      for (int j = 0; j < ADAPT_PPW16; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s = fmaf(dw[q], cur.fv[j][q], s);
+        sd[j] = s;
+      }
+#pragma unroll
+      for (int j = 0; j < ADAPT_PPW16; ++j) sd[j] = wave_sum_dpp(sd[j]);  // independent chains interleave
+#pragma unroll
+      for (int j = 0; j < ADAPT_PPW16; ++j) {
+        const int p = wv + ADAPT_NW * j;
+        if (p < ADAPT_NP && lane == 0) (&zd[0][0])[p] = sd[j];
+      }
+    }
+    lds_barrier();
+    // the other gs buffer was last read by the previous tile's dW pass, which every thread
+    // finished before the barrier above
+    if (t < ADAPT_NP) (&gs[buf ^ 1][0][0])[t] = 0.f;
+
+    // ---- hi-res pass: weighted-CE gradient, bilinear adjoint into gs (class-1 component) ----
+    if (!(a.dbg & 2)) {
+      const float wfg = G == 1 ? wfg_g[0] : (g == 0 ? wfg_g[0] : wfg_g[G - 1]);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (kk >= nrounds) break;  // wave-uniform
+        const int X = xw + 128 * kk + lane;
+        const bool xin = X < x_end;
+        // x interpolation, exact: S-1 == 8(w-1) so src = X/8
+        const int ix = min(X >> 3, a.w - 1);
+        const int xi0 = ix - x0, xi1 = (ix < a.w - 1) ? xi0 + 1 : xi0;
+        const float lx1 = (float)(X & 7) * inv8, lx0 = 1.f - lx1;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          if (e == 1 && !extra) break;  // wave-uniform
+          const int y = !y_in[kk] ? 255 : e ? cur.y_extra[kk] : cur.y_main[kk];
+          // row S-1 reads lo row r+1 with weight 1; rows 8r+i read rows r, r+1 with (1-i/8, i/8)
+          const int ri0 = e, ri1 = 1;
+          const float ly1 = e ? 0.f : (float)(Y & 7) * inv8, ly0 = 1.f - ly1;
+          float gv = 0.f;
+          if (xin && y != 255) {
+            const float dd = ly0 * (lx0 * zd[ri0][xi0] + lx1 * zd[ri0][xi1]) + ly1 * (lx0 * zd[ri1][xi0] + lx1 * zd[ri1][xi1]);
+            const float p1 = __builtin_amdgcn_rcpf(1.f + __expf(-dd));
+            gv = ((y == 1) ? wfg : 1.f) * (p1 - (float)y);
           }
-          atomicAdd(&gs[1][xi0], v10 + (e ? v00 : 0.f));
-          atomicAdd(&gs[1][xi1], v11 + (e ? v01 : 0.f));
+          // ly0 / ly1 are wave-uniform: reduce lx * g over the octet once, scale per row after
+          const float sa = octet_sum(lx0 * gv), sb = octet_sum(lx1 * gv);
+          const float v00 = ly0 * sa, v01 = ly0 * sb, v10 = ly1 * sa, v11 = ly1 * sb;
+          if ((lane & 7) == 0 && xin) {
+            if (e == 0) {
+              atomicAdd(&gs[buf][0][xi0], v00);
+              atomicAdd(&gs[buf][0][xi1], v01);
+            }
+            atomicAdd(&gs[buf][1][xi0], v10 + (e ? v00 : 0.f));
+            atomicAdd(&gs[buf][1][xi1], v11 + (e ? v01 : 0.f));
+          }
         }
       }
     }
-  }
-  __syncthreads();
+    lds_barrier();
 
-  // ---- dW[1] partial = sum_p g[p] f[p] over the tile ----
-  {
-    float d[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) d[q] = 0.f;
+    // ---- dW[1] partial += sum_p g[p] f[p] over the tile ----
 #pragma unroll
     for (int j = 0; j < ADAPT_PPW16; ++j) {
       const int p = wv + ADAPT_NW * j;
       if (p < ADAPT_NP) {
-        const float g = (&gs[0][0])[p];
+        const float gp = (&gs[buf][0][0])[p];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) d[q] = fmaf(g, fv[j][q], d[q]);
+        for (int q = 0; q < 8; ++q) d[q] = fmaf(gp, cur.fv[j][q], d[q]);
       }
     }
-    *(f32x4*)&red[wv][lane * 8] = f32x4{d[0], d[1], d[2], d[3]};
-    *(f32x4*)&red[wv][lane * 8 + 4] = f32x4{d[4], d[5], d[6], d[7]};
-  }
-  __syncthreads();
-  if (t < C && !(a.dbg & 4)) {
-    float s = 0.f;
+    if (n == a.nshot - 1) {  // last shot of episode ep0 + g: reduce over waves, one 2-KB atomic row
+      *(f32x4*)&red[wv][lane * 8] = f32x4{d[0], d[1], d[2], d[3]};
+      *(f32x4*)&red[wv][lane * 8 + 4] = f32x4{d[4], d[5], d[6], d[7]};
 #pragma unroll
-    for (int v = 0; v < ADAPT_NW; ++v) s += red[v][t];
-    atomicAdd(&a.acc_cur[eacc + ((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * n)) % a.nrep) * 512 + t], s);
+      for (int q = 0; q < 8; ++q) d[q] = 0.f;
+      lds_barrier();
+      if (t < C && !(a.dbg & 4)) {
+        float s = 0.f;
+#pragma unroll
+        for (int v = 0; v < ADAPT_NW; ++v) s += red[v][t];
+        atomicAdd(&a.acc_cur[(ep0 + g) * ADAPT_ESTRIDE + ((blockIdx.x + gridDim.x * blockIdx.y) % a.nrep) * 512 + t],
+                  s);
+      }
+      // red is rewritten only after the next episode's tiles, i.e. after >= 2 more barriers
+    }
+    if (k + 1 < T) cur = nxt;
   }
 }
 
@@ -427,16 +490,19 @@ __global__ void adapt_final_kernel(const float* w_src, const float* acc, const A
 }
 
 // The 200 step launches + the final update, enqueued on `st` (directly or while capturing).
-static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws, const AdaptScalars* sc, float* acc3,
-                               float* wbuf, int E, int n, int h, int w, int S, int iters, hipStream_t st) {
+static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const float* f_ws, const uint8_t* lbl_ws,
+                               const AdaptScalars* sc, float* acc3, float* wbuf, int E, int n, int h, int w, int S,
+                               int iters, hipStream_t st) {
   AdaptStepArgs a;
   a.dargs = dargs;
+  a.f = f_ws;
   a.lbl = lbl_ws;
   a.sc = sc;
   a.h = h;
   a.w = w;
   a.S = S;
   a.nshot = n;
+  a.nep = E;
   a.sy = align_corners_scale(h, S);
   a.sx = align_corners_scale(w, S);
   const char* dbg = getenv("CWT_ADAPT_DBG");
@@ -445,14 +511,20 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const uint8_t* lbl_ws,
   a.nrep = nr ? atoi(nr) : ADAPT_R_DEFAULT;
   if (a.nrep != 4 && a.nrep != 8 && a.nrep != 16 && a.nrep != 32) a.nrep = ADAPT_R_DEFAULT;
   const int ncb = cdiv(S - 1, 8 * ADAPT_CB);
-  dim3 grid(ncb, h - 1, E * n);
+  // episodes per workgroup: 2 when there are several (shares the launch between them)
+  const char* gs_env = getenv("CWT_ADAPT_G");
+  const int G = (gs_env ? atoi(gs_env) : 2) >= 2 && E > 1 ? 2 : 1;
+  dim3 grid(ncb, h - 1, cdiv(E, G));
   for (int s = 0; s < iters; ++s) {
     a.w_src = (s == 0) ? nullptr : wbuf + ((s - 1) & 1) * 1024;
     a.acc_prev = (s == 0) ? nullptr : acc3 + ((s - 1) % 3) * ADAPT_SLOT;
     a.w_dst = wbuf + (s & 1) * 1024;
     a.acc_cur = acc3 + (s % 3) * ADAPT_SLOT;
     a.acc_zero = acc3 + ((s + 1) % 3) * ADAPT_SLOT;
-    hipLaunchKernelGGL(adapt_step_kernel, grid, dim3(ADAPT_T), 0, st, a);
+    if (G == 2)
+      hipLaunchKernelGGL(adapt_step_kernel<2>, grid, dim3(ADAPT_T), 0, st, a);
+    else
+      hipLaunchKernelGGL(adapt_step_kernel<1>, grid, dim3(ADAPT_T), 0, st, a);
     CWT_LAUNCH_CHECK();
   }
   const int last = iters - 1;
@@ -467,7 +539,9 @@ AdaptGraphCache::~AdaptGraphCache() {
   if (cap_stream) (void)hipStreamDestroy(cap_stream);
 }
 
-size_t adapt_ws_sizes(int E, int n, int S, size_t* lbl, size_t* sc, size_t* acc, size_t* wbuf, size_t* dargs) {
+size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lbl, size_t* sc, size_t* acc,
+                      size_t* wbuf, size_t* dargs) {
+  *fws = (size_t)E * n * h * w * 512 * sizeof(float);
   *lbl = (size_t)E * n * S * S;
   *sc = (size_t)E * (sizeof(AdaptScalars) + 2 * PREP_MAXBLK * sizeof(unsigned long long)) + 64;
   *acc = (size_t)E * ADAPT_ESTRIDE * sizeof(float);
@@ -478,10 +552,13 @@ size_t adapt_ws_sizes(int E, int n, int S, size_t* lbl, size_t* sc, size_t* acc,
 
 // E episodes of n shots each: f [E][n][h][w][512], lbl64 [E][n][S][S], W [E][2][512].
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
-                 float* W, uint8_t* lbl_ws, AdaptScalars* sc /*[E] + partial counts*/,
+                 float* W, float* f_ws /*[E][n][h][w][512]*/, uint8_t* lbl_ws, AdaptScalars* sc /*[E] + partial counts*/,
                  float* acc3 /*[E][3][R][512]*/, float* wbuf /*[E][2][2][512]*/, AdaptDevArgs* dargs /*[E]*/,
                  AdaptGraphCache* cache, hipStream_t st) {
   const long total = (long)n * S * S;  // labels per episode
+  // the step graph reads f from the library's buffer (fixed address, baked into the graph)
+  if (iters > 0 && f != f_ws)
+    CWT_HIP(hipMemcpyAsync(f_ws, f, (size_t)E * n * h * w * 512 * sizeof(float), hipMemcpyDeviceToDevice, st));
   unsigned long long* part = (unsigned long long*)(sc + E);  // [E][PREP_MAXBLK][2] after the scalars
   const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
   hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks, E), dim3(1024), 0, st, lbl64, total, lbl_ws, part);
@@ -491,10 +568,10 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
                      iters > 0 ? acc3 : (float*)nullptr, ADAPT_ESTRIDE, ADAPT_SLOT, (double*)nullptr);
   CWT_LAUNCH_CHECK();
   if (iters <= 0) return 0;
-  if (!cache) return enqueue_adapt_steps(dargs, lbl_ws, sc, acc3, wbuf, E, n, h, w, S, iters, st);
+  if (!cache) return enqueue_adapt_steps(dargs, f_ws, lbl_ws, sc, acc3, wbuf, E, n, h, w, S, iters, st);
   // graph path: one instantiated graph per (geometry, workspace pointers)
-  AdaptGraphCache::Entry key{E, n, h, w, S, iters, (const void*)lbl_ws, (const void*)sc, (const void*)acc3,
-                             (const void*)wbuf, (const void*)dargs, nullptr};
+  AdaptGraphCache::Entry key{E, n, h, w, S, iters, (const void*)f_ws, (const void*)lbl_ws, (const void*)sc,
+                             (const void*)acc3, (const void*)wbuf, (const void*)dargs, nullptr};
   hipGraphExec_t exec = nullptr;
   for (auto& e : cache->entries)
     if (e.same(key)) exec = e.exec;
@@ -502,7 +579,7 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
     if (!cache->cap_stream) CWT_HIP(hipStreamCreateWithFlags(&cache->cap_stream, hipStreamNonBlocking));
     hipGraph_t g;
     CWT_HIP(hipStreamBeginCapture(cache->cap_stream, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_adapt_steps(dargs, lbl_ws, sc, acc3, wbuf, E, n, h, w, S, iters, cache->cap_stream);
+    int rc = enqueue_adapt_steps(dargs, f_ws, lbl_ws, sc, acc3, wbuf, E, n, h, w, S, iters, cache->cap_stream);
     hipError_t e2 = hipStreamEndCapture(cache->cap_stream, &g);
     if (rc) return rc;
     if (e2 != hipSuccess) return fail((int)e2, std::string("adapt graph capture: ") + hipGetErrorString(e2));

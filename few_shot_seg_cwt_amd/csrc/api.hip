@@ -28,9 +28,10 @@ int fail(int code, const std::string& msg) {
 struct AdaptScalars;
 struct AdaptDevArgs;
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
-                 float* W, uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf, AdaptDevArgs* dargs,
-                 AdaptGraphCache* cache, hipStream_t st);
-size_t adapt_ws_sizes(int E, int n, int S, size_t* lbl, size_t* sc, size_t* acc, size_t* wbuf, size_t* dargs);
+                 float* W, float* f_ws, uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf,
+                 AdaptDevArgs* dargs, AdaptGraphCache* cache, hipStream_t st);
+size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lbl, size_t* sc, size_t* acc,
+                      size_t* wbuf, size_t* dargs);
 int launch_seg_ce(const float* logits, const int64_t* target, int B, int h, int w, int S, float* loss_out,
                   float* dlogits, uint8_t* lbl_ws, AdaptScalars* sc, double* loss_num, hipStream_t st);
 int launch_normalize(const float* f, int B, int Pb, float* out, const float* W0, float* logits0, hipStream_t st);
@@ -780,10 +781,11 @@ int cwt_inner_adapt_batch(cwt_ctx* ctx, const float* f_s, const int64_t* s_label
   CWT_CHECK(E >= 1 && E <= 64 && n >= 1 && h >= 2 && w >= 2 && iters >= 0, "bad sizes");
   CWT_CHECK(S - 1 == 8 * (h - 1) && S - 1 == 8 * (w - 1), "need S-1 == 8*(h-1) == 8*(w-1)");
   CWT_HIP(hipSetDevice(ctx->device));
-  void *lbl, *sc, *acc, *wb, *dargs;
-  size_t b_lbl, b_sc, b_acc, b_wb, b_args;
-  adapt_ws_sizes(E, n, S, &b_lbl, &b_sc, &b_acc, &b_wb, &b_args);
+  void *fws, *lbl, *sc, *acc, *wb, *dargs;
+  size_t b_f, b_lbl, b_sc, b_acc, b_wb, b_args;
+  adapt_ws_sizes(E, n, h, w, S, &b_f, &b_lbl, &b_sc, &b_acc, &b_wb, &b_args);
   int rc;
+  if ((rc = ensure_ws(ctx, "adapt.f", b_f, &fws))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.args", b_args, &dargs))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.lbl", b_lbl, &lbl))) return rc;
   if ((rc = ensure_ws(ctx, "adapt.sc", b_sc, &sc))) return rc;
@@ -793,8 +795,8 @@ int cwt_inner_adapt_batch(cwt_ctx* ctx, const float* f_s, const int64_t* s_label
   Prof p(ctx, (hipStream_t)stream, "inner_adapt x" + std::to_string(iters) + (E > 1 ? " E=" + std::to_string(E) : ""),
          (double)E * iters * 2.0 * (4.0 * C * h * w * n), (double)E * iters * ((double)n * h * w * C * 4 + (double)n * S * S),
          1);
-  rc = launch_adapt(f_s, s_label, E, n, h, w, S, lr, iters, W_inout, (uint8_t*)lbl, (AdaptScalars*)sc, (float*)acc,
-                    (float*)wb, (AdaptDevArgs*)dargs, ctx->use_graph ? &ctx->adapt_graphs : nullptr,
+  rc = launch_adapt(f_s, s_label, E, n, h, w, S, lr, iters, W_inout, (float*)fws, (uint8_t*)lbl, (AdaptScalars*)sc,
+                    (float*)acc, (float*)wb, (AdaptDevArgs*)dargs, ctx->use_graph ? &ctx->adapt_graphs : nullptr,
                     (hipStream_t)stream);
   p.end();
   return rc;

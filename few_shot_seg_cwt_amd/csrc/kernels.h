@@ -133,11 +133,11 @@ int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipSt
 struct AdaptGraphCache {
   struct Entry {
     int E, n, h, w, S, iters;
-    const void *lbl, *sc, *acc, *wbuf, *dargs;
+    const void *fws, *lbl, *sc, *acc, *wbuf, *dargs;
     hipGraphExec_t exec;
     bool same(const Entry& o) const {
-      return E == o.E && n == o.n && h == o.h && w == o.w && S == o.S && iters == o.iters && lbl == o.lbl &&
-             sc == o.sc && acc == o.acc && wbuf == o.wbuf && dargs == o.dargs;
+      return E == o.E && n == o.n && h == o.h && w == o.w && S == o.S && iters == o.iters && fws == o.fws &&
+             lbl == o.lbl && sc == o.sc && acc == o.acc && wbuf == o.wbuf && dargs == o.dargs;
     }
   };
   std::vector<Entry> entries;

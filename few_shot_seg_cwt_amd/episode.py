@@ -169,6 +169,38 @@ class EpisodeEngine:
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, f_s=f_s, f_q=f_q)
 
 
+class TrainEngine:
+    """Device-resident CWT training episode (train.py:188-267 without the host-side batch
+    transfer): the backbone and inner loop as in inference, then CWT forward with saved
+    state, classifier, query CE forward/backward, classifier and CWT backward; gradients
+    ACCUMULATE into transformer.flat.grad.  The all-reduce and the optimiser step are the
+    caller's (do_epoch, bench.py --train)."""
+
+    def __init__(self, model, transformer, args):
+        self.model, self.transformer = model, transformer
+        self.lr = float(_a(args, "cls_lr", 0.1))
+        self.iters = int(_a(args, "adapt_iter", 200))
+
+    def step(self, imgs: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor, W0: torch.Tensor) -> dict:
+        shot = imgs.shape[0] - 1
+        t = self.transformer
+        if t.flat.grad is None:
+            t.flat.grad = torch.zeros_like(t.flat)
+        with torch.no_grad():
+            f_all, _ = self.model.extract_features(imgs)
+            f_s, f_q = f_all[:shot], f_all[shot:]
+            W = inner_adapt(f_s, s_label, W0, self.lr, self.iters)
+            Wb = W.view(1, 2, -1)
+            fqn, pred_q0 = normalize(f_q, Wb)
+            W2, state = t.forward_train(Wb, fqn)
+            pred_q = classify(W2, fqn)
+            loss, dl = seg_ce_fwd_bwd(pred_q, q_label)
+            dW2 = torch.zeros_like(W2)
+            classify_bwd(dl, fqn, dW2)
+            t.backward_into(state, dW2)
+        return dict(loss=loss, W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0)
+
+
 def new_binary_classifier_weight(bottleneck_dim: int = 512, num_classes: int = 2) -> torch.Tensor:
     """W0 exactly as the reference draws it: nn.Conv2d(512, 2, 1, bias=False) constructed on the
     host from the global torch RNG (test.py:164; train.py:206), returned as [2,512]."""
