@@ -9,7 +9,7 @@ mkdir -p $OUT
 run_pass() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $OUT/$name -o run -- \
-    python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/$name.bench.json 2> $OUT/$name.err
+    python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/$name.bench.json 2> $OUT/$name.err
   local rc=$?
   echo "pass $name rc=$rc"
   return $rc

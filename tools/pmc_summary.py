@@ -3,7 +3,7 @@ the gfx950 corrections of MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) x 1024 x 2 
 128-B requests at 64 B), WRITE_SIZE (KB) x 1024 as is.  traffic = fetch + write bytes per
 launch (memory-side L2 traffic; Infinity-Cache hits are included).
 
-    python tools/pmc_summary.py gpurun_out/pmc_r1b profiles/r1/pmc_summary.json
+    python tools/pmc_summary.py gpurun_out/pmc_r1b[,gpurun_out/pmc_r1b_bf16] profiles/r1/pmc_summary.json
 """
 import collections
 import csv
@@ -19,18 +19,21 @@ def load(path):
     return d
 
 
-def main(src, dst):
+def main(srcs, dst):
+    """srcs: one pass directory, or several separated by commas (e.g. the fp32 and the bf16
+    bench runs: their conv kernels have different names, so the summaries merge)."""
     out = collections.defaultdict(dict)
-    for ps in ("fetch", "write", "sq", "lds"):
-        p = os.path.join(src, ps, "run_counter_collection.csv")
-        if not os.path.exists(p):
-            continue
-        for k, cs in load(p).items():
-            if not k.startswith(("cwt::", "void cwt::")):
+    for src in srcs.split(","):
+        for ps in ("fetch", "write", "sq", "lds"):
+            p = os.path.join(src, ps, "run_counter_collection.csv")
+            if not os.path.exists(p):
                 continue
-            for c, v in cs.items():
-                out[k][c] = sum(v) / len(v)
-                out[k]["launches"] = len(v)
+            for k, cs in load(p).items():
+                if not k.startswith(("cwt::", "void cwt::")):
+                    continue
+                for c, v in cs.items():
+                    out[k][c] = sum(v) / len(v)
+                    out[k]["launches"] = len(v)
     res = {}
     for k, cs in out.items():
         e = dict(cs)
