@@ -85,6 +85,7 @@ constexpr int ADAPT_RMAX = 32;                 // replica rows allocated per slo
 constexpr int ADAPT_R_DEFAULT = 8;             // replica rows used (CWT_ADAPT_R overrides: 4, 8, 16 or 32)
 constexpr int ADAPT_SLOT = ADAPT_RMAX * 512;   // floats per accumulator slot
 constexpr int ADAPT_NP = 2 * (ADAPT_CB + 1);
+constexpr int ADAPT_NSTAMP = 10;  // timing-study stamps per (step, workgroup)
 constexpr long ADAPT_ESTRIDE = 3L * ADAPT_SLOT;  // accumulator floats per episode (3 slots)
 constexpr int ADAPT_WSTRIDE = 2 * 1024;          // W ping-pong floats per episode
 constexpr int ADAPT_PPW = (ADAPT_NP + 3) / 4;  // lo pixels per wave
@@ -156,6 +157,8 @@ struct AdaptStepArgs {
   int h, w, S, nshot, nep;  // shots per episode, episodes
   float sy, sx;          // align_corners scales (h-1)/(S-1), (w-1)/(S-1)
   int nrep;              // replica rows in use
+  unsigned long long* stamps;  // CWT_ADAPT_DBG & 32: per (step, workgroup) ADAPT_NSTAMP clock stamps
+  int step;
   int dbg;               // ablation flags for timing studies only (CWT_ADAPT_DBG): 1 skip replica
                          // reads, 2 skip the high-res pass, 4 skip the global atomics, 8 skip f loads,
                          // 16 return at entry
@@ -260,6 +263,16 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
   if (a.dbg & 16) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int cb = blockIdx.x, r = blockIdx.y;
+  unsigned long long* stp = nullptr;  // timing study (CWT_ADAPT_DBG & 32): wave 0's clock at each phase
+  if ((a.dbg & 32) && t == 0) {
+    stp = a.stamps + ((long)a.step * gridDim.x * gridDim.y * gridDim.z + blockIdx.x +
+                      gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * ADAPT_NSTAMP;
+    stp[0] = __builtin_amdgcn_s_memrealtime();
+    stp[1] = __builtin_amdgcn_s_memtime();
+  }
+  auto stamp = [&](int i) {
+    if (stp) stp[i] = __builtin_amdgcn_s_memtime();
+  };
   const int ep0 = blockIdx.z * G;
   const int ng = min(G, a.nep - ep0);  // episodes of this group
   const int T = ng * a.nshot;           // tiles walked
@@ -358,12 +371,18 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
       for (int i = t; i < a.nrep * 128; i += ADAPT_T)
         ((f32x4*)(a.acc_zero + (ep0 + g) * ADAPT_ESTRIDE))[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (t < ADAPT_NP) (&gs[0][0][0])[t] = 0.f;
+  stamp(2);
   lds_barrier();
+  stamp(3);
 
   const float inv8 = 0.125f;
   float d[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) d[q] = 0.f;
+  if (stp) {  // timing study: when tile 0's f and labels have landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stp[9] = __builtin_amdgcn_s_memtime();
+  }
   for (int k = 0; k < T; ++k) {
     const int g = k / a.nshot, n = k - g * a.nshot;
     const int buf = k & 1;
@@ -397,6 +416,7 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
       }
     }
     lds_barrier();
+    if (k == 0) stamp(4);
     // the other gs buffer was last read by the previous tile's dW pass, which every thread
     // finished before the barrier above
     if (t < ADAPT_NP) (&gs[buf ^ 1][0][0])[t] = 0.f;
@@ -441,6 +461,7 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
       }
     }
     lds_barrier();
+    if (k == 0) stamp(5);
 
     // ---- dW[1] partial += sum_p g[p] f[p] over the tile ----
 #pragma unroll
@@ -458,6 +479,7 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) d[q] = 0.f;
       lds_barrier();
+      if (k == 0) stamp(6);
       if (t < C && !(a.dbg & 4)) {
         float s = 0.f;
 #pragma unroll
@@ -468,6 +490,11 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
       // red is rewritten only after the next episode's tiles, i.e. after >= 2 more barriers
     }
     if (k + 1 < T) cur = nxt;
+  }
+  if (stp) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // thread 0's atomic has been performed
+    stp[7] = __builtin_amdgcn_s_memtime();
+    stp[8] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -490,6 +517,10 @@ __global__ void adapt_final_kernel(const float* w_src, const float* acc, const A
 }
 
 // The 200 step launches + the final update, enqueued on `st` (directly or while capturing).
+// timing study buffer (CWT_ADAPT_DBG & 32), read back by cwt_debug_adapt_stamps
+unsigned long long* g_adapt_stamps = nullptr;
+long g_adapt_stamps_n = 0;
+
 static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const float* f_ws, const uint8_t* lbl_ws,
                                const AdaptScalars* sc, float* acc3, float* wbuf, int E, int n, int h, int w, int S,
                                int iters, hipStream_t st) {
@@ -507,6 +538,7 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const float* f_ws, con
   a.sx = align_corners_scale(w, S);
   const char* dbg = getenv("CWT_ADAPT_DBG");
   a.dbg = dbg ? atoi(dbg) : 0;
+  a.stamps = nullptr;
   const char* nr = getenv("CWT_ADAPT_R");
   a.nrep = nr ? atoi(nr) : ADAPT_R_DEFAULT;
   if (a.nrep != 4 && a.nrep != 8 && a.nrep != 16 && a.nrep != 32) a.nrep = ADAPT_R_DEFAULT;
@@ -515,7 +547,13 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const float* f_ws, con
   const char* gs_env = getenv("CWT_ADAPT_G");
   const int G = (gs_env ? atoi(gs_env) : 2) >= 2 && E > 1 ? 2 : 1;
   dim3 grid(ncb, h - 1, cdiv(E, G));
+  if (a.dbg & 32) {
+    if ((long)iters * grid.x * grid.y * grid.z * ADAPT_NSTAMP > g_adapt_stamps_n)
+      return fail(CWT_ESTATE, "timing-study stamp buffer too small");
+    a.stamps = g_adapt_stamps;
+  }
   for (int s = 0; s < iters; ++s) {
+    a.step = s;
     a.w_src = (s == 0) ? nullptr : wbuf + ((s - 1) & 1) * 1024;
     a.acc_prev = (s == 0) ? nullptr : acc3 + ((s - 1) % 3) * ADAPT_SLOT;
     a.w_dst = wbuf + (s & 1) * 1024;
@@ -568,6 +606,16 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
                      iters > 0 ? acc3 : (float*)nullptr, ADAPT_ESTRIDE, ADAPT_SLOT, (double*)nullptr);
   CWT_LAUNCH_CHECK();
   if (iters <= 0) return 0;
+  const char* dbg = getenv("CWT_ADAPT_DBG");
+  if (dbg && (atoi(dbg) & 32)) {  // timing study: stamp buffer sized for G = 1 (allocated outside any capture)
+    const long n_st = (long)iters * cdiv(S - 1, 8 * ADAPT_CB) * (h - 1) * E * ADAPT_NSTAMP;
+    if (n_st > g_adapt_stamps_n) {
+      CWT_HIP(hipDeviceSynchronize());
+      if (g_adapt_stamps) CWT_HIP(hipFree(g_adapt_stamps));
+      CWT_HIP(hipMalloc(&g_adapt_stamps, n_st * sizeof(unsigned long long)));
+      g_adapt_stamps_n = n_st;
+    }
+  }
   if (!cache) return enqueue_adapt_steps(dargs, f_ws, lbl_ws, sc, acc3, wbuf, E, n, h, w, S, iters, st);
   // graph path: one instantiated graph per (geometry, workspace pointers)
   AdaptGraphCache::Entry key{E, n, h, w, S, iters, (const void*)f_ws, (const void*)lbl_ws, (const void*)sc,

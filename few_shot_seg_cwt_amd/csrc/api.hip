@@ -30,6 +30,8 @@ struct AdaptDevArgs;
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
                  float* W, float* f_ws, uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf,
                  AdaptDevArgs* dargs, AdaptGraphCache* cache, hipStream_t st);
+extern unsigned long long* g_adapt_stamps;
+extern long g_adapt_stamps_n;
 size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lbl, size_t* sc, size_t* acc,
                       size_t* wbuf, size_t* dargs);
 int launch_seg_ce(const float* logits, const int64_t* target, int B, int h, int w, int S, float* loss_out,
@@ -1084,6 +1086,18 @@ int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int 
                        int nsplit, void* stream) {
   return debug_conv_s(ctx, 1, xs, N, Hi, Wi, Ci, ws, scale, shift, Co, k, stride, pad, dil, res, res_ld, res_s, relu, y,
                       y_ld, y_off, ys, bm, bn, nsplit, stream);
+}
+
+int cwt_debug_adapt_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t max_count, int64_t* count) {
+  if (!ctx || !count) return fail(CWT_EARG, "null argument");
+  CWT_HIP(hipSetDevice(ctx->device));
+  *count = g_adapt_stamps ? g_adapt_stamps_n : 0;
+  if (host_out && g_adapt_stamps && max_count > 0) {
+    CWT_HIP(hipDeviceSynchronize());
+    CWT_HIP(hipMemcpy(host_out, g_adapt_stamps, (size_t)std::min<int64_t>(max_count, g_adapt_stamps_n) * 8,
+                      hipMemcpyDeviceToHost));
+  }
+  return 0;
 }
 
 int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int64_t n, int num_classes,

@@ -248,6 +248,12 @@ int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int 
                        int dil, const float* res, int res_ld, const void* res_s, int relu, float* y,
                        int y_ld, int y_off, void* ys, int bm, int bn, int nsplit, void* stream);
 
+/* Timing-study hook of the inner loop: with CWT_ADAPT_DBG=32 in the environment when the step
+ * graph is built, each step workgroup's wave 0 records 9 clock stamps per step (s_memrealtime at
+ * entry and exit, s_memtime at each phase boundary; tools/adapt_stamps.py).  Copies up to
+ * max_count of them to host_out (may be NULL) and stores the number available in *count. */
+int cwt_debug_adapt_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t max_count, int64_t* count);
+
 /* Test hook: per workgroup of a 64-thread grid, the raw HW_REG_HW_ID and HW_REG_XCC_ID of the
  * CU it ran on (out[2*b], out[2*b+1]); with a CU-masked stream this maps mask bits to CUs. */
 int cwt_debug_census(cwt_ctx* ctx, int nblocks, unsigned* out, void* stream);
