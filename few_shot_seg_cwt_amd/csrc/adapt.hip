@@ -253,7 +253,7 @@ struct AdaptTile {
   int y_main[2], y_extra[2];  // raw label bytes; y_in / y_ex_in below say which are real
 };
 
-template <int G>
+template <int G, bool STAMPS>  // STAMPS: the timing-study build (CWT_ADAPT_DBG & 32), never the timed one
 __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
   constexpr int C = 512;
   __shared__ float wl[G][2][C];
@@ -264,14 +264,14 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int cb = blockIdx.x, r = blockIdx.y;
   unsigned long long* stp = nullptr;  // timing study (CWT_ADAPT_DBG & 32): wave 0's clock at each phase
-  if ((a.dbg & 32) && t == 0) {
+  if (STAMPS && t == 0) {
     stp = a.stamps + ((long)a.step * gridDim.x * gridDim.y * gridDim.z + blockIdx.x +
                       gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * ADAPT_NSTAMP;
     stp[0] = __builtin_amdgcn_s_memrealtime();
     stp[1] = __builtin_amdgcn_s_memtime();
   }
   auto stamp = [&](int i) {
-    if (stp) stp[i] = __builtin_amdgcn_s_memtime();
+    if (STAMPS && stp) stp[i] = __builtin_amdgcn_s_memtime();
   };
   const int ep0 = blockIdx.z * G;
   const int ng = min(G, a.nep - ep0);  // episodes of this group
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
   float d[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) d[q] = 0.f;
-  if (stp) {  // timing study: when tile 0's f and labels have landed
+  if (STAMPS && stp) {  // timing study: when tile 0's f and labels have landed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stp[9] = __builtin_amdgcn_s_memtime();
   }
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
     }
     if (k + 1 < T) cur = nxt;
   }
-  if (stp) {
+  if (STAMPS && stp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // thread 0's atomic has been performed
     stp[7] = __builtin_amdgcn_s_memtime();
     stp[8] = __builtin_amdgcn_s_memrealtime();
@@ -559,10 +559,16 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const float* f_ws, con
     a.w_dst = wbuf + (s & 1) * 1024;
     a.acc_cur = acc3 + (s % 3) * ADAPT_SLOT;
     a.acc_zero = acc3 + ((s + 1) % 3) * ADAPT_SLOT;
-    if (G == 2)
-      hipLaunchKernelGGL(adapt_step_kernel<2>, grid, dim3(ADAPT_T), 0, st, a);
-    else
-      hipLaunchKernelGGL(adapt_step_kernel<1>, grid, dim3(ADAPT_T), 0, st, a);
+    if (a.stamps) {
+      if (G == 2)
+        hipLaunchKernelGGL((adapt_step_kernel<2, true>), grid, dim3(ADAPT_T), 0, st, a);
+      else
+        hipLaunchKernelGGL((adapt_step_kernel<1, true>), grid, dim3(ADAPT_T), 0, st, a);
+    } else if (G == 2) {
+      hipLaunchKernelGGL((adapt_step_kernel<2, false>), grid, dim3(ADAPT_T), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((adapt_step_kernel<1, false>), grid, dim3(ADAPT_T), 0, st, a);
+    }
     CWT_LAUNCH_CHECK();
   }
   const int last = iters - 1;
