@@ -1052,9 +1052,9 @@ static int debug_conv_s(cwt_ctx* ctx, int prec, const void* xs, int N, int Hi, i
   a.K = k * k * Ci;
   ConvPlan p = prec == 1 ? plan_conv_b16(a.M, a.Co, a.K) : plan_conv_x3s(a.M, a.Co, a.K);
   if (bm > 0) {
-    CWT_CHECK((bm == 256 && (bn == 256 || bn == 128)) || (bm == 128 && (bn == 128 || bn == 64)) ||
+    CWT_CHECK((bm == 256 && (bn == 256 || bn == 128)) || (bm == 128 && (bn == 256 || bn == 128 || bn == 64)) ||
                   (bm == 64 && (bn == 128 || bn == 64)),
-              "tile must be one of 256x256, 256x128, 128x128, 128x64, 64x128, 64x64");
+              "tile must be one of 256x256, 256x128, 128x256, 128x128, 128x64, 64x128, 64x64");
     CWT_CHECK(Co % bn == 0, "Co % bn");
     p.bm = bm;
     p.bn = bn;

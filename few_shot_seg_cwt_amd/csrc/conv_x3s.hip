@@ -465,6 +465,8 @@ static void launch_tiles_x3s(const ConvSArgs& a, const ConvPlan& p, dim3 grid, h
     hipLaunchKernelGGL((conv_igemm_x3s<256, 256, 2, 4, 2, STAGE>), grid, dim3(512), 0, st, a);
   else if (p.bm == 256 && p.bn == 128)
     hipLaunchKernelGGL((conv_igemm_x3s<256, 128, 4, 2, 3, STAGE>), grid, dim3(512), 0, st, a);
+  else if (p.bm == 128 && p.bn == 256)
+    hipLaunchKernelGGL((conv_igemm_x3s<128, 256, 2, 4, 3, STAGE>), grid, dim3(512), 0, st, a);
   else if (p.bm == 128 && p.bn == 128)
     hipLaunchKernelGGL((conv_igemm_x3s<128, 128, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
   else if (p.bm == 128 && p.bn == 64)
@@ -481,6 +483,8 @@ static void launch_tiles_b16(const ConvSArgs& a, const ConvPlan& p, dim3 grid, h
     hipLaunchKernelGGL((conv_igemm_b16<256, 256, 2, 4, 2, STAGE>), grid, dim3(512), 0, st, a);
   else if (p.bm == 256 && p.bn == 128)
     hipLaunchKernelGGL((conv_igemm_b16<256, 128, 4, 2, 3, STAGE>), grid, dim3(512), 0, st, a);
+  else if (p.bm == 128 && p.bn == 256)
+    hipLaunchKernelGGL((conv_igemm_b16<128, 256, 2, 4, 3, STAGE>), grid, dim3(512), 0, st, a);
   else if (p.bm == 128 && p.bn == 128)
     hipLaunchKernelGGL((conv_igemm_b16<128, 128, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
   else if (p.bm == 128 && p.bn == 64)
@@ -504,7 +508,7 @@ static const MeasuredPlanS kMeasuredPlansS[] = {
 // where the output grid is too small.
 static ConvPlan plan_heuristic_s(int M, int Co, int ktiles) {
   constexpr long kMinWG = 200;
-  static const int cand[6][2] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  static const int cand[7][2] = {{256, 256}, {256, 128}, {128, 256}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
   ConvPlan best;
   for (auto& c : cand) {
     if (Co % c[1] != 0) continue;
@@ -536,8 +540,25 @@ ConvPlan plan_conv_x3s(int M, int Co, int K) {
   return plan_heuristic_s(M, Co, ktiles);
 }
 
-// Plain bf16: 64-deep K-tiles (the sweep table is for bf16x3 and is not reused).
-ConvPlan plan_conv_b16(int M, int Co, int K) { return plan_heuristic_s(M, Co, K / 64); }
+static const MeasuredPlanS kMeasuredPlansB16[] = {
+#include "conv_plans_b16.inc"
+};
+
+// Plain bf16: 64-deep K-tiles; its own measured table (conv_plans_b16.inc, tools/conv_s_sweep.py
+// --prec 1), else the heuristic.
+ConvPlan plan_conv_b16(int M, int Co, int K) {
+  const int ktiles = K / 64;
+  for (const MeasuredPlanS& e : kMeasuredPlansB16)
+    if (e.M == M && e.Co == Co && e.K == K && Co % e.bn == 0) {
+      ConvPlan p;
+      p.bm = e.bm;
+      p.bn = e.bn;
+      p.kt_per_split = cdiv(ktiles, e.nsplit);
+      p.nsplit = cdiv(ktiles, p.kt_per_split);
+      return p;
+    }
+  return plan_heuristic_s(M, Co, ktiles);
+}
 
 template <int PREC>
 static void launch_splitk_s(const ConvSArgs& a, int nsplit, hipStream_t st) {

@@ -87,7 +87,7 @@ CASES = [  # N, Ci, Co, Hi, k, stride, dil, residual
     (3, 96, 64, 9, 1, 1, 1, True),
     (1, 64, 512, 19, 3, 1, 1, True),
 ]
-PLANS = [(0, 0, 0), (256, 256, 1), (256, 128, 1), (128, 128, 1), (128, 64, 1), (64, 128, 1), (64, 64, 1),
+PLANS = [(0, 0, 0), (256, 256, 1), (256, 128, 1), (128, 256, 1), (128, 256, 2), (128, 128, 1), (128, 64, 1), (64, 128, 1), (64, 64, 1),
          (64, 64, 3), (128, 128, 2), (256, 256, 4)]
 
 

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from few_shot_seg_cwt_amd import _lib  # noqa: E402
 from conv_sweep import shapes  # noqa: E402
 
-TILES = [(256, 256), (256, 128), (128, 128), (128, 64), (64, 128), (64, 64)]
+TILES = [(256, 256), (256, 128), (128, 256), (128, 128), (128, 64), (64, 128), (64, 64)]
 
 
 def timed(fn, reps):
@@ -32,7 +32,7 @@ def timed(fn, reps):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
-def sweep(layers, size, n_img, reps, quick):
+def sweep(layers, size, n_img, reps, quick, prec=3):
     print(f"== R{layers} S={size} N={n_img}", flush=True)
     dev = torch.device("cuda", 0)
     lib, ctx, sp = _lib.lib(), _lib.ctx(0), _lib.stream_ptr()
@@ -44,10 +44,14 @@ def sweep(layers, size, n_img, reps, quick):
         x = torch.randn(n_img, Hi, Hi, Ci, device=dev)
         w = torch.randn(Co, k, k, Ci, device=dev) * (2.0 / K) ** 0.5
         wp = torch.empty(Co * K, device=dev)
-        xs = torch.empty(n_img * Hi * Hi * Ci * 2, dtype=torch.bfloat16, device=dev)
-        ws = torch.empty(Co * K * 2, dtype=torch.bfloat16, device=dev)
-        _lib.check(lib.cwt_debug_split_act(ctx, _lib.ptr(x), n_img * Hi * Hi, Ci, Ci, _lib.ptr(xs), sp))
-        _lib.check(lib.cwt_debug_pack_wsplit(ctx, _lib.ptr(w), Co, k, Ci, _lib.ptr(ws), sp))
+        if prec == 1:   # plain bf16 operands (K order inside a row does not matter for timing)
+            xs = x.to(torch.bfloat16).contiguous()
+            ws = w.reshape(Co, K).to(torch.bfloat16).contiguous()
+        else:
+            xs = torch.empty(n_img * Hi * Hi * Ci * 2, dtype=torch.bfloat16, device=dev)
+            ws = torch.empty(Co * K * 2, dtype=torch.bfloat16, device=dev)
+            _lib.check(lib.cwt_debug_split_act(ctx, _lib.ptr(x), n_img * Hi * Hi, Ci, Ci, _lib.ptr(xs), sp))
+            _lib.check(lib.cwt_debug_pack_wsplit(ctx, _lib.ptr(w), Co, k, Ci, _lib.ptr(ws), sp))
         # old path: weights pre-split hi[Co][K] ++ lo[Co][K] (order within K does not matter for timing)
         wf = w.reshape(Co, K)
         hi = wf.to(torch.bfloat16)
@@ -57,11 +61,13 @@ def sweep(layers, size, n_img, reps, quick):
         sh = torch.zeros(Co, device=dev)
         r = torch.randn(n_img, Ho, Ho, Co, device=dev) if has_res else None
         rs = None
-        if has_res:
+        if has_res and prec == 1:
+            rs = r.to(torch.bfloat16).contiguous()
+        elif has_res:
             rs = torch.empty(M * Co * 2, dtype=torch.bfloat16, device=dev)
             _lib.check(lib.cwt_debug_split_act(ctx, _lib.ptr(r), M, Co, Co, _lib.ptr(rs), sp))
         y = torch.empty(n_img, Ho, Ho, Co, device=dev)
-        ys = torch.empty(M * Co * 2, dtype=torch.bfloat16, device=dev)
+        ys = torch.empty(M * Co * (1 if prec == 1 else 2), dtype=torch.bfloat16, device=dev)
         flops = 2.0 * M * Co * K
 
         def old():
@@ -69,12 +75,14 @@ def sweep(layers, size, n_img, reps, quick):
                                           _lib.ptr(sc), _lib.ptr(sh), Co, k, stride, pad, dil, _lib.ptr(r), Co, 1,
                                           _lib.ptr(y), Co, 0, 0, 0, 0, 2, sp))
 
+        conv_fn = lib.cwt_debug_conv_b16 if prec == 1 else lib.cwt_debug_conv_s
+
         def new(bm, bn, ns):
-            return lambda: _lib.check(lib.cwt_debug_conv_s(
+            return lambda: _lib.check(conv_fn(
                 ctx, _lib.ptr(xs), n_img, Hi, Hi, Ci, _lib.ptr(ws), _lib.ptr(sc), _lib.ptr(sh), Co, k, stride, pad,
                 dil, None, Co, _lib.ptr(rs), 1, None, Co, 0, _lib.ptr(ys), bm, bn, ns, sp))
 
-        t_old = timed(old, reps)
+        t_old = timed(old, reps) if prec == 3 else float("nan")
         t_auto = timed(new(0, 0, 0), reps)
         rows = []
         if not quick:
@@ -83,7 +91,7 @@ def sweep(layers, size, n_img, reps, quick):
                     continue
                 tiles = -(-M // bm) * (Co // bn)
                 for ns in (1, 2, 4, 8):
-                    if ns > 1 and ((K // 32) // ns < 4 or tiles * ns > 4096):
+                    if ns > 1 and ((K // (64 if prec == 1 else 32)) // ns < 4 or tiles * ns > 4096):
                         continue
                     us = timed(new(bm, bn, ns), reps)
                     rows.append({"bm": bm, "bn": bn, "ns": ns, "us": round(us, 2),
@@ -96,7 +104,7 @@ def sweep(layers, size, n_img, reps, quick):
         print(f"{name:10s} x{cnt:2d} {Ci:4d}->{Co:4d} k{k} @{Ho:3d} M={M:6d} K={K:6d}: old {t_old:7.1f} us "
               f"({flops / t_old / 1e6:6.1f} TF)  new-auto {t_auto:7.1f} ({flops / t_auto / 1e6:6.1f} TF)  best "
               f"{best['bm']}x{best['bn']}s{best['ns']} {best['us']:7.1f} ({best['tflops']:6.1f} TF)", flush=True)
-        res_all.append({"cfg": f"{layers}:{size}:{n_img}", "name": name, "count": cnt, "Ci": Ci, "Co": Co, "k": k,
+        res_all.append({"cfg": f"{layers}:{size}:{n_img}", "prec": prec, "name": name, "count": cnt, "Ci": Ci, "Co": Co, "k": k,
                         "Ho": Ho, "M": M, "K": K, "stride": stride, "dil": dil, "res": has_res,
                         "old_us": round(t_old, 2), "auto_us": round(t_auto, 2), "plans": rows})
         del x, w, wp, xs, ws, wsplit_old, r, rs, y, ys
@@ -112,12 +120,13 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--quick", action="store_true", help="old vs new automatic plan only")
     ap.add_argument("--out", default="conv_s_sweep.json")
+    ap.add_argument("--prec", type=int, default=3, choices=[1, 3], help="3 = bf16x3 (x3s), 1 = plain bf16 (b16)")
     args = ap.parse_args()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     res_all = []
     for cfg in args.configs.split(","):
         L, S, N = (int(v) for v in cfg.split(":"))
-        res_all += sweep(L, S, N, args.reps, args.quick)
+        res_all += sweep(L, S, N, args.reps, args.quick, args.prec)
         with open(os.path.join(ROOT, "gpurun_out", args.out), "w") as f:
             json.dump(res_all, f, indent=1)
 
