@@ -13,7 +13,8 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcwt.so")
+# CWT_LIB_PATH selects another build of the library (A/B timing of two builds in one session)
+LIB_PATH = os.environ.get("CWT_LIB_PATH") or os.path.join(_HERE, "libcwt.so")
 
 _P = C.c_void_p
 _I = C.c_int
