@@ -39,6 +39,10 @@ SIGNATURES = {
     "cwt_attention_fwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cwt_attention_saved_floats": (C.c_size_t, [_I, _I, _I, _I]),
     "cwt_attention_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cwt_attention_fwd_train": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, C.c_uint64,
+                                     _P]),
+    "cwt_attention_bwd_train": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F,
+                                     _F, C.c_uint64, _P]),
     "cwt_classify": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_seg_metrics": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "cwt_seg_ce_fwd_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),

@@ -49,11 +49,11 @@ size_t attention_saved_floats(int B, int hw, int C, int H);
 size_t attention_ws_floats(int B, int hw, int C, int H);
 int attention_fwd(const float* q, const float* f, int B, int hw, int C, int H, const float* w_qkvs,
                   const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b, float* out,
-                  float* saved, float* ws, hipStream_t st);
+                  float* saved, float* ws, hipStream_t st, float p_attn, float p_out, unsigned long long seed);
 int attention_bwd(const float* q, const float* f, int B, int hw, int C, int H, const float* w_qkvs,
                   const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b, const float* saved,
                   const float* d_out, float* g_w_qkvs, float* g_fc_w, float* g_fc_b, float* g_ln_w, float* g_ln_b,
-                  float* ws, hipStream_t st);
+                  float* ws, hipStream_t st, float p_attn, float p_out, unsigned long long seed);
 size_t attention_bwd_ws_floats(int B, int hw, int C, int H);
 
 // ------------------------------------------------------------------------------------------
@@ -820,12 +820,15 @@ int cwt_normalize(cwt_ctx* ctx, const float* f, int B, int P_per_b, int C, float
 
 size_t cwt_attention_saved_floats(int B, int hw, int C, int H) { return attention_saved_floats(B, hw, C, H); }
 
-int cwt_attention_fwd(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
-                      const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b,
-                      float* out, float* saved, void* stream) {
+int cwt_attention_fwd_train(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                            const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
+                            const float* ln_b, float* out, float* saved, float attn_dropout, float out_dropout,
+                            uint64_t seed, void* stream) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
   CWT_CHECK(q && f && w_qkvs && fc_w && fc_b && ln_w && ln_b && out, "null buffer");
   CWT_CHECK(B >= 1 && B <= 4 && hw >= 1 && C == 512, "need 1 <= B <= 4, C == 512");
+  CWT_CHECK(attn_dropout >= 0.f && attn_dropout < 1.f && out_dropout >= 0.f && out_dropout < 1.f,
+            "dropout probabilities must lie in [0, 1)");
   CWT_HIP(hipSetDevice(ctx->device));
   void* ws;
   int rc;
@@ -834,25 +837,45 @@ int cwt_attention_fwd(cwt_ctx* ctx, const float* q, const float* f, int B, int h
   Prof p(ctx, (hipStream_t)stream, "attention_fwd",
          (double)B * (2.0 * 2.0 * hw * C * C * H + 2.0 * 2.0 * H * 2.0 * hw * C),
          4.0 * ((double)B * hw * C + 2.0 * H * C * C + 2.0 * C), 1);
-  rc = attention_fwd(q, f, B, hw, C, H, w_qkvs, fc_w, fc_b, ln_w, ln_b, out, saved, (float*)ws, (hipStream_t)stream);
+  rc = attention_fwd(q, f, B, hw, C, H, w_qkvs, fc_w, fc_b, ln_w, ln_b, out, saved, (float*)ws, (hipStream_t)stream,
+                     attn_dropout, out_dropout, (unsigned long long)seed);
   p.end();
   return rc;
+}
+
+int cwt_attention_fwd(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                      const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b,
+                      float* out, float* saved, void* stream) {
+  return cwt_attention_fwd_train(ctx, q, f, B, hw, C, H, w_qkvs, fc_w, fc_b, ln_w, ln_b, out, saved, 0.f, 0.f, 0,
+                                 stream);
+}
+
+int cwt_attention_bwd_train(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                            const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
+                            const float* ln_b, const float* saved, const float* d_out, float* g_w_qkvs, float* g_fc_w,
+                            float* g_fc_b, float* g_ln_w, float* g_ln_b, float attn_dropout, float out_dropout,
+                            uint64_t seed, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(q && f && w_qkvs && fc_w && fc_b && ln_w && ln_b && saved && d_out, "null buffer");
+  CWT_CHECK(g_w_qkvs && g_fc_w && g_fc_b && g_ln_w && g_ln_b, "null gradient buffer");
+  CWT_CHECK(B >= 1 && B <= 4 && hw >= 1 && C == 512, "need 1 <= B <= 4, C == 512");
+  CWT_CHECK(attn_dropout >= 0.f && attn_dropout < 1.f && out_dropout >= 0.f && out_dropout < 1.f,
+            "dropout probabilities must lie in [0, 1)");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void* ws;
+  int rc;
+  if ((rc = ensure_ws(ctx, "attn.bws", attention_bwd_ws_floats(B, hw, C, H) * 4, &ws))) return rc;
+  return attention_bwd(q, f, B, hw, C, H, w_qkvs, fc_w, fc_b, ln_w, ln_b, saved, d_out, g_w_qkvs, g_fc_w, g_fc_b,
+                       g_ln_w, g_ln_b, (float*)ws, (hipStream_t)stream, attn_dropout, out_dropout,
+                       (unsigned long long)seed);
 }
 
 int cwt_attention_bwd(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
                       const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b,
                       const float* saved, const float* d_out, float* g_w_qkvs, float* g_fc_w, float* g_fc_b,
                       float* g_ln_w, float* g_ln_b, void* stream) {
-  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
-  CWT_CHECK(q && f && w_qkvs && fc_w && fc_b && ln_w && ln_b && saved && d_out, "null buffer");
-  CWT_CHECK(g_w_qkvs && g_fc_w && g_fc_b && g_ln_w && g_ln_b, "null gradient buffer");
-  CWT_CHECK(B >= 1 && B <= 4 && hw >= 1 && C == 512, "need 1 <= B <= 4, C == 512");
-  CWT_HIP(hipSetDevice(ctx->device));
-  void* ws;
-  int rc;
-  if ((rc = ensure_ws(ctx, "attn.bws", attention_bwd_ws_floats(B, hw, C, H) * 4, &ws))) return rc;
-  return attention_bwd(q, f, B, hw, C, H, w_qkvs, fc_w, fc_b, ln_w, ln_b, saved, d_out, g_w_qkvs, g_fc_w, g_fc_b,
-                       g_ln_w, g_ln_b, (float*)ws, (hipStream_t)stream);
+  return cwt_attention_bwd_train(ctx, q, f, B, hw, C, H, w_qkvs, fc_w, fc_b, ln_w, ln_b, saved, d_out, g_w_qkvs,
+                                 g_fc_w, g_fc_b, g_ln_w, g_ln_b, 0.f, 0.f, 0, stream);
 }
 
 int cwt_classify(cwt_ctx* ctx, const float* W, const float* f, int B, int P, int C, float* logits, void* stream) {

@@ -83,6 +83,24 @@ static inline float align_corners_scale(int in_size, int out_size) {
   return out_size > 1 ? (float)(in_size - 1) / (float)(out_size - 1) : 0.0f;
 }
 
+// Counter-based dropout draw (the CWT's training-mode dropouts): a splitmix64 finaliser of
+// (seed, stream, index) -> u in [0, 1) with 24 random bits; an element is kept iff u >= p and
+// then scaled by 1 / (1 - p), as nn.Dropout does.  The same function regenerates the mask in the
+// backward pass (nothing is stored) and in the tests (tests/dropout_ref.py restates it).
+// Streams: 1 = attention probabilities [B][2H][hw], 2 = fc output [2B][512].
+__host__ __device__ __forceinline__ float dropout_uniform(unsigned long long seed, unsigned stream,
+                                                         unsigned long long idx) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (idx + 1) + 0xD1B54A32D192ED03ull * (stream + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+__host__ __device__ __forceinline__ float dropout_scale(float p, unsigned long long seed, unsigned stream,
+                                                       unsigned long long idx) {
+  return dropout_uniform(seed, stream, idx) >= p ? 1.0f / (1.0f - p) : 0.0f;
+}
+
 }  // namespace cwt
 
 #ifndef CWT_EARG

@@ -128,10 +128,14 @@ constexpr int ATT_TPB = 4 * ATT_TPW;       // tokens per workgroup
 // r: [H][nv][C] scores queries (already / sqrt(C)), row rho = h*2 + i of batch b is r[h][b*2+i].
 // f: [B][hw][C].  part_g: [B][nchunk][NR][C]; part_ml: [B][nchunk][NR][2].
 // Optionally stores the raw scores for the backward pass: scores [B][NR][hw].
+// Training-mode attention dropout (transformer.py:17,28: dropout AFTER the softmax): token p of
+// row rho enters g with weight m = dropout_scale(p_drop, seed, 1, (b*NR + rho)*hw + p); the
+// softmax denominator l is unaffected.
 template <int NR>
 __global__ __launch_bounds__(256) void attn_partial_kernel(const float* __restrict__ r, const float* __restrict__ f,
                                                            int hw, int nv, float* __restrict__ part_g,
-                                                           float* __restrict__ part_ml, float* __restrict__ scores) {
+                                                           float* __restrict__ part_ml, float* __restrict__ scores,
+                                                           float p_drop, unsigned long long seed) {
   constexpr int C = 512;
   __shared__ float rs[NR][C];
   __shared__ float wml[4][NR][2];
@@ -195,8 +199,9 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(const float* __restri
     for (int tt = 0; tt < ATT_TPW; ++tt) {
       const float e = (tok0 + tt < hw) ? __expf(s[tt][rho] - m) : 0.f;
       l += e;
+      const float em = p_drop > 0.f ? e * dropout_scale(p_drop, seed, 1, ((long)b * NR + rho) * hw + tok0 + tt) : e;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) g[q] = fmaf(e, fv[tt][q], g[q]);
+      for (int q = 0; q < 8; ++q) g[q] = fmaf(em, fv[tt][q], g[q]);
     }
     if (lane == 0) {
       wml[wv][rho][0] = m;
@@ -285,6 +290,14 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
   }
 }
 
+// Training-mode output dropout (transformer.py:52,80): y = dropout(fc(o)) + q, in place on y =
+// fc(o) (stream 2, index v*C + k).
+__global__ void dropout_residual_kernel(float* __restrict__ y, const float* __restrict__ q, int n, float p,
+                                        unsigned long long seed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = y[i] * dropout_scale(p, seed, 2, i) + q[i];
+}
+
 // LayerNorm over C=512 per row (nn.LayerNorm(512), eps 1e-5, biased variance).
 __global__ void layernorm_kernel(const float* __restrict__ y, const float* __restrict__ w,
                                  const float* __restrict__ bb, float* __restrict__ out, float* __restrict__ stats,
@@ -351,7 +364,7 @@ size_t attention_ws_floats(int B, int hw, int C, int H) {
 
 int attention_fwd(const float* q, const float* f, int B, int hw, int C, int H, const float* w_qkvs,
                   const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b, float* out,
-                  float* saved, float* ws, hipStream_t st) {
+                  float* saved, float* ws, hipStream_t st, float p_attn, float p_out, unsigned long long seed) {
   if (C != 512) return fail(CWT_EARG, "attention: C must be 512");
   if (!(H == 1 || H == 2 || H == 4)) return fail(CWT_EARG, "attention: heads must be 1, 2 or 4");
   const int nv = 2 * B;
@@ -375,11 +388,14 @@ int attention_fwd(const float* q, const float* f, int B, int hw, int C, int H, c
   dim3 g3(nchunk, B);
   float* sc_out = saved ? sv + L.sc : nullptr;
   if (H == 1)
-    hipLaunchKernelGGL((attn_partial_kernel<2>), g3, dim3(256), 0, st, sv + L.r, f, hw, nv, part_g, part_ml, sc_out);
+    hipLaunchKernelGGL((attn_partial_kernel<2>), g3, dim3(256), 0, st, sv + L.r, f, hw, nv, part_g, part_ml, sc_out,
+                       p_attn, seed);
   else if (H == 2)
-    hipLaunchKernelGGL((attn_partial_kernel<4>), g3, dim3(256), 0, st, sv + L.r, f, hw, nv, part_g, part_ml, sc_out);
+    hipLaunchKernelGGL((attn_partial_kernel<4>), g3, dim3(256), 0, st, sv + L.r, f, hw, nv, part_g, part_ml, sc_out,
+                       p_attn, seed);
   else
-    hipLaunchKernelGGL((attn_partial_kernel<8>), g3, dim3(256), 0, st, sv + L.r, f, hw, nv, part_g, part_ml, sc_out);
+    hipLaunchKernelGGL((attn_partial_kernel<8>), g3, dim3(256), 0, st, sv + L.r, f, hw, nv, part_g, part_ml, sc_out,
+                       p_attn, seed);
   CWT_LAUNCH_CHECK();
   // 4. combine -> g[h][v][C]
   dim3 g4(C / 64, NR, B);
@@ -394,9 +410,15 @@ int attention_fwd(const float* q, const float* f, int B, int hw, int C, int H, c
   if ((rc = launch_rowdot(w_qkvs, H * C, C, sv + L.g, nv, C, (long)nv * C, C, nullptr, nullptr, 0, sv + L.o,
                           (long)H * C, 1.f, st)))
     return rc;
-  // 6. y[v][d] = fc_w[d] . o[v] + fc_b[d] + q[v][d]
-  if ((rc = launch_rowdot(fc_w, C, H * C, sv + L.o, nv, (long)H * C, 0, C, fc_b, q, C, sv + L.y, C, 1.f, st)))
+  // 6. y[v][d] = fc_w[d] . o[v] + fc_b[d] + q[v][d]   (with output dropout on the fc term)
+  if ((rc = launch_rowdot(fc_w, C, H * C, sv + L.o, nv, (long)H * C, 0, C, fc_b, p_out > 0.f ? nullptr : q, C,
+                          sv + L.y, C, 1.f, st)))
     return rc;
+  if (p_out > 0.f) {
+    hipLaunchKernelGGL(dropout_residual_kernel, dim3(cdiv(nv * C, 256)), dim3(256), 0, st, sv + L.y, q, nv * C, p_out,
+                       seed);
+    CWT_LAUNCH_CHECK();
+  }
   // 7. LayerNorm
   hipLaunchKernelGGL(layernorm_kernel, dim3(nv), dim3(64), 0, st, sv + L.y, ln_w, ln_b, out, sv + L.ln, 1e-5f);
   CWT_LAUNCH_CHECK();
@@ -416,10 +438,13 @@ int attention_fwd(const float* q, const float* f, int B, int hw, int C, int H, c
 // ---------------------------------------------------------------------------------------
 
 // One workgroup of 512 threads (thread = channel k) handles every row v.
+// dy is the gradient w.r.t. the fc output: the LayerNorm input gradient times the output-dropout
+// mask (p_out > 0; regenerated from the forward's seed).
 __global__ __launch_bounds__(512) void ln_bwd_kernel(const float* __restrict__ d_out, const float* __restrict__ y,
                                                      const float* __restrict__ stats, const float* __restrict__ w,
                                                      int nv, float* __restrict__ dy, float* __restrict__ g_w,
-                                                     float* __restrict__ g_b, float* __restrict__ g_fc_b) {
+                                                     float* __restrict__ g_b, float* __restrict__ g_fc_b, float p_out,
+                                                     unsigned long long seed) {
   constexpr int C = 512;
   __shared__ float red[2][8];
   const int k = threadIdx.x, lane = k & 63, wv = k >> 6;
@@ -446,7 +471,8 @@ __global__ __launch_bounds__(512) void ln_bwd_kernel(const float* __restrict__ d
     __syncthreads();
     m1 /= (float)C;
     m2 /= (float)C;
-    const float d = rstd * (dxh - m1 - xh * m2);
+    float d = rstd * (dxh - m1 - xh * m2);
+    if (p_out > 0.f) d *= dropout_scale(p_out, seed, 2, (unsigned long long)v * C + k);
     dy[(long)v * C + k] = d;
     gfb += d;
   }
@@ -498,11 +524,12 @@ static int launch_outer(float* G, int R, int K, int rows_per_group, int nv, Oute
 }
 
 // dr[h][b*2+i][k] += sum_p P_p (dg.f_p - dg.g) f_p over the workgroup's tokens
+// With attention dropout (g = sum_p m_p P_p f_p): ds_p = P_p (m_p dg.f_p - dg.g).
 template <int NR>
 __global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__ dg, const float* __restrict__ g,
                                                        const float* __restrict__ f, const float* __restrict__ scores,
                                                        const float* __restrict__ ml, int hw, int nv,
-                                                       float* __restrict__ dr) {
+                                                       float* __restrict__ dr, float p_drop, unsigned long long seed) {
   constexpr int C = 512;
   __shared__ float dgs[NR][C];
   __shared__ float dgg[NR];
@@ -556,7 +583,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__
       const int p = tok0 + tt;
       if (p < hw) {
         const float P = __expf(scores[((long)b * NR + rho) * hw + p] - M) * Linv;
-        const float ds = P * (d - dgg[rho]);
+        const float dm = p_drop > 0.f ? d * dropout_scale(p_drop, seed, 1, ((long)b * NR + rho) * hw + p) : d;
+        const float ds = P * (dm - dgg[rho]);
 #pragma unroll
         for (int q = 0; q < 8; ++q) acc[q] = fmaf(ds, fv[tt][q], acc[q]);
       }
@@ -581,7 +609,7 @@ size_t attention_bwd_ws_floats(int B, int hw, int C, int H) {
 int attention_bwd(const float* q, const float* f, int B, int hw, int C, int H, const float* w_qkvs,
                   const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b, const float* saved,
                   const float* d_out, float* g_w_qkvs, float* g_fc_w, float* g_fc_b, float* g_ln_w, float* g_ln_b,
-                  float* ws, hipStream_t st) {
+                  float* ws, hipStream_t st, float p_attn, float p_out, unsigned long long seed) {
   (void)fc_b;
   (void)ln_b;
   if (C != 512) return fail(CWT_EARG, "attention: C must be 512");
@@ -601,7 +629,7 @@ int attention_bwd(const float* q, const float* f, int B, int hw, int C, int H, c
   const float inv_t = 1.0f / sqrtf((float)C);
   int rc;
   hipLaunchKernelGGL(ln_bwd_kernel, dim3(1), dim3(512), 0, st, d_out, y, saved + L.ln, ln_w, nv, dy, g_ln_w, g_ln_b,
-                     g_fc_b);
+                     g_fc_b, p_out, seed);
   CWT_LAUNCH_CHECK();
   OuterTerm none{nullptr, 0, nullptr, 0, 0, 0.f};
   OuterTerm tfc{dy, C, o, HC, 0, 1.f};
@@ -614,11 +642,14 @@ int attention_bwd(const float* q, const float* f, int B, int hw, int C, int H, c
   const int nchunk = cdiv(hw, ATT_TPB);
   dim3 gb(nchunk, B);
   if (H == 1)
-    hipLaunchKernelGGL((attn_bwd_kernel<2>), gb, dim3(256), 0, st, dg, g, f, saved + L.sc, saved + L.ml, hw, nv, dr);
+    hipLaunchKernelGGL((attn_bwd_kernel<2>), gb, dim3(256), 0, st, dg, g, f, saved + L.sc, saved + L.ml, hw, nv, dr,
+                       p_attn, seed);
   else if (H == 2)
-    hipLaunchKernelGGL((attn_bwd_kernel<4>), gb, dim3(256), 0, st, dg, g, f, saved + L.sc, saved + L.ml, hw, nv, dr);
+    hipLaunchKernelGGL((attn_bwd_kernel<4>), gb, dim3(256), 0, st, dg, g, f, saved + L.sc, saved + L.ml, hw, nv, dr,
+                       p_attn, seed);
   else
-    hipLaunchKernelGGL((attn_bwd_kernel<8>), gb, dim3(256), 0, st, dg, g, f, saved + L.sc, saved + L.ml, hw, nv, dr);
+    hipLaunchKernelGGL((attn_bwd_kernel<8>), gb, dim3(256), 0, st, dg, g, f, saved + L.sc, saved + L.ml, hw, nv, dr,
+                       p_attn, seed);
   CWT_LAUNCH_CHECK();
   if ((rc = launch_rowdot(w_qkvs, (int)HC, C, dr, nv, C, (long)nv * C, C, nullptr, nullptr, 0, da, HC, inv_t, st)))
     return rc;

@@ -140,7 +140,7 @@ class EpisodeEngine:
         W = inner_adapt(f_s, s_label, W0, self.lr, self.iters)
         Wb = W.view(1, 2, -1)
         fqn, pred_q0 = normalize(f_q, Wb)
-        W2 = self.transformer(Wb, fqn, fqn)
+        W2 = self.transformer.infer(Wb, fqn)
         pred_q = classify(W2, fqn)
         iut, ce = seg_metrics(pred_q, q_label)
         iut0, _ = seg_metrics(pred_q0, q_label, with_ce=False)
@@ -162,7 +162,7 @@ class EpisodeEngine:
         f_s, f_q = f_all[:E * shot], f_all[E * shot:]
         W = inner_adapt_batch(f_s, s_label, W0, self.lr, self.iters)
         fqn, pred_q0 = normalize(f_q, W)
-        W2 = self.transformer(W, fqn, fqn)
+        W2 = self.transformer.infer(W, fqn)
         pred_q = classify(W2, fqn)
         iut, ce = seg_metrics(pred_q, q_label)
         iut0, _ = seg_metrics(pred_q0, q_label, with_ce=False)

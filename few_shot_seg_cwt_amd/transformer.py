@@ -11,8 +11,11 @@ views of it.  That makes the 8-GPU gradient all-reduce one RCCL call on one buck
 outer SGD step one kernel.
 
 Differences from the reference, by design: k and v must be the same tensor
-(the only way the CWT drivers call it, test.py:197 / train.py:257); dropout layers are
-not applied (the parity runs of the training path use p = 0).
+(the only way the CWT drivers call it, test.py:197 / train.py:257).  In training mode the two
+dropouts run as in the reference (``self.attention.dropout`` p=0.1 on the attention
+probabilities, ``self.dropout`` on the fc output; set their ``.p`` to 0 exactly as the
+reference would), with masks from the kernels' counter-based generator (a fresh seed per
+forward from torch's CPU RNG) instead of torch's Philox stream.
 """
 from __future__ import annotations
 
@@ -46,9 +49,9 @@ def as_tokens(k: torch.Tensor) -> torch.Tensor:
 
 class _CWTFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, f, flat, mod):
-        out, saved = mod._fwd(q, f, need_saved=True)
-        ctx.mod = mod
+    def forward(ctx, q, f, flat, mod, drop):
+        out, saved = mod._fwd(q, f, need_saved=True, drop=drop)
+        ctx.mod, ctx.drop = mod, drop
         ctx.save_for_backward(q, f, flat)
         ctx.saved_buf = saved
         return out
@@ -57,8 +60,18 @@ class _CWTFunction(torch.autograd.Function):
     def backward(ctx, d_out):
         q, f, flat = ctx.saved_tensors
         g = torch.zeros_like(flat)
-        ctx.mod._bwd(q, f, ctx.saved_buf, d_out.contiguous(), g)
-        return None, None, g, None
+        ctx.mod._bwd(q, f, ctx.saved_buf, d_out.contiguous(), g, drop=ctx.drop)
+        return None, None, g, None, None
+
+
+class _Attention(torch.nn.Module):
+    """Holder mirroring the reference's ScaledDotProductAttention attributes (transformer.py:12-19):
+    ``temperature`` and ``dropout`` (nn.Dropout(0.1), applied in training mode)."""
+
+    def __init__(self, temperature: float, attn_dropout: float = 0.1):
+        super().__init__()
+        self.temperature = temperature
+        self.dropout = torch.nn.Dropout(attn_dropout)
 
 
 class MultiHeadAttentionOne(torch.nn.Module):
@@ -71,7 +84,8 @@ class MultiHeadAttentionOne(torch.nn.Module):
         if n_head not in (1, 2, 4):
             raise NotImplementedError("n_head must be 1, 2 or 4 (heads 1 in the yaml, 4 in scripts/*.sh)")
         self.n_head, self.d_model = n_head, d_model
-        self.dropout_p = dropout  # recorded, not applied (module docstring)
+        self.attention = _Attention(temperature=float(np.power(d_k, 0.5)))  # transformer.py:47
+        self.dropout = torch.nn.Dropout(dropout)                              # transformer.py:52
         self._layout, total = _layout(n_head, d_model)
         dev = torch.device("cuda", device if device is not None else torch.cuda.current_device()) \
             if torch.cuda.is_available() else torch.device("cpu")
@@ -137,7 +151,19 @@ class MultiHeadAttentionOne(torch.nn.Module):
             hw = f.shape[1]
         return B, hw
 
-    def _fwd(self, q, f, need_saved: bool):
+    @property
+    def dropout_p(self) -> float:
+        return float(self.dropout.p)
+
+    def _drop(self):
+        """(attention p, output p, seed) in training mode with a dropout on, else None."""
+        pa, po = float(self.attention.dropout.p), float(self.dropout.p)
+        if not self.training or (pa == 0.0 and po == 0.0):
+            return None
+        seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())  # host RNG: no device sync
+        return pa, po, seed
+
+    def _fwd(self, q, f, need_saved: bool, drop=None):
         q = q.contiguous()
         B, hw = self._check(q, f)
         out = torch.empty((B, 2, self.d_model), device=q.device, dtype=torch.float32)
@@ -146,19 +172,22 @@ class MultiHeadAttentionOne(torch.nn.Module):
             n = _lib.lib().cwt_attention_saved_floats(B, hw, self.d_model, self.n_head)
             saved = torch.empty(n, device=q.device, dtype=torch.float32)
         w, fw, fb, lw, lb = self._ptrs(self.flat)
-        _lib.check(_lib.lib().cwt_attention_fwd(_lib.ctx(q.device.index), _lib.ptr(q), _lib.ptr(f), B, hw,
-                                                self.d_model, self.n_head, w, fw, fb, lw, lb, _lib.ptr(out),
-                                                _lib.ptr(saved), _lib.stream_ptr(q.device)), "cwt_attention_fwd")
+        pa, po, seed = drop if drop is not None else (0.0, 0.0, 0)
+        _lib.check(_lib.lib().cwt_attention_fwd_train(_lib.ctx(q.device.index), _lib.ptr(q), _lib.ptr(f), B, hw,
+                                                      self.d_model, self.n_head, w, fw, fb, lw, lb, _lib.ptr(out),
+                                                      _lib.ptr(saved), pa, po, seed, _lib.stream_ptr(q.device)),
+                   "cwt_attention_fwd_train")
         return out, saved
 
-    def _bwd(self, q, f, saved, d_out, grad_flat):
+    def _bwd(self, q, f, saved, d_out, grad_flat, drop=None):
         B, hw = self._check(q, f)
         w, fw, fb, lw, lb = self._ptrs(self.flat)
         gw, gfw, gfb, glw, glb = self._ptrs(grad_flat)
-        _lib.check(_lib.lib().cwt_attention_bwd(_lib.ctx(q.device.index), _lib.ptr(q), _lib.ptr(f), B, hw,
-                                                self.d_model, self.n_head, w, fw, fb, lw, lb, _lib.ptr(saved),
-                                                _lib.ptr(d_out), gw, gfw, gfb, glw, glb,
-                                                _lib.stream_ptr(q.device)), "cwt_attention_bwd")
+        pa, po, seed = drop if drop is not None else (0.0, 0.0, 0)
+        _lib.check(_lib.lib().cwt_attention_bwd_train(_lib.ctx(q.device.index), _lib.ptr(q), _lib.ptr(f), B, hw,
+                                                      self.d_model, self.n_head, w, fw, fb, lw, lb, _lib.ptr(saved),
+                                                      _lib.ptr(d_out), gw, gfw, gfb, glw, glb, pa, po, seed,
+                                                      _lib.stream_ptr(q.device)), "cwt_attention_bwd_train")
 
     # -- reference API --------------------------------------------------------------------
     def forward(self, q, k, v, query_input=False):
@@ -166,22 +195,29 @@ class MultiHeadAttentionOne(torch.nn.Module):
         if k is not v and k.data_ptr() != v.data_ptr():
             raise NotImplementedError("CWT kernels attend with k == v (test.py:197, train.py:257)")
         f = as_tokens(k)
+        drop = self._drop()
         if torch.is_grad_enabled() and self.flat.requires_grad:
-            return _CWTFunction.apply(q, f, self.flat, self)
-        out, _ = self._fwd(q, f, need_saved=False)
+            return _CWTFunction.apply(q, f, self.flat, self, drop)
+        out, _ = self._fwd(q, f, need_saved=False, drop=drop)
+        return out
+
+    def infer(self, q, k):
+        """Eval-mode forward whatever the module's mode (the inference engine's call)."""
+        out, _ = self._fwd(q, as_tokens(k), need_saved=False)
         return out
 
     # explicit training API (no autograd graph; used by the episode drivers)
     def forward_train(self, q, f):
         f = as_tokens(f)
-        out, saved = self._fwd(q, f, need_saved=True)
-        return out, (q.contiguous(), f, saved)
+        drop = self._drop()
+        out, saved = self._fwd(q, f, need_saved=True, drop=drop)
+        return out, (q.contiguous(), f, saved, drop)
 
     def backward_into(self, state, d_out, grad_flat=None):
-        q, f, saved = state
+        q, f, saved, drop = state
         if grad_flat is None:
             if self.flat.grad is None:
                 self.flat.grad = torch.zeros_like(self.flat)
             grad_flat = self.flat.grad
-        self._bwd(q, f, saved, d_out.contiguous(), grad_flat)
+        self._bwd(q, f, saved, d_out.contiguous(), grad_flat, drop=drop)
         return grad_flat

@@ -153,6 +153,25 @@ int cwt_attention_bwd(cwt_ctx* ctx, const float* q, const float* f, int B, int h
                       float* g_w_qkvs, float* g_fc_w, float* g_fc_b, float* g_ln_w, float* g_ln_b,
                       void* stream);
 
+/*
+ * Training-mode forms of the two calls above (MultiHeadAttentionOne.train(): transformer.py:17,28
+ * nn.Dropout(0.1) on the attention probabilities after the softmax, transformer.py:52,80
+ * nn.Dropout(dropout) on the fc output before the residual).  Kept elements are scaled by
+ * 1/(1-p).  The masks come from a counter-based generator keyed by `seed` (include/cwt.h has no
+ * state): pass the same seed to the backward call to regenerate them.  They are NOT torch's
+ * Philox masks, so a training run matches the reference in distribution, not bit for bit; with
+ * both probabilities 0 these are exactly cwt_attention_fwd / _bwd.
+ */
+int cwt_attention_fwd_train(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                            const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
+                            const float* ln_b, float* out, float* saved, float attn_dropout, float out_dropout,
+                            uint64_t seed, void* stream);
+int cwt_attention_bwd_train(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                            const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
+                            const float* ln_b, const float* saved, const float* d_out, float* g_w_qkvs,
+                            float* g_fc_w, float* g_fc_b, float* g_ln_w, float* g_ln_b, float attn_dropout,
+                            float out_dropout, uint64_t seed, void* stream);
+
 /* Per-pixel classifier logits = W . f (test.py:200-204 Pseudo_cls; train.py:259-261 matmul).
  * W: device [B,2,C]; f: NHWC [B,P,C]; logits: device [B,2,P] (NCHW [B,2,h,w]). */
 int cwt_classify(cwt_ctx* ctx, const float* W, const float* f, int B, int P, int C, float* logits,

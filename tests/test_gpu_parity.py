@@ -47,7 +47,7 @@ def transformer(heads=4):
     from few_shot_seg_cwt_amd import MultiHeadAttentionOne
     t = MultiHeadAttentionOne(heads, 512, 512, 512, dropout=0.5)
     t.load_state_dict(syn.make_transformer_state(heads, 512, SEED))
-    return t
+    return t.eval()   # eval semantics: the oracle and the fixtures have no dropout
 
 
 @pytest.fixture(scope="module")
@@ -244,6 +244,8 @@ def test_do_epoch_vs_reference(dev, golden_dir):
     g = dict(np.load(os.path.join(golden_dir, "train_pascal_r50_1shot.npz")))
     cfg = syn.cfg_defaults()
     t = transformer(4)
+    t.attention.dropout.p = 0.0   # dropout off, as make_golden.py does on the reference module
+    t.dropout.p = 0.0
     opt = get_optimizer(cfg, [dict(params=[t.flat], lr=cfg["trans_lr"] * cfg["scale_lr"])])
     torch.manual_seed(SEED)
     recs = []
