@@ -14,7 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "csrc", "build")
 LIB = os.path.join(HERE, "libcwt.so")
-SOURCES = ["api.hip", "conv.hip", "conv_x3.hip", "conv_x3s.hip", "backbone.hip", "adapt.hip", "cwt_attn.hip", "seg.hip"]
+SOURCES = ["api.hip", "conv.hip", "conv_x3.hip", "conv_x3s.hip", "backbone.hip", "adapt.hip", "cwt_attn.hip", "seg.hip",
+           "bn_train.hip"]
 HEADERS = ["common.h", "kernels.h", "conv_plans.inc", "conv_plans_x3s.inc", "conv_plans_b16.inc"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-Wall", "-Wno-unused-function",

@@ -66,6 +66,7 @@ struct ConvLayer {
   __bf16* w_b = nullptr;   // plain bf16 [Co][K], K in packed_k64 order (bf16 conv stack; Ci % 64 == 0)
   float* scale = nullptr;
   float* shift = nullptr;
+  float* bn = nullptr;  // [4][Co] gamma, beta, running_mean, running_var (training-mode BN)
 };
 
 struct Block {
@@ -83,6 +84,11 @@ struct Backbone {  // the opaque cwt_backbone of the C ABI
   float* ppm_wt[4] = {};  // their weights K-major [2048][512] for the small-M GEMM
   ConvLayer bott;       // bottleneck conv over the 2048 layer4 channels only
   float* ppm_q[4] = {};   // bottleneck weights of PPM bin b, K-major [512][9 * 512], BN scale folded in
+  float* ppm_q_raw[4] = {};  // the same without the BN scale (training-mode BN; ppm_q is refolded)
+  float* ones = nullptr;     // [2048] scale / shift of a raw conv (training-mode BN)
+  float* zeros = nullptr;
+  float eps = 1e-5f;
+  std::map<std::string, std::pair<float*, int>> bn_by_name;  // BN prefix -> (device [4][C], C)
   std::vector<void*> allocs;
 };
 
@@ -295,6 +301,15 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
   }
   if ((rc = upload(bb, sc, &L->scale))) return rc;
   if ((rc = upload(bb, sh, &L->shift))) return rc;
+  std::vector<float> bnp4((size_t)4 * Co);
+  for (int c = 0; c < Co; ++c) {
+    bnp4[c] = g[c];
+    bnp4[Co + c] = b[c];
+    bnp4[2 * Co + c] = rm[c];
+    bnp4[3 * Co + c] = rv[c];
+  }
+  if ((rc = upload(bb, bnp4, &L->bn))) return rc;
+  bb->bn_by_name[bnp] = {L->bn, Co};
   return 0;
 }
 
@@ -317,15 +332,18 @@ static int load_ppm_fold(Backbone* bb, const HostParams& hp, float eps) {
   const float* rv = g ? hp.get("bottleneck.1.running_var", 512, &err) : nullptr;
   if (!rv) return fail(CWT_EARG, err);
   for (int b = 0; b < 4; ++b) {
-    std::vector<float> q((size_t)512 * 4608);
+    std::vector<float> q((size_t)512 * 4608), qr((size_t)512 * 4608);
     for (int co = 0; co < 512; ++co) {
       const float sc = g[co] * (1.0f / std::sqrt(rv[co] + eps));  // as load_conv's BN fold
       for (int ci = 0; ci < 512; ++ci)
-        for (int tap = 0; tap < 9; ++tap)
-          q[(size_t)ci * 4608 + tap * 512 + co] = w[((size_t)co * 4096 + 2048 + 512 * b + ci) * 9 + tap] * sc;
+        for (int tap = 0; tap < 9; ++tap) {
+          const float v = w[((size_t)co * 4096 + 2048 + 512 * b + ci) * 9 + tap];
+          qr[(size_t)ci * 4608 + tap * 512 + co] = v;
+          q[(size_t)ci * 4608 + tap * 512 + co] = v * sc;
+        }
     }
     int rc;
-    if ((rc = upload(bb, q, &bb->ppm_q[b]))) return rc;
+    if ((rc = upload(bb, q, &bb->ppm_q[b])) || (rc = upload(bb, qr, &bb->ppm_q_raw[b]))) return rc;
   }
   return 0;
 }
@@ -338,6 +356,7 @@ static int load_backbone(int layers, const HostParams& hp, float eps, Backbone**
   if (layers != 50 && layers != 101) return fail(CWT_EARG, "layers must be 50 or 101");
   Backbone* bb = new Backbone();
   bb->layers = layers;
+  bb->eps = eps;
   int rc = 0;
   auto cleanup = [&]() {
     for (void* p : bb->allocs) (void)hipFree(p);
@@ -394,7 +413,8 @@ static int load_backbone(int layers, const HostParams& hp, float eps, Backbone**
   }
   if ((rc = load_conv(bb, hp, "bottleneck.0.weight", "bottleneck.1", 2048, 512, 3, 1, 1, 1, eps, false, &bb->bott,
                       4096, 0)) ||
-      (rc = load_ppm_fold(bb, hp, eps))) {
+      (rc = load_ppm_fold(bb, hp, eps)) || (rc = upload(bb, std::vector<float>(2048, 1.0f), &bb->ones)) ||
+      (rc = upload(bb, std::vector<float>(2048, 0.0f), &bb->zeros))) {
     cleanup();
     return rc;
   }
@@ -450,14 +470,26 @@ static ConvArgs make_args(const ConvCall& c) {
   return a;
 }
 
+// Training-mode BN of one extraction (cwt_extract_features_train_bn; bn_train.hip)
+struct TrainBn {
+  float momentum, drop_p;
+  unsigned long long seed;
+};
+
 // The whole extractor as a list of conv calls + byte kernels.  dry_run sizes the split-K workspace.
+// tb != null: every BN on batch statistics with running-statistic update, Dropout2d on the
+// bottleneck output (train.py:184 model.train() before the first support extraction).
 static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N, int S, float* feat,
-                       hipStream_t st) {
+                       hipStream_t st, const TrainBn* tb = nullptr) {
   // conv arithmetic / activation storage: plain bf16 (cwt_backbone_set_precision), else the
   // context's fp32-accurate mode (S-layout bf16x3 by default)
   const bool b16 = bb->precision == CWT_CONV_BF16;
-  const bool s_path = b16 || ctx->conv_split;  // conv_x3s.hip kernels
-  const int layout = b16 ? ACT_BF16 : ctx->conv_split ? ACT_SPLIT : ACT_F32;
+  // the training-mode BN pass (once per epoch) amplifies conv rounding ~100x through its
+  // batch statistics: in fp32 precision it runs the exact-fp32 conv path
+  const bool conv_split = ctx->conv_split && !(tb && !b16);
+  const bool conv_x3 = ctx->conv_x3 && !(tb && !b16);
+  const bool s_path = b16 || conv_split;  // conv_x3s.hip kernels
+  const int layout = b16 ? ACT_BF16 : conv_split ? ACT_SPLIT : ACT_F32;
   const int prec = b16 ? 1 : 3;
   const int Hs = down2(S), H1 = down2(Hs), h = down2(H1);
   const long sA = std::max({(long)N * Hs * Hs * 128, (long)N * H1 * H1 * 256, (long)N * h * h * 2048});
@@ -550,14 +582,50 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     ConvArgs a = make_args(c);
     if (b16 && !c.L->w_b) return fail(CWT_ESTATE, "bf16 conv weights missing (Ci % 64 != 0)");
     ConvPlan pl = b16              ? plan_conv_b16(a.M, a.Co, a.K)
-                  : ctx->conv_split ? plan_conv_x3s(a.M, a.Co, a.K)
-                  : ctx->conv_x3    ? plan_conv_x3(a.M, a.Co, a.K)
+                  : conv_split ? plan_conv_x3s(a.M, a.Co, a.K)
+                  : conv_x3    ? plan_conv_x3(a.M, a.Co, a.K)
                                     : plan_conv(a.M, a.Co, a.K);
     plans.push_back(pl);
     if (pl.nsplit > 1) part_floats = std::max(part_floats, (size_t)pl.nsplit * a.M * a.Co);
   }
   const __bf16* zero = nullptr;
   if (s_path && (rc = zero_line(ctx, &zero))) return rc;
+  float *BNPART = nullptr, *BNSC = nullptr;
+  size_t bn_part_floats = 0;
+  if (tb) {
+    bn_part_floats = bn_train_part_floats((long)N * Hs * Hs, 64);
+    for (auto& c : calls) {
+      ConvArgs a = make_args(c);
+      bn_part_floats = std::max(bn_part_floats, bn_train_part_floats(a.M, a.Co));
+    }
+    if ((rc = ensure_ws(ctx, "bn.part", bn_part_floats * 4, &p))) return rc;
+    BNPART = (float*)p;
+    if ((rc = ensure_ws(ctx, "bn.bsc", 2 * 2048 * 4, &p))) return rc;
+    BNSC = (float*)p;
+  }
+  // training-mode BN of a raw conv output y (layout / row stride), residual and ReLU after it
+  auto bn_train = [&](const ConvLayer* L, void* y, int lay, int ld, long M, const void* res, int res_ld, int relu,
+                      float drop_p, long rows_per_image) -> int {
+    BnTrainArgs b;
+    memset(&b, 0, sizeof(b));
+    b.y = y;
+    b.layout = lay;
+    b.ld = ld;
+    b.M = M;
+    b.C = L->Co;
+    b.res = res;
+    b.res_ld = res_ld;
+    b.relu = relu;
+    b.bn = L->bn;
+    b.scale = L->scale;
+    b.shift = L->shift;
+    b.eps = bb->eps;
+    b.momentum = tb->momentum;
+    b.drop_p = drop_p;
+    b.seed = tb->seed;
+    b.rows_per_image = rows_per_image;
+    return launch_bn_train(b, BNPART, bn_part_floats, BNSC, st);
+  };
   float* PART = nullptr;
   if (part_floats) {
     if ((rc = ensure_ws(ctx, "bb.PART", part_floats * 4, &p))) return rc;
@@ -565,12 +633,21 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   }
   auto run_call = [&](size_t i) -> int {
     ConvArgs a = make_args(calls[i]);
+    // training-mode BN: raw conv (scale 1, shift 0); the bottleneck keeps its residual (the
+    // raw PPM half of the same conv), every other residual / ReLU moves after the BN
+    const bool keep_res = calls[i].stage == 6;
+    if (tb) {
+      a.scale = bb->ones;
+      a.shift = bb->zeros;
+      a.relu = 0;
+      if (!keep_res) a.res = nullptr;
+    }
     const ConvPlan& pl = plans[i];
     const double flops = 2.0 * a.M * a.Co * a.K;
     const double bytes = 4.0 * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K + (double)a.M * a.Co +
                                 (a.res ? (double)a.M * a.Co : 0.0));
     Prof p(ctx, st,
-           std::string(b16 ? "conv_igemm_b16<" : ctx->conv_split ? "conv_igemm_x3s<" : ctx->conv_x3 ? "conv_igemm_bf16x3<"
+           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : conv_x3 ? "conv_igemm_bf16x3<"
                                                                                                      : "conv_igemm_f32<") +
                std::to_string(pl.bm) + "," +
                std::to_string(pl.bn) + "," +
@@ -593,13 +670,13 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
         sa.y = c.y;
         sa.y_ld = c.y_ld;
         sa.y_off = c.y_off;
-        sa.res = c.res;
+        sa.res = a.res;
         sa.res_ld = c.res_ld;
       } else {
         sa.ys = (__bf16*)c.y;
-        sa.res_s = (const __bf16*)c.res;
+        sa.res_s = (const __bf16*)a.res;
       }
-      sa.relu = c.relu;
+      sa.relu = a.relu;
       sa.N = a.N;
       sa.Hi = a.Hi;
       sa.Wi = a.Wi;
@@ -616,11 +693,15 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
       sa.K = a.K;
       r = launch_conv_x3s(sa, pl, c.stage, PART, part_floats, st, prec);
     } else {
-      r = ctx->conv_x3 ? launch_conv_x3(a, pl, calls[i].stage, PART, part_floats, st)
+      r = conv_x3 ? launch_conv_x3(a, pl, calls[i].stage, PART, part_floats, st)
                        : launch_conv(a, pl, calls[i].stage, PART, part_floats, st);
     }
     p.end();
-    return r;
+    if (r || !tb) return r;
+    const ConvCall& c = calls[i];
+    const bool f32 = c.out_f32 || !s_path;
+    return bn_train(c.L, c.y, f32 ? ACT_F32 : layout, f32 ? c.y_ld : c.L->Co, a.M, keep_res ? nullptr : c.res,
+                    f32 ? c.res_ld : c.L->Co, c.relu, c.stage == 6 ? tb->drop_p : 0.f, (long)a.Ho * a.Wo);
   };
 
   const long cells = (long)N * 50;
@@ -635,10 +716,12 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   Prof whole(ctx, st, "extract_features N=" + std::to_string(N) + " S=" + std::to_string(S), all_flops, all_bytes, 1);
   {
     Prof p(ctx, st, "stem_conv1 3x64k3s2", 2.0 * N * Hs * Hs * 64 * 27, 4.0 * ((double)N * 3 * S * S + (double)N * Hs * Hs * 64));
-    if ((rc = launch_stem_conv1(img, N, S, bb->stem[0].w, bb->stem[0].scale, bb->stem[0].shift, A, Hs, st,
-                                layout)))
+    if ((rc = launch_stem_conv1(img, N, S, bb->stem[0].w, tb ? bb->ones : bb->stem[0].scale,
+                                tb ? bb->zeros : bb->stem[0].shift, A, Hs, st, layout, tb ? 0 : 1)))
       return rc;
     p.end();
+    if (tb && (rc = bn_train(&bb->stem[0], A, layout, 64, (long)N * Hs * Hs, nullptr, 0, 1, 0.f, (long)Hs * Hs)))
+      return rc;
   }
   for (size_t i = 0; i < n_stem_calls; ++i)
     if ((rc = run_call(i))) return rc;
@@ -662,15 +745,25 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   for (int i = 0; i < 4; ++i) {
     Mb[i] = N * kBins[i] * kBins[i];
     Wp[i] = bb->ppm_wt[i];
-    Wq[i] = bb->ppm_q[i];
+    Wq[i] = tb ? bb->ppm_q_raw[i] : bb->ppm_q[i];
     Sc[i] = bb->ppm[i].scale;
     Sh[i] = bb->ppm[i].shift;
   }
   {  // PPM 1x1 conv + BN + ReLU over the pooled cells (pspnet.py:27-29)
     Prof p(ctx, st, "ppm_conv smallm 2048x512", 2.0 * cells * 512 * 2048, 4.0 * (4.0 * 2048 * 512 + cells * 2560.0));
-    if ((rc = launch_smallm_gemm(POOL, 2048, Wp, Mb, 4, 512, 2048, kKcPpm, PARTS, (size_t)sPartS, Sc, Sh, PPM, st)))
+    if ((rc = launch_smallm_gemm(POOL, 2048, Wp, Mb, 4, 512, 2048, kKcPpm, PARTS, (size_t)sPartS, tb ? nullptr : Sc,
+                                 tb ? nullptr : Sh, PPM, st)))
       return rc;
     p.end();
+  }
+  if (tb) {  // the PPM BNs on the batch statistics of their pooled cells
+    long row0 = 0;
+    for (int i = 0; i < 4; ++i) {
+      if ((rc = bn_train(&bb->ppm[i], PPM + row0 * 512, ACT_F32, 512, Mb[i], nullptr, 0, 1, 0.f,
+                         (long)kBins[i] * kBins[i])))
+        return rc;
+      row0 += Mb[i];
+    }
   }
   {  // per-tap products of the bottleneck's PPM channels with the cells
     Prof p(ctx, st, "ppm_fold_q smallm 512x4608", 2.0 * cells * 4608 * 512, 4.0 * (4.0 * 512 * 4608 + cells * 5120.0));
@@ -687,6 +780,9 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   }
   rc = run_call(n_backbone_calls);
   whole.end();
+  if (!rc && tb)  // refold the bottleneck's new eval BN scale into the PPM-branch weights
+    for (int i = 0; i < 4 && !rc; ++i)
+      rc = launch_scale_cols(bb->ppm_q_raw[i], bb->ppm_q[i], 512L * 4608, 512, bb->bott.scale, st);
   return rc;
 }
 
@@ -771,6 +867,34 @@ int cwt_extract_features(cwt_ctx* ctx, const cwt_backbone* handle, const float* 
   CWT_CHECK(N >= 1 && S >= 9 && (S - 1) % 8 == 0, "need N >= 1 and (S-1) % 8 == 0 (pspnet.py:150)");
   CWT_HIP(hipSetDevice(ctx->device));
   return run_extract(ctx, bb, img, N, S, feat, (hipStream_t)stream);
+}
+
+int cwt_extract_features_train_bn(cwt_ctx* ctx, cwt_backbone* handle, const float* img, int N, int S, float* feat,
+                                  float momentum, float dropout_p, uint64_t seed, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  Backbone* bb = reinterpret_cast<Backbone*>(handle);
+  if (!bb) return fail(CWT_ESTATE, "backbone is NULL (cwt_backbone_load)");
+  if (bb->device != ctx->device) return fail(CWT_EARG, "backbone and context are on different devices");
+  CWT_CHECK(img && feat, "null buffer");
+  CWT_CHECK(N >= 1 && S >= 9 && (S - 1) % 8 == 0, "need N >= 1 and (S-1) % 8 == 0 (pspnet.py:150)");
+  CWT_CHECK(N >= 2, "Expected more than 1 value per channel when training (the PPM bin-1 BatchNorm2d needs N >= 2)");
+  CWT_CHECK(momentum >= 0.f && momentum <= 1.f && dropout_p >= 0.f && dropout_p < 1.f, "bad momentum / dropout_p");
+  CWT_HIP(hipSetDevice(ctx->device));
+  TrainBn tb{momentum, dropout_p, (unsigned long long)seed};
+  return run_extract(ctx, bb, img, N, S, feat, (hipStream_t)stream, &tb);
+}
+
+int cwt_backbone_read_bn(const cwt_backbone* handle, const char* name, float* out, int C) {
+  const Backbone* bb = reinterpret_cast<const Backbone*>(handle);
+  if (!bb) return fail(CWT_ESTATE, "backbone is NULL (cwt_backbone_load)");
+  CWT_CHECK(name && out, "null argument");
+  auto it = bb->bn_by_name.find(name);
+  if (it == bb->bn_by_name.end()) return fail(CWT_EARG, std::string("no BatchNorm2d named ") + name);
+  CWT_CHECK(it->second.second == C, "C does not match the BatchNorm2d's channel count");
+  CWT_HIP(hipSetDevice(bb->device));
+  CWT_HIP(hipDeviceSynchronize());
+  CWT_HIP(hipMemcpy(out, it->second.first, sizeof(float) * 4 * C, hipMemcpyDeviceToHost));
+  return 0;
 }
 
 size_t cwt_workspace_bytes(cwt_ctx* ctx) { return ctx ? ctx->ws_total : 0; }

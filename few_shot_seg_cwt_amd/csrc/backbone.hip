@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void stem_conv1_kernel(const float* __restrict
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
-                                                         float* __restrict__ out, int Ho) {
+                                                         float* __restrict__ out, int Ho, float floor_) {
   __shared__ float ws[27 * 64];
   __shared__ float ss[64], bs[64];
   for (int i = threadIdx.x; i < 27 * 64; i += blockDim.x) ws[i] = w[i];
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void stem_conv1_kernel(const float* __restrict
         acc += in[k] * wv;
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) r[h * 4 + q] = fmaxf(fmaf(acc[q], ss[c4 * 4 + q], bs[c4 * 4 + q]), 0.f);
+      for (int q = 0; q < 4; ++q) r[h * 4 + q] = fmaxf(fmaf(acc[q], ss[c4 * 4 + q], bs[c4 * 4 + q]), floor_);
     }
     if (SPLIT) {
       bf16x8 hi, lo;
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void stem_conv1_s_kernel(const float* __restri
                                                            const float* __restrict__ w,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
-                                                           __bf16* __restrict__ out, int Ho) {
+                                                           __bf16* __restrict__ out, int Ho, float floor_) {
   __shared__ float ws[27 * 64];
   for (int i = threadIdx.x; i < 27 * 64; i += blockDim.x) ws[i] = w[i];
   __syncthreads();
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void stem_conv1_s_kernel(const float* __restri
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int c = g * 8 + q;
-    const float r = fmaxf(fmaf(q < 4 ? a0[q & 3] : a1[q & 3], scale[c], shift[c]), 0.f);
+    const float r = fmaxf(fmaf(q < 4 ? a0[q & 3] : a1[q & 3], scale[c], shift[c]), floor_);
     hi[q] = (__bf16)r;
     lo[q] = (__bf16)(r - (float)hi[q]);
   }
@@ -136,17 +136,18 @@ __global__ __launch_bounds__(256) void stem_conv1_s_kernel(const float* __restri
 }
 
 int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const float* scale,
-                      const float* shift, float* out, int Ho, hipStream_t st, int layout) {
+                      const float* shift, float* out, int Ho, hipStream_t st, int layout, int relu) {
   long total = (long)N * Ho * Ho;
+  const float floor_ = relu ? 0.f : -INFINITY;  // relu = 0: raw conv (training-mode BN follows)
   if (layout == ACT_SPLIT)
     hipLaunchKernelGGL(stem_conv1_s_kernel<false>, dim3(cdiv(total * 8, 256)), dim3(256), 0, st, img, N, S, w27x64,
-                       scale, shift, (__bf16*)out, Ho);
+                       scale, shift, (__bf16*)out, Ho, floor_);
   else if (layout == ACT_BF16)
     hipLaunchKernelGGL(stem_conv1_s_kernel<true>, dim3(cdiv(total * 8, 256)), dim3(256), 0, st, img, N, S, w27x64,
-                       scale, shift, (__bf16*)out, Ho);
+                       scale, shift, (__bf16*)out, Ho, floor_);
   else
     hipLaunchKernelGGL(stem_conv1_kernel<false>, dim3(cdiv(total, 256)), dim3(256), 0, st, img, N, S, w27x64, scale,
-                       shift, out, Ho);
+                       shift, out, Ho, floor_);
   CWT_LAUNCH_CHECK();
   return 0;
 }

@@ -148,7 +148,31 @@ struct AdaptGraphCache {
 // backbone helpers (backbone.hip).  Activation storage of the conv stack:
 enum ActLayout { ACT_F32 = 0, ACT_SPLIT = 1, ACT_BF16 = 2 };  // fp32 NHWC, S-layout, bf16 NHWC
 int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const float* scale,
-                      const float* shift, float* out, int Ho, hipStream_t st, int layout = ACT_F32);
+                      const float* shift, float* out, int Ho, hipStream_t st, int layout = ACT_F32,
+                      int relu = 1);
+// Training-mode BatchNorm over a raw conv output (bn_train.hip): batch statistics of the M
+// rows, running-statistic update (momentum, unbiased variance), eval fold rewritten from the
+// new running statistics, then y = [relu](bn(y) [+ res]) [* Dropout2d mask] in place.
+struct BnTrainArgs {
+  void* y;          // activation in `layout` (ACT_F32 rows of ld floats; S-layout / bf16: ld = C)
+  int layout, ld;
+  long M;           // rows (N * H * W)
+  int C;
+  const void* res;  // optional residual, same layout as y
+  int res_ld;
+  int relu;
+  float* bn;        // device [4][C]: gamma, beta, running_mean, running_var (updated)
+  float* scale;     // eval fold gamma / sqrt(rv + eps) and beta - rm * scale (rewritten)
+  float* shift;
+  float eps, momentum;
+  float drop_p;     // Dropout2d over (image, channel), stream 3 of dropout_scale
+  unsigned long long seed;
+  long rows_per_image;
+};
+size_t bn_train_part_floats(long M, int C);
+int launch_bn_train(const BnTrainArgs& a, float* part, size_t part_floats, float* batch_sc, hipStream_t st);
+// dst[i] = src[i] * sc[i % period] (the PPM fold of the bottleneck BN scale)
+int launch_scale_cols(const float* src, float* dst, long n, int period, const float* sc, hipStream_t st);
 int launch_maxpool3s2_s(const __bf16* in, int N, int H, int W, int C, __bf16* out, int Ho, int Wo, hipStream_t st);
 int launch_maxpool3s2_b16(const __bf16* in, int N, int H, int W, int C, __bf16* out, int Ho, int Wo, hipStream_t st);
 int launch_maxpool3s2(const float* in, int N, int H, int W, int C, float* out, int Ho, int Wo,

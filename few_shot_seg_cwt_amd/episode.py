@@ -335,18 +335,32 @@ def validate_transformer(args, val_loader, model, transformer, episodes_out: lis
 
 def train_episode(model, transformer, args, batch, W0: torch.Tensor, dev) -> dict:
     """Forward/backward of one training episode (train.py:188-267) without the optimiser
-    step; gradients are ACCUMULATED into transformer.flat.grad.  Backbone eval (frozen),
-    CWT dropout off.  The 1-shot support is not duplicated: the reference's two identical
-    copies (train.py:199-201) give exactly the same inner-loop loss and gradient as one."""
+    step; gradients are ACCUMULATED into transformer.flat.grad.  CWT dropouts follow
+    transformer.training.  In eval mode the 1-shot support is not duplicated: the reference's
+    two identical copies (train.py:199-201) give exactly the same inner-loop loss and gradient
+    as one, and support + query share one extractor pass.  With the model in train mode (the
+    first episode of an epoch, train.py:184) the support pass runs train-mode BN over the
+    duplicated batch (batch statistics of both copies, Dropout2d masks differ per copy), then
+    model.eval() (train.py:245) and the query pass sees the updated running statistics."""
     qry_img, q_label, spprt_imgs, s_label, subcls = batch[:5]
     S = int(_a(args, "image_size", 473))
     shot = spprt_imgs.shape[1]
     _class_weight_check(s_label)
-    imgs = torch.cat([spprt_imgs[0], qry_img], 0).to(dev, non_blocking=True)
     sl = s_label[0].to(dev, non_blocking=True).long()
     ql = q_label.to(dev, non_blocking=True).long()
-    f_all, _ = model.extract_features(imgs)
-    f_s, f_q = f_all[:shot], f_all[shot:]
+    if getattr(model, "training", False):
+        sp = spprt_imgs[0].to(dev, non_blocking=True)
+        if shot == 1:
+            sp = sp.expand(2, -1, -1, -1)
+            sl = sl.expand(2, -1, -1)
+        f_s, _ = model.extract_features(sp.contiguous())
+        model.eval()
+        f_q, _ = model.extract_features(qry_img.to(dev, non_blocking=True))
+        sl = sl.contiguous()
+    else:
+        imgs = torch.cat([spprt_imgs[0], qry_img], 0).to(dev, non_blocking=True)
+        f_all, _ = model.extract_features(imgs)
+        f_s, f_q = f_all[:shot], f_all[shot:]
     W = inner_adapt(f_s, sl, W0.to(dev), float(_a(args, "cls_lr", 0.1)), int(_a(args, "adapt_iter", 200)))
     Wb = W.view(1, 2, -1)
     fqn, pred_q0 = normalize(f_q, Wb)

@@ -7,9 +7,13 @@ HIP kernels in libcwt.so; ``f`` is returned as an [N,512,h,w] tensor in channels
 memory format (NHWC), which is what every downstream kernel reads.
 
 Weights are loaded with ``load_state_dict`` using the reference key names (the
-reference's ``PSPNet.state_dict()``, `gamma` first, pspnet.py:141).  Only eval semantics
-are implemented: the backbone is frozen in every CWT driver (train.py:77-91); the
-reference's first-episode train-mode BN quirk (train.py:184) is out of scope.
+reference's ``PSPNet.state_dict()``, `gamma` first, pspnet.py:141).  The backbone weights
+are frozen in every CWT driver (train.py:77-91), but the module follows ``train()`` /
+``eval()`` as the reference's does: after ``model.train()`` (train.py:184, the start of every
+epoch) ``extract_features`` runs every BatchNorm on batch statistics, moves the running
+statistics by momentum 0.1 (on the device; later eval extractions use them) and applies the
+bottleneck's Dropout2d(p=args.dropout) -- cwt_extract_features_train_bn.  ``bn_train_mode:
+False`` in args keeps eval semantics under ``train()`` (the golden fixture without the quirk).
 """
 from __future__ import annotations
 
@@ -20,6 +24,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .util import dropout_seed
 from .synthetic import BN_EPS, feature_side, pspnet_param_specs
 
 
@@ -55,6 +60,10 @@ class PSPNet:
         self._state = None
         self._handle = None
         self.training = False
+        self.bn_train_mode = bool(_arg(args, "bn_train_mode", True))
+        self.dropout_p = float(_arg(args, "dropout", 0.1))   # bottleneck Dropout2d (pspnet.py:128)
+        self.bn_momentum = 0.1                                 # nn.BatchNorm2d default
+        self._stats_moved = False
         # conv-stack arithmetic (BASELINE config #5): "fp32" (reference numerics, default) or
         # "bf16" (bf16 MFMA convs, bf16 activations between convs, fp32 feature map out)
         self.conv_dtype = str(_arg(args, "conv_dtype", "fp32"))
@@ -90,8 +99,8 @@ class PSPNet:
         return self
 
     def train(self, mode: bool = True):
-        # Eval semantics only (frozen backbone); see module docstring.
-        self.training = False
+        # train-mode BN + Dropout2d in extract_features (module docstring)
+        self.training = bool(mode) and self.bn_train_mode
         return self
 
     def cuda(self, *a, **k):
@@ -103,6 +112,17 @@ class PSPNet:
     def state_dict(self):
         if self._state is None:
             raise RuntimeError("no weights loaded")
+        if self._stats_moved:   # running statistics moved on the device by train-mode extractions
+            for k in list(self._state):
+                if k.endswith(".running_mean"):
+                    p = k[: -len(".running_mean")]
+                    C_ = self._state[k].shape[0]
+                    buf = np.empty((4, C_), np.float32)
+                    _lib.check(_lib.lib().cwt_backbone_read_bn(self._handle, p.encode(), buf.ctypes.data, C_),
+                               "cwt_backbone_read_bn")
+                    self._state[k] = buf[2].copy()
+                    self._state[p + ".running_var"] = buf[3].copy()
+            self._stats_moved = False
         return OrderedDict((k, torch.from_numpy(np.array(v))) for k, v in self._state.items())
 
     def load_state_dict(self, state_dict, strict: bool = True):
@@ -139,6 +159,7 @@ class PSPNet:
         self._release()
         self._handle = handle
         self._state = sd
+        self._stats_moved = False
         self.set_conv_dtype(self.conv_dtype)
         return self
 
@@ -163,6 +184,13 @@ class PSPNet:
                               memory_format=torch.channels_last)
         if x.device != self.device:
             raise ValueError(f"x is on {x.device}, the backbone on {self.device}")
+        if self.training:
+            seed = dropout_seed()   # Dropout2d masks; the host RNG stream stays the reference's
+            _lib.check(_lib.lib().cwt_extract_features_train_bn(
+                _lib.ctx(x.device.index), self._handle, _lib.ptr(x), N, S, _lib.ptr(out), self.bn_momentum,
+                self.dropout_p, seed, _lib.stream_ptr(x.device)), "cwt_extract_features_train_bn")
+            self._stats_moved = True
+            return out, []
         _lib.check(_lib.lib().cwt_extract_features(_lib.ctx(x.device.index), self._handle, _lib.ptr(x), N, S,
                                                    _lib.ptr(out),
                                                    _lib.stream_ptr(x.device)), "cwt_extract_features")

@@ -15,7 +15,8 @@ Differences from the reference, by design: k and v must be the same 
 dropouts run as in the reference (``self.attention.dropout`` p=0.1 on the attention
 probabilities, ``self.dropout`` on the fc output; set their ``.p`` to 0 exactly as the
 reference would), with masks from the kernels' counter-based generator (a fresh seed per
-forward from torch's CPU RNG) instead of torch's Philox stream.
+forward, util.dropout_seed: the host RNG stream that draws W0 is left untouched, as the
+reference's CUDA-generator dropouts leave it) instead of torch's Philox stream.
 """
 from __future__ import annotations
 
@@ -26,6 +27,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .util import dropout_seed
 
 
 def _layout(heads: int, C: int):
@@ -160,7 +162,7 @@ class MultiHeadAttentionOne(torch.nn.Module):
         pa, po = float(self.attention.dropout.p), float(self.dropout.p)
         if not self.training or (pa == 0.0 and po == 0.0):
             return None
-        seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())  # host RNG: no device sync
+        seed = dropout_seed()   # leaves the host RNG stream (W0 draws) as the reference's
         return pa, po, seed
 
     def _fwd(self, q, f, need_saved: bool, drop=None):

@@ -33,6 +33,23 @@ class AverageMeter:
         self.avg = self.sum / self.count
 
 
+_seed_state = [None, 0]
+
+
+def dropout_seed() -> int:
+    """Seed of one counter-based dropout draw (csrc/common.h dropout_uniform).  The reference's
+    dropouts run on CUDA tensors and draw from the CUDA generator, so they never move the host
+    RNG stream that the per-episode classifier init (nn.Conv2d, train.py:206) draws W0 from; to
+    keep that stream identical this seed comes from the device generator's initial seed and a
+    per-process counter (restarted when torch.manual_seed changes the initial seed)."""
+    base = int(torch.cuda.initial_seed()) if torch.cuda.is_available() else int(torch.initial_seed())
+    if _seed_state[0] != base:
+        _seed_state[0], _seed_state[1] = base, 0
+    n = _seed_state[1]
+    _seed_state[1] += 1
+    return (base * 0x9E3779B97F4A7C15 + n * 0xD1B54A32D192ED03 + 1) & ((1 << 62) - 1)
+
+
 def intersectionAndUnionGPU(preds: torch.Tensor, target: torch.Tensor, num_classes: int,
                             ignore_index: int = 255) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """util.py:280-308 on argmax maps: returns (intersection, union, target) [num_classes] float."""

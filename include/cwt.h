@@ -90,6 +90,32 @@ int cwt_backbone_set_precision(cwt_backbone* bb, int precision);
 int cwt_extract_features(cwt_ctx* ctx, const cwt_backbone* bb, const float* img, int N, int S,
                          float* feat, void* stream);
 
+/*
+ * Feature extractor forward in TRAINING mode (the reference's do_epoch quirk: model.train() at
+ * the start of each epoch, model.eval() only before the first query, so the first support
+ * extraction of every epoch runs train-mode; train.py:184,219,245).
+ * Replaces: PSPNet.extract_features(x) with model.training == True (pspnet.py:172-181):
+ *   every BatchNorm2d normalises with the batch statistics over N*h*w (PPM bins: N*b*b),
+ *   then moves its running statistics by `momentum` (torch: unbiased variance) -- the
+ *   backbone's eval-mode folds (and the PPM-branch weights) are rewritten on the device, so
+ *   later cwt_extract_features calls see the updated statistics;
+ *   Dropout2d(dropout_p) zeroes whole (image, channel) planes of the bottleneck output and
+ *   scales the rest by 1/(1-dropout_p); mask = counter draw (seed, stream 3, n*512+c).
+ * N >= 2 (the PPM bin-1 BatchNorm sees N values; torch raises for 1).  Not thread-safe
+ * against concurrent extractions with the same backbone.
+ */
+int cwt_extract_features_train_bn(cwt_ctx* ctx, cwt_backbone* bb, const float* img, int N, int S,
+                                  float* feat, float momentum, float dropout_p, uint64_t seed,
+                                  void* stream);
+
+/*
+ * Read back one BatchNorm2d's parameters as [4][C] floats (weight, bias, running_mean,
+ * running_var) into host memory; name = the reference module prefix ("layer0.1",
+ * "layer3.5.bn2", "ppm.features.2.2", "bottleneck.1").  Synchronises the device.  Replaces the
+ * BN entries of PSPNet.state_dict() after train-mode extractions moved the statistics.
+ */
+int cwt_backbone_read_bn(const cwt_backbone* bb, const char* name, float* out, int C);
+
 /* Bytes of device workspace the context holds (activations etc.; shared by all backbones). */
 size_t cwt_workspace_bytes(cwt_ctx* ctx);
 

@@ -30,21 +30,23 @@ def to_torch_state(sd) -> Dict[str, torch.Tensor]:
     return {k: (v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))) for k, v in sd.items()}
 
 
-def _bn(x, sd, p):
-    # nn.BatchNorm2d in eval mode (running statistics), eps 1e-5
+def _bn(x, sd, p, mom=None):
+    # nn.BatchNorm2d in eval mode (running statistics), eps 1e-5; mom != None: training mode
+    # (batch statistics, running statistics of sd moved in place by mom, unbiased variance)
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"],
-                        sd[p + ".bias"], training=False, momentum=0.0, eps=BN_EPS)
+                        sd[p + ".bias"], training=mom is not None, momentum=0.0 if mom is None else mom,
+                        eps=BN_EPS)
 
 
 def _conv(x, sd, name, stride=1, padding=0, dilation=1):
     return F.conv2d(x, sd[name], None, stride, padding, dilation)
 
 
-def stem(x, sd):
+def stem(x, sd, mom=None):
     """layer0 (pspnet.py:93-95; resnet.py:110-118): 3x[conv3x3+BN+ReLU] (first stride 2) + maxpool 3/2/1."""
-    x = F.relu(_bn(_conv(x, sd, "layer0.0.weight", 2, 1), sd, "layer0.1"))
-    x = F.relu(_bn(_conv(x, sd, "layer0.3.weight", 1, 1), sd, "layer0.4"))
-    x = F.relu(_bn(_conv(x, sd, "layer0.6.weight", 1, 1), sd, "layer0.7"))
+    x = F.relu(_bn(_conv(x, sd, "layer0.0.weight", 2, 1), sd, "layer0.1", mom))
+    x = F.relu(_bn(_conv(x, sd, "layer0.3.weight", 1, 1), sd, "layer0.4", mom))
+    x = F.relu(_bn(_conv(x, sd, "layer0.6.weight", 1, 1), sd, "layer0.7", mom))
     return F.max_pool2d(x, 3, 2, 1)
 
 
@@ -60,48 +62,52 @@ def block_geometry(layer: int, block: int) -> Tuple[int, int, int]:
     return 1, 4, 1
 
 
-def bottleneck(x, sd, layer: int, block: int):
+def bottleneck(x, sd, layer: int, block: int, mom=None):
     """Bottleneck.forward (resnet.py:74-96)."""
     p = f"layer{layer}.{block}"
     s, d, ds = block_geometry(layer, block)
-    out = F.relu(_bn(_conv(x, sd, p + ".conv1.weight"), sd, p + ".bn1"))
-    out = F.relu(_bn(_conv(out, sd, p + ".conv2.weight", s, d, d), sd, p + ".bn2"))
-    out = _bn(_conv(out, sd, p + ".conv3.weight"), sd, p + ".bn3")
+    out = F.relu(_bn(_conv(x, sd, p + ".conv1.weight"), sd, p + ".bn1", mom))
+    out = F.relu(_bn(_conv(out, sd, p + ".conv2.weight", s, d, d), sd, p + ".bn2", mom))
+    out = _bn(_conv(out, sd, p + ".conv3.weight"), sd, p + ".bn3", mom)
     if block == 0:
-        res = _bn(_conv(x, sd, p + ".downsample.0.weight", ds), sd, p + ".downsample.1")
+        res = _bn(_conv(x, sd, p + ".downsample.0.weight", ds), sd, p + ".downsample.1", mom)
     else:
         res = x
     return F.relu(out + res)
 
 
-def backbone(x, sd, layers: int = 50):
+def backbone(x, sd, layers: int = 50, mom=None):
     """get_feat_list (pspnet.py:272-287): layer0..layer4, returns the layer4 output."""
-    x = stem(x, sd)
+    x = stem(x, sd, mom)
     for li, nblk in enumerate(RESNET_BLOCKS[layers], start=1):
         for b in range(nblk):
-            x = bottleneck(x, sd, li, b)
+            x = bottleneck(x, sd, li, b, mom)
     return x
 
 
-def ppm(x, sd, bins=(1, 2, 3, 6)):
+def ppm(x, sd, bins=(1, 2, 3, 6), mom=None):
     """PPM.forward (pspnet.py:33-38): AdaptiveAvgPool -> 1x1 conv -> BN -> ReLU ->
     bilinear(align_corners=True) back to h x w; concat [x, b1..b4]."""
     h, w = x.shape[-2:]
     outs = [x]
     for i, b in enumerate(bins):
         y = F.adaptive_avg_pool2d(x, b)
-        y = F.relu(_bn(_conv(y, sd, f"ppm.features.{i}.1.weight"), sd, f"ppm.features.{i}.2"))
+        y = F.relu(_bn(_conv(y, sd, f"ppm.features.{i}.1.weight"), sd, f"ppm.features.{i}.2", mom))
         outs.append(F.interpolate(y, (h, w), mode="bilinear", align_corners=True))
     return torch.cat(outs, 1)
 
 
-def extract_features(x, sd, layers: int = 50):
+def extract_features(x, sd, layers: int = 50, train_bn_momentum=None, drop2d_scale=None):
     """PSPNet.extract_features (pspnet.py:172-181) in eval mode: backbone -> PPM ->
-    bottleneck conv3x3 4096->512 + BN + ReLU (+Dropout2d, identity in eval) (pspnet.py:124-129)."""
+    bottleneck conv3x3 4096->512 + BN + ReLU (+Dropout2d, identity in eval) (pspnet.py:124-129).
+    train_bn_momentum: the module in train mode (train.py:184): every BN on batch statistics,
+    sd's running statistics updated in place; drop2d_scale [N,512]: the Dropout2d mask x 1/(1-p)."""
     with torch.no_grad():
-        f = backbone(x, sd, layers)
-        f = ppm(f, sd)
-        f = F.relu(_bn(_conv(f, sd, "bottleneck.0.weight", 1, 1), sd, "bottleneck.1"))
+        f = backbone(x, sd, layers, train_bn_momentum)
+        f = ppm(f, sd, mom=train_bn_momentum)
+        f = F.relu(_bn(_conv(f, sd, "bottleneck.0.weight", 1, 1), sd, "bottleneck.1", train_bn_momentum))
+        if drop2d_scale is not None:
+            f = f * drop2d_scale[:, :, None, None]
     return f
 
 

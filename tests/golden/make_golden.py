@@ -16,6 +16,10 @@ Captured:
                                intersectionAndUnionGPU
   episode_*.npz                validate_transformer (test.py:103) full-size episodes
   train_pascal_r50_1shot.npz   do_epoch (train.py:166) training episodes, dropout off, BN eval
+  train_pascal_r50_1shot_bnq.npz  the same with the reference's first-episode train-mode BN
+                               (model.train() at train.py:184), Dropout2d p = 0
+  bn_train_small.npz           PSPNet.extract_features in train mode at S=33 (batch statistics,
+                               running-statistic update, Dropout2d p = 0), then eval on the query
 """
 from __future__ import annotations
 
@@ -201,14 +205,21 @@ def run_validate(rtest, rutil, rpsp, rtr, name, yaml_name, layers, S, shot, n_ep
     print(name, "mIoU", miou, "loss", loss)
 
 
-def run_train(rtrain, rutil, rpsp, rtr, name, n_iter):
+BN_PROBES = ["layer0.1", "layer1.0.downsample.1", "layer4.2.bn3", "ppm.features.0.2", "ppm.features.3.2",
+             "bottleneck.1"]
+
+
+def run_train(rtrain, rutil, rpsp, rtr, name, n_iter, bn_quirk=False):
     from src.optimizer import get_optimizer
     over = ["shot", "1", "layers", "50", "trans_lr", "0.001", "heads", "4", "cls_lr", "0.1", "batch_size", "1",
             "batch_size_val", "1"]
+    if bn_quirk:
+        over += ["dropout", "0.0"]                   # Dropout2d identity (its RNG is torch's)
     args = ref_args(rutil, "pascal.yaml", over)
     torch.manual_seed(SEED)
     model = build_model(rpsp, args, 50)
-    model.train = lambda mode=True: model            # exclude the first-episode BN quirk
+    if not bn_quirk:
+        model.train = lambda mode=True: model        # exclude the first-episode BN quirk
     transformer = build_transformer(rtr, 4)
     transformer.attention.dropout.p = 0.0            # dropout off for parity (SURVEY §7 hard part 3)
     transformer.dropout.p = 0.0
@@ -241,9 +252,17 @@ def run_train(rtrain, rutil, rpsp, rtr, name, n_iter):
         out[f"e{e}_W2"] = r["W2"].numpy().reshape(2, 512)
         out[f"e{e}_loss_q"] = r["loss_q"].numpy()
         out[f"e{e}_fs_stat"] = stat(r["feats"][0])
+        if bn_quirk:
+            out[f"e{e}_fs_sample"] = r["feats"][0].numpy().reshape(-1)[::997].copy()
+            out[f"e{e}_fq_sample"] = r["feats"][1].numpy().reshape(-1)[::997].copy()
         for n, g in grads[e].items():
             out[f"e{e}_grad_{n}_stat"] = stat(g)
             out[f"e{e}_grad_{n}_sample"] = g.numpy().reshape(-1)[::101].copy()
+    if bn_quirk:
+        sd = model.state_dict()
+        for p in BN_PROBES:
+            out[f"rm_{p}"] = sd[p + ".running_mean"].numpy().copy()
+            out[f"rv_{p}"] = sd[p + ".running_var"].numpy().copy()
     for n, p in transformer.named_parameters():
         out[f"final_{n}_stat"] = stat(p.detach())
         out[f"final_{n}_sample"] = p.detach().numpy().reshape(-1)[::101].copy()
@@ -306,10 +325,35 @@ def run_modules(rutil, rpsp, rtr):
     print("modules_small.npz written")
 
 
+def run_bn_train(rutil, rpsp):
+    """PSPNet.extract_features with the module in train mode (every BN on batch statistics,
+    running statistics moved by momentum 0.1), then eval mode over the updated statistics."""
+    out = {}
+    S = 33
+    for layers in (50, 101):
+        args = ref_args(rutil, "pascal.yaml", ["layers", str(layers), "dropout", "0.0"])
+        model = build_model(rpsp, args, layers)
+        ep = syn.make_episode(SEED, 7, S, 2)
+        model.train()
+        with torch.no_grad():
+            f_tr, _ = model.extract_features(torch.from_numpy(ep["spprt_imgs"][0]))
+        model.eval()
+        with torch.no_grad():
+            f_ev, _ = model.extract_features(torch.from_numpy(ep["qry_img"]))
+        out[f"feat_train_r{layers}"] = f_tr.numpy()
+        out[f"feat_eval_after_r{layers}"] = f_ev.numpy()
+        sd = model.state_dict()
+        for p in BN_PROBES:
+            out[f"r{layers}_rm_{p}"] = sd[p + ".running_mean"].numpy().copy()
+            out[f"r{layers}_rv_{p}"] = sd[p + ".running_var"].numpy().copy()
+    np.savez_compressed(os.path.join(HERE, "bn_train_small.npz"), **out)
+    print("bn_train_small.npz written")
+
+
 def main():
     torch.set_num_threads(8)
     rtest, rtrain, rutil, rpsp, rtr = import_reference()
-    which = sys.argv[1:] or ["modules", "pascal1", "pascal5", "coco1", "train"]
+    which = sys.argv[1:] or ["modules", "pascal1", "pascal5", "coco1", "train", "bn_train", "train_bnq"]
     if "modules" in which:
         run_modules(rutil, rpsp, rtr)
     if "pascal1" in which:
@@ -321,6 +365,10 @@ def main():
                      classes=syn.coco_val_classes(0))
     if "train" in which:
         run_train(rtrain, rutil, rpsp, rtr, "train_pascal_r50_1shot.npz", 2)
+    if "bn_train" in which:
+        run_bn_train(rutil, rpsp)
+    if "train_bnq" in which:
+        run_train(rtrain, rutil, rpsp, rtr, "train_pascal_r50_1shot_bnq.npz", 2, bn_quirk=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,140 @@
+"""Training-mode BatchNorm of the extractor (the reference's first-episode quirk: model.train()
+at train.py:184, model.eval() only before the first query at train.py:245).  The HIP path
+(cwt_extract_features_train_bn) against fixtures produced by the REFERENCE PSPNet itself
+(tests/golden/make_golden.py bn_train / train_bnq, Dropout2d p = 0) and, for the Dropout2d
+mask, against the oracle (F.batch_norm training=True) with the same counter-based mask.
+Bars: full size (S=473, do_epoch) 1e-3 relative as every other parity test.  At S=33 the
+train-mode BN is ill-conditioned (layer4 normalises over 2 x 5 x 5 values, PPM bin 1 over 2):
+the reference itself moves by 1.4e-4 between fp32 and fp64 there (eval mode: 4.6e-7) and a
+1e-6 relative weight perturbation moves it by 2.9e-4.  The train-mode pass therefore runs the
+exact-fp32 conv path (bf16x3 would land at 3.2e-3); measured 3.1e-4 (R50) and 1.5e-3 (R101),
+statistics within 1e-4 (tools/diag_bn_train.py) -- S=33 bars 5e-3 / 1e-3."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from few_shot_seg_cwt_amd import synthetic as syn  # noqa: E402
+from dropout_ref import dropout_scale  # noqa: E402
+
+SEED = 2021
+TOL = 1e-3
+TOL_S33 = 5e-3
+TOL_S33_STATS = 1e-3
+PROBES = ["layer0.1", "layer1.0.downsample.1", "layer4.2.bn3", "ppm.features.0.2", "ppm.features.3.2",
+          "bottleneck.1"]
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
+    b = b.detach().double().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def fresh_model(layers, **over):
+    """A model of its own: train-mode extractions move its running statistics."""
+    from few_shot_seg_cwt_amd import get_model
+    m = get_model(syn.cfg_defaults(layers=layers, **over))
+    m.load_state_dict(syn.make_pspnet_state(layers, SEED))
+    return m
+
+
+@pytest.mark.parametrize("layers", [50, 101])
+def test_train_bn_small_vs_reference(dev, golden_dir, layers):
+    g = dict(np.load(os.path.join(golden_dir, "bn_train_small.npz")))
+    m = fresh_model(layers, dropout=0.0)
+    ep = syn.make_episode(SEED, 7, 33, 2)
+    m.train()
+    f_tr, _ = m.extract_features(torch.from_numpy(ep["spprt_imgs"][0]).to(dev))
+    m.eval()
+    f_ev, _ = m.extract_features(torch.from_numpy(ep["qry_img"]).to(dev))
+    torch.cuda.synchronize()
+    assert rel(f_tr, g[f"feat_train_r{layers}"]) < TOL_S33
+    assert rel(f_ev, g[f"feat_eval_after_r{layers}"]) < TOL_S33
+    sd = m.state_dict()
+    for p in PROBES:
+        assert rel(sd[p + ".running_mean"], g[f"r{layers}_rm_{p}"]) < TOL_S33_STATS, p
+        assert rel(sd[p + ".running_var"], g[f"r{layers}_rv_{p}"]) < TOL_S33_STATS, p
+        # weight / bias untouched
+        np.testing.assert_array_equal(sd[p + ".weight"].numpy(), syn.make_pspnet_state(layers, SEED)[p + ".weight"])
+
+
+def test_train_bn_dropout2d_vs_oracle(dev):
+    """Dropout2d(p) on the bottleneck output: whole (image, channel) planes, mask = the
+    counter draw (seed, stream 3, n * 512 + c); BN batch statistics as the oracle's."""
+    from few_shot_seg_cwt_amd import _lib
+    from oracle import cwt_oracle as O
+    p, seed, S, N = 0.5, 12345, 33, 3
+    m = fresh_model(50, dropout=p)
+    sd = O.to_torch_state(syn.make_pspnet_state(50, SEED))
+    ep = syn.make_episode(SEED, 3, S, N)
+    x = torch.from_numpy(ep["spprt_imgs"][0])
+    h = syn.feature_side(S)
+    out = torch.empty((N, 512, h, h), device=dev, memory_format=torch.channels_last)
+    xd = x.to(dev).contiguous()
+    _lib.check(_lib.lib().cwt_extract_features_train_bn(_lib.ctx(0), m._handle, _lib.ptr(xd), N, S, _lib.ptr(out),
+                                                        0.1, p, seed, _lib.stream_ptr(dev)), "train_bn")
+    torch.cuda.synchronize()
+    mask = torch.from_numpy(dropout_scale(p, seed, 3, np.arange(N * 512)).reshape(N, 512))
+    ref = O.extract_features(x, sd, 50, train_bn_momentum=0.1, drop2d_scale=mask)
+    assert rel(out, ref) < TOL_S33
+    dropped = (mask == 0).float().mean().item()
+    assert 0.35 < dropped < 0.65
+    zero_planes = (out.abs().amax(dim=(2, 3)) == 0).cpu()
+    assert torch.equal(zero_planes, mask == 0)
+
+
+def test_train_bn_needs_two_values(dev):
+    from few_shot_seg_cwt_amd import _lib
+    m = fresh_model(50)
+    m.train()
+    x = torch.zeros((1, 3, 33, 33), device=dev)
+    with pytest.raises(_lib.CwtError, match="more than 1 value"):
+        m.extract_features(x)
+
+
+def test_do_epoch_bn_quirk_vs_reference(dev, golden_dir):
+    """do_epoch with the reference's first-episode train-mode BN (model.train() at the epoch
+    start; support pass of episode 0 on batch statistics of the 2 duplicated copies; then eval
+    for the rest of the epoch over the moved running statistics)."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne
+    from few_shot_seg_cwt_amd.episode import SyntheticEpisodes, do_epoch
+    from few_shot_seg_cwt_amd.optimizer import get_optimizer
+    g = dict(np.load(os.path.join(golden_dir, "train_pascal_r50_1shot_bnq.npz")))
+    cfg = syn.cfg_defaults(dropout=0.0)
+    m = fresh_model(50, dropout=0.0)
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    t.attention.dropout.p = 0.0
+    t.dropout.p = 0.0
+    opt = get_optimizer(cfg, [dict(params=[t.flat], lr=cfg["trans_lr"] * cfg["scale_lr"])])
+    torch.manual_seed(SEED)
+    recs = []
+    ious, losses = do_epoch(cfg, SyntheticEpisodes(2, start=int(g["start"])), m, t, opt, epoch=1,
+                            iter_per_epoch=2, log_iter=2, records=recs)
+    np.testing.assert_allclose(losses.numpy(), g["train_losses"], rtol=1e-3)
+    for e in range(2):
+        assert rel(recs[e]["W"], g[f"e{e}_W"]) < TOL, e
+        assert rel(recs[e]["W2"], g[f"e{e}_W2"]) < TOL, e
+    for e in range(2):   # bar as test_gpu_parity.test_do_epoch_vs_reference
+        gmax = max(float(np.abs(g[f"e{e}_grad_{n}_sample"]).max()) for n, _ in t.named_views())
+        for n, v in t.named_views():
+            gv = t.view(n, recs[e]["grad"]).reshape(-1)[::101].double().numpy()
+            ref = g[f"e{e}_grad_{n}_sample"].astype(np.float64)
+            assert np.abs(gv - ref).max() / max(np.abs(ref).max(), 1e-3 * gmax) < 5e-3, (e, n)
+    for n, v in t.named_views():
+        assert rel(v.reshape(-1)[::101], g[f"final_{n}_sample"]) < 1e-4, n
+    sd = m.state_dict()
+    for p in PROBES:
+        assert rel(sd[p + ".running_mean"], g[f"rm_{p}"]) < TOL, p
+        assert rel(sd[p + ".running_var"], g[f"rv_{p}"]) < TOL, p

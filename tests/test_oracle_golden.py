@@ -49,6 +49,21 @@ def test_extract_features_small(small, layers):
     assert rel(f.numpy(), small[f"feat_r{layers}_S33"]) < 1e-5
 
 
+@pytest.mark.parametrize("layers", [50, 101])
+def test_extract_features_train_bn_small(golden_dir, layers):
+    """Train-mode BN (model.train(), train.py:184): batch statistics, running statistics moved
+    in place, then eval over them -- against the reference PSPNet (bn_train_small.npz)."""
+    g = dict(np.load(os.path.join(golden_dir, "bn_train_small.npz")))
+    sd = O.to_torch_state(syn.make_pspnet_state(layers, SEED))
+    ep = syn.make_episode(SEED, 7, 33, 2)
+    f = O.extract_features(torch.from_numpy(ep["spprt_imgs"][0]), sd, layers, train_bn_momentum=0.1)
+    assert rel(f.numpy(), g[f"feat_train_r{layers}"]) < 1e-5
+    fe = O.extract_features(torch.from_numpy(ep["qry_img"]), sd, layers)
+    assert rel(fe.numpy(), g[f"feat_eval_after_r{layers}"]) < 1e-5
+    for p in ["layer0.1", "layer4.2.bn3", "ppm.features.0.2", "bottleneck.1"]:
+        assert rel(sd[p + ".running_var"].numpy(), g[f"r{layers}_rv_{p}"]) < 1e-6, p
+
+
 @pytest.mark.parametrize("heads", [1, 4])
 def test_cwt_forward(small, heads):
     tsd = O.to_torch_state(syn.make_transformer_state(heads, 512, SEED))
