@@ -105,6 +105,26 @@ def pmc_traffic(dom_name: str):
     return None, None
 
 
+def conv_roofline(fine, peak_tflops):
+    """Per-conv roofline of the stack from one episode's per-launch records (profile level 2):
+    each conv launch's bound is max(flops / MFMA peak, algorithmic bytes / HBM peak) (bytes =
+    input + weights + output [+ residual] at 4 B per element: fp32 / the bf16x3 S-layout);
+    roofline_frac = sum of bounds / sum of measured launch times (1.0 = every conv at its roof)."""
+    convs = [r for r in fine if r[0].startswith("conv_igemm")]
+    if not convs:
+        return {}
+    roof = t = 0.0
+    n_hbm = 0
+    for name, fl, by, ms in convs:
+        tm, tb = fl / (peak_tflops * 1e12), by / (PEAK_HBM_GBPS * 1e9)
+        n_hbm += tb > tm
+        roof += max(tm, tb)
+        t += ms * 1e-3
+    return {"roofline_frac": round(roof / t, 4), "convs": len(convs), "hbm_bound_convs": n_hbm,
+            "roofline_basis": f"per conv max(flops/{peak_tflops} TF, bytes/{PEAK_HBM_GBPS / 1e3:.0f} TB/s), "
+                              "summed over the stack's conv launches (one episode, per-launch events)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -262,7 +282,8 @@ def main():
                        "frac": round(ex_fl / (ex_ms * 1e-3) / 1e12 / peak, 4),
                        "gflop_per_step": round(ex_fl / args.steps / 1e9, 1),
                        "ms_per_step": round(ex_ms / args.steps, 3),
-                       "note": "whole extract_features bracket (convs + stem/maxpool/PPM byte kernels + gaps)"},
+                       "note": "whole extract_features bracket (convs + stem/maxpool/PPM byte kernels + gaps)",
+                       **conv_roofline(fine, peak)},
         "phases_ms_per_step": {"extract": round(ex_ms / args.steps, 3), "inner_adapt": round(ad_ms / args.steps, 3),
                                "attention": round(at_ms / args.steps, 3)},
         "iou_fg_timed": None if args.train else round(float((iu[0, 1] / iu[1, 1].clamp_min(1)).item()), 4),

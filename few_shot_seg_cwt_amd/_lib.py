@@ -34,6 +34,9 @@ SIGNATURES = {
     "cwt_extract_features": (_I, [_P, _P, _P, _I, _I, _P, _P]),
     "cwt_extract_features_train_bn": (_I, [_P, _P, _P, _I, _I, _P, _F, _F, C.c_uint64, _P]),
     "cwt_backbone_read_bn": (_I, [_P, C.c_char_p, _P, _I]),
+    "cwt_preprocess_image": (_I, [_P, _P, _I, _I, _I, _I, C.POINTER(_F), C.POINTER(_F), C.POINTER(_F), _I, _I, _P,
+                                  _P]),
+    "cwt_preprocess_label": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "cwt_workspace_bytes": (C.c_size_t, [_P]),
     "cwt_inner_adapt": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
     "cwt_inner_adapt_batch": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P]),

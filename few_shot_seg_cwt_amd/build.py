@@ -15,7 +15,7 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "csrc", "build")
 LIB = os.path.join(HERE, "libcwt.so")
 SOURCES = ["api.hip", "conv.hip", "conv_x3.hip", "conv_x3s.hip", "backbone.hip", "adapt.hip", "cwt_attn.hip", "seg.hip",
-           "bn_train.hip"]
+           "bn_train.hip", "preprocess.hip"]
 HEADERS = ["common.h", "kernels.h", "conv_plans.inc", "conv_plans_x3s.inc", "conv_plans_b16.inc"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-Wall", "-Wno-unused-function",

@@ -897,6 +897,26 @@ int cwt_backbone_read_bn(const cwt_backbone* handle, const char* name, float* ou
   return 0;
 }
 
+int cwt_preprocess_image(cwt_ctx* ctx, const void* src, int src_dtype, int H, int W, int S, const float* mean,
+                         const float* std_, const float* pad, int flip_h, int flip_v, float* dst, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(src && dst && mean && std_, "null argument");
+  CWT_CHECK(src_dtype == CWT_U8 || src_dtype == CWT_F32, "src_dtype must be CWT_U8 or CWT_F32");
+  CWT_CHECK(H >= 1 && W >= 1 && S >= 8, "bad sizes");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_episode_image(src, src_dtype == CWT_F32, H, W, S, mean, std_, pad, flip_h, flip_v, dst,
+                              (hipStream_t)stream);
+}
+
+int cwt_preprocess_label(cwt_ctx* ctx, const uint8_t* src, int H, int W, int S, int class_chosen, int flip_h,
+                         int flip_v, int64_t* dst, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(src && dst, "null argument");
+  CWT_CHECK(H >= 1 && W >= 1 && S >= 8, "bad sizes");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_episode_label(src, H, W, S, class_chosen, flip_h, flip_v, (long long*)dst, (hipStream_t)stream);
+}
+
 size_t cwt_workspace_bytes(cwt_ctx* ctx) { return ctx ? ctx->ws_total : 0; }
 
 int cwt_inner_adapt_batch(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int E, int n, int h, int w, int C,

@@ -173,6 +173,13 @@ size_t bn_train_part_floats(long M, int C);
 int launch_bn_train(const BnTrainArgs& a, float* part, size_t part_floats, float* batch_sc, hipStream_t st);
 // dst[i] = src[i] * sc[i % period] (the PPM fold of the bottleneck BN scale)
 int launch_scale_cols(const float* src, float* dst, long n, int period, const float* sc, hipStream_t st);
+// Episode preprocessing (preprocess.hip): Resize + ToTensor + Normalize of one HWC RGB image
+// into [3][S][S] fp32, and the remapped / resized / padded int64 label
+void find_new_hw(int h, int w, int S, int* nh, int* nw);
+int launch_episode_image(const void* src, int src_f32, int H, int W, int S, const float* mean, const float* stdv,
+                         const float* pad, int flip_h, int flip_v, float* dst, hipStream_t st);
+int launch_episode_label(const unsigned char* src, int H, int W, int S, int cls, int flip_h, int flip_v,
+                         long long* dst, hipStream_t st);
 int launch_maxpool3s2_s(const __bf16* in, int N, int H, int W, int C, __bf16* out, int Ho, int Wo, hipStream_t st);
 int launch_maxpool3s2_b16(const __bf16* in, int N, int H, int W, int C, __bf16* out, int Ho, int Wo, hipStream_t st);
 int launch_maxpool3s2(const float* in, int N, int H, int W, int C, float* out, int Ho, int Wo,

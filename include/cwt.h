@@ -116,6 +116,29 @@ int cwt_extract_features_train_bn(cwt_ctx* ctx, cwt_backbone* bb, const float* i
  */
 int cwt_backbone_read_bn(const cwt_backbone* bb, const char* name, float* out, int C);
 
+/*
+ * Episode preprocessing on the device (the loader's transforms; dataset.py:205-327,
+ * transform.py:59-167).  Replaces, per image: [RandomHorizontalFlip / RandomVerticalFlip
+ * (flip_h / flip_v, decided by the caller)] -> Resize(S) (aspect kept, sides floored to a
+ * multiple of 8, cv2 INTER_LINEAR, top-left placement, pad value `pad` (NULL: 0; 'avg'
+ * padding: mean*255)) -> ToTensor (/255) -> Normalize(mean, std).
+ * src: device HWC RGB, uint8 (CWT_U8) or fp32 (CWT_F32), H x W.  dst: device fp32 [3][S][S].
+ * mean, std, pad: HOST float[3].
+ */
+#define CWT_U8 0
+#define CWT_F32 1
+int cwt_preprocess_image(cwt_ctx* ctx, const void* src, int src_dtype, int H, int W, int S,
+                         const float* mean, const float* std_, const float* pad, int flip_h,
+                         int flip_v, float* dst, void* stream);
+/*
+ * The episode label: chosen class -> 1, 255 kept, every other value -> 0 (dataset.py:222-228,
+ * 261-266; class_chosen < 0 keeps the raw values), the same flips, cv2 INTER_NEAREST resize
+ * to the Resize target and 255 padding to S x S.  src: device uint8 H x W; dst: device int64
+ * [S][S].
+ */
+int cwt_preprocess_label(cwt_ctx* ctx, const uint8_t* src, int H, int W, int S, int class_chosen,
+                         int flip_h, int flip_v, int64_t* dst, void* stream);
+
 /* Bytes of device workspace the context holds (activations etc.; shared by all backbones). */
 size_t cwt_workspace_bytes(cwt_ctx* ctx);
 

@@ -1,0 +1,127 @@
+"""Episode data path (few_shot_seg_cwt_amd/dataset.py, csrc/preprocess.hip; SURVEY.md §8(f)
+rank 1).  CPU: class splits, the list filter, Resize geometry.  GPU: the preprocessing kernels
+bit-exact against oracle/data_oracle.py (the restated transform.py / cv2.resize arithmetic --
+parity against cv2 itself is unpinned: cv2 is not installed), and EpisodicData end to end on a
+small on-disk .npy dataset (sampling invariants of dataset.py:205-266)."""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from few_shot_seg_cwt_amd import dataset as D
+from oracle import data_oracle as DO
+
+MEAN, STD = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+
+
+def test_split_classes():
+    sc = D.get_split_classes({"use_split_coco": True})
+    assert sc["pascal"][0]["val"] == [1, 2, 3, 4, 5]
+    assert sorted(sc["pascal"][0]["train"]) == list(range(6, 21))
+    assert sc["coco"][0]["val"] == list(range(1, 78, 4))
+    assert len(sc["coco"][2]["train"]) == 60
+    assert D.filter_classes("pascal", 0, "pascal", 0, sc) == [1, 2, 3, 4, 5]
+    assert D.filter_classes("pascal", 0, "pascal", -1, sc) == [1, 2, 3, 4, 5]   # -1 = all, minus seen
+    sc2 = D.get_split_classes({"use_split_coco": False})
+    assert sc2["coco"][1]["val"] == list(range(21, 41))
+
+
+def test_find_new_hw_matches_oracle_and_quirk():
+    # 473 -> 472 (the %8 quirk of transform.py:128-135)
+    assert DO.find_new_hw(500, 375, 473) == (472, 352)
+    assert DO.find_new_hw(375, 500, 473) == (352, 472)
+    assert DO.find_new_hw(641, 641, 641) == (640, 640)
+
+
+def _write_dataset(root, n=8, H=(50, 70), classes=(1, 2, 3), seed=0):
+    rng = np.random.default_rng(seed)
+    lines = []
+    for i in range(n):
+        h, w = int(rng.integers(*H)), int(rng.integers(*H))
+        img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        lab = np.zeros((h, w), np.uint8)
+        c = classes[i % len(classes)]
+        lab[: h // 2 + 20, : w // 2 + 20] = c       # >= 2*32*32 pixels only for the large ones
+        lab[-3:, :] = 255
+        if i % 2:
+            lab[h // 2:, w // 2:] = classes[(i + 1) % len(classes)]
+        np.save(os.path.join(root, f"img{i}.npy"), img)
+        np.save(os.path.join(root, f"lab{i}.npy"), lab)
+        lines.append(f"img{i}.npy lab{i}.npy")
+    lst = os.path.join(root, "list.txt")
+    open(lst, "w").write("\n".join(lines) + "\n")
+    return lst
+
+
+def test_make_dataset_filter(tmp_path):
+    lst = _write_dataset(str(tmp_path), n=6, H=(90, 110))
+    items, by_cls = D.make_dataset(str(tmp_path), lst, [1, 2, 3])
+    for c, files in by_cls.items():
+        for _, lp in files:
+            assert int((np.load(lp) == c).sum()) >= 2048
+    assert len(items) == len({i for f in by_cls.values() for i in f})
+
+
+# ------------------------------------------------------------------------ GPU
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,S", [(500, 375, 473), (375, 500, 473), (333, 500, 473), (480, 640, 641),
+                                   (40, 33, 473), (473, 473, 473), (100, 60, 57)])
+@pytest.mark.parametrize("src_f32", [False, True])
+def test_preprocess_image_bitexact(dev, H, W, S, src_f32):
+    rng = np.random.default_rng(H * 7 + W)
+    img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    src = img.astype(np.float32) if src_f32 else img
+    for fh, fv, pad in [(False, False, None), (True, False, None), (True, True, [v * 255 for v in MEAN])]:
+        out = D.preprocess_image(torch.from_numpy(src).to(dev), S, MEAN, STD, pad, fh, fv)
+        ref, _ = DO.val_transform(img, None, S, MEAN, STD, pad, fh, fv)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,S", [(500, 375, 473), (375, 500, 473), (77, 91, 473), (480, 640, 641)])
+def test_preprocess_label_bitexact(dev, H, W, S):
+    rng = np.random.default_rng(H + W)
+    lab = rng.integers(0, 6, (H, W)).astype(np.uint8)
+    lab[rng.random((H, W)) < 0.05] = 255
+    for cls, fh, fv in [(3, False, False), (2, True, True), (-1, False, True)]:
+        out = D.preprocess_label(torch.from_numpy(lab).to(dev), S, cls, fh, fv)
+        rl = DO.remap_label(lab, cls) if cls >= 0 else lab
+        _, ref = DO.val_transform(np.zeros((H, W, 3), np.uint8), rl, S, MEAN, STD, None, fh, fv)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode_train", [False, True])
+def test_episodic_data_end_to_end(dev, tmp_path, mode_train):
+    lst = _write_dataset(str(tmp_path), n=12, H=(90, 130))
+    args = dict(shot=2, random_shot=False, image_size=97, mean=MEAN, std=STD, padding=None,
+                augmentations=["hor_flip", "vert_flip", "resize"], data_root=str(tmp_path),
+                train_list=lst, val_list=lst)
+    ds = D.EpisodicData(mode_train, [1, 2, 3], args, device=dev)
+    random.seed(5)
+    np.random.seed(5)
+    for i in range(len(ds)):
+        qry, tgt, simgs, slbls, subcls, (s_paths, s_raw), (qpath, qlab) = ds[i]
+        assert qry.shape == (3, 97, 97) and tgt.shape == (97, 97) and tgt.dtype == torch.int64
+        assert simgs.shape == (2, 3, 97, 97) and slbls.shape == (2, 97, 97)
+        assert qpath not in s_paths and len(set(s_paths)) == 2            # distinct supports, never the query
+        assert set(np.unique(tgt.cpu().numpy())) <= {0, 1, 255}
+        c = [1, 2, 3][subcls[0] - 1]
+        for p in s_paths:
+            lp = os.path.join(os.path.dirname(p), os.path.basename(p).replace("img", "lab"))
+            assert int((np.load(lp) == c).sum()) >= 2048
+        if not mode_train:   # no flips: the transform is the oracle's exactly
+            ref, reft = DO.val_transform(np.load(qpath), qlab, 97, MEAN, STD)
+            np.testing.assert_array_equal(qry.cpu().numpy(), ref)
+            np.testing.assert_array_equal(tgt.cpu().numpy(), reft)
