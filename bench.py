@@ -108,7 +108,8 @@ def pmc_traffic(dom_name: str):
 def conv_roofline(fine, peak_tflops):
     """Per-conv roofline of the stack from one episode's per-launch records (profile level 2):
     each conv launch's bound is max(flops / MFMA peak, algorithmic bytes / HBM peak) (bytes =
-    input + weights + output [+ residual] at 4 B per element: fp32 / the bf16x3 S-layout);
+    input + weights + output [+ residual], each once: 4 B per element for fp32 / the bf16x3
+    S-layout, 2 B for the bf16 stack);
     roofline_frac = sum of bounds / sum of measured launch times (1.0 = every conv at its roof)."""
     convs = [r for r in fine if r[0].startswith("conv_igemm")]
     if not convs:

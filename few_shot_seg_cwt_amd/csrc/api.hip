@@ -644,8 +644,11 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     }
     const ConvPlan& pl = plans[i];
     const double flops = 2.0 * a.M * a.Co * a.K;
-    const double bytes = 4.0 * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K + (double)a.M * a.Co +
-                                (a.res ? (double)a.M * a.Co : 0.0));
+    // algorithmic bytes: every operand once; 4 B per element (fp32 or the bf16x3 S-layout),
+    // 2 B for the bf16 stack's activations and weights (its fp32 bottleneck output: 4 B)
+    const double eb = b16 ? 2.0 : 4.0, ob = calls[i].out_f32 ? 4.0 : eb;
+    const double bytes = eb * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K) +
+                         ob * ((double)a.M * a.Co + (a.res ? (double)a.M * a.Co : 0.0));
     Prof p(ctx, st,
            std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : conv_x3 ? "conv_igemm_bf16x3<"
                                                                                                      : "conv_igemm_f32<") +
