@@ -235,3 +235,66 @@ class EpisodicData:
         spprt_labels = torch.stack([l for _, l in st])
         return qry_img, target, spprt_imgs, spprt_labels, subcls_list, [s_img_paths, support_labels_orig], \
             [image_path, label]
+
+
+class EpisodeLoader:
+    """``torch.utils.data.DataLoader(dataset, batch_size=1, shuffle=...)`` over
+    :class:`EpisodicData` in the calling process (dataset.py:51-58, 95-101): the batch
+    dimension is added and ``subcls_list`` collated to ``[tensor([c])]``.  The order comes from
+    torch's RNG as RandomSampler draws it (one int64 seed, then randperm); the reference's
+    worker processes (``workers: 2``) reseed their own RNGs, which is not reproduced."""
+
+    def __init__(self, dataset: EpisodicData, shuffle: bool):
+        self.dataset, self.shuffle = dataset, shuffle
+
+    def __len__(self):
+        return len(self.dataset)
+
+    def __iter__(self):
+        n = len(self.dataset)
+        if self.shuffle:
+            seed = int(torch.empty((), dtype=torch.int64).random_().item())
+            order = torch.randperm(n, generator=torch.Generator().manual_seed(seed)).tolist()
+        else:
+            order = list(range(n))
+        ds = self.dataset
+
+        class _It:
+            def __init__(self):
+                self.i = 0
+
+            def next(self):
+                if self.i >= len(order):
+                    raise StopIteration
+                q, t, si, sl, sub, sp, qp = ds[order[self.i]]
+                self.i += 1
+                return q[None], t[None], si[None], sl[None], [torch.tensor([c]) for c in sub], sp, qp
+
+            __next__ = next
+
+            def __iter__(self):
+                return self
+        return _It()
+
+
+def get_train_loader(args, read_image: Callable = read_npy, read_label: Callable = read_npy, device=None):
+    """dataset.py:17-63 (episodic, batch_size 1): (loader, sampler=None)."""
+    assert _g(args, "train_split") in [0, 1, 2, 3]
+    split_classes = get_split_classes(args)
+    class_list = split_classes[_g(args, "train_name")][_g(args, "train_split")]["train"]
+    ds = EpisodicData(True, class_list, args, read_image, read_label, device)
+    return EpisodeLoader(ds, shuffle=True), None
+
+
+def get_val_loader(args, read_image: Callable = read_npy, read_label: Callable = read_npy, device=None):
+    """dataset.py:66-117 (episodic): (loader, None).  test_name 'default' = the train dataset
+    and split."""
+    test_name = _g(args, "test_name", "default")
+    if test_name == "default":
+        test_name, test_split = _g(args, "train_name"), _g(args, "train_split")
+    else:
+        test_split = _g(args, "test_split")
+    class_list = filter_classes(_g(args, "train_name"), _g(args, "train_split"), test_name, test_split,
+                                get_split_classes(args))
+    ds = EpisodicData(False, class_list, args, read_image, read_label, device)
+    return EpisodeLoader(ds, shuffle=False), None

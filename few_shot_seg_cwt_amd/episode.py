@@ -208,11 +208,11 @@ def new_binary_classifier_weight(bottleneck_dim: int = 512, num_classes: int = 2
     return conv.weight.detach().reshape(num_classes, bottleneck_dim).clone()
 
 
-def _class_weight_check(s_label_cpu: torch.Tensor):
+def _class_weight_check(s_label: torch.Tensor):
     # test.py:169-175: len(back_pix) / len(target_pix) raises ZeroDivisionError without FG
-    arr = s_label_cpu.numpy()
-    nf = int(np.count_nonzero(arr == 1))
-    nb = int(np.count_nonzero(arr == 0))
+    # (host labels from the synthetic loader, device labels from dataset.EpisodicData)
+    nf = int((s_label == 1).sum().item())
+    nb = int((s_label == 0).sum().item())
     return nb / nf
 
 

