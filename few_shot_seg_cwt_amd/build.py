@@ -40,6 +40,12 @@ def _compile(src: str, force: bool) -> str:
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
+    srcs = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(os.path.dirname(HERE), "include", "cwt.h")]
+    if not force and _mtime(LIB) >= max(_mtime(p) for p in srcs):
+        # up to date (the GPU box gets the library but not the object files)
+        if verbose:
+            print(f"up to date: {LIB}")
+        return LIB
     os.makedirs(OBJ, exist_ok=True)
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
