@@ -49,3 +49,39 @@ def test_version_and_error_calls_without_gpu(lib):
 def test_code_object_targets_gfx950():
     so = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in so
+
+
+C_PROGRAM = r"""
+#include <stdio.h>
+#include <string.h>
+#include "cwt.h"
+int main(void) {
+  const char* v = cwt_version();
+  if (!v || !strstr(v, "gfx950")) return 2;
+  /* argument validation precedes any device call: no GPU needed */
+  if (cwt_extract_features(NULL, NULL, NULL, 1, 473, NULL, NULL) != 1001) return 3;
+  if (!strstr(cwt_last_error(), "ctx")) return 4;
+  if (cwt_attention_saved_floats(1, 3600, 512, 4) == 0) return 5;
+  printf("ok %s\n", v);
+  return 0;
+}
+"""
+
+
+def test_header_is_plain_c_and_links(lib, tmp_path):
+    """include/cwt.h compiles as C99 (no C++ or torch types in the signatures) and a C program
+    links against libcwt.so and calls it -- the boundary a cgo / JNI / N-API stub would bind."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    src = tmp_path / "abi.c"
+    src.write_text(C_PROGRAM)
+    exe = tmp_path / "abi"
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
+                        "-L", libdir, "-lcwt", f"-Wl,-rpath,{libdir}", "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, LD_LIBRARY_PATH="/opt/rocm/lib:" + os.environ.get("LD_LIBRARY_PATH", ""))
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), (r.returncode, r.stdout, r.stderr)
