@@ -136,7 +136,7 @@ def main():
     ap.add_argument("--size", type=int, default=473)
     ap.add_argument("--pool", type=int, default=4, help="distinct resident episodes cycled through")
     ap.add_argument("--inflight", type=int, default=1,
-                    help="independent episodes processed together per step (EpisodeEngine.run_batch, <= 4)")
+                    help="independent episodes processed together per step (EpisodeEngine.run_batch, <= 16)")
     ap.add_argument("--conv-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="conv-stack arithmetic: fp32 (reference numerics) or bf16 (config #5)")
     ap.add_argument("--train", action="store_true",

