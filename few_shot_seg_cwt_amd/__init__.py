@@ -6,6 +6,8 @@ Reference-shaped entry points:
   MultiHeadAttentionOne(n_head, 512, 512, 512)    src/model/transformer.py:33
   intersectionAndUnionGPU / batch_...             src/util.py:237,280
   validate_transformer / do_epoch                 src/test.py:103, src/train.py:166
+  get_train_loader / get_val_loader, EpisodicData src/dataset/dataset.py:17-117,180-327
+  checkpoint.load_backbone / *_transformer_checkpoint   src/train.py:57-75,147-163; src/test.py:61-89
 """
 from .pspnet import PSPNet, get_model  # noqa: F401
 from .transformer import MultiHeadAttentionOne  # noqa: F401
@@ -13,5 +15,7 @@ from .util import AverageMeter, batch_intersectionAndUnionGPU, intersectionAndUn
 from .optimizer import HipSGD, get_optimizer  # noqa: F401
 from .episode import (EpisodeEngine, SyntheticEpisodes, do_epoch, inner_adapt,  # noqa: F401
                       validate_transformer)
+from .dataset import EpisodicData, get_train_loader, get_val_loader  # noqa: F401
+from . import checkpoint  # noqa: F401
 
 __version__ = "0.1.0"
