@@ -745,6 +745,8 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   }
   int Mb[4];
   const float *Wp[4], *Wq[4], *Sc[4], *Sh[4];
+  static const bool ppm_splitk = getenv("CWT_PPM_SPLITK") != nullptr;  // A/B: the split-K form
+  const bool few_cells = cells <= kPpmGemmMaxRows && !ppm_splitk;
   for (int i = 0; i < 4; ++i) {
     Mb[i] = N * kBins[i] * kBins[i];
     Wp[i] = bb->ppm_wt[i];
@@ -754,8 +756,10 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   }
   {  // PPM 1x1 conv + BN + ReLU over the pooled cells (pspnet.py:27-29)
     Prof p(ctx, st, "ppm_conv smallm 2048x512", 2.0 * cells * 512 * 2048, 4.0 * (4.0 * 2048 * 512 + cells * 2560.0));
-    if ((rc = launch_smallm_gemm(POOL, 2048, Wp, Mb, 4, 512, 2048, kKcPpm, PARTS, (size_t)sPartS, tb ? nullptr : Sc,
-                                 tb ? nullptr : Sh, PPM, st)))
+    if ((rc = few_cells ? launch_ppm_gemm(POOL, 2048, Wp, Mb, 4, 512, 2048, tb ? nullptr : Sc, tb ? nullptr : Sh, PARTS,
+                                          (size_t)sPartS, PPM, st)
+                        : launch_smallm_gemm(POOL, 2048, Wp, Mb, 4, 512, 2048, kKcPpm, PARTS, (size_t)sPartS,
+                                             tb ? nullptr : Sc, tb ? nullptr : Sh, PPM, st)))
       return rc;
     p.end();
   }
@@ -770,8 +774,9 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   }
   {  // per-tap products of the bottleneck's PPM channels with the cells
     Prof p(ctx, st, "ppm_fold_q smallm 512x4608", 2.0 * cells * 4608 * 512, 4.0 * (4.0 * 512 * 4608 + cells * 5120.0));
-    if ((rc = launch_smallm_gemm(PPM, 512, Wq, Mb, 4, 4608, 512, kKcQ, PARTS, (size_t)sPartS, nullptr, nullptr, QB,
-                                 st)))
+    if ((rc = few_cells ? launch_ppm_gemm(PPM, 512, Wq, Mb, 4, 4608, 512, nullptr, nullptr, PARTS, (size_t)sPartS, QB, st)
+                        : launch_smallm_gemm(PPM, 512, Wq, Mb, 4, 4608, 512, kKcQ, PARTS, (size_t)sPartS, nullptr,
+                                             nullptr, QB, st)))
       return rc;
     p.end();
   }

@@ -602,6 +602,160 @@ int launch_smallm_gemm(const float* A, int lda, const float* const* Bt, const in
   return 0;
 }
 
+// Few-row form of the two PPM GEMMs (one or two episodes: <= kPpmGemmMaxRows cells) on the
+// exact f32 matrix cores: v_mfma_f32_16x16x4_f32 is an fmaf chain per output (MI355X_MICROARCH
+// "f32 in"), so this is plain fp32 arithmetic in a fixed order.  The VALU form of this GEMM is
+// LDS-bound (a 64-lane broadcast read per 4 FMAs), the split-K VALU form is bound by its
+// partials; here each workgroup owns up to 32 rows x 64 columns of one problem over a K slice:
+//  * its W waves take 64 consecutive k each, all loaded up front; a lane loads A[row l&15][4 k] and, for 4 k rows,
+//    B[k][4 columns] as 16-B vectors, and column block cb of the MFMA holds the columns
+//    n0 + 4j + cb (j = l&15), so B lines and the output rows are contiguous 256-B segments;
+//  * the W per-wave 16x64 tiles are summed in wave order through LDS (deterministic), then
+//    BN + ReLU (one K slice) or a partial row of [ks][Mtot][N] for smallm_finish_kernel;
+//  * tiles (problem, K slice, strip, row group), row group fastest, are dealt to the 8 XCDs in
+//    contiguous runs, so the row groups re-reading one weight strip share an L2.
+struct PpmMfmaArgs {
+  const float* A;
+  const float* Bt[4];
+  const float* scale[4];
+  const float* shift[4];
+  float* out;
+  int row0[4], M[4], nrg[4], tile0[5];
+  int np, N, lda, ksl, nks, nstrips, Mtot, per_xcd;
+};
+
+template <int W, int RTW, int KI>
+__global__ __launch_bounds__(64 * W) void ppm_mfma_kernel(PpmMfmaArgs g) {
+  static_assert(W >= 4, "the reduction gives waves 0..3 one output register each");
+  __shared__ __attribute__((aligned(16))) float red[W * 16 * 64];
+  const int tile = (int)(blockIdx.x & 7) * g.per_xcd + (int)(blockIdx.x >> 3);
+  if (tile >= g.tile0[g.np]) return;  // padding of the XCD runs: the whole workgroup leaves
+  int p = 0;
+  while (p + 1 < g.np && tile >= g.tile0[p + 1]) ++p;
+  int local = tile - g.tile0[p];
+  const int rg = local % g.nrg[p];
+  local /= g.nrg[p];
+  const int strip = local % g.nstrips, ks = local / g.nstrips;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g4 = lane >> 4, c16 = lane & 15;
+  const int m0 = g.row0[p] + rg * RTW * 16, mend = g.row0[p] + g.M[p];
+  const int n0 = strip * 64 + 4 * c16;
+  const int kb = ks * g.ksl + wv * 16 * KI;  // ksl == W * 16 * KI (checked at launch)
+  const float* ar[RTW];
+#pragma unroll
+  for (int rt = 0; rt < RTW; ++rt)  // rows past the problem read a valid row; never stored
+    ar[rt] = g.A + (long)min(m0 + rt * 16 + c16, mend - 1) * g.lda + kb + 4 * g4;
+  const float* bp = g.Bt[p] + (long)(kb + 4 * g4) * g.N + n0;
+  f32x4 acc[RTW][4];
+#pragma unroll
+  for (int rt = 0; rt < RTW; ++rt)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[rt][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // The wave's whole K range (KI steps of 16 k) is loaded up front: at one or two workgroups
+  // per CU a prefetch of one step leaves every step waiting out a memory round trip.
+  f32x4 a[KI][RTW], b[KI][4];
+#pragma unroll
+  for (int i = 0; i < KI; ++i) {
+#pragma unroll
+    for (int rt = 0; rt < RTW; ++rt) a[i][rt] = *(const f32x4*)(ar[rt] + 16 * i);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) b[i][q] = *(const f32x4*)(bp + (long)(16 * i + q) * g.N);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep every load ahead of the first MFMA
+#pragma unroll
+  for (int i = 0; i < KI; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int rt = 0; rt < RTW; ++rt)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+          acc[rt][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][rt][q], b[i][q][cb], acc[rt][cb], 0, 0, 0);
+  const float* sc = g.nks == 1 ? g.scale[p] : nullptr;
+  const float* sh = g.shift[p];
+  float* o = g.out + (long)ks * g.Mtot * g.N + n0;
+#pragma unroll
+  for (int rt = 0; rt < RTW; ++rt) {
+    if (m0 + rt * 16 >= mend) break;  // uniform
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) red[(wv * 16 + v * 4 + cb) * 64 + lane] = acc[rt][cb][v];
+    __syncthreads();
+    if (wv < 4) {  // D row 4*g4 + v, column block cb; summed over the waves in order
+      const int v = wv;
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) s[cb] += red[(w * 16 + v * 4 + cb) * 64 + lane];
+      const int row = m0 + rt * 16 + 4 * g4 + v;
+      if (row < mend) {
+        if (sc) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) s[q] = fmaxf(fmaf(s[q], sc[n0 + q], sh[n0 + q]), 0.f);
+        }
+        *(f32x4*)(o + (long)row * g.N) = s;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+int launch_ppm_gemm(const float* A, int lda, const float* const* Bt, const int* M, int np, int N, int K,
+                    const float* const* scale, const float* const* shift, float* part, size_t part_floats,
+                    float* out, hipStream_t st) {
+  // K = 512 (the per-tap fold, N = 4608): one K slice, 8 waves; K = 2048 (the 1x1 conv, N = 512:
+  // only 8 strips) in 8 slices of 4 waves, summed by smallm_finish_kernel.
+  const int nks = K == 2048 ? 8 : 1, W = K == 2048 ? 4 : 8;
+  constexpr int RTW = 2, KI = 4;  // 64 k per wave: 512 = 8 waves x 64, 2048 = 8 slices x 4 waves x 64
+  if (np < 1 || np > 4 || N % 64 != 0 || (K != 512 && K != 2048) || lda < K || lda % 4 ||
+      ((uintptr_t)A & 15))
+    return fail(CWT_EARG, "ppm_gemm: need 1..4 problems, N % 64 == 0, K in {512, 2048}, 16-B aligned rows");
+  PpmMfmaArgs g;
+  memset(&g, 0, sizeof(g));
+  SmallFinishArgs f;
+  memset(&f, 0, sizeof(f));
+  g.A = A;
+  g.np = f.np = np;
+  g.N = N;
+  g.lda = lda;
+  g.ksl = K / nks;
+  g.nks = nks;
+  g.nstrips = N / 64;
+  int row = 0, tiles = 0;
+  for (int q = 0; q < np; ++q) {
+    if (M[q] < 1) return fail(CWT_EARG, "ppm_gemm: empty problem");
+    g.Bt[q] = Bt[q];
+    g.scale[q] = f.scale[q] = scale ? scale[q] : nullptr;
+    g.shift[q] = f.shift[q] = shift ? shift[q] : nullptr;
+    g.row0[q] = f.row0[q] = row;
+    g.M[q] = M[q];
+    g.nrg[q] = cdiv(M[q], RTW * 16);
+    g.tile0[q] = tiles;
+    row += M[q];
+    tiles += g.nrg[q] * g.nstrips * nks;
+  }
+  g.tile0[np] = tiles;
+  f.row0[np] = row;
+  g.Mtot = row;
+  g.per_xcd = cdiv(tiles, 8);
+  g.out = nks == 1 ? out : part;
+  if (nks > 1 && (size_t)nks * row * N > part_floats) return fail(CWT_ESTATE, "ppm_gemm: partial workspace too small");
+  const dim3 grid(8 * g.per_xcd);
+  if (W == 8)
+    hipLaunchKernelGGL((ppm_mfma_kernel<8, RTW, KI>), grid, dim3(512), 0, st, g);
+  else
+    hipLaunchKernelGGL((ppm_mfma_kernel<4, RTW, KI>), grid, dim3(256), 0, st, g);
+  CWT_LAUNCH_CHECK();
+  if (nks > 1) {
+    const long total = (long)row * (N / 4);
+    hipLaunchKernelGGL(smallm_finish_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)part, nks, row,
+                       N, f, out);
+    CWT_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
 // Interpolation table for destination p in [-1, out] (the 3x3 conv's zero padding outside
 // [0, out)): source cells i0, i1 with weights l0, l1 of the align_corners upsample in -> out.
 struct LerpEntry {

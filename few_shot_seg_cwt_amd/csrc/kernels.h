@@ -190,6 +190,11 @@ int launch_repack_cblock(const float* src, float* dst, int Co, int taps, int Ci,
 int launch_smallm_gemm(const float* A, int lda, const float* const* Bt, const int* M, int np, int N, int K, int kc,
                        float* part, size_t part_floats, const float* const* scale, const float* const* shift,
                        float* out, hipStream_t st);
+// Few-row form of the two PPM GEMMs (K = 512 or 2048) on the f32 MFMA; cells <= kPpmGemmMaxRows.
+constexpr int kPpmGemmMaxRows = 200;
+int launch_ppm_gemm(const float* A, int lda, const float* const* Bt, const int* M, int np, int N, int K,
+                    const float* const* scale, const float* const* shift, float* part, size_t part_floats,
+                    float* out, hipStream_t st);
 int launch_ppm_field(const float* Q, int N, int h, int w, const int* bins, float* R, float* F, hipStream_t st);
 
 }  // namespace cwt
