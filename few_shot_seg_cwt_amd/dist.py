@@ -1,11 +1,13 @@
 """Multi-GPU plumbing: one process per GPU, torch.distributed over RCCL ("nccl" backend on
 ROCm) on the GPU box, gloo in the CPU tests.
 
-The CWT path has exactly two exchange points:
+The CWT path has exactly two data-path exchange points:
   * training: the mean of the CWT gradients, ONE all-reduce of the flat 2,098,688-float
     (H=4) bucket per step, before the identical SGD step on every rank;
   * inference: one sum all-reduce of the per-class intersection/union table at the end of
     a run (episodes are sharded round-robin, no data-path collective).
+Off the data path, training also broadcasts the extractor's BN running statistics from rank 0
+once per epoch, after the train-mode-BN episode (broadcast_backbone_bn_).
 The reference's own DDP code (src/train_ddp.py:106-119) wraps a different model (MMN) and
 is not runnable; this is the CWT's equivalent, not a translation of it.
 """
@@ -101,3 +103,37 @@ def barrier():
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
             dist.barrier()
+
+
+def broadcast_running_stats_(state: dict, src: int = 0) -> dict:
+    """Replace every ``*.running_mean`` / ``*.running_var`` entry of ``state`` (a state dict of
+    torch tensors or numpy arrays) by rank ``src``'s, in ONE broadcast of the flat fp32 bucket.
+    Other entries are left alone.  No-op at world size 1."""
+    _, world = rank_world()
+    keys = sorted(k for k in state if k.endswith((".running_mean", ".running_var")))
+    if world == 1 or not keys:
+        return state
+    vals = [torch.as_tensor(np.asarray(state[k]), dtype=torch.float32) for k in keys]
+    flat = torch.cat([v.reshape(-1) for v in vals]).to(_reduce_device())
+    dist.broadcast(flat, src)
+    flat = flat.cpu()
+    off = 0
+    for k, v in zip(keys, vals):
+        state[k] = flat[off:off + v.numel()].reshape(v.shape).clone()
+        off += v.numel()
+    return state
+
+
+def broadcast_backbone_bn_(model, src: int = 0):
+    """DDP ``broadcast_buffers`` semantics for the frozen extractor: after the first episode of
+    an epoch has moved each rank's BN running statistics with its own batch statistics
+    (train.py:184,245), every rank takes rank ``src``'s, so the replicas
+    extract identical features for the rest of the epoch.  The reference trains in one
+    process, where the question does not arise."""
+    rank, world = rank_world()
+    if world == 1:
+        return model
+    sd = broadcast_running_stats_(model.state_dict(), src)
+    if rank != src:
+        model.load_state_dict(sd)
+    return model

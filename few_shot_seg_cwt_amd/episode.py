@@ -401,6 +401,8 @@ def do_epoch(args, train_loader, model, transformer, optimizer_trans, epoch: int
         r = train_episode(model, transformer, args, batch, W0, dev)
         if world > 1:
             cdist.all_reduce_mean_(transformer.flat.grad)
+            if i == 0 and getattr(model, "_stats_moved", True):   # the train-mode-BN episode
+                cdist.broadcast_backbone_bn_(model)                 # moved each rank's statistics
         optimizer_trans.step()
         loss = float(r["loss"].item())
         iut = r["iut"].cpu().numpy()[0]
