@@ -138,3 +138,26 @@ def test_do_epoch_bn_quirk_vs_reference(dev, golden_dir):
     for p in PROBES:
         assert rel(sd[p + ".running_mean"], g[f"rm_{p}"]) < TOL, p
         assert rel(sd[p + ".running_var"], g[f"rv_{p}"]) < TOL, p
+
+
+def test_moved_stats_reload_matches(dev):
+    """What a non-source rank does in dist.broadcast_backbone_bn_: load a state dict carrying
+    the moved running statistics.  The reloaded extractor must match the one whose statistics
+    moved, in eval mode, to fp32 rounding: the moved one refolds its BN scale/shift (and the
+    PPM-branch weights) on the device, the reloaded one folds them on the host at load.
+    Measured on the MI355X: not bitwise equal, hence the 1e-5 bar (features are O(0.1-1))."""
+    from few_shot_seg_cwt_amd import get_model
+    m = fresh_model(50, dropout=0.0)
+    ep = syn.make_episode(SEED, 11, 33, 2)
+    m.train()
+    m.extract_features(torch.from_numpy(ep["spprt_imgs"][0]).to(dev))
+    m.eval()
+    q = torch.from_numpy(ep["qry_img"]).to(dev)
+    f_moved, _ = m.extract_features(q)
+    other = get_model(syn.cfg_defaults(layers=50, dropout=0.0))
+    other.load_state_dict(syn.make_pspnet_state(50, SEED))
+    other.load_state_dict(m.state_dict())
+    other.eval()
+    f_other, _ = other.extract_features(q)
+    torch.cuda.synchronize()
+    assert rel(f_other, f_moved) < 1e-5
