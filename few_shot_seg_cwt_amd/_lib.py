@@ -50,6 +50,7 @@ SIGNATURES = {
                                      _F, C.c_uint64, _P]),
     "cwt_classify": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_seg_metrics": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "cwt_seg_metrics_pair": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "cwt_seg_ce_fwd_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "cwt_classify_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_iou_preds": (_I, [_P, _P, _P, _I64, _I, _I, _P, _P]),

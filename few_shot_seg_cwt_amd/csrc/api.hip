@@ -40,7 +40,8 @@ int launch_normalize(const float* f, int B, int Pb, float* out, const float* W0,
 int launch_classify(const float* W, const float* f, int B, int Pb, float* logits, hipStream_t st);
 int launch_classify_bwd(const float* dl, const float* f, int B, int Pb, float* dW, hipStream_t st);
 int launch_seg_metrics(const float* logits, const int64_t* target, int B, int h, int w, int S, float* iut,
-                       double* ce, unsigned* counts_ws, hipStream_t st);
+                       double* ce, unsigned* counts_ws, hipStream_t st, const float* logits2 = nullptr,
+                       float* iut2 = nullptr);
 int launch_iou_preds(const int64_t* preds, const int64_t* target, long n, int K, int ignore, float* iut,
                      unsigned* counts_ws, hipStream_t st);
 int launch_sgd(float* p, const float* g, float* buf, long n, float lr, float mom, float wd, int nesterov, int first,
@@ -1052,8 +1053,21 @@ int cwt_seg_metrics(cwt_ctx* ctx, const float* logits, const int64_t* target, in
   CWT_HIP(hipSetDevice(ctx->device));
   void* cnt;
   int rc;
-  if ((rc = ensure_ws(ctx, "metrics.cnt", (size_t)B * 256 * (6 * 4 + 2 * 8) + 16, &cnt))) return rc;
+  if ((rc = ensure_ws(ctx, "metrics.cnt", (size_t)B * 256 * (2 * 6 * 4 + 2 * 8) + 16, &cnt))) return rc;
   return launch_seg_metrics(logits, target, B, h, w, S, iut_out, ce_out, (unsigned*)cnt, (hipStream_t)stream);
+}
+
+int cwt_seg_metrics_pair(cwt_ctx* ctx, const float* logits, const float* logits0, const int64_t* target, int B,
+                         int h, int w, int S, float* iut_out, double* ce_out, float* iut0_out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(logits && logits0 && target && iut_out && iut0_out && B >= 1 && B <= 64 && h >= 1 && w >= 1 && S >= 1,
+            "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void* cnt;
+  int rc;
+  if ((rc = ensure_ws(ctx, "metrics.cnt", (size_t)B * 256 * (2 * 6 * 4 + 2 * 8) + 16, &cnt))) return rc;
+  return launch_seg_metrics(logits, target, B, h, w, S, iut_out, ce_out, (unsigned*)cnt, (hipStream_t)stream,
+                            logits0, iut0_out);
 }
 
 int cwt_seg_ce_fwd_bwd(cwt_ctx* ctx, const float* logits, const int64_t* target, int B, int h, int w, int S,

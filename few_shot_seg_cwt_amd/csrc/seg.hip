@@ -134,18 +134,22 @@ int launch_classify_bwd(const float* dl, const float* f, int B, int Pb, float* d
   return 0;
 }
 
-// counts[b][0..5] = {inter0, inter1, out0, out1, tgt0, tgt1} (uint32), ce[b] = {sum nll, count}
+// counts[z][b][0..5] = {inter0, inter1, out0, out1, tgt0, tgt1} (uint32), ce[b] = {sum nll, count}
+// blockIdx.z = 1 (when logits2 is given) scores a second logits tensor against the same target
+// in the same launch (the episode's pred_q0 beside pred_q, test.py:192-204), without CE.
 __global__ __launch_bounds__(256) void seg_metrics_kernel(const float* __restrict__ logits,
+                                                          const float* __restrict__ logits2,
                                                           const int64_t* __restrict__ target, int h, int w, int S,
                                                           float sy, float sx, unsigned* __restrict__ counts,
                                                           double* __restrict__ ce) {
   __shared__ unsigned cnt[4][6];
   __shared__ double cel[4][2];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int b = blockIdx.y;
+  const int b = blockIdx.y, z = blockIdx.z;
   const long npix = (long)S * S;
   const long plane = (long)h * w;
-  const float* L0 = logits + (long)b * 2 * plane;
+  const float* L0 = (z ? logits2 : logits) + (long)b * 2 * plane;
+  if (z) ce = nullptr;
   const float* L1 = L0 + plane;
   unsigned c[6] = {0, 0, 0, 0, 0, 0};
   double nll = 0.0;
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(256) void seg_metrics_kernel(const float* __restric
   __syncthreads();
   // per-block partials (no atomics, nothing to zero first); seg_metrics_final sums them in
   // block order, so the double CE sum is deterministic
-  const long pb = (long)b * gridDim.x + blockIdx.x;
+  const long pb = ((long)z * gridDim.y + b) * gridDim.x + blockIdx.x;
   if (t < 6) counts[pb * 6 + t] = cnt[0][t] + cnt[1][t] + cnt[2][t] + cnt[3][t];
   if (ce && t < 2) ce[pb * 2 + t] = (cel[0][t] + cel[1][t]) + (cel[2][t] + cel[3][t]);
 }
@@ -195,11 +199,17 @@ __global__ __launch_bounds__(256) void seg_metrics_kernel(const float* __restric
 // LDS tree (deterministic) gives [inter, union, target] x 2 classes and (nll sum, valid count)
 __global__ __launch_bounds__(256) void seg_metrics_final_kernel(const unsigned* __restrict__ counts,
                                                                 const double* __restrict__ ce_part, int nblk,
-                                                                float* __restrict__ iut, double* __restrict__ ce) {
+                                                                float* __restrict__ iut, float* __restrict__ iut2,
+                                                                double* __restrict__ ce) {
   __shared__ unsigned c[6][256];
   __shared__ double d[2][256];
-  const int b = blockIdx.x, t = threadIdx.x;
+  const int b = blockIdx.x, t = threadIdx.x, z = blockIdx.y;
   const bool have = t < nblk;
+  if (z) {  // the second logits tensor: its own counts plane, no CE
+    counts += (long)gridDim.x * nblk * 6;
+    iut = iut2;
+    ce = nullptr;
+  }
 #pragma unroll
   for (int q = 0; q < 6; ++q) c[q][t] = have ? counts[((long)b * nblk + t) * 6 + q] : 0u;
   if (ce) {
@@ -226,18 +236,21 @@ __global__ __launch_bounds__(256) void seg_metrics_final_kernel(const unsigned* 
   }
 }
 
-// counts_ws: [B][nblk][6] unsigned, then (8-B aligned) [B][nblk][2] double partials
+// counts_ws: [nz][B][nblk][6] unsigned, then (8-B aligned) [B][nblk][2] double partials
+// (nz = 2 when logits2 / iut2 are given: both tensors scored in the same two launches)
 int launch_seg_metrics(const float* logits, const int64_t* target, int B, int h, int w, int S, float* iut,
-                       double* ce, unsigned* counts_ws, hipStream_t st) {
+                       double* ce, unsigned* counts_ws, hipStream_t st, const float* logits2, float* iut2) {
   const long npix = (long)S * S;
   const int nblk = (int)std::min<long>(256, cdiv(npix, 256));
-  double* ce_part = ce ? (double*)(counts_ws + (((long)B * nblk * 6 + 1) & ~1L)) : nullptr;
-  dim3 grid(nblk, B);
-  hipLaunchKernelGGL(seg_metrics_kernel, grid, dim3(256), 0, st, logits, target, h, w, S,
+  const int nz = logits2 ? 2 : 1;
+  if (logits2 && !iut2) return fail(CWT_EARG, "seg_metrics: a second logits tensor needs its iut output");
+  double* ce_part = ce ? (double*)(counts_ws + (((long)nz * B * nblk * 6 + 1) & ~1L)) : nullptr;
+  dim3 grid(nblk, B, nz);
+  hipLaunchKernelGGL(seg_metrics_kernel, grid, dim3(256), 0, st, logits, logits2, target, h, w, S,
                      align_corners_scale(h, S), align_corners_scale(w, S), counts_ws, ce_part);
   CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(seg_metrics_final_kernel, dim3(B), dim3(256), 0, st, (const unsigned*)counts_ws,
-                     (const double*)ce_part, nblk, iut, ce);
+  hipLaunchKernelGGL(seg_metrics_final_kernel, dim3(B, nz), dim3(256), 0, st, (const unsigned*)counts_ws,
+                     (const double*)ce_part, nblk, iut, iut2, ce);
   CWT_LAUNCH_CHECK();
   return 0;
 }

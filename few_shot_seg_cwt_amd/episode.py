@@ -24,7 +24,7 @@ import torch
 from . import _lib
 from . import dist as cdist
 from .synthetic import feature_side, make_episode, pascal_val_classes
-from .util import AverageMeter, seg_metrics
+from .util import AverageMeter, seg_metrics, seg_metrics_pair
 
 
 def _a(args, k, default=None):
@@ -142,8 +142,7 @@ class EpisodeEngine:
         fqn, pred_q0 = normalize(f_q, Wb)
         W2 = self.transformer.infer(Wb, fqn)
         pred_q = classify(W2, fqn)
-        iut, ce = seg_metrics(pred_q, q_label)
-        iut0, _ = seg_metrics(pred_q0, q_label, with_ce=False)
+        iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, f_s=f_s, f_q=f_q)
 
     @torch.no_grad()
@@ -165,8 +164,7 @@ class EpisodeEngine:
         W2 = self.transformer.infer(W, fqn) if E <= 4 else \
             torch.cat([self.transformer.infer(W[i:i + 4], fqn[i:i + 4]) for i in range(0, E, 4)])
         pred_q = classify(W2, fqn)
-        iut, ce = seg_metrics(pred_q, q_label)
-        iut0, _ = seg_metrics(pred_q0, q_label, with_ce=False)
+        iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, f_s=f_s, f_q=f_q)
 
 

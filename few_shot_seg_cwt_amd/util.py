@@ -83,6 +83,30 @@ def seg_metrics(logits: torch.Tensor, target: torch.Tensor, with_ce: bool = True
     return iut, ce
 
 
+def seg_metrics_pair(logits: torch.Tensor, logits0: torch.Tensor, target: torch.Tensor):
+    """seg_metrics of an episode's adapted logits (with CE) and of its baseline logits0
+    (test.py:192,200-204: pred_q0, without CE) against one target, in the same two launches.
+    Returns (iut, ce, iut0); equal to two seg_metrics calls."""
+    _lib.require(logits, "logits")
+    _lib.require(logits0, "logits0")
+    _lib.require(target, "target", torch.int64)
+    B, nc, h, w = logits.shape
+    if nc != 2:
+        raise NotImplementedError("2-way episodes only (num_classes_tr = 2)")
+    if tuple(logits0.shape) != tuple(logits.shape):
+        raise ValueError("logits0 must have the shape of logits")
+    S = target.shape[-1]
+    lg, lg0, tg = logits.contiguous(), logits0.contiguous(), target.contiguous()
+    iut = torch.empty((B, 3, 2), device=lg.device, dtype=torch.float32)
+    iut0 = torch.empty_like(iut)
+    ce = torch.empty((B, 2), device=lg.device, dtype=torch.float64)
+    _lib.check(_lib.lib().cwt_seg_metrics_pair(_lib.ctx(lg.device.index), _lib.ptr(lg), _lib.ptr(lg0), _lib.ptr(tg),
+                                               B, h, w, S, _lib.ptr(iut), _lib.ptr(ce), _lib.ptr(iut0),
+                                               _lib.stream_ptr(lg.device)),
+               "cwt_seg_metrics_pair")
+    return iut, ce, iut0
+
+
 def batch_intersectionAndUnionGPU(logits: torch.Tensor, target: torch.Tensor, num_classes: int,
                                   ignore_index: int = 255):
     """util.py:237-277: logits [n_task, shot, C, h, w], target [n_task, shot, H, W] ->

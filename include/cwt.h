@@ -240,6 +240,15 @@ int cwt_seg_metrics(cwt_ctx* ctx, const float* logits, const int64_t* target, in
                     int S, float* iut_out, double* ce_out, void* stream);
 
 /*
+ * cwt_seg_metrics for an episode's two logits tensors against one target in the same two
+ * launches: logits (pred_q: iut_out, ce_out as above) and logits0 (the un-adapted baseline
+ * pred_q0, test.py:192,200-204: iut0_out only).  Results equal two cwt_seg_metrics calls.
+ */
+int cwt_seg_metrics_pair(cwt_ctx* ctx, const float* logits, const float* logits0, const int64_t* target,
+                         int B, int h, int w, int S, float* iut_out, double* ce_out, float* iut0_out,
+                         void* stream);
+
+/*
  * Weighted CE of upsampled logits and its gradient w.r.t. the low-res logits, for the
  * outer loop (train.py:237-243,261-265): class weight [1, #bg/(#fg+1e-12)] from target,
  * loss = sum_p w_y * nll_p / sum_p w_y over non-ignored p.

@@ -168,6 +168,20 @@ def test_seg_metrics_vs_oracle(dev):
         assert abs(c[0] / c[1] - l) < 1e-4 * abs(l)
 
 
+def test_seg_metrics_pair_equals_two_calls(dev):
+    """The fused pred_q / pred_q0 scoring (cwt_seg_metrics_pair) against two single calls:
+    integer counts and the fixed-order double CE sum, bit for bit."""
+    from few_shot_seg_cwt_amd.util import seg_metrics, seg_metrics_pair
+    lg = torch.from_numpy(syn.normal(SEED, "lg", (2, 2, 60, 60), 1.0)).to(dev)
+    lg0 = torch.from_numpy(syn.normal(SEED, "lg0", (2, 2, 60, 60), 1.0)).to(dev)
+    tgt = torch.from_numpy(syn.make_episode(SEED, 5, 473, 2)["s_label"][0]).to(dev)
+    iut, ce, iut0 = seg_metrics_pair(lg, lg0, tgt)
+    r_iut, r_ce = seg_metrics(lg, tgt)
+    r_iut0, _ = seg_metrics(lg0, tgt, with_ce=False)
+    assert torch.equal(iut, r_iut) and torch.equal(ce, r_ce) and torch.equal(iut0, r_iut0)
+    assert not torch.equal(iut, iut0)   # the two tensors really are scored separately
+
+
 def test_iou_preds_vs_reference(dev, small):
     from few_shot_seg_cwt_amd.util import intersectionAndUnionGPU
     i, u, t = intersectionAndUnionGPU(torch.from_numpy(small["iou_preds"]).to(dev),
