@@ -22,7 +22,11 @@ template <int KPL>
 __global__ __launch_bounds__(256) void rowdot_kernel(const float* __restrict__ A, int R, const float* __restrict__ X,
                                                      int nv, long xvs, long xgs, int rows_per_group,
                                                      const float* __restrict__ bias, const float* __restrict__ res,
-                                                     long rvs, float* __restrict__ out, long ovs, float alpha) {
+                                                     long rvs, float* __restrict__ out, long ovs, float alpha,
+                                                     float* __restrict__ zero, long zero_n) {
+  // zero: a buffer the NEXT launch accumulates into, cleared here instead of by a memset launch
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (zero && gid < zero_n) zero[gid] = 0.f;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
@@ -57,20 +61,22 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* __restrict__ A
 }
 
 int launch_rowdot(const float* A, int R, int K, const float* X, int nv, long xvs, long xgs, int rows_per_group,
-                  const float* bias, const float* res, long rvs, float* out, long ovs, float alpha, hipStream_t st) {
+                  const float* bias, const float* res, long rvs, float* out, long ovs, float alpha, hipStream_t st,
+                  float* zero = nullptr, long zero_n = 0) {
   dim3 grid(cdiv(R, 4)), block(256);
+  if (zero && zero_n > (long)grid.x * 256) return fail(CWT_EARG, "rowdot: buffer to clear exceeds the grid");
   if (K == 512)
     hipLaunchKernelGGL((rowdot_kernel<8>), grid, block, 0, st, A, R, X, nv, xvs, xgs, rows_per_group, bias, res,
-                       rvs, out, ovs, alpha);
+                       rvs, out, ovs, alpha, zero, zero_n);
   else if (K == 1024)
     hipLaunchKernelGGL((rowdot_kernel<16>), grid, block, 0, st, A, R, X, nv, xvs, xgs, rows_per_group, bias, res,
-                       rvs, out, ovs, alpha);
+                       rvs, out, ovs, alpha, zero, zero_n);
   else if (K == 2048)
     hipLaunchKernelGGL((rowdot_kernel<32>), grid, block, 0, st, A, R, X, nv, xvs, xgs, rows_per_group, bias, res,
-                       rvs, out, ovs, alpha);
+                       rvs, out, ovs, alpha, zero, zero_n);
   else if (K == 4096)
     hipLaunchKernelGGL((rowdot_kernel<64>), grid, block, 0, st, A, R, X, nv, xvs, xgs, rows_per_group, bias, res,
-                       rvs, out, ovs, alpha);
+                       rvs, out, ovs, alpha, zero, zero_n);
   else
     return fail(CWT_EARG, "rowdot: unsupported K");
   CWT_LAUNCH_CHECK();
@@ -379,10 +385,9 @@ int attention_fwd(const float* q, const float* f, int B, int hw, int C, int H, c
   int rc;
   // 1. qp[v][j] = w_qkvs[j] . q[v]
   if ((rc = launch_rowdot(w_qkvs, H * C, C, q, nv, C, 0, H * C, nullptr, nullptr, 0, sv + L.qp, (long)H * C, 1.f,
-                          st)))
+                          st, sv + L.r, (long)H * nv * C)))
     return rc;
-  // 2. r[h][v][k] = sum_d w_qkvs[h*C+d][k] qp[v][h*C+d] / sqrt(C)
-  CWT_HIP(hipMemsetAsync(sv + L.r, 0, sizeof(float) * H * nv * C, st));
+  // 2. r[h][v][k] = sum_d w_qkvs[h*C+d][k] qp[v][h*C+d] / sqrt(C)  (r cleared by step 1's launch)
   if ((rc = launch_coldot(w_qkvs, H, C, C, sv + L.qp, nv, (long)H * C, sv + L.r, inv_t, st))) return rc;
   // 3. chunk partials over the token map
   dim3 g3(nchunk, B);
