@@ -126,6 +126,50 @@ def conv_roofline(fine, peak_tflops):
                               "summed over the stack's conv launches (one episode, per-launch events)"}
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int) -> int:
+    """``bench.py --gpus N`` outside torchrun: start N fresh child processes of this script, one
+    per GPU, with the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), before
+    this parent has touched the GPU (it never does), and return the worst exit code.  Rank 0's
+    JSON line reaches stdout through the inherited descriptor."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:   # one rank died: the collective would hang the others
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.send_signal(signal.SIGTERM)
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    try:
+                        codes[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[i] = p.wait()
+            break
+        time.sleep(0.2)
+    return max((abs(c) for c in codes), default=0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -146,8 +190,25 @@ def main():
     ap.add_argument("--profile-json", default=None, help="write per-launch records here (rank 0)")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        ngpu = torch.cuda.device_count()     # does not initialise the GPU
+        if 0 < ngpu < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but only {ngpu} GPUs are visible")
+        sys.exit(spawn_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} disagrees with WORLD_SIZE={env_world} from the launcher")
+
     from few_shot_seg_cwt_amd import dist as cdist
     rank, local, world = cdist.init_from_env()
+    if world != args.gpus:
+        raise SystemExit(f"process group has {world} ranks, --gpus asks for {args.gpus}")
+    if os.environ.get("CWT_BENCH_DRYRUN"):   # launch check without a device (tests/test_bench_launch.py)
+        tot = cdist.all_reduce_sum_np(np.array([1.0]))[0]
+        print(json.dumps({"rank": rank, "world": world, "ranks_seen": int(tot)}), flush=True)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -171,6 +232,7 @@ def main():
         raise SystemExit("--train runs one episode per rank per step (train.py batch_size 1)")
     if args.train:
         tengine = TrainEngine(model, trans, cfg)
+        cdist.broadcast_params_(trans.flat)          # DDP's start-of-training broadcast
         opt = get_optimizer(cfg, [dict(params=[trans.flat], lr=cfg["trans_lr"] * cfg["scale_lr"])])
 
     # resident inputs: a pool of distinct episodes per rank + one W0 buffer per step
@@ -256,7 +318,7 @@ def main():
         + (" [bf16 conv stack]" if args.conv_dtype == "bf16" else ""),
         "value": round(value, 3),
         "unit": "training episodes/s" if args.train else "episodes/s",
-        "n_gpus": world,
+        "n_gpus": cdist.rank_world()[1],
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3),

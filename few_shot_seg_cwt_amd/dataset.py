@@ -237,22 +237,46 @@ class EpisodicData:
             [image_path, label]
 
 
-class EpisodeLoader:
-    """``torch.utils.data.DataLoader(dataset, batch_size=1, shuffle=...)`` over
-    :class:`EpisodicData` in the calling process (dataset.py:51-58, 95-101): the batch
-    dimension is added and ``subcls_list`` collated to ``[tensor([c])]``.  The order comes from
-    torch's RNG as RandomSampler draws it (one int64 seed, then randperm); the reference's
-    worker processes (``workers: 2``) reseed their own RNGs, which is not reproduced."""
+class EpisodeSampler:
+    """``torch.utils.data.DistributedSampler(train_data)`` (dataset.py:57-59): rank ``rank`` of
+    ``world`` gets every ``world``-th position of one permutation seeded ``seed + epoch`` (the
+    same on every rank), padded by wrapping, so ranks train on disjoint episodes.  Call
+    ``set_epoch`` before each epoch as with the torch sampler."""
 
-    def __init__(self, dataset: EpisodicData, shuffle: bool):
-        self.dataset, self.shuffle = dataset, shuffle
+    def __init__(self, n: int, rank: int, world: int, shuffle: bool = True, seed: int = 0):
+        from .dist import shard_indices
+        self._shard = shard_indices
+        self.n, self.rank, self.world, self.shuffle, self.seed, self.epoch = n, rank, world, shuffle, seed, 0
+
+    def set_epoch(self, epoch: int):
+        self.epoch = int(epoch)
+
+    def __iter__(self):
+        return iter(self._shard(self.n, self.rank, self.world, self.shuffle, self.seed, self.epoch))
 
     def __len__(self):
-        return len(self.dataset)
+        return -(-self.n // self.world) if self.n else 0
+
+
+class EpisodeLoader:
+    """``torch.utils.data.DataLoader(dataset, batch_size=1, shuffle=..., sampler=...)`` over
+    :class:`EpisodicData` in the calling process (dataset.py:51-63, 95-101): the batch
+    dimension is added and ``subcls_list`` collated to ``[tensor([c])]``.  Without a sampler the
+    order comes from torch's RNG as RandomSampler draws it (one int64 seed, then randperm); with
+    one (multi-rank training) it is the sampler's shard.  The reference's worker processes
+    (``workers: 2``) reseed their own RNGs, which is not reproduced."""
+
+    def __init__(self, dataset: EpisodicData, shuffle: bool, sampler: EpisodeSampler | None = None):
+        self.dataset, self.shuffle, self.sampler = dataset, shuffle and sampler is None, sampler
+
+    def __len__(self):
+        return len(self.sampler) if self.sampler is not None else len(self.dataset)
 
     def __iter__(self):
         n = len(self.dataset)
-        if self.shuffle:
+        if self.sampler is not None:
+            order = list(self.sampler)
+        elif self.shuffle:
             seed = int(torch.empty((), dtype=torch.int64).random_().item())
             order = torch.randperm(n, generator=torch.Generator().manual_seed(seed)).tolist()
         else:
@@ -278,11 +302,22 @@ class EpisodeLoader:
 
 
 def get_train_loader(args, read_image: Callable = read_npy, read_label: Callable = read_npy, device=None):
-    """dataset.py:17-63 (episodic, batch_size 1): (loader, sampler=None)."""
+    """dataset.py:17-63 (episodic): (loader, sampler).  Distributed when ``args.distributed`` is
+    set or torch.distributed runs more than one rank: the loader iterates this rank's
+    :class:`EpisodeSampler` shard (``DistributedSampler`` in the reference) and the sampler is
+    returned for ``set_epoch``; otherwise (loader, None).  Each rank runs ONE episode per
+    iteration: the reference's per-rank ``int(batch_size / world_size)`` (dataset.py:59) would be
+    0 for the scripts' ``batch_size 1``, so the global batch is ``world`` episodes, all-reduced
+    (DESIGN.md §6)."""
+    from .dist import rank_world
     assert _g(args, "train_split") in [0, 1, 2, 3]
     split_classes = get_split_classes(args)
     class_list = split_classes[_g(args, "train_name")][_g(args, "train_split")]["train"]
     ds = EpisodicData(True, class_list, args, read_image, read_label, device)
+    rank, world = rank_world()
+    if _g(args, "distributed", False) or world > 1:
+        sampler = EpisodeSampler(len(ds), rank, world, shuffle=True)
+        return EpisodeLoader(ds, shuffle=False, sampler=sampler), sampler
     return EpisodeLoader(ds, shuffle=True), None
 
 

@@ -14,6 +14,7 @@ is not runnable; this is the CWT's equivalent, not a translation of it.
 from __future__ import annotations
 
 import os
+import random
 from typing import List, Tuple
 
 import numpy as np
@@ -43,6 +44,58 @@ def init_from_env(backend: str | None = None) -> Tuple[int, int, int]:
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
     return rank, local, world
+
+
+def seed_everything(manual_seed: int) -> int:
+    """Per-rank seeding of every host RNG the episode path draws from, as the reference's
+    multi-process trainer does it (src/train_ddp.py:62-66: ``manual_seed + rank`` for
+    ``random``, ``np.random``, ``torch`` and the CUDA generators).  Each rank then draws its own
+    episodes' support/query choice and its own classifier init W0 (train.py:206).  Returns the
+    seed used."""
+    rank, _ = rank_world()
+    s = int(manual_seed) + rank
+    random.seed(s)
+    np.random.seed(s)
+    torch.manual_seed(s)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(s)
+    return s
+
+
+def broadcast_params_(flat: torch.Tensor, src: int = 0) -> torch.Tensor:
+    """Make every rank start from rank ``src``'s parameters: one broadcast of the flat CWT
+    parameter buffer (transformer.flat).  This is what ``DDP(module)`` does at construction
+    (src/train_ddp.py:119); with per-rank seeds the modules' random inits differ otherwise.
+    No-op at world size 1."""
+    _, world = rank_world()
+    if world > 1:
+        if flat.device.type == _reduce_device().type:
+            dist.broadcast(flat.data, src)
+        else:
+            t = flat.detach().to(_reduce_device())
+            dist.broadcast(t, src)
+            flat.data.copy_(t)
+    return flat
+
+
+def shard_indices(n: int, rank: int, world: int, shuffle: bool, seed: int = 0, epoch: int = 0) -> List[int]:
+    """The indices ``torch.utils.data.DistributedSampler(dataset)`` hands rank ``rank`` in
+    epoch ``epoch`` (the reference's train sampler, src/dataset/dataset.py:57-59): a
+    permutation drawn from a generator seeded ``seed + epoch`` (identical on every rank), padded
+    by wrapping to a multiple of ``world``, then every ``world``-th entry from ``rank``.  Ranks get
+    disjoint positions of one permutation; with world 1 and shuffle off it is range(n)."""
+    if shuffle:
+        g = torch.Generator()
+        g.manual_seed(int(seed) + int(epoch))
+        idx = torch.randperm(n, generator=g).tolist()
+    else:
+        idx = list(range(n))
+    per = -(-n // world) if n else 0
+    total = per * world
+    if total > len(idx) and idx:
+        pad = total - len(idx)
+        idx += (idx * (-(-pad // len(idx))))[:pad]
+    return idx[rank:total:world]
 
 
 def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:
@@ -125,11 +178,15 @@ def broadcast_running_stats_(state: dict, src: int = 0) -> dict:
 
 
 def broadcast_backbone_bn_(model, src: int = 0):
-    """DDP ``broadcast_buffers`` semantics for the frozen extractor: after the first episode of
-    an epoch has moved each rank's BN running statistics with its own batch statistics
-    (train.py:184,245), every rank takes rank ``src``'s, so the replicas
-    extract identical features for the rest of the epoch.  The reference trains in one
-    process, where the question does not arise."""
+    """After the first episode of an epoch has moved each rank's BN running statistics with its
+    own batch statistics (train.py:184,245), every rank takes rank ``src``'s,
+    so the replicas extract identical features from that episode's query pass on.
+
+    Declared deviation: the reference's multi-process idiom wraps the extractor in
+    ``SyncBatchNorm`` (src/train_ddp.py:106), whose batch statistics span all ranks' batches; here
+    each rank's train-mode support pass normalises over its own batch (the CWT trainer the
+    north star names, src/train.py, is single-process, where the two agree), and the broadcast
+    keeps the replicas identical afterwards, as DDP's ``broadcast_buffers`` would."""
     rank, world = rank_world()
     if world == 1:
         return model

@@ -231,6 +231,12 @@ class SyntheticEpisodes:
     def __len__(self):
         return self.n
 
+    def shard(self, rank: int, world: int) -> "SyntheticEpisodes":
+        """This rank's share of the episode stream (episodes start + (rank + i*world)*stride):
+        disjoint across ranks, like the DistributedSampler shard of the real loader."""
+        return SyntheticEpisodes(self.n, self.S, self.shot, self.seed, self.start + rank * self.stride, self.classes,
+                                 self.stride * world)
+
     def episode(self, i: int):
         ep = make_episode(self.seed, self.start + i * self.stride, self.S, self.shot, self.classes)
         t = torch.from_numpy
@@ -312,7 +318,9 @@ def validate_transformer(args, val_loader, model, transformer, episodes_out: lis
             for c, row in zip(classes, table):
                 cls_iu[c] = row[:2]
                 cls_iu0[c] = row[2:]
-            loss_meter.avg = cdist.all_reduce_mean_scalar(loss_meter.avg)
+            tot = cdist.all_reduce_sum_np(np.array([loss_meter.sum, loss_meter.count], dtype=np.float64))
+            loss_meter.sum, loss_meter.count = float(tot[0]), int(tot[1])
+            loss_meter.avg = loss_meter.sum / max(loss_meter.count, 1)
         IoU = {c: cls_iu[c][0] / (cls_iu[c][1] + 1e-10) for c in classes}
         mIoU = float(np.mean(list(IoU.values()))) if IoU else 0.0
         if rank == 0:
@@ -354,6 +362,10 @@ def train_episode(model, transformer, args, batch, W0: torch.Tensor, dev) -> dic
             sl = sl.expand(2, -1, -1)
         f_s, _ = model.extract_features(sp.contiguous())
         model.eval()
+        if cdist.rank_world()[1] > 1:
+            # every rank moved its own running statistics; take rank 0's before the query pass
+            # so all replicas extract identical features from here on (dist.broadcast_backbone_bn_)
+            cdist.broadcast_backbone_bn_(model)
         f_q, _ = model.extract_features(qry_img.to(dev, non_blocking=True))
         sl = sl.contiguous()
     else:
@@ -377,11 +389,15 @@ def train_episode(model, transformer, args, batch, W0: torch.Tensor, dev) -> dic
 def do_epoch(args, train_loader, model, transformer, optimizer_trans, epoch: int, iter_per_epoch: int,
              log_iter: int, records: list | None = None):
     """Mirror of train.py:166-288 (batch_size 1).  With torch.distributed initialised each
-    rank runs its own episode per iteration and the CWT gradient bucket is all-reduced
-    (mean) before the identical SGD step on every rank (DESIGN.md §multi-GPU)."""
+    rank runs its own episode per iteration -- ``train_loader`` must then be this rank's shard
+    (``get_train_loader`` returns one; ``SyntheticEpisodes.shard``) and the host RNGs seeded per
+    rank (``dist.seed_everything``), so ranks draw different episodes and W0 -- the parameters
+    are broadcast from rank 0 once at the start, and the CWT gradient bucket is all-reduced
+    (mean) before the identical SGD step on every rank (DESIGN.md §6)."""
     if int(_a(args, "batch_size", 1)) != 1:
         raise NotImplementedError("batch_size must be 1 (scripts/train.sh)")
-    dev = torch.device("cuda", torch.cuda.current_device())
+    # (the HIP calls in train_episode raise without a device; the loop itself is host logic)
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     loss_meter = AverageMeter()
     train_losses = torch.zeros(log_iter)
     train_Ious = torch.zeros(log_iter)
@@ -390,17 +406,17 @@ def do_epoch(args, train_loader, model, transformer, optimizer_trans, epoch: int
     model.train()
     transformer.train()
     rank, world = cdist.rank_world()
+    if world > 1:   # identical starting parameters on every rank (DDP's construction-time broadcast)
+        cdist.broadcast_params_(transformer.flat)
     for i in range(iter_per_epoch):
         batch = it.next() if hasattr(it, "next") else next(it)
         W0 = new_binary_classifier_weight()              # train.py:206
-        if transformer.flat.grad is None:
-            transformer.flat.grad = torch.zeros_like(transformer.flat)
         optimizer_trans.zero_grad()
+        if transformer.flat.grad is None:    # torch optimisers zero_grad to None
+            transformer.flat.grad = torch.zeros_like(transformer.flat)
         r = train_episode(model, transformer, args, batch, W0, dev)
         if world > 1:
             cdist.all_reduce_mean_(transformer.flat.grad)
-            if i == 0 and getattr(model, "_stats_moved", True):   # the train-mode-BN episode
-                cdist.broadcast_backbone_bn_(model)                 # moved each rank's statistics
         optimizer_trans.step()
         loss = float(r["loss"].item())
         iut = r["iut"].cpu().numpy()[0]
@@ -413,6 +429,7 @@ def do_epoch(args, train_loader, model, transformer, optimizer_trans, epoch: int
         train_Ious0[i] = float((IoUb0 + IoUf0) / 2)
         if records is not None:
             records.append(dict(loss=loss, W=r["W"].detach().cpu(), W2=r["W2"].detach().cpu(),
+                                pred_q0=None if r.get("pred_q0") is None else r["pred_q0"].detach().cpu(),
                                 grad=transformer.flat.grad.detach().cpu().clone()))
         if ((epoch == 0 and i % 100 == 0) or i % 500 == 0) and rank == 0:
             print("iter {} IoUf {:.2f}, IoUb {:.2f}, IoUf0 {:.2f}, IoUb0 {:.2f}".format(i, IoUf, IoUb, IoUf0, IoUb0))

@@ -209,15 +209,16 @@ BN_PROBES = ["layer0.1", "layer1.0.downsample.1", "layer4.2.bn3", "ppm.features.
              "bottleneck.1"]
 
 
-def run_train(rtrain, rutil, rpsp, rtr, name, n_iter, bn_quirk=False):
+def run_train(rtrain, rutil, rpsp, rtr, name, n_iter, bn_quirk=False, yaml_name="pascal.yaml", layers=50, S=473,
+              classes=None):
     from src.optimizer import get_optimizer
-    over = ["shot", "1", "layers", "50", "trans_lr", "0.001", "heads", "4", "cls_lr", "0.1", "batch_size", "1",
-            "batch_size_val", "1"]
+    over = ["shot", "1", "layers", str(layers), "trans_lr", "0.001", "heads", "4", "cls_lr", "0.1", "batch_size", "1",
+            "batch_size_val", "1", "image_size", str(S)]
     if bn_quirk:
         over += ["dropout", "0.0"]                   # Dropout2d identity (its RNG is torch's)
-    args = ref_args(rutil, "pascal.yaml", over)
+    args = ref_args(rutil, yaml_name, over)
     torch.manual_seed(SEED)
-    model = build_model(rpsp, args, 50)
+    model = build_model(rpsp, args, layers)
     if not bn_quirk:
         model.train = lambda mode=True: model        # exclude the first-episode BN quirk
     transformer = build_transformer(rtr, 4)
@@ -240,18 +241,21 @@ def run_train(rtrain, rutil, rpsp, rtr, name, n_iter, bn_quirk=False):
         return orig_backward(t, *a, **k)
     torch.Tensor.backward = backward
     torch.manual_seed(SEED)
-    ious, tl = rtrain.do_epoch(args=args, train_loader=Loader(473, 1, n_iter, start=1000), model=model,
+    ious, tl = rtrain.do_epoch(args=args, train_loader=Loader(S, 1, n_iter, classes, start=1000), model=model,
                                transformer=transformer, optimizer_trans=opt, epoch=1, iter_per_epoch=n_iter,
                                log_iter=n_iter)
     torch.Tensor.backward = orig_backward
     cap.restore()
-    out = {"n_iter": n_iter, "train_ious": ious.numpy(), "train_losses": tl.numpy(), "seed": SEED, "start": 1000}
+    out = {"n_iter": n_iter, "train_ious": ious.numpy(), "train_losses": tl.numpy(), "seed": SEED, "start": 1000,
+           "S": S, "layers": layers}
     for e, r in enumerate(cap.rec):
         out[f"e{e}_W0"] = r["W0"].numpy().reshape(2, 512)
         out[f"e{e}_W"] = r["W"].numpy().reshape(2, 512)
         out[f"e{e}_W2"] = r["W2"].numpy().reshape(2, 512)
         out[f"e{e}_loss_q"] = r["loss_q"].numpy()
         out[f"e{e}_fs_stat"] = stat(r["feats"][0])
+        pred_q0 = r["cls_out"][0]                      # binary_cls(f_q) under no_grad (train.py:249)
+        out[f"e{e}_pred_q0"] = pred_q0.numpy()[0]
         if bn_quirk:
             out[f"e{e}_fs_sample"] = r["feats"][0].numpy().reshape(-1)[::997].copy()
             out[f"e{e}_fq_sample"] = r["feats"][1].numpy().reshape(-1)[::997].copy()
@@ -353,7 +357,8 @@ def run_bn_train(rutil, rpsp):
 def main():
     torch.set_num_threads(8)
     rtest, rtrain, rutil, rpsp, rtr = import_reference()
-    which = sys.argv[1:] or ["modules", "pascal1", "pascal5", "coco1", "train", "bn_train", "train_bnq"]
+    which = sys.argv[1:] or ["modules", "pascal1", "pascal5", "coco1", "coco5", "train", "train_coco", "bn_train",
+                             "train_bnq"]
     if "modules" in which:
         run_modules(rutil, rpsp, rtr)
     if "pascal1" in which:
@@ -363,8 +368,14 @@ def main():
     if "coco1" in which:
         run_validate(rtest, rutil, rpsp, rtr, "episode_coco_r101_1shot.npz", "coco.yaml", 101, 641, 1, 1,
                      classes=syn.coco_val_classes(0))
+    if "coco5" in which:       # BASELINE config #5's shapes (fp32 reference; the bf16 stack is scored by mIoU)
+        run_validate(rtest, rutil, rpsp, rtr, "episode_coco_r101_5shot.npz", "coco.yaml", 101, 641, 5, 1,
+                     classes=syn.coco_val_classes(0))
     if "train" in which:
         run_train(rtrain, rutil, rpsp, rtr, "train_pascal_r50_1shot.npz", 2)
+    if "train_coco" in which:  # BASELINE config #4: COCO 1-shot R101 641 training (do_epoch), dropout off, BN eval
+        run_train(rtrain, rutil, rpsp, rtr, "train_coco_r101_1shot.npz", 2, yaml_name="coco.yaml", layers=101, S=641,
+                  classes=syn.coco_val_classes(0))
     if "bn_train" in which:
         run_bn_train(rutil, rpsp)
     if "train_bnq" in which:

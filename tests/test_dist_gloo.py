@@ -135,3 +135,120 @@ def test_gloo_world2_bn_broadcast(tmp_path):
     port = _free_port()
     mp.spawn(_bn_worker, args=(port, str(tmp_path)), nprocs=WORLD, join=True)
     assert all((tmp_path / f"bn{r}").exists() for r in range(WORLD))
+
+
+# ------------------------------------------------------------------ multi-rank do_epoch
+def _stand_in_train_episode(model, transformer, args, batch, W0, dev):
+    """CPU stand-in for episode.train_episode (whose kernels need the GPU): the oracle's CWT
+    gradients of a tiny episode derived from the batch's query image and this rank's W0,
+    ACCUMULATED into transformer.flat.grad like the HIP path does."""
+    from few_shot_seg_cwt_amd.transformer import _layout
+    from oracle import cwt_oracle as O
+    qry_img, q_label = batch[0], batch[1]
+    heads = transformer.n_head
+    tsd = {n: transformer.view(n).detach().clone() for n, _, _, _ in _layout(heads, 512)[0]}
+    f_q = torch.nn.functional.adaptive_avg_pool2d(qry_img.float(), 5).repeat(1, 171, 1, 1)[:, :512]
+    W = W0.reshape(2, 512).float()
+    loss, grads, _ = O.cwt_train_step_grads(W, f_q, q_label, tsd, heads)
+    lay, _ = _layout(heads, 512)
+    for n, shp, off, k in lay:
+        transformer.flat.grad[off:off + k] += grads[n].reshape(-1)
+    z = torch.zeros(1, 3, 2)
+    _stand_in_train_episode.seen.append((float(qry_img.double().sum()), W0.clone(),
+                                         transformer.flat.grad.clone()))
+    return dict(loss=torch.tensor([float(loss)]), W=W, W2=W.view(1, 2, 512), pred_q=None, pred_q0=None,
+                iut=z + 1, iut0=z + 1)
+
+
+class _StubExtractor:
+    training = False
+
+    def train(self, mode=True):
+        self.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+
+def _train_worker(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from few_shot_seg_cwt_amd import dist as cdist
+    from few_shot_seg_cwt_amd import episode
+    from few_shot_seg_cwt_amd import synthetic as syn
+    from few_shot_seg_cwt_amd.transformer import MultiHeadAttentionOne
+    cdist.init_from_env(backend="gloo")
+    assert cdist.seed_everything(2021) == 2021 + rank          # train_ddp.py:62-66
+    t = MultiHeadAttentionOne(2, 512, 512, 512, dropout=0.0)    # per-rank init: differs before the broadcast
+    p0 = [torch.zeros_like(t.flat.data) for _ in range(WORLD)]
+    torch.distributed.all_gather(p0, t.flat.data.clone())
+    assert not torch.equal(p0[0], p0[1])
+    opt = torch.optim.SGD([t.flat], lr=1e-3, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    n_iter = 3
+    loader = episode.SyntheticEpisodes(n_iter * WORLD, S=33, seed=2021).shard(rank, WORLD)
+    _stand_in_train_episode.seen = []
+    episode.train_episode = _stand_in_train_episode
+    cfg = syn.cfg_defaults(image_size=33)
+    episode.do_epoch(cfg, loader, _StubExtractor(), t, opt, epoch=0, iter_per_epoch=n_iter, log_iter=n_iter)
+    seen = _stand_in_train_episode.seen
+    assert len(seen) == n_iter
+    # every rank started from rank 0's parameters, ran its own episodes with its own W0, and the
+    # identical SGD steps on the mean gradient kept the replicas bit-identical
+    pf = [torch.zeros_like(t.flat.data) for _ in range(WORLD)]
+    torch.distributed.all_gather(pf, t.flat.data.clone())
+    assert torch.equal(pf[0], pf[1])
+    ids = torch.tensor([s[0] for s in seen], dtype=torch.float64)
+    w0 = torch.stack([s[1] for s in seen])
+    all_ids = [torch.zeros_like(ids) for _ in range(WORLD)]
+    all_w0 = [torch.zeros_like(w0) for _ in range(WORLD)]
+    torch.distributed.all_gather(all_ids, ids)
+    torch.distributed.all_gather(all_w0, w0)
+    assert not set(all_ids[0].tolist()) & set(all_ids[1].tolist()), "ranks trained on the same episode"
+    assert not torch.equal(all_w0[0], all_w0[1]), "ranks drew the same classifier init"
+    # replay: rank 0's initial parameters, then per step the SGD update on the mean of the two
+    # ranks' local gradients (recorded inside train_episode, before the all-reduce)
+    local = torch.stack([s[2] for s in seen])
+    all_local = [torch.zeros_like(local) for _ in range(WORLD)]
+    torch.distributed.all_gather(all_local, local)
+    ref = torch.nn.Parameter(p0[0].clone())
+    ref_opt = torch.optim.SGD([ref], lr=1e-3, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    for k in range(n_iter):
+        ref.grad = (all_local[0][k] + all_local[1][k]) / 2
+        ref_opt.step()
+    assert torch.allclose(ref.data, t.flat.data, rtol=0, atol=1e-7)
+    torch.distributed.destroy_process_group()
+    open(os.path.join(out_dir, f"tr{rank}"), "w").write("ok")
+
+
+def test_gloo_world2_do_epoch_shards_episodes_and_seeds(tmp_path):
+    """do_epoch over 2 ranks: disjoint episodes (SyntheticEpisodes.shard), per-rank W0
+    (seed_everything), rank 0's starting parameters on both ranks (broadcast_params_), mean
+    gradient all-reduce, identical parameters after every step."""
+    port = _free_port()
+    mp.spawn(_train_worker, args=(port, str(tmp_path)), nprocs=WORLD, join=True)
+    assert all((tmp_path / f"tr{r}").exists() for r in range(WORLD))
+
+
+def test_episode_sampler_matches_distributed_sampler():
+    """EpisodeSampler (get_train_loader's shard) hands out exactly DistributedSampler's indices
+    (dataset.py:57-59): disjoint per rank, covering the permutation, per-epoch reshuffle."""
+    from torch.utils.data import DistributedSampler
+    from few_shot_seg_cwt_amd.dataset import EpisodeSampler
+    for n in (1, 7, 8, 13, 5953):
+        for world in (1, 2, 3, 8):
+            shards = []
+            for r in range(world):
+                ours = EpisodeSampler(n, r, world, shuffle=True)
+                ref = DistributedSampler(list(range(n)), num_replicas=world, rank=r, shuffle=True)
+                for ep in (0, 1):
+                    ours.set_epoch(ep)
+                    ref.set_epoch(ep)
+                    assert list(ours) == list(ref)
+                shards.append(list(ours))
+                assert len(ours) == len(ref)
+            flat = sum(shards, [])
+            assert set(flat) == set(range(n))
+            if n % world == 0:
+                assert len(flat) == len(set(flat)) == n

@@ -131,3 +131,26 @@ def test_train_step_grads(golden_dir, sd50, tsd4):
     assert abs(loss.item() - float(g["e0_loss_q"])) < 1e-4 * abs(float(g["e0_loss_q"]))
     for n, gr in grads.items():
         assert rel(gr.numpy().reshape(-1)[::101], g[f"e0_grad_{n}_sample"]) < 1e-3, n
+
+
+@pytest.mark.slow
+def test_episode_coco_r101_5shot(golden_dir, tsd4):
+    """BASELINE config #5's shapes (COCO 5-shot R101 641) in fp32, against the reference."""
+    g = dict(np.load(os.path.join(golden_dir, "episode_coco_r101_5shot.npz")))
+    sd = O.to_torch_state(syn.make_pspnet_state(101, SEED))
+    cfg = syn.cfg_defaults(image_size=641, layers=101, shot=5)
+    _episode_check(g, sd, tsd4, cfg, 0)
+
+
+@pytest.mark.slow
+def test_train_step_grads_coco_r101(golden_dir, tsd4):
+    """BASELINE config #4's training step (COCO 1-shot R101 641, do_epoch) against the reference."""
+    g = dict(np.load(os.path.join(golden_dir, "train_coco_r101_1shot.npz")))
+    sd = O.to_torch_state(syn.make_pspnet_state(101, SEED))
+    ep = syn.make_episode(SEED, int(g["start"]), 641, 1, syn.coco_val_classes(0))
+    f_q = O.extract_features(torch.from_numpy(ep["qry_img"]), sd, 101)
+    W = torch.from_numpy(g["e0_W"])
+    loss, grads, _ = O.cwt_train_step_grads(W, f_q, torch.from_numpy(ep["q_label"]), tsd4, 4)
+    assert abs(loss.item() - float(g["e0_loss_q"])) < 1e-4 * abs(float(g["e0_loss_q"]))
+    for n, gr in grads.items():
+        assert rel(gr.numpy().reshape(-1)[::101], g[f"e0_grad_{n}_sample"]) < 1e-3, n
