@@ -86,7 +86,8 @@ constexpr int ADAPT_R_DEFAULT = 8;             // replica rows used (CWT_ADAPT_R
 constexpr int ADAPT_SLOT = ADAPT_RMAX * 512;   // floats per accumulator slot
 constexpr int ADAPT_NP = 2 * (ADAPT_CB + 1);
 constexpr int ADAPT_NSTAMP = 10;  // timing-study stamps per (step, workgroup)
-constexpr long ADAPT_ESTRIDE = 3L * ADAPT_SLOT;  // accumulator floats per episode (3 slots)
+constexpr long ADAPT_ESTRIDE = 4L * ADAPT_SLOT;  // accumulator floats per episode (3 float slots; the
+                                                 // persistent loop's 4 int64 slots of 16 rows)
 constexpr int ADAPT_WSTRIDE = 2 * 1024;          // W ping-pong floats per episode
 constexpr int ADAPT_PPW = (ADAPT_NP + 3) / 4;  // lo pixels per wave
 
@@ -103,7 +104,7 @@ struct AdaptDevArgs {
 __global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, int nblk, AdaptScalars* sc, float lr,
                                    int mode, AdaptDevArgs* dargs, const float* f, long f_stride, const float* w_in,
                                    float* w_out, int w_stride, float* zero, long zero_stride, int nzero,
-                                   double* zero_d) {
+                                   double* zero_d, unsigned* zero_u = nullptr, int nzero_u = 0) {
   __shared__ unsigned long long red[2][PREP_MAXBLK];
   const int t = threadIdx.x;
   const int e = blockIdx.x;
@@ -139,6 +140,8 @@ __global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, 
   }
   if (zero)
     for (int i = t; i < nzero; i += blockDim.x) zero[i] = 0.f;
+  if (zero_u && e == 0)
+    for (int i = t; i < nzero_u; i += blockDim.x) zero_u[i] = 0u;
 }
 
 // Per-episode state e = blockIdx.z / nshot: dargs[e], sc[e], and the W / accumulator buffers
@@ -578,6 +581,493 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const float* f_ws, con
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Persistent inner loop: all `iters` SGD steps of every episode in ONE launch.
+//
+// The step kernel above pays, per step, a dependent-launch boundary (~1.8 us), the dispatch
+// skew of ~240 workgroups and a W publish that re-reads the previous step's replicas, and it
+// re-streams f_s from L2 every step.  Here G <= #CU workgroups (one per CU) stay resident for
+// the whole loop:
+//   * a unit = one step-kernel tile (lo-res rows r, r+1 x PA_NC columns incl. the right halo,
+//     i.e. 64 lo-res pixels) of one shot of one episode; workgroup g owns units
+//     [g*U/G, (g+1)*U/G).  A 1-shot 473^2 episode has 2 x 59 = 118 units, 641^2 3 x 80 = 240.
+//   * wave v owns channels [32v, 32v+32) and lane p lo-res pixel p of the unit, so f_s of a
+//     unit is 32 VGPRs per lane: with one unit per workgroup it is loaded ONCE and stays in
+//     registers for all 200 steps (no per-step f traffic at all); with more it is streamed.
+//   * z = (W1-W0).f per pixel: 32 FMAs per lane against the wave's slice of d = W1-W0 (LDS
+//     broadcast), then the 16 per-wave partials are summed in fixed order.
+//   * hi-res pass: the step kernel's (one pixel per lane, octet pre-reduction by DPP), but
+//     each octet writes its two adjoint terms to slots of its own (no LDS atomics; the 16
+//     slots of a lo-res pixel are summed in fixed order).
+//   * dW[1] = sum_p g_p f_p: 32 FMAs per lane per unit, then a 64-lane butterfly
+//     (pa_butterfly) leaves lane 2c+{0,1} holding channel 32v+c; 32 no-return float atomics
+//     per wave into replica row (g % nrep) of the step's slot (they execute at the memory side,
+//     MI355X_MICROARCH.md Global float atomics).
+//   * grid barrier: every wave waits for its atomics (vmcnt(0)), workgroup barrier, one lane
+//     adds 1 to arrival counter (g % nrep) (agent scope); wave 0 polls the counters with sc1
+//     loads until they sum to G*(s+1) (MI355X_MICROARCH.md hand-off table, counter row); every
+//     workgroup then reads the slot's replica rows with sc1 loads and applies W1 -= lr_eff*D,
+//     W0 += lr_eff*D in the same order, so W stays identical everywhere.
+//     (A barrier-free variant -- 64-bit fixed-point adds carrying a contribution count, polled
+//     element by element -- was exact and deterministic but 1.7x slower per step: 118 x 1024
+//     threads polling the same 32 KB contend with the adds at the memory side.)
+//   * slots: step s adds into slot s%4; workgroup G-1 zeroes slot (s+2)%4 at the start of step
+//     s (its last readers passed barrier s-1; its next adders start after barrier s+1; the
+//     write-through zero stores are complete when G-1 arrives at barrier s).
+// Every spin is bounded: a barrier that does not complete within ~4 s sets the error word and
+// the grid exits (wrong W, no hang).  Requires all G workgroups co-resident: G <= #CU and one
+// 1024-thread workgroup per CU.
+// ---------------------------------------------------------------------------------------
+constexpr int PA_T = 1024;
+constexpr int PA_NW = 16;
+constexpr int PA_UC = 31;            // max lo-res columns owned per unit (a.uc: 31, or 15 when that fits the CUs)
+constexpr int PA_NC = PA_UC + 1;     // storage stride of a unit's lo-res row (held columns: a.uc + 1)
+constexpr int PA_NPX = 2 * PA_NC;    // lo-res pixels per unit: one per lane
+constexpr int PA_CPW = 512 / PA_NW;  // channels per wave
+constexpr int PA_R = 16;             // max replica rows of dW[1] (and arrival counters) per slot
+constexpr int PA_R_DEFAULT = 8;      // rows used (CWT_ADAPT_PR: 2, 4, 8 or 16)
+constexpr int PA_NSLOT = 4;          // accumulator slots (step s adds into s % 4)
+constexpr int PA_EW = 4;             // episodes one workgroup's units may span
+constexpr int PA_CNT_STRIDE = 32;    // one control word per 128-B line
+constexpr int PA_CNT_WORDS = (PA_R + 1) * PA_CNT_STRIDE;  // arrival counters + error word
+constexpr long PA_SPIN_LIMIT = 4000000;
+static_assert(PA_NSLOT * ADAPT_SLOT <= ADAPT_ESTRIDE && PA_R <= ADAPT_RMAX, "slots must fit an episode's accumulators");
+
+struct PersistArgs {
+  const float* f;          // [E][n][h][w][512] (read in place: no per-call copy)
+  const uint8_t* lbl;      // [E][n][S][S]
+  const AdaptScalars* sc;  // [E]
+  const AdaptDevArgs* dargs;  // [E]: w_in / w_out
+  float* acc;              // [E][PA_NSLOT][ADAPT_RMAX][512]; slots 0 and 1 zeroed by the setup kernel
+  unsigned* cnt;           // [PA_CNT_WORDS], zeroed by the setup kernel
+  int h, w, S, nshot, nep, iters;
+  int ncb, ntile, units, G;
+  int nrep;    // replica rows in use
+  int uc;      // lo-res columns owned per unit (15 or 31)
+};
+
+struct PaUnit {
+  int e, img, r, x0, ncol, x_end;
+  bool extra_row;  // this unit's row pair is the last: it also owns hi-res row S-1
+};
+
+__device__ __forceinline__ PaUnit pa_unit(const PersistArgs& a, int u) {
+  PaUnit q;
+  const int per_ep = a.nshot * a.ntile;
+  q.e = u / per_ep;
+  const int rem = u - q.e * per_ep;
+  const int shot = rem / a.ntile, tile = rem - shot * a.ntile;
+  q.img = q.e * a.nshot + shot;
+  q.r = tile / a.ncb;
+  const int cb = tile - q.r * a.ncb;
+  q.x0 = cb * a.uc;
+  q.ncol = min(a.uc + 1, a.w - q.x0);
+  q.x_end = (cb == a.ncb - 1) ? a.S : 8 * (q.x0 + a.uc);
+  q.extra_row = q.r == a.h - 2;
+  return q;
+}
+
+// Per-lane state of one unit: f of lane p's pixel over the wave's 32 channels, and the labels
+// of the lane's hi-res pixels (2 column rounds x {row 8r + wv/2, row S-1}); 255 = no pixel.
+struct PaTile {
+  float fr[PA_CPW];
+  int y[2][2];
+};
+
+__device__ __forceinline__ void pa_load(PaTile& t, const PersistArgs& a, const PaUnit& q, int wv, int lane) {
+  const int ri = lane >> 5, xs = min(lane & 31, q.ncol - 1);
+  const float* src = a.f + (((long)q.img * a.h + q.r + ri) * a.w + q.x0 + xs) * 512 + wv * PA_CPW;
+#pragma unroll
+  for (int j = 0; j < PA_CPW / 4; ++j) {
+    const f32x4 v = *(const f32x4*)(src + 4 * j);
+    t.fr[4 * j] = v[0]; t.fr[4 * j + 1] = v[1]; t.fr[4 * j + 2] = v[2]; t.fr[4 * j + 3] = v[3];
+  }
+  const uint8_t* lb = a.lbl + (long)q.img * a.S * a.S;
+  const int Y = 8 * q.r + (wv >> 1);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int X = 8 * q.x0 + 64 * (wv & 1) + 128 * k + lane;
+    const int Xc = min(X, a.S - 1);
+    const int ym = lb[(long)Y * a.S + Xc], ye = lb[(long)(a.S - 1) * a.S + Xc];
+    const bool xin = X < q.x_end;
+    t.y[k][0] = xin ? ym : 255;
+    t.y[k][1] = (xin && q.extra_row && (wv >> 1) == 0) ? ye : 255;
+  }
+}
+
+// 64-lane reduction of 32 per-lane values (channel j in v[j]) leaving lane L with channel L >> 1:
+// five halving steps, each pairing lanes that differ in one lane bit (the lane with the bit set
+// keeps the upper half of the channels, its partner the lower), then one plain pair sum.
+//   bit 5, 4: v_permlane32_swap / v_permlane16_swap exchange whole halves / rows of two VGPRs,
+//             so after the swap both partners just add (no select);
+//   bit 3, 2: DPP row_mirror / row_half_mirror (partners 15-i / 7-i share the higher bits);
+//   bit 1, 0: DPP quad_perm xor 2 / xor 1.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void pa_butterfly(float (&v)[PA_CPW], int lane) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j + 16]), false, false);
+    v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[j]), __float_as_uint(v[j + 8]), false, false);
+    v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  {
+    const bool up = (lane & 8) != 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float send = up ? v[j] : v[j + 4], keep = up ? v[j + 4] : v[j];
+      v[j] = keep + dpp_mov<0x140>(send);
+    }
+  }
+  {
+    const bool up = (lane & 4) != 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float send = up ? v[j] : v[j + 2], keep = up ? v[j + 2] : v[j];
+      v[j] = keep + dpp_mov<0x141>(send);
+    }
+  }
+  {
+    const bool up = (lane & 2) != 0;
+    const float send = up ? v[0] : v[1], keep = up ? v[1] : v[0];
+    v[0] = keep + dpp_mov<0x4E>(send);
+  }
+  v[0] += dpp_mov<0xB1>(v[0]);
+}
+
+// STAMPS (CWT_ADAPT_DBG & 32, a separate instantiation; never the timed one): thread 0 records
+// s_memtime at 8 points of every step, realtime at its arrival ([8]) and when its poll matched
+// ([9]) into stamps[step][g][10], and realtime/memtime at entry and exit into
+// stamps[iters][g][0..3] (tools/persist_stamps.py).
+template <int NRES, bool STAMPS = false>  // NRES 1: one unit per workgroup, resident in registers; 0: streamed
+__global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsigned long long* stamps = nullptr) {
+  constexpr int C = 512;
+  __shared__ float wl[PA_EW][2][C];
+  __shared__ float dl[PA_EW][C];
+  __shared__ float zpart[PA_NW][PA_NPX];
+  __shared__ float zd[PA_NPX];
+  __shared__ float gs[PA_NPX];
+  __shared__ float P0[8][2][PA_NC + 1];
+  __shared__ float P1[8][2][PA_NC + 1];
+  __shared__ float dsum[C];
+  __shared__ float wfg_l[PA_EW], lr_l[PA_EW];
+  __shared__ int abort_flag;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int g = blockIdx.x, G = a.G;
+  const int u0 = (int)(((long)g * a.units) / G), u1 = (int)(((long)(g + 1) * a.units) / G);
+  const int per_ep = a.nshot * a.ntile;
+  const int e_lo = u0 / per_ep, e_hi = (u1 - 1) / per_ep;
+  const int new_ = e_hi - e_lo + 1;  // episodes spanned (<= PA_EW, checked on the host)
+  const int nrep = a.nrep;
+  const int rep = g % nrep;
+  unsigned* err = a.cnt + PA_R * PA_CNT_STRIDE;
+  unsigned long long* stp_end = (STAMPS && t == 0) ? stamps + ((long)a.iters * G + g) * 10 : nullptr;
+  if (STAMPS && t == 0) {
+    stp_end[0] = __builtin_amdgcn_s_memrealtime();
+    stp_end[1] = __builtin_amdgcn_s_memtime();
+  }
+
+  // initial W of the spanned episodes
+  for (int i = t; i < new_ * C; i += PA_T) {
+    const int ew = i / C, c = i - ew * C;
+    const float* wi = a.dargs[e_lo + ew].w_in;
+    const float w0 = wi[c], w1 = wi[C + c];
+    wl[ew][0][c] = w0;
+    wl[ew][1][c] = w1;
+    dl[ew][c] = w1 - w0;
+  }
+  if (t == 0) abort_flag = 0;
+  if (t < new_) {
+    wfg_l[t] = a.sc[e_lo + t].wfg;
+    lr_l[t] = a.sc[e_lo + t].lr_eff;
+  }
+  PaTile cur;
+  PaUnit q = pa_unit(a, u0);
+  pa_load(cur, a, q, wv, lane);
+  __syncthreads();
+
+  const int i_row = wv >> 1;
+  const float ly1 = (float)i_row * 0.125f, ly0 = 1.f - ly1;
+  for (int s = 0; s < a.iters; ++s) {
+    const int slot = s % PA_NSLOT;
+    unsigned long long* stp = (STAMPS && t == 0) ? stamps + ((long)s * G + g) * 10 : nullptr;
+    auto stamp = [&](int i) {
+      if (STAMPS && stp) stp[i] = __builtin_amdgcn_s_memtime();
+    };
+    stamp(0);
+    if (g == G - 1 && s + 2 < a.iters) {  // zero slot (s+2)%4 (write-through stores, done by our arrival)
+      const int zs = (s + 2) % PA_NSLOT;
+      for (int i = t; i < a.nep * nrep * C; i += PA_T) {
+        const int e = i / (nrep * C), k = i - e * (nrep * C);
+        __hip_atomic_store(a.acc + (long)e * ADAPT_ESTRIDE + (long)zs * ADAPT_SLOT + k, 0.f, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    for (int u = u0; u < u1; ++u) {
+      if (NRES == 0 && u != u0) {  // streamed: this unit's f and labels (the first one was prefetched)
+        q = pa_unit(a, u);
+        pa_load(cur, a, q, wv, lane);
+      } else if (NRES == 0) {
+        q = pa_unit(a, u);
+      }
+      const int ew = q.e - e_lo;
+      // ---- z = d . f: this wave's 32-channel partial for lane p's pixel ----
+      {
+        float sdot = 0.f;
+#pragma unroll
+        for (int j = 0; j < PA_CPW / 4; ++j) {
+          const f32x4 d4 = *(const f32x4*)&dl[ew][wv * PA_CPW + 4 * j];
+          sdot = fmaf(d4[0], cur.fr[4 * j], sdot);
+          sdot = fmaf(d4[1], cur.fr[4 * j + 1], sdot);
+          sdot = fmaf(d4[2], cur.fr[4 * j + 2], sdot);
+          sdot = fmaf(d4[3], cur.fr[4 * j + 3], sdot);
+        }
+        zpart[wv][lane] = sdot;
+      }
+      lds_barrier();
+      if (t < PA_NPX) {
+        float z = 0.f;
+#pragma unroll
+        for (int v = 0; v < PA_NW; ++v) z += zpart[v][t];
+        zd[t] = z;
+      }
+      lds_barrier();
+      if (u == u0) stamp(1);
+      // ---- hi-res pass: weighted-CE gradient, bilinear adjoint pre-reduced per octet ----
+      {
+        const bool has_extra = q.extra_row && i_row == 0;
+        const float wf = wfg_l[ew];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          if (k == 1 && a.uc < 16) break;  // 8 * 15 columns (+ the last block's tail) fit one round
+          const int X = 8 * q.x0 + 64 * (wv & 1) + 128 * k + lane;
+          const int slot_x = 8 * (wv & 1) + 16 * k + (lane >> 3);  // = (X >> 3) - x0 before clamping
+          const int ix = min(X >> 3, a.w - 1);
+          const int xi0 = min(ix - q.x0, PA_NC - 1);
+          const int xi1 = (ix < a.w - 1) ? min(xi0 + 1, PA_NC - 1) : xi0;
+          const float lx1 = (float)(X & 7) * 0.125f, lx0 = 1.f - lx1;
+          float sa[2] = {0.f, 0.f}, sb[2] = {0.f, 0.f};
+#pragma unroll
+          for (int e2 = 0; e2 < 2; ++e2) {
+            if (e2 == 1 && !has_extra) break;  // wave-uniform: only the last row pair's row-0 waves
+            const int y = cur.y[k][e2];
+            float gv = 0.f;
+            if (y != 255) {
+              const float dd = e2 ? (lx0 * zd[PA_NC + xi0] + lx1 * zd[PA_NC + xi1])
+                                  : ly0 * (lx0 * zd[xi0] + lx1 * zd[xi1]) +
+                                        ly1 * (lx0 * zd[PA_NC + xi0] + lx1 * zd[PA_NC + xi1]);
+              const float p1 = __builtin_amdgcn_rcpf(1.f + __expf(-dd));
+              gv = ((y == 1) ? wf : 1.f) * (p1 - (float)y);
+            }
+            sa[e2] = octet_sum(lx0 * gv);
+            sb[e2] = octet_sum(lx1 * gv);
+          }
+          if ((lane & 7) == 0) {
+            P0[i_row][0][slot_x] = ly0 * sa[0];
+            P1[i_row][0][slot_x + 1] = ly0 * sb[0];
+            P0[i_row][1][slot_x] = ly1 * sa[0] + sa[1];
+            P1[i_row][1][slot_x + 1] = ly1 * sb[0] + sb[1];
+          }
+        }
+      }
+      lds_barrier();
+      if (t < PA_NPX) {
+        const int ri = t >> 5, xi = t & 31;
+        float gsum = 0.f;
+        if (xi <= a.uc) {  // held columns only (the rest were not written this unit)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) gsum += P0[i][ri][xi];
+          if (xi > 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) gsum += P1[i][ri][xi];
+          }
+        }
+        gs[t] = gsum;
+      }
+      lds_barrier();
+      if (u == u0) stamp(2);
+      // ---- dW[1] of the unit: lane p's pixel times its gradient, over the wave's channels ----
+      {
+        float accd[PA_CPW];
+        const float gp = gs[lane];
+#pragma unroll
+        for (int j = 0; j < PA_CPW; ++j) accd[j] = gp * cur.fr[j];
+        pa_butterfly(accd, lane);  // lane L: channel (L >> 1) of the wave's slice, summed over 64 lanes
+        if ((lane & 1) == 0)
+          __hip_atomic_fetch_add(a.acc + (long)q.e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
+                                     wv * PA_CPW + (lane >> 1),
+                                 accd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    stamp(3);
+    // ---- grid barrier s ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics (and zero stores) performed
+    __syncthreads();
+    stamp(4);
+    if (STAMPS && stp) stp[8] = __builtin_amdgcn_s_memrealtime();
+    if (t == 0) __hip_atomic_fetch_add(a.cnt + rep * PA_CNT_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (NRES == 0 && s + 1 < a.iters) {  // next step's first unit: W-independent, lands during the wait
+      q = pa_unit(a, u0);
+      pa_load(cur, a, q, wv, lane);
+    }
+    if (wv == 0) {
+      const unsigned target = (unsigned)G * (unsigned)(s + 1);
+      long spins = 0;
+      while (true) {
+        unsigned c = lane < nrep ? __hip_atomic_load(a.cnt + lane * PA_CNT_STRIDE, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                 : 0u;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        c = __builtin_amdgcn_readfirstlane(c);
+        if (c >= target) break;
+        if (++spins > PA_SPIN_LIMIT || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          if (lane == 0) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            abort_flag = 1;
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    stamp(5);
+    if (STAMPS && stp) stp[9] = __builtin_amdgcn_s_memrealtime();
+    lds_barrier();
+    stamp(6);
+    if (abort_flag) return;
+    // ---- W of every spanned episode: W1 -= lr_eff * D, W0 += lr_eff * D (same order everywhere);
+    // thread halves t < 512 / t >= 512 sum replica rows [0, nrep/2) / [nrep/2, nrep) ----
+    const int nh = nrep >> 1;
+    for (int ew = 0; ew < new_; ++ew) {
+      const int c = t & (C - 1), hh = t >> 9;
+      const float* ap = a.acc + (long)(e_lo + ew) * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + (long)hh * nh * C + c;
+      float v[PA_R / 2];
+#pragma unroll
+      for (int r = 0; r < PA_R / 2; ++r)
+        v[r] = r < nh ? __hip_atomic_load(ap + r * C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+      float D = 0.f;
+#pragma unroll
+      for (int r = 0; r < PA_R / 2; ++r) D += v[r];
+      if (hh) dsum[c] = D;
+      lds_barrier();
+      if (!hh) {
+        D += dsum[c];
+        const float lr = lr_l[ew];
+        const float w1 = wl[ew][1][c] - lr * D, w0 = wl[ew][0][c] + lr * D;
+        wl[ew][1][c] = w1;
+        wl[ew][0][c] = w0;
+        dl[ew][c] = w1 - w0;
+      }
+      lds_barrier();
+    }
+    stamp(7);
+  }
+  if (STAMPS && t == 0) {
+    stp_end[2] = __builtin_amdgcn_s_memrealtime();
+    stp_end[3] = __builtin_amdgcn_s_memtime();
+  }
+  // ---- adapted W: written by the workgroup that owns the episode's first unit ----
+  for (int i = t; i < new_ * C; i += PA_T) {
+    const int ew = i / C, c = i - ew * C;
+    const int e = e_lo + ew;
+    if ((long)e * per_ep >= u0) {
+      float* wo = a.dargs[e].w_out;
+      wo[c] = wl[ew][0][c];
+      wo[C + c] = wl[ew][1][c];
+    }
+  }
+}
+
+// Host side of the persistent loop: G = min(units, CUs).  Returns 1 (not an error) when the
+// geometry does not fit it (the caller then uses the per-step launches).
+static int g_cu_count = 0;
+static int persist_geometry(int E, int n, int h, int w, int* G_out, int* units_out, int* ncb_out, int* nres_out,
+                            int* uc_out) {
+  if (!g_cu_count) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&g_cu_count, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      g_cu_count = 0;
+    if (g_cu_count <= 0) return 1;
+  }
+  // 31 owned columns: 15 halves each workgroup's hi-res pixels but doubles the workgroups, and
+  // the barrier's atomics and arrivals cost more than that saves (1-shot 473: 7.0 vs 5.9 us per
+  // step, tools/persist_stamps.py); CWT_ADAPT_UC=15 selects it
+  int uc = PA_UC;
+  const char* ucs = getenv("CWT_ADAPT_UC");
+  if (ucs && (atoi(ucs) == 15 || atoi(ucs) == 31)) uc = atoi(ucs);
+  const int ncb = cdiv(w - 1, uc);
+  const int ntile = (h - 1) * ncb;
+  const long units = (long)E * n * ntile;
+  const int G = (int)std::min<long>(units, g_cu_count);
+  const long k = (units + G - 1) / G;  // units per workgroup (max)
+  const long per_ep = (long)n * ntile;
+  const long span = (k - 1 + per_ep - 1) / per_ep + 1;  // episodes a workgroup's range can touch
+  if (span > PA_EW) return 1;
+  *G_out = G;
+  *units_out = (int)units;
+  *ncb_out = ncb;
+  *uc_out = uc;
+  *nres_out = (units <= G) ? 1 : 0;
+  // streamed units (multi-shot) are not yet faster than the step launches: opt in only
+  const char* pe = getenv("CWT_ADAPT_PERSIST");
+  if (!*nres_out && !(pe && pe[0] == '2')) return 1;
+  return 0;
+}
+
+static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const AdaptScalars* sc, float* acc3,
+                                 unsigned* cnt, const AdaptDevArgs* dargs, int E, int n, int h, int w, int S,
+                                 int iters, int G, int units, int ncb, int nres, int uc, hipStream_t st) {
+  PersistArgs a;
+  a.f = f;
+  a.lbl = lbl_ws;
+  a.sc = sc;
+  a.dargs = dargs;
+  a.acc = acc3;
+  a.cnt = cnt;
+  a.h = h;
+  a.w = w;
+  a.S = S;
+  a.nshot = n;
+  a.nep = E;
+  a.iters = iters;
+  a.ncb = ncb;
+  a.ntile = (h - 1) * ncb;
+  a.units = units;
+  a.G = G;
+  a.uc = uc;
+  const char* pr = getenv("CWT_ADAPT_PR");
+  a.nrep = pr ? atoi(pr) : PA_R_DEFAULT;
+  if (a.nrep != 2 && a.nrep != 4 && a.nrep != 8 && a.nrep != 16) a.nrep = PA_R_DEFAULT;
+  const char* dbg = getenv("CWT_ADAPT_DBG");
+  if (dbg && (atoi(dbg) & 32)) {  // timing study (tools/persist_stamps.py)
+    const long n_st = ((long)iters + 1) * G * 10;
+    if (n_st > g_adapt_stamps_n) {
+      CWT_HIP(hipDeviceSynchronize());
+      if (g_adapt_stamps) CWT_HIP(hipFree(g_adapt_stamps));
+      CWT_HIP(hipMalloc(&g_adapt_stamps, n_st * sizeof(unsigned long long)));
+      g_adapt_stamps_n = n_st;
+    }
+    if (nres)
+      hipLaunchKernelGGL((adapt_persist_kernel<1, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
+    else
+      hipLaunchKernelGGL((adapt_persist_kernel<0, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
+  } else if (nres) {
+    hipLaunchKernelGGL((adapt_persist_kernel<1, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
+  } else {
+    hipLaunchKernelGGL((adapt_persist_kernel<0, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
+  }
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 AdaptGraphCache::~AdaptGraphCache() {
   for (auto& e : entries) (void)hipGraphExecDestroy(e.exec);
   if (cap_stream) (void)hipStreamDestroy(cap_stream);
@@ -588,7 +1078,7 @@ size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lb
   *fws = (size_t)E * n * h * w * 512 * sizeof(float);
   *lbl = (size_t)E * n * S * S;
   *sc = (size_t)E * (sizeof(AdaptScalars) + 2 * PREP_MAXBLK * sizeof(unsigned long long)) + 64;
-  *acc = (size_t)E * ADAPT_ESTRIDE * sizeof(float);
+  *acc = (size_t)E * ADAPT_ESTRIDE * sizeof(float) + PA_CNT_WORDS * sizeof(unsigned);  // + persistent-loop counters
   *wbuf = (size_t)E * ADAPT_WSTRIDE * sizeof(float);
   *dargs = (size_t)E * sizeof(AdaptDevArgs);
   return 0;
@@ -600,18 +1090,28 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
                  float* acc3 /*[E][3][R][512]*/, float* wbuf /*[E][2][2][512]*/, AdaptDevArgs* dargs /*[E]*/,
                  AdaptGraphCache* cache, hipStream_t st) {
   const long total = (long)n * S * S;  // labels per episode
-  // the step graph reads f from the library's buffer (fixed address, baked into the graph)
-  if (iters > 0 && f != f_ws)
-    CWT_HIP(hipMemcpyAsync(f_ws, f, (size_t)E * n * h * w * 512 * sizeof(float), hipMemcpyDeviceToDevice, st));
   unsigned long long* part = (unsigned long long*)(sc + E);  // [E][PREP_MAXBLK][2] after the scalars
   const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
   hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks, E), dim3(1024), 0, st, lbl64, total, lbl_ws, part);
   CWT_LAUNCH_CHECK();
+  int pG = 0, punits = 0, pncb = 0, pnres = 0, puc = 0;
+  const char* pe = getenv("CWT_ADAPT_PERSIST");
+  const bool persist = iters > 0 && !(pe && pe[0] == '0') &&
+                       persist_geometry(E, n, h, w, &pG, &punits, &pncb, &pnres, &puc) == 0;
+  unsigned* cnt = (unsigned*)(acc3 + (long)E * ADAPT_ESTRIDE);
   hipLaunchKernelGGL(adapt_setup_kernel, dim3(E), dim3(PREP_MAXBLK), 0, st, (const unsigned long long*)part, pblocks,
                      sc, lr, 0, dargs, f, (long)n * h * w * 512, (const float*)W, W, 1024,
-                     iters > 0 ? acc3 : (float*)nullptr, ADAPT_ESTRIDE, ADAPT_SLOT, (double*)nullptr);
+                     iters > 0 ? acc3 : (float*)nullptr, ADAPT_ESTRIDE, persist ? 2 * ADAPT_SLOT : ADAPT_SLOT,
+                     (double*)nullptr,
+                     persist ? cnt : (unsigned*)nullptr, persist ? PA_CNT_WORDS : 0);
   CWT_LAUNCH_CHECK();
   if (iters <= 0) return 0;
+  if (persist)  // one launch for all steps, f read in place (no copy, no graph)
+    return enqueue_adapt_persist(f, lbl_ws, sc, acc3, cnt, dargs, E, n, h, w, S, iters, pG, punits, pncb, pnres, puc,
+                                 st);
+  // the step graph reads f from the library's buffer (fixed address, baked into the graph)
+  if (f != f_ws)
+    CWT_HIP(hipMemcpyAsync(f_ws, f, (size_t)E * n * h * w * 512 * sizeof(float), hipMemcpyDeviceToDevice, st));
   const char* dbg = getenv("CWT_ADAPT_DBG");
   if (dbg && (atoi(dbg) & 32)) {  // timing study: stamp buffer sized for G = 1 (allocated outside any capture)
     const long n_st = (long)iters * cdiv(S - 1, 8 * ADAPT_CB) * (h - 1) * E * ADAPT_NSTAMP;

@@ -1,0 +1,74 @@
+"""The persistent inner loop (adapt_persist_kernel: all 200 SGD steps in one launch, in-kernel
+grid barrier) against the per-step launches it replaces (CWT_ADAPT_PERSIST=0) on the same
+inputs, at the BASELINE shapes and in batched / multi-unit-per-workgroup geometries.  Both
+are fp32 with atomic (order-free) gradient sums, so they agree to rounding; the oracle and
+reference fixtures pin the absolute result (test_gpu_parity.py, test_gpu_shapes.py)."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from few_shot_seg_cwt_amd import synthetic as syn  # noqa: E402
+
+SEED = 2021
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def _run(persist, f, lbl, W0, iters, uc=None):
+    """persist: "0" per-step launches, "2" the persistent loop also where units are streamed."""
+    from few_shot_seg_cwt_amd.episode import inner_adapt_batch
+    env = {"CWT_ADAPT_PERSIST": persist, "CWT_ADAPT_UC": uc}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    try:
+        W = inner_adapt_batch(f, lbl, W0.clone(), 0.1, iters)
+        torch.cuda.synchronize()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return W
+
+
+@pytest.mark.parametrize("E,n,S,iters,uc", [
+    (1, 1, 473, 200, None),  # config #2: 236 15-column units, one per workgroup (f resident in registers)
+    (1, 1, 473, 200, "31"),  # ... as 118 31-column units
+    (1, 5, 473, 200, None),  # config #3: 590 units over 256 workgroups (streamed)
+    (1, 1, 641, 200, None),  # config #4 shapes: 240 units
+    (1, 5, 641, 50, None),   # config #5 shapes: 1200 units
+    (4, 1, 473, 50, None),   # episodes in flight: workgroups span two episodes
+    (16, 1, 129, 20, None),
+    (3, 2, 65, 20, None),
+    (2, 1, 33, 5, None),
+])
+def test_persist_equals_step_launches(dev, E, n, S, iters, uc):
+    h = (S - 1) // 8 + 1
+    f = torch.from_numpy(syn.normal(5, f"fp{E}{n}{S}", (E * n, 512, h, h), 0.1)).to(dev)
+    f = f.contiguous(memory_format=torch.channels_last)
+    lbl = torch.stack([torch.from_numpy(syn.make_episode(SEED, 70 + e, S, n)["s_label"][0]) for e in range(E)]).to(dev)
+    W0 = torch.from_numpy(syn.normal(6, f"wp{E}{n}{S}", (E, 2, 512), 0.04)).to(dev)
+    Wp = _run("2", f, lbl, W0, iters, uc)
+    Ws = _run("0", f, lbl, W0, iters)
+    errs = [rel(Wp[e], Ws[e]) for e in range(E)]
+    print(f"E={E} n={n} S={S} iters={iters}: max rel {max(errs):.3e}")
+    assert max(errs) < 1e-4, errs
+    assert torch.isfinite(Wp).all()
