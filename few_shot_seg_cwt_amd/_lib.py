@@ -84,6 +84,19 @@ class CwtError(RuntimeError):
     pass
 
 
+def check_provenance(version: str, path: str):
+    """Refuse a library built from other sources than the tree's (build.py source_hash, compiled
+    into cwt_version()).  CWT_LIB_PATH builds (A/B timing of another build) are exempt."""
+    from . import build as _build
+    if os.environ.get("CWT_LIB_PATH") or not os.path.isdir(_build.CSRC):
+        return
+    want = _build.source_hash()
+    got = version.rsplit("src=", 1)[-1] if "src=" in version else None
+    if got != want:
+        raise CwtError(f"{path} is stale: built from sources {got}, the tree's are {want}; "
+                       "run `python -m few_shot_seg_cwt_amd.build`")
+
+
 def load_library(path: str = LIB_PATH):
     """Load libcwt.so and declare every prototype (works without a GPU)."""
     global _lib
@@ -97,6 +110,7 @@ def load_library(path: str = LIB_PATH):
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
+            check_provenance(lib.cwt_version().decode(), path)
             _lib = lib
     return _lib
 

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/cwt.h"
+#include "../../include/cwt_debug.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -61,8 +62,6 @@ size_t attention_bwd_ws_floats(int B, int hw, int C, int H);
 struct ConvLayer {
   int Ci = 0, Co = 0, k = 1, stride = 1, pad = 0, dil = 1;
   float* w = nullptr;  // device, packed [Co][k][k][Ci] (stem conv1: [ci][ky][kx][co])
-  __bf16* w_hi = nullptr;  // bf16x3 split of w (same layout); null for the stem conv1
-  __bf16* w_lo = nullptr;
   __bf16* w_s = nullptr;   // S-layout [Co][K/32][hi 32 | lo 32] of the same split (conv_x3s.hip)
   __bf16* w_b = nullptr;   // plain bf16 [Co][K], K in packed_k64 order (bf16 conv stack; Ci % 64 == 0)
   float* scale = nullptr;
@@ -119,8 +118,7 @@ struct cwt_ctx {
   cwt::AdaptGraphCache adapt_graphs;
   bool use_graph = true;
   // conv arithmetic: bf16x3 on the bf16 matrix cores over S-layout activations (default,
-  // CWT_CONV=x3s), bf16x3 over fp32 activations (CWT_CONV=x3) or exact fp32 MFMA (CWT_CONV=f32)
-  bool conv_x3 = true;
+  // CWT_CONV=x3s) or exact fp32 MFMA over fp32 activations (CWT_CONV=f32)
   bool conv_split = true;
 };
 
@@ -281,7 +279,6 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
       hi[i] = bf16_rne(v);
       lo[i] = bf16_rne(v - bf16_to_float(hi[i]));
     }
-    if ((rc = upload_u16(bb, hi, &L->w_hi)) || (rc = upload_u16(bb, lo, &L->w_lo))) return rc;
     std::vector<uint16_t> sl(2 * packed.size());
     for (size_t r = 0; r < (size_t)Co; ++r)
       for (int kb = 0; kb < K / 32; ++kb)
@@ -444,8 +441,6 @@ static ConvArgs make_args(const ConvCall& c) {
   const ConvLayer& L = *c.L;
   a.x = c.x;
   a.w = L.w;
-  a.w_hi = L.w_hi;
-  a.w_lo = L.w_lo;
   a.scale = L.scale;
   a.shift = L.shift;
   a.res = c.res;
@@ -488,7 +483,6 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   // the training-mode BN pass (once per epoch) amplifies conv rounding ~100x through its
   // batch statistics: in fp32 precision it runs the exact-fp32 conv path
   const bool conv_split = ctx->conv_split && !(tb && !b16);
-  const bool conv_x3 = ctx->conv_x3 && !(tb && !b16);
   const bool s_path = b16 || conv_split;  // conv_x3s.hip kernels
   const int layout = b16 ? ACT_BF16 : conv_split ? ACT_SPLIT : ACT_F32;
   const int prec = b16 ? 1 : 3;
@@ -582,10 +576,8 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   for (auto& c : calls) {
     ConvArgs a = make_args(c);
     if (b16 && !c.L->w_b) return fail(CWT_ESTATE, "bf16 conv weights missing (Ci % 64 != 0)");
-    ConvPlan pl = b16              ? plan_conv_b16(a.M, a.Co, a.K)
-                  : conv_split ? plan_conv_x3s(a.M, a.Co, a.K)
-                  : conv_x3    ? plan_conv_x3(a.M, a.Co, a.K)
-                                    : plan_conv(a.M, a.Co, a.K);
+    ConvPlan pl = b16 ? plan_conv_b16(a.M, a.Co, a.K) : conv_split ? plan_conv_x3s(a.M, a.Co, a.K)
+                                                                  : plan_conv(a.M, a.Co, a.K);
     plans.push_back(pl);
     if (pl.nsplit > 1) part_floats = std::max(part_floats, (size_t)pl.nsplit * a.M * a.Co);
   }
@@ -651,8 +643,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     const double bytes = eb * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K) +
                          ob * ((double)a.M * a.Co + (a.res ? (double)a.M * a.Co : 0.0));
     Prof p(ctx, st,
-           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : conv_x3 ? "conv_igemm_bf16x3<"
-                                                                                                     : "conv_igemm_f32<") +
+           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : "conv_igemm_f32<") +
                std::to_string(pl.bm) + "," +
                std::to_string(pl.bn) + "," +
                std::to_string(calls[i].stage) + ">" +
@@ -697,8 +688,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
       sa.K = a.K;
       r = launch_conv_x3s(sa, pl, c.stage, PART, part_floats, st, prec);
     } else {
-      r = conv_x3 ? launch_conv_x3(a, pl, calls[i].stage, PART, part_floats, st)
-                       : launch_conv(a, pl, calls[i].stage, PART, part_floats, st);
+      r = launch_conv(a, pl, calls[i].stage, PART, part_floats, st);
     }
     p.end();
     if (r || !tb) return r;
@@ -801,7 +791,12 @@ using namespace cwt;
 
 extern "C" {
 
-const char* cwt_version(void) { return "libcwt 0.1 (gfx950, fp32 MFMA)"; }
+#ifndef CWT_SRC_HASH
+#define CWT_SRC_HASH "unknown"
+#endif
+// the content hash of the HIP sources and headers this library was built from (build.py
+// source_hash); _lib.load_library refuses a library whose hash differs from the tree's
+const char* cwt_version(void) { return "libcwt 0.2 (gfx950) src=" CWT_SRC_HASH; }
 
 const char* cwt_last_error(void) { return g_err.c_str(); }
 
@@ -817,7 +812,10 @@ int cwt_ctx_create(int device, cwt_ctx** out) {
   c->use_graph = !(g && g[0] == '0');
   const char* cv = getenv("CWT_CONV");
   const std::string mode = cv ? std::string(cv) : std::string("x3s");
-  c->conv_x3 = mode != "f32";
+  if (mode != "x3s" && mode != "f32") {
+    delete c;
+    return fail(CWT_EARG, "CWT_CONV must be x3s (default) or f32");
+  }
   c->conv_split = mode == "x3s";
   *out = c;
   return 0;
@@ -1102,7 +1100,7 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
   L.dil = dil;
   L.w = (float*)w_packed;
   int rc;
-  if (k > 1 && precision != 2) {  // caller layout [Co][k][k][Ci] -> packed_k order
+  if (k > 1) {  // caller layout [Co][k][k][Ci] -> packed_k order
     void* wp;
     if ((rc = ensure_ws(ctx, "dbg.wpack", (size_t)Co * k * k * Ci * 4, &wp))) return rc;
     if ((rc = launch_repack_cblock(w_packed, (float*)wp, Co, k * k, Ci, (hipStream_t)stream))) return rc;
@@ -1113,12 +1111,10 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
   L.shift = (float*)shift;
   ConvCall c{0, &L, x, N, Hi, Wi, x_ld, y, y_ld, y_off, res, res_ld, relu, true};
   ConvArgs a = make_args(c);
-  const bool x3 = precision == 1 || precision == 2;
-  ConvPlan p = x3 ? plan_conv_x3(a.M, a.Co, a.K) : plan_conv(a.M, a.Co, a.K);
+  CWT_CHECK(precision == 0, "cwt_debug_conv runs the exact-fp32 conv only (bf16x3 plans: cwt_debug_conv_s)");
+  ConvPlan p = plan_conv(a.M, a.Co, a.K);
   if (bm > 0) {
-    CWT_CHECK((bm == 128 && (bn == 128 || bn == 64)) || (bm == 64 && bn == 64) ||
-                  (x3 && ((bm == 64 && bn == 128) || (bm == 256 && (bn == 256 || bn == 128)))),
-              "tile must be 128x128, 128x64, 64x64 (or 64x128, 256x256, 256x128 for bf16x3)");
+    CWT_CHECK((bm == 128 && (bn == 128 || bn == 64)) || (bm == 64 && bn == 64), "tile must be 128x128, 128x64 or 64x64");
     CWT_CHECK(Co % bn == 0, "Co % bn");
     p.bm = bm;
     p.bn = bn;
@@ -1131,19 +1127,7 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
   void* part = nullptr;
   size_t pf = (size_t)p.nsplit * a.M * a.Co;
   if (p.nsplit > 1 && (rc = ensure_ws(ctx, "dbg.PART", pf * 4, &part))) return rc;
-  if (!x3) return launch_conv(a, p, 0, (float*)part, pf, (hipStream_t)stream);
-  void *hi, *lo;
-  const long nw = (long)Co * a.K;
-  if (precision == 2) {  // w_packed already holds bf16 hi [Co][K] followed by lo [Co][K]
-    a.w_hi = (const __bf16*)w_packed;
-    a.w_lo = (const __bf16*)w_packed + nw;
-    return launch_conv_x3(a, p, 0, (float*)part, pf, (hipStream_t)stream);
-  }
-  if ((rc = ensure_ws(ctx, "dbg.whi", nw * 2, &hi)) || (rc = ensure_ws(ctx, "dbg.wlo", nw * 2, &lo))) return rc;
-  if ((rc = launch_split_bf16(w_packed, (__bf16*)hi, (__bf16*)lo, nw, (hipStream_t)stream))) return rc;
-  a.w_hi = (const __bf16*)hi;
-  a.w_lo = (const __bf16*)lo;
-  return launch_conv_x3(a, p, 0, (float*)part, pf, (hipStream_t)stream);
+  return launch_conv(a, p, 0, (float*)part, pf, (hipStream_t)stream);
 }
 
 }  // extern "C"

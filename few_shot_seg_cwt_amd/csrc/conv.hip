@@ -298,21 +298,5 @@ int launch_repack_cblock(const float* src, float* dst, int Co, int taps, int Ci,
   return 0;
 }
 
-__global__ void split_bf16_kernel(const float* __restrict__ w, __bf16* __restrict__ hi, __bf16* __restrict__ lo,
-                                  long n) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const float v = w[i];
-    const __bf16 h = (__bf16)v;
-    hi[i] = h;
-    lo[i] = (__bf16)(v - (float)h);
-  }
-}
-
-int launch_split_bf16(const float* w, __bf16* hi, __bf16* lo, long n, hipStream_t st) {
-  hipLaunchKernelGGL(split_bf16_kernel, dim3((unsigned)std::min<long>(4096, cdiv(n, 256))), dim3(256), 0, st, w, hi,
-                     lo, n);
-  CWT_LAUNCH_CHECK();
-  return 0;
-}
 
 }  // namespace cwt

@@ -1,15 +1,16 @@
-// Implicit-GEMM convolution on split activations ("x3s"): bf16x3 arithmetic (see
-// conv_x3.hip) with BOTH operands stored pre-split in HBM, so the main loop moves bytes
+// Implicit-GEMM convolution on split activations ("x3s"): bf16x3 arithmetic (every fp32
+// operand x = hi + lo with hi = bf16_rne(x), lo = bf16_rne(x - hi); a.b = a_lo.b_hi +
+// a_hi.b_lo + a_hi.b_hi, three bf16 MFMAs with fp32 accumulation, only a_lo.b_lo ~ 2^-16
+// dropped) with BOTH operands stored pre-split in HBM, so the main loop moves bytes
 // HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4) and never touches them in VGPRs.
 //
 // Split layout ("S-layout") of an activation map with C channels, and of the packed weights:
 //   [row][C/32][64 bf16]: per 32-channel block, 32 x hi = bf16_rne(v) then 32 x lo =
 //   bf16_rne(v - hi).  One 128-B line holds one block of one pixel (or of one output
 //   channel's K-slice for the weights, rows = Co, blocks in packed_k order).
-// hi + lo carries 16 significant bits; the bf16x3 conv of conv_x3.hip splits its fp32
-// input the same way while staging, so the MFMA inputs are bit-identical: storing the split
-// instead of fp32 changes only what residual adds and the byte kernels see (hi + lo, a
-// 2^-17 relative rounding of the fp32 value).  Same bytes as fp32 (4 B per element).
+// hi + lo carries 16 significant bits, which is all the bf16x3 MFMAs see of an fp32 operand
+// anyway: storing the split instead of fp32 changes only what residual adds and the byte
+// kernels see (hi + lo, a 2^-17 relative rounding of the fp32 value).  Same bytes as fp32.
 //
 // Main loop (one barrier per 32-deep K-tile, NSTG-deep LDS ring):
 //   wait own LDS-DMA of tile t (counted vmcnt, later tiles stay in flight) -> barrier ->

@@ -9,8 +9,6 @@ namespace cwt {
 struct ConvArgs {
   const float* x;      // NHWC input, pixel stride x_ld floats
   const float* w;      // packed [Co][K], K = kh*kw*Ci (tap-major)
-  const __bf16* w_hi;  // bf16x3 path: round-to-nearest bf16(w), same layout
-  const __bf16* w_lo;  // bf16x3 path: bf16(w - w_hi)
   const float* scale;  // [Co] folded BN scale
   const float* shift;  // [Co] folded BN shift
   const float* res;    // optional residual, NHWC, pixel stride res_ld
@@ -114,11 +112,6 @@ struct ConvPlan {
 ConvPlan plan_conv(int M, int Co, int K);
 int launch_conv(ConvArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats, hipStream_t st);
 int launch_splitk_epilogue(const ConvArgs& a, int nsplit, hipStream_t st);
-// bf16x3 variant (conv_x3.hip)
-ConvPlan plan_conv_x3(int M, int Co, int K);
-int launch_conv_x3(ConvArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,
-                   hipStream_t st);
-int launch_split_bf16(const float* w, __bf16* hi, __bf16* lo, long n, hipStream_t st);
 // split-activation variant (conv_x3s.hip)
 ConvPlan plan_conv_x3s(int M, int Co, int K);
 ConvPlan plan_conv_b16(int M, int Co, int K);

@@ -286,66 +286,6 @@ int cwt_sgd_step(cwt_ctx* ctx, float* param, const float* grad, float* momentum_
  * (SURVEY.md §8(d)).  Enabling (level > 0) clears the records; 0 stops recording.
  * cwt_profile_record waits for record i's stop event and returns its elapsed time.
  */
-/*
- * Test hook: one implicit-GEMM conv + folded BN (+residual) (+ReLU), NHWC, with the tile
- * (bm x bn in {128x128, 128x64, 64x64}, plus 64x128, 256x256, 256x128 for bf16x3; 0 =
- * automatic) and split-K count (0 = automatic) forced, so every plan can be checked against a
- * reference conv.  precision: 0 = fp32 MFMA, 1 = bf16x3 (hi/lo split, 3 bf16 MFMAs per
- * product), 2 = bf16x3 with w_packed already split and packed (bf16 hi [Co][K] then lo
- * [Co][K] in the library's K order, for timing the conv alone).  w_packed: device [Co][k][k][Ci]; scale/shift: device [Co]; res:
- * NHWC (pixel stride res_ld) or NULL.
- */
-int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, int x_ld,
-                   const float* w_packed, const float* scale, const float* shift, int Co, int k,
-                   int stride, int pad, int dil, const float* res, int res_ld, int relu, float* y,
-                   int y_ld, int y_off, int bm, int bn, int nsplit, int precision, void* stream);
-
-/*
- * Test hooks of the split-activation conv (conv_x3s.hip).  S-layout = [rows][C/32][64 bf16]:
- * per 32-channel block 32 x hi = bf16_rne(v) then 32 x lo = bf16_rne(v - hi).
- * cwt_debug_split_act: fp32 [P][C] (pixel stride ld) -> S-layout; cwt_debug_unsplit_act the
- * inverse (hi + lo).  cwt_debug_pack_wsplit: weights [Co][k][k][Ci] fp32 -> S-layout rows of
- * K = k*k*Ci in the library's K order.  cwt_debug_conv_s: one conv on S-layout input and
- * weights, folded BN, optional fp32 (res) or S-layout (res_s) residual, ReLU; writes fp32 NHWC
- * y (pixel stride y_ld, channel offset y_off) and/or S-layout ys; bm/bn/nsplit force the plan
- * (0 = automatic).
- */
-int cwt_debug_split_act(cwt_ctx* ctx, const float* x, int64_t P, int C, int ld, void* out, void* stream);
-int cwt_debug_unsplit_act(cwt_ctx* ctx, const void* s, int64_t P, int C, float* out, int ld, void* stream);
-int cwt_debug_pack_wsplit(cwt_ctx* ctx, const float* w, int Co, int k, int Ci, void* out, void* stream);
-int cwt_debug_conv_s(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws,
-                     const float* scale, const float* shift, int Co, int k, int stride, int pad,
-                     int dil, const float* res, int res_ld, const void* res_s, int relu, float* y,
-                     int y_ld, int y_off, void* ys, int bm, int bn, int nsplit, void* stream);
-/* The same conv on plain bf16 operands (the CWT_CONV_BF16 kernel): xs bf16 NHWC [N*Hi*Wi][Ci]
- * (Ci % 64 == 0), ws bf16 [Co][K] with K ordered (64-channel block, tap, channel in block),
- * res_s / ys bf16 NHWC [M][Co]. */
-int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws,
-                       const float* scale, const float* shift, int Co, int k, int stride, int pad,
-                       int dil, const float* res, int res_ld, const void* res_s, int relu, float* y,
-                       int y_ld, int y_off, void* ys, int bm, int bn, int nsplit, void* stream);
-
-/* Timing-study hook of the inner loop: with CWT_ADAPT_DBG=32 in the environment when the step
- * graph is built, each step workgroup's wave 0 records 9 clock stamps per step (s_memrealtime at
- * entry and exit, s_memtime at each phase boundary; tools/adapt_stamps.py).  Copies up to
- * max_count of them to host_out (may be NULL) and stores the number available in *count. */
-int cwt_debug_adapt_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t max_count, int64_t* count);
-
-/* Test hook: per workgroup of a 64-thread grid, the raw HW_REG_HW_ID and HW_REG_XCC_ID of the
- * CU it ran on (out[2*b], out[2*b+1]); with a CU-masked stream this maps mask bits to CUs. */
-int cwt_debug_census(cwt_ctx* ctx, int nblocks, unsigned* out, void* stream);
-
-/*
- * CU-partitioned streams (MI355X-native episode pipelining): a HIP stream
- * whose kernels (including replays of graphs launched on it) only run on the CUs whose bits
- * are set in mask (mask_words 32-bit words, bit i = CU i of the device).  Used to run one
- * episode's latency-bound inner loop on a small partition while the next episode's conv
- * stack runs on the rest.  cwt_cu_count returns the device's CU count.
- */
-int cwt_cu_count(cwt_ctx* ctx, int* count);
-int cwt_stream_create_masked(cwt_ctx* ctx, const uint32_t* mask, int mask_words, void** stream);
-int cwt_stream_destroy(void* stream);
-
 int cwt_profile_enable(cwt_ctx* ctx, int level);
 int cwt_profile_count(cwt_ctx* ctx);
 int cwt_profile_record(cwt_ctx* ctx, int i, char* name, int name_len, double* flops, double* bytes,

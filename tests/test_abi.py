@@ -1,5 +1,6 @@
-"""The C-ABI library loads and exports every symbol include/cwt.h declares (no GPU needed),
-and the ctypes prototypes cover exactly that set."""
+"""The C-ABI library loads and exports every symbol include/cwt.h (the drop-in boundary) and
+include/cwt_debug.h (test / measurement hooks) declare (no GPU needed), the ctypes prototypes
+cover exactly that set, and the boundary header holds no debug hook."""
 import os
 import re
 
@@ -10,10 +11,19 @@ from few_shot_seg_cwt_amd import _lib, build
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "cwt.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(cwt_[a-z0-9_]+)\s*\(", src)))
+def header_functions(names=("cwt.h", "cwt_debug.h")):
+    fns = set()
+    for n in names:
+        src = open(os.path.join(ROOT, "include", n)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        fns |= set(re.findall(r"\b(cwt_[a-z0-9_]+)\s*\(", src))
+    return sorted(fns)
+
+
+def test_boundary_header_has_no_debug_hooks():
+    boundary = header_functions(("cwt.h",))
+    assert not [f for f in boundary if f.startswith("cwt_debug_") or "masked" in f], boundary
+    assert set(header_functions(("cwt_debug.h",))).isdisjoint(boundary)
 
 
 @pytest.fixture(scope="module")
@@ -55,6 +65,7 @@ C_PROGRAM = r"""
 #include <stdio.h>
 #include <string.h>
 #include "cwt.h"
+#include "cwt_debug.h"
 int main(void) {
   const char* v = cwt_version();
   if (!v || !strstr(v, "gfx950")) return 2;
@@ -85,3 +96,13 @@ def test_header_is_plain_c_and_links(lib, tmp_path):
     env = dict(os.environ, LD_LIBRARY_PATH="/opt/rocm/lib:" + os.environ.get("LD_LIBRARY_PATH", ""))
     r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("ok"), (r.returncode, r.stdout, r.stderr)
+
+
+def test_library_provenance_is_the_tree(lib):
+    """The library's compiled-in source hash is the tree's (build.source_hash), and a library
+    whose hash differs is refused at load instead of being run (build provenance)."""
+    from few_shot_seg_cwt_amd import _lib as L
+    assert build.built_hash() == build.source_hash()
+    assert lib.cwt_version().decode().endswith("src=" + build.source_hash())
+    with pytest.raises(L.CwtError, match="stale"):
+        L.check_provenance("libcwt 0.2 (gfx950) src=0000000000000000", "libcwt.so")
