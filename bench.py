@@ -217,6 +217,9 @@ def main():
     ap.add_argument("--pool", type=int, default=4, help="distinct resident episodes cycled through")
     ap.add_argument("--inflight", type=int, default=1,
                     help="independent episodes processed together per step (EpisodeEngine.run_batch, <= 16)")
+    ap.add_argument("--pipeline", type=int, default=0, nargs="?", const=1,
+                    help="EpisodePipeline with this many extractor streams (0: off): episode i+1's extractor "
+                         "pass overlaps episode i's inner loop; each episode alone, same kernels")
     ap.add_argument("--conv-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="conv-stack arithmetic: fp32 (reference numerics) or bf16 (config #5)")
     ap.add_argument("--train", action="store_true",
@@ -250,7 +253,7 @@ def main():
 
     from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib, get_model
     from few_shot_seg_cwt_amd import synthetic as syn
-    from few_shot_seg_cwt_amd.episode import EpisodeEngine, TrainEngine
+    from few_shot_seg_cwt_amd.episode import EpisodeEngine, EpisodePipeline, TrainEngine
     from few_shot_seg_cwt_amd.optimizer import get_optimizer
 
     _lib.load_library()
@@ -264,6 +267,9 @@ def main():
     trans = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
     trans.load_state_dict(tsd)
     engine = EpisodeEngine(model, trans, cfg)
+    if args.pipeline and (args.train or args.inflight != 1):
+        raise SystemExit("--pipeline runs inference episodes one at a time")
+    pipe = EpisodePipeline(engine, extract_streams=args.pipeline) if args.pipeline else None
     if args.train and args.inflight != 1:
         raise SystemExit("--train runs one episode per rank per step (train.py batch_size 1)")
     if args.train:
@@ -295,12 +301,16 @@ def main():
             cdist.all_reduce_mean_(trans.flat.grad)
             opt.step()
             return r["loss"].view(1, 1, 1).expand(1, 2, 2)
+        if pipe is not None:
+            return pipe.submit(imgs, sl[0], ql, Wbuf[0])["iut"]
         if E == 1:
             return engine.run(imgs, sl[0], ql, Wbuf[0])["iut"]
         return engine.run_batch(imgs, sl, ql, Wbuf)["iut"]
 
     # warm-up runs exactly the timed loop's code (lazy kernel loading, graph capture, workspaces)
     warm_iut = [step(s, W0[s]) for s in range(args.warmup)]
+    if pipe is not None:
+        pipe.wait()
     torch.cat(warm_iut).sum(0)
     torch.cuda.synchronize()
 
@@ -309,6 +319,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     iuts = [step(s, W0[args.warmup + s]) for s in range(args.steps)]
+    if pipe is not None:
+        pipe.wait()
     torch.cuda.synchronize()
     cdist.barrier()
     t1 = time.perf_counter()
@@ -355,6 +367,8 @@ def main():
     # per-launch table from one extra (untimed) episode at profile level 2
     _lib.profile_enable(2)
     step(0, W0[0].clone())
+    if pipe is not None:
+        pipe.wait()
     torch.cuda.synchronize()
     fine = _lib.profile_records()
     _lib.profile_enable(0)
@@ -382,7 +396,10 @@ def main():
                                f"{'PASCAL split-0' if layers == 50 else 'COCO-20i split-0'} {shot}-shot "
                                f"ResNet-{layers} PSPNet {S}x{S}, adapt_iter 200, heads 4",
                    "image_size": S, "shot": shot, "layers": layers, "episodes_per_step_per_gpu": E,
-                   "parallelism": f"{world} episode-sharded replicas" + (f", {E} episodes in flight per GPU" if E > 1 else "")},
+                   "parallelism": f"{world} episode-sharded replicas" + (f", {E} episodes in flight per GPU" if E > 1 else "")
+                   + (f", episode pipeline ({args.pipeline} extractor stream(s) beside the inner-loop / CWT stream: "
+                      "episode i+1's extractor pass overlaps episode i's inner loop, each episode alone)"
+                      if pipe is not None else "")},
         "roofline": {"bound": "hbm", "kernel": (ad_kernel + ", ...> (the 200-step inner loop, test.py:164-187; "
                                                 "the time-dominant kernel of the episode)"),
                      "achieved": round(ad_achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",

@@ -125,20 +125,66 @@ def check(rc: int, what: str = ""):
         raise CwtError(f"{what} failed (code {rc}): {msg}")
 
 
+_override = threading.local()
+_extra_ctx = {}   # device -> [additional contexts] (workspace sets of concurrent streams)
+
+
+def _create_ctx(device: int):
+    p = C.c_void_p()
+    rc = load_library().cwt_ctx_create(device, C.byref(p))
+    if rc != 0:
+        raise CwtError(f"cwt_ctx_create failed: {_lib.cwt_last_error().decode()}")
+    return p
+
+
 def ctx(device: int | None = None):
-    """Per-device context (one per process per device)."""
+    """The calling thread's context for the device: the per-device default, or the one a
+    ``using_ctx`` block selected (a context owns the workspaces; calls on one context are
+    externally serialised, so concurrent streams each use a context of their own)."""
     if not torch.cuda.is_available():
         raise CwtError("libcwt needs a HIP device (torch.cuda.is_available() is False); no CPU fallback")
     if device is None:
         device = torch.cuda.current_device()
+    sel = getattr(_override, "ctx", None)
+    if sel is not None and sel[0] == device:
+        return sel[1]
     with _lock:
         if device not in _ctx:
-            p = C.c_void_p()
-            rc = load_library().cwt_ctx_create(device, C.byref(p))
-            if rc != 0:
-                raise CwtError(f"cwt_ctx_create failed: {_lib.cwt_last_error().decode()}")
-            _ctx[device] = p
+            _ctx[device] = _create_ctx(device)
         return _ctx[device]
+
+
+def new_ctx(device: int | None = None):
+    """An additional context on the device (its own workspace set), kept for the process."""
+    if device is None:
+        device = torch.cuda.current_device()
+    ctx(device)
+    with _lock:
+        p = _create_ctx(device)
+        _extra_ctx.setdefault(device, []).append(p)
+        return p
+
+
+class using_ctx:
+    """``with using_ctx(c): ...`` routes this thread's libcwt calls on c's device to context c."""
+
+    def __init__(self, c, device: int | None = None):
+        self.c, self.device = c, torch.cuda.current_device() if device is None else device
+
+    def __enter__(self):
+        self.prev = getattr(_override, "ctx", None)
+        _override.ctx = (self.device, self.c)
+        return self.c
+
+    def __exit__(self, *exc):
+        _override.ctx = self.prev
+        return False
+
+
+def all_ctx(device: int | None = None):
+    if device is None:
+        device = torch.cuda.current_device()
+    return [ctx(device)] + list(_extra_ctx.get(device, []))
 
 
 def stream_ptr(device=None) -> C.c_void_p:
@@ -162,19 +208,23 @@ def require(t: torch.Tensor, name: str, dtype=torch.float32, device=None):
 
 
 def profile_enable(level: int, device=None):
-    """0 off; 1 phases + bottleneck conv (cheap, for timed regions); 2 every launch."""
-    check(lib().cwt_profile_enable(ctx(device), int(level)), "cwt_profile_enable")
+    """0 off; 1 phases + bottleneck conv (cheap, for timed regions); 2 every launch.  Applies
+    to every context of the device."""
+    for c in all_ctx(device):
+        check(lib().cwt_profile_enable(c, int(level)), "cwt_profile_enable")
 
 
 def profile_records(device=None):
-    """[(name, flops, bytes, ms)] of the launches recorded since profile_enable(True)."""
-    c = ctx(device)
+    """[(name, flops, bytes, ms)] of the launches recorded since profile_enable, over every
+    context of the device (default context first)."""
     out = []
     buf = C.create_string_buffer(256)
     fl, by, ms = C.c_double(), C.c_double(), C.c_float()
-    for i in range(lib().cwt_profile_count(c)):
-        check(lib().cwt_profile_record(c, i, buf, 256, C.byref(fl), C.byref(by), C.byref(ms)), "cwt_profile_record")
-        out.append((buf.value.decode(), fl.value, by.value, ms.value))
+    for c in all_ctx(device):
+        for i in range(lib().cwt_profile_count(c)):
+            check(lib().cwt_profile_record(c, i, buf, 256, C.byref(fl), C.byref(by), C.byref(ms)),
+                  "cwt_profile_record")
+            out.append((buf.value.decode(), fl.value, by.value, ms.value))
     return out
 
 

@@ -745,18 +745,24 @@ __device__ __forceinline__ void pa_butterfly(float (&v)[PA_CPW], int lane) {
 // s_memtime at 8 points of every step, realtime at its arrival ([8]) and when its poll matched
 // ([9]) into stamps[step][g][10], and realtime/memtime at entry and exit into
 // stamps[iters][g][0..3] (tools/persist_stamps.py).
-template <int NRES, bool STAMPS = false>  // NRES 1: one unit per workgroup, resident in registers; 0: streamed
+// NRES 1: one unit per workgroup, its f in registers; 2: up to two units per workgroup, the
+// first in registers, the second in LDS (128 KB, lane-major: conflict-free); 0: units streamed
+// from L2 every step.  Fewer workgroups make each step's barrier cheaper and leave CUs to the
+// next episode's extractor pass (EpisodePipeline).
+template <int NRES, bool STAMPS = false>
 __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsigned long long* stamps = nullptr) {
   constexpr int C = 512;
-  __shared__ float wl[PA_EW][2][C];
-  __shared__ float dl[PA_EW][C];
+  constexpr int EWK = NRES == 2 ? 2 : PA_EW;  // LDS budget: the second unit's f takes 128 KB
+  __shared__ float wl[EWK][2][C];
+  __shared__ float dl[EWK][C];
+  __shared__ float fl2[NRES == 2 ? PA_NW : 1][PA_CPW][NRES == 2 ? 64 : 1];
   __shared__ float zpart[PA_NW][PA_NPX];
   __shared__ float zd[PA_NPX];
   __shared__ float gs[PA_NPX];
   __shared__ float P0[8][2][PA_NC + 1];
   __shared__ float P1[8][2][PA_NC + 1];
   __shared__ float dsum[C];
-  __shared__ float wfg_l[PA_EW], lr_l[PA_EW];
+  __shared__ float wfg_l[EWK], lr_l[EWK];
   __shared__ int abort_flag;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int g = blockIdx.x, G = a.G;
@@ -790,6 +796,18 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
   PaTile cur;
   PaUnit q = pa_unit(a, u0);
   pa_load(cur, a, q, wv, lane);
+  int y2[2][2] = {{255, 255}, {255, 255}};  // NRES 2: labels of the second unit (its f is in fl2)
+  if (NRES == 2 && u1 - u0 > 1) {
+    PaTile tmp;
+    pa_load(tmp, a, pa_unit(a, u0 + 1), wv, lane);
+#pragma unroll
+    for (int j = 0; j < PA_CPW; ++j) fl2[wv][j][lane] = tmp.fr[j];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      y2[k][0] = tmp.y[k][0];
+      y2[k][1] = tmp.y[k][1];
+    }
+  }
   __syncthreads();
 
   const int i_row = wv >> 1;
@@ -809,13 +827,8 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
                            __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    for (int u = u0; u < u1; ++u) {
-      if (NRES == 0 && u != u0) {  // streamed: this unit's f and labels (the first one was prefetched)
-        q = pa_unit(a, u);
-        pa_load(cur, a, q, wv, lane);
-      } else if (NRES == 0) {
-        q = pa_unit(a, u);
-      }
+    // one unit's z / hi-res / dW passes; fget(j): f of lane p's pixel, channel 32*wv + j
+    auto unit_body = [&](const PaUnit& q, int u, auto fget, const int (&ylab)[2][2]) {
       const int ew = q.e - e_lo;
       // ---- z = d . f: this wave's 32-channel partial for lane p's pixel ----
       {
@@ -823,10 +836,10 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
 #pragma unroll
         for (int j = 0; j < PA_CPW / 4; ++j) {
           const f32x4 d4 = *(const f32x4*)&dl[ew][wv * PA_CPW + 4 * j];
-          sdot = fmaf(d4[0], cur.fr[4 * j], sdot);
-          sdot = fmaf(d4[1], cur.fr[4 * j + 1], sdot);
-          sdot = fmaf(d4[2], cur.fr[4 * j + 2], sdot);
-          sdot = fmaf(d4[3], cur.fr[4 * j + 3], sdot);
+          sdot = fmaf(d4[0], fget(4 * j), sdot);
+          sdot = fmaf(d4[1], fget(4 * j + 1), sdot);
+          sdot = fmaf(d4[2], fget(4 * j + 2), sdot);
+          sdot = fmaf(d4[3], fget(4 * j + 3), sdot);
         }
         zpart[wv][lane] = sdot;
       }
@@ -856,7 +869,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
 #pragma unroll
           for (int e2 = 0; e2 < 2; ++e2) {
             if (e2 == 1 && !has_extra) break;  // wave-uniform: only the last row pair's row-0 waves
-            const int y = cur.y[k][e2];
+            const int y = ylab[k][e2];
             float gv = 0.f;
             if (y != 255) {
               const float dd = e2 ? (lx0 * zd[PA_NC + xi0] + lx1 * zd[PA_NC + xi1])
@@ -897,13 +910,26 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
         float accd[PA_CPW];
         const float gp = gs[lane];
 #pragma unroll
-        for (int j = 0; j < PA_CPW; ++j) accd[j] = gp * cur.fr[j];
+        for (int j = 0; j < PA_CPW; ++j) accd[j] = gp * fget(j);
         pa_butterfly(accd, lane);  // lane L: channel (L >> 1) of the wave's slice, summed over 64 lanes
         if ((lane & 1) == 0)
           __hip_atomic_fetch_add(a.acc + (long)q.e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
                                      wv * PA_CPW + (lane >> 1),
                                  accd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+    };
+    for (int u = u0; u < u1; ++u) {
+      if (NRES == 2 && u != u0) {
+        unit_body(pa_unit(a, u), u, [&](int jj) { return fl2[wv][jj][lane]; }, y2);
+        continue;
+      }
+      if (NRES == 0 && u != u0) {  // streamed: this unit's f and labels (the first one was prefetched)
+        q = pa_unit(a, u);
+        pa_load(cur, a, q, wv, lane);
+      } else if (NRES == 0) {
+        q = pa_unit(a, u);
+      }
+      unit_body(q, u, [&](int jj) { return cur.fr[jj]; }, cur.y);
     }
     stamp(3);
     // ---- grid barrier s ----
@@ -1006,16 +1032,22 @@ static int persist_geometry(int E, int n, int h, int w, int* G_out, int* units_o
   const int ncb = cdiv(w - 1, uc);
   const int ntile = (h - 1) * ncb;
   const long units = (long)E * n * ntile;
-  const int G = (int)std::min<long>(units, g_cu_count);
+  // units per workgroup: 1 (f in registers) or 2 (the second unit's f in LDS): half the
+  // workgroups, a cheaper barrier, and CUs left for the next episode's extractor (CWT_ADAPT_UPW)
+  // (default: 1 while that takes at most half the CUs -- 1-shot 473^2: 118 -- else 2)
+  const char* upws = getenv("CWT_ADAPT_UPW");
+  const int upw = upws ? (atoi(upws) == 1 ? 1 : 2) : (units <= g_cu_count / 2 ? 1 : 2);
+  const int G = (int)std::min<long>((units + upw - 1) / upw, g_cu_count);
   const long k = (units + G - 1) / G;  // units per workgroup (max)
   const long per_ep = (long)n * ntile;
   const long span = (k - 1 + per_ep - 1) / per_ep + 1;  // episodes a workgroup's range can touch
-  if (span > PA_EW) return 1;
+  const int nres = k == 1 ? 1 : (k == 2 && span <= 2) ? 2 : 0;
+  if (span > (nres == 2 ? 2 : PA_EW)) return 1;
   *G_out = G;
   *units_out = (int)units;
   *ncb_out = ncb;
   *uc_out = uc;
-  *nres_out = (units <= G) ? 1 : 0;
+  *nres_out = nres;
   // streamed units (multi-shot) are not yet faster than the step launches: opt in only
   const char* pe = getenv("CWT_ADAPT_PERSIST");
   if (!*nres_out && !(pe && pe[0] == '2')) return 1;
@@ -1055,12 +1087,16 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
       CWT_HIP(hipMalloc(&g_adapt_stamps, n_st * sizeof(unsigned long long)));
       g_adapt_stamps_n = n_st;
     }
-    if (nres)
+    if (nres == 1)
       hipLaunchKernelGGL((adapt_persist_kernel<1, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
+    else if (nres == 2)
+      hipLaunchKernelGGL((adapt_persist_kernel<2, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
     else
       hipLaunchKernelGGL((adapt_persist_kernel<0, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
-  } else if (nres) {
+  } else if (nres == 1) {
     hipLaunchKernelGGL((adapt_persist_kernel<1, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
+  } else if (nres == 2) {
+    hipLaunchKernelGGL((adapt_persist_kernel<2, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
   } else {
     hipLaunchKernelGGL((adapt_persist_kernel<0, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
   }

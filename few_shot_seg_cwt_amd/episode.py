@@ -168,6 +168,67 @@ class EpisodeEngine:
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, f_s=f_s, f_q=f_q)
 
 
+class EpisodePipeline:
+    """Consecutive independent episodes on two HIP streams: the extractor pass of episode i+1
+    runs while episode i's inner loop (one persistent launch on ~118 of the 256 CUs, the rest
+    idle) and its CWT / classifier / metrics run.  Every episode executes exactly the kernels
+    ``EpisodeEngine.run`` launches, with the same inputs, so its outputs are the same (up to the
+    order of the inner loop's fp32 atomic adds); only their placement in time changes.  Each
+    episode is still processed alone (batch_size_val = 1): nothing is batched across episodes.
+
+    Stream use: the extractor's workspaces are only touched by the extract stream, the inner
+    loop's / CWT's by the adapt stream.  ``submit`` returns the episode's result tensors, valid
+    on the adapt stream (``wait`` makes the current stream wait for them)."""
+
+    def __init__(self, engine: "EpisodeEngine", extract_streams: int = 1):
+        """extract_streams > 1: consecutive episodes' extractor passes also overlap each other,
+        round-robin over that many streams, each with its own libcwt context (workspaces)."""
+        self.eng = engine
+        self.s_ext = [torch.cuda.Stream() for _ in range(max(1, int(extract_streams)))]
+        self.c_ext = [None] + [_lib.new_ctx() for _ in range(len(self.s_ext) - 1)]
+        self.s_extract = self.s_ext[0]
+        self.s_adapt = torch.cuda.Stream()
+        self.k = 0
+
+    @torch.no_grad()
+    def submit(self, imgs: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor, W0: torch.Tensor) -> dict:
+        eng = self.eng
+        cur = torch.cuda.current_stream()
+        shot = imgs.shape[0] - 1
+        i = self.k % len(self.s_ext)
+        self.k += 1
+        s_ex = self.s_ext[i]
+        s_ex.wait_stream(cur)   # inputs were produced on the caller's stream
+        self.s_adapt.wait_stream(cur)
+        with torch.cuda.stream(s_ex):
+            if self.c_ext[i] is None:
+                f_all, _ = eng.model.extract_features(imgs)
+            else:
+                with _lib.using_ctx(self.c_ext[i]):
+                    f_all, _ = eng.model.extract_features(imgs)
+            done = torch.cuda.Event()
+            done.record(s_ex)
+        with torch.cuda.stream(self.s_adapt):
+            self.s_adapt.wait_event(done)
+            for t in (f_all, imgs, s_label, q_label, W0):
+                t.record_stream(self.s_adapt)
+            f_s, f_q = f_all[:shot], f_all[shot:]
+            W = inner_adapt(f_s, s_label, W0, eng.lr, eng.iters)
+            Wb = W.view(1, 2, -1)
+            fqn, pred_q0 = normalize(f_q, Wb)
+            W2 = eng.transformer.infer(Wb, fqn)
+            pred_q = classify(W2, fqn)
+            iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
+        return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce)
+
+    def wait(self):
+        """Make the caller's current stream wait for everything submitted so far."""
+        cur = torch.cuda.current_stream()
+        for s in self.s_ext:
+            cur.wait_stream(s)
+        cur.wait_stream(self.s_adapt)
+
+
 class TrainEngine:
     """Device-resident CWT training episode (train.py:188-267 without the host-side batch
     transfer): the backbone and inner loop as in inference, then CWT forward with saved

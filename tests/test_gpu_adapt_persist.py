@@ -27,10 +27,11 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def _run(persist, f, lbl, W0, iters, uc=None):
-    """persist: "0" per-step launches, "2" the persistent loop also where units are streamed."""
+def _run(persist, f, lbl, W0, iters, uc=None, upw=None):
+    """persist: "0" per-step launches, "2" the persistent loop also where units are streamed;
+    upw: units per workgroup ("1": f in registers; "2", the default: the second unit in LDS)."""
     from few_shot_seg_cwt_amd.episode import inner_adapt_batch
-    env = {"CWT_ADAPT_PERSIST": persist, "CWT_ADAPT_UC": uc}
+    env = {"CWT_ADAPT_PERSIST": persist, "CWT_ADAPT_UC": uc, "CWT_ADAPT_UPW": upw}
     old = {k: os.environ.get(k) for k in env}
     for k, v in env.items():
         if v is None:
@@ -60,15 +61,16 @@ def _run(persist, f, lbl, W0, iters, uc=None):
     (3, 2, 65, 20, None),
     (2, 1, 33, 5, None),
 ])
-def test_persist_equals_step_launches(dev, E, n, S, iters, uc):
+@pytest.mark.parametrize("upw", ["1", "2"])
+def test_persist_equals_step_launches(dev, E, n, S, iters, uc, upw):
     h = (S - 1) // 8 + 1
     f = torch.from_numpy(syn.normal(5, f"fp{E}{n}{S}", (E * n, 512, h, h), 0.1)).to(dev)
     f = f.contiguous(memory_format=torch.channels_last)
     lbl = torch.stack([torch.from_numpy(syn.make_episode(SEED, 70 + e, S, n)["s_label"][0]) for e in range(E)]).to(dev)
     W0 = torch.from_numpy(syn.normal(6, f"wp{E}{n}{S}", (E, 2, 512), 0.04)).to(dev)
-    Wp = _run("2", f, lbl, W0, iters, uc)
+    Wp = _run("2", f, lbl, W0, iters, uc, upw)
     Ws = _run("0", f, lbl, W0, iters)
     errs = [rel(Wp[e], Ws[e]) for e in range(E)]
-    print(f"E={E} n={n} S={S} iters={iters}: max rel {max(errs):.3e}")
+    print(f"E={E} n={n} S={S} iters={iters} upw={upw}: max rel {max(errs):.3e}")
     assert max(errs) < 1e-4, errs
     assert torch.isfinite(Wp).all()

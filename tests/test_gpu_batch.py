@@ -68,3 +68,33 @@ def test_run_batch_equals_run(dev, E):
         assert rel(rb["pred_q"][e], r["pred_q"][0]) < TOL_RUN
         assert rel(rb["pred_q0"][e], r["pred_q0"][0]) < TOL_RUN
         assert float((rb["iut"][e] - r["iut"][0]).abs().max()) <= 2
+
+
+@pytest.mark.parametrize("streams", [1, 2])
+def test_pipeline_equals_run(dev, streams):
+    """EpisodePipeline (extractor of episode i+1 on one stream beside episode i's inner loop and
+    CWT on another) gives every episode what EpisodeEngine.run gives it alone."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, get_model
+    from few_shot_seg_cwt_amd.episode import EpisodeEngine, EpisodePipeline
+    S, shot, n = 129, 1, 4
+    cfg = syn.cfg_defaults(image_size=S)
+    m = get_model(cfg).load_state_dict(syn.make_pspnet_state(50, SEED))
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    eng = EpisodeEngine(m, t, cfg)
+    pipe = EpisodePipeline(eng, extract_streams=streams)
+    eps = [syn.make_episode(SEED, 80 + e, S, shot) for e in range(n)]
+    W0 = torch.from_numpy(syn.normal(8, "wpl", (n, 2, 512), 0.04)).to(dev)
+    ins = []
+    for ep in eps:
+        imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
+        ins.append((imgs, torch.from_numpy(ep["s_label"][0]).to(dev), torch.from_numpy(ep["q_label"]).to(dev)))
+    outs = [pipe.submit(i, s, q, W0[e].clone()) for e, (i, s, q) in enumerate(ins)]
+    pipe.wait()
+    torch.cuda.synchronize()
+    for e, (i, s, q) in enumerate(ins):
+        r = eng.run(i, s, q, W0[e].clone())
+        torch.cuda.synchronize()
+        assert rel(outs[e]["W"], r["W"]) < TOL, e
+        assert rel(outs[e]["pred_q"], r["pred_q"]) < TOL_RUN, e
+        assert torch.equal(outs[e]["iut0"], r["iut0"]), e
