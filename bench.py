@@ -217,9 +217,10 @@ def main():
     ap.add_argument("--pool", type=int, default=4, help="distinct resident episodes cycled through")
     ap.add_argument("--inflight", type=int, default=1,
                     help="independent episodes processed together per step (EpisodeEngine.run_batch, <= 16)")
-    ap.add_argument("--pipeline", type=int, default=0, nargs="?", const=1,
-                    help="EpisodePipeline with this many extractor streams (0: off): episode i+1's extractor "
-                         "pass overlaps episode i's inner loop; each episode alone, same kernels")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="EpisodePipeline with this many extractor streams (0: one episode after the other): the "
+                         "next episodes' extractor passes overlap the current episode's inner loop; every "
+                         "episode is still processed alone (batch 1), by the same kernels")
     ap.add_argument("--conv-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="conv-stack arithmetic: fp32 (reference numerics) or bf16 (config #5)")
     ap.add_argument("--train", action="store_true",
@@ -267,8 +268,8 @@ def main():
     trans = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
     trans.load_state_dict(tsd)
     engine = EpisodeEngine(model, trans, cfg)
-    if args.pipeline and (args.train or args.inflight != 1):
-        raise SystemExit("--pipeline runs inference episodes one at a time")
+    if args.inflight != 1:
+        args.pipeline = 0   # the batched throughput mode runs its E episodes in one pass
     pipe = EpisodePipeline(engine, extract_streams=args.pipeline) if args.pipeline else None
     if args.train and args.inflight != 1:
         raise SystemExit("--train runs one episode per rank per step (train.py batch_size 1)")
@@ -296,10 +297,15 @@ def main():
     def step(i: int, Wbuf):
         imgs, sl, ql = pool[i % len(pool)]
         if args.train:   # do_epoch iteration (train.py:188-267 + the all-reduce point of SURVEY §8(e))
-            trans.flat.grad.zero_() if trans.flat.grad is not None else None
-            r = tengine.step(imgs, sl[0], ql, Wbuf[0])
-            cdist.all_reduce_mean_(trans.flat.grad)
-            opt.step()
+            def after():
+                cdist.all_reduce_mean_(trans.flat.grad)
+                opt.step()
+                trans.flat.grad.zero_()
+            if pipe is not None:
+                r = pipe.submit_train(tengine, imgs, sl[0], ql, Wbuf[0], after)
+            else:
+                r = tengine.step(imgs, sl[0], ql, Wbuf[0])
+                after()
             return r["loss"].view(1, 1, 1).expand(1, 2, 2)
         if pipe is not None:
             return pipe.submit(imgs, sl[0], ql, Wbuf[0])["iut"]
@@ -327,6 +333,20 @@ def main():
     _lib.profile_enable(0)
     dt = cdist.all_reduce_max_scalar(t1 - t0)
     value = world * args.steps * E / dt
+    seq = None
+    if pipe is not None:   # the same episodes one after the other on one stream (no overlap), same run
+        pipe_saved, pipe = pipe, None
+        cdist.barrier()
+        torch.cuda.synchronize()
+        ts0 = time.perf_counter()
+        seq_out = [step(s, W0[args.warmup + s]) for s in range(args.steps)]
+        torch.cuda.synchronize()
+        cdist.barrier()
+        dts = cdist.all_reduce_max_scalar(time.perf_counter() - ts0)
+        seq = {"value": round(world * args.steps / dts, 3), "ms_per_step": round(dts / args.steps * 1e3, 3),
+               "note": "the same K steps one episode after the other on one stream (--pipeline 0)"}
+        del seq_out
+        pipe = pipe_saved
     recs = _lib.profile_records()
     iu = torch.cat(iuts).sum(0)
 
@@ -438,6 +458,7 @@ def main():
                           "gflop_reference_formulation_per_step": round(reference_cwt_flops(h_feat * h_feat) * E / 1e9, 2),
                           "note": "executed in the declared re-associated form (DESIGN.md §3, ~59 MFLOP of token work)"}},
         "iou_fg_timed": None if args.train else round(float((iu[0, 1] / iu[1, 1].clamp_min(1)).item()), 4),
+        "sequential": seq,
     }
     if rank == 0 and args.profile_json:
         with open(args.profile_json, "w") as f:

@@ -219,7 +219,40 @@ class EpisodePipeline:
             W2 = eng.transformer.infer(Wb, fqn)
             pred_q = classify(W2, fqn)
             iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
-        return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce)
+            done_all = torch.cuda.Event()
+            done_all.record(self.s_adapt)
+        return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, done=done_all)
+
+    def submit_train(self, tengine: "TrainEngine", imgs: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor,
+                     W0: torch.Tensor, after=None) -> dict:
+        """A training episode (train.py:188-267): the extractor pass on an extractor stream, then
+        on the adapt stream the inner loop, CWT forward, query CE and the CWT backward into
+        transformer.flat.grad, then ``after()`` (the caller's gradient all-reduce and optimiser
+        step) -- so the CWT parameter updates stay in episode order while the next episode's
+        extractor pass and inner loop (which do not read them) already run."""
+        cur = torch.cuda.current_stream()
+        shot = imgs.shape[0] - 1
+        i = self.k % len(self.s_ext)
+        self.k += 1
+        s_ex = self.s_ext[i]
+        s_ex.wait_stream(cur)
+        self.s_adapt.wait_stream(cur)
+        with torch.no_grad(), torch.cuda.stream(s_ex):
+            if self.c_ext[i] is None:
+                f_all, _ = tengine.model.extract_features(imgs)
+            else:
+                with _lib.using_ctx(self.c_ext[i]):
+                    f_all, _ = tengine.model.extract_features(imgs)
+            done = torch.cuda.Event()
+            done.record(s_ex)
+        with torch.cuda.stream(self.s_adapt):
+            self.s_adapt.wait_event(done)
+            for t in (f_all, imgs, s_label, q_label, W0):
+                t.record_stream(self.s_adapt)
+            r = tengine.step_from_features(f_all[:shot], f_all[shot:], s_label, q_label, W0)
+            if after is not None:
+                after()
+        return r
 
     def wait(self):
         """Make the caller's current stream wait for everything submitted so far."""
@@ -243,12 +276,16 @@ class TrainEngine:
 
     def step(self, imgs: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor, W0: torch.Tensor) -> dict:
         shot = imgs.shape[0] - 1
+        with torch.no_grad():
+            f_all, _ = self.model.extract_features(imgs)
+        return self.step_from_features(f_all[:shot], f_all[shot:], s_label, q_label, W0)
+
+    def step_from_features(self, f_s: torch.Tensor, f_q: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor,
+                           W0: torch.Tensor) -> dict:
         t = self.transformer
         if t.flat.grad is None:
             t.flat.grad = torch.zeros_like(t.flat)
         with torch.no_grad():
-            f_all, _ = self.model.extract_features(imgs)
-            f_s, f_q = f_all[:shot], f_all[shot:]
             W = inner_adapt(f_s, s_label, W0, self.lr, self.iters)
             Wb = W.view(1, 2, -1)
             fqn, pred_q0 = normalize(f_q, Wb)
@@ -329,7 +366,10 @@ def validate_transformer(args, val_loader, model, transformer, episodes_out: lis
     """Mirror of the reference's validate_transformer for batch_size_val = 1.  Returns
     (mean mIoU over runs, mean loss).  With torch.distributed initialised, rank r runs the
     episodes e with e % world == r and the per-class intersection/union sums are all-reduced
-    once at the end of each run."""
+    once at the end of each run.  Episodes run through an
+    EpisodePipeline (``args.pipeline`` extractor streams, default 2; 0 = strictly one after the
+    other); each is still computed alone and read back in order.  The runtime printed is the
+    run's wall time (test.py:252 sums per-episode times, which overlap here)."""
     if int(_a(args, "batch_size_val", 1)) != 1:
         raise NotImplementedError("batch_size_val must be 1 (scripts/test.sh)")
     model.eval()
@@ -343,34 +383,49 @@ def validate_transformer(args, val_loader, model, transformer, episodes_out: lis
     val_IoUs = np.zeros(n_runs)
     val_losses = np.zeros(n_runs)
     it = iter(val_loader)
+    # EpisodePipeline (args.pipeline extractor streams, 0 = one episode after the other): the
+    # next episode is submitted before this one's results are read back (same results, same
+    # accumulation order)
+    n_pipe = int(_a(args, "pipeline", 2))
+    pipe = EpisodePipeline(engine, extract_streams=n_pipe) if n_pipe > 0 else None
     for run in range(n_runs):
         loss_meter = AverageMeter()
-        runtime = 0.0
+        t_run = time.time()
         cls_iu = defaultdict(lambda: np.zeros(2))
         cls_iu0 = defaultdict(lambda: np.zeros(2))
-        for e in range(nb_episodes):
-            qry_img, q_label, spprt_imgs, s_label, subcls, _, _ = it.next() if hasattr(it, "next") else next(it)
-            W0 = new_binary_classifier_weight()          # consumes the torch RNG like test.py:164
-            new_binary_classifier_weight()               # ... and like Pseudo_cls (test.py:200)
-            if e % world != rank:
-                continue
-            t0 = time.time()
-            _class_weight_check(s_label)
-            imgs = torch.cat([spprt_imgs[0], qry_img], 0).to(dev, non_blocking=True)
-            sl = s_label[0].to(dev, non_blocking=True)
-            ql = q_label.to(dev, non_blocking=True)
-            r = engine.run(imgs, sl, ql, W0.to(dev))
+        pending = []
+
+        def finish(r, subcls):
+            if "done" in r:
+                torch.cuda.current_stream().wait_event(r["done"])
             iut = r["iut"].cpu().numpy()[0]
             iut0 = r["iut0"].cpu().numpy()[0]
             ce = r["ce"].cpu().numpy()[0]
-            runtime += time.time() - t0
             loss_meter.update(float(ce[0] / max(ce[1], 1.0)))
             for c in [int(x.item()) for x in subcls]:
                 cls_iu[c] += (iut[0, 1], iut[1, 1])       # FG only (test.py:227-228)
                 cls_iu0[c] += (iut0[0, 1], iut0[1, 1])
             if episodes_out is not None:
                 episodes_out.append({k: (v.detach().cpu() if isinstance(v, torch.Tensor) else v)
-                                     for k, v in r.items() if k not in ("f_s", "f_q")})
+                                     for k, v in r.items() if k not in ("f_s", "f_q", "done")})
+
+        for e in range(nb_episodes):
+            qry_img, q_label, spprt_imgs, s_label, subcls, _, _ = it.next() if hasattr(it, "next") else next(it)
+            W0 = new_binary_classifier_weight()          # consumes the torch RNG like test.py:164
+            new_binary_classifier_weight()               # ... and like Pseudo_cls (test.py:200)
+            if e % world != rank:
+                continue
+            _class_weight_check(s_label)
+            imgs = torch.cat([spprt_imgs[0], qry_img], 0).to(dev, non_blocking=True)
+            sl = s_label[0].to(dev, non_blocking=True)
+            ql = q_label.to(dev, non_blocking=True)
+            r = pipe.submit(imgs, sl, ql, W0.to(dev)) if pipe is not None else engine.run(imgs, sl, ql, W0.to(dev))
+            pending.append((r, subcls))
+            if len(pending) > (1 if pipe is not None else 0):
+                finish(*pending.pop(0))
+        while pending:
+            finish(*pending.pop(0))
+        runtime = time.time() - t_run
         classes = sorted(set(cls_iu) | set(cls_iu0))
         if world > 1:
             classes = cdist.union_keys(classes)
