@@ -54,6 +54,9 @@ SIGNATURES = {
     "cwt_seg_ce_fwd_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "cwt_classify_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_iou_preds": (_I, [_P, _P, _P, _I64, _I, _I, _P, _P]),
+    "cwt_cos_classify": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P]),
+    "cwt_cos_classify_bwd": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "cwt_corr": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "cwt_sgd_step": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _I, _I, _P]),
     "cwt_cu_count": (_I, [_P, _P]),
     "cwt_stream_create_masked": (_I, [_P, _P, _I, _P]),

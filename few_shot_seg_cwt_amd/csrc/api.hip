@@ -40,6 +40,16 @@ int launch_seg_ce(const float* logits, const int64_t* target, int B, int h, int 
 int launch_normalize(const float* f, int B, int Pb, float* out, const float* W0, float* logits0, hipStream_t st);
 int launch_classify(const float* W, const float* f, int B, int Pb, float* logits, hipStream_t st);
 int launch_classify_bwd(const float* dl, const float* f, int B, int Pb, float* dW, hipStream_t st);
+// variant heads (heads.hip)
+int launch_cos_weight(float* v, const float* g, int n, int C, int mode, float* w_eff, float* vnorm, hipStream_t st);
+int launch_cos_cls_fwd(const float* x, long P, int B, int n, const float* w_eff, const float* bias, const float* scale,
+                       float* out, hipStream_t st);
+int cos_cls_bwd_blocks(long total);
+int launch_cos_cls_bwd(const float* x, long P, int B, int n, const float* w_eff, const float* bias, const float* scale,
+                       const float* G, float* part, float* part_s, int mode, const float* v, const float* g,
+                       const float* vnorm, float* dv, float* dg, float* db, float* dscale, hipStream_t st);
+int launch_corr(const float* q, const float* k, int B, int Pq, int Pk, int C, float* qn, float* kn, float* sim,
+                hipStream_t st);
 int launch_seg_metrics(const float* logits, const int64_t* target, int B, int h, int w, int S, float* iut,
                        double* ce, unsigned* counts_ws, hipStream_t st, const float* logits2 = nullptr,
                        float* iut2 = nullptr);
@@ -1042,6 +1052,55 @@ int cwt_classify_bwd(cwt_ctx* ctx, const float* dlogits, const float* f, int B, 
   CWT_CHECK(dlogits && f && dW && C == 512 && B >= 1 && P >= 1, "bad arguments");
   CWT_HIP(hipSetDevice(ctx->device));
   return launch_classify_bwd(dlogits, f, B, P, dW, (hipStream_t)stream);
+}
+
+int cwt_cos_classify(cwt_ctx* ctx, const float* x, int B, int P, int C, int n, float* weight, const float* g,
+                     const float* bias, const float* scale, int mode, float* out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && weight && scale && out && C == 512 && B >= 1 && P >= 1, "bad arguments");
+  CWT_CHECK(n >= 1 && n <= 64, "n_classes must be in [1, 64]");
+  CWT_CHECK(mode >= 0 && mode <= 3 && (!(mode & 1) || g), "mode: bit 0 WeightNorm (needs g), bit 1 weight_norm");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void *weff, *vn;
+  int rc;
+  if ((rc = ensure_ws(ctx, "heads.weff", (size_t)n * C * 4, &weff)) || (rc = ensure_ws(ctx, "heads.vnorm", 64 * 4, &vn)))
+    return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = launch_cos_weight(weight, g, n, C, mode, (float*)weff, (float*)vn, st))) return rc;
+  return launch_cos_cls_fwd(x, P, B, n, (const float*)weff, bias, scale, out, st);
+}
+
+int cwt_cos_classify_bwd(cwt_ctx* ctx, const float* x, int B, int P, int C, int n, float* weight, const float* g,
+                         const float* bias, const float* scale, int mode, const float* dscores, float* d_weight,
+                         float* d_g, float* d_bias, float* d_scale, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && weight && scale && dscores && d_weight && C == 512 && B >= 1 && P >= 1, "bad arguments");
+  CWT_CHECK(n >= 1 && n <= 64, "n_classes must be in [1, 64]");
+  CWT_CHECK(mode >= 0 && mode <= 3 && (!(mode & 1) || (g && d_g)), "mode: bit 0 WeightNorm (needs g, d_g)");
+  CWT_HIP(hipSetDevice(ctx->device));
+  const int nb = cos_cls_bwd_blocks((long)B * P);
+  void *weff, *vn, *part, *parts;
+  int rc;
+  if ((rc = ensure_ws(ctx, "heads.weff", (size_t)n * C * 4, &weff)) || (rc = ensure_ws(ctx, "heads.vnorm", 64 * 4, &vn)) ||
+      (rc = ensure_ws(ctx, "heads.part", (size_t)nb * n * C * 4, &part)) ||
+      (rc = ensure_ws(ctx, "heads.parts", (size_t)nb * n * 2 * 4, &parts)))
+    return rc;
+  hipStream_t st = (hipStream_t)stream;
+  // the forward's weight (for weight_norm the stored weight is already normalised: idempotent)
+  if ((rc = launch_cos_weight(weight, g, n, C, mode, (float*)weff, (float*)vn, st))) return rc;
+  return launch_cos_cls_bwd(x, P, B, n, (const float*)weff, bias, scale, dscores, (float*)part, (float*)parts, mode,
+                            weight, g, (const float*)vn, d_weight, d_g, d_bias, d_scale, st);
+}
+
+int cwt_corr(cwt_ctx* ctx, const float* q, const float* k, int B, int Pq, int Pk, int C, float* sim, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(q && k && sim && B >= 1 && Pq >= 1 && Pk >= 1 && C >= 4 && C % 4 == 0, "bad arguments (C % 4 == 0)");
+  CWT_HIP(hipSetDevice(ctx->device));
+  void *qn, *kn;
+  int rc;
+  if ((rc = ensure_ws(ctx, "corr.q", (size_t)B * Pq * C * 4, &qn)) || (rc = ensure_ws(ctx, "corr.k", (size_t)B * Pk * C * 4, &kn)))
+    return rc;
+  return launch_corr(q, k, B, Pq, Pk, C, (float*)qn, (float*)kn, sim, (hipStream_t)stream);
 }
 
 int cwt_seg_metrics(cwt_ctx* ctx, const float* logits, const int64_t* target, int B, int h, int w, int S,

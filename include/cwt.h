@@ -268,6 +268,35 @@ int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int
 int cwt_classify_bwd(cwt_ctx* ctx, const float* dlogits, const float* f, int B, int P, int C,
                      float* dW, void* stream);
 
+/*
+ * Variant heads on the same features.
+ *
+ * CosCls.forward (src/model/pspnet.py:290-309, cls_type parsed by parse_param_coscls :318-324):
+ * x device [B, P, C] (NHWC tokens, C = 512); weight device [n, C] (the stored cls.weight, or
+ * cls.weight_v under WeightNorm), g device [n] (cls.weight_g, WeightNorm only), bias device
+ * [n] or NULL, scale device [1] (scale_factor: the constant 2.0 or the learnable parameter);
+ * mode bit 0 = WeightNorm ('r': W = g v / ||v||), bit 1 = weight_norm ('n': rows of the stored
+ * weight normalised in place with eps 1e-5 before use -- no effect under WeightNorm, whose
+ * pre-forward hook recomputes the weight, as in the reference).  out device [B, n, P]:
+ * scale * (W . x / max(||x||, 1e-5) + bias).  n <= 64.
+ * cwt_cos_classify_bwd: the gradients of sum(dscores * out) w.r.t. the head's parameters:
+ * d_weight [n, C] (w.r.t. weight_v under WeightNorm), d_g [n] (WeightNorm), d_bias [n] (may be
+ * NULL), d_scale [1] (may be NULL); written, not accumulated; fixed-order sums.
+ */
+int cwt_cos_classify(cwt_ctx* ctx, const float* x, int B, int P, int C, int n, float* weight,
+                     const float* g, const float* bias, const float* scale, int mode, float* out,
+                     void* stream);
+int cwt_cos_classify_bwd(cwt_ctx* ctx, const float* x, int B, int P, int C, int n, float* weight,
+                         const float* g, const float* bias, const float* scale, int mode,
+                         const float* dscores, float* d_weight, float* d_g, float* d_bias,
+                         float* d_scale, void* stream);
+
+/* get_corr (src/model/model_util.py:101-109; the MMN / MatchNet correlation, mmn.py:57):
+ * q device [B, Pq, C], k device [B, Pk, C] (NHWC tokens); sim device [B, Pq, Pk] =
+ * normalize(q) . normalize(k)^T per token (eps 1e-12), exact fp32 (fp32 MFMA). */
+int cwt_corr(cwt_ctx* ctx, const float* q, const float* k, int B, int Pq, int Pk, int C, float* sim,
+             void* stream);
+
 /* torch.optim.SGD(momentum, dampening 0, weight_decay, nesterov) step over one flat
  * fp32 parameter buffer (optimizer.py:8-15): buf = m*buf + (g + wd*p) (buf = g+wd*p on
  * the first step, first_step != 0); p -= lr * (nesterov ? g + wd*p + m*buf : buf). */

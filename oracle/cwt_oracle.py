@@ -232,3 +232,27 @@ def sgd_nesterov(params: dict, grads: dict, bufs: dict, lr: float, momentum: flo
         nb[k] = b
         out[k] = p - lr * (g + momentum * b)
     return out, nb
+
+
+# ---------------------------------------------------------------- variant heads (§8(f) rank 4)
+def cos_cls(x, weight, g=None, bias=None, scale=2.0, weight_norm_r=False, weight_norm=False):
+    """CosCls.forward (pspnet.py:300-309): x [B, C, h, w]; weight [n, C, 1, 1] (weight_v under
+    WeightNorm, pspnet.py:294-295, W = g v / ||v|| per output channel, torch._weight_norm dim 0);
+    weight_norm: the stored weight normalised (eps 1e-5) before use -- under WeightNorm the
+    pre-forward hook recomputes the weight from (g, v) afterwards, so it has no effect there.
+    Returns (scores [B, n, h, w], the weight the conv used)."""
+    if weight_norm_r:
+        v = weight
+        w = v * (g / v.flatten(1).norm(dim=1).view(-1, 1, 1, 1))
+    else:
+        w = F.normalize(weight, p=2, dim=1, eps=1e-5) if weight_norm else weight
+    x_norm = F.normalize(x, p=2, dim=1, eps=1e-5)
+    return scale * F.conv2d(x_norm, w, bias), w
+
+
+def get_corr(q, k):
+    """model_util.py:101-109: cosine similarity of every (q token, k token) pair."""
+    bs, ch, h, w = q.shape
+    pq = F.normalize(q.view(bs, ch, h * w).permute(0, 2, 1), dim=-1)
+    pk = F.normalize(k.view(bs, -1, k.shape[2] * k.shape[3]), dim=-2)
+    return torch.bmm(pq, pk)

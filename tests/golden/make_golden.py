@@ -20,6 +20,10 @@ Captured:
                                (model.train() at train.py:184), Dropout2d p = 0
   bn_train_small.npz           PSPNet.extract_features in train mode at S=33 (batch statistics,
                                running-statistic update, Dropout2d p = 0), then eval on the query
+  variants_small.npz           CosCls (every cls_type flag, n = 2 / 16: output, parameter gradients,
+                               parameters after the forward) and get_corr (small + 60x60 samples)
+  episode_coco_r101_5shot.npz  validate_transformer 5-shot R101@641 (BASELINE config #5's shapes)
+  train_coco_r101_1shot.npz    do_epoch COCO R101@641 (BASELINE config #4), dropout off, BN eval
 """
 from __future__ import annotations
 
@@ -354,11 +358,54 @@ def run_bn_train(rutil, rpsp):
     print("bn_train_small.npz written")
 
 
+COS_TYPES = ["0000", "0n00", "00b0", "000t", "r000", "rnbt", "0nbt", "r0b0"]
+
+
+def run_variants(rpsp):
+    """CosCls (pspnet.py:290-313) for every cls_type flag combination at n = 2 and 16: output,
+    the gradients of sum(G * out) w.r.t. its parameters, and the parameters after the forward
+    (weight_norm rewrites the stored weight); get_corr (model_util.py:101-109) at a small size
+    and at 60 x 60 (samples + checksums)."""
+    import src.model.model_util as rmu
+    out = {}
+    x = torch.from_numpy(syn.normal(SEED, "cosx", (2, 512, 5, 7), 1.0))
+    for ct in COS_TYPES:
+        for n in (2, 16):
+            m = rpsp.CosCls(512, n, ct)
+            tag = f"cos_{ct}_{n}"
+            with torch.no_grad():
+                for name, prm in m.named_parameters():
+                    if name == "cls.weight_g":
+                        prm.copy_(torch.from_numpy(syn.uniform(SEED, tag + name, tuple(prm.shape), 0.5, 1.5)))
+                    elif name == "scale_factor":
+                        prm.fill_(1.7)
+                    else:
+                        prm.copy_(torch.from_numpy(syn.normal(SEED, tag + name, tuple(prm.shape), 0.05)))
+            y = m(x)
+            G = torch.from_numpy(syn.normal(SEED, tag + "G", tuple(y.shape), 1.0))
+            (y * G).sum().backward()
+            out[f"{tag}_out"] = y.detach().numpy()
+            for name, prm in m.named_parameters():   # inputs are regenerated from the same streams
+                out[f"{tag}_grad_{name}"] = prm.grad.detach().numpy().copy()
+                if ct[1] == "n" and name == "cls.weight":   # rewritten in place by the forward
+                    out[f"{tag}_after_{name}"] = prm.detach().numpy().copy()
+    q = torch.from_numpy(syn.normal(SEED, "corrq", (2, 512, 5, 7), 1.0))
+    k = torch.from_numpy(syn.normal(SEED, "corrk", (2, 512, 5, 7), 1.0))
+    out["corr_small"] = rmu.get_corr(q, k).numpy()
+    q = torch.from_numpy(syn.normal(SEED, "corrQ", (1, 512, 60, 60), 1.0)).abs()
+    k = torch.from_numpy(syn.normal(SEED, "corrK", (1, 512, 60, 60), 1.0)).abs()
+    sim = rmu.get_corr(q, k)
+    out["corr60_stat"] = stat(sim)
+    out["corr60_sample"] = sim.numpy().reshape(-1)[::9973].copy()
+    np.savez_compressed(os.path.join(HERE, "variants_small.npz"), **out)
+    print("variants_small.npz written")
+
+
 def main():
     torch.set_num_threads(8)
     rtest, rtrain, rutil, rpsp, rtr = import_reference()
     which = sys.argv[1:] or ["modules", "pascal1", "pascal5", "coco1", "coco5", "train", "train_coco", "bn_train",
-                             "train_bnq"]
+                             "train_bnq", "variants"]
     if "modules" in which:
         run_modules(rutil, rpsp, rtr)
     if "pascal1" in which:
@@ -380,6 +427,8 @@ def main():
         run_bn_train(rutil, rpsp)
     if "train_bnq" in which:
         run_train(rtrain, rutil, rpsp, rtr, "train_pascal_r50_1shot_bnq.npz", 2, bn_quirk=True)
+    if "variants" in which:
+        run_variants(rpsp)
 
 
 if __name__ == "__main__":

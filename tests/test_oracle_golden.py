@@ -154,3 +154,63 @@ def test_train_step_grads_coco_r101(golden_dir, tsd4):
     assert abs(loss.item() - float(g["e0_loss_q"])) < 1e-4 * abs(float(g["e0_loss_q"]))
     for n, gr in grads.items():
         assert rel(gr.numpy().reshape(-1)[::101], g[f"e0_grad_{n}_sample"]) < 1e-3, n
+
+
+COS_TYPES = ["0000", "0n00", "00b0", "000t", "r000", "rnbt", "0nbt", "r0b0"]
+
+
+def cos_params(ct, n):
+    """The deterministic CosCls parameters make_golden.py set (same PRNG streams)."""
+    tag = f"cos_{ct}_{n}"
+    wn_r, _, has_b, temp = ct[0] == "r", ct[1] == "n", ct[2] == "b", ct[3] == "t"
+    p = {}
+    if wn_r:
+        p["cls.weight_g"] = torch.from_numpy(syn.uniform(SEED, tag + "cls.weight_g", (n, 1, 1, 1), 0.5, 1.5))
+        p["cls.weight_v"] = torch.from_numpy(syn.normal(SEED, tag + "cls.weight_v", (n, 512, 1, 1), 0.05))
+    else:
+        p["cls.weight"] = torch.from_numpy(syn.normal(SEED, tag + "cls.weight", (n, 512, 1, 1), 0.05))
+    if has_b:
+        p["cls.bias"] = torch.from_numpy(syn.normal(SEED, tag + "cls.bias", (n,), 0.05))
+    if temp:
+        p["scale_factor"] = torch.tensor(1.7)
+    return p
+
+
+@pytest.mark.parametrize("ct", COS_TYPES)
+@pytest.mark.parametrize("n", [2, 16])
+def test_cos_cls_oracle(golden_dir, ct, n):
+    """oracle.cos_cls (and its autograd) against the reference CosCls (variants_small.npz)."""
+    g = dict(np.load(os.path.join(golden_dir, "variants_small.npz")))
+    tag = f"cos_{ct}_{n}"
+    p = {k: v.clone().requires_grad_(True) for k, v in cos_params(ct, n).items()}
+    x = torch.from_numpy(syn.normal(SEED, "cosx", (2, 512, 5, 7), 1.0))
+    wkey = "cls.weight_v" if ct[0] == "r" else "cls.weight"
+    y, w_used = O.cos_cls(x, p[wkey], p.get("cls.weight_g"), p.get("cls.bias"), p.get("scale_factor", 2.0),
+                          weight_norm_r=ct[0] == "r", weight_norm=ct[1] == "n")
+    assert rel(y.detach().numpy(), g[f"{tag}_out"]) < 1e-5
+    G = torch.from_numpy(syn.normal(SEED, tag + "G", tuple(y.shape), 1.0))
+    grads = torch.autograd.grad((y * G).sum(), list(p.values()))
+    for (name, _), gr in zip(p.items(), grads):
+        ref = g[f"{tag}_grad_{name}"]
+        if ct[1] == "n" and ct[0] != "r" and name == "cls.weight":
+            continue   # the reference's gradient is w.r.t. the normalised tensor it stored (checked below)
+        assert rel(gr.numpy(), ref) < 1e-4, name
+    if ct[1] == "n" and ct[0] != "r":
+        assert rel(w_used.detach().numpy(), g[f"{tag}_after_cls.weight"]) < 1e-6
+        # the gradient lands on the stored (normalised) weight: dL/dW_used
+        w2 = w_used.detach().clone().requires_grad_(True)
+        y2, _ = O.cos_cls(x, w2, None, p.get("cls.bias"), p.get("scale_factor", 2.0))
+        (gw,) = torch.autograd.grad((y2 * G).sum(), [w2])
+        assert rel(gw.numpy(), g[f"{tag}_grad_cls.weight"]) < 1e-4
+
+
+def test_get_corr_oracle(golden_dir):
+    g = dict(np.load(os.path.join(golden_dir, "variants_small.npz")))
+    q = torch.from_numpy(syn.normal(SEED, "corrq", (2, 512, 5, 7), 1.0))
+    k = torch.from_numpy(syn.normal(SEED, "corrk", (2, 512, 5, 7), 1.0))
+    assert rel(O.get_corr(q, k).numpy(), g["corr_small"]) < 1e-6
+    q = torch.from_numpy(syn.normal(SEED, "corrQ", (1, 512, 60, 60), 1.0)).abs()
+    k = torch.from_numpy(syn.normal(SEED, "corrK", (1, 512, 60, 60), 1.0)).abs()
+    sim = O.get_corr(q, k)
+    assert rel(sim.numpy().reshape(-1)[::9973], g["corr60_sample"]) < 1e-5
+    np.testing.assert_allclose(np.array([sim.double().sum().item()]), g["corr60_stat"][:1], rtol=1e-6)
