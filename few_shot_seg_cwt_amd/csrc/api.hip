@@ -1284,12 +1284,20 @@ static int debug_conv_s(cwt_ctx* ctx, int prec, const void* xs, int N, int Hi, i
   a.K = k * k * Ci;
   ConvPlan p = prec == 1 ? plan_conv_b16(a.M, a.Co, a.K) : plan_conv_x3s(a.M, a.Co, a.K);
   if (bm > 0) {
+    const int var = bm / 1000;  // bm = 1000 * variant + rows (cwt_debug.h)
+    bm %= 1000;
     CWT_CHECK((bm == 256 && (bn == 256 || bn == 128)) || (bm == 128 && (bn == 256 || bn == 128 || bn == 64)) ||
                   (bm == 64 && (bn == 128 || bn == 64)),
               "tile must be one of 256x256, 256x128, 128x256, 128x128, 128x64, 64x128, 64x64");
+    CWT_CHECK((var >= 0 && var <= 2) || (var == 4 && bm == 128 && bn == 128) || (var >= 8 && var <= 11),
+              "variant must be 0, 1, 2, 4 (128x128 only) or 8 .. 11 (timing study)");
+    if (var >= 8) {  // the timing-study kernels have fixed tiles: the grid must be theirs
+      bm = bn = var < 10 ? 64 : 128;
+    }
     CWT_CHECK(Co % bn == 0, "Co % bn");
     p.bm = bm;
     p.bn = bn;
+    p.var = var;
   }
   if (nsplit > 0) {
     const int kt = a.K / kb;

@@ -51,7 +51,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// vmcnt(n * LPT) for a runtime n in [0, 3]
+// vmcnt(n * LPT) for a runtime n in [0, 5]
 template <int LPT>
 __device__ __forceinline__ void wait_tiles(int n) {
   if (n <= 0)
@@ -60,8 +60,12 @@ __device__ __forceinline__ void wait_tiles(int n) {
     wait_vmcnt<LPT>();
   else if (n == 2)
     wait_vmcnt<2 * LPT>();
-  else
+  else if (n == 3)
     wait_vmcnt<3 * LPT>();
+  else if (n == 4)
+    wait_vmcnt<4 * LPT>();
+  else
+    wait_vmcnt<5 * LPT>();
 }
 
 __device__ __forceinline__ void block_sync_lds() {
@@ -140,7 +144,12 @@ __device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, co
   }
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC>
+// PF = 0: fragments of tile t are read after the barrier that publishes it, then its MFMAs.
+// PF = 1: fragments of tile t+1 are read (into a second register set) right after the barrier
+// that publishes it, BEFORE the MFMAs of tile t, so their LDS latency hides under the MFMAs;
+// the slot tile t occupied is refilled (tile t + NSTG) as soon as every wave has passed that
+// barrier, so the ring keeps NSTG - 1 tiles in flight either way.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF = 0>
 __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   static_assert(PREC == 1 || PREC == 3, "PREC: 3 = bf16x3 over the S-layout, 1 = plain bf16");
   constexpr int NW = WAVES_M * WAVES_N;
@@ -150,7 +159,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   constexpr int LPT = LA + LB;
   constexpr int STG_BYTES = (BM + BN) * 128;
   static_assert(LA * 8 * NW == BM && LB * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
-  static_assert(NSTG >= 2 && NSTG <= 5, "ring depth");
+  static_assert(NSTG >= 2 && NSTG <= 6, "ring depth");
   constexpr int EP_ROWS = WM < 32 ? WM : 32;
   constexpr int EP_LD = WN + 4;  // floats per row of a wave's epilogue tile
   constexpr int EP_BYTES = NW * EP_ROWS * EP_LD * 4;
@@ -211,6 +220,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   }
   int i_kt = kt_begin;
   auto issue = [&](int stg) {
+    if (PF & 4) return;  // timing study: no operand traffic
     char* sb = smem + stg * STG_BYTES;
     const int dy = i_ky * a.dil, dx = i_kx * a.dil;
     const int shift = dy * a.Wi + dx;
@@ -265,6 +275,13 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
     }
   };
   auto mfmas = [&](const Frags& F) {
+    if (PF & 2) {  // timing study: no MFMAs (keep the fragments live)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(F.ah[i]), "v"(F.al[i]));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(F.bh[j]), "v"(F.bl[j]));
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -280,17 +297,45 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       }
   };
 
+  if ((PF & 1) == 0) {
 #pragma unroll
-  for (int s = 0; s < NSTG - 1; ++s)
-    if (s < T) issue(s);
+    for (int s = 0; s < NSTG - 1; ++s)
+      if (s < T) issue(s);
 
-  for (int t = 0; t < T; ++t) {
-    wait_tiles<LPT>(min(NSTG - 2, T - 1 - t));
-    block_sync_lds();
-    if (t + NSTG - 1 < T) issue((t + NSTG - 1) % NSTG);
-    Frags F;
-    read_frags(F, t % NSTG);
-    mfmas(F);
+    for (int t = 0; t < T; ++t) {
+      wait_tiles<LPT>(min(NSTG - 2, T - 1 - t));
+      block_sync_lds();
+      if (t + NSTG - 1 < T) issue((t + NSTG - 1) % NSTG);
+      Frags F;
+      read_frags(F, t % NSTG);
+      mfmas(F);
+    }
+  } else {
+    // prologue: tiles 0 .. NSTG-1 fill every slot; tile 0's fragments
+#pragma unroll
+    for (int s = 0; s < NSTG; ++s)
+      if (s < T) issue(s);
+    Frags F0, F1;
+    if (T > 0) {
+      wait_tiles<LPT>(min(NSTG - 1, T - 1));
+      block_sync_lds();
+      read_frags(F0, 0);
+    }
+    // step t: publish tile t+1 (issued: min(T, NSTG + t) tiles, so min(T-t-2, NSTG-2) may stay
+    // in flight), refill tile t's slot with tile t+NSTG, read tile t+1's fragments, MFMAs of t
+    auto step = [&](int t, Frags& cur, Frags& nxt) {
+      if (t + 1 < T) {
+        wait_tiles<LPT>(min(T - t - 2, NSTG - 2));
+        block_sync_lds();
+        if (t + NSTG < T) issue(t % NSTG);
+        read_frags(nxt, (t + 1) % NSTG);
+      }
+      mfmas(cur);
+    };
+    for (int t = 0; t < T; t += 2) {
+      step(t, F0, F1);
+      if (t + 1 < T) step(t + 1, F1, F0);
+    }
   }
 
   // ---- epilogue through a per-wave LDS tile ----
@@ -357,13 +402,13 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
 }
 
 // STAGE only names the instantiation (rocprofv3 reports the conv stack by stage).
-template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArgs a) {
-  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 3>(a);
+  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 3, PF>(a);
 }
-template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_b16(ConvSArgs a) {
-  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 1>(a);
+  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 1, PF>(a);
 }
 
 // Split-K reduction (fixed order, deterministic) + the same epilogue math.
@@ -460,44 +505,56 @@ int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipSt
   return 0;
 }
 
-template <int STAGE>
-static void launch_tiles_x3s(const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
-  if (p.bm == 256 && p.bn == 256)
-    hipLaunchKernelGGL((conv_igemm_x3s<256, 256, 2, 4, 2, STAGE>), grid, dim3(512), 0, st, a);
-  else if (p.bm == 256 && p.bn == 128)
-    hipLaunchKernelGGL((conv_igemm_x3s<256, 128, 4, 2, 3, STAGE>), grid, dim3(512), 0, st, a);
-  else if (p.bm == 128 && p.bn == 256)
-    hipLaunchKernelGGL((conv_igemm_x3s<128, 256, 2, 4, 3, STAGE>), grid, dim3(512), 0, st, a);
-  else if (p.bm == 128 && p.bn == 128)
-    hipLaunchKernelGGL((conv_igemm_x3s<128, 128, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
-  else if (p.bm == 128 && p.bn == 64)
-    hipLaunchKernelGGL((conv_igemm_x3s<128, 64, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
-  else if (p.bm == 64 && p.bn == 128)
-    hipLaunchKernelGGL((conv_igemm_x3s<64, 128, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_igemm_x3s<64, 64, 2, 2, 4, STAGE>), grid, dim3(256), 0, st, a);
-}
-
-template <int STAGE>
-static void launch_tiles_b16(const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
-  if (p.bm == 256 && p.bn == 256)
-    hipLaunchKernelGGL((conv_igemm_b16<256, 256, 2, 4, 2, STAGE>), grid, dim3(512), 0, st, a);
-  else if (p.bm == 256 && p.bn == 128)
-    hipLaunchKernelGGL((conv_igemm_b16<256, 128, 4, 2, 3, STAGE>), grid, dim3(512), 0, st, a);
-  else if (p.bm == 128 && p.bn == 256)
-    hipLaunchKernelGGL((conv_igemm_b16<128, 256, 2, 4, 3, STAGE>), grid, dim3(512), 0, st, a);
-  else if (p.bm == 128 && p.bn == 128)
-    hipLaunchKernelGGL((conv_igemm_b16<128, 128, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
-  else if (p.bm == 128 && p.bn == 64)
-    hipLaunchKernelGGL((conv_igemm_b16<128, 64, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
-  else if (p.bm == 64 && p.bn == 128)
-    hipLaunchKernelGGL((conv_igemm_b16<64, 128, 2, 2, 3, STAGE>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_igemm_b16<64, 64, 2, 2, 4, STAGE>), grid, dim3(256), 0, st, a);
-}
+// plan.var: 0 = the base loop; 1 = fragment prefetch (PF), same waves; 2 = PF with 8 waves
+// (two per SIMD) on the 128- and 64-row tiles; 4 = 128x128 with a 2-stage ring (64 KB: two
+// workgroups per CU).  Deeper rings (one workgroup per CU, 4-5 tiles in flight) measured no
+// faster: a workgroup's LDS-DMA intake, not its bytes in flight, is the limit.  256x256 has no PF form: its second fragment
+// set does not fit the 256 VGPRs of a wave at two waves per SIMD.
+#define CWT_TILE_LAUNCH(KERNEL)                                                                                  \
+  template <int STAGE>                                                                                       \
+  static void launch_tiles_##KERNEL(const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {      \
+    const int v = p.var;                                                                                     \
+    if (v >= 8) { /* timing study (cwt_debug_conv_s only): 8/9 base 64x64 w/o MFMA / w/o DMA,            */ \
+      /* 10/11 the 8-wave prefetch 128x128 w/o MFMA / w/o DMA                                              */ \
+      if (v == 8) hipLaunchKernelGGL((KERNEL<64, 64, 2, 2, 4, 0, 2>), grid, dim3(256), 0, st, a);           \
+      else if (v == 9) hipLaunchKernelGGL((KERNEL<64, 64, 2, 2, 4, 0, 4>), grid, dim3(256), 0, st, a);      \
+      else if (v == 10) hipLaunchKernelGGL((KERNEL<128, 128, 2, 4, 3, 0, 3>), grid, dim3(512), 0, st, a);   \
+      else hipLaunchKernelGGL((KERNEL<128, 128, 2, 4, 3, 0, 5>), grid, dim3(512), 0, st, a);                \
+      return;                                                                                                \
+    }                                                                                                        \
+    if (p.bm == 256 && p.bn == 256) {                                                                        \
+      hipLaunchKernelGGL((KERNEL<256, 256, 2, 4, 2, STAGE, 0>), grid, dim3(512), 0, st, a); /* PF: no VGPRs */ \
+    } else if (p.bm == 256 && p.bn == 128) {                                                                 \
+      if (v) hipLaunchKernelGGL((KERNEL<256, 128, 4, 2, 3, STAGE, 1>), grid, dim3(512), 0, st, a);           \
+      else hipLaunchKernelGGL((KERNEL<256, 128, 4, 2, 3, STAGE, 0>), grid, dim3(512), 0, st, a);             \
+    } else if (p.bm == 128 && p.bn == 256) {                                                                 \
+      if (v) hipLaunchKernelGGL((KERNEL<128, 256, 2, 4, 3, STAGE, 1>), grid, dim3(512), 0, st, a);           \
+      else hipLaunchKernelGGL((KERNEL<128, 256, 2, 4, 3, STAGE, 0>), grid, dim3(512), 0, st, a);             \
+    } else if (p.bm == 128 && p.bn == 128) {                                                                 \
+      if (v == 4) hipLaunchKernelGGL((KERNEL<128, 128, 2, 2, 2, STAGE, 0>), grid, dim3(256), 0, st, a);      \
+      else if (v == 2) hipLaunchKernelGGL((KERNEL<128, 128, 2, 4, 3, STAGE, 1>), grid, dim3(512), 0, st, a); \
+      else if (v) hipLaunchKernelGGL((KERNEL<128, 128, 2, 2, 3, STAGE, 1>), grid, dim3(256), 0, st, a);      \
+      else hipLaunchKernelGGL((KERNEL<128, 128, 2, 2, 3, STAGE, 0>), grid, dim3(256), 0, st, a);             \
+    } else if (p.bm == 128 && p.bn == 64) {                                                                  \
+      if (v == 2) hipLaunchKernelGGL((KERNEL<128, 64, 4, 2, 3, STAGE, 1>), grid, dim3(512), 0, st, a);  \
+      else if (v) hipLaunchKernelGGL((KERNEL<128, 64, 2, 2, 3, STAGE, 1>), grid, dim3(256), 0, st, a);       \
+      else hipLaunchKernelGGL((KERNEL<128, 64, 2, 2, 3, STAGE, 0>), grid, dim3(256), 0, st, a);              \
+    } else if (p.bm == 64 && p.bn == 128) {                                                                  \
+      if (v == 2) hipLaunchKernelGGL((KERNEL<64, 128, 2, 4, 3, STAGE, 1>), grid, dim3(512), 0, st, a);  \
+      else if (v) hipLaunchKernelGGL((KERNEL<64, 128, 2, 2, 3, STAGE, 1>), grid, dim3(256), 0, st, a);       \
+      else hipLaunchKernelGGL((KERNEL<64, 128, 2, 2, 3, STAGE, 0>), grid, dim3(256), 0, st, a);              \
+    } else {                                                                                                 \
+      if (v == 2) hipLaunchKernelGGL((KERNEL<64, 64, 2, 4, 4, STAGE, 1>), grid, dim3(512), 0, st, a);   \
+      else if (v) hipLaunchKernelGGL((KERNEL<64, 64, 2, 2, 4, STAGE, 1>), grid, dim3(256), 0, st, a);        \
+      else hipLaunchKernelGGL((KERNEL<64, 64, 2, 2, 4, STAGE, 0>), grid, dim3(256), 0, st, a);               \
+    }                                                                                                        \
+  }
+CWT_TILE_LAUNCH(conv_igemm_x3s)
+CWT_TILE_LAUNCH(conv_igemm_b16)
+#undef CWT_TILE_LAUNCH
 
 struct MeasuredPlanS {
-  int M, Co, K, bm, bn, nsplit;
+  int M, Co, K, bm, bn, nsplit, var;  // var: main-loop variant (launch_tiles_*; 0 where a line omits it)
 };
 static const MeasuredPlanS kMeasuredPlansS[] = {
 #include "conv_plans_x3s.inc"
@@ -534,6 +591,7 @@ ConvPlan plan_conv_x3s(int M, int Co, int K) {
       ConvPlan p;
       p.bm = e.bm;
       p.bn = e.bn;
+      p.var = e.var;
       p.kt_per_split = cdiv(ktiles, e.nsplit);
       p.nsplit = cdiv(ktiles, p.kt_per_split);
       return p;
@@ -554,6 +612,7 @@ ConvPlan plan_conv_b16(int M, int Co, int K) {
       ConvPlan p;
       p.bm = e.bm;
       p.bn = e.bn;
+      p.var = e.var;
       p.kt_per_split = cdiv(ktiles, e.nsplit);
       p.nsplit = cdiv(ktiles, p.kt_per_split);
       return p;
@@ -599,23 +658,23 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
   dim3 grid(cdiv(a.M, p.bm), a.Co / p.bn, nsplit);
   if (prec == 1) {
     switch (stage) {
-      case 0: launch_tiles_b16<0>(main, p, grid, st); break;
-      case 1: launch_tiles_b16<1>(main, p, grid, st); break;
-      case 2: launch_tiles_b16<2>(main, p, grid, st); break;
-      case 3: launch_tiles_b16<3>(main, p, grid, st); break;
-      case 4: launch_tiles_b16<4>(main, p, grid, st); break;
-      case 5: launch_tiles_b16<5>(main, p, grid, st); break;
-      default: launch_tiles_b16<6>(main, p, grid, st); break;
+      case 0: launch_tiles_conv_igemm_b16<0>(main, p, grid, st); break;
+      case 1: launch_tiles_conv_igemm_b16<1>(main, p, grid, st); break;
+      case 2: launch_tiles_conv_igemm_b16<2>(main, p, grid, st); break;
+      case 3: launch_tiles_conv_igemm_b16<3>(main, p, grid, st); break;
+      case 4: launch_tiles_conv_igemm_b16<4>(main, p, grid, st); break;
+      case 5: launch_tiles_conv_igemm_b16<5>(main, p, grid, st); break;
+      default: launch_tiles_conv_igemm_b16<6>(main, p, grid, st); break;
     }
   } else {
     switch (stage) {
-      case 0: launch_tiles_x3s<0>(main, p, grid, st); break;
-      case 1: launch_tiles_x3s<1>(main, p, grid, st); break;
-      case 2: launch_tiles_x3s<2>(main, p, grid, st); break;
-      case 3: launch_tiles_x3s<3>(main, p, grid, st); break;
-      case 4: launch_tiles_x3s<4>(main, p, grid, st); break;
-      case 5: launch_tiles_x3s<5>(main, p, grid, st); break;
-      default: launch_tiles_x3s<6>(main, p, grid, st); break;
+      case 0: launch_tiles_conv_igemm_x3s<0>(main, p, grid, st); break;
+      case 1: launch_tiles_conv_igemm_x3s<1>(main, p, grid, st); break;
+      case 2: launch_tiles_conv_igemm_x3s<2>(main, p, grid, st); break;
+      case 3: launch_tiles_conv_igemm_x3s<3>(main, p, grid, st); break;
+      case 4: launch_tiles_conv_igemm_x3s<4>(main, p, grid, st); break;
+      case 5: launch_tiles_conv_igemm_x3s<5>(main, p, grid, st); break;
+      default: launch_tiles_conv_igemm_x3s<6>(main, p, grid, st); break;
     }
   }
   CWT_LAUNCH_CHECK();

@@ -107,6 +107,7 @@ __device__ __forceinline__ void conv_store_fragment(const ConvArgs& a, const f32
 
 struct ConvPlan {
   int bm = 128, bn = 128, kt_per_split = 1, nsplit = 1;
+  int var = 0;  // S-layout convs: 0 base main loop, 1 fragment prefetch, 2 prefetch with 8 waves (conv_x3s.hip)
 };
 
 ConvPlan plan_conv(int M, int Co, int K);

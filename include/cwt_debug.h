@@ -34,7 +34,9 @@ int cwt_debug_conv(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, 
  * K = k*k*Ci in the library's K order.  cwt_debug_conv_s: one conv on S-layout input and
  * weights, folded BN, optional fp32 (res) or S-layout (res_s) residual, ReLU; writes fp32 NHWC
  * y (pixel stride y_ld, channel offset y_off) and/or S-layout ys; bm/bn/nsplit force the plan
- * (0 = automatic).
+ * (0 = automatic); bm = 1000 * variant + rows also forces the main-loop variant (0 base,
+ * 1 fragment prefetch, 2 prefetch with 8 waves, 4 = 128x128 with a 2-stage ring; 8 .. 11 timing
+ * study: 64x64 without MFMAs / without operand loads, 128x128 8-wave prefetch the same).
  */
 int cwt_debug_split_act(cwt_ctx* ctx, const float* x, int64_t P, int C, int ld, void* out, void* stream);
 int cwt_debug_unsplit_act(cwt_ctx* ctx, const void* s, int64_t P, int C, float* out, int ld, void* stream);

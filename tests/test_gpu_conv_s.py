@@ -88,7 +88,12 @@ CASES = [  # N, Ci, Co, Hi, k, stride, dil, residual
     (1, 64, 512, 19, 3, 1, 1, True),
 ]
 PLANS = [(0, 0, 0), (256, 256, 1), (256, 128, 1), (128, 256, 1), (128, 256, 2), (128, 128, 1), (128, 64, 1), (64, 128, 1), (64, 64, 1),
-         (64, 64, 3), (128, 128, 2), (256, 256, 4)]
+         (64, 64, 3), (128, 128, 2), (256, 256, 4),
+         # main-loop variants (bm = 1000 * variant + rows): 1 fragment prefetch, 2 prefetch with 8 waves,
+         # 4 = 128x128 with a 2-stage ring
+         (1064, 64, 1), (1064, 64, 3), (1128, 128, 1), (1128, 64, 2), (1064, 128, 1), (1128, 256, 1), (1256, 128, 2),
+         (2064, 64, 1), (2064, 64, 2), (2128, 128, 1), (2128, 128, 3), (2128, 64, 1), (2064, 128, 1),
+         (4128, 128, 1), (4128, 128, 3)]
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))

@@ -1,8 +1,8 @@
-"""Time the split-activation conv (conv_x3s, cwt_debug_conv_s) over every tile / split-K plan
-for each distinct conv shape of the extractor, beside the current bf16x3 conv's automatic plan
-(cwt_debug_conv precision 2).  Writes gpurun_out/<out>.
+"""Time the split-activation conv (conv_x3s, cwt_debug_conv_s) over every tile / split-K /
+main-loop-variant plan for each distinct conv shape of the extractor, beside the automatic plan
+the library picks today.  Writes gpurun_out/<out>.
 
-    python tools/conv_s_sweep.py [--configs 50:473:2] [--quick]
+    python tools/conv_s_sweep.py [--configs 50:473:2] [--vars 0,1,2] [--only l3c2,l3c1] [--quick]
 """
 import argparse
 import json
@@ -15,7 +15,39 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from few_shot_seg_cwt_amd import _lib  # noqa: E402
-from conv_sweep import shapes  # noqa: E402
+
+
+def shapes(layers, S, N):
+    """(name, count, Ci, Co, Hi, k, stride, dil, res) of the implicit-GEMM convs of one
+    extractor pass (api.hip run_extract; resnet.py:57-96 blocks with pspnet.py:124-129's
+    dilation surgery, the PPM-folded bottleneck conv), identical shapes merged."""
+    d2 = lambda x: (x - 1) // 2 + 1  # noqa: E731
+    Hs = d2(S)
+    H1 = d2(Hs)
+    h = d2(H1)
+    out = [("stem2", 1, 64, 64, Hs, 3, 1, 1, False), ("stem3", 1, 64, 128, Hs, 3, 1, 1, False)]
+    nb = [3, 4, 6, 3] if layers == 50 else [3, 4, 23, 3]
+    inpl, H = 128, H1
+    for li, planes in enumerate([64, 128, 256, 512]):
+        for bi in range(nb[li]):
+            s2 = 2 if (li == 1 and bi == 0) else 1
+            d = [1, 1, 2, 4][li]
+            Ho = d2(H) if s2 == 2 else H
+            out.append((f"l{li+1}c1", 1, inpl, planes, H, 1, 1, 1, False))
+            out.append((f"l{li+1}c2", 1, planes, planes, H, 3, s2, d, False))
+            if bi == 0:
+                out.append((f"l{li+1}down", 1, inpl, planes * 4, H, 1, s2, 1, False))
+            out.append((f"l{li+1}c3", 1, planes, planes * 4, Ho, 1, 1, 1, True))
+            inpl, H = planes * 4, Ho
+    out.append(("bottleneck", 1, 2048, 512, h, 3, 1, 1, True))
+    merged = {}
+    for s in out:
+        key = s[2:]
+        if key in merged:
+            merged[key][1] += 1
+        else:
+            merged[key] = [s[0], 1]
+    return [(v[0], v[1]) + k for k, v in merged.items()]
 
 TILES = [(256, 256), (256, 128), (128, 256), (128, 128), (128, 64), (64, 128), (64, 64)]
 
@@ -32,12 +64,14 @@ def timed(fn, reps):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
-def sweep(layers, size, n_img, reps, quick, prec=3):
+def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
     print(f"== R{layers} S={size} N={n_img}", flush=True)
     dev = torch.device("cuda", 0)
     lib, ctx, sp = _lib.lib(), _lib.ctx(0), _lib.stream_ptr()
-    res_all, tot_old, tot_auto, tot_best = [], 0.0, 0.0, 0.0
+    res_all, tot_auto, tot_best = [], 0.0, 0.0
     for name, cnt, Ci, Co, Hi, k, stride, dil, has_res in shapes(layers, size, n_img):
+        if only and name not in only:
+            continue
         pad = dil if k == 3 else 0
         Ho = (Hi + 2 * pad - dil * (k - 1) - 1) // stride + 1
         M, K = n_img * Ho * Ho, Ci * k * k
@@ -52,11 +86,6 @@ def sweep(layers, size, n_img, reps, quick, prec=3):
             ws = torch.empty(Co * K * 2, dtype=torch.bfloat16, device=dev)
             _lib.check(lib.cwt_debug_split_act(ctx, _lib.ptr(x), n_img * Hi * Hi, Ci, Ci, _lib.ptr(xs), sp))
             _lib.check(lib.cwt_debug_pack_wsplit(ctx, _lib.ptr(w), Co, k, Ci, _lib.ptr(ws), sp))
-        # old path: weights pre-split hi[Co][K] ++ lo[Co][K] (order within K does not matter for timing)
-        wf = w.reshape(Co, K)
-        hi = wf.to(torch.bfloat16)
-        lo = (wf - hi.float()).to(torch.bfloat16)
-        wsplit_old = torch.cat([hi.flatten(), lo.flatten()]).contiguous()
         sc = torch.ones(Co, device=dev)
         sh = torch.zeros(Co, device=dev)
         r = torch.randn(n_img, Ho, Ho, Co, device=dev) if has_res else None
@@ -70,11 +99,6 @@ def sweep(layers, size, n_img, reps, quick, prec=3):
         ys = torch.empty(M * Co * (1 if prec == 1 else 2), dtype=torch.bfloat16, device=dev)
         flops = 2.0 * M * Co * K
 
-        def old():
-            _lib.check(lib.cwt_debug_conv(ctx, _lib.ptr(x), n_img, Hi, Hi, Ci, Ci, _lib.ptr(wsplit_old),
-                                          _lib.ptr(sc), _lib.ptr(sh), Co, k, stride, pad, dil, _lib.ptr(r), Co, 1,
-                                          _lib.ptr(y), Co, 0, 0, 0, 0, 2, sp))
-
         conv_fn = lib.cwt_debug_conv_b16 if prec == 1 else lib.cwt_debug_conv_s
 
         def new(bm, bn, ns):
@@ -82,7 +106,6 @@ def sweep(layers, size, n_img, reps, quick, prec=3):
                 ctx, _lib.ptr(xs), n_img, Hi, Hi, Ci, _lib.ptr(ws), _lib.ptr(sc), _lib.ptr(sh), Co, k, stride, pad,
                 dil, None, Co, _lib.ptr(rs), 1, None, Co, 0, _lib.ptr(ys), bm, bn, ns, sp))
 
-        t_old = timed(old, reps) if prec == 3 else float("nan")
         t_auto = timed(new(0, 0, 0), reps)
         rows = []
         if not quick:
@@ -90,26 +113,34 @@ def sweep(layers, size, n_img, reps, quick, prec=3):
                 if Co % bn:
                     continue
                 tiles = -(-M // bm) * (Co // bn)
-                for ns in (1, 2, 4, 8):
-                    if ns > 1 and ((K // (64 if prec == 1 else 32)) // ns < 4 or tiles * ns > 4096):
-                        continue
-                    us = timed(new(bm, bn, ns), reps)
-                    rows.append({"bm": bm, "bn": bn, "ns": ns, "us": round(us, 2),
-                                 "tflops": round(flops / us / 1e6, 1)})
-        best = min(rows, key=lambda q: q["us"]) if rows else {"bm": 0, "bn": 0, "ns": 0, "us": t_auto,
+                for var in variants:
+                    if var and bm == 256 and bn == 256:
+                        continue   # no prefetch form of 256x256
+                    if var == 4 and (bm, bn) != (128, 128):
+                        continue   # two-workgroups-per-CU 128x128 form
+                    if var >= 8 and (bm, bn) != ((64, 64) if var < 10 else (128, 128)):
+                        continue   # timing-study kernels: fixed tiles
+                    if var >= 2 and (bm == 256 or bn == 256):
+                        continue   # 8-wave form only for the 128/64 tiles
+                    for ns in (1, 2, 4, 8):
+                        if ns > 1 and ((K // (64 if prec == 1 else 32)) // ns < 4 or tiles * ns > 4096):
+                            continue
+                        us = timed(new(1000 * var + bm, bn, ns), reps)
+                        rows.append({"bm": bm, "bn": bn, "ns": ns, "var": var, "us": round(us, 2),
+                                     "tflops": round(flops / us / 1e6, 1)})
+        best = min(rows, key=lambda q: q["us"]) if rows else {"bm": 0, "bn": 0, "ns": 0, "var": 0, "us": t_auto,
                                                                   "tflops": flops / t_auto / 1e6}
-        tot_old += cnt * t_old
         tot_auto += cnt * t_auto
         tot_best += cnt * best["us"]
-        print(f"{name:10s} x{cnt:2d} {Ci:4d}->{Co:4d} k{k} @{Ho:3d} M={M:6d} K={K:6d}: old {t_old:7.1f} us "
-              f"({flops / t_old / 1e6:6.1f} TF)  new-auto {t_auto:7.1f} ({flops / t_auto / 1e6:6.1f} TF)  best "
-              f"{best['bm']}x{best['bn']}s{best['ns']} {best['us']:7.1f} ({best['tflops']:6.1f} TF)", flush=True)
+        print(f"{name:10s} x{cnt:2d} {Ci:4d}->{Co:4d} k{k} @{Ho:3d} M={M:6d} K={K:6d}: "
+              f"auto {t_auto:7.1f} ({flops / t_auto / 1e6:6.1f} TF)  best "
+              f"{best['bm']}x{best['bn']}s{best['ns']}v{best['var']} {best['us']:7.1f} ({best['tflops']:6.1f} TF)",
+              flush=True)
         res_all.append({"cfg": f"{layers}:{size}:{n_img}", "prec": prec, "name": name, "count": cnt, "Ci": Ci, "Co": Co, "k": k,
                         "Ho": Ho, "M": M, "K": K, "stride": stride, "dil": dil, "res": has_res,
-                        "old_us": round(t_old, 2), "auto_us": round(t_auto, 2), "plans": rows})
-        del x, w, wp, xs, ws, wsplit_old, r, rs, y, ys
-    print(f"sum over the stack: old {tot_old:.1f} us, new auto {tot_auto:.1f} us, new best {tot_best:.1f} us",
-          flush=True)
+                        "auto_us": round(t_auto, 2), "plans": rows})
+        del x, w, wp, xs, ws, r, rs, y, ys
+    print(f"sum over the stack: auto {tot_auto:.1f} us, best {tot_best:.1f} us", flush=True)
     torch.cuda.empty_cache()
     return res_all
 
@@ -121,12 +152,15 @@ def main():
     ap.add_argument("--quick", action="store_true", help="old vs new automatic plan only")
     ap.add_argument("--out", default="conv_s_sweep.json")
     ap.add_argument("--prec", type=int, default=3, choices=[1, 3], help="3 = bf16x3 (x3s), 1 = plain bf16 (b16)")
+    ap.add_argument("--vars", default="0,1,2,4", help="main-loop variants (0 base, 1 prefetch, 2 prefetch 8 waves, 4 128x128 two per CU; 8-11 timing study)")
+    ap.add_argument("--only", default="", help="comma list of shape names (default: all)")
     args = ap.parse_args()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     res_all = []
     for cfg in args.configs.split(","):
         L, S, N = (int(v) for v in cfg.split(":"))
-        res_all += sweep(L, S, N, args.reps, args.quick, args.prec)
+        res_all += sweep(L, S, N, args.reps, args.quick, args.prec,
+                         tuple(int(v) for v in args.vars.split(",")), set(filter(None, args.only.split(","))))
         with open(os.path.join(ROOT, "gpurun_out", args.out), "w") as f:
             json.dump(res_all, f, indent=1)
 
