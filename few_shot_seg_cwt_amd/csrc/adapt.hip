@@ -611,9 +611,10 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const float* f_ws, con
 //     (A barrier-free variant -- 64-bit fixed-point adds carrying a contribution count, polled
 //     element by element -- was exact and deterministic but 1.7x slower per step: 118 x 1024
 //     threads polling the same 32 KB contend with the adds at the memory side.)
-//   * slots: step s adds into slot s%4; workgroup G-1 zeroes slot (s+2)%4 at the start of step
-//     s (its last readers passed barrier s-1; its next adders start after barrier s+1; the
-//     write-through zero stores are complete when G-1 arrives at barrier s).
+//   * slots: step s adds into slot s%4; at the start of step s every workgroup zeroes its 1/G
+//     share of slot (s+2)%4 (its last readers passed barrier s-1; its next adders start after
+//     barrier s+1; the write-through zero stores are complete when the workgroup arrives at
+//     barrier s).  (One workgroup zeroing the whole slot made it the last arriver of most steps.)
 // Every spin is bounded: a barrier that does not complete within ~4 s sets the error word and
 // the grid exits (wrong W, no hang).  Requires all G workgroups co-resident: G <= #CU and one
 // 1024-thread workgroup per CU.
@@ -628,9 +629,15 @@ constexpr int PA_R = 16;             // max replica rows of dW[1] (and arrival c
 constexpr int PA_R_DEFAULT = 8;      // rows used (CWT_ADAPT_PR: 2, 4, 8 or 16)
 constexpr int PA_NSLOT = 4;          // accumulator slots (step s adds into s % 4)
 constexpr int PA_EW = 4;             // episodes one workgroup's units may span
-constexpr int PA_CNT_STRIDE = 32;    // one control word per 128-B line
+#ifndef PA_CNT_STRIDE_WORDS
+#define PA_CNT_STRIDE_WORDS 32
+#endif
+constexpr int PA_CNT_STRIDE = PA_CNT_STRIDE_WORDS;  // words between control words (32: one per 128-B line)
 constexpr int PA_CNT_WORDS = (PA_R + 1) * PA_CNT_STRIDE;  // arrival counters + error word
 constexpr long PA_SPIN_LIMIT = 4000000;
+#ifndef PA_POLL_SLEEP
+#define PA_POLL_SLEEP 1  // s_sleep units (64 clocks) between arrival polls
+#endif
 static_assert(PA_NSLOT * ADAPT_SLOT <= ADAPT_ESTRIDE && PA_R <= ADAPT_RMAX, "slots must fit an episode's accumulators");
 
 struct PersistArgs {
@@ -752,16 +759,15 @@ __device__ __forceinline__ void pa_butterfly(float (&v)[PA_CPW], int lane) {
 template <int NRES, bool STAMPS = false>
 __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsigned long long* stamps = nullptr) {
   constexpr int C = 512;
-  constexpr int EWK = NRES == 2 ? 2 : PA_EW;  // LDS budget: the second unit's f takes 128 KB
-  __shared__ float wl[EWK][2][C];
-  __shared__ float dl[EWK][C];
+  constexpr int EWK = NRES == 2 ? 2 : NRES == 1 ? 1 : PA_EW;  // episodes one workgroup's units may span
   __shared__ float fl2[NRES == 2 ? PA_NW : 1][PA_CPW][NRES == 2 ? 64 : 1];
+  __shared__ float dlw[PA_NW][EWK][PA_CPW];     // d = W1 - W0 of each wave's channels (wave-private)
+  __shared__ float wlw[PA_NW][EWK][2][PA_CPW];  // W0, W1 of each wave's channels (wave-private)
   __shared__ float zpart[PA_NW][PA_NPX];
   __shared__ float zd[PA_NPX];
   __shared__ float gs[PA_NPX];
   __shared__ float P0[8][2][PA_NC + 1];
   __shared__ float P1[8][2][PA_NC + 1];
-  __shared__ float dsum[C];
   __shared__ float wfg_l[EWK], lr_l[EWK];
   __shared__ int abort_flag;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -779,14 +785,20 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
     stp_end[1] = __builtin_amdgcn_s_memtime();
   }
 
-  // initial W of the spanned episodes
-  for (int i = t; i < new_ * C; i += PA_T) {
-    const int ew = i / C, c = i - ew * C;
-    const float* wi = a.dargs[e_lo + ew].w_in;
-    const float w0 = wi[c], w1 = wi[C + c];
-    wl[ew][0][c] = w0;
-    wl[ew][1][c] = w1;
-    dl[ew][c] = w1 - w0;
+  // W of the spanned episodes is split over the waves: wave wv keeps channels [32wv, 32wv+32)
+  // in a private LDS slice (lane L < 32: channel 32wv + L) and only ever touches its own slice,
+  // so W needs no workgroup barrier; every workgroup applies the same updates in the same
+  // order, so the copies stay identical
+  const int cw = wv * PA_CPW + (lane & 31);
+#pragma unroll
+  for (int ew = 0; ew < EWK; ++ew) {
+    const float* wi = a.dargs[min(e_lo + ew, a.nep - 1)].w_in;
+    const float w0 = wi[cw], w1 = wi[C + cw];
+    if (lane < 32) {
+      wlw[wv][ew][0][lane] = w0;
+      wlw[wv][ew][1][lane] = w1;
+      dlw[wv][ew][lane] = w1 - w0;
+    }
   }
   if (t == 0) abort_flag = 0;
   if (t < new_) {
@@ -819,9 +831,10 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       if (STAMPS && stp) stp[i] = __builtin_amdgcn_s_memtime();
     };
     stamp(0);
-    if (g == G - 1 && s + 2 < a.iters) {  // zero slot (s+2)%4 (write-through stores, done by our arrival)
+    if (s + 2 < a.iters) {  // zero this workgroup's share of slot (s+2)%4 (write-through stores, done by our arrival)
       const int zs = (s + 2) % PA_NSLOT;
-      for (int i = t; i < a.nep * nrep * C; i += PA_T) {
+      const int tot = a.nep * nrep * C, per = (tot + G - 1) / G;
+      for (int i = g * per + t; i < min(tot, (g + 1) * per); i += PA_T) {
         const int e = i / (nrep * C), k = i - e * (nrep * C);
         __hip_atomic_store(a.acc + (long)e * ADAPT_ESTRIDE + (long)zs * ADAPT_SLOT + k, 0.f, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -830,12 +843,14 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
     // one unit's z / hi-res / dW passes; fget(j): f of lane p's pixel, channel 32*wv + j
     auto unit_body = [&](const PaUnit& q, int u, auto fget, const int (&ylab)[2][2]) {
       const int ew = q.e - e_lo;
-      // ---- z = d . f: this wave's 32-channel partial for lane p's pixel ----
+      // ---- z = d . f: this wave's 32-channel partial for lane p's pixel; d = W1 - W0 of the
+      // wave's channels from its private LDS slice (LDS broadcast; written by this wave only,
+      // so no workgroup barrier) ----
       {
         float sdot = 0.f;
 #pragma unroll
         for (int j = 0; j < PA_CPW / 4; ++j) {
-          const f32x4 d4 = *(const f32x4*)&dl[ew][wv * PA_CPW + 4 * j];
+          const f32x4 d4 = *(const f32x4*)&dlw[wv][ew][4 * j];
           sdot = fmaf(d4[0], fget(4 * j), sdot);
           sdot = fmaf(d4[1], fget(4 * j + 1), sdot);
           sdot = fmaf(d4[2], fget(4 * j + 2), sdot);
@@ -943,16 +958,19 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       pa_load(cur, a, q, wv, lane);
     }
     if (wv == 0) {
+      // one sc1 poll of the arrival counters at a time (two in flight measured slower: the extra
+      // polls delay the arrivals' atomics at the memory side), summed by DPP
       const unsigned target = (unsigned)G * (unsigned)(s + 1);
+      const unsigned* cp = a.cnt + (lane < nrep ? lane : 0) * PA_CNT_STRIDE;
       long spins = 0;
       while (true) {
-        unsigned c = lane < nrep ? __hip_atomic_load(a.cnt + lane * PA_CNT_STRIDE, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)
-                                 : 0u;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-        c = __builtin_amdgcn_readfirstlane(c);
-        if (c >= target) break;
+        unsigned c = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c = lane < nrep ? c : 0u;  // sum over lanes 0..15 (nrep <= 16) by DPP row shifts, read from lane 15
+        c += __builtin_amdgcn_update_dpp(0u, c, 0x111, 0xF, 0xF, true);  // row_shr:1
+        c += __builtin_amdgcn_update_dpp(0u, c, 0x112, 0xF, 0xF, true);  // row_shr:2
+        c += __builtin_amdgcn_update_dpp(0u, c, 0x114, 0xF, 0xF, true);  // row_shr:4
+        c += __builtin_amdgcn_update_dpp(0u, c, 0x118, 0xF, 0xF, true);  // row_shr:8
+        if ((unsigned)__builtin_amdgcn_readlane((int)c, 15) >= target) break;
         if (++spins > PA_SPIN_LIMIT || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
           if (lane == 0) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -960,7 +978,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
           }
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(PA_POLL_SLEEP);
       }
     }
     stamp(5);
@@ -968,30 +986,33 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
     lds_barrier();
     stamp(6);
     if (abort_flag) return;
-    // ---- W of every spanned episode: W1 -= lr_eff * D, W0 += lr_eff * D (same order everywhere);
-    // thread halves t < 512 / t >= 512 sum replica rows [0, nrep/2) / [nrep/2, nrep) ----
-    const int nh = nrep >> 1;
-    for (int ew = 0; ew < new_; ++ew) {
-      const int c = t & (C - 1), hh = t >> 9;
-      const float* ap = a.acc + (long)(e_lo + ew) * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + (long)hh * nh * C + c;
-      float v[PA_R / 2];
+    // ---- W of every spanned episode: W1 -= lr_eff * D, W0 += lr_eff * D (same order everywhere).
+    // Each wave reads D of its own 32 channels only (its W slice): lanes L < 32 sum replica rows [0, nrep/2),
+    // lanes L + 32 rows [nrep/2, nrep), and one v_permlane32_swap adds the halves (the same two
+    // partial sums in every workgroup: a + b == b + a) -- no workgroup barrier, no LDS ----
+    {
+      const int nh = nrep >> 1, hh = lane >> 5;
 #pragma unroll
-      for (int r = 0; r < PA_R / 2; ++r)
-        v[r] = r < nh ? __hip_atomic_load(ap + r * C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-      float D = 0.f;
+      for (int ew = 0; ew < EWK; ++ew) {
+        if (ew >= new_) break;
+        const float* ap = a.acc + (long)(e_lo + ew) * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + (long)hh * nh * C + cw;
+        float v[PA_R / 2];
 #pragma unroll
-      for (int r = 0; r < PA_R / 2; ++r) D += v[r];
-      if (hh) dsum[c] = D;
-      lds_barrier();
-      if (!hh) {
-        D += dsum[c];
-        const float lr = lr_l[ew];
-        const float w1 = wl[ew][1][c] - lr * D, w0 = wl[ew][0][c] + lr * D;
-        wl[ew][1][c] = w1;
-        wl[ew][0][c] = w0;
-        dl[ew][c] = w1 - w0;
+        for (int r = 0; r < PA_R / 2; ++r)
+          v[r] = r < nh ? __hip_atomic_load(ap + r * C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+        float D = 0.f;
+#pragma unroll
+        for (int r = 0; r < PA_R / 2; ++r) D += v[r];
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(D), __float_as_uint(D), false, false);
+        D = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);  // rows [0,nh) + rows [nh,nrep) in every lane
+        if (lane < 32) {
+          const float lr = lr_l[ew];
+          const float w1 = wlw[wv][ew][1][lane] - lr * D, w0 = wlw[wv][ew][0][lane] + lr * D;
+          wlw[wv][ew][1][lane] = w1;
+          wlw[wv][ew][0][lane] = w0;
+          dlw[wv][ew][lane] = w1 - w0;
+        }
       }
-      lds_barrier();
     }
     stamp(7);
   }
@@ -1000,13 +1021,13 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
     stp_end[3] = __builtin_amdgcn_s_memtime();
   }
   // ---- adapted W: written by the workgroup that owns the episode's first unit ----
-  for (int i = t; i < new_ * C; i += PA_T) {
-    const int ew = i / C, c = i - ew * C;
+#pragma unroll
+  for (int ew = 0; ew < EWK; ++ew) {
     const int e = e_lo + ew;
-    if ((long)e * per_ep >= u0) {
+    if (ew < new_ && (long)e * per_ep >= u0 && lane < 32) {
       float* wo = a.dargs[e].w_out;
-      wo[c] = wl[ew][0][c];
-      wo[C + c] = wl[ew][1][c];
+      wo[cw] = wlw[wv][ew][0][lane];
+      wo[C + cw] = wlw[wv][ew][1][lane];
     }
   }
 }

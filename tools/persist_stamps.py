@@ -60,6 +60,13 @@ ph["most frequent last arriver (workgroup)"] = int(np.argmax(np.bincount(np.argm
 work = us(np.mean(body[:, :, 4] - body[:, :, 0], axis=0))   # step start -> atomics performed, per workgroup
 ph["step work per workgroup min/median/max"] = [round(float(x), 3) for x in (work.min(), np.median(work), work.max())]
 ph["slowest workgroups"] = [int(i) for i in np.argsort(work)[-4:]]
+per_wg = np.stack([us(np.mean(body[:, :, i + 1] - body[:, :, i], axis=0)) for i in range(4)], 1)   # [G, 4]
+med = np.median(per_wg, axis=0)
+ph["phases z/hires/dW/atomics: median workgroup"] = [round(float(x), 3) for x in med]
+ph["phases z/hires/dW/atomics: slowest workgroups"] = {
+    int(g): [round(float(x), 3) for x in per_wg[g]] for g in np.argsort(work)[-8:]}
+ph["mean arrival rank (0 first) of the slowest workgroups"] = {
+    int(g): round(float(np.mean(np.argsort(np.argsort(arr, axis=1), axis=1)[:, g])), 1) for g in np.argsort(work)[-8:]}
 ph["step period"] = round(float(us(np.mean(np.diff(st[:iters, :, 0], axis=0)))), 3)
 ph["loop per step (realtime)"] = round(float(np.median(rt)) / 100.0 / iters, 3)
 ph["workgroups"] = G
