@@ -187,7 +187,7 @@ class EpisodePipeline:
         self.s_ext = [torch.cuda.Stream() for _ in range(max(1, int(extract_streams)))]
         self.c_ext = [None] + [_lib.new_ctx() for _ in range(len(self.s_ext) - 1)]
         self.s_extract = self.s_ext[0]
-        self.s_adapt = torch.cuda.Stream()
+        self.s_adapt = torch.cuda.Stream()  # (high priority measured no different)
         self.k = 0
 
     @torch.no_grad()
