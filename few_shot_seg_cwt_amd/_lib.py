@@ -72,6 +72,7 @@ SIGNATURES = {
                                 _P, _I, _I, _I, _P]),
     "cwt_debug_census": (_I, [_P, _I, _P, _P]),
     "cwt_debug_adapt_stamps": (_I, [_P, _P, _I64, C.POINTER(_I64)]),
+    "cwt_ctx_set_adapt_units": (_I, [_P, _I]),
     "cwt_profile_enable": (_I, [_P, _I]),
     "cwt_profile_count": (_I, [_P]),
     "cwt_profile_record": (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_double),

@@ -1035,8 +1035,8 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
 // Host side of the persistent loop: G = min(units, CUs).  Returns 1 (not an error) when the
 // geometry does not fit it (the caller then uses the per-step launches).
 static int g_cu_count = 0;
-static int persist_geometry(int E, int n, int h, int w, int* G_out, int* units_out, int* ncb_out, int* nres_out,
-                            int* uc_out) {
+static int persist_geometry(int E, int n, int h, int w, int upw_pref, int* G_out, int* units_out, int* ncb_out,
+                            int* nres_out, int* uc_out) {
   if (!g_cu_count) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -1054,10 +1054,11 @@ static int persist_geometry(int E, int n, int h, int w, int* G_out, int* units_o
   const int ntile = (h - 1) * ncb;
   const long units = (long)E * n * ntile;
   // units per workgroup: 1 (f in registers) or 2 (the second unit's f in LDS): half the
-  // workgroups, a cheaper barrier, and CUs left for the next episode's extractor (CWT_ADAPT_UPW)
-  // (default: 1 while that takes at most half the CUs -- 1-shot 473^2: 118 -- else 2)
+  // workgroups and CUs left for a concurrent extractor pass.  The context's choice
+  // (cwt_ctx_set_adapt_units: EpisodePipeline asks for 2), else CWT_ADAPT_UPW, else 1 while
+  // that takes at most half the CUs (1-shot 473^2: 118 workgroups) and 2 beyond
   const char* upws = getenv("CWT_ADAPT_UPW");
-  const int upw = upws ? (atoi(upws) == 1 ? 1 : 2) : (units <= g_cu_count / 2 ? 1 : 2);
+  const int upw = upw_pref ? upw_pref : upws ? (atoi(upws) == 1 ? 1 : 2) : (units <= g_cu_count / 2 ? 1 : 2);
   const int G = (int)std::min<long>((units + upw - 1) / upw, g_cu_count);
   const long k = (units + G - 1) / G;  // units per workgroup (max)
   const long per_ep = (long)n * ntile;
@@ -1145,7 +1146,7 @@ size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lb
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
                  float* W, float* f_ws /*[E][n][h][w][512]*/, uint8_t* lbl_ws, AdaptScalars* sc /*[E] + partial counts*/,
                  float* acc3 /*[E][3][R][512]*/, float* wbuf /*[E][2][2][512]*/, AdaptDevArgs* dargs /*[E]*/,
-                 AdaptGraphCache* cache, hipStream_t st) {
+                 AdaptGraphCache* cache, int upw, hipStream_t st) {
   const long total = (long)n * S * S;  // labels per episode
   unsigned long long* part = (unsigned long long*)(sc + E);  // [E][PREP_MAXBLK][2] after the scalars
   const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
@@ -1154,7 +1155,7 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
   int pG = 0, punits = 0, pncb = 0, pnres = 0, puc = 0;
   const char* pe = getenv("CWT_ADAPT_PERSIST");
   const bool persist = iters > 0 && !(pe && pe[0] == '0') &&
-                       persist_geometry(E, n, h, w, &pG, &punits, &pncb, &pnres, &puc) == 0;
+                       persist_geometry(E, n, h, w, upw, &pG, &punits, &pncb, &pnres, &puc) == 0;
   unsigned* cnt = (unsigned*)(acc3 + (long)E * ADAPT_ESTRIDE);
   hipLaunchKernelGGL(adapt_setup_kernel, dim3(E), dim3(PREP_MAXBLK), 0, st, (const unsigned long long*)part, pblocks,
                      sc, lr, 0, dargs, f, (long)n * h * w * 512, (const float*)W, W, 1024,

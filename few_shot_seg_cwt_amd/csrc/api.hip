@@ -30,7 +30,7 @@ struct AdaptScalars;
 struct AdaptDevArgs;
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
                  float* W, float* f_ws, uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf,
-                 AdaptDevArgs* dargs, AdaptGraphCache* cache, hipStream_t st);
+                 AdaptDevArgs* dargs, AdaptGraphCache* cache, int upw, hipStream_t st);
 extern unsigned long long* g_adapt_stamps;
 extern long g_adapt_stamps_n;
 size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lbl, size_t* sc, size_t* acc,
@@ -130,6 +130,8 @@ struct cwt_ctx {
   // conv arithmetic: bf16x3 on the bf16 matrix cores over S-layout activations (default,
   // CWT_CONV=x3s) or exact fp32 MFMA over fp32 activations (CWT_CONV=f32)
   bool conv_split = true;
+  // persistent inner loop: units per workgroup (0 automatic, 1, 2), cwt_ctx_set_adapt_units
+  int adapt_upw = 0;
 };
 
 namespace cwt {
@@ -960,7 +962,7 @@ int cwt_inner_adapt_batch(cwt_ctx* ctx, const float* f_s, const int64_t* s_label
          1);
   rc = launch_adapt(f_s, s_label, E, n, h, w, S, lr, iters, W_inout, (float*)fws, (uint8_t*)lbl, (AdaptScalars*)sc,
                     (float*)acc, (float*)wb, (AdaptDevArgs*)dargs, ctx->use_graph ? &ctx->adapt_graphs : nullptr,
-                    (hipStream_t)stream);
+                    ctx->adapt_upw, (hipStream_t)stream);
   p.end();
   return rc;
 }
@@ -1349,6 +1351,13 @@ int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int
   int rc;
   if ((rc = ensure_ws(ctx, "iou.cnt", 3 * 16 * 4, &cnt))) return rc;
   return launch_iou_preds(preds, target, n, num_classes, ignore_index, iut_out, (unsigned*)cnt, (hipStream_t)stream);
+}
+
+int cwt_ctx_set_adapt_units(cwt_ctx* ctx, int units_per_workgroup) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(units_per_workgroup >= 0 && units_per_workgroup <= 2, "units per workgroup must be 0 (automatic), 1 or 2");
+  ctx->adapt_upw = units_per_workgroup;
+  return 0;
 }
 
 int cwt_profile_enable(cwt_ctx* ctx, int on) {

@@ -315,6 +315,14 @@ int cwt_sgd_step(cwt_ctx* ctx, float* param, const float* grad, float* momentum_
  * (SURVEY.md §8(d)).  Enabling (level > 0) clears the records; 0 stops recording.
  * cwt_profile_record waits for record i's stop event and returns its elapsed time.
  */
+/*
+ * Scheduling knob (no reference counterpart): how many 64-pixel units of the support map one
+ * workgroup of the persistent inner loop holds (0 = automatic, 1 or 2).  2 halves the CUs the
+ * loop occupies, for contexts whose inner loops run beside another stream's extractor pass
+ * (few_shot_seg_cwt_amd.episode.EpisodePipeline); results are the same either way.
+ */
+int cwt_ctx_set_adapt_units(cwt_ctx* ctx, int units_per_workgroup);
+
 int cwt_profile_enable(cwt_ctx* ctx, int level);
 int cwt_profile_count(cwt_ctx* ctx);
 int cwt_profile_record(cwt_ctx* ctx, int i, char* name, int name_len, double* flops, double* bytes,
