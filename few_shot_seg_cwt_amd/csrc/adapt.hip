@@ -702,6 +702,43 @@ __device__ __forceinline__ void pa_load(PaTile& t, const PersistArgs& a, const P
   }
 }
 
+// NRES 3 (units streamed): wave wv moves its 32-channel slice of a unit's f (64 pixels x 128 B)
+// into its private 8-KB LDS region by LDS-DMA, 8 pieces of 8 pixels; 16-B chunk c of pixel p is
+// stored at slot c ^ ((p >> 1) & 7), so the per-pixel ds_read_b128 of pa_read_f are
+// conflict-free.  Only the wave itself reads its region: the hand-off needs no barrier.
+__device__ __forceinline__ void pa_issue_f(const PersistArgs& a, const PaUnit& q, int wv, int lane, float* fw) {
+  const int pr = lane >> 3, sl = lane & 7;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int p = j * 8 + pr;
+    const int c = sl ^ ((p >> 1) & 7);
+    const int ri = p >> 5, xs = min(p & 31, q.ncol - 1);
+    const float* src = a.f + (((long)q.img * a.h + q.r + ri) * a.w + q.x0 + xs) * 512 + wv * PA_CPW + c * 4;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)((char*)fw + j * 1024), 16, 0, 0);
+  }
+}
+__device__ __forceinline__ void pa_read_f(float (&fr)[PA_CPW], const float* fw, int lane) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const f32x4 v = *(const f32x4*)(fw + lane * PA_CPW + ((c ^ ((lane >> 1) & 7)) << 2));
+    fr[4 * c] = v[0]; fr[4 * c + 1] = v[1]; fr[4 * c + 2] = v[2]; fr[4 * c + 3] = v[3];
+  }
+}
+__device__ __forceinline__ void pa_labels(int (&y)[2][2], const PersistArgs& a, const PaUnit& q, int wv, int lane) {
+  const uint8_t* lb = a.lbl + (long)q.img * a.S * a.S;
+  const int Y = 8 * q.r + (wv >> 1);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int X = 8 * q.x0 + 64 * (wv & 1) + 128 * k + lane;
+    const int Xc = min(X, a.S - 1);
+    const int ym = lb[(long)Y * a.S + Xc], ye = lb[(long)(a.S - 1) * a.S + Xc];
+    const bool xin = X < q.x_end;
+    y[k][0] = xin ? ym : 255;
+    y[k][1] = (xin && q.extra_row && (wv >> 1) == 0) ? ye : 255;
+  }
+}
+
 // 64-lane reduction of 32 per-lane values (channel j in v[j]) leaving lane L with channel L >> 1:
 // five halving steps, each pairing lanes that differ in one lane bit (the lane with the bit set
 // keeps the upper half of the channels, its partner the lower), then one plain pair sum.
@@ -753,14 +790,16 @@ __device__ __forceinline__ void pa_butterfly(float (&v)[PA_CPW], int lane) {
 // ([9]) into stamps[step][g][10], and realtime/memtime at entry and exit into
 // stamps[iters][g][0..3] (tools/persist_stamps.py).
 // NRES 1: one unit per workgroup, its f in registers; 2: up to two units per workgroup, the
-// first in registers, the second in LDS (128 KB, lane-major: conflict-free); 0: units streamed
-// from L2 every step.  Fewer workgroups make each step's barrier cheaper and leave CUs to the
+// first in registers, the second in LDS (128 KB, lane-major: conflict-free); 3: units streamed
+// every step, each wave's slice by LDS-DMA into its private 8 KB while the previous unit is
+// computed; 0: units streamed from L2 into registers (opt-in, slower).  Fewer workgroups make each step's barrier cheaper and leave CUs to the
 // next episode's extractor pass (EpisodePipeline).
 template <int NRES, bool STAMPS = false>
 __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsigned long long* stamps = nullptr) {
   constexpr int C = 512;
-  constexpr int EWK = NRES == 2 ? 2 : NRES == 1 ? 1 : PA_EW;  // episodes one workgroup's units may span
+  constexpr int EWK = (NRES == 2 || NRES == 3) ? 2 : NRES == 1 ? 1 : PA_EW;  // episodes a workgroup's units may span
   __shared__ float fl2[NRES == 2 ? PA_NW : 1][PA_CPW][NRES == 2 ? 64 : 1];
+  __shared__ __attribute__((aligned(16))) float fs3[NRES == 3 ? PA_NW * 64 * PA_CPW : 4];  // NRES 3: per-wave f slices
   __shared__ float dlw[PA_NW][EWK][PA_CPW];     // d = W1 - W0 of each wave's channels (wave-private)
   __shared__ float wlw[PA_NW][EWK][2][PA_CPW];  // W0, W1 of each wave's channels (wave-private)
   __shared__ float zpart[PA_NW][PA_NPX];
@@ -807,7 +846,14 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
   }
   PaTile cur;
   PaUnit q = pa_unit(a, u0);
-  pa_load(cur, a, q, wv, lane);
+  float* fw = fs3 + (NRES == 3 ? wv * 64 * PA_CPW : 0);
+  int ynx[2][2];  // NRES 3: labels of the unit whose f is in flight
+  if (NRES == 3) {
+    pa_issue_f(a, q, wv, lane, fw);
+    pa_labels(ynx, a, q, wv, lane);
+  } else {
+    pa_load(cur, a, q, wv, lane);
+  }
   int y2[2][2] = {{255, 255}, {255, 255}};  // NRES 2: labels of the second unit (its f is in fl2)
   if (NRES == 2 && u1 - u0 > 1) {
     PaTile tmp;
@@ -831,15 +877,32 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       if (STAMPS && stp) stp[i] = __builtin_amdgcn_s_memtime();
     };
     stamp(0);
-    if (s + 2 < a.iters) {  // zero this workgroup's share of slot (s+2)%4 (write-through stores, done by our arrival)
-      const int zs = (s + 2) % PA_NSLOT;
-      const int tot = a.nep * nrep * C, per = (tot + G - 1) / G;
-      for (int i = g * per + t; i < min(tot, (g + 1) * per); i += PA_T) {
-        const int e = i / (nrep * C), k = i - e * (nrep * C);
-        __hip_atomic_store(a.acc + (long)e * ADAPT_ESTRIDE + (long)zs * ADAPT_SLOT + k, 0.f, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    // zero this workgroup's share of slot (s+2)%4 (write-through stores, done by our arrival);
+    // NRES 3 does it after its units, so that its per-unit DMA waits do not wait for the stores
+    auto zero_share = [&]() {
+      if (s + 2 < a.iters) {
+        const int zs = (s + 2) % PA_NSLOT;
+        const int tot = a.nep * nrep * C, per = (tot + G - 1) / G;
+        for (int i = g * per + t; i < min(tot, (g + 1) * per); i += PA_T) {
+          const int e = i / (nrep * C), k = i - e * (nrep * C);
+          __hip_atomic_store(a.acc + (long)e * ADAPT_ESTRIDE + (long)zs * ADAPT_SLOT + k, 0.f, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
-    }
+    };
+    if (NRES != 3) zero_share();
+    // NRES 3: each unit's dW is reduced over the wave by the butterfly as usual, and the one
+    // value a lane then holds (channel lane >> 1) is summed over the step's units of one episode
+    // in a register; one atomic per episode and step (none in flight at the next unit's DMA wait)
+    float dsum3 = 0.f;
+    int dsum3_e = e_lo;
+    auto flush3 = [&]() {
+      if ((lane & 1) == 0)
+        __hip_atomic_fetch_add(a.acc + (long)dsum3_e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
+                                   wv * PA_CPW + (lane >> 1),
+                               dsum3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      dsum3 = 0.f;
+    };
     // one unit's z / hi-res / dW passes; fget(j): f of lane p's pixel, channel 32*wv + j
     auto unit_body = [&](const PaUnit& q, int u, auto fget, const int (&ylab)[2][2]) {
       const int ew = q.e - e_lo;
@@ -927,13 +990,39 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
 #pragma unroll
         for (int j = 0; j < PA_CPW; ++j) accd[j] = gp * fget(j);
         pa_butterfly(accd, lane);  // lane L: channel (L >> 1) of the wave's slice, summed over 64 lanes
-        if ((lane & 1) == 0)
+        if (NRES == 3) {  // summed over the step's units of the episode, flushed on a change of episode
+          if (q.e != dsum3_e) {
+            flush3();
+            dsum3_e = q.e;
+          }
+          dsum3 += accd[0];
+        } else if ((lane & 1) == 0) {
           __hip_atomic_fetch_add(a.acc + (long)q.e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
                                      wv * PA_CPW + (lane >> 1),
                                  accd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     };
     for (int u = u0; u < u1; ++u) {
+      if (NRES == 3) {  // this wave's slice of unit u landed (nothing younger is in flight), then
+                        // the next unit's DMA goes out while unit u is computed
+        const PaUnit qu = pa_unit(a, u);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        pa_read_f(cur.fr, fw, lane);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          cur.y[k][0] = ynx[k][0];
+          cur.y[k][1] = ynx[k][1];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slice is read: it may be refilled
+        if (u + 1 < u1) {  // (the next step's first unit goes out after this step's arrival)
+          const PaUnit qn = pa_unit(a, u + 1);
+          pa_issue_f(a, qn, wv, lane, fw);
+          pa_labels(ynx, a, qn, wv, lane);
+        }
+        unit_body(qu, u, [&](int jj) { return cur.fr[jj]; }, cur.y);
+        continue;
+      }
       if (NRES == 2 && u != u0) {
         unit_body(pa_unit(a, u), u, [&](int jj) { return fl2[wv][jj][lane]; }, y2);
         continue;
@@ -946,6 +1035,10 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       }
       unit_body(q, u, [&](int jj) { return cur.fr[jj]; }, cur.y);
     }
+    if (NRES == 3) {
+      flush3();
+      zero_share();
+    }
     stamp(3);
     // ---- grid barrier s ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics (and zero stores) performed
@@ -953,6 +1046,10 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
     stamp(4);
     if (STAMPS && stp) stp[8] = __builtin_amdgcn_s_memrealtime();
     if (t == 0) __hip_atomic_fetch_add(a.cnt + rep * PA_CNT_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (NRES == 3 && s + 1 < a.iters) {  // next step's first unit: W-independent, lands during the wait
+      pa_issue_f(a, pa_unit(a, u0), wv, lane, fw);
+      pa_labels(ynx, a, pa_unit(a, u0), wv, lane);
+    }
     if (NRES == 0 && s + 1 < a.iters) {  // next step's first unit: W-independent, lands during the wait
       q = pa_unit(a, u0);
       pa_load(cur, a, q, wv, lane);
@@ -1063,14 +1160,22 @@ static int persist_geometry(int E, int n, int h, int w, int upw_pref, int* G_out
   const long k = (units + G - 1) / G;  // units per workgroup (max)
   const long per_ep = (long)n * ntile;
   const long span = (k - 1 + per_ep - 1) / per_ep + 1;  // episodes a workgroup's range can touch
-  const int nres = k == 1 ? 1 : (k == 2 && span <= 2) ? 2 : 0;
-  if (span > (nres == 2 ? 2 : PA_EW)) return 1;
+  // k >= 4 (5-shot 641^2: 1200 units, 4-5 per workgroup): units streamed per wave through LDS
+  // (nres 3), 6.04 against 6.35 ms for the step launches; at k = 3 (5-shot 473^2) the stream is
+  // slower than the step launches (4.09 against 3.53 ms: the 37 MB per step of f come from the
+  // Infinity Cache and the 3-unit workgroups set the pace), so those keep the step launches.
+  // CWT_ADAPT_STREAM=0 disables it, =1 allows it from k = 3.
+  const char* sts = getenv("CWT_ADAPT_STREAM");
+  const int stream_from = sts ? (sts[0] == '0' ? 1 << 30 : 3) : 4;
+  int nres = k == 1 ? 1 : (k == 2 && span <= 2) ? 2 : 0;
+  if (nres == 0 && k >= stream_from && span <= 2) nres = 3;
+  if (span > (nres == 2 || nres == 3 ? 2 : PA_EW)) return 1;
   *G_out = G;
   *units_out = (int)units;
   *ncb_out = ncb;
   *uc_out = uc;
   *nres_out = nres;
-  // streamed units (multi-shot) are not yet faster than the step launches: opt in only
+  // the register-streamed form (nres 0) is not faster than the step launches: opt in only
   const char* pe = getenv("CWT_ADAPT_PERSIST");
   if (!*nres_out && !(pe && pe[0] == '2')) return 1;
   return 0;
@@ -1109,12 +1214,16 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
       CWT_HIP(hipMalloc(&g_adapt_stamps, n_st * sizeof(unsigned long long)));
       g_adapt_stamps_n = n_st;
     }
-    if (nres == 1)
+    if (nres == 3)
+      hipLaunchKernelGGL((adapt_persist_kernel<3, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
+    else if (nres == 1)
       hipLaunchKernelGGL((adapt_persist_kernel<1, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
     else if (nres == 2)
       hipLaunchKernelGGL((adapt_persist_kernel<2, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
     else
       hipLaunchKernelGGL((adapt_persist_kernel<0, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
+  } else if (nres == 3) {
+    hipLaunchKernelGGL((adapt_persist_kernel<3, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
   } else if (nres == 1) {
     hipLaunchKernelGGL((adapt_persist_kernel<1, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
   } else if (nres == 2) {

@@ -27,11 +27,12 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def _run(persist, f, lbl, W0, iters, uc=None, upw=None):
+def _run(persist, f, lbl, W0, iters, uc=None, upw=None, stream=None):
     """persist: "0" per-step launches, "2" the persistent loop also where units are streamed;
-    upw: units per workgroup ("1": f in registers; "2", the default: the second unit in LDS)."""
+    upw: units per workgroup ("1": f in registers; "2", the default: the second unit in LDS);
+    stream: "1" the LDS-streamed form from 3 units per workgroup, "0" never."""
     from few_shot_seg_cwt_amd.episode import inner_adapt_batch
-    env = {"CWT_ADAPT_PERSIST": persist, "CWT_ADAPT_UC": uc, "CWT_ADAPT_UPW": upw}
+    env = {"CWT_ADAPT_PERSIST": persist, "CWT_ADAPT_UC": uc, "CWT_ADAPT_UPW": upw, "CWT_ADAPT_STREAM": stream}
     old = {k: os.environ.get(k) for k in env}
     for k, v in env.items():
         if v is None:
@@ -74,3 +75,26 @@ def test_persist_equals_step_launches(dev, E, n, S, iters, uc, upw):
     print(f"E={E} n={n} S={S} iters={iters} upw={upw}: max rel {max(errs):.3e}")
     assert max(errs) < 1e-4, errs
     assert torch.isfinite(Wp).all()
+
+
+@pytest.mark.parametrize("E,n,S,iters", [
+    (1, 5, 473, 50),   # 590 units over 256 workgroups: 2-3 streamed units each
+    (1, 5, 641, 20),   # 1200 units: 4-5 each
+    (2, 3, 129, 20),   # workgroups spanning two episodes
+    (6, 1, 65, 10),
+])
+def test_lds_streamed_units_equal_step_launches(dev, E, n, S, iters):
+    """The LDS-streamed form (each wave DMAs its 32-channel slice of the next unit into its own
+    LDS while the current unit is computed; per-episode register sums of the butterfly results)
+    forced on from 3 units per workgroup."""
+    h = (S - 1) // 8 + 1
+    f = torch.from_numpy(syn.normal(7, f"fs{E}{n}{S}", (E * n, 512, h, h), 0.1)).to(dev)
+    f = f.contiguous(memory_format=torch.channels_last)
+    lbl = torch.stack([torch.from_numpy(syn.make_episode(SEED, 90 + e, S, n)["s_label"][0]) for e in range(E)]).to(dev)
+    W0 = torch.from_numpy(syn.normal(8, f"ws{E}{n}{S}", (E, 2, 512), 0.04)).to(dev)
+    Wp = _run("2", f, lbl, W0, iters, upw="1" if E * n * ((h - 1) * ((h - 2) // 31 + 1)) > 256 else "2",
+              stream="1")
+    Ws = _run("0", f, lbl, W0, iters)
+    errs = [rel(Wp[e], Ws[e]) for e in range(E)]
+    print(f"stream E={E} n={n} S={S}: max rel {max(errs):.2e}")
+    assert max(errs) < 1e-4, errs
