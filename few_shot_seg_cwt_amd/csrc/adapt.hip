@@ -1251,6 +1251,19 @@ size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lb
   return 0;
 }
 
+// Which inner-loop kernel launch_adapt will use for this geometry (profile record names):
+// "adapt_persist_kernel<NRES" or "adapt_step_kernel<"
+const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw) {
+  int pG = 0, punits = 0, pncb = 0, pnres = 0, puc = 0;
+  const char* pe = getenv("CWT_ADAPT_PERSIST");
+  if (iters > 0 && !(pe && pe[0] == '0') && persist_geometry(E, n, h, w, upw, &pG, &punits, &pncb, &pnres, &puc) == 0) {
+    static const char* names[4] = {"adapt_persist_kernel<0", "adapt_persist_kernel<1", "adapt_persist_kernel<2",
+                                   "adapt_persist_kernel<3"};
+    return names[pnres & 3];
+  }
+  return "adapt_step_kernel<";
+}
+
 // E episodes of n shots each: f [E][n][h][w][512], lbl64 [E][n][S][S], W [E][2][512].
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
                  float* W, float* f_ws /*[E][n][h][w][512]*/, uint8_t* lbl_ws, AdaptScalars* sc /*[E] + partial counts*/,

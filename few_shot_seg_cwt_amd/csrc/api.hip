@@ -31,6 +31,7 @@ struct AdaptDevArgs;
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
                  float* W, float* f_ws, uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf,
                  AdaptDevArgs* dargs, AdaptGraphCache* cache, int upw, hipStream_t st);
+const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw);
 extern unsigned long long* g_adapt_stamps;
 extern long g_adapt_stamps_n;
 size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lbl, size_t* sc, size_t* acc,
@@ -957,7 +958,9 @@ int cwt_inner_adapt_batch(cwt_ctx* ctx, const float* f_s, const int64_t* s_label
   if ((rc = ensure_ws(ctx, "adapt.acc", b_acc, &acc))) return rc;  // [E][3][ADAPT_RMAX][512]
   if ((rc = ensure_ws(ctx, "adapt.wbuf", b_wb, &wb))) return rc;
   // algorithmic work: per step 2 x (2*2*C*h*w*n) FLOPs; minimal bytes = f_s + labels once per step
-  Prof p(ctx, (hipStream_t)stream, "inner_adapt x" + std::to_string(iters) + (E > 1 ? " E=" + std::to_string(E) : ""),
+  Prof p(ctx, (hipStream_t)stream,
+         "inner_adapt x" + std::to_string(iters) + (E > 1 ? " E=" + std::to_string(E) : "") + " [" +
+             adapt_kernel_name(E, n, h, w, iters, ctx->adapt_upw) + "]",
          (double)E * iters * 2.0 * (4.0 * C * h * w * n), (double)E * iters * ((double)n * h * w * C * 4 + (double)n * S * S),
          1);
   rc = launch_adapt(f_s, s_label, E, n, h, w, S, lr, iters, W_inout, (float*)fws, (uint8_t*)lbl, (AdaptScalars*)sc,
