@@ -58,6 +58,13 @@ SIGNATURES = {
     "cwt_cos_classify_bwd": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P]),
     "cwt_corr": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "cwt_sgd_step": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _I, _I, _P]),
+    "cwt_pretrain_create": (_I, [_P, _I, _I, _I, C.POINTER(C.c_char_p), C.POINTER(_P), C.POINTER(_I64), _F,
+                                 C.POINTER(_P)]),
+    "cwt_pretrain_destroy": (_I, [_P]),
+    "cwt_pretrain_step": (_I, [_P, _P, _P, _P, _I, _I, _P, _P, _P]),
+    "cwt_pretrain_forward": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
+    "cwt_pretrain_get": (_I, [_P, C.c_char_p, _I, _P, _I64]),
+    "cwt_pretrain_num_params": (_I, [_P, C.POINTER(_I64), C.POINTER(_I64)]),
     "cwt_cu_count": (_I, [_P, _P]),
     "cwt_stream_create_masked": (_I, [_P, _P, _I, _P]),
     "cwt_stream_destroy": (_I, [_P]),

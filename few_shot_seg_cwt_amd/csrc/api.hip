@@ -798,6 +798,9 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   return rc;
 }
 
+// device of a context (pretrain.hip)
+int ctx_device(const cwt_ctx* ctx) { return ctx->device; }
+
 }  // namespace cwt
 
 using namespace cwt;

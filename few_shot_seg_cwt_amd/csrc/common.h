@@ -79,7 +79,7 @@ __device__ __forceinline__ Lerp lerp_coord(int dst, int in_size, float scale) {
   r.l0 = 1.0f - r.l1;
   return r;
 }
-static inline float align_corners_scale(int in_size, int out_size) {
+__host__ __device__ static inline float align_corners_scale(int in_size, int out_size) {
   return out_size > 1 ? (float)(in_size - 1) / (float)(out_size - 1) : 0.0f;
 }
 

@@ -1,0 +1,208 @@
+"""Stage-1 pretraining of the PSPNet on HIP (reference src/pretrain.py).
+
+The reference trains the whole PSPNet on the base classes before the CWT stage: per iteration
+``model.train()``, ``loss = compute_loss(args, model, images, gt, num_classes_tr)`` (label-
+smoothed CE of the upsampled logits, pretrain.py:163-219), ``optimizer.zero_grad()``,
+``loss.backward()``, ``optimizer.step()`` (SGD with momentum / weight decay / nesterov over two
+parameter groups: layer0-4 at ``lr``, ppm / bottleneck / classifier at ``lr * scale_lr``,
+pretrain.py:60-72), and the cosine schedule per iteration (pretrain.py:118-119).
+
+Here :class:`PretrainPSPNet` holds the model on the device (libcwt ``cwt_pretrain``) and
+:meth:`PretrainPSPNet.train_step` is that whole iteration as one call: forward with training-mode
+BN, loss, backward of every conv / BN / PPM / classifier parameter and both SGD groups, in exact
+fp32 (f32 MFMA).  No torch op computes anything on this path; it raises without the library or a
+GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+from .synthetic import BN_EPS, pspnet_param_specs
+
+
+class PretrainHparams(C.Structure):
+    """cwt_pretrain_hparams (include/cwt.h)."""
+    _fields_ = [("lr", C.c_float), ("lr_head", C.c_float), ("momentum", C.c_float), ("weight_decay", C.c_float),
+                ("nesterov", C.c_int), ("smoothing", C.c_int), ("bn_momentum", C.c_float), ("drop_p", C.c_float),
+                ("seed", C.c_uint64), ("ignore_index", C.c_int)]
+
+
+def _arg(args, k, default=None):
+    if isinstance(args, dict):
+        return args.get(k, default)
+    return getattr(args, k, default)
+
+
+def cosine_lr(base_lr: float, it: int, total: int, eta_min: float = 1e-6) -> float:
+    """CosineAnnealingLR(optimizer, T_max=total, eta_min=1e-6) after ``it`` scheduler steps
+    (optimizer.py:33; stepped every iteration, pretrain.py:118-119), closed form."""
+    return eta_min + (base_lr - eta_min) * (1.0 + math.cos(math.pi * it / total)) / 2.0
+
+
+class PretrainPSPNet:
+    """``get_model(args)`` + ``get_optimizer(args, params_list)`` of pretrain.py:60-72 on HIP.
+
+    ``state_dict``: a PSPNet state dict with the reference key names (tensors or arrays);
+    ``classifier.weight`` is [num_classes_tr, 512, 1, 1].  ``state_dict()`` reads the trained
+    model back in the same names and layouts.
+    """
+
+    def __init__(self, args, state_dict, device=None):
+        self.layers = int(_arg(args, "layers", 50))
+        self.num_classes = int(_arg(args, "num_classes_tr", 16))
+        self.args = args
+        if device is None:
+            device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self._names, self._shapes = [], {}
+        names, arrs = [], []
+        for k, v in state_dict.items():
+            if k.endswith("num_batches_tracked") or k == "gamma":
+                continue
+            a = np.ascontiguousarray(v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v),
+                                     dtype=np.float32)
+            names.append(k)
+            arrs.append(a)
+            self._shapes[k] = a.shape
+        self._keep = arrs
+        cn = (C.c_char_p * len(names))(*[n.encode() for n in names])
+        cd = (C.c_void_p * len(names))(*[a.ctypes.data for a in arrs])
+        ce = (C.c_int64 * len(names))(*[a.size for a in arrs])
+        h = C.c_void_p()
+        _lib.check(_lib.lib().cwt_pretrain_create(_lib.ctx(self.device.index), self.layers, self.num_classes,
+                                                  len(names), cn, cd, ce, BN_EPS, C.byref(h)),
+                   "cwt_pretrain_create")
+        self._h = h
+        self._keep = None
+        self.loss = torch.zeros(1, device=self.device)
+        self.iteration = 0
+        self.training = True
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                _lib.lib().cwt_pretrain_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def train(self, mode: bool = True):
+        self.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def hparams(self, lr: float | None = None, seed: int = 0) -> PretrainHparams:
+        a = self.args
+        lr = float(_arg(a, "lr", 0.0025)) if lr is None else float(lr)
+        hp = PretrainHparams()
+        hp.lr = lr
+        hp.lr_head = lr * float(_arg(a, "scale_lr", 1.0))
+        hp.momentum = float(_arg(a, "momentum", 0.9))
+        hp.weight_decay = float(_arg(a, "weight_decay", 1e-4))
+        hp.nesterov = int(bool(_arg(a, "nesterov", False)))
+        hp.smoothing = int(bool(_arg(a, "smoothing", True)))
+        hp.bn_momentum = 0.1
+        hp.drop_p = float(_arg(a, "dropout", 0.1))
+        hp.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        hp.ignore_index = 255
+        return hp
+
+    def train_step(self, images: torch.Tensor, targets: torch.Tensor, lr: float | None = None, seed: int | None = None,
+                   hp: PretrainHparams | None = None) -> torch.Tensor:
+        """One iteration of pretrain.py:104-121: images [N, 3, S, S] fp32, targets [N, S, S]
+        int64 (255 ignored), both on the device.  Returns the loss (device scalar, the value
+        before the step)."""
+        _lib.require(images, "images")
+        _lib.require(targets, "targets", torch.int64)
+        if images.dim() != 4 or images.shape[1] != 3 or targets.shape != (images.shape[0], *images.shape[2:]):
+            raise ValueError("images must be [N,3,S,S] and targets [N,S,S]")
+        images, targets = images.contiguous(), targets.contiguous()
+        if hp is None:
+            hp = self.hparams(lr, self.iteration if seed is None else seed)
+        _lib.check(_lib.lib().cwt_pretrain_step(_lib.ctx(self.device.index), self._h, _lib.ptr(images),
+                                                _lib.ptr(targets), images.shape[0], images.shape[2],
+                                                C.addressof(hp), _lib.ptr(self.loss), _lib.stream_ptr(self.device)),
+                   "cwt_pretrain_step")
+        self.iteration += 1
+        return self.loss[0]
+
+    def logits(self, images: torch.Tensor) -> torch.Tensor:
+        """The classifier output before PSPNet.classify's upsample (pspnet.py:183-187) under the
+        current mode: [N, num_classes, h, h] in channels_last memory format."""
+        _lib.require(images, "images")
+        images = images.contiguous()
+        N, S = images.shape[0], images.shape[2]
+        h = (S - 1) // 8 + 1
+        out = torch.empty(N, h, h, self.num_classes, device=self.device)
+        _lib.check(_lib.lib().cwt_pretrain_forward(_lib.ctx(self.device.index), self._h, _lib.ptr(images), N, S,
+                                                   int(self.training), _lib.ptr(out), _lib.stream_ptr(self.device)),
+                   "cwt_pretrain_forward")
+        return out.permute(0, 3, 1, 2)
+
+    def _get(self, name: str, what: int, shape) -> torch.Tensor:
+        out = np.empty(shape, np.float32)
+        _lib.check(_lib.lib().cwt_pretrain_get(self._h, name.encode(), what, out.ctypes.data, out.size),
+                   f"cwt_pretrain_get({name})")
+        return torch.from_numpy(out)
+
+    def parameter_names(self):
+        return [n for n in self._shapes if not (n.endswith("running_mean") or n.endswith("running_var"))]
+
+    def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
+        """Host copy in the reference's names (parameters and BN running statistics)."""
+        sd = OrderedDict()
+        for n, shp in self._shapes.items():
+            if n.endswith("running_mean") or n.endswith("running_var"):
+                sd[n] = self._get(n, 3, shp)
+            else:
+                sd[n] = self._get(n, 0, shp)
+        return sd
+
+    def param(self, name: str) -> torch.Tensor:
+        """One parameter, host copy in PyTorch layout."""
+        return self._get(name, 0, self._shapes[name])
+
+    state_dict_entry = param
+
+    def running(self, name: str) -> torch.Tensor:
+        """``<bn>.running_mean`` / ``<bn>.running_var``."""
+        return self._get(name, 3, self._shapes[name])
+
+    def grad(self, name: str) -> torch.Tensor:
+        """The gradient of the last step (after zero_grad + backward, before the SGD update)."""
+        return self._get(name, 1, self._shapes[name])
+
+    def momentum_buffer(self, name: str) -> torch.Tensor:
+        return self._get(name, 2, self._shapes[name])
+
+    def num_params(self):
+        t, b = C.c_int64(), C.c_int64()
+        _lib.check(_lib.lib().cwt_pretrain_num_params(self._h, C.byref(t), C.byref(b)), "cwt_pretrain_num_params")
+        return t.value, b.value
+
+
+def synthetic_pretrain_state(layers: int = 50, num_classes: int = 16, seed: int = 2021):
+    """PRNG PSPNet state with a num_classes classifier (synthetic.make_pspnet_state)."""
+    from .synthetic import make_pspnet_state
+    return make_pspnet_state(layers=layers, seed=seed, num_classes_tr=num_classes)
+
+
+def train_epoch(model: PretrainPSPNet, batches, epoch: int, iters_per_epoch: int, epochs: int, base_lr: float):
+    """The inner loop of pretrain.py:104-121 over ``batches`` (an iterable of (images, gt)
+    device tensors) with the per-iteration cosine schedule; returns the running loss (the
+    reference's loss_meter average over the logged iterations is host-side bookkeeping)."""
+    losses = []
+    for i, (images, gt) in enumerate(batches):
+        it = epoch * iters_per_epoch + i
+        lr = cosine_lr(base_lr, it, iters_per_epoch * epochs)
+        losses.append(model.train_step(images, gt, lr=lr))
+    return torch.stack(losses).mean() if losses else torch.zeros(())

@@ -114,11 +114,11 @@ def _damped_bn(name: str) -> bool:
     return name.endswith(".bn3.weight") or name.endswith("downsample.1.weight")
 
 
-def make_pspnet_state(layers: int = 50, seed: int = 2021,
-                      bottleneck_dim: int = 512) -> "OrderedDict[str, np.ndarray]":
+def make_pspnet_state(layers: int = 50, seed: int = 2021, bottleneck_dim: int = 512,
+                      num_classes_tr: int = 2) -> "OrderedDict[str, np.ndarray]":
     """Synthetic frozen backbone: Kaiming(fan_in) convs, non-trivial eval-mode BN."""
     sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
-    for name, shape, kind in pspnet_param_specs(layers, bottleneck_dim):
+    for name, shape, kind in pspnet_param_specs(layers, bottleneck_dim, num_classes_tr):
         if kind == "gamma":
             sd[name] = np.array(0.2, dtype=np.float32)
         elif kind == "conv":

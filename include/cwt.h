@@ -305,6 +305,61 @@ int cwt_sgd_step(cwt_ctx* ctx, float* param, const float* grad, float* momentum_
                  void* stream);
 
 /*
+ * Stage-1 pretraining of the whole PSPNet (reference src/pretrain.py).
+ * A cwt_pretrain holds the trainable model: every parameter, its gradient and SGD momentum
+ * buffer in one flat fp32 device buffer each (layer0-4 = SGD group 1, ppm / bottleneck /
+ * classifier = group 2, pretrain.py:60-72), the BN running statistics, and the activations
+ * of the last forward.  All arithmetic is exact fp32 (f32 MFMA convs, weight gradients and
+ * input gradients), BN in training mode as model.train() (pretrain.py:106).
+ */
+typedef struct cwt_pretrain cwt_pretrain;
+
+typedef struct cwt_pretrain_hparams {
+  float lr;            /* group 1 (layer0-4): args.lr (scheduler value of this iteration) */
+  float lr_head;       /* group 2 (ppm, bottleneck, classifier): args.lr * args.scale_lr */
+  float momentum;      /* args.momentum (SGD, dampening 0) */
+  float weight_decay;  /* args.weight_decay (applied to every parameter, as torch.optim.SGD) */
+  int nesterov;        /* args.nesterov */
+  int smoothing;       /* args.smoothing: one-hot smoothed to 0.9 / 0.1 / (C - 1) (pretrain.py:197-199) */
+  float bn_momentum;   /* nn.BatchNorm2d momentum (0.1) */
+  float drop_p;        /* Dropout2d of the bottleneck (args.dropout; counter-based masks, seed below) */
+  uint64_t seed;
+  int ignore_index;    /* 255 */
+} cwt_pretrain_hparams;
+
+#define CWT_PT_PARAM 0
+#define CWT_PT_GRAD 1
+#define CWT_PT_MOMENTUM 2
+#define CWT_PT_RUNNING 3
+
+/* Replaces: get_model(args) + the SGD param groups (pretrain.py:60-72), from a PSPNet
+ * state_dict given by name as in cwt_backbone_load (classifier.weight [num_classes, 512, 1, 1],
+ * num_classes = args.num_classes_tr: 2, 16 or 61). */
+int cwt_pretrain_create(cwt_ctx* ctx, int layers, int num_classes, int n_tensors, const char* const* names,
+                        const float* const* host_data, const int64_t* numel, float bn_eps, cwt_pretrain** out);
+int cwt_pretrain_destroy(cwt_pretrain* pt);
+
+/* One training iteration (pretrain.py:104-121): model.train(); loss = compute_loss(...)
+ * (:182-219, mixup off); optimizer.zero_grad(); loss.backward(); optimizer.step().
+ * images device [N, 3, S, S] fp32 (NCHW, as the reference's loader yields), labels device
+ * [N, S, S] int64 (255 = ignore); N >= 2; (S - 1) % 8 == 0.  *loss_out (device float) = the
+ * loss before the step.  Gradients are left in place (CWT_PT_GRAD) until the next step. */
+int cwt_pretrain_step(cwt_ctx* ctx, cwt_pretrain* pt, const float* images, const int64_t* labels, int N, int S,
+                      const cwt_pretrain_hparams* hp, float* loss_out, void* stream);
+
+/* model(images) before the upsample (pspnet.py:147-156 with classify's conv only): logits
+ * device [N, h, h, num_classes] (NHWC), h = (S - 1) / 8 + 1.  train = 0: eval mode (running
+ * statistics); train = 1: batch statistics, running statistics untouched, no dropout. */
+int cwt_pretrain_forward(cwt_ctx* ctx, cwt_pretrain* pt, const float* images, int N, int S, int train,
+                         float* logits, void* stream);
+
+/* Host copy of one tensor in PyTorch layout by state_dict name: what = CWT_PT_PARAM, _GRAD,
+ * _MOMENTUM (a parameter name) or CWT_PT_RUNNING ("<bn>.running_mean" / ".running_var").
+ * Synchronises the device. */
+int cwt_pretrain_get(cwt_pretrain* pt, const char* name, int what, float* host_out, int64_t numel);
+int cwt_pretrain_num_params(const cwt_pretrain* pt, int64_t* total, int64_t* backbone);
+
+/*
  * Per-launch profiling (no reference counterpart; measurement support for bench.py).
  * level 1: the context records a hipEvent pair on the call's stream around each whole
  *          cwt_extract_features, its bottleneck conv (the largest single launch), the whole

@@ -1,0 +1,121 @@
+"""Stage-1 pretraining (reference src/pretrain.py:104-121, 163-219): the
+HIP iteration (PretrainPSPNet.train_step -> cwt_pretrain_step) against the oracle
+(oracle/pretrain_oracle.py: the reference's forward in torch autograd, SGD groups of :60-72).
+
+Compared per iteration: the loss, EVERY parameter gradient, every parameter after the SGD step,
+the momentum buffers and the BN running statistics; two iterations (the second exercises the
+momentum recurrence).  Training-mode BN over small batches amplifies rounding,
+so each tensor's bar is max(1e-3, 8 x the fp32 oracle's own distance to a float64 run of the
+same oracle) relative to the tensor's max |value|; the measured distances are printed."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from few_shot_seg_cwt_amd import synthetic as syn  # noqa: E402
+from dropout_ref import dropout_scale  # noqa: E402
+
+SEED = 2021
+BAR = 1e-3
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().numpy()
+    b = b.detach().double().cpu().numpy()
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def make_batch(N, S, nc, seed=SEED):
+    x = torch.from_numpy(syn.normal(seed, "pt_img", (N, 3, S, S), 1.0))
+    t = (syn.uniform01(seed, "pt_lbl", N * S * S) * nc).astype(np.int64).reshape(N, S, S)
+    ign = syn.uniform01(seed, "pt_ign", N * S * S).reshape(N, S, S) < 0.05
+    t[ign] = 255
+    return x, torch.from_numpy(t)
+
+
+def args(**over):
+    a = dict(layers=50, num_classes_tr=16, lr=0.0025, scale_lr=2.0, momentum=0.9, weight_decay=1e-4,
+             nesterov=True, smoothing=True, dropout=0.0)
+    a.update(over)
+    return a
+
+
+def run_case(dev, layers, N, S, nc, drop, steps=2):
+    from few_shot_seg_cwt_amd.pretrain import PretrainPSPNet
+    from oracle.pretrain_oracle import pretrain_step
+    a = args(layers=layers, num_classes_tr=nc, dropout=drop)
+    state = syn.make_pspnet_state(layers, SEED, num_classes_tr=nc)
+    model = PretrainPSPNet(a, state, dev)
+    sd32 = {k: torch.from_numpy(np.array(v, dtype=np.float32 if v.dtype != np.int64 else np.int64))
+            for k, v in state.items()}
+    sd64 = {k: (v.double() if v.dtype == torch.float32 else v) for k, v in sd32.items()}
+    b32, b64 = None, None
+    h = (S - 1) // 8 + 1
+    worst = {}
+    for it in range(steps):
+        x, t = make_batch(N, S, nc, SEED + it)
+        seed = 1000 + it
+        drop_scale = None
+        if drop > 0:
+            idx = np.arange(N * 512, dtype=np.uint64)
+            drop_scale = torch.from_numpy(dropout_scale(drop, seed, 3, idx).reshape(N, 512))
+        loss = model.train_step(x.to(dev), t.to(dev), lr=a["lr"], seed=seed)
+        torch.cuda.synchronize()
+        l32, g32, n32, b32 = pretrain_step(sd32, x, t, nc, layers, a["lr"], a["scale_lr"], a["momentum"],
+                                           a["weight_decay"], a["nesterov"], True, b32, drop_scale)
+        l64, g64, n64, b64 = pretrain_step(sd64, x.double(), t, nc, layers, a["lr"], a["scale_lr"], a["momentum"],
+                                           a["weight_decay"], a["nesterov"], True, b64,
+                                           None if drop_scale is None else drop_scale.double())
+        d_loss = abs(float(loss) - float(l64)) / abs(float(l64))
+        assert d_loss < max(BAR, 8 * abs(float(l32) - float(l64)) / abs(float(l64))), (it, float(loss), float(l64))
+        msgs = []
+        for k in g64:
+            for what, mine, o32, o64 in (("grad", model.grad(k), g32[k], g64[k]),
+                                         ("param", model.state_dict_entry(k), n32[k], n64[k]),
+                                         ("momentum", model.momentum_buffer(k), b32[k], b64[k])):
+                d = rel(mine, o64)
+                bar = max(BAR, 8 * rel(o32, o64))
+                worst[what] = max(worst.get(what, 0.0), d)
+                if not d < bar:
+                    msgs.append(f"it {it} {what} {k}: {d:.3g} (bar {bar:.3g})")
+        for k in [k for k in sd64 if k.endswith("running_mean") or k.endswith("running_var")]:
+            d = rel(model.running(k), sd64[k])
+            bar = max(BAR, 8 * rel(sd32[k], sd64[k]))
+            worst["running"] = max(worst.get("running", 0.0), d)
+            if not d < bar:
+                msgs.append(f"it {it} running {k}: {d:.3g} (bar {bar:.3g})")
+        assert not msgs, "\n".join(msgs[:20])
+        sd32.update(n32)
+        sd64.update(n64)
+    print(f"pretrain R{layers} N={N} S={S} nc={nc} drop={drop}: worst rel vs fp64 {worst}")
+
+
+@pytest.mark.parametrize("layers,N,S,nc,drop", [(50, 4, 65, 16, 0.0), (50, 2, 33, 61, 0.1), (101, 2, 33, 16, 0.0)])
+def test_pretrain_step_vs_oracle(dev, layers, N, S, nc, drop):
+    run_case(dev, layers, N, S, nc, drop)
+
+
+def test_pretrain_logits_eval_and_roundtrip(dev):
+    """eval-mode logits (running statistics) against the oracle; state_dict round trip."""
+    from few_shot_seg_cwt_amd.pretrain import PretrainPSPNet
+    from oracle.pretrain_oracle import pspnet_logits
+    state = syn.make_pspnet_state(50, SEED, num_classes_tr=16)
+    model = PretrainPSPNet(args(), state, dev).eval()
+    x, _ = make_batch(2, 33, 16)
+    lg = model.logits(x.to(dev))
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in state.items()}
+    with torch.no_grad():
+        ref = pspnet_logits(x.double(), {k: (v.double() if v.dtype == torch.float32 else v) for k, v in sd.items()},
+                            50, train=False)
+    assert rel(lg, ref) < 1e-4
+    back = model.state_dict()
+    for k, v in back.items():
+        assert np.array_equal(v.numpy(), np.asarray(state[k], np.float32)), k
