@@ -206,6 +206,97 @@ def spawn_ranks(n: int) -> int:
     return max((abs(c) for c in codes), default=0)
 
 
+def cpu_baseline_pretrain(layers, S, nc, budget_s: float = 25.0):
+    """The oracle's pretraining iteration (torch CPU fp32 autograd) on a bounded batch."""
+    from few_shot_seg_cwt_amd import synthetic as syn
+    from oracle.pretrain_oracle import pretrain_step
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = {k: torch.from_numpy(np.array(v)) for k, v in syn.make_pspnet_state(layers, 2021, num_classes_tr=nc).items()}
+    B = 2
+    x = torch.from_numpy(syn.normal(7, "cpu_pt", (B, 3, S, S), 1.0))
+    t = torch.from_numpy((syn.uniform01(7, "cpu_pt_l", B * S * S) * nc).astype(np.int64).reshape(B, S, S))
+    t0 = time.time()
+    n = 0
+    while n == 0 or (time.time() - t0 < budget_s and n < 3):
+        pretrain_step(sd, x, t, nc, layers)
+        n += 1
+    dt = time.time() - t0
+    return {"value": n * B / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} iterations of batch {B} ({S}x{S}, R{layers}, {nc} classes) through "
+                      f"oracle/pretrain_oracle.py pretrain_step (torch CPU fp32 autograd, {threads} threads); "
+                      f"s/iteration {dt / n:.2f}"}
+
+
+def main_pretrain(args, dev, rank, world, cdist):
+    """Stage-1 pretraining throughput: images/s of whole iterations
+    (forward with training BN, loss, backward of every parameter, both SGD groups).  Several
+    ranks run independent replicas (the reference's pretrain.py is single-process)."""
+    from few_shot_seg_cwt_amd import _lib
+    from few_shot_seg_cwt_amd import synthetic as syn
+    from few_shot_seg_cwt_amd.pretrain import PretrainPSPNet
+    _lib.load_library()
+    S, layers, B, nc = args.size, args.layers, args.batch, args.num_classes
+    cfg = dict(layers=layers, num_classes_tr=nc, lr=0.0025, scale_lr=2.0, momentum=0.9, weight_decay=1e-4,
+               nesterov=True, smoothing=True, dropout=0.1)
+    model = PretrainPSPNet(cfg, syn.make_pspnet_state(layers, 2021, num_classes_tr=nc), dev)
+    batches = []
+    for i in range(2):
+        x = torch.from_numpy(syn.normal(100 + rank * 10 + i, "pt_bench", (B, 3, S, S), 1.0)).to(dev)
+        # blocky labels: 8x8 regions of one class, 5 % ignored
+        lab = (syn.uniform01(200 + rank * 10 + i, "pt_lab", B * ((S + 7) // 8) ** 2) * nc).astype(np.int64)
+        lab = np.repeat(np.repeat(lab.reshape(B, (S + 7) // 8, (S + 7) // 8), 8, 1), 8, 2)[:, :S, :S].copy()
+        lab[syn.uniform01(300 + i, "pt_ign", B * S * S).reshape(B, S, S) < 0.05] = 255
+        batches.append((x, torch.from_numpy(lab).to(dev)))
+    for i in range(args.warmup):
+        model.train_step(*batches[i % 2], lr=0.0025)
+    torch.cuda.synchronize()
+    cdist.barrier()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(st)
+    losses = [model.train_step(*batches[i % 2], lr=0.0025) for i in range(args.steps)]
+    e1.record(st)
+    torch.cuda.synchronize()
+    cdist.barrier()
+    dt = cdist.all_reduce_max_scalar(time.perf_counter() - t0)
+    ev_ms = e0.elapsed_time(e1) / args.steps
+    flops_step = 3.0 * reference_conv_flops(layers, S) * B   # conv forward + input gradient + weight gradient
+    achieved = flops_step / (ev_ms * 1e-3) / 1e12
+    out = {
+        "metric": f"pretraining images/sec ({S}x{S}, R{layers} PSPNet, batch {B}, {nc} classes)",
+        "value": round(world * args.steps * B / dt, 3),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32 (exact f32 MFMA for every conv forward / input gradient / weight gradient)",
+        "data": "synthetic (PRNG weights, PRNG images, blocky PRNG labels)",
+        "config": {"workload": "stage-1 pretraining iteration (pretrain.py:104-121): model.train(), PSPNet "
+                               "forward, label-smoothed CE, backward of every parameter, SGD nesterov two groups",
+                   "image_size": S, "layers": layers, "batch": B, "num_classes_tr": nc,
+                   "parallelism": f"{world} independent replicas"},
+        "roofline": {"bound": "mfma", "kernel": "whole iteration (conv fwd + dgrad + wgrad FLOPs of the reference "
+                                                "formulation; PPM / BN / loss kernels in the time)",
+                     "achieved": round(achieved, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                     "flops_per_step": flops_step, "event_ms_per_step": round(ev_ms, 3)},
+        "loss_last": round(float(losses[-1]), 5),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_pretrain(layers, S, nc)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -226,6 +317,11 @@ def main():
     ap.add_argument("--train", action="store_true",
                     help="training episodes (do_epoch step: inner loop, CWT fwd/bwd, RCCL gradient all-reduce, SGD); "
                          "BASELINE config #4 is --train --layers 101 --size 641")
+    ap.add_argument("--pretrain", action="store_true",
+                    help="stage-1 pretraining iterations (pretrain.py:104-121: whole-PSPNet forward + backward + "
+                         "SGD, training BN, label-smoothed CE), batch --batch of --size images, --num-classes")
+    ap.add_argument("--batch", type=int, default=10, help="--pretrain: images per iteration (pascal_pretrain.yaml: 10)")
+    ap.add_argument("--num-classes", type=int, default=16, help="--pretrain: num_classes_tr (16 PASCAL, 61 COCO)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-json", default=None, help="write per-launch records here (rank 0)")
     args = ap.parse_args()
@@ -251,6 +347,8 @@ def main():
         return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.pretrain:
+        return main_pretrain(args, dev, rank, world, cdist)
 
     from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib, get_model
     from few_shot_seg_cwt_amd import synthetic as syn

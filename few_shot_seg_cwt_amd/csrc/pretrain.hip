@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/cwt.h"
+#include "../../include/cwt_debug.h"
 #include "common.h"
 #include "kernels.h"
 #include "pretrain.h"
@@ -482,7 +483,8 @@ static int pt_workspaces(cwt_pretrain* pt, PtStep& s) {
   const int N = pt->N;
   const long Ms = (long)N * pt->Hs * pt->Hs;
   int rc;
-  s.part_floats = ptbn_part_floats(Ms, 128);
+  const long M1 = (long)N * pt->H1 * pt->H1, Mh = (long)N * pt->h * pt->h;
+  s.part_floats = std::max({ptbn_part_floats(Ms, 128), ptbn_part_floats(M1, 256), ptbn_part_floats(Mh, 2048)});
   if ((rc = pt_ws(pt, "bnpart", s.part_floats * 4, &s.part))) return rc;
   if ((rc = pt_ws(pt, "bnsums", 2 * 4096 * 4, &s.sums))) return rc;
   // weight-gradient slabs: up to 32 M floats (128 MB)
@@ -870,3 +872,158 @@ int cwt_pretrain_num_params(const cwt_pretrain* pt, int64_t* total, int64_t* bac
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- single-op test hooks
+namespace cwt {
+static float* dbg_ws(size_t bytes) {
+  static void* p = nullptr;
+  static size_t have = 0;
+  if (have < bytes) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    have = 0;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    have = bytes;
+  }
+  return (float*)p;
+}
+}  // namespace cwt
+
+extern "C" int cwt_debug_pretrain_op(cwt_ctx* ctx, int op, void* const* b, const int64_t* ia, const float* fa,
+                                     void* stream) {
+  if (!ctx || !b || !ia) return fail(CWT_EARG, "null argument");
+  CWT_HIP(hipSetDevice(ctx_device(ctx)));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t wsf = (size_t)64 << 20;
+  float* ws = dbg_ws(wsf * 4);
+  if (!ws) return fail(CWT_ESTATE, "debug workspace allocation failed");
+  if (op == 0 || op == 1) {  // 0: weight gradient, 1: input gradient of a conv (ia: N Hi Ci Co k stride pad dil)
+    const int N = (int)ia[0], Hi = (int)ia[1], Ci = (int)ia[2], Co = (int)ia[3], k = (int)ia[4], s = (int)ia[5],
+              pad = (int)ia[6], dil = (int)ia[7];
+    const int Ho = (Hi + 2 * pad - dil * (k - 1) - 1) / s + 1;
+    if (op == 0) {
+      WgradArgs w;
+      std::memset(&w, 0, sizeof(w));
+      w.dy = (const float*)b[0];
+      w.dy_ld = Co;
+      w.x = (const float*)b[1];
+      w.x_ld = Ci;
+      w.N = N;
+      w.Hi = w.Wi = Hi;
+      w.Ho = w.Wo = Ho;
+      w.M = (long)N * Ho * Ho;
+      w.Co = Co;
+      w.K = k * k * Ci;
+      w.kh = w.kw = k;
+      w.stride = s;
+      w.pad = pad;
+      w.dil = dil;
+      return launch_conv_wgrad(w, (float*)b[2], ws, wsf, st);
+    }
+    // input gradient: transposed weights, zero-interleave (stride 2), stride-1 conv
+    float* wt = ws;
+    float* z = ws + (size_t)Co * Ci * k * k;
+    float* ones = z + (size_t)N * Hi * Hi * Co;
+    float* zeros = ones + 4096;
+    float* part = zeros + 4096;
+    std::vector<float> o(4096, 1.f);
+    CWT_HIP(hipMemcpyAsync(ones, o.data(), 4096 * 4, hipMemcpyHostToDevice, st));
+    CWT_HIP(hipMemsetAsync(zeros, 0, 4096 * 4, st));
+    int rc;
+    if ((rc = launch_wt_transpose((const float*)b[1], wt, Co, Ci, k * k, st))) return rc;
+    const float* src = (const float*)b[0];
+    if (s == 2) {
+      if ((rc = launch_zero_insert(src, N, Ho, Ho, Co, z, Hi, Hi, st))) return rc;
+      src = z;
+    }
+    ConvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.x = src;
+    a.w = wt;
+    a.scale = ones;
+    a.shift = zeros;
+    a.y = (float*)b[2];
+    a.N = N;
+    a.Hi = a.Wi = Hi;
+    a.Ci = Co;
+    a.Co = Ci;
+    a.x_ld = Co;
+    a.kh = a.kw = k;
+    a.stride = 1;
+    a.pad = dil * (k - 1) - pad;
+    a.dil = dil;
+    a.Ho = a.Wo = Hi;
+    a.M = N * Hi * Hi;
+    a.K = k * k * Co;
+    a.y_ld = Ci;
+    const ConvPlan pl = plan_conv(a.M, a.Co, a.K);
+    const size_t left = wsf - (size_t)(part - ws);
+    return launch_conv(a, pl, 0, part, left, st);
+  }
+  if (op == 2) {  // label-smoothed CE: b = logits, target, dlogits, loss; ia = N S h nc; fa = on off
+    PtLoss L;
+    std::memset(&L, 0, sizeof(L));
+    L.logits = (const float*)b[0];
+    L.target = (const int64_t*)b[1];
+    L.dlogits = (float*)b[2];
+    L.N = (int)ia[0];
+    L.S = (int)ia[1];
+    L.h = L.w = (int)ia[2];
+    L.nc = (int)ia[3];
+    L.ignore = 255;
+    L.on = fa[0];
+    L.off = fa[1];
+    return launch_seg_ce_smooth(L, ws, wsf * 4, (float*)b[3], st);
+  }
+  if (op == 3) {  // BN train fwd + ReLU, then backward: b = y gamma beta out dout dy dgamma dbeta; ia = M C
+    const long M = (long)ia[0];
+    const int Cc = (int)ia[1];
+    float* run = ws;
+    float* stats = run + 2 * Cc;
+    float* sums = stats + 2 * Cc;
+    float* part = sums + 2 * Cc;
+    CWT_HIP(hipMemsetAsync(run, 0, (size_t)2 * Cc * 4, st));
+    int rc;
+    if ((rc = launch_ptbn_fwd((const float*)b[0], Cc, M, Cc, run, fa ? fa[0] : 1e-5f, 0.1f, 1, stats, part,
+                              wsf - 6 * Cc, st)))
+      return rc;
+    PtBnApply ap;
+    std::memset(&ap, 0, sizeof(ap));
+    ap.y = (const float*)b[0];
+    ap.y_ld = Cc;
+    ap.M = M;
+    ap.C = Cc;
+    ap.gamma = (const float*)b[1];
+    ap.beta = (const float*)b[2];
+    ap.stats = stats;
+    ap.relu = 1;
+    ap.rows_per_image = 1;
+    ap.out = (float*)b[3];
+    ap.out_ld = Cc;
+    if ((rc = launch_ptbn_apply(ap, st))) return rc;
+    PtBnBwd bw;
+    std::memset(&bw, 0, sizeof(bw));
+    bw.dout = (const float*)b[4];
+    bw.dout_ld = Cc;
+    bw.act = (const float*)b[3];
+    bw.act_ld = Cc;
+    bw.rows_per_image = 1;
+    bw.y = (const float*)b[0];
+    bw.y_ld = Cc;
+    bw.gamma = (const float*)b[1];
+    bw.stats = stats;
+    bw.M = M;
+    bw.C = Cc;
+    bw.dy = (float*)b[5];
+    bw.dy_ld = Cc;
+    return launch_ptbn_bwd(bw, (float*)b[6], (float*)b[7], part, wsf - 6 * Cc, sums, st);
+  }
+  if (op == 4) {  // max pool 3x3 s2 p1 forward + adjoint: b = in out dout din; ia = N H C
+    const int N = (int)ia[0], H = (int)ia[1], Cc = (int)ia[2];
+    const int Ho = (H - 1) / 2 + 1;
+    int rc;
+    if ((rc = launch_maxpool_idx((const float*)b[0], N, H, Cc, (float*)b[1], (uint8_t*)ws, Ho, st))) return rc;
+    return launch_maxpool_bwd((const float*)b[2], (const uint8_t*)ws, N, H, Cc, Ho, (float*)b[3], st);
+  }
+  return fail(CWT_EARG, "unknown op");
+}

