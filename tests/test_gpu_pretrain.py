@@ -22,6 +22,7 @@ from dropout_ref import dropout_scale  # noqa: E402
 
 SEED = 2021
 BAR = 1e-3
+NPERT = 4
 
 
 def rel(a, b):
@@ -80,26 +81,31 @@ def run_case(dev, layers, N, S, nc, drop, steps=2):
         l64, g64, n64, b64 = pretrain_step(sd64, x.double(), t, nc, layers, a["lr"], a["scale_lr"], a["momentum"],
                                            a["weight_decay"], a["nesterov"], True, b64,
                                            None if drop_scale is None else drop_scale.double())
-        # the same fp32 oracle on a 1e-7-perturbed input (running statistics on a copy)
-        sdp = {k: v.clone() for k, v in sd32_prev.items()}
-        xp = x * (1 + 1e-7 * torch.from_numpy(syn.normal(SEED + it, "pt_pert", tuple(x.shape), 1.0)))
-        _, gp, np_, bp = pretrain_step(sdp, xp, t, nc, layers, a["lr"], a["scale_lr"], a["momentum"],
-                                       a["weight_decay"], a["nesterov"], True, bprev, drop_scale)
+        # the same fp32 oracle on NPERT 1e-7-perturbed inputs (running statistics on copies): the
+        # spread is often bimodal (a ReLU / BN-branch flip moves a tensor by ~0.1 or not at all)
+        perts = []
+        for pi in range(NPERT):
+            sdp = {k: v.clone() for k, v in sd32_prev.items()}
+            xp = x * (1 + 1e-7 * torch.from_numpy(syn.normal(SEED + 97 * it + pi, "pt_pert", tuple(x.shape), 1.0)))
+            _, gp, np_, bp = pretrain_step(sdp, xp, t, nc, layers, a["lr"], a["scale_lr"], a["momentum"],
+                                           a["weight_decay"], a["nesterov"], True, bprev, drop_scale)
+            perts.append((sdp, gp, np_, bp))
         d_loss = abs(float(loss) - float(l64)) / abs(float(l64))
         assert d_loss < max(BAR, 8 * abs(float(l32) - float(l64)) / abs(float(l64))), (it, float(loss), float(l64))
         msgs = []
         for k in g64:
-            for what, mine, o32, o64, op in (("grad", model.grad(k), g32[k], g64[k], gp[k]),
-                                             ("param", model.state_dict_entry(k), n32[k], n64[k], np_[k]),
-                                             ("momentum", model.momentum_buffer(k), b32[k], b64[k], bp[k])):
+            for what, mine, o32, o64, j in (("grad", model.grad(k), g32[k], g64[k], 1),
+                                            ("param", model.state_dict_entry(k), n32[k], n64[k], 2),
+                                            ("momentum", model.momentum_buffer(k), b32[k], b64[k], 3)):
                 d = rel(mine, o64)
-                bar = max(BAR, 8 * max(rel(o32, o64), rel(op, o32)))
+                spread = max([rel(o32, o64)] + [rel(p[j][k], o32) for p in perts])
+                bar = max(BAR, 8 * spread)
                 worst[what] = max(worst.get(what, 0.0), d)
                 if not d < bar:
                     msgs.append(f"it {it} {what} {k}: {d:.3g} (bar {bar:.3g})")
         for k in [k for k in sd64 if k.endswith("running_mean") or k.endswith("running_var")]:
             d = rel(model.running(k), sd64[k])
-            bar = max(BAR, 8 * max(rel(sd32[k], sd64[k]), rel(sdp[k], sd32[k])))
+            bar = max(BAR, 8 * max([rel(sd32[k], sd64[k])] + [rel(p[0][k], sd32[k]) for p in perts]))
             worst["running"] = max(worst.get("running", 0.0), d)
             if not d < bar:
                 msgs.append(f"it {it} running {k}: {d:.3g} (bar {bar:.3g})")
