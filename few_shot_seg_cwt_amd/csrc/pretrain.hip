@@ -604,7 +604,7 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
     const long Mb = (long)N * b * b;
     PtConv& L = pt->ppm[i];
     const float* pool = pt->POOL + base * N * 2048;
-    if ((rc = launch_ppm_upsample_bwd(dcat, 4096, 2048 + 512 * i, N, b, h, gT, s.st)) ||
+    if ((rc = launch_ppm_upsample_bwd(dcat, 4096, 2048 + 512 * i, N, b, h, gT, s.slab, s.st)) ||
         (rc = s.bn_bwd(L, Mb, gT, 512, L.a, 512, gY)) ||
         (rc = s.gemm(gY, 1, 512, pool, 2048, 1, pt->G + L.w_off, 2048, 512, 2048, Mb)) ||
         (rc = s.gemm(gY, 512, 1, pt->P + L.w_off, 2048, 1, dpool + base * N * 2048, 2048, (int)Mb, 2048, 512)))

@@ -303,25 +303,36 @@ int launch_stem1_wgrad(const float* img, int N, int S, const float* dy, int Ho, 
 //            dgamma = sum g * xhat, dbeta = sum g,
 //            dy = gamma * istd * (g - dbeta / M - xhat * dgamma / M).
 // ------------------------------------------------------------------------------------------
-constexpr int kRows = 256;
+// Row blocking of the per-channel reductions: at most kBnBlocks blocks of >= 256 rows (the
+// per-channel merge over the blocks then stays short), 4 row groups x 64 channels per block.
+constexpr int kBnBlocks = 128;
+static inline int bn_nblk(long M) { return (int)std::min<long>(kBnBlocks, cdiv(M, 256L)); }
+static inline long bn_rows_per_blk(long M) { return ((M + bn_nblk(M) - 1) / bn_nblk(M) + 3) & ~3L; }
 
-__global__ __launch_bounds__(256) void ptbn_stats_kernel(const float* __restrict__ y, int ld, long M, int C,
+// per (row block, channel): n, mean, M2 from shifted sums (shift = the thread's first value, no
+// per-element division), the 4 row groups merged by Chan's formula
+__global__ __launch_bounds__(256) void ptbn_stats_kernel(const float* __restrict__ y, int ld, long M, int C, long rpb,
                                                          float* __restrict__ part) {
   __shared__ float sn[4][64], sm[4][64], sq[4][64];
   const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + lane;
-  const long r0 = (long)blockIdx.x * kRows;
+  const long r0 = (long)blockIdx.x * rpb, r1 = std::min(M, r0 + rpb);
   float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (c < C)
-    for (int i = rg; i < kRows; i += 4) {
-      const long r = r0 + i;
-      if (r >= M) break;
-      const float v = y[r * ld + c];
-      n += 1.f;
-      const float d = v - mean;
-      mean += d / n;
-      m2 += d * (v - mean);
+  if (c < C && r0 + rg < r1) {
+    const float K = y[(r0 + rg) * ld + c];
+    float s1 = 0.f, s2 = 0.f;
+    int k = 0;
+#pragma unroll 4
+    for (long r = r0 + rg; r < r1; r += 4) {
+      const float d = y[r * ld + c] - K;
+      s1 += d;
+      s2 = fmaf(d, d, s2);
+      ++k;
     }
+    n = (float)k;
+    mean = K + s1 / n;
+    m2 = fmaxf(s2 - s1 * (s1 / n), 0.f);
+  }
   sn[rg][lane] = n;
   sm[rg][lane] = mean;
   sq[rg][lane] = m2;
@@ -372,7 +383,7 @@ __global__ void ptbn_finalize_kernel(const float* __restrict__ part, int nblk, i
 
 // out = [relu](gamma (y - mu) istd + beta [+ res]) (the residual itself a raw conv output under
 // its own BN when res_stats != null); drop_p > 0: Dropout2d (image, channel) mask after the ReLU,
-// the pre-dropout value kept in out_pre (the ReLU mask of the backward).  8 channels per thread.
+// the pre-dropout value kept in out_pre (the ReLU mask of the backward).  4 channels per thread.
 __global__ __launch_bounds__(256) void ptbn_apply_kernel(PtBnApply a) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cg = a.C >> 2;
@@ -410,18 +421,17 @@ __device__ __forceinline__ float ptbn_grad_at(const PtBnBwd& a, long row, int c)
   return g;
 }
 
-// per (256-row block, channel) partial sums of g and g * xhat (fixed order)
-__global__ __launch_bounds__(256) void ptbn_bwd_stats_kernel(PtBnBwd a, float* __restrict__ part) {
+// per (row block, channel) partial sums of g and g * xhat (fixed order)
+__global__ __launch_bounds__(256) void ptbn_bwd_stats_kernel(PtBnBwd a, long rpb, float* __restrict__ part) {
   __shared__ float s1[4][64], s2[4][64];
   const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + lane;
-  const long r0 = (long)blockIdx.x * kRows;
+  const long r0 = (long)blockIdx.x * rpb, r1 = std::min(a.M, r0 + rpb);
   float sg = 0.f, sgx = 0.f;
   if (c < a.C) {
     const float mu = a.stats[c], is = a.stats[a.C + c];
-    for (int i = rg; i < kRows; i += 4) {
-      const long r = r0 + i;
-      if (r >= a.M) break;
+#pragma unroll 4
+    for (long r = r0 + rg; r < r1; r += 4) {
       const float g = ptbn_grad_at(a, r, c);
       sg += g;
       sgx = fmaf(g, (a.y[r * a.y_ld + c] - mu) * is, sgx);
@@ -457,32 +467,46 @@ __global__ void ptbn_bwd_finalize_kernel(const float* __restrict__ part, int nbl
 }
 
 // dy = gamma istd (g - sum_g / M - xhat sum_gx / M); optionally g itself into g_out (the
-// gradient of an identity residual)
+// gradient of an identity residual).  4 channels per thread.
 __global__ __launch_bounds__(256) void ptbn_bwd_apply_kernel(PtBnBwd a, const float* __restrict__ sums) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= a.M * a.C) return;
-  const long row = idx / a.C;
-  const int c = (int)(idx - row * a.C);
-  const float g = ptbn_grad_at(a, row, c);
-  const float mu = a.stats[c], is = a.stats[a.C + c];
+  const int cg = a.C >> 2;
+  if (idx >= a.M * cg) return;
+  const long row = idx / cg;
+  const int c0 = (int)(idx - row * cg) * 4;
+  f32x4 g = *(const f32x4*)(a.dout + row * a.dout_ld + c0);
+  const f32x4 y = *(const f32x4*)(a.y + row * a.y_ld + c0);
+  f32x4 act = {1.f, 1.f, 1.f, 1.f};
+  if (a.act) act = *(const f32x4*)(a.act + row * a.act_ld + c0);
   const float inv_m = 1.0f / (float)a.M;
-  const float xh = (a.y[row * a.y_ld + c] - mu) * is;
-  a.dy[row * a.dy_ld + c] = a.gamma[c] * is * (g - sums[c] * inv_m - xh * (sums[a.C + c] * inv_m));
-  if (a.g_out) a.g_out[row * a.g_ld + c] = g;
+  const long img = row / a.rows_per_image;
+  f32x4 dy;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = c0 + q;
+    if (a.drop_p > 0.f) g[q] *= dropout_scale(a.drop_p, a.seed, 3, (unsigned long long)img * a.C + c);
+    if (!(act[q] > 0.f)) g[q] = 0.f;
+    const float mu = a.stats[c], is = a.stats[a.C + c];
+    const float xh = (y[q] - mu) * is;
+    dy[q] = a.gamma[c] * is * (g[q] - sums[c] * inv_m - xh * (sums[a.C + c] * inv_m));
+  }
+  *(f32x4*)(a.dy + row * a.dy_ld + c0) = dy;
+  if (a.g_out) *(f32x4*)(a.g_out + row * a.g_ld + c0) = g;
 }
 
-size_t ptbn_part_floats(long M, int C) { return (size_t)3 * cdiv(M, (long)kRows) * C; }
+size_t ptbn_part_floats(long M, int C) { return (size_t)3 * bn_nblk(M) * C; }
 
 int launch_ptbn_fwd(const float* y, int ld, long M, int C, float* run, float eps, float momentum, int train,
                     float* stats, float* part, size_t part_floats, hipStream_t st) {
   if (train && M < 2) return fail(CWT_EARG, "Expected more than 1 value per channel when training (BatchNorm2d)");
-  const int nblk = (int)cdiv(M, (long)kRows);
+  const int nblk = bn_nblk(M);
   if (train) {
     if (ptbn_part_floats(M, C) > part_floats) return fail(CWT_ESTATE, "ptbn: partial workspace too small");
-    hipLaunchKernelGGL(ptbn_stats_kernel, dim3(nblk, cdiv(C, 64)), dim3(256), 0, st, y, ld, M, C, part);
+    hipLaunchKernelGGL(ptbn_stats_kernel, dim3(nblk, cdiv(C, 64)), dim3(256), 0, st, y, ld, M, C, bn_rows_per_blk(M),
+                       part);
     CWT_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(ptbn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, (const float*)part, nblk, C, run, eps,
+  hipLaunchKernelGGL(ptbn_finalize_kernel, dim3(cdiv(C, 64)), dim3(64), 0, st, (const float*)part, nblk, C, run, eps,
                      momentum, train, stats);
   CWT_LAUNCH_CHECK();
   return 0;
@@ -498,14 +522,17 @@ int launch_ptbn_apply(const PtBnApply& a, hipStream_t st) {
 
 int launch_ptbn_bwd(const PtBnBwd& a, float* dgamma, float* dbeta, float* part, size_t part_floats, float* sums,
                     hipStream_t st) {
-  const int nblk = (int)cdiv(a.M, (long)kRows);
+  if (a.C % 4 || a.dout_ld % 4 || a.y_ld % 4 || a.dy_ld % 4 || (a.act && a.act_ld % 4) || (a.g_out && a.g_ld % 4))
+    return fail(CWT_EARG, "ptbn_bwd: alignment");
+  const int nblk = bn_nblk(a.M);
   if ((size_t)2 * nblk * a.C > part_floats) return fail(CWT_ESTATE, "ptbn_bwd: partial workspace too small");
-  hipLaunchKernelGGL(ptbn_bwd_stats_kernel, dim3(nblk, cdiv(a.C, 64)), dim3(256), 0, st, a, part);
+  hipLaunchKernelGGL(ptbn_bwd_stats_kernel, dim3(nblk, cdiv(a.C, 64)), dim3(256), 0, st, a, bn_rows_per_blk(a.M), part);
   CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ptbn_bwd_finalize_kernel, dim3(cdiv(a.C, 256)), dim3(256), 0, st, (const float*)part, nblk, a.C,
+  hipLaunchKernelGGL(ptbn_bwd_finalize_kernel, dim3(cdiv(a.C, 64)), dim3(64), 0, st, (const float*)part, nblk, a.C,
                      dgamma, dbeta, sums);
   CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ptbn_bwd_apply_kernel, dim3(cdiv(a.M * a.C, 256)), dim3(256), 0, st, a, (const float*)sums);
+  const long total = a.M * (a.C / 4);
+  hipLaunchKernelGGL(ptbn_bwd_apply_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, a, (const float*)sums);
   CWT_LAUNCH_CHECK();
   return 0;
 }
@@ -600,60 +627,85 @@ __global__ void ppm_upsample_kernel(const float* __restrict__ P, int N, int b, i
   *(f32x4*)(cat + p * ld + off + 4 * c4) = o;
 }
 
-// one thread per (n, cell, channel); loops over the rows / columns whose interpolation touches the cell
-__global__ void ppm_upsample_bwd_kernel(const float* __restrict__ dcat, int ld, int off, int N, int b, int h,
-                                        float* __restrict__ dP) {
-  const long total = (long)N * b * b * 512;
+// adjoint of the upsample in two separable passes (f32x4 over channels):
+//   R[n][y][j][c] = sum_x u_x(j) dcat[n][y][x][off + c]     (thread per (n, y, j, c4))
+//   dP[n][i][j][c] = sum_y u_y(i) R[n][y][j][c]              (thread per (n, i, j, c4))
+// the loops run over the full row / column with the weight test (h <= ~80, b <= 6)
+__global__ void ppm_upsample_bwd_x_kernel(const float* __restrict__ dcat, int ld, int off, int N, int b, int h,
+                                          float* __restrict__ R) {
+  const long total = (long)N * h * b * 128;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int c = (int)(i & 511);
-  const long cell = i >> 9;
+  const int c4 = (int)(i & 127);
+  const long p = i >> 7;
+  const int j = (int)(p % b), y = (int)((p / b) % h), n = (int)(p / ((long)b * h));
+  const float sc = align_corners_scale(b, h);
+  const float* row = dcat + (((long)n * h + y) * h) * ld + off + 4 * c4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int x = 0; x < h; ++x) {
+    const Lerp lx = lerp_coord(x, b, sc);
+    const float wx = (lx.i0 == j ? lx.l0 : 0.f) + (lx.i1 == j ? lx.l1 : 0.f);
+    if (wx == 0.f) continue;
+    const f32x4 v = *(const f32x4*)(row + (long)x * ld);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] = fmaf(wx, v[q], s[q]);
+  }
+  *(f32x4*)(R + p * 512 + 4 * c4) = s;
+}
+
+__global__ void ppm_upsample_bwd_y_kernel(const float* __restrict__ R, int N, int b, int h, float* __restrict__ dP) {
+  const long total = (long)N * b * b * 128;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c4 = (int)(i & 127);
+  const long cell = i >> 7;
   const int j = (int)(cell % b), ii = (int)((cell / b) % b), n = (int)(cell / ((long)b * b));
   const float sc = align_corners_scale(b, h);
-  float s = 0.f;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
   for (int y = 0; y < h; ++y) {
     const Lerp ly = lerp_coord(y, b, sc);
     const float wy = (ly.i0 == ii ? ly.l0 : 0.f) + (ly.i1 == ii ? ly.l1 : 0.f);
     if (wy == 0.f) continue;
-    float sr = 0.f;
-    for (int x = 0; x < h; ++x) {
-      const Lerp lx = lerp_coord(x, b, sc);
-      const float wx = (lx.i0 == j ? lx.l0 : 0.f) + (lx.i1 == j ? lx.l1 : 0.f);
-      if (wx == 0.f) continue;
-      sr = fmaf(wx, dcat[(((long)n * h + y) * h + x) * ld + off + c], sr);
-    }
-    s = fmaf(wy, sr, s);
+    const f32x4 v = *(const f32x4*)(R + (((long)n * h + y) * b + j) * 512 + 4 * c4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] = fmaf(wy, v[q], s[q]);
   }
-  dP[i] = s;
+  *(f32x4*)(dP + cell * 512 + 4 * c4) = s;
 }
 
-// pooled gradient rows bin-major as launch_ppm writes them: bin k's rows [base_k N, (base_k + b^2) N)
+// pooled gradient rows bin-major as launch_ppm writes them: bin k's rows [base_k N, (base_k + b^2) N);
+// 4 channels per thread, only the windows near (y, x) b / h per bin and axis visited
 __global__ void avgpool_bwd_kernel(const float* __restrict__ dpool, int N, int h, int C, int b0, int b1, int b2, int b3,
                                    float* __restrict__ dx, int ld) {
-  const long total = (long)N * h * h * C;
+  const int cg = C >> 2;
+  const long total = (long)N * h * h * cg;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int c = (int)(i % C);
-  const long p = i / C;
+  const int c0 = (int)(i % cg) * 4;
+  const long p = i / cg;
   const int x = (int)(p % h), y = (int)((p / h) % h), n = (int)(p / ((long)h * h));
   const int bins[4] = {b0, b1, b2, b3};
-  float s = 0.f;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
   int base = 0;
   for (int k = 0; k < 4; ++k) {
     const int b = bins[k];
-    for (int ci = 0; ci < b; ++ci) {
+    const int cy = (y * b) / h, cx = (x * b) / h;  // windows [floor(i h / b), ceil((i+1) h / b)) near y / b * h
+    for (int ci = max(0, cy - 2); ci <= min(b - 1, cy + 2); ++ci) {
       const int ya = (ci * h) / b, yb = ((ci + 1) * h + b - 1) / b;
       if (y < ya || y >= yb) continue;
-      for (int cj = 0; cj < b; ++cj) {
+      for (int cj = max(0, cx - 2); cj <= min(b - 1, cx + 2); ++cj) {
         const int xa = (cj * h) / b, xb = ((cj + 1) * h + b - 1) / b;
         if (x < xa || x >= xb) continue;
-        const float g = dpool[((long)base * N + (long)n * b * b + ci * b + cj) * C + c];
-        s += g / (float)(yb - ya) / (float)(xb - xa);
+        const f32x4 g = *(const f32x4*)(dpool + ((long)base * N + (long)n * b * b + ci * b + cj) * C + c0);
+        const float kh = (float)(yb - ya), kw = (float)(xb - xa);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[q] += g[q] / kh / kw;
       }
     }
     base += b * b;
   }
-  dx[p * ld + c] += s;
+  f32x4* d = (f32x4*)(dx + p * ld + c0);
+  *d = *d + s;
 }
 
 int launch_ppm_upsample(const float* P, int N, int b, int h, float* cat, int ld, int off, hipStream_t st) {
@@ -663,15 +715,19 @@ int launch_ppm_upsample(const float* P, int N, int b, int h, float* cat, int ld,
   return 0;
 }
 
-int launch_ppm_upsample_bwd(const float* dcat, int ld, int off, int N, int b, int h, float* dP, hipStream_t st) {
-  const long total = (long)N * b * b * 512;
-  hipLaunchKernelGGL(ppm_upsample_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, dcat, ld, off, N, b, h, dP);
+int launch_ppm_upsample_bwd(const float* dcat, int ld, int off, int N, int b, int h, float* dP, float* ws,
+                            hipStream_t st) {
+  const long t1 = (long)N * h * b * 128, t2 = (long)N * b * b * 128;
+  hipLaunchKernelGGL(ppm_upsample_bwd_x_kernel, dim3(cdiv(t1, 256)), dim3(256), 0, st, dcat, ld, off, N, b, h, ws);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ppm_upsample_bwd_y_kernel, dim3(cdiv(t2, 256)), dim3(256), 0, st, (const float*)ws, N, b, h, dP);
   CWT_LAUNCH_CHECK();
   return 0;
 }
 
 int launch_avgpool_bwd(const float* dpool, int N, int h, int C, const int* bins, float* dx, int ld, hipStream_t st) {
-  const long total = (long)N * h * h * C;
+  if (C % 4 || ld % 4) return fail(CWT_EARG, "avgpool_bwd: alignment");
+  const long total = (long)N * h * h * (C / 4);
   hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, dpool, N, h, C, bins[0], bins[1],
                      bins[2], bins[3], dx, ld);
   CWT_LAUNCH_CHECK();
