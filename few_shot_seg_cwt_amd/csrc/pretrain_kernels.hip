@@ -365,14 +365,24 @@ __global__ void ptbn_finalize_kernel(const float* __restrict__ part, int nblk, i
   }
   const long plane = (long)nblk * C;
   double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    const double nb = part[(long)b * C + c];
-    if (nb == 0.0) continue;
-    const double mb = part[plane + (long)b * C + c], qb = part[2 * plane + (long)b * C + c];
-    const double nt = n + nb, d = mb - mean;
-    mean += d * (nb / nt);
-    m2 += qb + d * d * (n * nb / nt);
-    n = nt;
+  for (int b0 = 0; b0 < nblk; b0 += 8) {  // 8 blocks' partials loaded together, merged in block order
+    float pn[8], pm[8], pq[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const long o = (long)min(b0 + k, nblk - 1) * C + c;
+      pn[k] = b0 + k < nblk ? part[o] : 0.f;
+      pm[k] = part[plane + o];
+      pq[k] = part[2 * plane + o];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const double nb = pn[k];
+      if (nb == 0.0) continue;
+      const double nt = n + nb, d = (double)pm[k] - mean;
+      mean += d * (nb / nt);
+      m2 += (double)pq[k] + d * d * (n * nb / nt);
+      n = nt;
+    }
   }
   const float mu = (float)mean, var_b = (float)(m2 / n);
   stats[c] = mu;
@@ -456,9 +466,19 @@ __global__ void ptbn_bwd_finalize_kernel(const float* __restrict__ part, int nbl
   if (c >= C) return;
   const long plane = (long)nblk * C;
   double sg = 0.0, sgx = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    sg += part[(long)b * C + c];
-    sgx += part[plane + (long)b * C + c];
+  for (int b0 = 0; b0 < nblk; b0 += 8) {
+    float p1[8], p2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const long o = (long)min(b0 + k, nblk - 1) * C + c;
+      p1[k] = b0 + k < nblk ? part[o] : 0.f;
+      p2[k] = b0 + k < nblk ? part[plane + o] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sg += p1[k];
+      sgx += p2[k];
+    }
   }
   dbeta[c] = (float)sg;
   dgamma[c] = (float)sgx;
