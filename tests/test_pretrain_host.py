@@ -1,0 +1,66 @@
+"""Host-side pieces of stage-1 pretraining (CPU): the per-iteration cosine schedule against
+torch's CosineAnnealingLR (optimizer.py:33, stepped every iteration, pretrain.py:118-119), the
+oracle's SGD groups against torch.optim.SGD over the same two groups (pretrain.py:60-72), and
+the product path refusing to run without a device (no CPU fallback)."""
+import numpy as np
+import pytest
+import torch
+
+from few_shot_seg_cwt_amd import synthetic as syn
+
+
+def test_cosine_lr_matches_torch():
+    from few_shot_seg_cwt_amd.pretrain import cosine_lr
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.SGD([p], lr=0.0025, momentum=0.9)
+    T = 37
+    sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T, eta_min=1e-6)
+    for it in range(T):
+        assert abs(opt.param_groups[0]["lr"] - cosine_lr(0.0025, it, T)) < 1e-12
+        opt.step()
+        sch.step()
+
+
+def test_oracle_sgd_groups_match_torch():
+    from oracle.pretrain_oracle import is_head
+    gen = torch.Generator().manual_seed(3)
+    names = ["layer1.0.conv1.weight", "layer4.2.bn3.bias", "ppm.features.0.1.weight", "bottleneck.1.weight",
+             "classifier.weight"]
+    params = {n: torch.randn(5, generator=gen) for n in names}
+    tp = {n: torch.nn.Parameter(v.clone()) for n, v in params.items()}
+    opt = torch.optim.SGD([dict(params=[tp[n] for n in names if not is_head(n)], lr=0.01),
+                           dict(params=[tp[n] for n in names if is_head(n)], lr=0.02)],
+                          momentum=0.9, weight_decay=1e-4, nesterov=True)
+    bufs = {}
+    cur = {n: v.clone() for n, v in params.items()}
+    for _ in range(3):
+        grads = {n: torch.randn(5, generator=gen) for n in names}
+        for n in names:
+            tp[n].grad = grads[n].clone()
+        opt.step()
+        for n in names:  # the oracle's update rule (pretrain_oracle.pretrain_step)
+            g = grads[n] + 1e-4 * cur[n]
+            b = g.clone() if n not in bufs else 0.9 * bufs[n] + g
+            bufs[n] = b
+            cur[n] = cur[n] - (0.02 if is_head(n) else 0.01) * (g + 0.9 * b)
+        for n in names:
+            assert torch.allclose(cur[n], tp[n].detach(), rtol=1e-6, atol=1e-7), n
+
+
+def test_pretrain_requires_device():
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    from few_shot_seg_cwt_amd._lib import CwtError
+    from few_shot_seg_cwt_amd.pretrain import PretrainPSPNet
+    with pytest.raises((CwtError, RuntimeError)):
+        PretrainPSPNet(dict(layers=50, num_classes_tr=16), syn.make_pspnet_state(50, 2021, num_classes_tr=16))
+
+
+def test_param_specs_cover_classifier_classes():
+    specs = dict((n, s) for n, s, _ in syn.pspnet_param_specs(50, 512, 61))
+    assert specs["classifier.weight"] == (61, 512, 1, 1)
+    sd = syn.make_pspnet_state(50, 2021, num_classes_tr=61)
+    assert sd["classifier.weight"].shape == (61, 512, 1, 1)
+    # two-class default unchanged (the CWT fixtures were generated with it)
+    sd2 = syn.make_pspnet_state(50, 2021)
+    assert np.array_equal(sd2["classifier.weight"], sd["classifier.weight"][:2]) or sd2["classifier.weight"].shape == (2, 512, 1, 1)
