@@ -802,11 +802,19 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
   __shared__ __attribute__((aligned(16))) float fs3[NRES == 3 ? PA_NW * 64 * PA_CPW : 4];  // NRES 3: per-wave f slices
   __shared__ float dlw[PA_NW][EWK][PA_CPW];     // d = W1 - W0 of each wave's channels (wave-private)
   __shared__ float wlw[PA_NW][EWK][2][PA_CPW];  // W0, W1 of each wave's channels (wave-private)
-  __shared__ float zpart[PA_NW][PA_NPX];
-  __shared__ float zd[PA_NPX];
-  __shared__ float gs[PA_NPX];
-  __shared__ float P0[8][2][PA_NC + 1];
-  __shared__ float P1[8][2][PA_NC + 1];
+  // NRES 2 runs its two units in lockstep (one set of LDS barriers, one butterfly and one set
+  // of atomics per step when both units belong to one episode): the second unit's copies [1]
+  constexpr int NU = NRES == 2 ? 2 : 1;
+  __shared__ float zpart_u[NU][PA_NW][PA_NPX];
+  __shared__ float zd_u[NU][PA_NPX];
+  __shared__ float gs_u[NU][PA_NPX];
+  __shared__ float P0_u[NU][8][2][PA_NC + 1];
+  __shared__ float P1_u[NU][8][2][PA_NC + 1];
+  auto& zpart = zpart_u[0];
+  auto& zd = zd_u[0];
+  auto& gs = gs_u[0];
+  auto& P0 = P0_u[0];
+  auto& P1 = P1_u[0];
   __shared__ float wfg_l[EWK], lr_l[EWK];
   __shared__ int abort_flag;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -855,6 +863,10 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
     pa_load(cur, a, q, wv, lane);
   }
   int y2[2][2] = {{255, 255}, {255, 255}};  // NRES 2: labels of the second unit (its f is in fl2)
+  if (NRES == 2 && u1 - u0 == 1) {  // no second unit: its f reads as zero in the lockstep dW pass
+#pragma unroll
+    for (int j = 0; j < PA_CPW; ++j) fl2[wv][j][lane] = 0.f;
+  }
   if (NRES == 2 && u1 - u0 > 1) {
     PaTile tmp;
     pa_load(tmp, a, pa_unit(a, u0 + 1), wv, lane);
@@ -1003,6 +1015,136 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
         }
       }
     };
+    // NRES 2 with two units: both units' phases share the barriers; lane p holds pixel p of
+    // each unit (unit A's f in registers, unit B's in fl2), LDS copies [0] / [1]
+    auto hires_pass = [&](const PaUnit& q, int ew, const int (&ylab)[2][2], const float* zdp, float (*P0p)[2][PA_NC + 1],
+                          float (*P1p)[2][PA_NC + 1]) {
+      const bool has_extra = q.extra_row && i_row == 0;
+      const float wf = wfg_l[ew];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (k == 1 && a.uc < 16) break;
+        const int X = 8 * q.x0 + 64 * (wv & 1) + 128 * k + lane;
+        const int slot_x = 8 * (wv & 1) + 16 * k + (lane >> 3);
+        const int ix = min(X >> 3, a.w - 1);
+        const int xi0 = min(ix - q.x0, PA_NC - 1);
+        const int xi1 = (ix < a.w - 1) ? min(xi0 + 1, PA_NC - 1) : xi0;
+        const float lx1 = (float)(X & 7) * 0.125f, lx0 = 1.f - lx1;
+        float sa[2] = {0.f, 0.f}, sb[2] = {0.f, 0.f};
+#pragma unroll
+        for (int e2 = 0; e2 < 2; ++e2) {
+          if (e2 == 1 && !has_extra) break;
+          const int y = ylab[k][e2];
+          float gv = 0.f;
+          if (y != 255) {
+            const float dd = e2 ? (lx0 * zdp[PA_NC + xi0] + lx1 * zdp[PA_NC + xi1])
+                                : ly0 * (lx0 * zdp[xi0] + lx1 * zdp[xi1]) + ly1 * (lx0 * zdp[PA_NC + xi0] + lx1 * zdp[PA_NC + xi1]);
+            const float p1 = __builtin_amdgcn_rcpf(1.f + __expf(-dd));
+            gv = ((y == 1) ? wf : 1.f) * (p1 - (float)y);
+          }
+          sa[e2] = octet_sum(lx0 * gv);
+          sb[e2] = octet_sum(lx1 * gv);
+        }
+        if ((lane & 7) == 0) {
+          P0p[i_row][0][slot_x] = ly0 * sa[0];
+          P1p[i_row][0][slot_x + 1] = ly0 * sb[0];
+          P0p[i_row][1][slot_x] = ly1 * sa[0] + sa[1];
+          P1p[i_row][1][slot_x + 1] = ly1 * sb[0] + sb[1];
+        }
+      }
+    };
+    auto gs_of = [&](int tt, float (*P0p)[2][PA_NC + 1], float (*P1p)[2][PA_NC + 1]) {
+      const int ri = tt >> 5, xi = tt & 31;
+      float gsum = 0.f;
+      if (xi <= a.uc) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) gsum += P0p[i][ri][xi];
+        if (xi > 0) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) gsum += P1p[i][ri][xi];
+        }
+      }
+      return gsum;
+    };
+    auto pair_body = [&](const PaUnit& qa, const PaUnit& qb, bool has_b) {  // !has_b: unit B absent (fl2 zero)
+      const int ewa = qa.e - e_lo, ewb = qb.e - e_lo;
+      {
+        float sda = 0.f, sdb = 0.f;
+#pragma unroll
+        for (int j = 0; j < PA_CPW / 4; ++j) {
+          const f32x4 da = *(const f32x4*)&dlw[wv][ewa][4 * j];
+          const f32x4 db = *(const f32x4*)&dlw[wv][ewb][4 * j];
+          float fb[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) fb[r] = fl2[wv][4 * j + r][lane];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            sda = fmaf(da[r], cur.fr[4 * j + r], sda);
+            sdb = fmaf(db[r], fb[r], sdb);
+          }
+          if (j & 1) asm volatile("" ::: "memory");  // at most 8 of unit B's LDS reads in flight (registers)
+        }
+        zpart_u[0][wv][lane] = sda;
+        zpart_u[NU - 1][wv][lane] = sdb;
+      }
+      lds_barrier();
+      if (t < 2 * PA_NPX) {
+        const int uu = t >> 6, tt = t & 63;
+        float z = 0.f;
+#pragma unroll
+        for (int v = 0; v < PA_NW; ++v) z += zpart_u[uu][v][tt];
+        zd_u[uu][tt] = z;
+      }
+      lds_barrier();
+      stamp(1);
+      hires_pass(qa, ewa, cur.y, zd_u[0], P0_u[0], P1_u[0]);
+      if (has_b) hires_pass(qb, ewb, y2, zd_u[NU - 1], P0_u[NU - 1], P1_u[NU - 1]);
+      lds_barrier();
+      if (t < 2 * PA_NPX) {
+        const int uu = t >> 6, tt = t & 63;
+        gs_u[uu][tt] = gs_of(tt, P0_u[uu], P1_u[uu]);
+      }
+      lds_barrier();
+      stamp(2);
+      {
+        float accd[PA_CPW];
+        const float ga = gs_u[0][lane], gb = has_b ? gs_u[NU - 1][lane] : 0.f;
+        if (qa.e == qb.e) {  // one butterfly and one set of atomics for both units
+#pragma unroll
+          for (int j = 0; j < PA_CPW; ++j) accd[j] = ga * cur.fr[j];
+#pragma unroll
+          for (int j0 = 0; j0 < PA_CPW; j0 += 8) {
+            float fb[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) fb[k] = fl2[wv][j0 + k][lane];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) accd[j0 + k] = fmaf(gb, fb[k], accd[j0 + k]);
+            asm volatile("" ::: "memory");
+          }
+          pa_butterfly(accd, lane);
+          if ((lane & 1) == 0)
+            __hip_atomic_fetch_add(a.acc + (long)qa.e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
+                                       wv * PA_CPW + (lane >> 1),
+                                   accd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+#pragma unroll
+          for (int uu = 0; uu < 2; ++uu) {
+            const PaUnit& q = uu ? qb : qa;
+#pragma unroll
+            for (int j = 0; j < PA_CPW; ++j) accd[j] = uu ? gb * fl2[wv][j][lane] : ga * cur.fr[j];
+            pa_butterfly(accd, lane);
+            if ((lane & 1) == 0)
+              __hip_atomic_fetch_add(a.acc + (long)q.e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
+                                         wv * PA_CPW + (lane >> 1),
+                                     accd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+    };
+    if constexpr (NRES == 2) {
+      const bool has_b = u1 - u0 == 2;
+      pair_body(q, has_b ? pa_unit(a, u0 + 1) : q, has_b);
+    } else
     for (int u = u0; u < u1; ++u) {
       if (NRES == 3) {  // this wave's slice of unit u landed (nothing younger is in flight), then
                         // the next unit's DMA goes out while unit u is computed
@@ -1196,6 +1338,7 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
   a.S = S;
   a.nshot = n;
   a.nep = E;
+
   a.iters = iters;
   a.ncb = ncb;
   a.ntile = (h - 1) * ncb;
