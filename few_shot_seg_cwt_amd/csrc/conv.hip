@@ -30,7 +30,7 @@ namespace cwt {
 // STAGE only names the instantiation (0 stem, 1-4 layer1-4, 5 PPM, 6 bottleneck) so that
 // rocprofv3's per-kernel statistics break the conv stack down by stage.
 template <int BM, int BN, int STAGE>
-__global__ __launch_bounds__(256) void conv_igemm_f32(ConvArgs a) {
+__global__ __launch_bounds__(256, 2) void conv_igemm_f32(ConvArgs a) {
   constexpr int BK = 32;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
@@ -74,8 +74,8 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(ConvArgs a) {
   }
   const float* wbase = a.w + (long)(n0 + lr) * a.K + lc * 4;
 
-  f32x4 ra[A_LD], rb[B_LD];
-  auto load_slice = [&](int kt) {
+  f32x4 ra[A_LD], rb[B_LD], ra2[A_LD], rb2[B_LD];  // two register sets (two slices in flight)
+  auto load_slice = [&](int kt, f32x4(&ra)[A_LD], f32x4(&rb)[B_LD]) {
     const int k0 = kt * BK;
     const int taps = a.kh * a.kw;  // packed_k order: 32-channel block major, taps inner
     const int cb = kt / taps;
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) rb[j] = *(const f32x4*)(wbase + (long)(32 * j) * a.K + k0);
   };
-  auto store_slice = [&](int buf) {
+  auto store_slice = [&](int buf, const f32x4(&ra)[A_LD], const f32x4(&rb)[B_LD]) {
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       int row = lr + 32 * j;
@@ -120,37 +120,49 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(ConvArgs a) {
   const int h = lane >> 5;
   const int l31 = lane & 31;
 
-  if (kt_begin < kt_end) {
-    load_slice(kt_begin);
-    store_slice(0);
-    __syncthreads();
-    for (int kt = kt_begin; kt < kt_end; ++kt) {
-      const int cur = (kt - kt_begin) & 1;
-      const bool more = kt + 1 < kt_end;
-      if (more) load_slice(kt + 1);
-      const f32x4* sb = smem[cur];
+  // Register prefetch two K-slices ahead: two register sets used alternately (the loop is unrolled
+  // by two so each set is static); the loads of slice t+2 go out before slice t's MFMAs and have
+  // two slices of MFMA time (~3.4 us at 128 x 128) to land before they are stored to LDS.
+  auto compute_slice = [&](int cur) {
+    const f32x4* sb = smem[cur];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f32x4 av[TM], bv[TN];
+    for (int g = 0; g < 4; ++g) {
+      f32x4 av[TM], bv[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          int row = wm * WM + i * 32 + l31;
-          av[i] = sb[row * 8 + ((2 * g + h) ^ ((row >> 1) & 7))];
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          int row = BM + wn * WN + j * 32 + l31;
-          bv[j] = sb[row * 8 + ((2 * g + h) ^ ((row >> 1) & 7))];
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][s], bv[j][s], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < TM; ++i) {
+        int row = wm * WM + i * 32 + l31;
+        av[i] = sb[row * 8 + ((2 * g + h) ^ ((row >> 1) & 7))];
       }
-      if (more) store_slice(cur ^ 1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int row = BM + wn * WN + j * 32 + l31;
+        bv[j] = sb[row * 8 + ((2 * g + h) ^ ((row >> 1) & 7))];
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][s], bv[j][s], acc[i][j], 0, 0, 0);
+    }
+  };
+  if (kt_begin < kt_end) {
+    load_slice(kt_begin, ra, rb);
+    if (kt_begin + 1 < kt_end) load_slice(kt_begin + 1, ra2, rb2);
+    store_slice(0, ra, rb);
+    __syncthreads();
+    for (int kt = kt_begin; kt < kt_end; kt += 2) {
+      // LDS buffer 0 holds slice kt, set 2 slice kt+1, set 1 is free
+      if (kt + 2 < kt_end) load_slice(kt + 2, ra, rb);
+      compute_slice(0);
+      if (kt + 1 < kt_end) store_slice(1, ra2, rb2);
+      __syncthreads();
+      if (kt + 1 >= kt_end) break;
+      // LDS buffer 1 holds slice kt+1, set 1 slice kt+2, set 2 is free
+      if (kt + 3 < kt_end) load_slice(kt + 3, ra2, rb2);
+      compute_slice(1);
+      if (kt + 2 < kt_end) store_slice(0, ra, rb);
       __syncthreads();
     }
   }
