@@ -93,6 +93,9 @@ struct PtLoss {
 };
 size_t seg_ce_ws_bytes(int N, int S, int w, int nc);
 int launch_seg_ce_smooth(PtLoss a, void* ws, size_t ws_bytes, float* loss, hipStream_t st);
+// evaluation: out[0] mean CE (plain one-hot), out[1] valid pixels; iu [3][nc] intersection / union / target
+size_t seg_eval_ws_bytes(int N, int S, int w, int nc);
+int launch_seg_eval(PtLoss a, void* ws, size_t ws_bytes, float* out, float* iu, hipStream_t st);
 
 // torch.optim.SGD step over a flat buffer (seg.hip)
 int launch_sgd(float* p, const float* g, float* buf, long n, float lr, float mom, float wd, int nesterov, int first,

@@ -829,6 +829,35 @@ int cwt_pretrain_forward(cwt_ctx* ctx, cwt_pretrain* pt, const float* images, in
   return 0;
 }
 
+int cwt_pretrain_evaluate(cwt_ctx* ctx, cwt_pretrain* pt, const float* images, const int64_t* labels, int N, int S,
+                          int train, float* loss_out, float* iu_out, void* stream) {
+  if (!ctx || !pt || !images || !labels || !loss_out || !iu_out) return fail(CWT_EARG, "null argument");
+  CWT_CHECK(N >= 1 && S >= 17 && (S - 1) % 8 == 0, "need (S-1) % 8 == 0 (pspnet.py:150)");
+  CWT_CHECK(!train || N >= 2, "training-mode BN needs N >= 2");
+  CWT_HIP(hipSetDevice(pt->device));
+  hipStream_t st = (hipStream_t)stream;
+  int rc;
+  if ((rc = pt_ensure_acts(pt, N, S))) return rc;
+  PtStep s{pt, st};
+  if ((rc = pt_workspaces(pt, s))) return rc;
+  pt->img = images;
+  pt->drop_p = 0.f;
+  if ((rc = pt_forward(pt, s, images, train ? 1 : 0, 0.f))) return rc;
+  float* ws;
+  const size_t wsb = seg_eval_ws_bytes(N, S, pt->h, pt->nc);
+  if ((rc = pt_ws(pt, "evalws", wsb, &ws))) return rc;
+  PtLoss L;
+  std::memset(&L, 0, sizeof(L));
+  L.logits = pt->LOGITS;
+  L.target = labels;
+  L.N = N;
+  L.S = S;
+  L.h = L.w = pt->h;
+  L.nc = pt->nc;
+  L.ignore = 255;
+  return launch_seg_eval(L, ws, wsb, loss_out, iu_out, st);
+}
+
 int cwt_pretrain_get(cwt_pretrain* pt, const char* name, int what, float* host_out, int64_t numel) {
   if (!pt || !name || !host_out) return fail(CWT_EARG, "null argument");
   CWT_HIP(hipSetDevice(pt->device));

@@ -999,3 +999,143 @@ int launch_seg_ce_smooth(PtLoss a, void* ws, size_t ws_bytes, float* loss, hipSt
 }
 
 }  // namespace cwt
+
+namespace cwt {
+
+// ------------------------------------------------------------------------------------------
+// Evaluation of the upsampled logits (pretrain.py:223-250 standard_validate and the logging
+// block :123-131): per high-res pixel the bilinear (align_corners) logits, their argmax (first
+// maximum, as torch's CPU argmax) and nn.CrossEntropyLoss(ignore_index=255) (plain one-hot);
+// intersectionAndUnionGPU (util.py:280-308) counts per class: pixels with target 255 are
+// excluded from every count.  Integer counts through LDS then global atomics (order-free,
+// exact); the loss as per-block partials summed in fixed order.
+// counts: [3][NC] unsigned (intersection, prediction, target); part: 2 doubles per block.
+// ------------------------------------------------------------------------------------------
+template <int NC>
+__global__ __launch_bounds__(64) void seg_eval_kernel(PtLoss a, unsigned* __restrict__ counts, double* __restrict__ part) {
+  __shared__ unsigned sc[3][NC];
+  for (int i = threadIdx.x; i < 3 * NC; i += 64) (&sc[0][0])[i] = 0u;
+  __syncthreads();
+  const int n = blockIdx.z, Y = blockIdx.y;
+  const int j = blockIdx.x * 64 + threadIdx.x;
+  const int S = a.S, h = a.h, w = a.w;
+  const float sy = align_corners_scale(h, S), sx = align_corners_scale(w, S);
+  const Lerp ly = lerp_coord(Y, h, sy);
+  double lsum = 0.0;
+  unsigned cnt = 0;
+  if (j < w) {
+    const int xa = max(0, (int)floorf((float)j / sx) - 2), xb = min(S, (int)ceilf((float)(j + 1) / sx) + 2);
+    const float* L0 = a.logits + (((long)n * h + ly.i0) * w) * NC;
+    const float* L1 = a.logits + (((long)n * h + ly.i1) * w) * NC;
+    const int64_t* tg = a.target + ((long)n * S + Y) * S;
+    for (int X = xa; X < xb; ++X) {
+      const Lerp lx = lerp_coord(X, w, sx);
+      if (lx.i0 != j) continue;
+      const int y = (int)tg[X];
+      if (y == a.ignore) continue;
+      float z[NC];
+      float m = -INFINITY;
+      int am = 0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        z[c] = ly.l0 * (lx.l0 * L0[lx.i0 * NC + c] + lx.l1 * L0[lx.i1 * NC + c]) +
+               ly.l1 * (lx.l0 * L1[lx.i0 * NC + c] + lx.l1 * L1[lx.i1 * NC + c]);
+        if (z[c] > m) {
+          m = z[c];
+          am = c;
+        }
+      }
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) se += expf(z[c] - m);
+      float zy = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) zy = (c == y) ? z[c] : zy;
+      lsum += (double)(m + logf(se) - zy);
+      ++cnt;
+      atomicAdd(&sc[1][am], 1u);
+      if (y >= 0 && y < NC) {
+        atomicAdd(&sc[2][y], 1u);
+        if (am == y) atomicAdd(&sc[0][y], 1u);
+      }
+    }
+  }
+  __shared__ double sl[64];
+  __shared__ unsigned sk[64];
+  sl[threadIdx.x] = lsum;
+  sk[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * NC; i += 64)
+    if ((&sc[0][0])[i]) atomicAdd(&counts[i], (&sc[0][0])[i]);
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    unsigned k = 0;
+    for (int i = 0; i < 64; ++i) {
+      s += sl[i];
+      k += sk[i];
+    }
+    const long b = ((long)n * gridDim.y + Y) * gridDim.x + blockIdx.x;
+    part[2 * b] = s;
+    part[2 * b + 1] = (double)k;
+  }
+}
+
+// out[0] = mean loss over the valid pixels, out[1] = their count; iu[3][nc] floats from the counts
+// (intersection, union = prediction + target - intersection, target), as intersectionAndUnionGPU
+__global__ void seg_eval_final_kernel(const double* __restrict__ part, long nblk, const unsigned* __restrict__ counts,
+                                      int nc, float* __restrict__ out, float* __restrict__ iu) {
+  __shared__ double s1[256], s2[256];
+  double a = 0.0, b = 0.0;
+  for (long i = threadIdx.x; i < nblk; i += 256) {
+    a += part[2 * i];
+    b += part[2 * i + 1];
+  }
+  s1[threadIdx.x] = a;
+  s2[threadIdx.x] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      s1[threadIdx.x] += s1[threadIdx.x + o];
+      s2[threadIdx.x] += s2[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = (float)(s1[0] / s2[0]);
+    out[1] = (float)s2[0];
+  }
+  for (int c = threadIdx.x; c < nc; c += 256) {
+    const float in = (float)counts[c], pr = (float)counts[nc + c], tg = (float)counts[2 * nc + c];
+    iu[c] = in;
+    iu[nc + c] = pr + tg - in;
+    iu[2 * nc + c] = tg;
+  }
+}
+
+template <int NC>
+static int launch_seg_eval_nc(PtLoss a, unsigned* counts, double* part, float* out, float* iu, hipStream_t st) {
+  const dim3 g(cdiv(a.w, 64), a.S, a.N);
+  hipLaunchKernelGGL((seg_eval_kernel<NC>), g, dim3(64), 0, st, a, counts, part);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(seg_eval_final_kernel, dim3(1), dim3(256), 0, st, (const double*)part, (long)g.x * g.y * g.z,
+                     (const unsigned*)counts, NC, out, iu);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+size_t seg_eval_ws_bytes(int N, int S, int w, int nc) { return (size_t)3 * nc * 4 + 256 + (size_t)2 * cdiv(w, 64) * S * N * 8; }
+
+int launch_seg_eval(PtLoss a, void* ws, size_t ws_bytes, float* out, float* iu, hipStream_t st) {
+  if (seg_eval_ws_bytes(a.N, a.S, a.w, a.nc) > ws_bytes) return fail(CWT_ESTATE, "seg_eval: workspace too small");
+  unsigned* counts = (unsigned*)ws;
+  double* part = (double*)((char*)ws + (((size_t)3 * a.nc * 4 + 255) & ~(size_t)255));
+  CWT_HIP(hipMemsetAsync(counts, 0, (size_t)3 * a.nc * 4, st));
+  switch (a.nc) {
+    case 16: return launch_seg_eval_nc<16>(a, counts, part, out, iu, st);
+    case 61: return launch_seg_eval_nc<61>(a, counts, part, out, iu, st);
+    case 2: return launch_seg_eval_nc<2>(a, counts, part, out, iu, st);
+    default: return fail(CWT_EARG, "seg_eval: num_classes must be 2, 16 or 61");
+  }
+}
+
+}  // namespace cwt

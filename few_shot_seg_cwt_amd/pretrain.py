@@ -148,6 +148,22 @@ class PretrainPSPNet:
                    "cwt_pretrain_forward")
         return out.permute(0, 3, 1, 2)
 
+    def evaluate(self, images: torch.Tensor, targets: torch.Tensor):
+        """One batch of standard_validate (pretrain.py:223-250) / the logging block (:123-131)
+        under the current mode: returns (loss, n_valid, intersection, union, target) as device
+        tensors -- nn.CrossEntropyLoss(ignore_index=255) of the upsampled logits and
+        intersectionAndUnionGPU(logits.argmax(1), gt, num_classes_tr, 255)."""
+        _lib.require(images, "images")
+        _lib.require(targets, "targets", torch.int64)
+        images, targets = images.contiguous(), targets.contiguous()
+        lo = torch.empty(2, device=self.device)
+        iu = torch.empty(3, self.num_classes, device=self.device)
+        _lib.check(_lib.lib().cwt_pretrain_evaluate(_lib.ctx(self.device.index), self._h, _lib.ptr(images),
+                                                    _lib.ptr(targets), images.shape[0], images.shape[2],
+                                                    int(self.training), _lib.ptr(lo), _lib.ptr(iu),
+                                                    _lib.stream_ptr(self.device)), "cwt_pretrain_evaluate")
+        return lo[0], lo[1], iu[0], iu[1], iu[2]
+
     def _get(self, name: str, what: int, shape) -> torch.Tensor:
         out = np.empty(shape, np.float32)
         _lib.check(_lib.lib().cwt_pretrain_get(self._h, name.encode(), what, out.ctypes.data, out.size),
@@ -206,3 +222,22 @@ def train_epoch(model: PretrainPSPNet, batches, epoch: int, iters_per_epoch: int
         lr = cosine_lr(base_lr, it, iters_per_epoch * epochs)
         losses.append(model.train_step(images, gt, lr=lr))
     return torch.stack(losses).mean() if losses else torch.zeros(())
+
+
+def standard_validate(args, val_loader, model: PretrainPSPNet):
+    """pretrain.py:223-250: eval mode over the loader's (images, gt) batches (device tensors);
+    per-class intersections and unions summed over batches, the loss averaged per batch as the
+    reference's AverageMeter does.  Returns (mIoU, mean loss) as host floats."""
+    model.eval()
+    inter = uni = None
+    losses = []
+    for images, gt in val_loader:
+        loss, _, i, u, _ = model.evaluate(images, gt)
+        inter = i.clone() if inter is None else inter + i
+        uni = u.clone() if uni is None else uni + u
+        losses.append(loss)
+    model.train()
+    if inter is None:
+        return 0.0, 0.0
+    miou = float((inter / (uni + 1e-10)).mean())
+    return miou, float(torch.stack(losses).mean())

@@ -353,6 +353,15 @@ int cwt_pretrain_step(cwt_ctx* ctx, cwt_pretrain* pt, const float* images, const
 int cwt_pretrain_forward(cwt_ctx* ctx, cwt_pretrain* pt, const float* images, int N, int S, int train,
                          float* logits, void* stream);
 
+/* Evaluation pass of pretrain.py:223-250 (standard_validate) / :123-131 (the logging block) for
+ * one batch: logits = model(images) (train = 0: eval mode as model.eval(); 1: batch statistics,
+ * running statistics untouched), nn.CrossEntropyLoss(ignore_index=255) of the upsampled logits ->
+ * loss_out device float[2] = {mean loss, valid pixels}; intersectionAndUnionGPU(logits.argmax(1),
+ * gt, num_classes, 255) (util.py:280-308) -> iu_out device float[3][num_classes] = intersection,
+ * union, target.  labels device [N, S, S] int64. */
+int cwt_pretrain_evaluate(cwt_ctx* ctx, cwt_pretrain* pt, const float* images, const int64_t* labels, int N, int S,
+                          int train, float* loss_out, float* iu_out, void* stream);
+
 /* Host copy of one tensor in PyTorch layout by state_dict name: what = CWT_PT_PARAM, _GRAD,
  * _MOMENTUM (a parameter name) or CWT_PT_RUNNING ("<bn>.running_mean" / ".running_var").
  * Synchronises the device. */

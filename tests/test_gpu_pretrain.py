@@ -136,3 +136,39 @@ def test_pretrain_logits_eval_and_roundtrip(dev):
     back = model.state_dict()
     for k, v in back.items():
         assert np.array_equal(v.numpy(), np.asarray(state[k], np.float32)), k
+
+
+@pytest.mark.parametrize("nc,S", [(16, 65), (61, 33)])
+def test_pretrain_evaluate_vs_oracle(dev, nc, S):
+    """standard_validate's per-batch numbers (pretrain.py:223-250): CE loss of the upsampled
+    eval-mode logits and intersectionAndUnionGPU of their argmax over num_classes_tr classes,
+    against the oracle in float64.  Counts equal up to the pixels whose oracle top-2 logit margin
+    is below 1e-4 x max |logit| (reported; an fp32 argmax may flip there)."""
+    import torch.nn.functional as F
+    from few_shot_seg_cwt_amd.pretrain import PretrainPSPNet
+    from oracle.pretrain_oracle import pspnet_logits
+    state = syn.make_pspnet_state(50, SEED, num_classes_tr=nc)
+    model = PretrainPSPNet(args(num_classes_tr=nc), state, dev).eval()
+    x, t = make_batch(2, S, nc, SEED + 5)
+    loss, nvalid, inter, union, target = model.evaluate(x.to(dev), t.to(dev))
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in state.items()}
+    with torch.no_grad():
+        lg = pspnet_logits(x.double(), {k: (v.double() if v.dtype == torch.float32 else v) for k, v in sd.items()},
+                           50, train=False)
+        up = F.interpolate(lg, size=(S, S), mode="bilinear", align_corners=True)
+        ref_loss = F.cross_entropy(up, t, ignore_index=255)
+        pred = up.argmax(1)
+        top2 = up.topk(2, dim=1).values
+        low = ((top2[:, 0] - top2[:, 1]) < 1e-4 * up.abs().max()) & (t != 255)
+    valid = t != 255
+    p, tt = pred[valid], t[valid]
+    ri = torch.bincount(p[p == tt], minlength=nc).double()
+    ro = torch.bincount(p, minlength=nc).double()
+    rt = torch.bincount(tt, minlength=nc).double()
+    flips = int(low.sum())
+    print(f"evaluate nc={nc} S={S}: loss {float(loss):.6f} vs {float(ref_loss):.6f}, low-margin pixels {flips}")
+    assert abs(float(loss) - float(ref_loss)) / float(ref_loss) < 1e-4
+    assert int(nvalid) == int(valid.sum())
+    assert torch.equal(target.cpu().double(), rt)
+    assert float((inter.cpu().double() - ri).abs().sum()) <= 2 * flips
+    assert float((union.cpu().double() - (ro + rt - ri)).abs().sum()) <= 4 * flips
