@@ -99,11 +99,17 @@ def shard_indices(n: int, rank: int, world: int, shuffle: bool, seed: int = 0, e
 
 
 def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:
-    """In-place mean over ranks of one flat bucket (the CWT gradient)."""
+    """In-place mean over ranks of one flat bucket (the CWT gradient); staged through the host
+    when the backend's device is not the tensor's (gloo with device tensors)."""
     _, world = rank_world()
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        t.div_(world)
+        if t.device.type == _reduce_device().type:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            t.div_(world)
+        else:
+            h = t.detach().to(_reduce_device())
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            t.copy_(h.div_(world))
     return t
 
 
