@@ -41,8 +41,28 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a) {
   const int taps = a.kh * a.kw;
   const int HoWo = a.Ho * a.Wo;
 
+  // per-thread gather geometry: the (channel block, tap) of each B group is fixed for the
+  // workgroup; the pixel of each loaded row advances by 32 per chunk (no divisions in the loop)
+  int b_coff[B_LD], b_dy[B_LD], b_dx[B_LD], b_n[B_LD], b_oh[B_LD], b_ow[B_LD];
+#pragma unroll
+  for (int j = 0; j < B_LD; ++j) {
+    const int idx = t + 256 * j;
+    const int row = idx / (BN / 4), rem = idx % (BN / 4);
+    const int grp = rem >> 3, c4 = rem & 7;
+    const int ks = k0 / 32 + grp;
+    const int cb = ks / taps, tap = ks - cb * taps;
+    const int ky = tap / a.kw, kx = tap - ky * a.kw;
+    b_coff[j] = cb * 32 + 4 * c4;
+    b_dy[j] = ky * a.dil - a.pad;
+    b_dx[j] = kx * a.dil - a.pad;
+    const long m = m_begin + row;
+    const int n = (int)(m / HoWo), rr = (int)(m - (long)n * HoWo);
+    b_n[j] = n;
+    b_oh[j] = rr / a.Wo;
+    b_ow[j] = rr - b_oh[j] * a.Wo;
+  }
   f32x4 ra[A_LD], rb[B_LD];
-  auto load_chunk = [&](long mc) {
+  auto load_chunk = [&](long mc) {  // mc = m_begin + 32 * (chunks so far); B geometry is at mc
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       const int idx = t + 256 * j;
@@ -53,21 +73,27 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
       const int idx = t + 256 * j;
-      const int row = idx / (BN / 4), rem = idx % (BN / 4);
-      const int grp = rem >> 3, c4 = rem & 7;
-      const long m = mc + row;
+      const int row = idx / (BN / 4);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (m < m_end) {
-        const int ks = k0 / 32 + grp;
-        const int cb = ks / taps, tap = ks - cb * taps;
-        const int ky = tap / a.kw, kx = tap - ky * a.kw;
-        const int n = (int)(m / HoWo), rr = (int)(m - (long)n * HoWo);
-        const int oh = rr / a.Wo, ow = rr - oh * a.Wo;
-        const int ih = oh * a.stride - a.pad + ky * a.dil, iw = ow * a.stride - a.pad + kx * a.dil;
+      if (mc + row < m_end) {
+        const int ih = b_oh[j] * a.stride + b_dy[j], iw = b_ow[j] * a.stride + b_dx[j];
         if ((unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi)
-          v = *(const f32x4*)(a.x + ((long)(n * a.Hi + ih) * a.Wi + iw) * a.x_ld + cb * 32 + 4 * c4);
+          v = *(const f32x4*)(a.x + ((long)(b_n[j] * a.Hi + ih) * a.Wi + iw) * a.x_ld + b_coff[j]);
       }
       rb[j] = v;
+    }
+  };
+  auto advance_chunk = [&]() {  // every loaded row's pixel += 32
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+      b_ow[j] += 32;
+      while (b_ow[j] >= a.Wo) {
+        b_ow[j] -= a.Wo;
+        if (++b_oh[j] == a.Ho) {
+          b_oh[j] = 0;
+          ++b_n[j];
+        }
+      }
     }
   };
   auto store_chunk = [&](int buf) {
@@ -98,7 +124,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a) {
     int cur = 0;
     for (long mc = m_begin; mc < m_end; mc += 32) {
       const bool more = mc + 32 < m_end;
-      if (more) load_chunk(mc + 32);
+      if (more) {
+        advance_chunk();
+        load_chunk(mc + 32);
+      }
 #pragma unroll 4
       for (int s = 0; s < 16; ++s) {
         float av[TM], bv[TN];
