@@ -334,7 +334,7 @@ int launch_stem1_wgrad(const float* img, int N, int S, const float* dy, int Ho, 
 // ------------------------------------------------------------------------------------------
 // Row blocking of the per-channel reductions: at most kBnBlocks blocks of >= 256 rows (the
 // per-channel merge over the blocks then stays short), 4 row groups x 64 channels per block.
-constexpr int kBnBlocks = 128;
+constexpr int kBnBlocks = 256;
 static inline int bn_nblk(long M) { return (int)std::min<long>(kBnBlocks, cdiv(M, 256L)); }
 static inline long bn_rows_per_blk(long M) { return ((M + bn_nblk(M) - 1) / bn_nblk(M) + 3) & ~3L; }
 
@@ -382,36 +382,58 @@ __global__ __launch_bounds__(256) void ptbn_stats_kernel(const float* __restrict
   }
 }
 
-// stats[0..C) mean, [C..2C) 1/sqrt(var + eps) of the batch (train) or of the running statistics (eval)
-__global__ void ptbn_finalize_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ run,
-                                     float eps, float momentum, int train, float* __restrict__ stats) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// stats[0..C) mean, [C..2C) 1/sqrt(var + eps) of the batch (train) or of the running statistics (eval).
+// 256 threads per 64 channels: row group g merges the partials of blocks b = g (mod 4) (loads in
+// batches of 8), then the 4 group results are merged in group order (Chan, double).
+__global__ __launch_bounds__(256) void ptbn_finalize_kernel(const float* __restrict__ part, int nblk, int C,
+                                                            float* __restrict__ run, float eps, float momentum,
+                                                            int train, float* __restrict__ stats) {
+  __shared__ double sn[4][64], sm[4][64], sq[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   if (!train) {
-    stats[c] = run[c];
-    stats[C + c] = 1.0f / sqrtf(run[C + c] + eps);
+    if (g == 0 && c < C) {
+      stats[c] = run[c];
+      stats[C + c] = 1.0f / sqrtf(run[C + c] + eps);
+    }
     return;
   }
   const long plane = (long)nblk * C;
   double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int b0 = 0; b0 < nblk; b0 += 8) {  // 8 blocks' partials loaded together, merged in block order
-    float pn[8], pm[8], pq[8];
+  if (c < C) {
+    for (int b0 = g; b0 < nblk; b0 += 32) {
+      float pn[8], pm[8], pq[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const long o = (long)min(b0 + k, nblk - 1) * C + c;
-      pn[k] = b0 + k < nblk ? part[o] : 0.f;
-      pm[k] = part[plane + o];
-      pq[k] = part[2 * plane + o];
-    }
+      for (int k = 0; k < 8; ++k) {
+        const int b = b0 + 4 * k;
+        const long o = (long)min(b, nblk - 1) * C + c;
+        pn[k] = b < nblk ? part[o] : 0.f;
+        pm[k] = part[plane + o];
+        pq[k] = part[2 * plane + o];
+      }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const double nb = pn[k];
-      if (nb == 0.0) continue;
-      const double nt = n + nb, d = (double)pm[k] - mean;
-      mean += d * (nb / nt);
-      m2 += (double)pq[k] + d * d * (n * nb / nt);
-      n = nt;
+      for (int k = 0; k < 8; ++k) {
+        const double nb = pn[k];
+        if (nb == 0.0) continue;
+        const double nt = n + nb, d = (double)pm[k] - mean;
+        mean += d * (nb / nt);
+        m2 += (double)pq[k] + d * d * (n * nb / nt);
+        n = nt;
+      }
     }
+  }
+  sn[g][lane] = n;
+  sm[g][lane] = mean;
+  sq[g][lane] = m2;
+  __syncthreads();
+  if (g != 0 || c >= C) return;
+  for (int k = 1; k < 4; ++k) {
+    const double nb = sn[k][lane];
+    if (nb == 0.0) continue;
+    const double nt = n + nb, d = sm[k][lane] - mean;
+    mean += d * (nb / nt);
+    m2 += sq[k][lane] + d * d * (n * nb / nt);
+    n = nt;
   }
   const float mu = (float)mean, var_b = (float)(m2 / n);
   stats[c] = mu;
@@ -488,27 +510,39 @@ __global__ __launch_bounds__(256) void ptbn_bwd_stats_kernel(PtBnBwd a, long rpb
   }
 }
 
-// dbeta, dgamma (written to the parameter gradients) summed over the blocks in double
-__global__ void ptbn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ dgamma,
-                                         float* __restrict__ dbeta, float* __restrict__ sums) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// dbeta, dgamma (written to the parameter gradients) summed over the blocks in double: 4 row
+// groups of 64 channels each sum the blocks b = g (mod 4), then the groups in order
+__global__ __launch_bounds__(256) void ptbn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C,
+                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                float* __restrict__ sums) {
+  __shared__ double s1[4][64], s2[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   const long plane = (long)nblk * C;
   double sg = 0.0, sgx = 0.0;
-  for (int b0 = 0; b0 < nblk; b0 += 8) {
-    float p1[8], p2[8];
+  if (c < C) {
+    for (int b0 = g; b0 < nblk; b0 += 32) {
+      float p1[8], p2[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const long o = (long)min(b0 + k, nblk - 1) * C + c;
-      p1[k] = b0 + k < nblk ? part[o] : 0.f;
-      p2[k] = b0 + k < nblk ? part[plane + o] : 0.f;
-    }
+      for (int k = 0; k < 8; ++k) {
+        const int b = b0 + 4 * k;
+        const long o = (long)min(b, nblk - 1) * C + c;
+        p1[k] = b < nblk ? part[o] : 0.f;
+        p2[k] = b < nblk ? part[plane + o] : 0.f;
+      }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      sg += p1[k];
-      sgx += p2[k];
+      for (int k = 0; k < 8; ++k) {
+        sg += p1[k];
+        sgx += p2[k];
+      }
     }
   }
+  s1[g][lane] = sg;
+  s2[g][lane] = sgx;
+  __syncthreads();
+  if (g != 0 || c >= C) return;
+  sg = ((s1[0][lane] + s1[1][lane]) + s1[2][lane]) + s1[3][lane];
+  sgx = ((s2[0][lane] + s2[1][lane]) + s2[2][lane]) + s2[3][lane];
   dbeta[c] = (float)sg;
   dgamma[c] = (float)sgx;
   sums[c] = (float)sg;
@@ -555,7 +589,7 @@ int launch_ptbn_fwd(const float* y, int ld, long M, int C, float* run, float eps
                        part);
     CWT_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(ptbn_finalize_kernel, dim3(cdiv(C, 64)), dim3(64), 0, st, (const float*)part, nblk, C, run, eps,
+  hipLaunchKernelGGL(ptbn_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, (const float*)part, nblk, C, run, eps,
                      momentum, train, stats);
   CWT_LAUNCH_CHECK();
   return 0;
@@ -577,7 +611,7 @@ int launch_ptbn_bwd(const PtBnBwd& a, float* dgamma, float* dbeta, float* part, 
   if ((size_t)2 * nblk * a.C > part_floats) return fail(CWT_ESTATE, "ptbn_bwd: partial workspace too small");
   hipLaunchKernelGGL(ptbn_bwd_stats_kernel, dim3(nblk, cdiv(a.C, 64)), dim3(256), 0, st, a, bn_rows_per_blk(a.M), part);
   CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ptbn_bwd_finalize_kernel, dim3(cdiv(a.C, 64)), dim3(64), 0, st, (const float*)part, nblk, a.C,
+  hipLaunchKernelGGL(ptbn_bwd_finalize_kernel, dim3(cdiv(a.C, 64)), dim3(256), 0, st, (const float*)part, nblk, a.C,
                      dgamma, dbeta, sums);
   CWT_LAUNCH_CHECK();
   const long total = a.M * (a.C / 4);
