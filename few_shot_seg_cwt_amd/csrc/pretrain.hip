@@ -888,6 +888,38 @@ int cwt_pretrain_get(cwt_pretrain* pt, const char* name, int what, float* host_o
   return 0;
 }
 
+int cwt_pretrain_set(cwt_pretrain* pt, const char* name, int what, const float* host_in, int64_t numel) {
+  if (!pt || !name || !host_in) return fail(CWT_EARG, "null argument");
+  CWT_HIP(hipSetDevice(pt->device));
+  CWT_HIP(hipDeviceSynchronize());
+  const std::string nm(name);
+  if (what == CWT_PT_RUNNING) {
+    for (const char* suf : {".running_mean", ".running_var"}) {
+      const size_t L = std::strlen(suf);
+      if (nm.size() > L && nm.compare(nm.size() - L, L, suf) == 0) {
+        auto it = pt->bn_by_name.find(nm.substr(0, nm.size() - L));
+        if (it == pt->bn_by_name.end()) break;
+        const PtBn& b = *it->second;
+        if (numel != b.C) return fail(CWT_EARG, "numel mismatch for '" + nm + "'");
+        CWT_HIP(hipMemcpy(b.run + (suf[9] == 'm' ? 0 : b.C), host_in, (size_t)b.C * 4, hipMemcpyHostToDevice));
+        return 0;
+      }
+    }
+    return fail(CWT_EARG, "no running statistic '" + nm + "'");
+  }
+  if (what != CWT_PT_PARAM && what != CWT_PT_MOMENTUM) return fail(CWT_EARG, "what: parameter, momentum or running");
+  auto it = pt->by_name.find(nm);
+  if (it == pt->by_name.end()) return fail(CWT_EARG, "no parameter '" + nm + "'");
+  const PtParam& p = pt->params[it->second];
+  if (numel != p.numel) return fail(CWT_EARG, "numel mismatch for '" + nm + "'");
+  std::vector<float> buf;
+  pt_pack(p, host_in, buf);
+  CWT_HIP(hipMemcpy((what == CWT_PT_MOMENTUM ? pt->MOM : pt->P) + p.off, buf.data(), (size_t)p.numel * 4,
+                    hipMemcpyHostToDevice));
+  if (what == CWT_PT_MOMENTUM) pt->first_step = false;  // a resumed optimizer has its momentum buffers
+  return 0;
+}
+
 int cwt_pretrain_num_params(const cwt_pretrain* pt, int64_t* total, int64_t* backbone) {
   if (!pt) return fail(CWT_EARG, "null argument");
   long t = 0, b = 0;

@@ -200,6 +200,68 @@ class PretrainPSPNet:
     def momentum_buffer(self, name: str) -> torch.Tensor:
         return self._get(name, 2, self._shapes[name])
 
+    def _set(self, name: str, what: int, value) -> None:
+        a = np.ascontiguousarray(value.detach().cpu().numpy() if isinstance(value, torch.Tensor) else value,
+                                 dtype=np.float32)
+        if a.size != int(np.prod(self._shapes[name])):
+            raise ValueError(f"{name}: {a.shape} does not match {self._shapes[name]}")
+        _lib.check(_lib.lib().cwt_pretrain_set(self._h, name.encode(), what, a.ctypes.data, a.size),
+                   f"cwt_pretrain_set({name})")
+
+    def load_state_dict(self, sd) -> None:
+        """model.load_state_dict (strict over the trainable tensors and BN running statistics)."""
+        for n in self._shapes:
+            if n not in sd:
+                raise KeyError(f"missing key {n}")
+            what = 3 if (n.endswith("running_mean") or n.endswith("running_var")) else 0
+            self._set(n, what, sd[n])
+
+    def param_groups(self):
+        """The two groups of pretrain.py:60-72 as parameter-name lists in module order (layer0-4;
+        ppm, bottleneck, classifier)."""
+        names = self.parameter_names()
+        head = ("ppm.", "bottleneck.", "classifier.")
+        return [[n for n in names if not n.startswith(head)], [n for n in names if n.startswith(head)]]
+
+    def optimizer_state_dict(self, lr: float | None = None) -> dict:
+        """torch.optim.SGD.state_dict() of the reference's optimizer (pretrain.py:60-72): state
+        keyed by the parameter's position over both groups, momentum buffers in PyTorch layout."""
+        a = self.args
+        base = float(_arg(a, "lr", 0.0025)) if lr is None else float(lr)
+        groups, state, idx = [], {}, 0
+        for gi, names in enumerate(self.param_groups()):
+            ids = []
+            for n in names:
+                if self.iteration > 0:
+                    state[idx] = {"momentum_buffer": self.momentum_buffer(n)}
+                ids.append(idx)
+                idx += 1
+            groups.append({"lr": base * (float(_arg(a, "scale_lr", 1.0)) if gi == 1 else 1.0),
+                           "momentum": float(_arg(a, "momentum", 0.9)), "dampening": 0,
+                           "weight_decay": float(_arg(a, "weight_decay", 1e-4)),
+                           "nesterov": bool(_arg(a, "nesterov", False)), "params": ids})
+        return {"state": state, "param_groups": groups}
+
+    def load_optimizer_state_dict(self, sd: dict) -> None:
+        names = sum(self.param_groups(), [])
+        for i, n in enumerate(names):
+            st = sd.get("state", {}).get(i)
+            if st is not None and st.get("momentum_buffer") is not None:
+                self._set(n, 2, st["momentum_buffer"])
+                self.iteration = max(self.iteration, 1)
+
+    def save_checkpoint(self, path: str, epoch: int, lr: float | None = None) -> None:
+        """torch.save({'epoch', 'state_dict', 'optimizer'}) as pretrain.py:147-152 / 157-159."""
+        torch.save({"epoch": epoch, "state_dict": self.state_dict(), "optimizer": self.optimizer_state_dict(lr)},
+                   path)
+
+    def load_checkpoint(self, path: str) -> dict:
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        self.load_state_dict(ck["state_dict"])
+        if "optimizer" in ck:
+            self.load_optimizer_state_dict(ck["optimizer"])
+        return ck
+
     def num_params(self):
         t, b = C.c_int64(), C.c_int64()
         _lib.check(_lib.lib().cwt_pretrain_num_params(self._h, C.byref(t), C.byref(b)), "cwt_pretrain_num_params")

@@ -366,6 +366,11 @@ int cwt_pretrain_evaluate(cwt_ctx* ctx, cwt_pretrain* pt, const float* images, c
  * _MOMENTUM (a parameter name) or CWT_PT_RUNNING ("<bn>.running_mean" / ".running_var").
  * Synchronises the device. */
 int cwt_pretrain_get(cwt_pretrain* pt, const char* name, int what, float* host_out, int64_t numel);
+/* The inverse of cwt_pretrain_get (what = CWT_PT_PARAM, _MOMENTUM or _RUNNING; PyTorch layout):
+ * model.load_state_dict / optimizer.load_state_dict when training resumes from a checkpoint
+ * (pretrain.py:147-152 writes {'epoch', 'state_dict', 'optimizer'}).  Setting a momentum buffer
+ * marks the optimizer as started (no first-step initialisation of the buffers).  Synchronises. */
+int cwt_pretrain_set(cwt_pretrain* pt, const char* name, int what, const float* host_in, int64_t numel);
 int cwt_pretrain_num_params(const cwt_pretrain* pt, int64_t* total, int64_t* backbone);
 
 /*

@@ -172,3 +172,28 @@ def test_pretrain_evaluate_vs_oracle(dev, nc, S):
     assert torch.equal(target.cpu().double(), rt)
     assert float((inter.cpu().double() - ri).abs().sum()) <= 2 * flips
     assert float((union.cpu().double() - (ro + rt - ri)).abs().sum()) <= 4 * flips
+
+
+def test_pretrain_checkpoint_resume(dev, tmp_path):
+    """pretrain.py:147-152 checkpoints: a model saved after one step, reloaded into a fresh one
+    (parameters, BN running statistics, SGD momentum buffers), continues bit-identically to the
+    uninterrupted run; the optimizer state dict has torch.optim.SGD's layout (two groups)."""
+    from few_shot_seg_cwt_amd.pretrain import PretrainPSPNet
+    state = syn.make_pspnet_state(50, SEED, num_classes_tr=16)
+    a = args()
+    x0, t0 = make_batch(2, 33, 16, SEED + 11)
+    x1, t1 = make_batch(2, 33, 16, SEED + 12)
+    m = PretrainPSPNet(a, state, dev)
+    m.train_step(x0.to(dev), t0.to(dev), seed=1)
+    path = str(tmp_path / "ck.pth")
+    m.save_checkpoint(path, epoch=3)
+    m.train_step(x1.to(dev), t1.to(dev), seed=2)
+    ref = m.state_dict()
+    r = PretrainPSPNet(a, state, dev)
+    ck = r.load_checkpoint(path)
+    assert ck["epoch"] == 3 and len(ck["optimizer"]["param_groups"]) == 2
+    assert ck["optimizer"]["param_groups"][1]["lr"] == pytest.approx(a["lr"] * a["scale_lr"])
+    r.train_step(x1.to(dev), t1.to(dev), seed=2)
+    got = r.state_dict()
+    for k in ref:
+        assert torch.equal(ref[k], got[k]), k
