@@ -46,8 +46,10 @@ int launch_ptbn_apply(const PtBnApply& a, hipStream_t st);
 struct PtBnBwd {
   const float* dout;  // gradient at the activation (after dropout / ReLU)
   int dout_ld;
-  const float* act;   // activation before dropout (ReLU mask), or null (no ReLU)
+  const float* act;   // activation before dropout (ReLU mask), or null
   int act_ld;
+  int relu_from_y;    // act == null: the ReLU mask recomputed from y (gamma x_hat + beta > 0, no residual)
+  const float* beta;
   float drop_p;
   unsigned long long seed;
   long rows_per_image;

@@ -256,6 +256,8 @@ static void pt_unpack(const PtParam& p, const float* src, float* dst) {
 }
 
 // ---------------------------------------------------------------- layer helpers
+static const float* const kReluFromY = reinterpret_cast<const float*>(1);  // bn_bwd: mask from y
+
 struct PtStep {
   cwt_pretrain* pt;
   hipStream_t st;
@@ -335,14 +337,17 @@ struct PtStep {
   }
 
   // gradient at a BN's raw conv output; dgamma / dbeta into G
+  // act == RELU_FROM_Y: the BN has no residual, its ReLU mask is recomputed from y (no act read)
   int bn_bwd(const PtConv& L, long M, const float* dout, int dout_ld, const float* act, int act_ld, float* dy,
              float* g_out = nullptr, int g_ld = 0, long rows_per_image = 1, float drop = 0.f) {
     PtBnBwd b;
     std::memset(&b, 0, sizeof(b));
     b.dout = dout;
     b.dout_ld = dout_ld;
-    b.act = act;
+    b.relu_from_y = act == kReluFromY;
+    b.act = b.relu_from_y ? nullptr : act;
     b.act_ld = act_ld;
+    b.beta = pt->P + L.bn.b_off;
     b.drop_p = drop;
     b.seed = pt->seed;
     b.rows_per_image = rows_per_image;
@@ -590,7 +595,7 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
     return rc;
   // bottleneck: Dropout2d + ReLU + BN backward, weight gradient over the concat map, input gradient
   PtConv& Bt = pt->bott;
-  if ((rc = s.bn_bwd(Bt, Mh, gA, 512, pt->Fpre, 512, gY, nullptr, 0, (long)h * h, drop)) ||
+  if ((rc = s.bn_bwd(Bt, Mh, gA, 512, kReluFromY, 512, gY, nullptr, 0, (long)h * h, drop)) ||
       (rc = s.wgrad(Bt, gY, pt->CAT, 4096, N, h)) || (rc = s.dgrad(Bt, gY, N, h, dcat, 4096, nullptr, 0, 6)))
     return rc;
   // PPM branch: upsample adjoint -> ReLU + BN backward -> 1x1 conv gradients -> pool adjoint
@@ -605,7 +610,7 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
     PtConv& L = pt->ppm[i];
     const float* pool = pt->POOL + base * N * 2048;
     if ((rc = launch_ppm_upsample_bwd(dcat, 4096, 2048 + 512 * i, N, b, h, gT, s.slab, s.st)) ||
-        (rc = s.bn_bwd(L, Mb, gT, 512, L.a, 512, gY)) ||
+        (rc = s.bn_bwd(L, Mb, gT, 512, kReluFromY, 512, gY)) ||
         (rc = s.gemm(gY, 1, 512, pool, 2048, 1, pt->G + L.w_off, 2048, 512, 2048, Mb)) ||
         (rc = s.gemm(gY, 512, 1, pt->P + L.w_off, 2048, 1, dpool + base * N * 2048, 2048, (int)Mb, 2048, 512)))
       return rc;
@@ -638,9 +643,9 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
           return rc;
       }
       // conv2 (stride / dilation), conv1; the input gradient of conv1 adds the residual branch's
-      if ((rc = s.bn_bwd(b.c2, Mo, gT, b.c2.Co, b.c2.a, b.c2.Co, gY)) || (rc = s.wgrad(b.c2, gY, b.c1.a, b.c1.Co, N, H)) ||
+      if ((rc = s.bn_bwd(b.c2, Mo, gT, b.c2.Co, kReluFromY, b.c2.Co, gY)) || (rc = s.wgrad(b.c2, gY, b.c1.a, b.c1.Co, N, H)) ||
           (rc = s.dgrad(b.c2, gY, N, H, gT, b.c1.Co, nullptr, 0, li + 1)) ||
-          (rc = s.bn_bwd(b.c1, Mi, gT, b.c1.Co, b.c1.a, b.c1.Co, gY)) || (rc = s.wgrad(b.c1, gY, b.x, b.x_ld, N, H)) ||
+          (rc = s.bn_bwd(b.c1, Mi, gT, b.c1.Co, kReluFromY, b.c1.Co, gY)) || (rc = s.wgrad(b.c1, gY, b.x, b.x_ld, N, H)) ||
           (rc = s.dgrad(b.c1, gY, N, H, dx, b.c1.Ci, gR, b.c1.Ci, li + 1)))
         return rc;
       dout = dx;
@@ -653,13 +658,13 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
   const float* d = dmp;
   for (int i = 2; i >= 1; --i) {
     float* nx = (d == gA) ? gB : gA;
-    if ((rc = s.bn_bwd(sm[i], Ms, d, sm[i].Co, sm[i].a, sm[i].Co, gY)) ||
+    if ((rc = s.bn_bwd(sm[i], Ms, d, sm[i].Co, kReluFromY, sm[i].Co, gY)) ||
         (rc = s.wgrad(sm[i], gY, sm[i - 1].a, sm[i].Ci, N, Hs)) ||
         (rc = s.dgrad(sm[i], gY, N, Hs, nx, sm[i].Ci, nullptr, 0, 0)))
       return rc;
     d = nx;
   }
-  if ((rc = s.bn_bwd(sm[0], Ms, d, 64, sm[0].a, 64, gY))) return rc;
+  if ((rc = s.bn_bwd(sm[0], Ms, d, 64, kReluFromY, 64, gY))) return rc;
   return launch_stem1_wgrad(pt->img, N, pt->S, gY, Hs, pt->G + sm[0].w_off, s.slab, s.slab_floats, s.st);
 }
 

@@ -474,11 +474,17 @@ __global__ __launch_bounds__(256) void ptbn_apply_kernel(PtBnApply a) {
   if (a.out_pre) *(f32x4*)(a.out_pre + row * a.out_ld + c0) = pre;
 }
 
+// ReLU mask of a BN without residual, recomputed from its raw input exactly as ptbn_apply_kernel
+// evaluated it (the same expression: the same float result)
+__device__ __forceinline__ bool ptbn_relu_on(const PtBnBwd& a, float y, float mu, float is, int c) {
+  return fmaf(a.gamma[c], (y - mu) * is, a.beta[c]) > 0.f;
+}
+
 // Gradient at the BN output: g = dout [* drop mask] [* (act > 0)]
-__device__ __forceinline__ float ptbn_grad_at(const PtBnBwd& a, long row, int c) {
+__device__ __forceinline__ float ptbn_grad_at(const PtBnBwd& a, long row, int c, float y, float mu, float is) {
   float g = a.dout[row * a.dout_ld + c];
   if (a.drop_p > 0.f) g *= dropout_scale(a.drop_p, a.seed, 3, (unsigned long long)(row / a.rows_per_image) * a.C + c);
-  if (a.act && !(a.act[row * a.act_ld + c] > 0.f)) g = 0.f;
+  if (a.act ? !(a.act[row * a.act_ld + c] > 0.f) : (a.relu_from_y && !ptbn_relu_on(a, y, mu, is, c))) g = 0.f;
   return g;
 }
 
@@ -493,9 +499,10 @@ __global__ __launch_bounds__(256) void ptbn_bwd_stats_kernel(PtBnBwd a, long rpb
     const float mu = a.stats[c], is = a.stats[a.C + c];
 #pragma unroll 4
     for (long r = r0 + rg; r < r1; r += 4) {
-      const float g = ptbn_grad_at(a, r, c);
+      const float yv = a.y[r * a.y_ld + c];
+      const float g = ptbn_grad_at(a, r, c, yv, mu, is);
       sg += g;
-      sgx = fmaf(g, (a.y[r * a.y_ld + c] - mu) * is, sgx);
+      sgx = fmaf(g, (yv - mu) * is, sgx);
     }
   }
   s1[rg][lane] = sg;
@@ -567,9 +574,9 @@ __global__ __launch_bounds__(256) void ptbn_bwd_apply_kernel(PtBnBwd a, const fl
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = c0 + q;
-    if (a.drop_p > 0.f) g[q] *= dropout_scale(a.drop_p, a.seed, 3, (unsigned long long)img * a.C + c);
-    if (!(act[q] > 0.f)) g[q] = 0.f;
     const float mu = a.stats[c], is = a.stats[a.C + c];
+    if (a.drop_p > 0.f) g[q] *= dropout_scale(a.drop_p, a.seed, 3, (unsigned long long)img * a.C + c);
+    if (a.act ? !(act[q] > 0.f) : (a.relu_from_y && !ptbn_relu_on(a, y[q], mu, is, c))) g[q] = 0.f;
     const float xh = (y[q] - mu) * is;
     dy[q] = a.gamma[c] * is * (g[q] - sums[c] * inv_m - xh * (sums[a.C + c] * inv_m));
   }
