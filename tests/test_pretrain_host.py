@@ -64,3 +64,43 @@ def test_param_specs_cover_classifier_classes():
     # two-class default unchanged (the CWT fixtures were generated with it)
     sd2 = syn.make_pspnet_state(50, 2021)
     assert np.array_equal(sd2["classifier.weight"], sd["classifier.weight"][:2]) or sd2["classifier.weight"].shape == (2, 512, 1, 1)
+
+
+def test_pretrain_oracle_forward_is_the_pinned_extractor():
+    """oracle/pretrain_oracle.pspnet_logits in eval mode is cwt_oracle.extract_features (pinned by
+    the reference-run fixtures, test_oracle_golden.py) followed by the 1x1 classifier conv
+    (pspnet.py:131-132,183-187): the pretraining oracle's forward is the pinned one."""
+    import torch.nn.functional as F
+    from oracle import cwt_oracle as O
+    from oracle.pretrain_oracle import pspnet_logits
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in syn.make_pspnet_state(50, 2021, num_classes_tr=16).items()}
+    x = torch.from_numpy(syn.normal(3, "ptx", (2, 3, 33, 33), 1.0))
+    with torch.no_grad():
+        a = pspnet_logits(x, sd, 50, train=False)
+        b = F.conv2d(O.extract_features(x, sd, 50), sd["classifier.weight"])
+    assert torch.equal(a, b)
+
+
+def test_smoothed_ce_matches_reference_formula():
+    """pretrain.py:163-179 cross_entropy with the smoothed one-hot of compute_loss :188-199,
+    against a direct per-pixel float64 evaluation."""
+    from oracle.pretrain_oracle import smoothed_ce
+    gen = torch.Generator().manual_seed(7)
+    nc = 16
+    lg = torch.randn(2, nc, 9, 9, generator=gen, dtype=torch.float64)
+    t = torch.randint(0, nc, (2, 9, 9), generator=gen)
+    t[0, 0, :4] = 255
+    got = smoothed_ce(lg, t, nc, True)
+    logp = torch.log_softmax(lg, 1)
+    tot, n = 0.0, 0
+    for b in range(2):
+        for i in range(9):
+            for j in range(9):
+                if int(t[b, i, j]) == 255:
+                    continue
+                y = int(t[b, i, j])
+                oh = torch.full((nc,), 0.1 / (nc - 1), dtype=torch.float64)
+                oh[y] = 0.9
+                tot += float(-(oh * logp[b, :, i, j]).sum())
+                n += 1
+    assert abs(float(got) - tot / n) < 1e-12
