@@ -941,17 +941,21 @@ int cwt_pretrain_num_params(const cwt_pretrain* pt, int64_t* total, int64_t* bac
 
 // ---------------------------------------------------------------- single-op test hooks
 namespace cwt {
-static float* dbg_ws(size_t bytes) {
-  static void* p = nullptr;
-  static size_t have = 0;
-  if (have < bytes) {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    have = 0;
-    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-    have = bytes;
+// test-hook workspace, one per device (the hook runs on the calling thread's current device;
+// calls are serialised like every call on a context)
+static float* dbg_ws(int device, size_t bytes) {
+  static std::map<int, std::pair<void*, size_t>> ws;
+  auto& b = ws[device];
+  if (b.second < bytes) {
+    if (b.first) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(b.first);
+    }
+    b = {nullptr, 0};
+    if (hipMalloc(&b.first, bytes) != hipSuccess) return nullptr;
+    b.second = bytes;
   }
-  return (float*)p;
+  return (float*)b.first;
 }
 }  // namespace cwt
 
@@ -961,7 +965,7 @@ extern "C" int cwt_debug_pretrain_op(cwt_ctx* ctx, int op, void* const* b, const
   CWT_HIP(hipSetDevice(ctx_device(ctx)));
   hipStream_t st = (hipStream_t)stream;
   const size_t wsf = (size_t)64 << 20;
-  float* ws = dbg_ws(wsf * 4);
+  float* ws = dbg_ws(ctx_device(ctx), wsf * 4);
   if (!ws) return fail(CWT_ESTATE, "debug workspace allocation failed");
   if (op == 0 || op == 1) {  // 0: weight gradient, 1: input gradient of a conv (ia: N Hi Ci Co k stride pad dil)
     const int N = (int)ia[0], Hi = (int)ia[1], Ci = (int)ia[2], Co = (int)ia[3], k = (int)ia[4], s = (int)ia[5],
