@@ -21,13 +21,13 @@ namespace cwt {
 // a GEMM (Co x K) reduced over the output pixels m.  Workgroup tile BM (co) x BN (kk), 4 waves
 // 2 x 2; the pixel range of split blockIdx.z is walked 32 pixels at a time: dy rows and the
 // gathered input rows (BN/32 (channel block, tap) groups of 32 channels) go to LDS row-major
-// (one row per pixel), register prefetch of the next 32 pixels during the MFMAs.  The lane
+// (one row per pixel), register prefetch two chunks ahead during the MFMAs.  The lane
 // operands are single floats (A[co][pixel], B[pixel][kk] of a 2-pixel k-step), read
 // conflict-free from consecutive LDS words.  Output: the split's slab [Co][K] (summed in fixed
 // order by wgrad_reduce_kernel: deterministic) or gw itself when there is one split.
 // ------------------------------------------------------------------------------------------
 template <int BM, int BN>
-__global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a) {
+__global__ __launch_bounds__(256, 2) void conv_wgrad_f32(WgradArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int A_LD = BM / 32, B_LD = BN / 32;  // float4 per thread per 32-pixel chunk
   __shared__ float sA[2][32][BM];
@@ -61,14 +61,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a) {
     b_oh[j] = rr / a.Wo;
     b_ow[j] = rr - b_oh[j] * a.Wo;
   }
-  f32x4 ra[A_LD], rb[B_LD];
-  auto load_chunk = [&](long mc) {  // mc = m_begin + 32 * (chunks so far); B geometry is at mc
+  // two register sets: the chunk two ahead is in flight while one chunk is in the MFMAs
+  f32x4 ra[A_LD], rb[B_LD], ra2[A_LD], rb2[B_LD];
+  // mc = the chunk's first pixel; loads happen in chunk order, B geometry is at mc
+  auto load_chunk = [&](long mc, f32x4(&A)[A_LD], f32x4(&B)[B_LD]) {
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       const int idx = t + 256 * j;
       const int row = idx / (BM / 4), c4 = idx % (BM / 4);
       const long m = mc + row;
-      ra[j] = (m < m_end) ? *(const f32x4*)(a.dy + m * a.dy_ld + co0 + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      A[j] = (m < m_end) ? *(const f32x4*)(a.dy + m * a.dy_ld + co0 + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
@@ -80,7 +82,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a) {
         if ((unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi)
           v = *(const f32x4*)(a.x + ((long)(b_n[j] * a.Hi + ih) * a.Wi + iw) * a.x_ld + b_coff[j]);
       }
-      rb[j] = v;
+      B[j] = v;
     }
   };
   auto advance_chunk = [&]() {  // every loaded row's pixel += 32
@@ -96,16 +98,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a) {
       }
     }
   };
-  auto store_chunk = [&](int buf) {
+  auto store_chunk = [&](int buf, const f32x4(&A)[A_LD], const f32x4(&B)[B_LD]) {
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       const int idx = t + 256 * j;
-      *(f32x4*)&sA[buf][idx / (BM / 4)][4 * (idx % (BM / 4))] = ra[j];
+      *(f32x4*)&sA[buf][idx / (BM / 4)][4 * (idx % (BM / 4))] = A[j];
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
       const int idx = t + 256 * j;
-      *(f32x4*)&sB[buf][idx / (BN / 4)][4 * (idx % (BN / 4))] = rb[j];
+      *(f32x4*)&sB[buf][idx / (BN / 4)][4 * (idx % (BN / 4))] = B[j];
     }
   };
 
@@ -117,32 +119,52 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(WgradArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   const int h = lane >> 5, l31 = lane & 31;
+  auto compute = [&](int cur) {
+#pragma unroll 4
+    for (int s = 0; s < 16; ++s) {
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = sA[cur][2 * s + h][wm * WM + i * 32 + l31];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = sB[cur][2 * s + h][wn * WN + j * 32 + l31];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  };
   if (m_begin < m_end) {
-    load_chunk(m_begin);
-    store_chunk(0);
+    load_chunk(m_begin, ra, rb);
+    store_chunk(0, ra, rb);
+    if (m_begin + 32 < m_end) {
+      advance_chunk();
+      load_chunk(m_begin + 32, ra, rb);
+    }
     __syncthreads();
     int cur = 0;
-    for (long mc = m_begin; mc < m_end; mc += 32) {
-      const bool more = mc + 32 < m_end;
-      if (more) {
+    long mc = m_begin;
+    // invariant at the top of each half: LDS[cur] holds chunk mc, one register set chunk mc+32
+    while (true) {
+      if (mc + 64 < m_end) {
         advance_chunk();
-        load_chunk(mc + 32);
+        load_chunk(mc + 64, ra2, rb2);
       }
-#pragma unroll 4
-      for (int s = 0; s < 16; ++s) {
-        float av[TM], bv[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) av[i] = sA[cur][2 * s + h][wm * WM + i * 32 + l31];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bv[j] = sB[cur][2 * s + h][wn * WN + j * 32 + l31];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-      }
-      if (more) store_chunk(cur ^ 1);
+      compute(cur);
+      if (mc + 32 < m_end) store_chunk(cur ^ 1, ra, rb);
       __syncthreads();
       cur ^= 1;
+      mc += 32;
+      if (mc >= m_end) break;
+      if (mc + 64 < m_end) {
+        advance_chunk();
+        load_chunk(mc + 64, ra, rb);
+      }
+      compute(cur);
+      if (mc + 32 < m_end) store_chunk(cur ^ 1, ra2, rb2);
+      __syncthreads();
+      cur ^= 1;
+      mc += 32;
+      if (mc >= m_end) break;
     }
   }
   float* out = a.out + (long)split * a.Co * a.K;
