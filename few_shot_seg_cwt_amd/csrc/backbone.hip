@@ -865,4 +865,107 @@ int launch_ppm_field(const float* Q, int N, int h, int w, const int* bins, float
   return 0;
 }
 
+
+// Adjoint of the PPM field (stage-1 pretraining, pretrain.hip): dQ = field^T(dF), gathered in
+// fixed order (no atomics), the two passes of launch_ppm_field in reverse.
+// Pass 1 (rows): dR[n][row(k, i)][x][ky][c] = sum_y u_k(y+ky-1 -> i) dF[n][y][x][c].
+// Workgroup = (n, x, 64 channels); the dF column (h x 64 channels) staged in LDS.
+__global__ __launch_bounds__(256) void ppm_field_bwd_rows_kernel(const float* __restrict__ dF, int N, int h, int w,
+                                                                 PPMBins bn, float* __restrict__ dR) {
+  __shared__ f32x4 gs[PPM_MAXS * 16];
+  __shared__ LerpEntry tab[4][PPM_MAXS + 2];
+  const int t = threadIdx.x;
+  const int n = blockIdx.x / w, x = blockIdx.x % w, c0 = blockIdx.y * 64;
+  for (int e = t; e < h * 16; e += 256) {
+    const int c4 = e & 15, y = e >> 4;
+    gs[e] = *(const f32x4*)(dF + (((long)n * h + y) * w + x) * 512 + c0 + 4 * c4);
+  }
+  for (int e = t; e < 4 * (h + 2); e += 256) {
+    const int k = e / (h + 2), p = e - k * (h + 2);
+    tab[k][p] = lerp_entry(p - 1, h, bn.b[k]);
+  }
+  __syncthreads();
+  for (int e = t; e < 12 * 3 * 16; e += 256) {
+    const int c4 = e & 15, rk = e >> 4;
+    const int row = rk / 3, ky = rk - 3 * row;
+    int k = 3;
+    while (row < bn.row0[k]) --k;
+    const int i = row - bn.row0[k];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int y = 0; y < h; ++y) {
+      const LerpEntry l = tab[k][y + ky];  // destination y + ky - 1
+      const float u = (l.i0 == i ? l.l0 : 0.f) + (l.i1 == i ? l.l1 : 0.f);
+      acc += u * gs[y * 16 + c4];
+    }
+    *(f32x4*)(dR + ((((long)n * 12 + row) * w + x) * 3 + ky) * 512 + c0 + 4 * c4) = acc;
+  }
+}
+
+// Pass 2 (columns): dQ[cell(row, j)][ky*3+kx][c] = sum_x u(x+kx-1 -> j) dR[n][row][x][ky][c].
+// Workgroup = (n, grid row, 64 channels); dR staged in LDS 32 columns at a time.
+constexpr int PPM_BWD_XC = 32;
+__global__ __launch_bounds__(256) void ppm_field_bwd_cols_kernel(const float* __restrict__ dR, int N, int w,
+                                                                 PPMBins bn, float* __restrict__ dQ) {
+  __shared__ f32x4 rs[PPM_BWD_XC * 3 * 16];
+  __shared__ LerpEntry tab[PPM_MAXS + 2];
+  const int t = threadIdx.x;
+  const int n = blockIdx.x / 12, row = blockIdx.x % 12, c0 = blockIdx.y * 64;
+  int k = 3;
+  while (row < bn.row0[k]) --k;
+  const int b = bn.b[k], i = row - bn.row0[k];
+  const long cell0 = (long)bn.cell0[k] * N + (long)n * b * b + (long)i * b;
+  for (int p = t; p < w + 2; p += 256) tab[p] = lerp_entry(p - 1, w, b);
+  const int nout = b * 9 * 16;  // (j, tap, c4), at most 864: 4 per thread
+  f32x4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int xc = 0; xc < w; xc += PPM_BWD_XC) {
+    const int nx = min(PPM_BWD_XC, w - xc);
+    __syncthreads();
+    for (int e = t; e < nx * 3 * 16; e += 256) {
+      const int c4 = e & 15, xk = e >> 4;  // xk = x * 3 + ky
+      rs[e] = *(const f32x4*)(dR + ((((long)n * 12 + row) * w + xc + xk / 3) * 3 + xk % 3) * 512 + c0 + 4 * c4);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + 256 * q;
+      if (e >= nout) break;
+      const int c4 = e & 15, jt = e >> 4;
+      const int j = jt / 9, tap = jt - 9 * j, ky = tap / 3, kx = tap - 3 * ky;
+      for (int xl = 0; xl < nx; ++xl) {
+        const LerpEntry l = tab[xc + xl + kx];  // destination x + kx - 1
+        const float u = (l.i0 == j ? l.l0 : 0.f) + (l.i1 == j ? l.l1 : 0.f);
+        acc[q] += u * rs[(xl * 3 + ky) * 16 + c4];
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = t + 256 * q;
+    if (e >= nout) break;
+    const int c4 = e & 15, jt = e >> 4;
+    *(f32x4*)(dQ + (cell0 + jt / 9) * 4608 + (jt % 9) * 512 + c0 + 4 * c4) = acc[q];
+  }
+}
+
+int launch_ppm_field_bwd(const float* dF, int N, int h, int w, const int* bins, float* dR, float* dQ, hipStream_t st) {
+  PPMBins bn;
+  int cell = 0, row = 0;
+  for (int k = 0; k < 4; ++k) {
+    bn.b[k] = bins[k];
+    bn.cell0[k] = cell;
+    bn.row0[k] = row;
+    cell += bins[k] * bins[k];
+    row += bins[k];
+  }
+  if (row != 12 || bins[3] > 6 || h > PPM_MAXS || w > PPM_MAXS)
+    return fail(CWT_EARG, "PPM field adjoint expects bins {1,2,3,6} and a feature side <= 160");
+  hipLaunchKernelGGL(ppm_field_bwd_rows_kernel, dim3(N * w, 8), dim3(256), 0, st, dF, N, h, w, bn, dR);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ppm_field_bwd_cols_kernel, dim3(N * 12, 8), dim3(256), 0, st, (const float*)dR, N, w, bn, dQ);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // namespace cwt

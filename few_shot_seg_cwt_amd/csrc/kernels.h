@@ -190,5 +190,7 @@ int launch_ppm_gemm(const float* A, int lda, const float* const* Bt, const int* 
                     const float* const* scale, const float* const* shift, float* part, size_t part_floats,
                     float* out, hipStream_t st);
 int launch_ppm_field(const float* Q, int N, int h, int w, const int* bins, float* R, float* F, hipStream_t st);
+// its adjoint: dQ [cells][9 * 512] from dF [N][h][w][512] (dR: R's shape, scratch)
+int launch_ppm_field_bwd(const float* dF, int N, int h, int w, const int* bins, float* dR, float* dQ, hipStream_t st);
 
 }  // namespace cwt

@@ -84,6 +84,8 @@ struct PtGemm {
   float* slab;
 };
 int launch_pt_gemm(PtGemm g, float* ws, size_t ws_floats, hipStream_t st);
+// bottleneck weights' PPM-branch columns <-> GEMM form wq[4][512 ci][9 * 512] (dir 0: w -> wq, 1: wq -> w)
+int launch_ppm_wq(float* w, long w_ld, float* wq, int dir, hipStream_t st);
 
 struct PtLoss {
   const float* logits;    // [N][h][w][nc]

@@ -10,8 +10,8 @@
 // in that order; stem conv1 as [ci*9 + tap][co] (launch_stem_conv1); the rest as in PyTorch.
 // cwt_pretrain_get converts to PyTorch layouts by name.  Activations are fp32 NHWC; the forward
 // keeps each conv's raw output (for its BN backward) and each BN's output (ReLU mask, next conv's
-// input for the weight gradient).  The PPM branch runs unfolded here (the 4096-channel concat
-// map), since its weights train.
+// input for the weight gradient).  The PPM branch is folded into the bottleneck conv as in the
+// episode path (its field as the conv's residual), with the field's adjoint for its gradients.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -364,7 +364,9 @@ struct PtStep {
     return launch_ptbn_bwd(b, pt->G + L.bn.g_off, pt->G + L.bn.b_off, part, part_floats, sums, st);
   }
 
-  int wgrad(const PtConv& L, const float* dy, const float* x, int x_ld, int N, int Hi) {
+  // Ci >= 0: only the first Ci input channels (a K prefix of the packed order), into out [Co][k k Ci]
+  int wgrad(const PtConv& L, const float* dy, const float* x, int x_ld, int N, int Hi, int Ci = -1,
+            float* out = nullptr) {
     WgradArgs w;
     std::memset(&w, 0, sizeof(w));
     w.dy = dy;
@@ -376,16 +378,18 @@ struct PtStep {
     w.Ho = w.Wo = (Hi + 2 * L.pad - L.dil * (L.k - 1) - 1) / L.stride + 1;
     w.M = (long)N * w.Ho * w.Wo;
     w.Co = L.Co;
-    w.K = L.k * L.k * L.Ci;
+    w.K = L.k * L.k * (Ci >= 0 ? Ci : L.Ci);
     w.kh = w.kw = L.k;
     w.stride = L.stride;
     w.pad = L.pad;
     w.dil = L.dil;
-    return launch_conv_wgrad(w, pt->G + L.w_off, slab, slab_floats, st);
+    return launch_conv_wgrad(w, out ? out : pt->G + L.w_off, slab, slab_floats, st);
   }
 
-  // dx (row stride dx_ld) = input gradient of conv L from dy [N][Ho][Ho][Co] (+ res)
-  int dgrad(PtConv& L, const float* dy, int N, int Hi, float* dx, int dx_ld, const float* res, int res_ld, int stage) {
+  // dx (row stride dx_ld) = input gradient of conv L from dy [N][Ho][Ho][Co] (+ res); Ci >= 0:
+  // only the first Ci input channels
+  int dgrad(PtConv& L, const float* dy, int N, int Hi, float* dx, int dx_ld, const float* res, int res_ld, int stage,
+            int Ci = -1) {
     int rc;
     const int taps = L.k * L.k;
     if ((rc = launch_wt_transpose(pt->P + L.w_off, L.wt, L.Co, L.Ci, taps, st))) return rc;
@@ -397,8 +401,8 @@ struct PtStep {
       if ((rc = launch_zero_insert(dy, N, Ho, Ho, L.Co, z, Hi, Hi, st))) return rc;
       src = z;
     }
-    return conv_fwd(L, src, N, Hi, L.Co, dx, dx_ld, stage, L.wt, L.Co, L.Ci, 1, L.dil * (L.k - 1) - L.pad, res,
-                    res_ld);
+    return conv_fwd(L, src, N, Hi, L.Co, dx, dx_ld, stage, L.wt, L.Co, Ci >= 0 ? Ci : L.Ci, 1,
+                    L.dil * (L.k - 1) - L.pad, res, res_ld);
   }
 
   int gemm(const float* A, long sai, long sak, const float* Bm, long sbk, long sbj, float* C, long ldc, int M, int N,
@@ -549,10 +553,22 @@ static int pt_forward(cwt_pretrain* pt, PtStep& s, const float* img, int train, 
       x_ld = b.c3.a_ld;
       H = b.c2.Ho;
     }
-  // PPM (pspnet.py:19-38): adaptive pools of layer4 (the concat map's first 2048 channels)
-  float* col;
+  // PPM (pspnet.py:19-38): adaptive pools of layer4 (the concat map's first 2048 channels).
+  // The branch outputs P_b stay on their b x b grids and enter the bottleneck conv folded
+  // (backbone.hip, "PPM branch of the bottleneck conv, folded"): Q_b = P_b . W_b[tap] over the
+  // bottleneck weights' PPM columns (GEMM form Wq), the field F = sum over taps and cells of the
+  // interpolation weights times Q is the residual of the conv over the 2048 layer4 channels.
+  PtConv& Bt = pt->bott;
+  int ncells = 0;
+  for (int b : kPtBins) ncells += b * b;
+  float *col, *Wq, *Q, *R, *Fld, *Wl;
   if ((rc = pt_ws(pt, "ppmcol", ((size_t)N * h * 16 * 2048 + (size_t)N * 16 * 16 * 2048) * 4, &col)) ||
-      (rc = launch_ppm(pt->CAT, N, h, h, 4096, kPtBins, 4, col, pt->POOL, st, ACT_F32)))
+      (rc = pt_ws(pt, "wq", (size_t)4 * 512 * 4608 * 4, &Wq)) ||
+      (rc = pt_ws(pt, "q", (size_t)N * ncells * 4608 * 4, &Q)) ||
+      (rc = pt_ws(pt, "r", (size_t)N * 12 * h * 3 * 512 * 4, &R)) || (rc = pt_ws(pt, "field", (size_t)Mh * 512 * 4, &Fld)) ||
+      (rc = pt_ws(pt, "wl", (size_t)512 * 2048 * 9 * 4, &Wl)) ||
+      (rc = launch_ppm(pt->CAT, N, h, h, 4096, kPtBins, 4, col, pt->POOL, st, ACT_F32)) ||
+      (rc = launch_ppm_wq(pt->P + Bt.w_off, 4096 * 9, Wq, 0, st)))
     return rc;
   long base = 0;
   for (int i = 0; i < 4; ++i) {
@@ -562,13 +578,17 @@ static int pt_forward(cwt_pretrain* pt, PtStep& s, const float* img, int train, 
     const float* pool = pt->POOL + base * N * 2048;
     if ((rc = s.gemm(pool, 2048, 1, pt->P + L.w_off, 1, 2048, L.y, 512, (int)Mb, 512, 2048)) ||
         (rc = s.bn_fwd(L, L.y, 512, Mb, train, bn_mom)) || (rc = s.bn_apply(L, Mb, L.a, 512, 1)) ||
-        (rc = launch_ppm_upsample(L.a, N, b, h, pt->CAT, 4096, 2048 + 512 * i, st)))
+        (rc = s.gemm(L.a, 512, 1, Wq + (size_t)i * 512 * 4608, 4608, 1, Q + base * N * 4608, 4608, (int)Mb, 4608, 512)))
       return rc;
     base += b * b;
   }
-  // bottleneck conv3x3 4096 -> 512 + BN + ReLU + Dropout2d (pspnet.py:124-129)
-  PtConv& Bt = pt->bott;
-  if ((rc = s.conv_fwd(Bt, pt->CAT, N, h, 4096, Bt.y, 512, 6)) || (rc = s.bn_fwd(Bt, Bt.y, 512, Mh, train, bn_mom)) ||
+  // bottleneck conv3x3 4096 -> 512 + BN + ReLU + Dropout2d (pspnet.py:124-129): the layer4
+  // columns of the packed weights are a K prefix (packed_k's 32-channel blocks), copied dense
+  if ((rc = launch_ppm_field(Q, N, h, h, kPtBins, R, Fld, st))) return rc;
+  CWT_HIP(hipMemcpy2DAsync(Wl, (size_t)2048 * 9 * 4, pt->P + Bt.w_off, (size_t)4096 * 9 * 4, (size_t)2048 * 9 * 4, 512,
+                           hipMemcpyDeviceToDevice, st));
+  if ((rc = s.conv_fwd(Bt, pt->CAT, N, h, 4096, Bt.y, 512, 6, Wl, 2048, 512, -1, -1, Fld, 512)) ||
+      (rc = s.bn_fwd(Bt, Bt.y, 512, Mh, train, bn_mom)) ||
       (rc = s.bn_apply(Bt, Mh, pt->F, 512, 1, nullptr, nullptr, 0, (long)h * h, train ? pt->drop_p : 0.f, pt->Fpre)))
     return rc;
   // classifier conv1x1 512 -> nc (pspnet.py:131-132), logits [M][nc]
@@ -593,15 +613,25 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
   if ((rc = s.gemm(dlogits, pt->nc, 1, pt->P + pt->cls_off, 512, 1, gA, 512, (int)Mh, 512, pt->nc)) ||
       (rc = s.gemm(dlogits, 1, pt->nc, pt->F, 512, 1, pt->G + pt->cls_off, 512, pt->nc, 512, Mh)))
     return rc;
-  // bottleneck: Dropout2d + ReLU + BN backward, weight gradient over the concat map, input gradient
+  // bottleneck: Dropout2d + ReLU + BN backward; the layer4 columns' weight gradient (dense, copied
+  // into the packed rows) and input gradient; the PPM columns through the field's adjoint
   PtConv& Bt = pt->bott;
-  if ((rc = s.bn_bwd(Bt, Mh, gA, 512, kReluFromY, 512, gY, nullptr, 0, (long)h * h, drop)) ||
-      (rc = s.wgrad(Bt, gY, pt->CAT, 4096, N, h)) || (rc = s.dgrad(Bt, gY, N, h, dcat, 4096, nullptr, 0, 6)))
-    return rc;
-  // PPM branch: upsample adjoint -> ReLU + BN backward -> 1x1 conv gradients -> pool adjoint
-  float* dpool;
   int ncells = 0;
   for (int b : kPtBins) ncells += b * b;
+  float *gWl, *gWq, *dQ, *R, *Wq;  // Wq: the forward's GEMM-form weights
+  if ((rc = pt_ws(pt, "wq", (size_t)4 * 512 * 4608 * 4, &Wq)) || (rc = pt_ws(pt, "gwl", (size_t)512 * 2048 * 9 * 4, &gWl)) || (rc = pt_ws(pt, "gwq", (size_t)4 * 512 * 4608 * 4, &gWq)) ||
+      (rc = pt_ws(pt, "dq", (size_t)N * ncells * 4608 * 4, &dQ)) || (rc = pt_ws(pt, "r", (size_t)N * 12 * h * 3 * 512 * 4, &R)))
+    return rc;
+  if ((rc = s.bn_bwd(Bt, Mh, gA, 512, kReluFromY, 512, gY, nullptr, 0, (long)h * h, drop)) ||
+      (rc = s.wgrad(Bt, gY, pt->CAT, 4096, N, h, 2048, gWl)) ||
+      (rc = s.dgrad(Bt, gY, N, h, dcat, 4096, nullptr, 0, 6, 2048)) ||
+      (rc = launch_ppm_field_bwd(gY, N, h, h, kPtBins, R, dQ, s.st)))
+    return rc;
+  CWT_HIP(hipMemcpy2DAsync(pt->G + Bt.w_off, (size_t)4096 * 9 * 4, gWl, (size_t)2048 * 9 * 4, (size_t)2048 * 9 * 4, 512,
+                           hipMemcpyDeviceToDevice, s.st));
+  // PPM branch: dP_b = dQ_b . W_b^T and dW_b = P_b^T . dQ_b, then ReLU + BN backward -> 1x1 conv
+  // gradients -> pool adjoint
+  float* dpool;
   if ((rc = pt_ws(pt, "dpool", (size_t)N * ncells * 2048 * 4, &dpool))) return rc;
   long base = 0;
   for (int i = 0; i < 4; ++i) {
@@ -609,14 +639,18 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
     const long Mb = (long)N * b * b;
     PtConv& L = pt->ppm[i];
     const float* pool = pt->POOL + base * N * 2048;
-    if ((rc = launch_ppm_upsample_bwd(dcat, 4096, 2048 + 512 * i, N, b, h, gT, s.slab, s.st)) ||
+    const float* dQb = dQ + base * N * 4608;
+    if ((rc = s.gemm(dQb, 4608, 1, Wq + (size_t)i * 512 * 4608, 1, 4608, gT, 512, (int)Mb, 512, 4608)) ||
+        (rc = s.gemm(L.a, 1, 512, dQb, 4608, 1, gWq + (size_t)i * 512 * 4608, 4608, 512, 4608, Mb)) ||
         (rc = s.bn_bwd(L, Mb, gT, 512, kReluFromY, 512, gY)) ||
         (rc = s.gemm(gY, 1, 512, pool, 2048, 1, pt->G + L.w_off, 2048, 512, 2048, Mb)) ||
         (rc = s.gemm(gY, 512, 1, pt->P + L.w_off, 2048, 1, dpool + base * N * 2048, 2048, (int)Mb, 2048, 512)))
       return rc;
     base += b * b;
   }
-  if ((rc = launch_avgpool_bwd(dpool, N, h, 2048, kPtBins, dcat, 4096, s.st))) return rc;
+  if ((rc = launch_ppm_wq(pt->G + Bt.w_off, 4096 * 9, gWq, 1, s.st)) ||
+      (rc = launch_avgpool_bwd(dpool, N, h, 2048, kPtBins, dcat, 4096, s.st)))
+    return rc;
   // ResNet blocks in reverse (resnet.py:74-96)
   const float* dout = dcat;
   int dout_ld = 4096;

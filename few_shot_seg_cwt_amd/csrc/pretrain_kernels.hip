@@ -905,6 +905,33 @@ __global__ void slab_reduce_2d_kernel(const float* __restrict__ slabs, int nspli
   C[(i / N) * ldc + i % N] = v;
 }
 
+// The PPM-branch columns of the bottleneck weights (input channels 2048 + 512 i + ci) in GEMM
+// form for the folded PPM field:  dir 0  wq[i][ci][tap * 512 + co] = w[co][packed_k(2048 + 512 i + ci, tap)];
+// dir 1 writes wq back into w (the weight gradient).  32 x 32 tiles transposed through LDS.
+__global__ __launch_bounds__(256) void ppm_wq_kernel(float* __restrict__ w, long w_ld, float* __restrict__ wq, int dir) {
+  __shared__ float tile[32][33];
+  const int i = blockIdx.x / 9, tap = blockIdx.x % 9;
+  const int cb = blockIdx.y, co0 = blockIdx.z * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const long kb = packed_k(2048 + 512 * i + 32 * cb, tap, 9);  // the block's 32 channels are contiguous
+  float* q = wq + ((long)i * 512 + 32 * cb) * 4608 + tap * 512 + co0;
+  if (dir == 0) {
+    for (int r = ty; r < 32; r += 8) tile[r][tx] = w[(long)(co0 + r) * w_ld + kb + tx];
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) q[(long)r * 4608 + tx] = tile[tx][r];
+  } else {
+    for (int r = ty; r < 32; r += 8) tile[r][tx] = q[(long)r * 4608 + tx];
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) w[(long)(co0 + r) * w_ld + kb + tx] = tile[tx][r];
+  }
+}
+
+int launch_ppm_wq(float* w, long w_ld, float* wq, int dir, hipStream_t st) {
+  hipLaunchKernelGGL(ppm_wq_kernel, dim3(36, 16, 16), dim3(256), 0, st, w, w_ld, wq, dir);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 int launch_pt_gemm(PtGemm g, float* ws, size_t ws_floats, hipStream_t st) {
   const long tiles = (long)cdiv(g.M, 64) * cdiv(g.N, 64);
   int ns = 1;
