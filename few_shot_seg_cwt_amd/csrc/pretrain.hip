@@ -1064,6 +1064,63 @@ extern "C" int cwt_debug_pretrain_op(cwt_ctx* ctx, int op, void* const* b, const
     const size_t left = wsf - (size_t)(part - ws);
     return launch_conv(a, pl, 0, part, left, st);
   }
+  if (op == 5) {  // folded PPM field and its adjoint: b = P dF F dP W dW; ia = N h
+    // P [cells][512] bin-major (bins 1 2 3 6, cell = bin start * N + n b b + i b + j), W / dW the
+    // packed bottleneck weights [512][4096 * 9] (dW: only the PPM columns written), F / dF [N][h][h][512]
+    const int N = (int)ia[0], h = (int)ia[1];
+    int ncells = 0;
+    for (int bb : kPtBins) ncells += bb * bb;
+    float* Wq = ws;
+    float* gWq = Wq + (size_t)4 * 512 * 4608;
+    float* Q = gWq + (size_t)4 * 512 * 4608;
+    float* dQ = Q + (size_t)N * ncells * 4608;
+    float* R = dQ + (size_t)N * ncells * 4608;
+    float* slab = R + (size_t)N * 12 * h * 1536;
+    const size_t used = (size_t)(slab - ws);
+    if (used + ((size_t)8 << 20) > wsf) return fail(CWT_EARG, "debug PPM field: too large");
+    auto gemm = [&](const float* A, long sai, long sak, const float* Bm, long sbk, long sbj, float* C, long ldc, int M,
+                    int Nn, long K) {
+      PtGemm g;
+      std::memset(&g, 0, sizeof(g));
+      g.A = A;
+      g.sai = sai;
+      g.sak = sak;
+      g.B = Bm;
+      g.sbk = sbk;
+      g.sbj = sbj;
+      g.C = C;
+      g.ldc = ldc;
+      g.M = M;
+      g.N = Nn;
+      g.K = K;
+      return launch_pt_gemm(g, slab, wsf - used, st);
+    };
+    const float* P = (const float*)b[0];
+    float* dP = (float*)b[3];
+    int rc;
+    if ((rc = launch_ppm_wq((float*)b[4], 4096 * 9, Wq, 0, st))) return rc;
+    long base = 0;
+    for (int i = 0; i < 4; ++i) {
+      const int Mb = N * kPtBins[i] * kPtBins[i];
+      if ((rc = gemm(P + base * N * 512, 512, 1, Wq + (size_t)i * 512 * 4608, 4608, 1, Q + base * N * 4608, 4608, Mb,
+                     4608, 512)))
+        return rc;
+      base += kPtBins[i] * kPtBins[i];
+    }
+    if ((rc = launch_ppm_field(Q, N, h, h, kPtBins, R, (float*)b[2], st)) ||
+        (rc = launch_ppm_field_bwd((const float*)b[1], N, h, h, kPtBins, R, dQ, st)))
+      return rc;
+    base = 0;
+    for (int i = 0; i < 4; ++i) {
+      const int Mb = N * kPtBins[i] * kPtBins[i];
+      const float* dQb = dQ + base * N * 4608;
+      if ((rc = gemm(dQb, 4608, 1, Wq + (size_t)i * 512 * 4608, 1, 4608, dP + base * N * 512, 512, Mb, 512, 4608)) ||
+          (rc = gemm(P + base * N * 512, 1, 512, dQb, 4608, 1, gWq + (size_t)i * 512 * 4608, 4608, 512, 4608, Mb)))
+        return rc;
+      base += kPtBins[i] * kPtBins[i];
+    }
+    return launch_ppm_wq((float*)b[5], 4096 * 9, gWq, 1, st);
+  }
   if (op == 2) {  // label-smoothed CE: b = logits, target, dlogits, loss; ia = N S h nc; fa = on off
     PtLoss L;
     std::memset(&L, 0, sizeof(L));

@@ -79,7 +79,9 @@ int cwt_stream_destroy(void* stream);
  * pad dil; NHWC fp32, weights packed [Co][K] as conv.hip), 2 label-smoothed CE (b = logits
  * [N][h][h][nc], int64 target, dlogits, loss; ia = N S h nc; fa = on off), 3 training BN + ReLU
  * forward and backward (b = y gamma beta out dout dy dgamma dbeta; ia = M C; fa = eps), 4 max
- * pool 3x3 s2 p1 forward and adjoint (b = in out dout din; ia = N H C). */
+ * pool 3x3 s2 p1 forward and adjoint (b = in out dout din; ia = N H C), 5 the folded PPM field of
+ * the bottleneck conv and its adjoint (b = P dF F dP W dW; ia = N h; P [cells][512] bin-major,
+ * W / dW packed [512][4096 * 9], only dW's PPM columns written). */
 int cwt_debug_pretrain_op(cwt_ctx* ctx, int op, void* const* bufs, const int64_t* iargs, const float* fargs,
                           void* stream);
 

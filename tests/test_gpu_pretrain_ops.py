@@ -2,7 +2,8 @@
 autograd on random data -- well conditioned, unlike the whole-network step (test_gpu_pretrain.py),
 so the bars are tight: conv weight / input gradients over every conv geometry of the ResNet
 (1x1, 3x3 dilated, stride 2, the 4096-channel bottleneck shape reduced), training BN + ReLU
-backward, max-pool adjoint, label-smoothed CE of the upsampled logits and its gradient."""
+backward, max-pool adjoint, label-smoothed CE of the upsampled logits and its gradient, the
+folded PPM field of the bottleneck conv and its adjoint."""
 import ctypes as C
 
 import numpy as np
@@ -112,5 +113,33 @@ def test_smoothed_ce(dev, nc, S):
     dl, lo = torch.empty(N, h, h, nc, device=dev), torch.empty(1, device=dev)
     op(2, [lg.detach().permute(0, 2, 3, 1).contiguous().float().to(dev), t.to(dev), dl, lo], [N, S, h, nc],
        [0.9, 0.1 / (nc - 1)])
-    assert abs(float(lo) - float(loss)) / float(loss) < 1e-5
+    assert abs(float(lo) - loss.item()) / loss.item() < 1e-5
     assert rel(dl.cpu(), g.permute(0, 2, 3, 1)) < 1e-4
+
+
+@pytest.mark.parametrize("N,h", [(2, 17), (1, 60)])
+def test_ppm_field_fold_and_adjoint(dev, N, h):
+    """The pretraining bottleneck's folded PPM branch (pretrain.hip pt_forward / pt_backward):
+    F = conv3x3(W_ppm, cat_b upsample_b(P_b)) without the upsampled maps, and its adjoint dP, dW
+    (the field's transpose), against the unfolded float64 form of pspnet.py:19-38,124-128."""
+    gen = torch.Generator().manual_seed(h)
+    bins = (1, 2, 3, 6)
+    Ps = [torch.randn(N, 512, b, b, generator=gen, dtype=torch.float64, requires_grad=True) for b in bins]
+    Wfull = torch.randn(512, 4096, 3, 3, generator=gen, dtype=torch.float64) * 0.02
+    Wp = Wfull[:, 2048:].clone().requires_grad_(True)
+    up = torch.cat([F.interpolate(p, size=(h, h), mode="bilinear", align_corners=True) for p in Ps], 1)
+    Fr = F.conv2d(up, Wp, padding=1)
+    dF = torch.randn(Fr.shape, generator=gen, dtype=torch.float64)
+    gps = torch.autograd.grad(Fr, Ps + [Wp], dF)
+    cells = lambda ts: torch.cat([t.detach().permute(0, 2, 3, 1).reshape(-1, 512) for t in ts], 0)
+    nhwc = lambda t: t.detach().permute(0, 2, 3, 1).contiguous().float().to(dev)
+    Pd = cells(Ps).float().contiguous().to(dev)
+    Fo, dP = torch.empty(N, h, h, 512, device=dev), torch.empty_like(Pd)
+    W = pack(Wfull).float().contiguous().to(dev)
+    dW = torch.zeros_like(W)
+    op(5, [Pd, nhwc(dF), Fo, dP, W, dW], [N, h])
+    assert rel(Fo.cpu(), Fr.permute(0, 2, 3, 1)) < 1e-5
+    assert rel(dP.cpu(), cells(gps[:4])) < 1e-5
+    gW = torch.zeros_like(Wfull)
+    gW[:, 2048:] = gps[4]
+    assert rel(dW.cpu(), pack(gW)) < 1e-5
