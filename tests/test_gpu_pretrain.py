@@ -53,7 +53,7 @@ def args(**over):
     return a
 
 
-def run_case(dev, layers, N, S, nc, drop, steps=2):
+def run_case(dev, layers, N, S, nc, drop, steps=2, npert=NPERT):
     from few_shot_seg_cwt_amd.pretrain import PretrainPSPNet
     from oracle.pretrain_oracle import pretrain_step
     a = args(layers=layers, num_classes_tr=nc, dropout=drop)
@@ -84,7 +84,7 @@ def run_case(dev, layers, N, S, nc, drop, steps=2):
         # the same fp32 oracle on NPERT 1e-7-perturbed inputs (running statistics on copies): the
         # spread is often bimodal (a ReLU / BN-branch flip moves a tensor by ~0.1 or not at all)
         perts = []
-        for pi in range(NPERT):
+        for pi in range(npert):
             sdp = {k: v.clone() for k, v in sd32_prev.items()}
             xp = x * (1 + 1e-7 * torch.from_numpy(syn.normal(SEED + 97 * it + pi, "pt_pert", tuple(x.shape), 1.0)))
             _, gp, np_, bp = pretrain_step(sdp, xp, t, nc, layers, a["lr"], a["scale_lr"], a["momentum"],
@@ -118,6 +118,13 @@ def run_case(dev, layers, N, S, nc, drop, steps=2):
 @pytest.mark.parametrize("layers,N,S,nc,drop", [(50, 4, 65, 16, 0.0), (50, 4, 65, 61, 0.1), (101, 2, 65, 16, 0.0)])
 def test_pretrain_step_vs_oracle(dev, layers, N, S, nc, drop):
     run_case(dev, layers, N, S, nc, drop)
+
+
+def test_pretrain_step_full_size(dev):
+    """One iteration at the benchmark's image size (473, R50, 2 images, 16 classes): the folded
+    PPM field over the 60 x 60 map, the split-pixel weight gradients at full M, the CE over
+    473^2 pixels, against the oracle (fp32 / float64, two perturbed runs for the bar)."""
+    run_case(dev, 50, 2, 473, 16, 0.0, steps=1, npert=2)
 
 
 def test_pretrain_logits_eval_and_roundtrip(dev):
