@@ -68,9 +68,6 @@ int launch_ptbn_bwd(const PtBnBwd& a, float* dgamma, float* dbeta, float* part, 
 
 int launch_maxpool_idx(const float* in, int N, int H, int C, float* out, uint8_t* idx, int Ho, hipStream_t st);
 int launch_maxpool_bwd(const float* dout, const uint8_t* idx, int N, int H, int C, int Ho, float* din, hipStream_t st);
-int launch_ppm_upsample(const float* P, int N, int b, int h, float* cat, int ld, int off, hipStream_t st);
-int launch_ppm_upsample_bwd(const float* dcat, int ld, int off, int N, int b, int h, float* dP, float* ws,
-                            hipStream_t st);
 int launch_avgpool_bwd(const float* dpool, int N, int h, int C, const int* bins, float* dx, int ld, hipStream_t st);
 
 struct PtGemm {

@@ -447,7 +447,7 @@ static int pt_ensure_acts(cwt_pretrain* pt, int N, int S) {
   float* idx;
   if ((rc = pt_ws(pt, "mpidx", (size_t)M1 * 128, &idx))) return rc;
   pt->MPIDX = (uint8_t*)idx;
-  if ((rc = pt_ws(pt, "cat", (size_t)Mh * 4096 * 4, &pt->CAT))) return rc;
+  if ((rc = pt_ws(pt, "cat", (size_t)Mh * 2048 * 4, &pt->CAT))) return rc;
   int H = H1;
   for (int li = 0; li < 4; ++li)
     for (int bi = 0; bi < (int)pt->blocks[li].size(); ++bi) {
@@ -466,8 +466,8 @@ static int pt_ensure_acts(cwt_pretrain* pt, int N, int S) {
       const bool last = li == 3 && bi == (int)pt->blocks[3].size() - 1;
       if (last) {
         if ((rc = act(b.c3, p + ".c3", Mo, false))) return rc;
-        b.c3.a = pt->CAT;  // layer4's output is the concat map's first 2048 channels
-        b.c3.a_ld = 4096;
+        b.c3.a = pt->CAT;  // layer4's output: the PPM's and the bottleneck conv's input
+        b.c3.a_ld = 2048;
       } else if ((rc = act(b.c3, p + ".c3", Mo, true))) {
         return rc;
       }
@@ -553,7 +553,7 @@ static int pt_forward(cwt_pretrain* pt, PtStep& s, const float* img, int train, 
       x_ld = b.c3.a_ld;
       H = b.c2.Ho;
     }
-  // PPM (pspnet.py:19-38): adaptive pools of layer4 (the concat map's first 2048 channels).
+  // PPM (pspnet.py:19-38): adaptive pools of layer4 (CAT, 2048 channels).
   // The branch outputs P_b stay on their b x b grids and enter the bottleneck conv folded
   // (backbone.hip, "PPM branch of the bottleneck conv, folded"): Q_b = P_b . W_b[tap] over the
   // bottleneck weights' PPM columns (GEMM form Wq), the field F = sum over taps and cells of the
@@ -567,7 +567,7 @@ static int pt_forward(cwt_pretrain* pt, PtStep& s, const float* img, int train, 
       (rc = pt_ws(pt, "q", (size_t)N * ncells * 4608 * 4, &Q)) ||
       (rc = pt_ws(pt, "r", (size_t)N * 12 * h * 3 * 512 * 4, &R)) || (rc = pt_ws(pt, "field", (size_t)Mh * 512 * 4, &Fld)) ||
       (rc = pt_ws(pt, "wl", (size_t)512 * 2048 * 9 * 4, &Wl)) ||
-      (rc = launch_ppm(pt->CAT, N, h, h, 4096, kPtBins, 4, col, pt->POOL, st, ACT_F32)) ||
+      (rc = launch_ppm(pt->CAT, N, h, h, 2048, kPtBins, 4, col, pt->POOL, st, ACT_F32)) ||
       (rc = launch_ppm_wq(pt->P + Bt.w_off, 4096 * 9, Wq, 0, st)))
     return rc;
   long base = 0;
@@ -587,7 +587,7 @@ static int pt_forward(cwt_pretrain* pt, PtStep& s, const float* img, int train, 
   if ((rc = launch_ppm_field(Q, N, h, h, kPtBins, R, Fld, st))) return rc;
   CWT_HIP(hipMemcpy2DAsync(Wl, (size_t)2048 * 9 * 4, pt->P + Bt.w_off, (size_t)4096 * 9 * 4, (size_t)2048 * 9 * 4, 512,
                            hipMemcpyDeviceToDevice, st));
-  if ((rc = s.conv_fwd(Bt, pt->CAT, N, h, 4096, Bt.y, 512, 6, Wl, 2048, 512, -1, -1, Fld, 512)) ||
+  if ((rc = s.conv_fwd(Bt, pt->CAT, N, h, 2048, Bt.y, 512, 6, Wl, 2048, 512, -1, -1, Fld, 512)) ||
       (rc = s.bn_fwd(Bt, Bt.y, 512, Mh, train, bn_mom)) ||
       (rc = s.bn_apply(Bt, Mh, pt->F, 512, 1, nullptr, nullptr, 0, (long)h * h, train ? pt->drop_p : 0.f, pt->Fpre)))
     return rc;
@@ -600,14 +600,14 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
   const long Ms = (long)N * Hs * Hs, Mh = (long)N * h * h;
   const float drop = pt->drop_p;
   int rc;
-  // scratch gradients: the widest activation is the concat map (Mh x 4096) or layer1 / stem
-  size_t mx = (size_t)Mh * 4096;
+  // scratch gradients: the widest activation is the layer4 map (Mh x 2048) or layer1 / stem
+  size_t mx = (size_t)Mh * 2048;
   mx = std::max(mx, (size_t)Ms * 128);
   mx = std::max(mx, (size_t)N * H1 * H1 * 256);
   float *gA, *gB, *gY, *gT, *gR, *dcat;
   if ((rc = pt_ws(pt, "gA", mx * 4, &gA)) || (rc = pt_ws(pt, "gB", mx * 4, &gB)) || (rc = pt_ws(pt, "gY", mx * 4, &gY)) ||
       (rc = pt_ws(pt, "gT", mx * 4, &gT)) || (rc = pt_ws(pt, "gR", mx * 4, &gR)) ||
-      (rc = pt_ws(pt, "dcat", (size_t)Mh * 4096 * 4, &dcat)))
+      (rc = pt_ws(pt, "dcat", (size_t)Mh * 2048 * 4, &dcat)))
     return rc;
   // classifier: dF = dlogits . Wc, dWc = dlogits^T . F
   if ((rc = s.gemm(dlogits, pt->nc, 1, pt->P + pt->cls_off, 512, 1, gA, 512, (int)Mh, 512, pt->nc)) ||
@@ -623,8 +623,8 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
       (rc = pt_ws(pt, "dq", (size_t)N * ncells * 4608 * 4, &dQ)) || (rc = pt_ws(pt, "r", (size_t)N * 12 * h * 3 * 512 * 4, &R)))
     return rc;
   if ((rc = s.bn_bwd(Bt, Mh, gA, 512, kReluFromY, 512, gY, nullptr, 0, (long)h * h, drop)) ||
-      (rc = s.wgrad(Bt, gY, pt->CAT, 4096, N, h, 2048, gWl)) ||
-      (rc = s.dgrad(Bt, gY, N, h, dcat, 4096, nullptr, 0, 6, 2048)) ||
+      (rc = s.wgrad(Bt, gY, pt->CAT, 2048, N, h, 2048, gWl)) ||
+      (rc = s.dgrad(Bt, gY, N, h, dcat, 2048, nullptr, 0, 6, 2048)) ||
       (rc = launch_ppm_field_bwd(gY, N, h, h, kPtBins, R, dQ, s.st)))
     return rc;
   CWT_HIP(hipMemcpy2DAsync(pt->G + Bt.w_off, (size_t)4096 * 9 * 4, gWl, (size_t)2048 * 9 * 4, (size_t)2048 * 9 * 4, 512,
@@ -649,11 +649,11 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
     base += b * b;
   }
   if ((rc = launch_ppm_wq(pt->G + Bt.w_off, 4096 * 9, gWq, 1, s.st)) ||
-      (rc = launch_avgpool_bwd(dpool, N, h, 2048, kPtBins, dcat, 4096, s.st)))
+      (rc = launch_avgpool_bwd(dpool, N, h, 2048, kPtBins, dcat, 2048, s.st)))
     return rc;
   // ResNet blocks in reverse (resnet.py:74-96)
   const float* dout = dcat;
-  int dout_ld = 4096;
+  int dout_ld = 2048;
   float* bufs[2] = {gA, gB};
   int nb = 0;
   for (int li = 3; li >= 0; --li)

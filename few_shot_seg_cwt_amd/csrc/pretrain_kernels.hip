@@ -713,78 +713,10 @@ int launch_maxpool_bwd(const float* dout, const uint8_t* idx, int N, int H, int 
 }
 
 // ------------------------------------------------------------------------------------------
-// PPM branch (pspnet.py:19-38) in its unfolded training form.
-//   upsample: cells P_b [N][b][b][512] -> channels [off, off+512) of the concat map, bilinear
-//             align_corners=True (common.h lerp_coord: PyTorch's CPU source-index arithmetic)
-//   upsample adjoint: dP_b[n][i][j][c] = sum_{y,x} u_y(i) u_x(j) dcat[n][y][x][off + c]
+// PPM branch (pspnet.py:19-38) backward outside the folded field (backbone.hip):
 //   adaptive-average-pool adjoint: dx[n][y][x][c] += sum over the bins' windows holding (y, x)
 //             of dpooled / kh / kw (torch adaptive_avg_pool2d_backward), added in place
 // ------------------------------------------------------------------------------------------
-__global__ void ppm_upsample_kernel(const float* __restrict__ P, int N, int b, int h, float* __restrict__ cat, int ld,
-                                    int off) {
-  const long total = (long)N * h * h * 128;
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int c4 = (int)(i & 127);
-  const long p = i >> 7;
-  const int x = (int)(p % h), y = (int)((p / h) % h), n = (int)(p / ((long)h * h));
-  const float sc = align_corners_scale(b, h);
-  const Lerp ly = lerp_coord(y, b, sc), lx = lerp_coord(x, b, sc);
-  const float* q = P + (long)n * b * b * 512 + 4 * c4;
-  const f32x4 v00 = *(const f32x4*)(q + (ly.i0 * b + lx.i0) * 512), v01 = *(const f32x4*)(q + (ly.i0 * b + lx.i1) * 512);
-  const f32x4 v10 = *(const f32x4*)(q + (ly.i1 * b + lx.i0) * 512), v11 = *(const f32x4*)(q + (ly.i1 * b + lx.i1) * 512);
-  f32x4 o;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) o[k] = ly.l0 * (lx.l0 * v00[k] + lx.l1 * v01[k]) + ly.l1 * (lx.l0 * v10[k] + lx.l1 * v11[k]);
-  *(f32x4*)(cat + p * ld + off + 4 * c4) = o;
-}
-
-// adjoint of the upsample in two separable passes (f32x4 over channels):
-//   R[n][y][j][c] = sum_x u_x(j) dcat[n][y][x][off + c]     (thread per (n, y, j, c4))
-//   dP[n][i][j][c] = sum_y u_y(i) R[n][y][j][c]              (thread per (n, i, j, c4))
-// the loops run over the full row / column with the weight test (h <= ~80, b <= 6)
-__global__ void ppm_upsample_bwd_x_kernel(const float* __restrict__ dcat, int ld, int off, int N, int b, int h,
-                                          float* __restrict__ R) {
-  const long total = (long)N * h * b * 128;
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int c4 = (int)(i & 127);
-  const long p = i >> 7;
-  const int j = (int)(p % b), y = (int)((p / b) % h), n = (int)(p / ((long)b * h));
-  const float sc = align_corners_scale(b, h);
-  const float* row = dcat + (((long)n * h + y) * h) * ld + off + 4 * c4;
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  for (int x = 0; x < h; ++x) {
-    const Lerp lx = lerp_coord(x, b, sc);
-    const float wx = (lx.i0 == j ? lx.l0 : 0.f) + (lx.i1 == j ? lx.l1 : 0.f);
-    if (wx == 0.f) continue;
-    const f32x4 v = *(const f32x4*)(row + (long)x * ld);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) s[q] = fmaf(wx, v[q], s[q]);
-  }
-  *(f32x4*)(R + p * 512 + 4 * c4) = s;
-}
-
-__global__ void ppm_upsample_bwd_y_kernel(const float* __restrict__ R, int N, int b, int h, float* __restrict__ dP) {
-  const long total = (long)N * b * b * 128;
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int c4 = (int)(i & 127);
-  const long cell = i >> 7;
-  const int j = (int)(cell % b), ii = (int)((cell / b) % b), n = (int)(cell / ((long)b * b));
-  const float sc = align_corners_scale(b, h);
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  for (int y = 0; y < h; ++y) {
-    const Lerp ly = lerp_coord(y, b, sc);
-    const float wy = (ly.i0 == ii ? ly.l0 : 0.f) + (ly.i1 == ii ? ly.l1 : 0.f);
-    if (wy == 0.f) continue;
-    const f32x4 v = *(const f32x4*)(R + (((long)n * h + y) * b + j) * 512 + 4 * c4);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) s[q] = fmaf(wy, v[q], s[q]);
-  }
-  *(f32x4*)(dP + cell * 512 + 4 * c4) = s;
-}
-
 // pooled gradient rows bin-major as launch_ppm writes them: bin k's rows [base_k N, (base_k + b^2) N);
 // 4 channels per thread, only the windows near (y, x) b / h per bin and axis visited
 __global__ void avgpool_bwd_kernel(const float* __restrict__ dpool, int N, int h, int C, int b0, int b1, int b2, int b3,
@@ -818,23 +750,6 @@ __global__ void avgpool_bwd_kernel(const float* __restrict__ dpool, int N, int h
   }
   f32x4* d = (f32x4*)(dx + p * ld + c0);
   *d = *d + s;
-}
-
-int launch_ppm_upsample(const float* P, int N, int b, int h, float* cat, int ld, int off, hipStream_t st) {
-  const long total = (long)N * h * h * 128;
-  hipLaunchKernelGGL(ppm_upsample_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, P, N, b, h, cat, ld, off);
-  CWT_LAUNCH_CHECK();
-  return 0;
-}
-
-int launch_ppm_upsample_bwd(const float* dcat, int ld, int off, int N, int b, int h, float* dP, float* ws,
-                            hipStream_t st) {
-  const long t1 = (long)N * h * b * 128, t2 = (long)N * b * b * 128;
-  hipLaunchKernelGGL(ppm_upsample_bwd_x_kernel, dim3(cdiv(t1, 256)), dim3(256), 0, st, dcat, ld, off, N, b, h, ws);
-  CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ppm_upsample_bwd_y_kernel, dim3(cdiv(t2, 256)), dim3(256), 0, st, (const float*)ws, N, b, h, dP);
-  CWT_LAUNCH_CHECK();
-  return 0;
 }
 
 int launch_avgpool_bwd(const float* dpool, int N, int h, int C, const int* bins, float* dx, int ld, hipStream_t st) {
