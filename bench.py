@@ -33,11 +33,36 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg, sd, tsd, budget_s: float = 25.0, max_eps: int = 4):
-    """The oracle (CPU restatement of the reference path) on the host cores, bounded sample."""
+def host_cpu_info() -> dict:
+    """The host's CPU facts SURVEY.md §8(d) asks the CPU baseline to state: `nproc` (GNU
+    coreutils: the CPUs this process may use, capped by OMP_NUM_THREADS where the launcher sets
+    it -- the gpurun box grants 16 per GPU), os.cpu_count() (every CPU of the machine), the CPU
+    model and OMP_NUM_THREADS."""
+    import subprocess
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=10).stdout.strip())
+    except Exception:
+        nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": nproc, "os_cpu_count": os.cpu_count(), "cpu_model": model,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(cfg, sd, tsd, budget_s: float = 25.0, min_eps: int = 5, max_eps: int = 8):
+    """The oracle (CPU restatement of the reference path) on the host cores: >= 5 episodes
+    after one warm-up, torch.set_num_threads(nproc), bounded by budget_s."""
     from few_shot_seg_cwt_amd import synthetic as syn
     from oracle import cwt_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    info = host_cpu_info()
+    threads = info["nproc"]
     torch.set_num_threads(threads)
     sdt, tsdt = O.to_torch_state(sd), O.to_torch_state(tsd)
     eps = [syn.make_episode(2021, 100 + i, cfg["image_size"], cfg["shot"]) for i in range(max_eps + 1)]
@@ -48,20 +73,22 @@ def cpu_baseline(cfg, sd, tsd, budget_s: float = 25.0, max_eps: int = 4):
     for ep in eps[1:]:
         O.run_inference_episode(ep, sdt, tsdt, W0, cfg)
         n += 1
-        if time.time() - t0 > budget_s:
+        if n >= min_eps and time.time() - t0 > budget_s:
             break
     dt = time.time() - t0
-    return {"value": n / dt, "unit": "episodes/s", "cores": threads, "kind": "port",
+    return {"value": n / dt, "unit": "episodes/s", "cores": threads, "kind": "port", **info,
             "sample": f"{n} episodes (after 1 warm-up) of the same workload through oracle/cwt_oracle.py "
-                      f"run_inference_episode (torch CPU fp32, {threads} threads); s/episode {dt / n:.2f}"}
+                      f"run_inference_episode (torch CPU fp32, torch.set_num_threads(nproc = {threads})); "
+                      f"s/episode {dt / n:.2f}"}
 
 
-def cpu_baseline_train(cfg, sd, tsd, budget_s: float = 25.0, max_eps: int = 3):
+def cpu_baseline_train(cfg, sd, tsd, budget_s: float = 25.0, min_eps: int = 5, max_eps: int = 6):
     """The oracle's training episode (inference pieces + CWT loss/gradients + SGD) on the
-    host cores, bounded sample."""
+    host cores: >= 5 episodes after one warm-up, torch.set_num_threads(nproc)."""
     from few_shot_seg_cwt_amd import synthetic as syn
     from oracle import cwt_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    info = host_cpu_info()
+    threads = info["nproc"]
     torch.set_num_threads(threads)
     sdt, tsdt = O.to_torch_state(sd), O.to_torch_state(tsd)
     classes = syn.coco_val_classes(0) if cfg["layers"] == 101 else None
@@ -79,10 +106,10 @@ def cpu_baseline_train(cfg, sd, tsd, budget_s: float = 25.0, max_eps: int = 3):
     for ep in eps[1:]:
         one(ep)
         n += 1
-        if time.time() - t0 > budget_s:
+        if n >= min_eps and time.time() - t0 > budget_s:
             break
     dt = time.time() - t0
-    return {"value": n / dt, "unit": "training episodes/s", "cores": threads, "kind": "port",
+    return {"value": n / dt, "unit": "training episodes/s", "cores": threads, "kind": "port", **info,
             "sample": f"{n} training episodes (after 1 warm-up) through oracle/cwt_oracle.py (inference episode + "
                       f"cwt_train_step_grads + sgd_nesterov, torch CPU fp32, {threads} threads); s/episode {dt / n:.2f}"}
 
@@ -210,7 +237,8 @@ def cpu_baseline_pretrain(layers, S, nc, budget_s: float = 25.0):
     """The oracle's pretraining iteration (torch CPU fp32 autograd) on a bounded batch."""
     from few_shot_seg_cwt_amd import synthetic as syn
     from oracle.pretrain_oracle import pretrain_step
-    threads = min(16, os.cpu_count() or 1)
+    info = host_cpu_info()
+    threads = info["nproc"]
     torch.set_num_threads(threads)
     sd = {k: torch.from_numpy(np.array(v)) for k, v in syn.make_pspnet_state(layers, 2021, num_classes_tr=nc).items()}
     B = 2
@@ -222,7 +250,7 @@ def cpu_baseline_pretrain(layers, S, nc, budget_s: float = 25.0):
         pretrain_step(sd, x, t, nc, layers)
         n += 1
     dt = time.time() - t0
-    return {"value": n * B / dt, "unit": "images/s", "cores": threads, "kind": "port",
+    return {"value": n * B / dt, "unit": "images/s", "cores": threads, "kind": "port", **info,
             "sample": f"{n} iterations of batch {B} ({S}x{S}, R{layers}, {nc} classes) through "
                       f"oracle/pretrain_oracle.py pretrain_step (torch CPU fp32 autograd, {threads} threads); "
                       f"s/iteration {dt / n:.2f}"}
@@ -323,6 +351,8 @@ def main():
     ap.add_argument("--batch", type=int, default=10, help="--pretrain: images per iteration (pascal_pretrain.yaml: 10)")
     ap.add_argument("--num-classes", type=int, default=16, help="--pretrain: num_classes_tr (16 PASCAL, 61 COCO)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exact-steps", type=int, default=10,
+                    help="episodes of the exact-fp32 conv leg (cwt_ctx_set_conv_arith F32, sequential); 0 = skip")
     ap.add_argument("--profile-json", default=None, help="write per-launch records here (rank 0)")
     args = ap.parse_args()
 
@@ -507,6 +537,115 @@ def main():
     torch.cuda.synchronize()
     fine = _lib.profile_records()
     _lib.profile_enable(0)
+    _lib.check_status()   # every launch so far has completed: surface an inner-loop barrier timeout
+
+    # ---- the inner loop's latency floor: the same persistent kernel at the
+    # same G with every unit's arithmetic and atomics skipped (CWT_ADAPT_DBG & 64) -- the per-step
+    # exchange alone (slot zeroing, arrival, poll, replica reads, W update) x adapt_iter ----
+    latency_floor = None
+    if not args.train and E == 1 and ad_kernel.startswith("adapt_persist_kernel"):
+        imgs0, sl0, ql0 = pool[0]
+        with torch.no_grad():
+            f_s0 = model.extract_features(imgs0)[0][:shot]
+        from few_shot_seg_cwt_amd.episode import inner_adapt
+
+        def time_loop(ctx_sel, dbg, reps=5):
+            old = os.environ.get("CWT_ADAPT_DBG")
+            if dbg:
+                os.environ["CWT_ADAPT_DBG"] = str(dbg)
+            try:
+                st = torch.cuda.current_stream()
+                evs = []
+                for r in range(reps + 1):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    if ctx_sel is None:
+                        inner_adapt(f_s0, sl0[0], W0[0, 0].clone(), cfg["cls_lr"], cfg["adapt_iter"])
+                    else:
+                        with _lib.using_ctx(ctx_sel):
+                            inner_adapt(f_s0, sl0[0], W0[0, 0].clone(), cfg["cls_lr"], cfg["adapt_iter"])
+                    e1.record(st)
+                    evs.append((e0, e1))
+                torch.cuda.synchronize()
+            finally:
+                if dbg:
+                    if old is None:
+                        os.environ.pop("CWT_ADAPT_DBG", None)
+                    else:
+                        os.environ["CWT_ADAPT_DBG"] = old
+            return float(np.median([a.elapsed_time(b) for a, b in evs[1:]]))
+
+        geos = [("sequential_leg (default context)", None)]
+        if pipe is not None:
+            geos.insert(0, ("timed region's geometry (the pipeline's adapt context)", pipe.c_adapt))
+        latency_floor = {"basis": "the same persistent kernel at the same G, alone on the GPU, with every unit's "
+                                  "arithmetic and atomics skipped (CWT_ADAPT_DBG & 64): the per-step exchange "
+                                  "(slot zeroing, arrival, poll, replica reads, W update) x adapt_iter -- the "
+                                  "loop's dependency-chain floor in this design; bracket includes the label prep "
+                                  "and setup kernels as the timed one does"}
+        bytes_floor_ms = ad_bytes_launch / (PEAK_HBM_GBPS * 1e9) * 1e3
+        for label, c in geos:
+            full = time_loop(c, 0)
+            floor = time_loop(c, 64)
+            latency_floor[label.split(" ")[0]] = {"what": label, "floor_ms": round(floor, 4),
+                                                  "alone_ms": round(full, 4),
+                                                  "frac_alone_vs_floor": round(max(floor, bytes_floor_ms) / full, 4)}
+        lf = latency_floor[geos[0][0].split(" ")[0]]
+        latency_floor["bytes_floor_ms"] = round(bytes_floor_ms, 4)
+        latency_floor["frac"] = round(max(lf["floor_ms"], bytes_floor_ms) / ad_ms_launch, 4)
+        latency_floor["frac_note"] = ("max(bytes floor, latency floor) / the timed region's average launch: how "
+                                      "close the measured loop is to ITS floor (the byte frac above prices it as "
+                                      "a bandwidth kernel, which it is not)")
+        _lib.check_status()
+
+    # ---- exact-fp32 leg: the same episodes with the conv stack on the exact
+    # fp32 MFMA (CWT_CONV=f32 semantics, cwt_ctx_set_conv_arith), sequential, its conv roofline
+    # priced against the 157.3 TF fp32 matrix peak ----
+    exact_fp32 = None
+    if not args.train and E == 1 and conv_x3 and args.exact_steps > 0:
+        c0 = _lib.ctx(dev.index)
+        _lib.check(_lib.lib().cwt_ctx_set_conv_arith(c0, 1), "cwt_ctx_set_conv_arith")
+        try:
+            for s_ in range(2):
+                im, sl_, ql_ = pool[s_ % len(pool)]
+                engine.run(im, sl_[0], ql_, W0[s_, 0].clone())
+            torch.cuda.synchronize()
+            _lib.profile_enable(1)
+            cdist.barrier()
+            torch.cuda.synchronize()
+            tf0 = time.perf_counter()
+            for s_ in range(args.exact_steps):
+                im, sl_, ql_ = pool[s_ % len(pool)]
+                engine.run(im, sl_[0], ql_, W0[args.warmup + s_ % args.steps, 0].clone())
+            torch.cuda.synchronize()
+            cdist.barrier()
+            dtf = cdist.all_reduce_max_scalar(time.perf_counter() - tf0)
+            frecs = _lib.profile_records()
+            _lib.profile_enable(2)
+            engine.run(pool[0][0], pool[0][1][0], pool[0][2], W0[0, 0].clone())
+            torch.cuda.synchronize()
+            ffine = _lib.profile_records()
+            _lib.profile_enable(0)
+        finally:
+            _lib.check(_lib.lib().cwt_ctx_set_conv_arith(c0, 0), "cwt_ctx_set_conv_arith")
+        fex = [r for r in frecs if r[0].startswith("extract_features")]
+        fdom = [r for r in frecs if r[0].startswith("conv_igemm")]
+        fex_fl, fex_ms = sum(r[1] for r in fex), sum(r[3] for r in fex)
+        exact_fp32 = {
+            "value": round(world * args.exact_steps / dtf, 3), "unit": "episodes/s",
+            "ms_per_step": round(dtf / args.exact_steps * 1e3, 3), "steps": args.exact_steps,
+            "mode": "sequential (one episode after the other), conv stack on v_mfma_f32 (exact fp32, the "
+                    "reference's numerics without the bf16x3 split)",
+            "conv_stack": {"tflops": round(fex_fl / (fex_ms * 1e-3) / 1e12, 2),
+                           "ms_per_step": round(fex_ms / args.exact_steps, 3),
+                           **conv_roofline(ffine, PEAK_FP32_MFMA_TFLOPS)},
+            "conv_roofline": None if not fdom else {
+                "kernel": fdom[0][0].split(" ")[0] + " (bottleneck conv)",
+                "achieved": round(sum(r[1] for r in fdom) / (sum(r[3] for r in fdom) * 1e-3) / 1e12, 2),
+                "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(sum(r[1] for r in fdom) / (sum(r[3] for r in fdom) * 1e-3) / 1e12
+                              / PEAK_FP32_MFMA_TFLOPS, 4)}}
+        _lib.check_status()
 
     out = {
         "metric": (f"training episodes/sec ({S}x{S}, {shot}-shot, R{layers})" if args.train else
@@ -547,7 +686,7 @@ def main():
                                     "per-step grid-wide reduction, not by bytes",
                      "measured_in": "the timed region" + (" (pipelined: the loop shares the GPU with the next "
                                                           "episodes' extractor passes)" if args.pipeline else ""),
-                     "sequential_leg": seq_ad},
+                     "sequential_leg": seq_ad, "latency_floor": latency_floor},
         "conv_roofline": {"bound": "mfma", "kernel": dom_name + " (bottleneck conv 4096->512 3x3, pspnet.py:125)",
                           "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                           "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
@@ -577,6 +716,7 @@ def main():
                           "note": "executed in the declared re-associated form (DESIGN.md §3, ~59 MFLOP of token work)"}},
         "iou_fg_timed": None if args.train else round(float((iu[0, 1] / iu[1, 1].clamp_min(1)).item()), 4),
         "sequential": seq,
+        "exact_fp32": exact_fp32,
     }
     if rank == 0 and args.profile_json:
         with open(args.profile_json, "w") as f:

@@ -83,6 +83,9 @@ SIGNATURES = {
     "cwt_debug_pretrain_op": (_I, [_P, _I, C.POINTER(_P), C.POINTER(_I64), C.POINTER(_F), _P]),
     "cwt_debug_adapt_stamps": (_I, [_P, _P, _I64, C.POINTER(_I64)]),
     "cwt_ctx_set_adapt_units": (_I, [_P, _I]),
+    "cwt_ctx_status": (_I, [_P, C.POINTER(C.c_uint32), _I]),
+    "cwt_ctx_set_conv_arith": (_I, [_P, _I]),
+    "cwt_debug_adapt_spin_limit": (_I, [_P, _I64]),
     "cwt_profile_enable": (_I, [_P, _I]),
     "cwt_profile_count": (_I, [_P]),
     "cwt_profile_record": (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -179,6 +182,21 @@ def new_ctx(device: int | None = None):
         return p
 
 
+def destroy_ctx(p, device: int | None = None) -> None:
+    """Destroy an additional context made by :func:`new_ctx` (its workspaces are freed; the
+    caller has synchronised every stream that used it)."""
+    if device is None:
+        device = torch.cuda.current_device()
+    with _lock:
+        lst = _extra_ctx.get(device, [])
+        for i, q in enumerate(lst):
+            if q is p or getattr(q, "value", None) == getattr(p, "value", p):
+                del lst[i]
+                check(load_library().cwt_ctx_destroy(p), "cwt_ctx_destroy")
+                return
+    raise CwtError("destroy_ctx: not an additional context of this device")
+
+
 class using_ctx:
     """``with using_ctx(c): ...`` routes this thread's libcwt calls on c's device to context c."""
 
@@ -199,6 +217,24 @@ def all_ctx(device: int | None = None):
     if device is None:
         device = torch.cuda.current_device()
     return [ctx(device)] + list(_extra_ctx.get(device, []))
+
+
+STATUS_ADAPT_BARRIER = 1   # CWT_STATUS_ADAPT_BARRIER (include/cwt.h)
+
+
+def check_status(device: int | None = None, clear: bool = True) -> None:
+    """Raise CwtError if a kernel enqueued on any of the device's contexts reported an
+    asynchronous failure (cwt_ctx_status).  Call after a synchronising readback; no GPU call."""
+    w = C.c_uint32()
+    bad = 0
+    for c in all_ctx(device):
+        check(lib().cwt_ctx_status(c, C.byref(w), int(clear)), "cwt_ctx_status")
+        bad |= w.value
+    if bad & STATUS_ADAPT_BARRIER:
+        raise CwtError("the persistent inner loop's grid barrier timed out (its workgroups were not all "
+                       "co-resident): the adapted classifier W of an episode on this device is wrong")
+    if bad:
+        raise CwtError(f"asynchronous libcwt failure, status 0x{bad:x}")
 
 
 def stream_ptr(device=None) -> C.c_void_p:

@@ -651,6 +651,11 @@ struct PersistArgs {
   int ncb, ntile, units, G;
   int nrep;    // replica rows in use
   int uc;      // lo-res columns owned per unit (15 or 31)
+  long spin_limit;   // polls per barrier before the grid gives up (PA_SPIN_LIMIT by default)
+  unsigned* status;  // the context's mapped host status word (cwt_ctx_status), or null
+  int floor_only;    // timing study (CWT_ADAPT_DBG & 64): skip every unit's arithmetic and atomics --
+                     // what is left is the per-step exchange (slot zeroing, arrival, poll, replica
+                     // reads, W update): the loop's latency floor at this G (bench.py latency_floor)
 };
 
 struct PaUnit {
@@ -1141,7 +1146,10 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
         }
       }
     };
-    if constexpr (NRES == 2) {
+    if (a.floor_only) {
+      // timing study: no unit work (NRES 3 still drains its in-flight DMA)
+      if (NRES == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (NRES == 2) {
       const bool has_b = u1 - u0 == 2;
       pair_body(q, has_b ? pa_unit(a, u0 + 1) : q, has_b);
     } else
@@ -1210,9 +1218,13 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
         c += __builtin_amdgcn_update_dpp(0u, c, 0x114, 0xF, 0xF, true);  // row_shr:4
         c += __builtin_amdgcn_update_dpp(0u, c, 0x118, 0xF, 0xF, true);  // row_shr:8
         if ((unsigned)__builtin_amdgcn_readlane((int)c, 15) >= target) break;
-        if (++spins > PA_SPIN_LIMIT || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        if (++spins > a.spin_limit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
           if (lane == 0) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // surface it: the host reads this word after its next synchronising readback
+            // (a plain system-scope store, not an atomic: PCIe atomics to host memory are not assumed)
+            if (a.status) __hip_atomic_store(a.status, 1u /*CWT_STATUS_ADAPT_BARRIER*/, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
             abort_flag = 1;
           }
           break;
@@ -1325,8 +1337,15 @@ static int persist_geometry(int E, int n, int h, int w, int upw_pref, int* G_out
 
 static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const AdaptScalars* sc, float* acc3,
                                  unsigned* cnt, const AdaptDevArgs* dargs, int E, int n, int h, int w, int S,
-                                 int iters, int G, int units, int ncb, int nres, int uc, hipStream_t st) {
+                                 int iters, int G, int units, int ncb, int nres, int uc, unsigned* status,
+                                 long spin_limit, hipStream_t st) {
   PersistArgs a;
+  a.status = status;
+  a.spin_limit = spin_limit > 0 ? spin_limit : PA_SPIN_LIMIT;
+  {
+    const char* fd = getenv("CWT_ADAPT_DBG");
+    a.floor_only = (fd && (atoi(fd) & 64)) ? 1 : 0;
+  }
   a.f = f;
   a.lbl = lbl_ws;
   a.sc = sc;
@@ -1411,7 +1430,7 @@ const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw) {
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
                  float* W, float* f_ws /*[E][n][h][w][512]*/, uint8_t* lbl_ws, AdaptScalars* sc /*[E] + partial counts*/,
                  float* acc3 /*[E][3][R][512]*/, float* wbuf /*[E][2][2][512]*/, AdaptDevArgs* dargs /*[E]*/,
-                 AdaptGraphCache* cache, int upw, hipStream_t st) {
+                 AdaptGraphCache* cache, int upw, unsigned* status, long spin_limit, hipStream_t st) {
   const long total = (long)n * S * S;  // labels per episode
   unsigned long long* part = (unsigned long long*)(sc + E);  // [E][PREP_MAXBLK][2] after the scalars
   const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
@@ -1431,7 +1450,7 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
   if (iters <= 0) return 0;
   if (persist)  // one launch for all steps, f read in place (no copy, no graph)
     return enqueue_adapt_persist(f, lbl_ws, sc, acc3, cnt, dargs, E, n, h, w, S, iters, pG, punits, pncb, pnres, puc,
-                                 st);
+                                 status, spin_limit, st);
   // the step graph reads f from the library's buffer (fixed address, baked into the graph)
   if (f != f_ws)
     CWT_HIP(hipMemcpyAsync(f_ws, f, (size_t)E * n * h * w * 512 * sizeof(float), hipMemcpyDeviceToDevice, st));

@@ -30,7 +30,8 @@ struct AdaptScalars;
 struct AdaptDevArgs;
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
                  float* W, float* f_ws, uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf,
-                 AdaptDevArgs* dargs, AdaptGraphCache* cache, int upw, hipStream_t st);
+                 AdaptDevArgs* dargs, AdaptGraphCache* cache, int upw, unsigned* status, long spin_limit,
+                 hipStream_t st);
 const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw);
 extern unsigned long long* g_adapt_stamps;
 extern long g_adapt_stamps_n;
@@ -133,6 +134,11 @@ struct cwt_ctx {
   bool conv_split = true;
   // persistent inner loop: units per workgroup (0 automatic, 1, 2), cwt_ctx_set_adapt_units
   int adapt_upw = 0;
+  // asynchronous status word (cwt_ctx_status): mapped, coherent host memory the kernels OR
+  // CWT_STATUS_* bits into (system-scope stores; written only on failure)
+  unsigned* status_host = nullptr;
+  unsigned* status_dev = nullptr;
+  long adapt_spin_limit = 0;  // 0: the persistent loop's default bound (cwt_debug_adapt_spin_limit)
 };
 
 namespace cwt {
@@ -833,6 +839,13 @@ int cwt_ctx_create(int device, cwt_ctx** out) {
     return fail(CWT_EARG, "CWT_CONV must be x3s (default) or f32");
   }
   c->conv_split = mode == "x3s";
+  if (hipHostMalloc((void**)&c->status_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&c->status_dev, c->status_host, 0) != hipSuccess) {
+    if (c->status_host) (void)hipHostFree(c->status_host);
+    delete c;
+    return fail(CWT_ESTATE, "cwt_ctx_create: mapped status word");
+  }
+  *(volatile unsigned*)c->status_host = 0u;
   *out = c;
   return 0;
 }
@@ -843,7 +856,16 @@ int cwt_ctx_destroy(cwt_ctx* ctx) {
   (void)hipDeviceSynchronize();
   for (auto& kv : ctx->ws)
     if (kv.second.p) (void)hipFree(kv.second.p);
+  if (ctx->status_host) (void)hipHostFree(ctx->status_host);
   delete ctx;
+  return 0;
+}
+
+int cwt_ctx_status(cwt_ctx* ctx, uint32_t* status, int clear) {
+  if (!ctx || !status) return fail(CWT_EARG, "null argument");
+  volatile unsigned* w = ctx->status_host;
+  *status = *w;
+  if (clear) *w = 0u;
   return 0;
 }
 
@@ -968,7 +990,7 @@ int cwt_inner_adapt_batch(cwt_ctx* ctx, const float* f_s, const int64_t* s_label
          1);
   rc = launch_adapt(f_s, s_label, E, n, h, w, S, lr, iters, W_inout, (float*)fws, (uint8_t*)lbl, (AdaptScalars*)sc,
                     (float*)acc, (float*)wb, (AdaptDevArgs*)dargs, ctx->use_graph ? &ctx->adapt_graphs : nullptr,
-                    ctx->adapt_upw, (hipStream_t)stream);
+                    ctx->adapt_upw, ctx->status_dev, ctx->adapt_spin_limit, (hipStream_t)stream);
   p.end();
   return rc;
 }
@@ -1357,6 +1379,21 @@ int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int
   int rc;
   if ((rc = ensure_ws(ctx, "iou.cnt", 3 * 16 * 4, &cnt))) return rc;
   return launch_iou_preds(preds, target, n, num_classes, ignore_index, iut_out, (unsigned*)cnt, (hipStream_t)stream);
+}
+
+int cwt_ctx_set_conv_arith(cwt_ctx* ctx, int arith) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(arith == CWT_CONV_ARITH_BF16X3 || arith == CWT_CONV_ARITH_F32,
+            "arith must be CWT_CONV_ARITH_BF16X3 (0) or CWT_CONV_ARITH_F32 (1)");
+  ctx->conv_split = arith == CWT_CONV_ARITH_BF16X3;
+  return 0;
+}
+
+int cwt_debug_adapt_spin_limit(cwt_ctx* ctx, int64_t limit) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(limit >= 0, "limit must be >= 0");
+  ctx->adapt_spin_limit = (long)limit;
+  return 0;
 }
 
 int cwt_ctx_set_adapt_units(cwt_ctx* ctx, int units_per_workgroup) {

@@ -180,9 +180,25 @@ class EpisodePipeline:
     loop's / CWT's by the adapt stream.  ``submit`` returns the episode's result tensors, valid
     on the adapt stream (``wait`` makes the current stream wait for them)."""
 
+    _shared = {}   # (device, extract_streams) -> the process's pipeline (streams + contexts reused)
+
+    @classmethod
+    def shared(cls, engine: "EpisodeEngine", extract_streams: int = 1) -> "EpisodePipeline":
+        """The pipeline of this device and stream count, created once per process and reused by
+        every later caller (validate_transformer runs every epoch: a pipeline per call would
+        leave its libcwt contexts and their workspaces behind each time)."""
+        key = (torch.cuda.current_device(), max(1, int(extract_streams)))
+        p = cls._shared.get(key)
+        if p is None or p.closed:
+            p = cls._shared[key] = cls(engine, extract_streams)
+        p.eng = engine
+        return p
+
     def __init__(self, engine: "EpisodeEngine", extract_streams: int = 1):
         """extract_streams > 1: consecutive episodes' extractor passes also overlap each other,
         round-robin over that many streams, each with its own libcwt context (workspaces)."""
+        self.closed = False
+        self.device = torch.cuda.current_device()
         self.eng = engine
         self.s_ext = [torch.cuda.Stream() for _ in range(max(1, int(extract_streams)))]
         self.c_ext = [None] + [_lib.new_ctx() for _ in range(len(self.s_ext) - 1)]
@@ -265,6 +281,19 @@ class EpisodePipeline:
         for s in self.s_ext:
             cur.wait_stream(s)
         cur.wait_stream(self.s_adapt)
+
+    def close(self):
+        """Synchronise the pipeline's streams and destroy its libcwt contexts."""
+        if self.closed:
+            return
+        for s in self.s_ext + [self.s_adapt]:
+            s.synchronize()
+        for c in [c for c in self.c_ext if c is not None] + [self.c_adapt]:
+            _lib.destroy_ctx(c, self.device)
+        self.closed = True
+        for k, v in list(EpisodePipeline._shared.items()):
+            if v is self:
+                del EpisodePipeline._shared[k]
 
 
 class TrainEngine:
@@ -392,7 +421,7 @@ def validate_transformer(args, val_loader, model, transformer, episodes_out: lis
     # next episode is submitted before this one's results are read back (same results, same
     # accumulation order)
     n_pipe = int(_a(args, "pipeline", 2))
-    pipe = EpisodePipeline(engine, extract_streams=n_pipe) if n_pipe > 0 else None
+    pipe = EpisodePipeline.shared(engine, extract_streams=n_pipe) if n_pipe > 0 else None
     for run in range(n_runs):
         loss_meter = AverageMeter()
         t_run = time.time()
@@ -406,6 +435,7 @@ def validate_transformer(args, val_loader, model, transformer, episodes_out: lis
             iut = r["iut"].cpu().numpy()[0]
             iut0 = r["iut0"].cpu().numpy()[0]
             ce = r["ce"].cpu().numpy()[0]
+            _lib.check_status()     # the readback synchronised: surface an inner-loop barrier timeout
             loss_meter.update(float(ce[0] / max(ce[1], 1.0)))
             for c in [int(x.item()) for x in subcls]:
                 cls_iu[c] += (iut[0, 1], iut[1, 1])       # FG only (test.py:227-228)
@@ -540,6 +570,8 @@ def do_epoch(args, train_loader, model, transformer, optimizer_trans, epoch: int
             cdist.all_reduce_mean_(transformer.flat.grad)
         optimizer_trans.step()
         loss = float(r["loss"].item())
+        if dev.type == "cuda":
+            _lib.check_status()     # after the .item() sync: surface an inner-loop barrier timeout
         iut = r["iut"].cpu().numpy()[0]
         iut0 = r["iut0"].cpu().numpy()[0]
         IoUb, IoUf = iut[0] / (iut[1] + 1e-10)

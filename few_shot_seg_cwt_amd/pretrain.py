@@ -60,16 +60,7 @@ class PretrainPSPNet:
         if device is None:
             device = torch.cuda.current_device() if torch.cuda.is_available() else 0
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
-        self._names, self._shapes = [], {}
-        names, arrs = [], []
-        for k, v in state_dict.items():
-            if k.endswith("num_batches_tracked") or k == "gamma":
-                continue
-            a = np.ascontiguousarray(v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v),
-                                     dtype=np.float32)
-            names.append(k)
-            arrs.append(a)
-            self._shapes[k] = a.shape
+        names, arrs = self._index_state(state_dict)
         self._keep = arrs
         cn = (C.c_char_p * len(names))(*[n.encode() for n in names])
         cd = (C.c_void_p * len(names))(*[a.ctypes.data for a in arrs])
@@ -83,6 +74,34 @@ class PretrainPSPNet:
         self.loss = torch.zeros(1, device=self.device)
         self.iteration = 0
         self.training = True
+
+    def _index_state(self, state_dict):
+        """Host bookkeeping over a reference PSPNet state dict; returns the device tensors'
+        (names, float32 arrays)."""
+        self._shapes = {}
+        # the full reference key sequence (pspnet.py:70-141 state_dict order): ``gamma`` is a
+        # PSPNet parameter outside every optimizer group (pretrain.py:68-76), carried unchanged;
+        # ``*.num_batches_tracked`` counts the training-mode forwards as nn.BatchNorm2d does
+        self._order = []
+        self._gamma = torch.tensor(0.2)
+        self._nbt0 = {}
+        self._train_forwards = 0
+        names, arrs = [], []
+        for k, v in state_dict.items():
+            self._order.append(k)
+            if k == "gamma":
+                self._gamma = torch.as_tensor(np.asarray(v.detach().cpu() if isinstance(v, torch.Tensor) else v,
+                                                         dtype=np.float32)).clone()
+                continue
+            if k.endswith("num_batches_tracked"):
+                self._nbt0[k] = int(np.asarray(v.detach().cpu() if isinstance(v, torch.Tensor) else v))
+                continue
+            a = np.ascontiguousarray(v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v),
+                                     dtype=np.float32)
+            names.append(k)
+            arrs.append(a)
+            self._shapes[k] = a.shape
+        return names, arrs
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -100,12 +119,17 @@ class PretrainPSPNet:
     def eval(self):
         return self.train(False)
 
-    def hparams(self, lr: float | None = None, seed: int = 0) -> PretrainHparams:
+    def hparams(self, lr: float | None = None, seed: int = 0, lr_head: float | None = None) -> PretrainHparams:
+        """``lr`` is the backbone groups' current lr (layer0-4), ``lr_head`` the head groups'
+        (ppm, bottleneck, classifier; default ``lr * scale_lr``, their base ratio).  Under the
+        cosine schedule each group anneals from its OWN base lr to eta_min (optimizer.py:32), so
+        :func:`train_epoch` passes both."""
         a = self.args
         lr = float(_arg(a, "lr", 0.0025)) if lr is None else float(lr)
         hp = PretrainHparams()
         hp.lr = lr
-        hp.lr_head = lr * float(_arg(a, "scale_lr", 1.0))
+        hp.lr_head = lr * float(_arg(a, "scale_lr", 1.0)) if lr_head is None else float(lr_head)
+        self._group_lr = (hp.lr, hp.lr_head)
         hp.momentum = float(_arg(a, "momentum", 0.9))
         hp.weight_decay = float(_arg(a, "weight_decay", 1e-4))
         hp.nesterov = int(bool(_arg(a, "nesterov", False)))
@@ -117,7 +141,7 @@ class PretrainPSPNet:
         return hp
 
     def train_step(self, images: torch.Tensor, targets: torch.Tensor, lr: float | None = None, seed: int | None = None,
-                   hp: PretrainHparams | None = None) -> torch.Tensor:
+                   hp: PretrainHparams | None = None, lr_head: float | None = None) -> torch.Tensor:
         """One iteration of pretrain.py:104-121: images [N, 3, S, S] fp32, targets [N, S, S]
         int64 (255 ignored), both on the device.  Returns the loss (device scalar, the value
         before the step)."""
@@ -127,12 +151,15 @@ class PretrainPSPNet:
             raise ValueError("images must be [N,3,S,S] and targets [N,S,S]")
         images, targets = images.contiguous(), targets.contiguous()
         if hp is None:
-            hp = self.hparams(lr, self.iteration if seed is None else seed)
+            hp = self.hparams(lr, self.iteration if seed is None else seed, lr_head)
+        else:
+            self._group_lr = (float(hp.lr), float(hp.lr_head))
         _lib.check(_lib.lib().cwt_pretrain_step(_lib.ctx(self.device.index), self._h, _lib.ptr(images),
                                                 _lib.ptr(targets), images.shape[0], images.shape[2],
                                                 C.addressof(hp), _lib.ptr(self.loss), _lib.stream_ptr(self.device)),
                    "cwt_pretrain_step")
         self.iteration += 1
+        self._train_forwards += 1
         return self.loss[0]
 
     def logits(self, images: torch.Tensor) -> torch.Tensor:
@@ -174,13 +201,20 @@ class PretrainPSPNet:
         return [n for n in self._shapes if not (n.endswith("running_mean") or n.endswith("running_var"))]
 
     def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
-        """Host copy in the reference's names (parameters and BN running statistics)."""
+        """Host copy of the reference ``PSPNet.state_dict()``: every key in the reference order
+        (``gamma`` first, pspnet.py:141), parameters, BN running statistics and
+        ``num_batches_tracked`` (int64, +1 per training step), so the position-wise loader of
+        test.py:61-81 pairs every key with its own tensor."""
         sd = OrderedDict()
-        for n, shp in self._shapes.items():
-            if n.endswith("running_mean") or n.endswith("running_var"):
-                sd[n] = self._get(n, 3, shp)
+        for n in self._order:
+            if n == "gamma":
+                sd[n] = self._gamma.clone()
+            elif n.endswith("num_batches_tracked"):
+                sd[n] = torch.tensor(self._nbt0[n] + self._train_forwards, dtype=torch.int64)
+            elif n.endswith("running_mean") or n.endswith("running_var"):
+                sd[n] = self._get(n, 3, self._shapes[n])
             else:
-                sd[n] = self._get(n, 0, shp)
+                sd[n] = self._get(n, 0, self._shapes[n])
         return sd
 
     def param(self, name: str) -> torch.Tensor:
@@ -209,37 +243,58 @@ class PretrainPSPNet:
                    f"cwt_pretrain_set({name})")
 
     def load_state_dict(self, sd) -> None:
-        """model.load_state_dict (strict over the trainable tensors and BN running statistics)."""
+        """model.load_state_dict (strict over the trainable tensors and BN running statistics;
+        ``gamma`` and ``num_batches_tracked`` are taken when present)."""
         for n in self._shapes:
             if n not in sd:
                 raise KeyError(f"missing key {n}")
             what = 3 if (n.endswith("running_mean") or n.endswith("running_var")) else 0
             self._set(n, what, sd[n])
+        if "gamma" in sd:
+            self._gamma = torch.as_tensor(np.asarray(sd["gamma"], dtype=np.float32)).clone()
+        for n in self._nbt0:
+            if n in sd:
+                self._nbt0[n] = int(np.asarray(sd[n])) - self._train_forwards
+
+    MODULES = ("layer0", "layer1", "layer2", "layer3", "layer4", "ppm", "bottleneck", "classifier")
+    HEAD_MODULES = ("ppm", "bottleneck", "classifier")
 
     def param_groups(self):
-        """The two groups of pretrain.py:60-72 as parameter-name lists in module order (layer0-4;
-        ppm, bottleneck, classifier)."""
+        """The eight groups of pretrain.py:68-76, one per module in the reference order
+        (layer0-4 at ``lr``; ppm, bottleneck, classifier at ``lr * scale_lr``), each the
+        module's ``parameters()`` names in registration order (``gamma`` is in none)."""
         names = self.parameter_names()
-        head = ("ppm.", "bottleneck.", "classifier.")
-        return [[n for n in names if not n.startswith(head)], [n for n in names if n.startswith(head)]]
+        return [[n for n in names if n.split(".", 1)[0] == m] for m in self.MODULES]
 
-    def optimizer_state_dict(self, lr: float | None = None) -> dict:
-        """torch.optim.SGD.state_dict() of the reference's optimizer (pretrain.py:60-72): state
-        keyed by the parameter's position over both groups, momentum buffers in PyTorch layout."""
+    def optimizer_state_dict(self, lr: float | None = None, lr_head: float | None = None) -> dict:
+        """torch.optim.SGD.state_dict() of the reference's optimizer (pretrain.py:68-76): eight
+        param_groups, state keyed by the parameter's position over all groups, momentum buffers
+        in PyTorch layout.  Each group carries its current lr (the last step's, or ``lr`` /
+        ``lr_head`` when given) and the scheduler's ``initial_lr`` (its base lr)."""
         a = self.args
-        base = float(_arg(a, "lr", 0.0025)) if lr is None else float(lr)
+        base = float(_arg(a, "lr", 0.0025))
+        scale = float(_arg(a, "scale_lr", 1.0))
+        cur_b, cur_h = getattr(self, "_group_lr", (base, base * scale))
+        if lr is not None:
+            cur_b = float(lr)
+            cur_h = cur_b * scale if lr_head is None else float(lr_head)
+        elif lr_head is not None:
+            cur_h = float(lr_head)
         groups, state, idx = [], {}, 0
-        for gi, names in enumerate(self.param_groups()):
+        for m, names in zip(self.MODULES, self.param_groups()):
+            head = m in self.HEAD_MODULES
             ids = []
             for n in names:
                 if self.iteration > 0:
                     state[idx] = {"momentum_buffer": self.momentum_buffer(n)}
                 ids.append(idx)
                 idx += 1
-            groups.append({"lr": base * (float(_arg(a, "scale_lr", 1.0)) if gi == 1 else 1.0),
+            groups.append({"lr": cur_h if head else cur_b,
                            "momentum": float(_arg(a, "momentum", 0.9)), "dampening": 0,
                            "weight_decay": float(_arg(a, "weight_decay", 1e-4)),
-                           "nesterov": bool(_arg(a, "nesterov", False)), "params": ids})
+                           "nesterov": bool(_arg(a, "nesterov", False)), "maximize": False, "foreach": None,
+                           "differentiable": False, "fused": None,
+                           "initial_lr": base * scale if head else base, "params": ids})
         return {"state": state, "param_groups": groups}
 
     def load_optimizer_state_dict(self, sd: dict) -> None:
@@ -250,10 +305,10 @@ class PretrainPSPNet:
                 self._set(n, 2, st["momentum_buffer"])
                 self.iteration = max(self.iteration, 1)
 
-    def save_checkpoint(self, path: str, epoch: int, lr: float | None = None) -> None:
+    def save_checkpoint(self, path: str, epoch: int, lr: float | None = None, lr_head: float | None = None) -> None:
         """torch.save({'epoch', 'state_dict', 'optimizer'}) as pretrain.py:147-152 / 157-159."""
-        torch.save({"epoch": epoch, "state_dict": self.state_dict(), "optimizer": self.optimizer_state_dict(lr)},
-                   path)
+        torch.save({"epoch": epoch, "state_dict": self.state_dict(),
+                    "optimizer": self.optimizer_state_dict(lr, lr_head)}, path)
 
     def load_checkpoint(self, path: str) -> dict:
         ck = torch.load(path, map_location="cpu", weights_only=True)
@@ -279,10 +334,13 @@ def train_epoch(model: PretrainPSPNet, batches, epoch: int, iters_per_epoch: int
     device tensors) with the per-iteration cosine schedule; returns the running loss (the
     reference's loss_meter average over the logged iterations is host-side bookkeeping)."""
     losses = []
+    scale = float(_arg(model.args, "scale_lr", 1.0))
     for i, (images, gt) in enumerate(batches):
         it = epoch * iters_per_epoch + i
-        lr = cosine_lr(base_lr, it, iters_per_epoch * epochs)
-        losses.append(model.train_step(images, gt, lr=lr))
+        total = iters_per_epoch * epochs
+        # CosineAnnealingLR anneals every group from its own base lr to eta_min (optimizer.py:32)
+        losses.append(model.train_step(images, gt, lr=cosine_lr(base_lr, it, total),
+                                       lr_head=cosine_lr(base_lr * scale, it, total)))
     return torch.stack(losses).mean() if losses else torch.zeros(())
 
 

@@ -35,6 +35,9 @@ extern "C" {
 #define CWT_ESTATE 1002    /* weights not loaded / wrong call order */
 #define CWT_ENOFG 1003     /* support mask has no foreground (reference: ZeroDivisionError, test.py:174) */
 
+/* Bits of the context's asynchronous status word (cwt_ctx_status). */
+#define CWT_STATUS_ADAPT_BARRIER 1u  /* the persistent inner loop's grid barrier timed out: W is wrong */
+
 typedef struct cwt_ctx cwt_ctx;
 typedef struct cwt_backbone cwt_backbone;  /* one loaded (frozen) PSPNet extractor */
 
@@ -391,6 +394,27 @@ int cwt_pretrain_num_params(const cwt_pretrain* pt, int64_t* total, int64_t* bac
  * (few_shot_seg_cwt_amd.episode.EpisodePipeline); results are the same either way.
  */
 int cwt_ctx_set_adapt_units(cwt_ctx* ctx, int units_per_workgroup);
+
+/*
+ * Asynchronous failures of work already enqueued on this context (no reference counterpart:
+ * the reference's torch ops fail synchronously).  A kernel that detects a failure it cannot
+ * return -- today the persistent inner loop whose grid barrier does not complete within its
+ * bound (co-residency lost), leaving W unadapted -- ORs a CWT_STATUS_* bit into a word in
+ * mapped host memory.  Read it after the caller has synchronised the stream (e.g. after the
+ * episode's IoU readback): *status receives the word; clear != 0 resets it.  No GPU call.
+ */
+int cwt_ctx_status(cwt_ctx* ctx, uint32_t* status, int clear);
+
+/*
+ * Arithmetic of this context's fp32 conv stack (no reference counterpart; the reference's
+ * torch convs are fp32): CWT_CONV_ARITH_BF16X3 (default, or CWT_CONV=x3s) = fp32 operands split
+ * into bf16 hi + lo, three bf16 MFMA products; CWT_CONV_ARITH_F32 (CWT_CONV=f32) = exact fp32
+ * MFMA over fp32 activations.  Both packings are built at cwt_backbone_load, so this switches
+ * between calls.  A bf16 backbone (cwt_backbone_set_precision) is unaffected.
+ */
+#define CWT_CONV_ARITH_BF16X3 0
+#define CWT_CONV_ARITH_F32 1
+int cwt_ctx_set_conv_arith(cwt_ctx* ctx, int arith);
 
 int cwt_profile_enable(cwt_ctx* ctx, int level);
 int cwt_profile_count(cwt_ctx* ctx);

@@ -60,6 +60,11 @@ int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int 
  * (may be NULL) and stores the number available in *count. */
 int cwt_debug_adapt_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t max_count, int64_t* count);
 
+/* Test hook: the persistent inner loop's per-barrier spin bound on this context (polls before
+ * the grid gives up and raises CWT_STATUS_ADAPT_BARRIER); 0 restores the default (~4 s).  A
+ * bound of 1 makes nearly every barrier time out, to exercise the error path. */
+int cwt_debug_adapt_spin_limit(cwt_ctx* ctx, int64_t limit);
+
 /* Test hook: per workgroup of a 64-thread grid, the raw HW_REG_HW_ID and HW_REG_XCC_ID of the
  * CU it ran on (out[2*b], out[2*b+1]); with a CU-masked stream this maps mask bits to CUs. */
 int cwt_debug_census(cwt_ctx* ctx, int nblocks, unsigned* out, void* stream);

@@ -98,3 +98,41 @@ def test_lds_streamed_units_equal_step_launches(dev, E, n, S, iters):
     errs = [rel(Wp[e], Ws[e]) for e in range(E)]
     print(f"stream E={E} n={n} S={S}: max rel {max(errs):.2e}")
     assert max(errs) < 1e-4, errs
+
+
+@pytest.mark.parametrize("upw", ["1", "2"])
+def test_barrier_timeout_is_raised(dev, upw):
+    """A persistent loop whose grid barrier gives up (cwt_debug_adapt_spin_limit = 1: nearly
+    every poll exhausts its bound) drains the grid, reports CWT_STATUS_ADAPT_BARRIER in the
+    context's status word, and the host raises CwtError at its next check (the readbacks of
+    validate_transformer / do_epoch call _lib.check_status); with the default bound restored
+    the same call is clean and matches the step launches."""
+    from few_shot_seg_cwt_amd import _lib
+    from few_shot_seg_cwt_amd.episode import inner_adapt_batch
+    S, n = 473, 1
+    h = (S - 1) // 8 + 1
+    f = torch.from_numpy(syn.normal(3, "fto", (n, 512, h, h), 0.1)).to(dev)
+    f = f.contiguous(memory_format=torch.channels_last)
+    lbl = torch.from_numpy(syn.make_episode(SEED, 9, S, n)["s_label"][0]).to(dev)[None]
+    W0 = torch.from_numpy(syn.normal(4, "wto", (1, 2, 512), 0.04)).to(dev)
+    _lib.check_status()   # clean before
+    c = _lib.ctx(dev.index)
+    _lib.check(_lib.lib().cwt_debug_adapt_spin_limit(c, 1), "spin limit")
+    old = os.environ.get("CWT_ADAPT_UPW")
+    os.environ["CWT_ADAPT_UPW"] = upw
+    try:
+        inner_adapt_batch(f, lbl, W0.clone(), 0.1, 200)
+        torch.cuda.synchronize()
+        with pytest.raises(_lib.CwtError, match="grid barrier timed out"):
+            _lib.check_status()
+        _lib.check_status()   # the check cleared the word
+    finally:
+        _lib.check(_lib.lib().cwt_debug_adapt_spin_limit(c, 0), "spin limit")
+        if old is None:
+            os.environ.pop("CWT_ADAPT_UPW", None)
+        else:
+            os.environ["CWT_ADAPT_UPW"] = old
+    W = _run("1", f, lbl, W0, 200, upw=upw)
+    _lib.check_status()
+    Wr = _run("0", f, lbl, W0, 200)
+    assert rel(W, Wr) < 1e-4

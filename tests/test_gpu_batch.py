@@ -98,3 +98,27 @@ def test_pipeline_equals_run(dev, streams):
         assert rel(outs[e]["W"], r["W"]) < TOL, e
         assert rel(outs[e]["pred_q"], r["pred_q"]) < TOL_RUN, e
         assert torch.equal(outs[e]["iut0"], r["iut0"]), e
+    pipe.close()
+
+
+def test_validate_transformer_reuses_its_pipeline(dev):
+    """validate_transformer runs every epoch: its EpisodePipeline (and the libcwt contexts it
+    holds) is created once per device and reused, so repeated calls do not pile up contexts."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib, get_model
+    from few_shot_seg_cwt_amd.episode import EpisodePipeline, SyntheticEpisodes, validate_transformer
+    S = 65
+    cfg = syn.cfg_defaults(image_size=S)
+    cfg.update(test_num=2, n_runs=1, pipeline=2, adapt_iter=5)
+    m = get_model(cfg).load_state_dict(syn.make_pspnet_state(50, SEED))
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    torch.manual_seed(0)
+    a = validate_transformer(cfg, SyntheticEpisodes(2, S), m, t)
+    n_ctx = len(_lib.all_ctx())
+    torch.manual_seed(0)
+    b = validate_transformer(cfg, SyntheticEpisodes(2, S), m, t)
+    assert len(_lib.all_ctx()) == n_ctx
+    assert abs(a[0] - b[0]) < 1e-2 and abs(a[1] - b[1]) < 1e-3 * max(1.0, abs(a[1]))
+    pipe = EpisodePipeline._shared[(torch.cuda.current_device(), 2)]
+    pipe.close()
+    assert len(_lib.all_ctx()) == n_ctx - 2   # its second extractor context and the adapt context

@@ -184,7 +184,7 @@ def test_pretrain_evaluate_vs_oracle(dev, nc, S):
 def test_pretrain_checkpoint_resume(dev, tmp_path):
     """pretrain.py:147-152 checkpoints: a model saved after one step, reloaded into a fresh one
     (parameters, BN running statistics, SGD momentum buffers), continues bit-identically to the
-    uninterrupted run; the optimizer state dict has torch.optim.SGD's layout (two groups)."""
+    uninterrupted run; the optimizer state dict has torch.optim.SGD's layout (eight groups)."""
     from few_shot_seg_cwt_amd.pretrain import PretrainPSPNet
     state = syn.make_pspnet_state(50, SEED, num_classes_tr=16)
     a = args()
@@ -198,8 +198,10 @@ def test_pretrain_checkpoint_resume(dev, tmp_path):
     ref = m.state_dict()
     r = PretrainPSPNet(a, state, dev)
     ck = r.load_checkpoint(path)
-    assert ck["epoch"] == 3 and len(ck["optimizer"]["param_groups"]) == 2
-    assert ck["optimizer"]["param_groups"][1]["lr"] == pytest.approx(a["lr"] * a["scale_lr"])
+    assert ck["epoch"] == 3 and len(ck["optimizer"]["param_groups"]) == 8
+    assert ck["optimizer"]["param_groups"][0]["lr"] == pytest.approx(a["lr"])
+    assert ck["optimizer"]["param_groups"][5]["lr"] == pytest.approx(a["lr"] * a["scale_lr"])
+    assert int(ck["state_dict"]["layer0.1.num_batches_tracked"]) == 1
     r.train_step(x1.to(dev), t1.to(dev), seed=2)
     got = r.state_dict()
     for k in ref:

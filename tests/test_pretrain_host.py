@@ -105,3 +105,92 @@ def test_smoothed_ce_matches_reference_formula():
                 n += 1
     # the one-hot is a float32 tensor as in the reference (torch.zeros default dtype): ~1e-8 relative
     assert abs(float(got) - tot / n) < 1e-6 * abs(tot / n)
+
+
+def _host_model(args, state):
+    """PretrainPSPNet's host bookkeeping without a device (the device getters read ``state``)."""
+    from few_shot_seg_cwt_amd.pretrain import PretrainPSPNet
+    m = PretrainPSPNet.__new__(PretrainPSPNet)
+    m.args = args
+    m.layers = args["layers"]
+    m.num_classes = args["num_classes_tr"]
+    m._index_state(state)
+    m.iteration = 0
+    m._get = lambda n, what, shp: torch.from_numpy(np.array(state[n], dtype=np.float32)).reshape(shp)
+    return m
+
+
+def _reference_groups(state, base_lr, scale_lr):
+    """pretrain.py:68-76 over placeholder tensors of the reference parameters: one group per
+    module (layer0-4 at lr, ppm / bottleneck / classifier at lr * scale_lr), each module's
+    parameters() in registration (= state_dict) order, buffers and gamma excluded."""
+    groups = []
+    for mod in ("layer0", "layer1", "layer2", "layer3", "layer4", "ppm", "bottleneck", "classifier"):
+        ps = [torch.nn.Parameter(torch.zeros(np.shape(v))) for k, v in state.items()
+              if k.split(".", 1)[0] == mod and not k.endswith(("running_mean", "running_var", "num_batches_tracked"))]
+        lr = base_lr * (scale_lr if mod in ("ppm", "bottleneck", "classifier") else 1.0)
+        groups.append(dict(params=ps, lr=lr))
+    return groups
+
+
+@pytest.mark.parametrize("layers", [50, 101])
+def test_optimizer_state_dict_has_reference_groups(layers):
+    """optimizer_state_dict() has the reference SGD's eight param_groups (pretrain.py:68-76):
+    same count, same parameter positions, and each group's lr under CosineAnnealingLR
+    (optimizer.py:32) annealed from its OWN base lr -- and torch's SGD loads it."""
+    from few_shot_seg_cwt_amd.pretrain import cosine_lr
+    a = dict(layers=layers, num_classes_tr=16, lr=0.0025, scale_lr=2.0, momentum=0.9, weight_decay=1e-4,
+             nesterov=True)
+    state = syn.make_pspnet_state(layers, 2021, num_classes_tr=16)
+    m = _host_model(a, state)
+    opt = torch.optim.SGD(_reference_groups(state, a["lr"], a["scale_lr"]), momentum=0.9, weight_decay=1e-4,
+                          nesterov=True)
+    T = 11
+    sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T, eta_min=1e-6)
+    for it in range(T):
+        ours = m.optimizer_state_dict(lr=cosine_lr(a["lr"], it, T), lr_head=cosine_lr(a["lr"] * a["scale_lr"], it, T))
+        ref = opt.state_dict()
+        assert len(ours["param_groups"]) == len(ref["param_groups"]) == 8
+        for g, r in zip(ours["param_groups"], ref["param_groups"]):
+            assert g["params"] == r["params"]
+            assert abs(g["lr"] - r["lr"]) < 1e-12 * max(1.0, r["lr"]) + 1e-15, (it, g["lr"], r["lr"])
+            assert g["initial_lr"] == pytest.approx(r["initial_lr"])
+            assert set(r) <= set(g)
+        opt.step()
+        sch.step()
+    # the last head lr reaches eta_min = 1e-6 from lr * scale_lr, not lr's cosine times scale_lr
+    assert cosine_lr(a["lr"] * a["scale_lr"], T, T) == pytest.approx(1e-6)
+    fresh = torch.optim.SGD(_reference_groups(state, a["lr"], a["scale_lr"]), momentum=0.9)
+    fresh.load_state_dict(m.optimizer_state_dict())
+    assert [g["lr"] for g in fresh.param_groups][-1] == pytest.approx(a["lr"] * a["scale_lr"])
+
+
+def test_pretrain_state_dict_keeps_reference_key_order(tmp_path):
+    """state_dict() emits every reference key in PSPNet.state_dict() order (gamma first,
+    num_batches_tracked per BN), so test.py:61-81's position-wise loader and train.py:57-75's
+    name-wise loader (after DDP's 'module.' prefix) pair every key with its own tensor."""
+    from collections import OrderedDict
+    from few_shot_seg_cwt_amd.checkpoint import map_backbone_by_name, map_backbone_by_position
+    a = dict(layers=50, num_classes_tr=16)
+    state = syn.make_pspnet_state(50, 2021, num_classes_tr=16)
+    m = _host_model(a, state)
+    m._train_forwards = 3
+    sd = m.state_dict()
+    specs = syn.pspnet_param_specs(50, 512, 16)
+    assert list(sd) == [n for n, _, _ in specs]
+    assert float(sd["gamma"]) == pytest.approx(0.2)
+    assert sd["layer0.1.num_batches_tracked"].dtype == torch.int64 and int(sd["layer0.1.num_batches_tracked"]) == 3
+    path = tmp_path / "pre.pth"
+    torch.save({"state_dict": sd}, path)
+    back = torch.load(path, map_location="cpu", weights_only=True)["state_dict"]
+    base = OrderedDict((n, torch.zeros(s, dtype=torch.int64 if k == "bn_nbt" else torch.float32))
+                       for n, s, k in specs)
+    by_pos = map_backbone_by_position(base, back, log=lambda *_: None)
+    by_name = map_backbone_by_name(base, OrderedDict(("module." + k, v) for k, v in back.items()),
+                                   log=lambda *_: None)
+    for k in base:
+        if "classifier" in k:
+            continue
+        assert torch.equal(by_pos[k], back[k]), k
+        if k != "gamma":
+            assert torch.equal(by_name[k], back[k]), k

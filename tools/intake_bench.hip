@@ -1,0 +1,141 @@
+// Per-CU operand intake from the XCD's L2, the limit DESIGN.md §3 puts under the small convs:
+// how fast can one workgroup per CU (or two) pull a GEMM operand stream of 128-B rows into
+//   mode 0: LDS by LDS-DMA (global_load_lds_dwordx4, the conv kernels' form), a DEPTH-slot ring,
+//           one counted vmcnt wait + barrier per 32-KB tile;
+//   mode 1: VGPRs by global_load_dwordx4 (no LDS), two register sets (tile t+1 in flight while
+//           tile t is summed);
+//   mode 2: VGPRs by global_load_dwordx4, then ds_write_b128 into a DEPTH-slot LDS ring, one
+//           barrier per tile (register-staged operand loads).
+// Every workgroup streams its own rotation of a shared 2 MB row set (L2-resident, like the
+// weight / activation rows of a conv tile).  Prints GB/s per CU for each form.
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/intake_bench.hip -o tools/intake_bench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+#define LDSP __attribute__((address_space(3)))
+#define GLBP __attribute__((address_space(1)))
+
+constexpr int TILE = 32768;             // bytes per tile (256 rows x 128 B)
+constexpr int PIECES = TILE / 1024;     // wave-instructions of 1 KB per tile
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int MODE, int NW, int DEPTH>
+__global__ __launch_bounds__(NW * 64) void intake(const char* __restrict__ buf, int nrows, int iters, float* sink) {
+  constexpr int PW = PIECES / NW;  // pieces per wave per tile
+  __shared__ __attribute__((aligned(16))) char lds[MODE == 1 ? 16 : DEPTH * TILE];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int rsub = lane >> 3, csub = (lane & 7) * 16;
+  const int base = (blockIdx.x * 977) % nrows;
+  auto src_of = [&](int t, int j) {
+    const int row = (base + t * 256 + (wv * PW + j) * 8 + rsub) % nrows;
+    return buf + (long)row * 128 + csub;
+  };
+  float acc = 0.f;
+  if (MODE == 0) {
+    for (int t = 0; t < DEPTH - 1 && t < iters; ++t)
+#pragma unroll
+      for (int j = 0; j < PW; ++j)
+        __builtin_amdgcn_global_load_lds((const GLBP void*)src_of(t, j),
+                                         (LDSP void*)(lds + (t % DEPTH) * TILE + (wv * PW + j) * 1024), 16, 0, 0);
+    for (int t = 0; t < iters; ++t) {
+      if (t + DEPTH - 1 < iters)
+        wait_vm<PW * (DEPTH - 2)>();
+      else
+        wait_vm<0>();
+      __syncthreads();
+      if (t + DEPTH - 1 < iters) {
+        const int tt = t + DEPTH - 1;
+#pragma unroll
+        for (int j = 0; j < PW; ++j)
+          __builtin_amdgcn_global_load_lds((const GLBP void*)src_of(tt, j),
+                                           (LDSP void*)(lds + (tt % DEPTH) * TILE + (wv * PW + j) * 1024), 16, 0, 0);
+      }
+      acc += *(const float*)(lds + (t % DEPTH) * TILE + threadIdx.x * 16);
+    }
+  } else if (MODE == 1) {
+    f32x4 a[PW], b[PW];
+#pragma unroll
+    for (int j = 0; j < PW; ++j) a[j] = *(const f32x4*)src_of(0, j);
+    for (int t = 0; t < iters; t += 2) {
+#pragma unroll
+      for (int j = 0; j < PW; ++j) b[j] = *(const f32x4*)src_of(t + 1, j);
+#pragma unroll
+      for (int j = 0; j < PW; ++j) acc += a[j][0] + a[j][3];
+#pragma unroll
+      for (int j = 0; j < PW; ++j) a[j] = *(const f32x4*)src_of(t + 2, j);
+#pragma unroll
+      for (int j = 0; j < PW; ++j) acc += b[j][0] + b[j][3];
+    }
+  } else {
+    f32x4 a[PW];
+#pragma unroll
+    for (int j = 0; j < PW; ++j) a[j] = *(const f32x4*)src_of(0, j);
+    for (int t = 0; t < iters; ++t) {
+      char* slot = lds + (t % DEPTH) * TILE;
+#pragma unroll
+      for (int j = 0; j < PW; ++j) *(f32x4*)(slot + (wv * PW + j) * 1024 + lane * 16) = a[j];
+      if (t + 1 < iters) {
+#pragma unroll
+        for (int j = 0; j < PW; ++j) a[j] = *(const f32x4*)src_of(t + 1, j);
+      }
+      __syncthreads();
+      acc += *(const float*)(lds + (t % DEPTH) * TILE + ((threadIdx.x * 16 + 4096) % TILE));
+    }
+  }
+  if (acc == 12345.678f) sink[blockIdx.x] = acc;
+}
+
+template <int MODE, int NW, int DEPTH>
+static void run(const char* buf, int nrows, float* sink, int grid, const char* name) {
+  const int iters = 400;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((intake<MODE, NW, DEPTH>), dim3(grid), dim3(NW * 64), 0, 0, buf, nrows, iters, sink);
+  hipDeviceSynchronize();
+  float best = 1e30f;
+  for (int r = 0; r < 5; ++r) {
+    hipEventRecord(e0);
+    hipLaunchKernelGGL((intake<MODE, NW, DEPTH>), dim3(grid), dim3(NW * 64), 0, 0, buf, nrows, iters, sink);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) best = ms;
+  }
+  const double bytes = (double)grid * iters * TILE;
+  printf("%-44s grid %4d: %8.1f us  %7.1f GB/s per CU  %6.2f TB/s chip\n", name, grid, best * 1e3,
+         bytes / (best * 1e-3) / 1e9 / 256.0, bytes / (best * 1e-3) / 1e12);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+}
+
+int main() {
+  const int nrows = 16384;  // 2 MB of 128-B rows
+  char* buf;
+  float* sink;
+  hipMalloc(&buf, (size_t)nrows * 128);
+  hipMalloc(&sink, 4096 * sizeof(float));
+  hipMemset(buf, 0, (size_t)nrows * 128);
+  for (int grid : {256, 512}) {
+    run<0, 4, 3>(buf, nrows, sink, grid, "lds-dma  4 waves ring 3");
+    run<0, 4, 4>(buf, nrows, sink, grid, "lds-dma  4 waves ring 4");
+    run<0, 8, 3>(buf, nrows, sink, grid, "lds-dma  8 waves ring 3");
+    run<1, 4, 2>(buf, nrows, sink, grid, "regs     4 waves (2 sets)");
+    run<1, 8, 2>(buf, nrows, sink, grid, "regs     8 waves (2 sets)");
+    run<1, 16, 2>(buf, nrows, sink, grid, "regs    16 waves (2 sets)");
+    run<2, 4, 2>(buf, nrows, sink, grid, "regs+ds_write 4 waves ring 2");
+    run<2, 8, 2>(buf, nrows, sink, grid, "regs+ds_write 8 waves ring 2");
+  }
+  hipError_t e = hipGetLastError();
+  printf("status %s\n", hipGetErrorString(e));
+  return e == hipSuccess ? 0 : 1;
+}
