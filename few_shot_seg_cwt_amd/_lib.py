@@ -86,6 +86,8 @@ SIGNATURES = {
     "cwt_ctx_status": (_I, [_P, C.POINTER(C.c_uint32), _I]),
     "cwt_ctx_set_conv_arith": (_I, [_P, _I]),
     "cwt_debug_adapt_spin_limit": (_I, [_P, _I64]),
+    "cwt_debug_pretrain_capture": (_I, [_P, _I]),
+    "cwt_debug_pretrain_tensor": (_I, [_P, C.c_char_p, _P, _I64]),
     "cwt_profile_enable": (_I, [_P, _I]),
     "cwt_profile_count": (_I, [_P]),
     "cwt_profile_record": (_I, [_P, _I, C.c_char_p, _I, C.POINTER(C.c_double), C.POINTER(C.c_double),

@@ -97,6 +97,10 @@ struct cwt_pretrain {
   const float* img = nullptr;
   float drop_p = 0.f;
   unsigned long long seed = 0;
+  // test hook (cwt_debug_pretrain_capture): copies of the backward's transient gradients at the
+  // block boundaries, for the teacher-forced per-block parity test
+  bool capture = false;
+  std::map<std::string, std::pair<const float*, long>> cap;  // name -> (device copy, floats)
 };
 
 namespace cwt {
@@ -600,6 +604,18 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
   const long Ms = (long)N * Hs * Hs, Mh = (long)N * h * h;
   const float drop = pt->drop_p;
   int rc;
+  // test hook: keep a dense copy of a transient gradient (rows x cols, row stride ld)
+  auto capture = [&](const std::string& nm, const float* src, long rows, int cols, int ld) -> int {
+    if (!pt->capture) return 0;
+    float* dst;
+    int r;
+    if ((r = pt_ws(pt, "cap." + nm, (size_t)rows * cols * 4, &dst))) return r;
+    CWT_HIP(hipMemcpy2DAsync(dst, (size_t)cols * 4, src, (size_t)ld * 4, (size_t)cols * 4, rows, hipMemcpyDeviceToDevice,
+                             s.st));
+    pt->cap[nm] = {dst, rows * cols};
+    return 0;
+  };
+  if ((rc = capture("dlogits", dlogits, Mh, pt->nc, pt->nc))) return rc;
   // scratch gradients: the widest activation is the layer4 map (Mh x 2048) or layer1 / stem
   size_t mx = (size_t)Mh * 2048;
   mx = std::max(mx, (size_t)Ms * 128);
@@ -649,7 +665,8 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
     base += b * b;
   }
   if ((rc = launch_ppm_wq(pt->G + Bt.w_off, 4096 * 9, gWq, 1, s.st)) ||
-      (rc = launch_avgpool_bwd(dpool, N, h, 2048, kPtBins, dcat, 2048, s.st)))
+      (rc = launch_avgpool_bwd(dpool, N, h, 2048, kPtBins, dcat, 2048, s.st)) ||
+      (rc = capture("dcat", dcat, Mh, 2048, 2048)))
     return rc;
   // ResNet blocks in reverse (resnet.py:74-96)
   const float* dout = dcat;
@@ -680,7 +697,8 @@ static int pt_backward(cwt_pretrain* pt, PtStep& s, const float* dlogits) {
       if ((rc = s.bn_bwd(b.c2, Mo, gT, b.c2.Co, kReluFromY, b.c2.Co, gY)) || (rc = s.wgrad(b.c2, gY, b.c1.a, b.c1.Co, N, H)) ||
           (rc = s.dgrad(b.c2, gY, N, H, gT, b.c1.Co, nullptr, 0, li + 1)) ||
           (rc = s.bn_bwd(b.c1, Mi, gT, b.c1.Co, kReluFromY, b.c1.Co, gY)) || (rc = s.wgrad(b.c1, gY, b.x, b.x_ld, N, H)) ||
-          (rc = s.dgrad(b.c1, gY, N, H, dx, b.c1.Ci, gR, b.c1.Ci, li + 1)))
+          (rc = s.dgrad(b.c1, gY, N, H, dx, b.c1.Ci, gR, b.c1.Ci, li + 1)) ||
+          (rc = capture("dx:l" + std::to_string(li + 1) + "." + std::to_string(bi), dx, Mi, b.c1.Ci, b.c1.Ci)))
         return rc;
       dout = dx;
       dout_ld = b.c1.Ci;
@@ -968,6 +986,75 @@ int cwt_pretrain_num_params(const cwt_pretrain* pt, int64_t* total, int64_t* bac
   }
   if (total) *total = t;
   if (backbone) *backbone = b;
+  return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- teacher-forced test hooks
+extern "C" {
+
+int cwt_debug_pretrain_capture(cwt_pretrain* pt, int on) {
+  if (!pt) return fail(CWT_EARG, "null argument");
+  pt->capture = on != 0;
+  if (!on) pt->cap.clear();
+  return 0;
+}
+
+// Forward tensors of the last step / forward ("in:l<layer>.<block>": a ResNet block's input,
+// [M][C]; "cat": layer4's output [M][2048]; "mp": the stem's max-pool output [M][128]) and the
+// captured backward gradients ("dlogits", "dcat", "dx:l<layer>.<block>": a block's input gradient).
+int cwt_debug_pretrain_tensor(cwt_pretrain* pt, const char* name, float* host_out, int64_t numel) {
+  if (!pt || !name || !host_out) return fail(CWT_EARG, "null argument");
+  CWT_HIP(hipSetDevice(pt->device));
+  CWT_HIP(hipDeviceSynchronize());
+  const std::string nm(name);
+  const float* src = nullptr;
+  long rows = 0;
+  int cols = 0, ld = 0;
+  if (nm == "cat") {
+    src = pt->CAT, rows = (long)pt->N * pt->h * pt->h, cols = ld = 2048;
+  } else if (nm == "mp") {
+    src = pt->MP, rows = (long)pt->N * pt->H1 * pt->H1, cols = ld = 128;
+  } else if (nm == "logits") {
+    src = pt->LOGITS, rows = (long)pt->N * pt->h * pt->h, cols = ld = pt->nc;
+  } else if (nm == "fpre") {  // the bottleneck's BN + ReLU output before Dropout2d
+    src = pt->Fpre, rows = (long)pt->N * pt->h * pt->h, cols = ld = 512;
+  } else if (nm.rfind("a:stem", 0) == 0) {
+    const int i = std::atoi(nm.c_str() + 6);
+    if (i < 0 || i > 2) return fail(CWT_EARG, "no activation '" + nm + "'");
+    src = pt->stem[i].a, rows = (long)pt->N * pt->Hs * pt->Hs, cols = ld = pt->stem[i].Co;
+  } else if (nm.rfind("a:ppm", 0) == 0) {
+    const int i = std::atoi(nm.c_str() + 5);
+    if (i < 0 || i > 3) return fail(CWT_EARG, "no activation '" + nm + "'");
+    src = pt->ppm[i].a, rows = (long)pt->N * kPtBins[i] * kPtBins[i], cols = ld = 512;
+  } else if (nm.rfind("a:l", 0) == 0) {  // "a:l<layer>.<block>.c<1|2|3>": BN (+ residual) + ReLU output
+    const int li = std::atoi(nm.c_str() + 3) - 1;
+    const size_t d1 = nm.find('.'), d2 = nm.rfind(".c");
+    const int bi = d1 == std::string::npos ? -1 : std::atoi(nm.c_str() + d1 + 1);
+    const int ci = d2 == std::string::npos ? 0 : std::atoi(nm.c_str() + d2 + 2);
+    if (li < 0 || li > 3 || bi < 0 || bi >= (int)pt->blocks[li].size() || ci < 1 || ci > 3)
+      return fail(CWT_EARG, "no activation '" + nm + "'");
+    const PtBlock& b = pt->blocks[li][bi];
+    const PtConv& L = ci == 1 ? b.c1 : ci == 2 ? b.c2 : b.c3;
+    src = L.a, rows = (long)pt->N * L.Ho * L.Ho, cols = L.Co, ld = L.a_ld;
+  } else if (nm.rfind("in:l", 0) == 0) {
+    const int li = std::atoi(nm.c_str() + 4) - 1;
+    const size_t dot = nm.find('.');
+    const int bi = dot == std::string::npos ? -1 : std::atoi(nm.c_str() + dot + 1);
+    if (li < 0 || li > 3 || bi < 0 || bi >= (int)pt->blocks[li].size() || !pt->blocks[li][bi].x)
+      return fail(CWT_EARG, "no block input '" + nm + "'");
+    const PtBlock& b = pt->blocks[li][bi];
+    src = b.x, rows = (long)pt->N * b.c1.Hi * b.c1.Hi, cols = b.c1.Ci, ld = b.x_ld;
+  } else {
+    auto it = pt->cap.find(nm);
+    if (it == pt->cap.end()) return fail(CWT_EARG, "nothing captured as '" + nm + "' (cwt_debug_pretrain_capture)");
+    if (numel != it->second.second) return fail(CWT_EARG, "numel mismatch for '" + nm + "'");
+    CWT_HIP(hipMemcpy(host_out, it->second.first, (size_t)numel * 4, hipMemcpyDeviceToHost));
+    return 0;
+  }
+  if (numel != rows * cols) return fail(CWT_EARG, "numel mismatch for '" + nm + "'");
+  CWT_HIP(hipMemcpy2D(host_out, (size_t)cols * 4, src, (size_t)ld * 4, (size_t)cols * 4, rows, hipMemcpyDeviceToHost));
   return 0;
 }
 

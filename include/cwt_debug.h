@@ -65,6 +65,18 @@ int cwt_debug_adapt_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t m
  * bound of 1 makes nearly every barrier time out, to exercise the error path. */
 int cwt_debug_adapt_spin_limit(cwt_ctx* ctx, int64_t limit);
 
+/* Test hooks of the pretraining step's teacher-forced per-block parity test
+ * (tests/test_gpu_pretrain_chain.py).  capture != 0: the next cwt_pretrain_step keeps copies of
+ * its transient backward gradients ("dlogits" [M][nc], "dcat" [M][2048] = the gradient at
+ * layer4's output, "dx:l<layer>.<block>" = a ResNet block's input gradient [M][Ci]).
+ * cwt_debug_pretrain_tensor copies one of those, or a forward tensor of the last step
+ * ("in:l<layer>.<block>" = a block's input [M][Ci], "a:l<layer>.<block>.c<1|2|3>" = a conv's
+ * BN (+ residual) + ReLU output, "a:stem<i>", "a:ppm<i>", "fpre" = the bottleneck's output before
+ * Dropout2d, "cat" = layer4's output, "mp" = the stem's max-pool output, "logits" [M][nc]), to
+ * host_out (numel floats, NHWC rows). */
+int cwt_debug_pretrain_capture(cwt_pretrain* pt, int on);
+int cwt_debug_pretrain_tensor(cwt_pretrain* pt, const char* name, float* host_out, int64_t numel);
+
 /* Test hook: per workgroup of a 64-thread grid, the raw HW_REG_HW_ID and HW_REG_XCC_ID of the
  * CU it ran on (out[2*b], out[2*b+1]); with a CU-masked stream this maps mask bits to CUs. */
 int cwt_debug_census(cwt_ctx* ctx, int nblocks, unsigned* out, void* stream);
