@@ -49,6 +49,8 @@ SIGNATURES = {
     "cwt_attention_bwd_train": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F,
                                      _F, C.c_uint64, _P]),
     "cwt_classify": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
+    "cwt_attention_infer": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
+    "cwt_classify_scaled": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_seg_metrics": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "cwt_seg_metrics_pair": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "cwt_seg_ce_fwd_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),

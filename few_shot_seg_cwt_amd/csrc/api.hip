@@ -41,6 +41,15 @@ int launch_seg_ce(const float* logits, const int64_t* target, int B, int h, int 
                   float* dlogits, uint8_t* lbl_ws, AdaptScalars* sc, double* loss_num, hipStream_t st);
 int launch_normalize(const float* f, int B, int Pb, float* out, const float* W0, float* logits0, hipStream_t st);
 int launch_classify(const float* W, const float* f, int B, int Pb, float* logits, hipStream_t st);
+int launch_classify_scaled(const float* W, const float* f, const float* inv, int B, int Pb, float* logits,
+                           hipStream_t st);
+size_t attention_fold_floats(int C, int H);
+int attention_fold(const float* w_qkvs, const float* fc_w, int C, int H, float* fold, float* ws, size_t ws_floats,
+                   hipStream_t st);
+size_t attention_infer_ws_floats(int B, int hw, int C, int H);
+int attention_infer(const float* q, const float* f, int B, int hw, int C, int H, const float* fold, const float* fc_b,
+                    const float* ln_w, const float* ln_b, float* out, float* inv_norm, float* logits0, float* ws,
+                    hipStream_t st);
 int launch_classify_bwd(const float* dl, const float* f, int B, int Pb, float* dW, hipStream_t st);
 // variant heads (heads.hip)
 int launch_cos_weight(float* v, const float* g, int n, int C, int mode, float* w_eff, float* vnorm, hipStream_t st);
@@ -139,6 +148,12 @@ struct cwt_ctx {
   unsigned* status_host = nullptr;
   unsigned* status_dev = nullptr;
   long adapt_spin_limit = 0;  // 0: the persistent loop's default bound (cwt_debug_adapt_spin_limit)
+  // folded CWT weights of cwt_attention_infer (M_h = W_h^T W_h, P = [fc_h W_h]) and the
+  // parameter identity they were folded from (buffers + the caller's version counter)
+  const float* fold_w = nullptr;
+  const float* fold_fc = nullptr;
+  int64_t fold_ver = -1;
+  int fold_H = 0;
 };
 
 namespace cwt {
@@ -1067,6 +1082,43 @@ int cwt_attention_bwd(cwt_ctx* ctx, const float* q, const float* f, int B, int h
                       float* g_ln_w, float* g_ln_b, void* stream) {
   return cwt_attention_bwd_train(ctx, q, f, B, hw, C, H, w_qkvs, fc_w, fc_b, ln_w, ln_b, saved, d_out, g_w_qkvs,
                                  g_fc_w, g_fc_b, g_ln_w, g_ln_b, 0.f, 0.f, 0, stream);
+}
+
+int cwt_attention_infer(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                        const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
+                        const float* ln_b, int64_t params_version, float* out, float* inv_norm, float* logits0,
+                        void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(q && f && w_qkvs && fc_w && fc_b && ln_w && ln_b && out && inv_norm, "null buffer");
+  CWT_CHECK(B >= 1 && B <= 4 && hw >= 1 && hw <= 512 * 32 && C == 512 && H == 4,
+            "need 1 <= B <= 4, 1 <= hw <= 16384, C == 512, H == 4");
+  CWT_HIP(hipSetDevice(ctx->device));
+  const hipStream_t st = (hipStream_t)stream;
+  void *fold, *ws;
+  int rc;
+  if ((rc = ensure_ws(ctx, "attn.fold", attention_fold_floats(C, H) * 4, &fold))) return rc;
+  if ((rc = ensure_ws(ctx, "attn.iws", std::max(attention_infer_ws_floats(B, hw, C, H), (size_t)4 << 20) * 4, &ws)))
+    return rc;
+  Prof p(ctx, st, "attention_fwd", (double)B * (2.0 * 2.0 * hw * C * C * H + 2.0 * 2.0 * H * 2.0 * hw * C),
+         4.0 * ((double)B * hw * C + 2.0 * H * C * C + 2.0 * C), 1);
+  if (ctx->fold_w != w_qkvs || ctx->fold_fc != fc_w || ctx->fold_ver != params_version || ctx->fold_H != H) {
+    if ((rc = attention_fold(w_qkvs, fc_w, C, H, (float*)fold, (float*)ws, (size_t)4 << 20, st))) return rc;
+    ctx->fold_w = w_qkvs;
+    ctx->fold_fc = fc_w;
+    ctx->fold_ver = params_version;
+    ctx->fold_H = H;
+  }
+  rc = attention_infer(q, f, B, hw, C, H, (const float*)fold, fc_b, ln_w, ln_b, out, inv_norm, logits0, (float*)ws, st);
+  p.end();
+  return rc;
+}
+
+int cwt_classify_scaled(cwt_ctx* ctx, const float* W, const float* f, const float* inv_norm, int B, int P, int C,
+                        float* logits, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(W && f && inv_norm && logits && C == 512 && B >= 1 && P >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_classify_scaled(W, f, inv_norm, B, P, logits, (hipStream_t)stream);
 }
 
 int cwt_classify(cwt_ctx* ctx, const float* W, const float* f, int B, int P, int C, float* logits, void* stream) {

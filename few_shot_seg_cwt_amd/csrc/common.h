@@ -57,6 +57,66 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
          (__int_as_float(__builtin_amdgcn_readlane(i, 32)) + __int_as_float(__builtin_amdgcn_readlane(i, 48)));
 }
 
+// Transposing 64-lane reduction of NV per-lane values v[0..NV) (NV = 64 or 32): every halving
+// step pairs lanes that differ in one lane bit (bit 5: v_permlane32_swap, bit 4:
+// v_permlane16_swap -- whole halves / rows exchanged, so both partners just add; bits 3, 2:
+// DPP row / half-row mirror; bits 1, 0: DPP quad perms), the lane with the bit set keeping the
+// upper half of the values.  Returns, summed over the 64 lanes: NV = 64 -> value L in lane L;
+// NV = 32 -> value L >> 1 in lanes L (pairs).  NV reductions for the price of ~NV adds.
+template <int CTRL>
+__device__ __forceinline__ float dpp_get(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int NV>
+__device__ __forceinline__ float butterfly_sum(float (&v)[NV], int lane) {
+  static_assert(NV == 64 || NV == 32, "64 or 32 values");
+  constexpr int H0 = NV / 2, H1 = H0 / 2, H2 = H1 / 2, H3 = H2 / 2;
+#pragma unroll
+  for (int j = 0; j < H0; ++j) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j + H0]), false, false);
+    v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < H1; ++j) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[j]), __float_as_uint(v[j + H1]), false, false);
+    v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  {
+    const bool up = (lane & 8) != 0;
+#pragma unroll
+    for (int j = 0; j < H2; ++j) {
+      const float send = up ? v[j] : v[j + H2], keep = up ? v[j + H2] : v[j];
+      v[j] = keep + dpp_get<0x140>(send);
+    }
+  }
+  {
+    const bool up = (lane & 4) != 0;
+#pragma unroll
+    for (int j = 0; j < H3; ++j) {
+      const float send = up ? v[j] : v[j + H3], keep = up ? v[j + H3] : v[j];
+      v[j] = keep + dpp_get<0x141>(send);
+    }
+  }
+  if constexpr (NV == 64) {
+    {
+      const bool up = (lane & 2) != 0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float send = up ? v[j] : v[j + 2], keep = up ? v[j + 2] : v[j];
+        v[j] = keep + dpp_get<0x4E>(send);
+      }
+    }
+    const bool up = (lane & 1) != 0;
+    const float send = up ? v[0] : v[1], keep = up ? v[1] : v[0];
+    return keep + dpp_get<0xB1>(send);
+  } else {
+    const bool up = (lane & 2) != 0;
+    const float send = up ? v[0] : v[1], keep = up ? v[1] : v[0];
+    const float x = keep + dpp_get<0x4E>(send);
+    return x + dpp_get<0xB1>(x);
+  }
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -13,6 +13,9 @@
 // the 7.4 MB token map exactly once (flash-decoding style chunk partials + a combine).
 #include "common.h"
 #include "kernels.h"
+#include "pretrain.h"
+
+#include <cstring>
 
 namespace cwt {
 
@@ -296,6 +299,201 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Inference tail with the token normalisation fused (test.py:190-197: f_hat = F.normalize(f_q),
+// pred_q0 = W . f_q, W' = transformer(W, f_hat, f_hat)).  The token map is read ONCE, raw: per
+// token p, inv_p = 1 / max(||f_p||, 1e-12) (so f_hat_p = inv_p f_p), the scores
+// s = (r . f_p) inv_p, the baseline logits W . f_p, and the softmax partials with weight
+// e inv_p on f_p.  No normalised copy of the map is written; the classifier then scales W'.f_p by
+// inv_p (classify_scaled_kernel).  Rows are [B][NR][C] with rho = qi * H + h.
+// ---------------------------------------------------------------------------------------
+constexpr int TOK_TPW = 4;                 // tokens per wave
+constexpr int TOK_NW = 8;                  // waves per workgroup (two per SIMD)
+constexpr int TOK_TPB = TOK_NW * TOK_TPW;  // tokens per workgroup (one chunk)
+
+template <int NR>
+__global__ __launch_bounds__(TOK_NW * 64) void attn_tokens_kernel(const float* __restrict__ r,
+                                                                  const float* __restrict__ f, int hw,
+                                                                  const float* __restrict__ W0,
+                                                                  float* __restrict__ part_g,
+                                                                  float* __restrict__ part_ml,
+                                                                  float* __restrict__ inv_norm,
+                                                                  float* __restrict__ logits0) {
+  static_assert(NR * TOK_TPW == 32, "NR rows x 4 tokens = the first 32 lanes of the butterfly");
+  constexpr int C = 512;
+  constexpr int NT = TOK_NW * 64;
+  __shared__ __attribute__((aligned(16))) float rs[NR + 2][C];       // score rows, then the two rows of W0
+  __shared__ __attribute__((aligned(16))) float wg[TOK_NW][NR][C];   // per-wave exp-weighted token sums
+  __shared__ float wml[TOK_NW][NR][2];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int chunk = blockIdx.x, b = blockIdx.y, nchunk = gridDim.x;
+  for (int i = t; i < (NR + 2) * (C / 4); i += NT) {
+    const int row = i / (C / 4), c4 = i - row * (C / 4);
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (row < NR)
+      v = ((const f32x4*)(r + ((long)b * NR + row) * C))[c4];
+    else if (W0)
+      v = ((const f32x4*)(W0 + ((long)b * 2 + row - NR) * C))[c4];
+    *(f32x4*)&rs[row][c4 * 4] = v;
+  }
+  // lane owns channels [4 lane, 4 lane + 4) and [256 + 4 lane, 256 + 4 lane + 4): every f load
+  // and LDS access of the wave is one contiguous 1-KB row (conflict-free)
+  const int tok0 = chunk * TOK_TPB + wv * TOK_TPW;
+  f32x4 fa[TOK_TPW], fb[TOK_TPW];
+#pragma unroll
+  for (int tt = 0; tt < TOK_TPW; ++tt) {
+    const int p = tok0 + tt;
+    if (p < hw) {
+      const float* src = f + ((long)b * hw + p) * C + 4 * lane;
+      fa[tt] = *(const f32x4*)src;
+      fb[tt] = *(const f32x4*)(src + 256);
+    } else {
+      fa[tt] = fb[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __syncthreads();
+  auto dot8 = [](f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1) {
+    float d = a0[0] * b0[0];
+    d = fmaf(a0[1], b0[1], d);
+    d = fmaf(a0[2], b0[2], d);
+    d = fmaf(a0[3], b0[3], d);
+    d = fmaf(a1[0], b1[0], d);
+    d = fmaf(a1[1], b1[1], d);
+    d = fmaf(a1[2], b1[2], d);
+    return fmaf(a1[3], b1[3], d);
+  };
+  // 64 per-lane partial dot products, reduced over the wave by ONE butterfly:
+  //   [tt * NR + rho] (32): r_rho . f_tt;   [32 + tt * 8 + j] (32): |f_tt|^2, W0_0 . f_tt, W0_1 . f_tt
+  float v[64];
+#pragma unroll
+  for (int rho = 0; rho < NR; ++rho) {
+    const f32x4 ra = *(const f32x4*)&rs[rho][4 * lane], rb = *(const f32x4*)&rs[rho][256 + 4 * lane];
+#pragma unroll
+    for (int tt = 0; tt < TOK_TPW; ++tt) v[tt * NR + rho] = dot8(ra, rb, fa[tt], fb[tt]);
+  }
+  {
+    const f32x4 w0a = *(const f32x4*)&rs[NR][4 * lane], w0b = *(const f32x4*)&rs[NR][256 + 4 * lane];
+    const f32x4 w1a = *(const f32x4*)&rs[NR + 1][4 * lane], w1b = *(const f32x4*)&rs[NR + 1][256 + 4 * lane];
+#pragma unroll
+    for (int tt = 0; tt < TOK_TPW; ++tt) {
+      v[32 + tt * 8] = dot8(fa[tt], fb[tt], fa[tt], fb[tt]);
+      v[32 + tt * 8 + 1] = dot8(w0a, w0b, fa[tt], fb[tt]);
+      v[32 + tt * 8 + 2] = dot8(w1a, w1b, fa[tt], fb[tt]);
+#pragma unroll
+      for (int j = 3; j < 8; ++j) v[32 + tt * 8 + j] = 0.f;
+    }
+  }
+  const float red = butterfly_sum<64>(v, lane);  // lane L: value L
+  const bool score_lane = lane < 32;
+  const int my_t = (lane & 31) / NR, my_rho = lane % NR;
+  const int p = tok0 + my_t;
+  const bool valid = score_lane && p < hw;
+  const float nrm2 = __shfl(red, 32 + my_t * 8, 64);  // |f|^2 of this lane's token
+  const float inv = 1.0f / fmaxf(sqrtf(nrm2), 1e-12f);
+  if (valid && my_rho == 0) inv_norm[(long)b * hw + p] = inv;
+  if (logits0 && lane >= 32 && ((lane & 7) == 1 || (lane & 7) == 2)) {  // W0 . f of token (lane - 32) / 8
+    const int pt = tok0 + ((lane - 32) >> 3);
+    if (pt < hw) logits0[((long)b * 2 + (lane & 7) - 1) * hw + pt] = red;
+  }
+  const float sc = valid ? red * inv : -INFINITY;
+  // softmax partial per row over the wave's 4 tokens (score lanes of one row differ in bits 3, 4)
+  float m = sc;
+  m = fmaxf(m, __shfl_xor(m, 8, 64));
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  const float e = valid ? __expf(sc - m) : 0.f;
+  float l = e;
+  l += __shfl_xor(l, 8, 64);
+  l += __shfl_xor(l, 16, 64);
+  const float wgt = e * inv;  // f_hat = inv f: the token's weight on the raw f
+  f32x4 ga[NR], gb[NR];
+#pragma unroll
+  for (int rho = 0; rho < NR; ++rho) ga[rho] = gb[rho] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tt = 0; tt < TOK_TPW; ++tt)
+#pragma unroll
+    for (int rho = 0; rho < NR; ++rho) {
+      const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wgt), tt * NR + rho));
+      ga[rho] += w * fa[tt];
+      gb[rho] += w * fb[tt];
+    }
+#pragma unroll
+  for (int rho = 0; rho < NR; ++rho) {
+    *(f32x4*)&wg[wv][rho][4 * lane] = ga[rho];
+    *(f32x4*)&wg[wv][rho][256 + 4 * lane] = gb[rho];
+  }
+  if (lane < NR) {  // lane rho (token 0) carries its row's max and sum
+    wml[wv][lane][0] = m;
+    wml[wv][lane][1] = l;
+  }
+  __syncthreads();
+  for (int i = t; i < NR * (C / 4); i += NT) {
+    const int rho = i / (C / 4), c4 = i - rho * (C / 4);
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < TOK_NW; ++w) M = fmaxf(M, wml[w][rho][0]);
+    f32x4 G = f32x4{0.f, 0.f, 0.f, 0.f};
+    float L = 0.f;
+#pragma unroll
+    for (int w = 0; w < TOK_NW; ++w) {
+      const float s = (wml[w][rho][0] == -INFINITY) ? 0.f : __expf(wml[w][rho][0] - M);
+      G += s * *(const f32x4*)&wg[w][rho][c4 * 4];
+      L = fmaf(s, wml[w][rho][1], L);
+    }
+    *(f32x4*)&part_g[(((long)b * nchunk + chunk) * NR + rho) * C + c4 * 4] = G;
+    if (c4 == 0) {
+      part_ml[(((long)b * nchunk + chunk) * NR + rho) * 2] = M;
+      part_ml[(((long)b * nchunk + chunk) * NR + rho) * 2 + 1] = L;
+    }
+  }
+}
+
+// g[b][rho][k] = sum_c e^{m_c - M} G_c[k] / sum_c e^{m_c - M} l_c in ONE pass: the chunk maxima
+// and sums go to LDS first (M from there), then each thread issues all its chunks' loads.
+// Block = (64 channels, row rho, batch b); its 4 waves take every 4th chunk.
+constexpr int TOK_MAXCHUNK = 512;
+template <int NR>
+__global__ __launch_bounds__(256) void attn_combine1_kernel(const float* __restrict__ part_g,
+                                                            const float* __restrict__ part_ml, int nchunk,
+                                                            float* __restrict__ g) {
+  constexpr int C = 512;
+  __shared__ float ms[TOK_MAXCHUNK], ls[TOK_MAXCHUNK];
+  __shared__ float sg[4][64], red[4];
+  const int t = threadIdx.x, kk = t & 63, cg = t >> 6;
+  const int k = blockIdx.x * 64 + kk;
+  const int rho = blockIdx.y, b = blockIdx.z;
+  for (int c = t; c < nchunk; c += 256) {
+    ms[c] = part_ml[(((long)b * nchunk + c) * NR + rho) * 2];
+    ls[c] = part_ml[(((long)b * nchunk + c) * NR + rho) * 2 + 1];
+  }
+  __syncthreads();
+  float M = -INFINITY;
+  for (int c = kk; c < nchunk; c += 64) M = fmaxf(M, ms[c]);
+  M = wave_max(M);
+  const float* pg = part_g + ((long)b * nchunk * NR + rho) * C + k;
+  float G = 0.f, L = 0.f;
+  for (int c0 = cg; c0 < nchunk; c0 += 64) {  // 16 chunks per round, all loads in flight
+    float gc[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) gc[u] = pg[(long)min(c0 + 4 * u, nchunk - 1) * NR * C];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int c = c0 + 4 * u;
+      if (c >= nchunk) break;
+      const float s = (ms[c] == -INFINITY) ? 0.f : __expf(ms[c] - M);
+      G = fmaf(s, gc[u], G);
+      L = fmaf(s, ls[c], L);
+    }
+  }
+  sg[cg][kk] = G;
+  if (kk == 0) red[cg] = L;
+  __syncthreads();
+  if (cg == 0) {
+    const float Gs = (sg[0][kk] + sg[1][kk]) + (sg[2][kk] + sg[3][kk]);
+    const float Ls = (red[0] + red[1]) + (red[2] + red[3]);
+    g[((long)b * NR + rho) * C + k] = Gs / Ls;
+  }
+}
+
 // Training-mode output dropout (transformer.py:52,80): y = dropout(fc(o)) + q, in place on y =
 // fc(o) (stream 2, index v*C + k).
 __global__ void dropout_residual_kernel(float* __restrict__ y, const float* __restrict__ q, int n, float p,
@@ -430,6 +628,95 @@ int attention_fwd(const float* q, const float* f, int B, int hw, int C, int H, c
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Inference with folded weights.  For fixed parameters the two products around the token pass
+// fold into per-head 512 x 512 matrices (computed once per parameter version, attention_fold):
+//   M_h = W_h^T W_h          =>  r_h = M_h q / sqrt(C)            (replaces W_h q, then W_h^T a)
+//   P   = [fc_h W_h]_h       =>  y = P [g_h]_h + fc_b + q          (replaces W_h g, then fc)
+// the same function re-associated once more (fp32 rounding only), 5 launches instead of 8 and
+// 8 MB of weight reads per episode instead of 16.
+// ---------------------------------------------------------------------------------------
+size_t attention_fold_floats(int C, int H) { return 2 * (size_t)H * C * C; }
+
+int attention_fold(const float* w_qkvs, const float* fc_w, int C, int H, float* fold, float* ws, size_t ws_floats,
+                   hipStream_t st) {
+  float* M = fold;                      // [H][C][C]
+  float* P = fold + (size_t)H * C * C;  // [C][H*C]
+  int rc;
+  for (int h = 0; h < H; ++h) {
+    PtGemm g;
+    std::memset(&g, 0, sizeof(g));
+    g.A = w_qkvs + (size_t)h * C * C;   // A(i, d) = W[h*C + d][i]
+    g.sai = 1;
+    g.sak = C;
+    g.B = w_qkvs + (size_t)h * C * C;   // B(d, j) = W[h*C + d][j]
+    g.sbk = C;
+    g.sbj = 1;
+    g.C = M + (size_t)h * C * C;
+    g.ldc = C;
+    g.M = C;
+    g.N = C;
+    g.K = C;
+    if ((rc = launch_pt_gemm(g, ws, ws_floats, st))) return rc;
+    std::memset(&g, 0, sizeof(g));
+    g.A = fc_w + (size_t)h * C;         // A(j, d) = fc_w[j][h*C + d]
+    g.sai = (long)H * C;
+    g.sak = 1;
+    g.B = w_qkvs + (size_t)h * C * C;   // B(d, k) = W[h*C + d][k]
+    g.sbk = C;
+    g.sbj = 1;
+    g.C = P + (size_t)h * C;            // P[j][h*C + k]
+    g.ldc = (long)H * C;
+    g.M = C;
+    g.N = C;
+    g.K = C;
+    if ((rc = launch_pt_gemm(g, ws, ws_floats, st))) return rc;
+  }
+  return 0;
+}
+
+size_t attention_infer_ws_floats(int B, int hw, int C, int H) {
+  const long NR = 2L * H, nchunk = cdiv(hw, TOK_TPB);
+  return (size_t)(B * NR * C + B * nchunk * NR * (C + 2) + B * NR * C + 2L * B * C);
+}
+
+// q [B][2][C] (the inner loop's W), f [B][hw][C] raw query features; outputs W' [B][2][C],
+// inv_norm [B][hw] and, when logits0 is given, the baseline logits W . f [B][2][hw].
+int attention_infer(const float* q, const float* f, int B, int hw, int C, int H, const float* fold, const float* fc_b,
+                    const float* ln_w, const float* ln_b, float* out, float* inv_norm, float* logits0, float* ws,
+                    hipStream_t st) {
+  if (C != 512 || H != 4) return fail(CWT_EARG, "attention_infer: C = 512 and 4 heads (the fused token pass)");
+  constexpr int NR = 8;
+  const int nv = 2 * B, nchunk = cdiv(hw, TOK_TPB);
+  if (nchunk > TOK_MAXCHUNK) return fail(CWT_EARG, "attention_infer: hw too large");
+  const float* M = fold;
+  const float* P = fold + (size_t)H * C * C;
+  float* r = ws;                                  // [B][NR][C] = [nv][H][C]
+  float* part_g = r + (size_t)B * NR * C;          // [B][nchunk][NR][C]
+  float* part_ml = part_g + (size_t)B * nchunk * NR * C;
+  float* g = part_ml + (size_t)B * nchunk * NR * 2;  // [B][NR][C] = [nv][H][C]
+  float* y = g + (size_t)B * NR * C;              // [nv][C]
+  int rc;
+  // 1. r[v][h*C + k] = M_h[k] . q[v] / sqrt(C)
+  if ((rc = launch_rowdot(M, H * C, C, q, nv, C, 0, H * C, nullptr, nullptr, 0, r, (long)H * C,
+                          1.0f / sqrtf((float)C), st)))
+    return rc;
+  // 2. the token pass (normalisation, baseline logits, chunk partials)
+  hipLaunchKernelGGL((attn_tokens_kernel<NR>), dim3(nchunk, B), dim3(TOK_NW * 64), 0, st, (const float*)r, f, hw, q, part_g,
+                     part_ml, inv_norm, logits0);
+  CWT_LAUNCH_CHECK();
+  // 3. g = softmax-weighted token means
+  hipLaunchKernelGGL((attn_combine1_kernel<NR>), dim3(C / 64, NR, B), dim3(256), 0, st, (const float*)part_g,
+                     (const float*)part_ml, nchunk, g);
+  CWT_LAUNCH_CHECK();
+  // 4. y[v] = P . g[v] + fc_b + q[v]
+  if ((rc = launch_rowdot(P, C, H * C, g, nv, (long)H * C, 0, C, fc_b, q, C, y, C, 1.f, st))) return rc;
+  // 5. LayerNorm
+  hipLaunchKernelGGL(layernorm_kernel, dim3(nv), dim3(64), 0, st, (const float*)y, ln_w, ln_b, out, (float*)nullptr,
+                     1e-5f);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
 
 // ---------------------------------------------------------------------------------------
 // Backward (train.py:264 loss_q.backward through the CWT; q and f carry no gradient).

@@ -82,6 +82,47 @@ __global__ __launch_bounds__(256) void classify_kernel(const float* __restrict__
   }
 }
 
+// the classifier over raw features with the normalisation as a per-pixel scale (the fused
+// inference tail): logits = (W' . f_p) inv_p = W' . f_hat_p (test.py:200-204)
+__global__ __launch_bounds__(256) void classify_scaled_kernel(const float* __restrict__ W, const float* __restrict__ f,
+                                                              const float* __restrict__ inv, long P, int Pb,
+                                                              float* __restrict__ logits) {
+  constexpr int C = 512;
+  const int lane = threadIdx.x & 63;
+  const long p = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= P) return;
+  const int b = (int)(p / Pb);
+  const long pp = p - (long)b * Pb;
+  const float* src = f + p * C + lane * 4;
+  const f32x4 u = *(const f32x4*)src, v = *(const f32x4*)(src + 256);
+  const float* w = W + (long)b * 2 * C + lane * 4;
+  const f32x4 w0a = *(const f32x4*)w, w0b = *(const f32x4*)(w + 256);
+  const f32x4 w1a = *(const f32x4*)(w + C), w1b = *(const f32x4*)(w + C + 256);
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    s0 = fmaf(w0a[q], u[q], s0);
+    s0 = fmaf(w0b[q], v[q], s0);
+    s1 = fmaf(w1a[q], u[q], s1);
+    s1 = fmaf(w1b[q], v[q], s1);
+  }
+  s0 = wave_sum_dpp(s0);
+  s1 = wave_sum_dpp(s1);
+  if (lane == 0) {
+    const float iv = inv[p];
+    logits[(long)b * 2 * Pb + pp] = s0 * iv;
+    logits[(long)b * 2 * Pb + Pb + pp] = s1 * iv;
+  }
+}
+
+int launch_classify_scaled(const float* W, const float* f, const float* inv, int B, int Pb, float* logits,
+                           hipStream_t st) {
+  long P = (long)B * Pb;
+  hipLaunchKernelGGL(classify_scaled_kernel, dim3(cdiv(P, 4)), dim3(256), 0, st, W, f, inv, P, Pb, logits);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 int launch_classify(const float* W, const float* f, int B, int Pb, float* logits, hipStream_t st) {
   long P = (long)B * Pb;
   hipLaunchKernelGGL(classify_kernel, dim3(cdiv(P, 4)), dim3(256), 0, st, W, f, P, Pb, logits);

@@ -144,6 +144,124 @@ def preprocess_label(label: torch.Tensor, S: int, class_chosen: int = -1, flip_h
     return out
 
 
+def standard_label(label: np.ndarray, class_list: List[int]) -> np.ndarray:
+    """StandardData's label remap (dataset.py:144-168): every class of class_list present becomes
+    class_list.index(c) + 1, other classes 255, everything else -- including the source's own 255
+    void pixels -- background 0 (new_label starts as zeros and the void value is never copied)."""
+    label_class = np.unique(label).tolist()
+    for v in (0, 255):
+        if v in label_class:
+            label_class.remove(v)
+    wanted = [c for c in label_class if c in class_list]
+    unwanted = [c for c in label_class if c not in class_list]
+    assert len(wanted) > 0
+    new_label = np.zeros_like(label)
+    for c in wanted:
+        new_label[label == c] = class_list.index(c) + 1
+    for c in unwanted:
+        new_label[label == c] = 255
+    return new_label
+
+
+class StandardData:
+    """dataset.py:120-177 (the non-episodic loader stage-1 pretraining reads, pretrain.py:83) with
+    the transforms on the device: ``__getitem__`` returns (image fp32 [3,S,S], label int64 [S,S])
+    on ``device`` (+ the paths with ``return_paths``).  The pretraining configs' augmentations are
+    hor_flip, vert_flip, resize (pascal_pretrain.yaml / coco_pretrain.yaml); one
+    ``random.random()`` per flip as transform.py:403-422 draws it."""
+
+    SUPPORTED_AUG = ("hor_flip", "vert_flip", "resize")
+
+    def __init__(self, args, data_list_path: str, class_list: List[int], return_paths: bool = False,
+                 augmentations=None, read_image: Callable = read_npy, read_label: Callable = read_npy, device=None):
+        self.S = int(_g(args, "image_size", 473))
+        self.mean, self.std = list(_g(args, "mean")), list(_g(args, "std"))
+        self.padding = [v * 255 for v in self.mean] if _g(args, "padding") == "avg" else None
+        augs = list(augmentations if augmentations is not None else ["resize"])
+        bad = [a for a in augs if a not in self.SUPPORTED_AUG]
+        if bad or "resize" not in augs:
+            raise NotImplementedError(f"augmentations {bad or augs}: the pretraining configs use hor_flip, "
+                                      "vert_flip, resize")
+        self.flips = [a for a in augs if a != "resize"]
+        self.class_list = class_list
+        self.return_paths = return_paths
+        self.read_image, self.read_label = read_image, read_label
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.data_list, _ = make_dataset(_g(args, "data_root"), data_list_path, class_list, read_label)
+
+    def __len__(self):
+        return len(self.data_list)
+
+    def host_item(self, index: int):
+        """The decoded image and the remapped label before the transform (host arrays)."""
+        image_path, label_path = self.data_list[index]
+        image = self.read_image(image_path)
+        label = self.read_label(label_path)
+        if image.shape[0] != label.shape[0] or image.shape[1] != label.shape[1]:
+            raise RuntimeError("Query Image & label shape mismatch: " + image_path + " " + label_path + "\n")
+        return image, standard_label(label, self.class_list), image_path, label_path
+
+    def __getitem__(self, index: int):
+        image, label, image_path, label_path = self.host_item(index)
+        fl = {"hor_flip": False, "vert_flip": False}
+        for a in self.flips:
+            fl[a] = random.random() < 0.5
+        img = torch.from_numpy(np.ascontiguousarray(image)).to(self.device)
+        lab = torch.from_numpy(np.ascontiguousarray(label.astype(np.uint8))).to(self.device)
+        t = preprocess_image(img, self.S, self.mean, self.std, self.padding, fl["hor_flip"], fl["vert_flip"])
+        lt = preprocess_label(lab, self.S, -1, fl["hor_flip"], fl["vert_flip"])
+        if self.return_paths:
+            return t, lt, image_path, label_path
+        return t, lt
+
+
+class StandardLoader:
+    """``torch.utils.data.DataLoader(StandardData, batch_size, shuffle, sampler, drop_last)``
+    (dataset.py:61-68) in the calling process: batches stacked on the device, order from torch's
+    RNG as RandomSampler draws it (or the sampler's shard).  The iterator has ``.next()`` like the
+    torch-1.6 iterators pretrain.py:105,110 use."""
+
+    def __init__(self, dataset: StandardData, batch_size: int, shuffle: bool, drop_last: bool,
+                 sampler: "EpisodeSampler | None" = None):
+        self.dataset, self.batch_size, self.drop_last, self.sampler = dataset, int(batch_size), drop_last, sampler
+        self.shuffle = shuffle and sampler is None
+
+    def __len__(self):
+        n = len(self.sampler) if self.sampler is not None else len(self.dataset)
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+    def __iter__(self):
+        n = len(self.dataset)
+        if self.sampler is not None:
+            order = list(self.sampler)
+        elif self.shuffle:
+            seed = int(torch.empty((), dtype=torch.int64).random_().item())
+            order = torch.randperm(n, generator=torch.Generator().manual_seed(seed)).tolist()
+        else:
+            order = list(range(n))
+        nb, bs, ds = len(self), self.batch_size, self.dataset
+
+        class _It:
+            def __init__(self):
+                self.i = 0
+
+            def next(self):
+                if self.i >= nb:
+                    raise StopIteration
+                items = [ds[j] for j in order[self.i * bs:(self.i + 1) * bs]]
+                self.i += 1
+                out = [torch.stack([it[0] for it in items]), torch.stack([it[1] for it in items])]
+                if ds.return_paths:
+                    out += [[it[2] for it in items], [it[3] for it in items]]
+                return tuple(out)
+
+            __next__ = next
+
+            def __iter__(self):
+                return self
+        return _It()
+
+
 class EpisodicData:
     """dataset.py:180-327 with the transforms on the device.  ``__getitem__`` returns the
     reference's 7-tuple: (qry_img [3,S,S], target [S,S], spprt_imgs [shot,3,S,S],
@@ -301,8 +419,12 @@ class EpisodeLoader:
         return _It()
 
 
-def get_train_loader(args, read_image: Callable = read_npy, read_label: Callable = read_npy, device=None):
-    """dataset.py:17-63 (episodic): (loader, sampler).  Distributed when ``args.distributed`` is
+def get_train_loader(args, read_image: Callable = read_npy, read_label: Callable = read_npy, device=None,
+                     episodic: bool = True, return_path: bool = False):
+    """dataset.py:17-63: (loader, sampler).  ``episodic=False`` (pretrain.py:83): StandardData over
+    ``args.train_list`` with ``args.augmentations``, batches of ``batch_size`` (per rank
+    ``batch_size / world`` when distributed, as dataset.py:59), shuffled, drop_last.  Episodic:
+    distributed when ``args.distributed`` is
     set or torch.distributed runs more than one rank: the loader iterates this rank's
     :class:`EpisodeSampler` shard (``DistributedSampler`` in the reference) and the sampler is
     returned for ``set_epoch``; otherwise (loader, None).  Each rank runs ONE episode per
@@ -313,8 +435,15 @@ def get_train_loader(args, read_image: Callable = read_npy, read_label: Callable
     assert _g(args, "train_split") in [0, 1, 2, 3]
     split_classes = get_split_classes(args)
     class_list = split_classes[_g(args, "train_name")][_g(args, "train_split")]["train"]
-    ds = EpisodicData(True, class_list, args, read_image, read_label, device)
     rank, world = rank_world()
+    distributed = bool(_g(args, "distributed", False)) or world > 1
+    if not episodic:
+        ds = StandardData(args, _g(args, "train_list"), class_list, return_path, _g(args, "augmentations", ["resize"]),
+                          read_image, read_label, device)
+        sampler = EpisodeSampler(len(ds), rank, world, shuffle=True) if distributed else None
+        bs = int(_g(args, "batch_size", 1)) // (world if distributed else 1)
+        return StandardLoader(ds, max(bs, 1), shuffle=sampler is None, drop_last=True, sampler=sampler), sampler
+    ds = EpisodicData(True, class_list, args, read_image, read_label, device)
     if _g(args, "distributed", False) or world > 1:
         sampler = EpisodeSampler(len(ds), rank, world, shuffle=True)
         return EpisodeLoader(ds, shuffle=False, sampler=sampler), sampler

@@ -97,6 +97,33 @@ def classify(W: torch.Tensor, f: torch.Tensor) -> torch.Tensor:
     return logits
 
 
+def classify_scaled(W: torch.Tensor, f: torch.Tensor, inv_norm: torch.Tensor) -> torch.Tensor:
+    """W [B,2,512] . F.normalize(f) with the normalisation as the per-pixel scale inv_norm [B,hw]
+    (cwt_classify_scaled; f the RAW features [B,512,h,w] channels_last) -> logits [B,2,h,w]."""
+    B, Cc, h, w = f.shape
+    logits = torch.empty((B, 2, h, w), device=f.device, dtype=torch.float32)
+    W = W.contiguous()
+    _lib.check(_lib.lib().cwt_classify_scaled(_lib.ctx(f.device.index), _lib.ptr(W), _lib.ptr(f),
+                                              _lib.ptr(inv_norm), B, h * w, Cc, _lib.ptr(logits),
+                                              _lib.stream_ptr(f.device)), "cwt_classify_scaled")
+    return logits
+
+
+def cwt_tail(transformer, Wb: torch.Tensor, f_q: torch.Tensor):
+    """test.py:190-204 after the inner loop: pred_q0 = W . f_q, f_hat = F.normalize(f_q),
+    W' = CWT(W, f_hat, f_hat), pred_q = W' . f_hat.  4 heads: the fused form (one pass over the
+    raw tokens, no normalised copy; cwt_attention_infer + cwt_classify_scaled); otherwise the
+    module-by-module kernels.  Returns (W', pred_q, pred_q0)."""
+    if transformer.n_head == 4:
+        if not f_q.is_contiguous(memory_format=torch.channels_last):
+            f_q = f_q.contiguous(memory_format=torch.channels_last)
+        W2, inv, pred_q0 = transformer.infer_raw(Wb, f_q)
+        return W2, classify_scaled(W2, f_q, inv), pred_q0
+    fqn, pred_q0 = normalize(f_q, Wb)
+    W2 = transformer.infer(Wb, fqn)
+    return W2, classify(W2, fqn), pred_q0
+
+
 def classify_bwd(dlogits: torch.Tensor, f: torch.Tensor, dW: torch.Tensor):
     B, Cc, h, w = f.shape
     dlogits = dlogits.contiguous()
@@ -139,9 +166,7 @@ class EpisodeEngine:
         f_s, f_q = f_all[:shot], f_all[shot:]
         W = inner_adapt(f_s, s_label, W0, self.lr, self.iters)
         Wb = W.view(1, 2, -1)
-        fqn, pred_q0 = normalize(f_q, Wb)
-        W2 = self.transformer.infer(Wb, fqn)
-        pred_q = classify(W2, fqn)
+        W2, pred_q, pred_q0 = cwt_tail(self.transformer, Wb, f_q)
         iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, f_s=f_s, f_q=f_q)
 
@@ -160,10 +185,8 @@ class EpisodeEngine:
         f_all, _ = self.model.extract_features(imgs)
         f_s, f_q = f_all[:E * shot], f_all[E * shot:]
         W = inner_adapt_batch(f_s, s_label, W0, self.lr, self.iters)
-        fqn, pred_q0 = normalize(f_q, W)
-        W2 = self.transformer.infer(W, fqn) if E <= 4 else \
-            torch.cat([self.transformer.infer(W[i:i + 4], fqn[i:i + 4]) for i in range(0, E, 4)])
-        pred_q = classify(W2, fqn)
+        parts = [cwt_tail(self.transformer, W[i:i + 4], f_q[i:i + 4]) for i in range(0, E, 4)]
+        W2, pred_q, pred_q0 = (torch.cat([p[j] for p in parts]) for j in range(3))
         iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, f_s=f_s, f_q=f_q)
 
@@ -236,9 +259,7 @@ class EpisodePipeline:
             f_s, f_q = f_all[:shot], f_all[shot:]
             W = inner_adapt(f_s, s_label, W0, eng.lr, eng.iters)
             Wb = W.view(1, 2, -1)
-            fqn, pred_q0 = normalize(f_q, Wb)
-            W2 = eng.transformer.infer(Wb, fqn)
-            pred_q = classify(W2, fqn)
+            W2, pred_q, pred_q0 = cwt_tail(eng.transformer, Wb, f_q)
             iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
             done_all = torch.cuda.Event()
             done_all.record(self.s_adapt)

@@ -37,6 +37,7 @@ class HipSGD:
                                                _lib.ptr(buf), p.numel(), self.lr, self.momentum, self.weight_decay,
                                                int(self.nesterov), int(first), _lib.stream_ptr(p.device)),
                        "cwt_sgd_step")
+            torch.autograd.graph.increment_version(p)   # the kernel wrote p: caches keyed on its version
 
     def state_dict(self):
         return {"state": {i: {"momentum_buffer": b} for i, b in enumerate(self.bufs) if b is not None},

@@ -78,6 +78,7 @@ class _Attention(torch.nn.Module):
 
 class MultiHeadAttentionOne(torch.nn.Module):
     """transformer.py:33-83 (shared projection, d_k = d_v = d_model per head)."""
+    _uid = 0
 
     def __init__(self, n_head: int, d_model: int, d_k: int, d_v: int, dropout: float = 0.1, device=None):
         super().__init__()
@@ -89,6 +90,8 @@ class MultiHeadAttentionOne(torch.nn.Module):
         self.attention = _Attention(temperature=float(np.power(d_k, 0.5)))  # transformer.py:47
         self.dropout = torch.nn.Dropout(dropout)                              # transformer.py:52
         self._layout, total = _layout(n_head, d_model)
+        MultiHeadAttentionOne._uid += 1
+        self._uid = MultiHeadAttentionOne._uid   # with flat._version: the identity of the folded weights
         dev = torch.device("cuda", device if device is not None else torch.cuda.current_device()) \
             if torch.cuda.is_available() else torch.device("cpu")
         self.flat = torch.nn.Parameter(torch.zeros(total, dtype=torch.float32, device=dev))
@@ -129,6 +132,7 @@ class MultiHeadAttentionOne(torch.nn.Module):
                 raise ValueError(f"{n}: {tuple(v.shape)} != {shp}")
             with torch.no_grad():
                 self.flat.data[off:off + k].copy_(v.reshape(-1).to(self.flat.device, torch.float32))
+        torch.autograd.graph.increment_version(self.flat)   # writes through .data do not bump it
         return self
 
     def named_views(self):
@@ -207,6 +211,32 @@ class MultiHeadAttentionOne(torch.nn.Module):
         """Eval-mode forward whatever the module's mode (the inference engine's call)."""
         out, _ = self._fwd(q, as_tokens(k), need_saved=False)
         return out
+
+    def params_version(self) -> int:
+        """Identity of the current parameter values for libcwt's folded-weight cache: this module's
+        id and flat's in-place version counter (bumped by load_state_dict, the optimisers and any
+        in-place op on flat; code writing through flat.data must call
+        torch.autograd.graph.increment_version(flat))."""
+        return (self._uid << 40) | (int(self.flat._version) & ((1 << 40) - 1))
+
+    def infer_raw(self, q, f, with_logits0: bool = True):
+        """The inference episode's normalize + baseline logits + eval-mode CWT (test.py:190-197) over
+        the RAW query features in one pass (cwt_attention_infer, 4 heads): returns (W' [B,2,512],
+        inv_norm [B,hw] with F.normalize(f) = f * inv_norm, pred_q0 = W . f [B,2,h,w] or None)."""
+        if self.n_head != 4:
+            raise NotImplementedError("the fused inference tail needs 4 heads (scripts/*.sh); use infer()")
+        q = q.contiguous()
+        B, hw = self._check(q, f)
+        ft = as_tokens(f)
+        out = torch.empty((B, 2, self.d_model), device=q.device, dtype=torch.float32)
+        inv = torch.empty((B, hw), device=q.device, dtype=torch.float32)
+        lg0 = torch.empty((B, 2) + tuple(f.shape[2:]), device=q.device, dtype=torch.float32) if with_logits0 else None
+        w, fw, fb, lw, lb = self._ptrs(self.flat)
+        _lib.check(_lib.lib().cwt_attention_infer(_lib.ctx(q.device.index), _lib.ptr(q), _lib.ptr(ft), B, hw,
+                                                  self.d_model, self.n_head, w, fw, fb, lw, lb, self.params_version(),
+                                                  _lib.ptr(out), _lib.ptr(inv), _lib.ptr(lg0),
+                                                  _lib.stream_ptr(q.device)), "cwt_attention_infer")
+        return out, inv, lg0
 
     # explicit training API (no autograd graph; used by the episode drivers)
     def forward_train(self, q, f):

@@ -224,6 +224,30 @@ int cwt_attention_bwd_train(cwt_ctx* ctx, const float* q, const float* f, int B,
                             float* g_fc_w, float* g_fc_b, float* g_ln_w, float* g_ln_b, float attn_dropout,
                             float out_dropout, uint64_t seed, void* stream);
 
+/*
+ * The inference episode's tail before the classifier as ONE call over the RAW query features:
+ * f_hat = F.normalize(f_q) (test.py:194), pred_q0 = W . f_q (test.py:192) and
+ * W' = MultiHeadAttentionOne(H, C, C, C).eval()(W, f_hat, f_hat) (test.py:195-197,
+ * transformer.py:54-83), with the normalisation fused into the single pass over the tokens:
+ * no normalised copy of f is written; inv_norm [B,hw] = 1 / max(||f_p||, 1e-12) is returned for
+ * cwt_classify_scaled.  For fixed parameters the projections fold into per-head matrices
+ * (W_h^T W_h and fc_h W_h), computed on this context's stream once per parameter identity --
+ * (w_qkvs, fc_w, params_version): the caller bumps params_version whenever it modifies the
+ * parameters in place (torch's tensor._version does).  Same function as cwt_normalize +
+ * cwt_attention_fwd up to fp32 rounding (re-associated).  H must be 4.
+ * q: device fp32 [B,2,C] (the adapted classifier, also the baseline's weights); f: NHWC [B,hw,C];
+ * out [B,2,C]; inv_norm [B,hw]; logits0 [B,2,hw] or NULL.
+ */
+int cwt_attention_infer(cwt_ctx* ctx, const float* q, const float* f, int B, int hw, int C, int H,
+                        const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
+                        const float* ln_b, int64_t params_version, float* out, float* inv_norm, float* logits0,
+                        void* stream);
+
+/* logits = (W . f_p) * inv_norm[p] = W . F.normalize(f)_p (test.py:200-204 over the raw features
+ * and cwt_attention_infer's inv_norm).  W [B,2,C]; f NHWC [B,P,C]; inv_norm [B,P]; logits [B,2,P]. */
+int cwt_classify_scaled(cwt_ctx* ctx, const float* W, const float* f, const float* inv_norm, int B, int P, int C,
+                        float* logits, void* stream);
+
 /* Per-pixel classifier logits = W . f (test.py:200-204 Pseudo_cls; train.py:259-261 matmul).
  * W: device [B,2,C]; f: NHWC [B,P,C]; logits: device [B,2,P] (NCHW [B,2,h,w]). */
 int cwt_classify(cwt_ctx* ctx, const float* W, const float* f, int B, int P, int C, float* logits,

@@ -150,3 +150,53 @@ def test_validate_transformer_over_episodic_loader(dev, tmp_path):
     eps = []
     miou, loss = validate_transformer(args, loader, model, t, episodes_out=eps)
     assert np.isfinite(miou) and np.isfinite(loss) and len(eps) == 3
+
+
+def test_standard_label_remap():
+    """dataset.py:144-168: classes of class_list -> index + 1, other classes 255, the source's
+    own void (255) and background -> 0."""
+    lab = np.array([[0, 3, 3, 255], [5, 5, 7, 0]], np.uint8)
+    out = D.standard_label(lab, [3, 7, 9])
+    np.testing.assert_array_equal(out, np.array([[0, 1, 1, 0], [255, 255, 2, 0]], np.uint8))
+    with pytest.raises(AssertionError):
+        D.standard_label(np.array([[0, 5]], np.uint8), [3])
+
+
+def test_standard_data_host_items(tmp_path):
+    """StandardData over make_dataset's list (utils.py filter), remapped labels (host part)."""
+    lst = _write_dataset(str(tmp_path), n=6, H=(90, 110))
+    args = dict(image_size=65, mean=MEAN, std=STD, data_root=str(tmp_path))
+    ds = D.StandardData.__new__(D.StandardData)
+    ds.class_list, ds.read_image, ds.read_label = [1, 2, 3], D.read_npy, D.read_npy
+    ds.data_list, _ = D.make_dataset(args["data_root"], lst, [1, 2, 3])
+    for i in range(len(ds.data_list)):
+        img, lab, ip, lp = D.StandardData.host_item(ds, i)
+        raw = np.load(lp)
+        assert img.shape[:2] == lab.shape
+        np.testing.assert_array_equal(lab[raw == 255], 0)
+        for c in (1, 2, 3):
+            np.testing.assert_array_equal(lab[raw == c], c)   # index + 1 with class_list [1, 2, 3]
+
+
+@pytest.mark.gpu
+def test_standard_loader_end_to_end(dev, tmp_path):
+    """get_train_loader(args, episodic=False) (pretrain.py:83): batches of batch_size, drop_last,
+    every item the oracle's transform of the remapped pair (no flips here: bit-exact)."""
+    lst = _write_dataset(str(tmp_path), n=9, H=(90, 130))
+    args = dict(image_size=65, mean=MEAN, std=STD, padding=None, augmentations=["resize"], data_root=str(tmp_path),
+                train_list=lst, train_name="pascal", train_split=0, batch_size=2, use_split_coco=False)
+    # the synthetic classes 1..3 are PASCAL split-0 val classes: a split-1 train list holds them
+    args["train_split"] = 1
+    loader, sampler = D.get_train_loader(args, device=dev, episodic=False, return_path=True)
+    assert sampler is None and len(loader) == len(loader.dataset) // 2
+    cl = D.get_split_classes(args)["pascal"][1]["train"]
+    n = 0
+    for images, gt, ipaths, lpaths in loader:
+        assert images.shape == (2, 3, 65, 65) and gt.shape == (2, 65, 65) and gt.dtype == torch.int64
+        for k in range(2):
+            lab = D.standard_label(np.load(lpaths[k]), cl)
+            ref, reft = DO.val_transform(np.load(ipaths[k]), lab, 65, MEAN, STD)
+            np.testing.assert_array_equal(images[k].cpu().numpy(), ref)
+            np.testing.assert_array_equal(gt[k].cpu().numpy(), reft)
+        n += 1
+    assert n == len(loader)

@@ -10,7 +10,12 @@ training-mode BN over a few images is chaotic: the oracle's own gradients move b
 the input (ReLU masks flip and BN over tiny batches amplifies).  So each tensor's bar is
 max(1e-3, 8 x that rounding-level spread of the oracle itself), relative to the tensor's max
 |value|, measured per tensor; the single kernels are pinned tightly on well-conditioned data in
-test_gpu_pretrain_ops.py.  The measured distances are printed."""
+test_gpu_pretrain_ops.py.  The measured distances and the bars are printed.
+
+This whole-step comparison bounds the chain (wiring, kernel order, BN-statistics flow); the
+per-stage parity of the same backward -- each stage recomputed in float64 from the HIP step's own
+inputs, masks and upstream gradient, every gradient at 1e-4 -- is tests/test_gpu_pretrain_chain.py.
+Tensors whose oracle spread is below 1.25e-4 are held to the flat 1e-3 bar here."""
 import numpy as np
 import pytest
 import torch
@@ -65,6 +70,7 @@ def run_case(dev, layers, N, S, nc, drop, steps=2, npert=NPERT):
     b32, b64 = None, None
     h = (S - 1) // 8 + 1
     worst = {}
+    bars = []
     for it in range(steps):
         x, t = make_batch(N, S, nc, SEED + it)
         seed = 1000 + it
@@ -100,6 +106,7 @@ def run_case(dev, layers, N, S, nc, drop, steps=2, npert=NPERT):
                 d = rel(mine, o64)
                 spread = max([rel(o32, o64)] + [rel(p[j][k], o32) for p in perts])
                 bar = max(BAR, 8 * spread)
+                bars.append(bar)
                 worst[what] = max(worst.get(what, 0.0), d)
                 if not d < bar:
                     msgs.append(f"it {it} {what} {k}: {d:.3g} (bar {bar:.3g})")
@@ -112,7 +119,11 @@ def run_case(dev, layers, N, S, nc, drop, steps=2, npert=NPERT):
         assert not msgs, "\n".join(msgs[:20])
         sd32.update(n32)
         sd64.update(n64)
-    print(f"pretrain R{layers} N={N} S={S} nc={nc} drop={drop}: worst rel vs fp64 {worst}")
+    bars = np.array(bars)
+    print(f"pretrain R{layers} N={N} S={S} nc={nc} drop={drop}: worst rel vs fp64 {worst}; bars: "
+          f"{int((bars <= BAR).sum())} at the flat {BAR:g}, {int(((bars > BAR) & (bars <= 1e-2)).sum())} in "
+          f"(1e-3, 1e-2], {int((bars > 1e-2).sum())} above 1e-2 (max {bars.max():.3g}: the oracle's own "
+          f"fp32-vs-fp64 spread x 8)")
 
 
 @pytest.mark.parametrize("layers,N,S,nc,drop", [(50, 4, 65, 16, 0.0), (50, 4, 65, 61, 0.1), (101, 2, 65, 16, 0.0)])

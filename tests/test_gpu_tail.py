@@ -1,0 +1,108 @@
+"""The fused inference tail (test.py:190-204): cwt_attention_infer (F.normalize fused into the single
+token pass, baseline logits W . f_q in the same pass, the CWT with its projections folded per head)
++ cwt_classify_scaled, against the module-by-module kernels it replaces (cwt_normalize,
+cwt_attention_fwd, cwt_classify) and against the oracle (oracle/cwt_oracle.py, pinned by the
+reference's fixtures).  The fused form is the same function re-associated, so the bar is fp32
+rounding: 1e-5 relative.  Also: the folded weights follow every parameter change (load_state_dict,
+the optimiser's step) -- a stale fold would be a silent error."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from few_shot_seg_cwt_amd import synthetic as syn  # noqa: E402
+
+SEED = 2021
+TOL = 1e-5
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def _inputs(dev, B, h, tag):
+    f = torch.from_numpy(syn.normal(3, "tf" + tag, (B, 512, h, h), 1.0)).abs().to(dev)
+    f = f.contiguous(memory_format=torch.channels_last)
+    W = torch.from_numpy(syn.normal(4, "tw" + tag, (B, 2, 512), 0.05)).to(dev)
+    return f, W
+
+
+def _modules(t, W, f):
+    from few_shot_seg_cwt_amd.episode import classify, normalize
+    fqn, pred_q0 = normalize(f, W)
+    W2 = t.infer(W, fqn)
+    return W2, classify(W2, fqn), pred_q0, fqn
+
+
+@pytest.mark.parametrize("B,h", [(1, 60), (1, 81), (2, 60), (4, 33), (3, 9), (1, 2)])
+def test_fused_tail_equals_modules(dev, B, h):
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne
+    from few_shot_seg_cwt_amd.episode import cwt_tail
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    t.eval()
+    f, W = _inputs(dev, B, h, f"{B}_{h}")
+    W2, pq, pq0 = cwt_tail(t, W, f)
+    W2r, pqr, pq0r, fqn = _modules(t, W, f)
+    _, inv, _ = t.infer_raw(W, f, with_logits0=False)
+    torch.cuda.synchronize()
+    fn_fused = f.permute(0, 2, 3, 1).reshape(B, h * h, 512) * inv[..., None]
+    errs = dict(W2=rel(W2, W2r), pred_q=rel(pq, pqr), pred_q0=rel(pq0, pq0r),
+                f_hat=rel(fn_fused, fqn.permute(0, 2, 3, 1).reshape(B, h * h, 512)))
+    print(f"fused tail B={B} h={h}: {errs}")
+    assert max(errs.values()) < TOL, errs
+
+
+def test_fused_tail_vs_oracle(dev):
+    """One 473-shaped tail against the oracle's normalize / cwt_forward / classify (float64)."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne
+    from few_shot_seg_cwt_amd.episode import cwt_tail
+    from oracle import cwt_oracle as O
+    tsd = syn.make_transformer_state(4, 512, SEED)
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(tsd)
+    f, W = _inputs(dev, 1, 60, "or")
+    W2, pq, pq0 = cwt_tail(t, W, f)
+    tsd64 = {k: torch.from_numpy(np.asarray(v, np.float64)) for k, v in tsd.items()}
+    f64, W64 = f.double().cpu().contiguous(), W.double().cpu()
+    with torch.no_grad():
+        fh = O.normalize(f64)
+        W2o = O.cwt_forward(W64, fh, fh, tsd64, 4)
+        pqo = O.classify(W2o, fh)
+        pq0o = O.classify(W64, f64)
+    errs = dict(W2=rel(W2, W2o), pred_q=rel(pq, pqo), pred_q0=rel(pq0, pq0o))
+    print(f"fused tail vs oracle: {errs}")
+    assert max(errs.values()) < 1e-5, errs
+
+
+def test_fold_follows_parameter_changes(dev):
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne
+    from few_shot_seg_cwt_amd.episode import cwt_tail
+    from few_shot_seg_cwt_amd.optimizer import HipSGD
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    f, W = _inputs(dev, 1, 33, "fold")
+    a = cwt_tail(t, W, f)[0].clone()
+    # new parameters through load_state_dict
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED + 1))
+    b = cwt_tail(t, W, f)[0].clone()
+    assert rel(b, _modules(t, W, f)[0]) < TOL and rel(a, b) > 1e-3
+    # an optimiser step writes the parameters in place (a kernel): the fold must follow it
+    t.flat.grad = torch.from_numpy(syn.normal(9, "g", (t.flat.numel(),), 1.0)).to(dev)
+    HipSGD([t.flat], lr=0.05).step()
+    c = cwt_tail(t, W, f)[0].clone()
+    assert rel(c, _modules(t, W, f)[0]) < TOL and rel(b, c) > 1e-4
+    # a second module at a recycled address with the same version number does not hit the cache
+    del t
+    t2 = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t2.load_state_dict(syn.make_transformer_state(4, 512, SEED + 2))
+    assert rel(cwt_tail(t2, W, f)[0], _modules(t2, W, f)[0]) < TOL
