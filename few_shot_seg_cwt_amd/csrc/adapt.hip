@@ -20,6 +20,7 @@
 // accumulators) run in the same launches: grid.z = E * shots.  A step is latency-bound (one
 // dependent launch per SGD step), so E episodes share the ~200 launch boundaries of one.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(ADAPT_T) void adapt_step_kernel(AdaptStepArgs a) {
   __shared__ float gs[2][2][ADAPT_CB + 1];  // double-buffered over tiles
   __shared__ float red[ADAPT_NW][C];
   if (a.dbg & 16) return;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);  // wv: SGPR
   const int cb = blockIdx.x, r = blockIdx.y;
   unsigned long long* stp = nullptr;  // timing study (CWT_ADAPT_DBG & 32): wave 0's clock at each phase
   if (STAMPS && t == 0) {
@@ -744,6 +745,10 @@ __device__ __forceinline__ void pa_labels(int (&y)[2][2], const PersistArgs& a, 
   }
 }
 
+__device__ __forceinline__ unsigned pack_y(const int (&y)[2][2]) {
+  return (unsigned)y[0][0] | ((unsigned)y[0][1] << 8) | ((unsigned)y[1][0] << 16) | ((unsigned)y[1][1] << 24);
+}
+
 // 64-lane reduction of 32 per-lane values (channel j in v[j]) leaving lane L with channel L >> 1:
 // five halving steps, each pairing lanes that differ in one lane bit (the lane with the bit set
 // keeps the upper half of the channels, its partner the lower), then one plain pair sum.
@@ -755,12 +760,8 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
-__device__ __forceinline__ void pa_butterfly(float (&v)[PA_CPW], int lane) {
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j + 16]), false, false);
-    v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
+// bits 4 .. 0 of the butterfly on the 16 values left after the permlane32 step
+__device__ __forceinline__ void pa_butterfly16(float (&v)[PA_CPW], int lane) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[j]), __float_as_uint(v[j + 8]), false, false);
@@ -789,32 +790,78 @@ __device__ __forceinline__ void pa_butterfly(float (&v)[PA_CPW], int lane) {
   }
   v[0] += dpp_mov<0xB1>(v[0]);
 }
+__device__ __forceinline__ void pa_butterfly(float (&v)[PA_CPW], int lane) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j + 16]), false, false);
+    v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  pa_butterfly16(v, lane);
+}
+// The same reduction of 32 values produced on the fly (fv(j): channel j's value): channels j and
+// j + 16 are formed together and enter the permlane32 step at once, so at most 16 of them are
+// live (the three-unit form keeps two units' f in registers beside them)
+template <class FV>
+__device__ __forceinline__ float pa_butterfly_fn(FV fv, int lane) {
+  float v[PA_CPW];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(fv(j)), __float_as_uint(fv(j + 16)), false, false);
+    v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    if (j & 1) asm volatile("" ::: "memory");  // bounds the LDS reads fv may issue ahead (registers)
+  }
+  pa_butterfly16(v, lane);
+  return v[0];
+}
+
+// Per-unit LDS scratch of the lockstep forms: the z partials, and the hi-res pass's per-octet
+// adjoint slots.  Three units (NRES 4) alias them: the z partials are dead (summed into zd)
+// two barriers before the slots are written, and the slots are read before the next step's z.
+template <int NU>
+struct PaScrSep {
+  float zpart[NU][PA_NW][PA_NPX];
+  float P0[NU][8][2][PA_NC + 1];
+  float P1[NU][8][2][PA_NC + 1];
+};
+template <int NU>
+struct PaScrAlias {
+  union {
+    float zpart[NU][PA_NW][PA_NPX];
+    struct {
+      float P0[NU][8][2][PA_NC + 1];
+      float P1[NU][8][2][PA_NC + 1];
+    };
+  };
+};
 
 // STAMPS (CWT_ADAPT_DBG & 32, a separate instantiation; never the timed one): thread 0 records
 // s_memtime at 8 points of every step, realtime at its arrival ([8]) and when its poll matched
 // ([9]) into stamps[step][g][10], and realtime/memtime at entry and exit into
 // stamps[iters][g][0..3] (tools/persist_stamps.py).
 // NRES 1: one unit per workgroup, its f in registers; 2: up to two units per workgroup, the
-// first in registers, the second in LDS (128 KB, lane-major: conflict-free); 3: units streamed
+// first in registers, the second in LDS (128 KB, lane-major: conflict-free); 4: up to three
+// units in lockstep, the first and third in registers, the second in LDS; 3: units streamed
 // every step, each wave's slice by LDS-DMA into its private 8 KB while the previous unit is
 // computed; 0: units streamed from L2 into registers (opt-in, slower).  Fewer workgroups make each step's barrier cheaper and leave CUs to the
 // next episode's extractor pass (EpisodePipeline).
 template <int NRES, bool STAMPS = false>
 __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsigned long long* stamps = nullptr) {
   constexpr int C = 512;
-  constexpr int EWK = (NRES == 2 || NRES == 3) ? 2 : NRES == 1 ? 1 : PA_EW;  // episodes a workgroup's units may span
-  __shared__ float fl2[NRES == 2 ? PA_NW : 1][PA_CPW][NRES == 2 ? 64 : 1];
+  constexpr int EWK = (NRES >= 2) ? 2 : NRES == 1 ? 1 : PA_EW;  // episodes a workgroup's units may span
+  constexpr bool LOCK = NRES == 2 || NRES == 4;  // units in lockstep, the second one's f in fl2
+  __shared__ float fl2[LOCK ? PA_NW : 1][PA_CPW][LOCK ? 64 : 1];
   __shared__ __attribute__((aligned(16))) float fs3[NRES == 3 ? PA_NW * 64 * PA_CPW : 4];  // NRES 3: per-wave f slices
   __shared__ float dlw[PA_NW][EWK][PA_CPW];     // d = W1 - W0 of each wave's channels (wave-private)
   __shared__ float wlw[PA_NW][EWK][2][PA_CPW];  // W0, W1 of each wave's channels (wave-private)
   // NRES 2 runs its two units in lockstep (one set of LDS barriers, one butterfly and one set
   // of atomics per step when both units belong to one episode): the second unit's copies [1]
-  constexpr int NU = NRES == 2 ? 2 : 1;
-  __shared__ float zpart_u[NU][PA_NW][PA_NPX];
+  constexpr int NU = NRES == 2 ? 2 : NRES == 4 ? 3 : 1;
+  __shared__ std::conditional_t<NRES == 4, PaScrAlias<NU>, PaScrSep<NU>> scr;
+  auto& zpart_u = scr.zpart;
+  auto& P0_u = scr.P0;
+  auto& P1_u = scr.P1;
   __shared__ float zd_u[NU][PA_NPX];
   __shared__ float gs_u[NU][PA_NPX];
-  __shared__ float P0_u[NU][8][2][PA_NC + 1];
-  __shared__ float P1_u[NU][8][2][PA_NC + 1];
   auto& zpart = zpart_u[0];
   auto& zd = zd_u[0];
   auto& gs = gs_u[0];
@@ -822,7 +869,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
   auto& P1 = P1_u[0];
   __shared__ float wfg_l[EWK], lr_l[EWK];
   __shared__ int abort_flag;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);  // wv: SGPR
   const int g = blockIdx.x, G = a.G;
   const int u0 = (int)(((long)g * a.units) / G), u1 = (int)(((long)(g + 1) * a.units) / G);
   const int per_ep = a.nshot * a.ntile;
@@ -867,12 +914,23 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
   } else {
     pa_load(cur, a, q, wv, lane);
   }
-  int y2[2][2] = {{255, 255}, {255, 255}};  // NRES 2: labels of the second unit (its f is in fl2)
-  if (NRES == 2 && u1 - u0 == 1) {  // no second unit: its f reads as zero in the lockstep dW pass
+  int y2[2][2] = {{255, 255}, {255, 255}};  // NRES 2 / 4: labels of the second unit (its f is in fl2)
+  if (LOCK && u1 - u0 == 1) {  // no second unit: its f reads as zero in the lockstep dW pass
 #pragma unroll
     for (int j = 0; j < PA_CPW; ++j) fl2[wv][j][lane] = 0.f;
   }
-  if (NRES == 2 && u1 - u0 > 1) {
+  PaTile cur2;  // NRES 4: the third unit (registers); zero when the workgroup has fewer
+  if (NRES == 4) {
+    if (u1 - u0 > 2) {
+      pa_load(cur2, a, pa_unit(a, u0 + 2), wv, lane);
+    } else {
+#pragma unroll
+      for (int j = 0; j < PA_CPW; ++j) cur2.fr[j] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) cur2.y[k][0] = cur2.y[k][1] = 255;
+    }
+  }
+  if (LOCK && u1 - u0 > 1) {
     PaTile tmp;
     pa_load(tmp, a, pa_unit(a, u0 + 1), wv, lane);
 #pragma unroll
@@ -883,11 +941,21 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       y2[k][1] = tmp.y[k][1];
     }
   }
+  // NRES 4: the three units' labels one byte each (unit A's f stays in cur.fr)
+  const unsigned yap = pack_y(cur.y), ycp = pack_y(cur2.y);
+  const unsigned y2p = pack_y(y2);
   __syncthreads();
 
   const int i_row = wv >> 1;
   const float ly1 = (float)i_row * 0.125f, ly0 = 1.f - ly1;
   for (int s = 0; s < a.iters; ++s) {
+    // an opaque copy of the thread id per step: lane-dependent addresses and label decodes are
+    // recomputed (a few VALU ops) instead of being hoisted out of the 200-step loop, where they
+    // would hold registers the lockstep forms need for f (or be spilled to scratch)
+    int t_op = (int)threadIdx.x;
+    if constexpr (NRES >= 2) asm volatile("" : "+v"(t_op));  // (NRES 1 has the registers: hoisting wins)
+    const int t = t_op, lane = t_op & 63;
+    const int cw = wv * PA_CPW + (lane & 31);
     const int slot = s % PA_NSLOT;
     unsigned long long* stp = (STAMPS && t == 0) ? stamps + ((long)s * G + g) * 10 : nullptr;
     auto stamp = [&](int i) {
@@ -1022,15 +1090,20 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
     };
     // NRES 2 with two units: both units' phases share the barriers; lane p holds pixel p of
     // each unit (unit A's f in registers, unit B's in fl2), LDS copies [0] / [1]
-    auto hires_pass = [&](const PaUnit& q, int ew, const int (&ylab)[2][2], const float* zdp, float (*P0p)[2][PA_NC + 1],
+    // ylab: the lane's four labels packed one per byte (k * 2 + e2).  The lane-dependent geometry
+    // is derived from an opaque copy of the lane id, so it is recomputed every step instead of
+    // being hoisted out of the 200-step loop into registers the lockstep forms do not have
+    auto hires_pass = [&](const PaUnit& q, int ew, unsigned ylab, const float* zdp, float (*P0p)[2][PA_NC + 1],
                           float (*P1p)[2][PA_NC + 1]) {
       const bool has_extra = q.extra_row && i_row == 0;
       const float wf = wfg_l[ew];
+      int ln = lane;
+      asm volatile("" : "+v"(ln), "+v"(ylab));
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         if (k == 1 && a.uc < 16) break;
-        const int X = 8 * q.x0 + 64 * (wv & 1) + 128 * k + lane;
-        const int slot_x = 8 * (wv & 1) + 16 * k + (lane >> 3);
+        const int X = 8 * q.x0 + 64 * (wv & 1) + 128 * k + ln;
+        const int slot_x = 8 * (wv & 1) + 16 * k + (ln >> 3);
         const int ix = min(X >> 3, a.w - 1);
         const int xi0 = min(ix - q.x0, PA_NC - 1);
         const int xi1 = (ix < a.w - 1) ? min(xi0 + 1, PA_NC - 1) : xi0;
@@ -1039,7 +1112,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
 #pragma unroll
         for (int e2 = 0; e2 < 2; ++e2) {
           if (e2 == 1 && !has_extra) break;
-          const int y = ylab[k][e2];
+          const int y = (int)((ylab >> (8 * (2 * k + e2))) & 255u);
           float gv = 0.f;
           if (y != 255) {
             const float dd = e2 ? (lx0 * zdp[PA_NC + xi0] + lx1 * zdp[PA_NC + xi1])
@@ -1102,8 +1175,8 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       }
       lds_barrier();
       stamp(1);
-      hires_pass(qa, ewa, cur.y, zd_u[0], P0_u[0], P1_u[0]);
-      if (has_b) hires_pass(qb, ewb, y2, zd_u[NU - 1], P0_u[NU - 1], P1_u[NU - 1]);
+      hires_pass(qa, ewa, pack_y(cur.y), zd_u[0], P0_u[0], P1_u[0]);
+      if (has_b) hires_pass(qb, ewb, y2p, zd_u[NU - 1], P0_u[NU - 1], P1_u[NU - 1]);
       lds_barrier();
       if (t < 2 * PA_NPX) {
         const int uu = t >> 6, tt = t & 63;
@@ -1146,9 +1219,75 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
         }
       }
     };
+    // NRES 4: three units in lockstep (A = u0 and C = u0 + 2 in registers, B = u0 + 1 in fl2),
+    // one set of LDS barriers; units of one episode share one butterfly and one set of atomics
+    auto triple_body = [&](int nb) {
+      const PaUnit qa = pa_unit(a, u0);
+      const PaUnit qb = pa_unit(a, nb > 1 ? u0 + 1 : u0);
+      const PaUnit qc = pa_unit(a, nb > 2 ? u0 + 2 : u0);
+      const int ewa = qa.e - e_lo, ewb = qb.e - e_lo, ewc = qc.e - e_lo;
+      {
+        float sda = 0.f, sdb = 0.f, sdc = 0.f;
+#pragma unroll
+        for (int j = 0; j < PA_CPW / 4; ++j) {
+          const f32x4 da = *(const f32x4*)&dlw[wv][ewa][4 * j];
+          const f32x4 db = *(const f32x4*)&dlw[wv][ewb][4 * j];
+          const f32x4 dc = *(const f32x4*)&dlw[wv][ewc][4 * j];
+          float fb[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) fb[r] = fl2[wv][4 * j + r][lane];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            sda = fmaf(da[r], cur.fr[4 * j + r], sda);
+            sdb = fmaf(db[r], fb[r], sdb);
+            sdc = fmaf(dc[r], cur2.fr[4 * j + r], sdc);
+          }
+          if (j & 1) asm volatile("" ::: "memory");
+        }
+        zpart_u[0][wv][lane] = sda;
+        zpart_u[1][wv][lane] = sdb;
+        zpart_u[NU - 1][wv][lane] = sdc;
+      }
+      lds_barrier();
+      if (t < NU * PA_NPX) {
+        const int uu = t >> 6, tt = t & 63;
+        float z = 0.f;
+#pragma unroll
+        for (int v = 0; v < PA_NW; ++v) z += zpart_u[uu][v][tt];
+        zd_u[uu][tt] = z;
+      }
+      lds_barrier();
+      stamp(1);
+      hires_pass(qa, ewa, yap, zd_u[0], P0_u[0], P1_u[0]);
+      if (nb > 1) hires_pass(qb, ewb, y2p, zd_u[1], P0_u[1], P1_u[1]);
+      if (nb > 2) hires_pass(qc, ewc, ycp, zd_u[NU - 1], P0_u[NU - 1], P1_u[NU - 1]);
+      lds_barrier();
+      if (t < NU * PA_NPX) {
+        const int uu = t >> 6, tt = t & 63;
+        gs_u[uu][tt] = gs_of(tt, P0_u[uu], P1_u[uu]);
+      }
+      lds_barrier();
+      stamp(2);
+      const float ga = gs_u[0][lane], gb = nb > 1 ? gs_u[1][lane] : 0.f, gc = nb > 2 ? gs_u[NU - 1][lane] : 0.f;
+      // consecutive units: qa.e <= qb.e <= qc.e, at most two episodes (span <= 2, host-checked)
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        const int e = pass ? qc.e : qa.e;
+        if (pass && qc.e == qa.e) break;
+        const float ma = qa.e == e ? ga : 0.f, mb = qb.e == e ? gb : 0.f, mc = qc.e == e ? gc : 0.f;
+        const float dsum = pa_butterfly_fn(
+            [&](int j) { return fmaf(mc, cur2.fr[j], fmaf(mb, fl2[wv][j][lane], ma * cur.fr[j])); }, lane);
+        if ((lane & 1) == 0)
+          __hip_atomic_fetch_add(a.acc + (long)e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C + wv * PA_CPW +
+                                     (lane >> 1),
+                                 dsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    };
     if (a.floor_only) {
       // timing study: no unit work (NRES 3 still drains its in-flight DMA)
       if (NRES == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (NRES == 4) {
+      triple_body(u1 - u0);
     } else if constexpr (NRES == 2) {
       const bool has_b = u1 - u0 == 2;
       pair_body(q, has_b ? pa_unit(a, u0 + 1) : q, has_b);
@@ -1310,7 +1449,7 @@ static int persist_geometry(int E, int n, int h, int w, int upw_pref, int* G_out
   // that takes at most half the CUs (1-shot 473^2: 118 workgroups) and 2 beyond
   const char* upws = getenv("CWT_ADAPT_UPW");
   const int upw = upw_pref ? upw_pref : upws ? (atoi(upws) == 1 ? 1 : 2) : (units <= g_cu_count / 2 ? 1 : 2);
-  const int G = (int)std::min<long>((units + upw - 1) / upw, g_cu_count);
+  int G = (int)std::min<long>((units + upw - 1) / upw, g_cu_count);
   const long k = (units + G - 1) / G;  // units per workgroup (max)
   const long per_ep = (long)n * ntile;
   const long span = (k - 1 + per_ep - 1) / per_ep + 1;  // episodes a workgroup's range can touch
@@ -1321,9 +1460,17 @@ static int persist_geometry(int E, int n, int h, int w, int upw_pref, int* G_out
   // CWT_ADAPT_STREAM=0 disables it, =1 allows it from k = 3.
   const char* sts = getenv("CWT_ADAPT_STREAM");
   const int stream_from = sts ? (sts[0] == '0' ? 1 << 30 : 3) : 4;
-  int nres = k == 1 ? 1 : (k == 2 && span <= 2) ? 2 : 0;
+  // k = 3 (5-shot 473^2: 590 units on 197 workgroups): three units in lockstep, two in
+  // registers and one in LDS (nres 4); CWT_ADAPT_LOCK3=0 returns it to the step launches
+  const char* l3s = getenv("CWT_ADAPT_LOCK3");
+  const bool lock3 = !(l3s && l3s[0] == '0');
+  int nres = k == 1 ? 1 : (k == 2 && span <= 2) ? 2 : (k == 3 && span <= 2 && lock3) ? 4 : 0;
   if (nres == 0 && k >= stream_from && span <= 2) nres = 3;
-  if (span > (nres == 2 || nres == 3 ? 2 : PA_EW)) return 1;
+  if (span > (nres >= 2 ? 2 : PA_EW)) return 1;
+  // three units per workgroup: as few workgroups as that takes (5-shot 473^2: 197, not 256 with
+  // two or three units each -- the step waits for the three-unit ones either way, and fewer
+  // workgroups make the barrier cheaper and leave CUs free)
+  if (nres == 4) G = (int)((units + 2) / 3);
   *G_out = G;
   *units_out = (int)units;
   *ncb_out = ncb;
@@ -1376,7 +1523,9 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
       CWT_HIP(hipMalloc(&g_adapt_stamps, n_st * sizeof(unsigned long long)));
       g_adapt_stamps_n = n_st;
     }
-    if (nres == 3)
+    if (nres == 4)
+      hipLaunchKernelGGL((adapt_persist_kernel<4, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
+    else if (nres == 3)
       hipLaunchKernelGGL((adapt_persist_kernel<3, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
     else if (nres == 1)
       hipLaunchKernelGGL((adapt_persist_kernel<1, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
@@ -1384,6 +1533,8 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
       hipLaunchKernelGGL((adapt_persist_kernel<2, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
     else
       hipLaunchKernelGGL((adapt_persist_kernel<0, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
+  } else if (nres == 4) {
+    hipLaunchKernelGGL((adapt_persist_kernel<4, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
   } else if (nres == 3) {
     hipLaunchKernelGGL((adapt_persist_kernel<3, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
   } else if (nres == 1) {
@@ -1419,9 +1570,9 @@ const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw) {
   int pG = 0, punits = 0, pncb = 0, pnres = 0, puc = 0;
   const char* pe = getenv("CWT_ADAPT_PERSIST");
   if (iters > 0 && !(pe && pe[0] == '0') && persist_geometry(E, n, h, w, upw, &pG, &punits, &pncb, &pnres, &puc) == 0) {
-    static const char* names[4] = {"adapt_persist_kernel<0", "adapt_persist_kernel<1", "adapt_persist_kernel<2",
-                                   "adapt_persist_kernel<3"};
-    return names[pnres & 3];
+    static const char* names[5] = {"adapt_persist_kernel<0", "adapt_persist_kernel<1", "adapt_persist_kernel<2",
+                                   "adapt_persist_kernel<3", "adapt_persist_kernel<4"};
+    return names[pnres <= 4 ? pnres : 0];
   }
   return "adapt_step_kernel<";
 }

@@ -1371,10 +1371,8 @@ static int debug_conv_s(cwt_ctx* ctx, int prec, const void* xs, int N, int Hi, i
     CWT_CHECK((bm == 256 && (bn == 256 || bn == 128)) || (bm == 128 && (bn == 256 || bn == 128 || bn == 64)) ||
                   (bm == 64 && (bn == 128 || bn == 64)),
               "tile must be one of 256x256, 256x128, 128x256, 128x128, 128x64, 64x128, 64x64");
-    CWT_CHECK((var >= 0 && var <= 2) || (var == 4 && bm == 128 && bn == 128) || (var >= 8 && var <= 11) ||
-                  (var >= 16 && var <= 19 && !(bm == 256 && bn == 256)),
-              "variant must be 0, 1, 2, 4 (128x128 only), 8 .. 11 (timing study) or 16 .. 19 (register-staged, "
-              "not 256x256)");
+    CWT_CHECK((var >= 0 && var <= 2) || (var == 4 && bm == 128 && bn == 128) || (var >= 8 && var <= 11),
+              "variant must be 0, 1, 2, 4 (128x128 only) or 8 .. 11 (timing study)");
     if (var >= 8 && var <= 11) {  // the timing-study kernels have fixed tiles: the grid must be theirs
       bm = bn = var < 10 ? 64 : 128;
     }

@@ -149,15 +149,9 @@ __device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, co
 // that publishes it, BEFORE the MFMAs of tile t, so their LDS latency hides under the MFMAs;
 // the slot tile t occupied is refilled (tile t + NSTG) as soon as every wave has passed that
 // barrier, so the ring keeps NSTG - 1 tiles in flight either way.
-// RS > 0: register-staged operand loads instead of LDS-DMA.  Each wave moves its pieces of a
-// K-tile HBM/L2 -> VGPRs by global_load_dwordx4 (same 16-B chunks, same swizzled source
-// addresses as the DMA) and then ds_write_b128s them into a 2-slot LDS ring (the same image), RS
-// tiles in flight in RS register sets.  One barrier per K-tile: MFMAs of tile t (slot t&1) ->
-// the compiler's counted vmcnt wait for tile t+1's registers -> ds_write into slot (t+1)&1 (its
-// readers passed the previous barrier) -> loads of tile t+1+RS into the freed set -> barrier.
-// tools/intake_bench.hip measured the L2 -> CU intake of this form at 89-95 GB/s per CU with two
-// workgroups per CU against 56-70 for LDS-DMA.
-template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF = 0, int RS = 0>
+// PF bits: 1 fragment prefetch; 2 / 4 timing studies (no MFMAs / no operand DMA); 8 buffer
+// addressing of the operand DMA (every production instantiation sets it).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF>
 __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   static_assert(PREC == 1 || PREC == 3, "PREC: 3 = bf16x3 over the S-layout, 1 = plain bf16");
   constexpr int NW = WAVES_M * WAVES_N;
@@ -168,7 +162,6 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   constexpr int STG_BYTES = (BM + BN) * 128;
   static_assert(LA * 8 * NW == BM && LB * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
   static_assert(NSTG >= 2 && NSTG <= 6, "ring depth");
-  static_assert(RS == 0 || NSTG == 2, "the register-staged form uses a 2-slot LDS ring");
   constexpr int EP_ROWS = WM < 32 ? WM : 32;
   constexpr int EP_LD = WN + 4;  // floats per row of a wave's epilogue tile
   constexpr int EP_BYTES = NW * EP_ROWS * EP_LD * 4;
@@ -228,9 +221,54 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
     i_kx = tap - i_ky * a.kw;
   }
   int i_kt = kt_begin;
+  // PF & 8: buffer addressing (buffer_load_dwordx4 ... lds).  A piece's 32-bit byte offset is its
+  // row's constant part plus ONE uniform per-tap / per-channel-block term; an out-of-image tap or
+  // a row past M gets an offset past the buffer's end, which the hardware reads as zeros (no zero
+  // line, no 64-bit address math, no exec-masked branch per piece).  The weights' K offset goes in
+  // the uniform soffset.
+  __amdgpu_buffer_rsrc_t rsA, rsB;
+  int a_roff[LA], b_voff[LB];
+#if defined(__HIP_DEVICE_COMPILE__)  // the buffer builtins exist for the device pass only
+  if constexpr ((PF & 8) != 0) {
+    const int cbl = a.Ci >> (PREC == 1 ? 6 : 5);
+    const long a_bytes = (long)a.N * a.Hi * a.Wi * cbl * 128;
+    rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.xs, (short)0, (int)a_bytes, 0x00020000);
+    rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.ws, (short)0, (int)((long)a.Co * a.ktiles_total * 128), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < LA; ++j) a_roff[j] = (a_pix0[j] * cbl * 64 + a_ch[j]) * 2;
+#pragma unroll
+    for (int j = 0; j < LB; ++j) b_voff[j] = b_off[j] * 2;
+  }
+#endif
   auto issue = [&](int stg) {
     if (PF & 4) return;  // timing study: no operand traffic
     char* sb = smem + stg * STG_BYTES;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr ((PF & 8) != 0) {
+      const int dy = i_ky * a.dil, dx = i_kx * a.dil;
+      const int uni = ((dy * a.Wi + dx) * cblocks + i_cb) * 128;
+#pragma unroll
+      for (int j = 0; j < LA; ++j) {
+        const int ih = a_ih0[j] + dy, iw = a_iw0[j] + dx;
+        const bool in = (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (CWT_LDS void*)(sb + (wv * LA + j) * 1024), 16,
+                                                 in ? a_roff[j] + uni : (int)0x80000000, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < LB; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (CWT_LDS void*)(sb + BM * 128 + (wv * LB + j) * 1024), 16,
+                                                 b_voff[j], i_kt * 128, 0, 0);
+      ++i_kt;
+      if (++i_kx == a.kw) {
+        i_kx = 0;
+        if (++i_ky == a.kh) {
+          i_ky = 0;
+          ++i_cb;
+        }
+      }
+      return;
+    }
+#endif
     const int dy = i_ky * a.dil, dx = i_kx * a.dil;
     const int shift = dy * a.Wi + dx;
 #pragma unroll
@@ -306,70 +344,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       }
   };
 
-  if constexpr (RS > 0) {
-    f32x4 ra[RS][LA > 0 ? LA : 1], rb[RS][LB];
-    // global loads of the next K-tile (i_kt) into register set SET (compile-time index).  Past the
-    // split's last K-tile the loads read the zero line instead: every step of the steady-state
-    // loop then loads unconditionally, which lets the compiler count exactly RS-1 younger tiles
-    // at each wait (a conditional load makes its waitcnt pass assume the worst: vmcnt(LPT-1))
-    auto load = [&](auto setc) {
-      constexpr int SET = decltype(setc)::value;
-      const bool live = i_kt < kt_end;
-      const int dy = i_ky * a.dil, dx = i_kx * a.dil;
-      const int shift = dy * a.Wi + dx;
-#pragma unroll
-      for (int j = 0; j < LA; ++j) {
-        const int ih = a_ih0[j] + dy, iw = a_iw0[j] + dx;
-        const bool in = live && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
-        const __bf16* src = in ? a.xs + ((a_pix0[j] + shift) * cblocks + i_cb) * 64 + a_ch[j] : a.zero;
-        ra[SET][j] = *(const f32x4*)src;
-      }
-#pragma unroll
-      for (int j = 0; j < LB; ++j) rb[SET][j] = *(const f32x4*)(live ? a.ws + b_off[j] + i_kt * 64 : a.zero);
-      ++i_kt;
-      if (++i_kx == a.kw) {
-        i_kx = 0;
-        if (++i_ky == a.kh) {
-          i_ky = 0;
-          ++i_cb;
-        }
-      }
-    };
-    auto store = [&](auto setc, int stg) {
-      constexpr int SET = decltype(setc)::value;
-      char* sb = smem + stg * STG_BYTES;
-#pragma unroll
-      for (int j = 0; j < LA; ++j) *(f32x4*)(sb + (wv * LA + j) * 1024 + lane * 16) = ra[SET][j];
-#pragma unroll
-      for (int j = 0; j < LB; ++j) *(f32x4*)(sb + BM * 128 + (wv * LB + j) * 1024 + lane * 16) = rb[SET][j];
-    };
-    // prologue: tiles 0 .. RS-1 into sets 0 .. RS-1; tile 0 -> slot 0; tile RS into set 0
-    [&]<int... I>(std::integer_sequence<int, I...>) {
-      (load(std::integral_constant<int, I>{}), ...);
-    }(std::make_integer_sequence<int, RS>{});
-    store(std::integral_constant<int, 0>{}, 0);
-    load(std::integral_constant<int, 0>{});
-    block_sync_lds();
-    // step t: MFMAs of tile t (slot t & 1), tile t+1 (set (t+1) % RS, compile-time: the loop is
-    // unrolled RS-fold) into slot (t+1) & 1, tile t+1+RS into that set, barrier
-    auto step = [&](int t, auto s1c) {
-      Frags F;
-      read_frags(F, t & 1);
-      mfmas(F);
-      store(s1c, (t + 1) & 1);
-      load(s1c);
-      block_sync_lds();
-    };
-    int t0 = 0;
-    for (; t0 + RS <= T; t0 += RS) {
-      [&]<int... I>(std::integer_sequence<int, I...>) {
-        (step(t0 + I, std::integral_constant<int, (I + 1) % RS>{}), ...);
-      }(std::make_integer_sequence<int, RS>{});
-    }
-    [&]<int... I>(std::integer_sequence<int, I...>) {  // the last T % RS tiles
-      ((t0 + I < T ? step(t0 + I, std::integral_constant<int, (I + 1) % RS>{}) : void()), ...);
-    }(std::make_integer_sequence<int, RS - 1>{});
-  } else if ((PF & 1) == 0) {
+  if constexpr ((PF & 1) == 0) {
 #pragma unroll
     for (int s = 0; s < NSTG - 1; ++s)
       if (s < T) issue(s);
@@ -474,13 +449,13 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
 }
 
 // STAGE only names the instantiation (rocprofv3 reports the conv stack by stage).
-template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0, int RS = 0>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArgs a) {
-  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 3, PF, RS>(a);
+  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 3, (PF | 8)>(a);
 }
-template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0, int RS = 0>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_b16(ConvSArgs a) {
-  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 1, PF, RS>(a);
+  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 1, (PF | 8)>(a);
 }
 
 // Split-K reduction (fixed order, deterministic) + the same epilogue math.
@@ -582,44 +557,10 @@ int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipSt
 // workgroups per CU).  Deeper rings (one workgroup per CU, 4-5 tiles in flight) measured no
 // faster: a workgroup's LDS-DMA intake, not its bytes in flight, is the limit.  256x256 has no PF form: its second fragment
 // set does not fit the 256 VGPRs of a wave at two waves per SIMD.
-// Register-staged variants (var 16-19; timing sweep first, stage 0 only)
-#define CWT_RS_LAUNCH(KERNEL)                                                                                    \
-  template <int RS, int W8>                                                                                  \
-  static void launch_rs2_##KERNEL(const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {        \
-    constexpr int T = W8 ? 512 : 256;                                                                        \
-    if (p.bm == 256 && p.bn == 128)                                                                          \
-      hipLaunchKernelGGL((KERNEL<256, 128, 4, 2, 2, 0, 0, RS>), grid, dim3(512), 0, st, a);                   \
-    else if (p.bm == 128 && p.bn == 256)                                                                     \
-      hipLaunchKernelGGL((KERNEL<128, 256, 2, 4, 2, 0, 0, RS>), grid, dim3(512), 0, st, a);                   \
-    else if (p.bm == 128 && p.bn == 128)                                                                     \
-      hipLaunchKernelGGL((KERNEL<128, 128, 2, W8 ? 4 : 2, 2, 0, 0, RS>), grid, dim3(T), 0, st, a);            \
-    else if (p.bm == 128 && p.bn == 64)                                                                      \
-      hipLaunchKernelGGL((KERNEL<128, 64, W8 ? 4 : 2, 2, 2, 0, 0, RS>), grid, dim3(T), 0, st, a);             \
-    else if (p.bm == 64 && p.bn == 128)                                                                      \
-      hipLaunchKernelGGL((KERNEL<64, 128, 2, W8 ? 4 : 2, 2, 0, 0, RS>), grid, dim3(T), 0, st, a);             \
-    else                                                                                                     \
-      hipLaunchKernelGGL((KERNEL<64, 64, 2, W8 ? 4 : 2, 2, 0, 0, RS>), grid, dim3(T), 0, st, a);              \
-  }                                                                                                          \
-  static void launch_rs_##KERNEL(const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {         \
-    switch (p.var) {                                                                                         \
-      case 16: launch_rs2_##KERNEL<2, 0>(a, p, grid, st); break;                                             \
-      case 17: launch_rs2_##KERNEL<3, 0>(a, p, grid, st); break;                                             \
-      case 18: launch_rs2_##KERNEL<2, 1>(a, p, grid, st); break;                                             \
-      default: launch_rs2_##KERNEL<3, 1>(a, p, grid, st); break;                                             \
-    }                                                                                                        \
-  }
-CWT_RS_LAUNCH(conv_igemm_x3s)
-CWT_RS_LAUNCH(conv_igemm_b16)
-#undef CWT_RS_LAUNCH
-
 #define CWT_TILE_LAUNCH(KERNEL)                                                                                  \
   template <int STAGE>                                                                                       \
   static void launch_tiles_##KERNEL(const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {      \
     const int v = p.var;                                                                                     \
-    if (v >= 16) { /* register-staged operand loads: 16/17 RS 2/3 with the base waves, 18/19 8 waves      */ \
-      if constexpr (STAGE == 0) launch_rs_##KERNEL(a, p, grid, st);                                          \
-      return;                                                                                                \
-    }                                                                                                        \
     if (v >= 8) { /* timing study (cwt_debug_conv_s only): 8/9 base 64x64 w/o MFMA / w/o DMA,            */ \
       /* 10/11 the 8-wave prefetch 128x128 w/o MFMA / w/o DMA                                              */ \
       if (v == 8) hipLaunchKernelGGL((KERNEL<64, 64, 2, 2, 4, 0, 2>), grid, dim3(256), 0, st, a);           \

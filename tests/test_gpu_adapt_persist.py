@@ -54,7 +54,8 @@ def _run(persist, f, lbl, W0, iters, uc=None, upw=None, stream=None):
 @pytest.mark.parametrize("E,n,S,iters,uc", [
     (1, 1, 473, 200, None),  # config #2: 236 15-column units, one per workgroup (f resident in registers)
     (1, 1, 473, 200, "31"),  # ... as 118 31-column units
-    (1, 5, 473, 200, None),  # config #3: 590 units over 256 workgroups (streamed)
+    (1, 5, 473, 200, None),  # config #3: 590 units, three per workgroup in lockstep (197 workgroups)
+    (8, 5, 129, 20, None),   # 640 units, three per workgroup, workgroups spanning two episodes
     (1, 1, 641, 200, None),  # config #4 shapes: 240 units
     (1, 5, 641, 50, None),   # config #5 shapes: 1200 units
     (4, 1, 473, 50, None),   # episodes in flight: workgroups span two episodes

@@ -93,11 +93,7 @@ PLANS = [(0, 0, 0), (256, 256, 1), (256, 128, 1), (128, 256, 1), (128, 256, 2), 
          # 4 = 128x128 with a 2-stage ring
          (1064, 64, 1), (1064, 64, 3), (1128, 128, 1), (1128, 64, 2), (1064, 128, 1), (1128, 256, 1), (1256, 128, 2),
          (2064, 64, 1), (2064, 64, 2), (2128, 128, 1), (2128, 128, 3), (2128, 64, 1), (2064, 128, 1),
-         (4128, 128, 1), (4128, 128, 3),
-         # register-staged operand loads (16/17: 2/3 register sets, base waves; 18/19: 8 waves)
-         (16064, 64, 1), (16064, 64, 3), (17064, 64, 1), (17128, 128, 2), (16128, 256, 1), (17256, 128, 1),
-         (16064, 128, 1), (17128, 64, 1), (18064, 64, 1), (18128, 128, 2), (19064, 64, 3), (19128, 64, 1),
-         (19064, 128, 1), (16128, 128, 1)]
+         (4128, 128, 1), (4128, 128, 3)]
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))

@@ -114,16 +114,13 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
                     continue
                 tiles = -(-M // bm) * (Co // bn)
                 for var in variants:
-                    if var >= 16:   # register-staged forms: not 256x256; 18/19 (8 waves) only below 256 rows/cols
-                        if (bm, bn) == (256, 256) or (var >= 18 and (bm == 256 or bn == 256)):
-                            continue
-                    elif var and bm == 256 and bn == 256:
+                    if var and bm == 256 and bn == 256:
                         continue   # no prefetch form of 256x256
                     if var == 4 and (bm, bn) != (128, 128):
                         continue   # two-workgroups-per-CU 128x128 form
-                    if 8 <= var < 16 and (bm, bn) != ((64, 64) if var < 10 else (128, 128)):
+                    if var >= 8 and (bm, bn) != ((64, 64) if var < 10 else (128, 128)):
                         continue   # timing-study kernels: fixed tiles
-                    if 2 <= var < 16 and (bm == 256 or bn == 256):
+                    if var >= 2 and (bm == 256 or bn == 256):
                         continue   # 8-wave form only for the 128/64 tiles
                     for ns in (1, 2, 4, 8):
                         if ns > 1 and ((K // (64 if prec == 1 else 32)) // ns < 4 or tiles * ns > 4096):
