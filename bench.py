@@ -168,58 +168,29 @@ def reference_cwt_flops(hw: int, heads: int = 4, C: int = 512) -> float:
     return 2.0 * (2 + 2 * hw) * C * C * heads + 2.0 * 2 * 2 * hw * C * heads + 2.0 * 2 * C * heads * C
 
 
-EXTRACT_LAUNCHES = ("conv_igemm", "stem_conv1", "maxpool", "ppm_")
-
-
-def event_overhead_ms(fine, extract_ms_clean):
-    """Per-launch cost of the level-2 event pairs themselves: the per-launch episode's
-    extract_features bracket minus the same bracket timed without per-launch events (profile
-    level 1, sequential leg), spread over the extract's bracketed launches."""
-    if not extract_ms_clean:
-        return None
-    i0 = next((i for i, r in enumerate(fine) if r[0].startswith("extract_features")), None)
-    if i0 is None:
-        return None
-    inner = []
-    for r in fine[i0 + 1:]:
-        if not r[0].startswith(EXTRACT_LAUNCHES):
-            break
-        inner.append(r)
-    if not inner:
-        return None
-    return max(0.0, (fine[i0][3] - extract_ms_clean) / len(inner))
-
-
-def conv_roofline(fine, peak_tflops, extract_ms_clean=None):
+def conv_roofline(fine, peak_tflops):
     """Per-conv roofline of the stack from one episode's per-launch records (profile level 2):
     each conv launch's bound is max(flops / MFMA peak, algorithmic bytes / HBM peak) (bytes =
     input + weights + output [+ residual], each once: 4 B per element for fp32 / the bf16x3
     S-layout, 2 B for the bf16 stack);
     roofline_frac = sum of bounds / sum of measured launch times (1.0 = every conv at its roof).
-    Each launch's time carries the cost of its own event pair (~2-4 us against 10-90 us convs);
-    roofline_frac subtracts that cost, measured as event_overhead_ms, and roofline_frac_raw keeps
-    the uncorrected per-launch times (rocprofv3's kernel durations, profiles/, agree with the
-    corrected ones)."""
+    The per-launch event pairs cost time BETWEEN the brackets (the level-2 extract bracket is
+    ~0.5 ms longer than the level-1 one), not inside them: rocprofv3's kernel durations for the
+    same stack sum to within ~4 % of conv_kernel_ms (profiles/r3)."""
     convs = [r for r in fine if r[0].startswith("conv_igemm")]
     if not convs:
         return {}
-    ov = event_overhead_ms(fine, extract_ms_clean)
-    roof = t = t_raw = 0.0
+    roof = t = 0.0
     n_hbm = 0
     for name, fl, by, ms in convs:
         tm, tb = fl / (peak_tflops * 1e12), by / (PEAK_HBM_GBPS * 1e9)
         n_hbm += tb > tm
         roof += max(tm, tb)
-        t_raw += ms * 1e-3
-        t += max(ms - (ov or 0.0), 0.5 * ms) * 1e-3
-    out = {"roofline_frac": round(roof / t, 4), "roofline_frac_raw": round(roof / t_raw, 4),
-           "event_overhead_us_per_launch": None if ov is None else round(ov * 1e3, 2),
-           "conv_kernel_ms": round(t * 1e3, 4), "conv_floor_ms": round(roof * 1e3, 4),
-           "convs": len(convs), "hbm_bound_convs": n_hbm,
-           "roofline_basis": f"per conv max(flops/{peak_tflops} TF, bytes/{PEAK_HBM_GBPS / 1e3:.0f} TB/s), "
-                             "summed over the stack's conv launches (one episode, per-launch events, "
-                             "less the measured per-launch event cost)"}
-    return out
+        t += ms * 1e-3
+    return {"roofline_frac": round(roof / t, 4), "conv_kernel_ms": round(t * 1e3, 4),
+            "conv_floor_ms": round(roof * 1e3, 4), "convs": len(convs), "hbm_bound_convs": n_hbm,
+            "roofline_basis": f"per conv max(flops/{peak_tflops} TF, bytes/{PEAK_HBM_GBPS / 1e3:.0f} TB/s), "
+                              "summed over the stack's conv launches (one episode, per-launch events)"}
 
 
 def _free_port() -> int:
@@ -562,11 +533,6 @@ def main():
     images = (shot + 1) * E
     ref_ex_fl = reference_conv_flops(layers, S) * images * args.steps
 
-    # the extract bracket without per-launch events, one episode alone on the GPU (the sequential
-    # leg, or the timed run when it is sequential): conv_roofline's event-cost reference
-    _ex_clean = [r[3] for r in (seq_recs if seq_recs else (recs if pipe is None else [])) if r[0].startswith("extract_features")]
-    ex_clean_ms = sum(_ex_clean) / len(_ex_clean) if _ex_clean else None
-
     # per-launch table from one extra (untimed) episode at profile level 2
     _lib.profile_enable(2)
     step(0, W0[0].clone())
@@ -676,8 +642,7 @@ def main():
                     "reference's numerics without the bf16x3 split)",
             "conv_stack": {"tflops": round(fex_fl / (fex_ms * 1e-3) / 1e12, 2),
                            "ms_per_step": round(fex_ms / args.exact_steps, 3),
-                           **conv_roofline(ffine, PEAK_FP32_MFMA_TFLOPS,
-                                           fex_ms / len(fex) if fex else None)},
+                           **conv_roofline(ffine, PEAK_FP32_MFMA_TFLOPS)},
             "conv_roofline": None if not fdom else {
                 "kernel": fdom[0][0].split(" ")[0] + " (bottleneck conv)",
                 "achieved": round(sum(r[1] for r in fdom) / (sum(r[3] for r in fdom) * 1e-3) / 1e12, 2),
@@ -741,7 +706,7 @@ def main():
                        "note": "whole extract_features bracket (convs + stem/maxpool/PPM byte kernels + gaps); "
                                "executed FLOPs exclude the declared PPM fold (DESIGN.md §3), the reference "
                                "formulation counts the 4096-channel bottleneck conv as written",
-                       **conv_roofline(fine, peak, ex_clean_ms)},
+                       **conv_roofline(fine, peak)},
         "phases_ms_per_step": {"extract": round(ex_ms / args.steps, 3), "inner_adapt": round(ad_ms / args.steps, 3),
                                "attention": round(at_ms / args.steps, 3)},
         "phases_roofline": {

@@ -14,6 +14,7 @@ Everything stays on the device; the host reads back per-episode IoU counts only.
 """
 from __future__ import annotations
 
+import os
 import time
 from collections import defaultdict
 from typing import Iterable, Tuple
@@ -231,7 +232,8 @@ class EpisodePipeline:
         # workgroup (59 instead of 118 CUs at 1-shot 473^2), leaving the rest to the extractor
         # passes beside it -- 466 against 443 episodes/s (same session); results are unchanged
         self.c_adapt = _lib.new_ctx()
-        _lib.check(_lib.lib().cwt_ctx_set_adapt_units(self.c_adapt, 2), "cwt_ctx_set_adapt_units")
+        upw = int(os.environ.get("CWT_PIPE_ADAPT_UNITS", "2"))   # (1 or 2: A/B of the geometry)
+        _lib.check(_lib.lib().cwt_ctx_set_adapt_units(self.c_adapt, upw), "cwt_ctx_set_adapt_units")
         self.k = 0
 
     @torch.no_grad()
