@@ -61,6 +61,15 @@ int launch_cos_cls_bwd(const float* x, long P, int B, int n, const float* w_eff,
                        const float* vnorm, float* dv, float* dg, float* db, float* dscale, hipStream_t st);
 int launch_corr(const float* q, const float* k, int B, int Pq, int Pk, int C, float* qn, float* kn, float* sim,
                 hipStream_t st);
+int launch_gemm_abt(const float* A, const float* Bm, int B, int M, int N, int K, float* Cm, hipStream_t st);
+int launch_mutual_matching(const float* x, int B, int NA, int NB, int C, float* y, float* rowmax, float* colpart,
+                           float* colmax, hipStream_t st);
+int launch_cp4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* Wa,
+                      const float* ba, const float* Wb, const float* bb, float* y, hipStream_t st);
+int launch_to_channels_last(const float* x, int B, int C, long P, float* y, hipStream_t st);
+int launch_add_inplace(float* y, const float* x, long n, hipStream_t st);
+int launch_match_softmax(const float* corr, int B, int NA, int NB, float temp, int ldp, float* P, hipStream_t st);
+int launch_match_vt(const float* v, int B, int NB, int C, int ldp, float* vt, hipStream_t st);
 int launch_seg_metrics(const float* logits, const int64_t* target, int B, int h, int w, int S, float* iut,
                        double* ce, unsigned* counts_ws, hipStream_t st, const float* logits2 = nullptr,
                        float* iut2 = nullptr);
@@ -1183,6 +1192,105 @@ int cwt_corr(cwt_ctx* ctx, const float* q, const float* k, int B, int Pq, int Pk
   if ((rc = ensure_ws(ctx, "corr.q", (size_t)B * Pq * C * 4, &qn)) || (rc = ensure_ws(ctx, "corr.k", (size_t)B * Pk * C * 4, &kn)))
     return rc;
   return launch_corr(q, k, B, Pq, Pk, C, (float*)qn, (float*)kn, sim, (hipStream_t)stream);
+}
+
+// ---- MatchNet (match.py:21-163, conv4d.py:11-62) ----
+static int mm_ws(cwt_ctx* ctx, int B, int NA, int NB, int C, float** rowmax, float** colpart, float** colmax) {
+  void *r, *p, *c;
+  int rc;
+  const long nrb = cdiv(NA, 16);
+  if ((rc = ensure_ws(ctx, "match.rowmax", (size_t)B * C * NA * 4, &r)) ||
+      (rc = ensure_ws(ctx, "match.colpart", (size_t)B * C * nrb * NB * 4, &p)) ||
+      (rc = ensure_ws(ctx, "match.colmax", (size_t)B * C * NB * 4, &c)))
+    return rc;
+  *rowmax = (float*)r;
+  *colpart = (float*)p;
+  *colmax = (float*)c;
+  return 0;
+}
+
+int cwt_mutual_matching(cwt_ctx* ctx, const float* x, int B, int NA, int NB, int C, float* y, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && y && B >= 1 && NA >= 1 && NB >= 1 && C >= 1 && C <= 64, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  float *rm, *cp, *cm;
+  int rc;
+  if ((rc = mm_ws(ctx, B, NA, NB, C, &rm, &cp, &cm))) return rc;
+  return launch_mutual_matching(x, B, NA, NB, C, y, rm, cp, cm, (hipStream_t)stream);
+}
+
+int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
+                           int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
+                           void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(corr && nc_params && corr2d && B >= 1 && (L == 1 || L == 2) && h >= 1 && w >= 1,
+            "bad arguments (in_channel 1 or 2)");
+  CWT_CHECK(!weighted_v || (v && Cv >= 1), "weighted_v needs v");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  const long NA = (long)h * w, NB = NA, P = NA * NB;
+  void *x0, *x1, *x2, *y1, *y2;
+  int rc;
+  if ((rc = ensure_ws(ctx, "match.x0", (size_t)B * P * L * 4, &x0)) ||
+      (rc = ensure_ws(ctx, "match.x1", (size_t)B * P * 10 * 4, &x1)) ||
+      (rc = ensure_ws(ctx, "match.x2", (size_t)B * P * 10 * 4, &x2)) ||
+      (rc = ensure_ws(ctx, "match.y1", (size_t)B * P * 4, &y1)) ||
+      (rc = ensure_ws(ctx, "match.y2", (size_t)B * P * 4, &y2)))
+    return rc;
+  float *rm, *cp, *cm;
+  if ((rc = mm_ws(ctx, B, (int)NA, (int)NB, L, &rm, &cp, &cm))) return rc;
+  Prof p(ctx, st, "match_corr_forward", 2.0 * B * P * 2 * (18.0 * L * 10 + 18.0 * 100 + 18.0 * 10), 4.0 * B * P * (L + 1));
+  // run_match_model: MutualMatching -> NeighConsensus -> MutualMatching (match.py:159-163)
+  if (L == 1) {
+    if ((rc = launch_mutual_matching(corr, B, (int)NA, (int)NB, 1, (float*)x0, rm, cp, cm, st))) return rc;
+  } else {
+    if ((rc = launch_to_channels_last(corr, B, L, P, (float*)x0, st))) return rc;
+    if ((rc = launch_mutual_matching((const float*)x0, B, (int)NA, (int)NB, L, (float*)x0, rm, cp, cm, st))) return rc;
+  }
+  // parameters per layer: conv1.weight [co][ci][3][3], conv1.bias [co], conv2.weight, conv2.bias
+  const int ch[4] = {L, 10, 10, 1};
+  const float* lw[3][4];
+  {
+    const float* q = nc_params;
+    for (int l = 0; l < 3; ++l) {
+      const int n = ch[l + 1] * ch[l] * 9;
+      lw[l][0] = q; q += n;
+      lw[l][1] = q; q += ch[l + 1];
+      lw[l][2] = q; q += n;
+      lw[l][3] = q; q += ch[l + 1];
+    }
+  }
+  // branch 0: conv(x) (conv1 over the query positions a, conv2 over the support positions b);
+  // branch 1 (symmetric mode): conv(x^T)^T = the same stack with the two roles swapped
+  for (int br = 0; br < (symmetric ? 2 : 1); ++br) {
+    const float* in = (const float*)x0;
+    float* outs[3] = {(float*)x1, (float*)x2, br ? (float*)y2 : (float*)y1};
+    for (int l = 0; l < 3; ++l) {
+      const float* Wa = br ? lw[l][2] : lw[l][0];
+      const float* ba = br ? lw[l][3] : lw[l][1];
+      const float* Wb = br ? lw[l][0] : lw[l][2];
+      const float* bb = br ? lw[l][1] : lw[l][3];
+      if ((rc = launch_cp4d_layer(in, B, h, w, h, w, ch[l], ch[l + 1], Wa, ba, Wb, bb, outs[l], st))) return rc;
+      in = outs[l];
+    }
+  }
+  if (symmetric && (rc = launch_add_inplace((float*)y1, (const float*)y2, B * P, st))) return rc;
+  if ((rc = mm_ws(ctx, B, (int)NA, (int)NB, 1, &rm, &cp, &cm))) return rc;
+  if ((rc = launch_mutual_matching((const float*)y1, B, (int)NA, (int)NB, 1, corr2d, rm, cp, cm, st))) return rc;
+  if (weighted_v) {
+    // attn = softmax(temp * corr2d, dim=-1); weighted_v = bmm(v, attn^T) (match.py:151-153),
+    // here as tokens [B][NA][Cv] = attn . v
+    const int ldp = (int)((NB + 3) & ~3L);
+    void *pw, *vt;
+    if ((rc = ensure_ws(ctx, "match.attn", (size_t)B * NA * ldp * 4, &pw)) ||
+        (rc = ensure_ws(ctx, "match.vt", (size_t)B * Cv * ldp * 4, &vt)))
+      return rc;
+    if ((rc = launch_match_softmax(corr2d, B, (int)NA, (int)NB, temp, ldp, (float*)pw, st))) return rc;
+    if ((rc = launch_match_vt(v, B, (int)NB, Cv, ldp, (float*)vt, st))) return rc;
+    if ((rc = launch_gemm_abt((const float*)pw, (const float*)vt, B, (int)NA, Cv, ldp, weighted_v, st))) return rc;
+  }
+  p.end();
+  return 0;
 }
 
 int cwt_seg_metrics(cwt_ctx* ctx, const float* logits, const int64_t* target, int B, int h, int w, int S,

@@ -382,4 +382,12 @@ int launch_corr(const float* q, const float* k, int B, int Pq, int Pk, int C, fl
   return 0;
 }
 
+// C[b] = A[b] . Bm[b]^T (A [M][K], Bm [N][K], K % 4 == 0), exact fp32 (MatchNet's v . attn^T)
+int launch_gemm_abt(const float* A, const float* Bm, int B, int M, int N, int K, float* Cm, hipStream_t st) {
+  dim3 grid(cdiv(N, CG_T), cdiv(M, CG_T), B);
+  hipLaunchKernelGGL(corr_gemm_kernel, grid, dim3(256), 0, st, A, Bm, M, N, K, Cm);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // namespace cwt

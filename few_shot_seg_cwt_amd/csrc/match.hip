@@ -1,0 +1,299 @@
+// MatchNet's 4-D matching head (reference src/model/match.py:21-163,
+// src/model/conv4d.py:11-62): the run_match_model chain of corr_forward,
+//   MutualMatching -> NeighConsensus (symmetric, three CenterPivotConv4d + ReLU) ->
+//   MutualMatching -> softmax(temp * corr2d) -> v . attn^T,
+// over a correlation of NA = hA*wA query positions by NB = hB*wB support positions.
+//
+// Layout: a 4-D tensor x[B][C][hA][wA][hB][wB] (torch) is held channels-last,
+// [B][a][b][C] with a = (ha, wa), b = (hb, wb) row-major: the C <= 10 channels of one (a, b)
+// pair are one contiguous run, the b positions of one a a contiguous [hB][wB][C] image.
+//
+// CenterPivotConv4d (stride 1, kernel 3, padding 1) is two 2-D convolutions summed: conv1 over
+// the a plane for every fixed b, conv2 over the b plane for every fixed a (conv4d.py:40-62).
+// NeighConsensus in symmetric mode is conv(x) + conv(x^T)^T (match.py:75-80); the transposed
+// branch is the same layer stack with the two convolutions' roles swapped (conv1 over b, conv2
+// over a), so neither branch moves the 4-D tensor: cp4d_layer_kernel takes the a-plane and
+// b-plane weights as arguments.
+//
+// Arithmetic: exact fp32 everywhere (VALU fmaf for the tiny-channel 4-D convs, the f32 MFMA
+// GEMM of heads.hip for v . attn^T); MutualMatching uses the reference's operation order
+// (corr * ((corr / (max_B + eps)) * (corr / (max_A + eps)))).
+#include "common.h"
+#include "kernels.h"
+
+namespace cwt {
+
+// ---- MutualMatching (match.py:34-53), per channel of x[B][NA][NB][C] ----
+// row maxima (over b for each a) and per-row-block partial column maxima
+constexpr int MM_RB = 16;  // rows of a per block
+__global__ __launch_bounds__(256) void mm_rowcol_kernel(const float* __restrict__ x, int NA, int NB, int C,
+                                                        float* __restrict__ rowmax, float* __restrict__ colpart) {
+  // grid: (cdiv(NA, MM_RB), B * C); rowmax [B*C][NA], colpart [B*C][cdiv(NA,MM_RB)][NB]
+  const int bc = blockIdx.y, b = bc / C, c = bc - b * C;
+  const int a0 = blockIdx.x * MM_RB;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const float* xb = x + (long)b * NA * NB * C + c;
+  __shared__ float rm[4][MM_RB];
+  float rmax[MM_RB];
+#pragma unroll
+  for (int r = 0; r < MM_RB; ++r) rmax[r] = -INFINITY;
+  for (int j = t; j < NB; j += 256) {
+    float cm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < MM_RB; ++r) {
+      const int a = a0 + r;
+      if (a < NA) {
+        const float v = xb[((long)a * NB + j) * C];
+        cm = fmaxf(cm, v);
+        rmax[r] = fmaxf(rmax[r], v);
+      }
+    }
+    colpart[((long)bc * gridDim.x + blockIdx.x) * NB + j] = cm;
+  }
+#pragma unroll
+  for (int r = 0; r < MM_RB; ++r) {
+    float v = rmax[r];
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    if (lane == 0) rm[wv][r] = v;
+  }
+  __syncthreads();
+  if (t < MM_RB && a0 + t < NA)
+    rowmax[(long)bc * NA + a0 + t] = fmaxf(fmaxf(rm[0][t], rm[1][t]), fmaxf(rm[2][t], rm[3][t]));
+}
+
+__global__ __launch_bounds__(256) void mm_colmax_kernel(const float* __restrict__ colpart, int nrb, int NB,
+                                                        float* __restrict__ colmax) {
+  const int bc = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= NB) return;
+  float m = -INFINITY;
+  for (int rb = 0; rb < nrb; ++rb) m = fmaxf(m, colpart[((long)bc * nrb + rb) * NB + j]);
+  colmax[(long)bc * NB + j] = m;
+}
+
+// y = x * ((x / (rowmax + eps)) * (x / (colmax + eps))); x, y [B][NA][NB][C] (y may alias x)
+__global__ __launch_bounds__(256) void mm_apply_kernel(const float* x, long total, int NA, int NB, int C,
+                                                       const float* __restrict__ rowmax,
+                                                       const float* __restrict__ colmax, float* y) {
+  const float eps = 1e-5f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long p = i / C;
+    const int j = (int)(p % NB);
+    const long ab = p / NB;
+    const int a = (int)(ab % NA), b = (int)(ab / NA);
+    const int bc = b * C + c;
+    const float v = x[i];
+    const float vb = v / (colmax[(long)bc * NB + j] + eps);  // corr4d_B: max over the A positions
+    const float va = v / (rowmax[(long)bc * NA + a] + eps);  // corr4d_A: max over the B positions
+    y[i] = v * (va * vb);
+  }
+}
+
+// ---- one CenterPivotConv4d layer (+ ReLU) on x[B][NA][NB][CIN] -> y[B][NA][NB][COUT] ----
+// y[a][b][o] = relu( sum_{c,ky,kx} Wa[o][c][ky][kx] x[(ha+ky-1, wa+kx-1)][b][c] + ba[o]
+//                  + sum_{c,ky,kx} Wb[o][c][ky][kx] x[a][(hb+ky-1, wb+kx-1)][c] + bb[o] )
+// (zero padding).  Workgroup tile: an a patch of TAH x TAW positions by a b patch of TBH x TBW;
+// its cross-shaped input (a patch + halo at the tile's b positions, b patch + halo at its a
+// positions) is staged in LDS; thread = one (a, b) pair, all COUT outputs.
+constexpr int CP_TAH = 2, CP_TAW = 8, CP_TBH = 2, CP_TBW = 8;
+constexpr int CP_NA = CP_TAH * CP_TAW, CP_NB = CP_TBH * CP_TBW;             // 16 x 16 = 256 pairs
+constexpr int CP_HA = (CP_TAH + 2) * (CP_TAW + 2), CP_HB = (CP_TBH + 2) * (CP_TBW + 2);  // 40 halo positions
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void cp4d_layer_kernel(const float* __restrict__ x, int hA, int wA, int hB, int wB,
+                                                         const float* __restrict__ Wa, const float* __restrict__ ba,
+                                                         const float* __restrict__ Wb, const float* __restrict__ bb,
+                                                         float* __restrict__ y) {
+  __shared__ float xa[CP_HA][CP_NB][CIN];  // a halo box x b tile
+  __shared__ float xb[CP_NA][CP_HB][CIN];  // a tile x b halo box
+  __shared__ float wl[2][COUT][CIN * 9 + 1];
+  __shared__ float bl[COUT];
+  const int NA = hA * wA, NB = hB * wB;
+  const int ntb = (wB + CP_TBW - 1) / CP_TBW;
+  const int ta = blockIdx.y, tb = blockIdx.x;  // a tile, b tile
+  const int ntaw = (wA + CP_TAW - 1) / CP_TAW;
+  const int ha0 = (ta / ntaw) * CP_TAH, wa0 = (ta % ntaw) * CP_TAW;
+  const int hb0 = (tb / ntb) * CP_TBH, wb0 = (tb % ntb) * CP_TBW;
+  const long xoff = (long)blockIdx.z * NA * NB * CIN;
+  const int t = threadIdx.x;
+  for (int i = t; i < 2 * COUT * CIN * 9; i += 256) {
+    const int s = i / (COUT * CIN * 9), r = i - s * (COUT * CIN * 9);
+    const int o = r / (CIN * 9), k = r - o * (CIN * 9);
+    wl[s][o][k] = (s ? Wb : Wa)[r];
+  }
+  if (t < COUT) bl[t] = ba[t] + bb[t];
+  // a halo box at the tile's b positions
+  for (int i = t; i < CP_HA * CP_NB * CIN; i += 256) {
+    const int c = i % CIN, p = i / CIN;
+    const int bi = p % CP_NB, ai = p / CP_NB;
+    const int ha = ha0 - 1 + ai / (CP_TAW + 2), wa = wa0 - 1 + ai % (CP_TAW + 2);
+    const int hb = hb0 + bi / CP_TBW, wb = wb0 + bi % CP_TBW;
+    float v = 0.f;
+    if ((unsigned)ha < (unsigned)hA && (unsigned)wa < (unsigned)wA && hb < hB && wb < wB)
+      v = x[xoff + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + c];
+    xa[ai][bi][c] = v;
+  }
+  // b halo box at the tile's a positions
+  for (int i = t; i < CP_NA * CP_HB * CIN; i += 256) {
+    const int c = i % CIN, p = i / CIN;
+    const int bi = p % CP_HB, ai = p / CP_HB;
+    const int ha = ha0 + ai / CP_TAW, wa = wa0 + ai % CP_TAW;
+    const int hb = hb0 - 1 + bi / (CP_TBW + 2), wb = wb0 - 1 + bi % (CP_TBW + 2);
+    float v = 0.f;
+    if (ha < hA && wa < wA && (unsigned)hb < (unsigned)hB && (unsigned)wb < (unsigned)wB)
+      v = x[xoff + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + c];
+    xb[ai][bi][c] = v;
+  }
+  __syncthreads();
+  const int ai = t / CP_NB, bi = t % CP_NB;  // this thread's pair within the tile
+  const int ha = ha0 + ai / CP_TAW, wa = wa0 + ai % CP_TAW;
+  const int hb = hb0 + bi / CP_TBW, wb = wb0 + bi % CP_TBW;
+  float acc[COUT];
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) acc[o] = bl[o];
+  const int aiy = ai / CP_TAW, aix = ai % CP_TAW, biy = bi / CP_TBW, bix = bi % CP_TBW;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const float* pa = xa[(aiy + ky) * (CP_TAW + 2) + aix + kx][bi];
+      const float* pb = xb[ai][(biy + ky) * (CP_TBW + 2) + bix + kx];
+      float va[CIN], vb[CIN];
+#pragma unroll
+      for (int c = 0; c < CIN; ++c) {
+        va[c] = pa[c];
+        vb[c] = pb[c];
+      }
+#pragma unroll
+      for (int o = 0; o < COUT; ++o)
+#pragma unroll
+        for (int c = 0; c < CIN; ++c) {
+          acc[o] = fmaf(wl[0][o][c * 9 + ky * 3 + kx], va[c], acc[o]);
+          acc[o] = fmaf(wl[1][o][c * 9 + ky * 3 + kx], vb[c], acc[o]);
+        }
+    }
+  if (ha < hA && wa < wA && hb < hB && wb < wB) {
+    float* yp = y + (long)blockIdx.z * NA * NB * COUT + ((long)(ha * wA + wa) * NB + hb * wB + wb) * COUT;
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) yp[o] = fmaxf(acc[o], 0.f);
+  }
+}
+
+// x [B][C][P] (channel planes) -> y [B][P][C] (channels last)
+__global__ void to_channels_last_kernel(const float* __restrict__ x, int B, int C, long P, float* __restrict__ y) {
+  const long total = (long)B * C * P;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long p = (i / C) % P;
+    const long b = i / ((long)C * P);
+    y[i] = x[(b * C + c) * P + p];
+  }
+}
+
+// y += x (element count n)
+__global__ void add_inplace_kernel(float* __restrict__ y, const float* __restrict__ x, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] += x[i];
+}
+
+// softmax(temp * corr2d) over b, one workgroup per row a, written with row stride ldp (the pad
+// columns zero): P[B][NA][ldp]
+__global__ __launch_bounds__(256) void match_softmax_kernel(const float* __restrict__ corr, int NA, int NB, float temp,
+                                                            int ldp, float* __restrict__ P) {
+  const long row = blockIdx.x;  // b * NA + a
+  const float* cr = corr + row * NB;
+  float* pr = P + row * ldp;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  __shared__ float red[4];
+  float m = -INFINITY;
+  for (int j = t; j < NB; j += 256) m = fmaxf(m, cr[j] * temp);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (lane == 0) red[wv] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int j = t; j < NB; j += 256) s += __expf(cr[j] * temp - m);
+  s = wave_sum_dpp(s);
+  if (lane == 0) red[wv] = s;
+  __syncthreads();
+  const float inv = 1.f / ((red[0] + red[1]) + (red[2] + red[3]));
+  for (int j = t; j < ldp; j += 256) pr[j] = j < NB ? __expf(cr[j] * temp - m) * inv : 0.f;
+}
+
+// v tokens [B][NB][C] -> vT [B][C][ldp] (pad columns zero)
+__global__ __launch_bounds__(256) void match_vt_kernel(const float* __restrict__ v, int NB, int C, int ldp,
+                                                       float* __restrict__ vt) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const int j0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int r = ty; r < 32; r += 8) {
+    const int j = j0 + r, c = c0 + tx;
+    tile[r][tx] = (j < NB && c < C) ? v[((long)b * NB + j) * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int c = c0 + r, j = j0 + tx;
+    if (c < C && j < ldp) vt[((long)b * C + c) * ldp + j] = tile[tx][r];
+  }
+}
+
+int launch_mutual_matching(const float* x, int B, int NA, int NB, int C, float* y, float* rowmax, float* colpart,
+                           float* colmax, hipStream_t st) {
+  const int nrb = cdiv(NA, MM_RB);
+  hipLaunchKernelGGL(mm_rowcol_kernel, dim3(nrb, B * C), dim3(256), 0, st, x, NA, NB, C, rowmax, colpart);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mm_colmax_kernel, dim3(cdiv(NB, 256), B * C), dim3(256), 0, st, (const float*)colpart, nrb, NB,
+                     colmax);
+  CWT_LAUNCH_CHECK();
+  const long total = (long)B * NA * NB * C;
+  hipLaunchKernelGGL(mm_apply_kernel, dim3((unsigned)std::min<long>(65536, cdiv(total, 256))), dim3(256), 0, st, x,
+                     total, NA, NB, C, (const float*)rowmax, (const float*)colmax, y);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_cp4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* Wa,
+                      const float* ba, const float* Wb, const float* bb, float* y, hipStream_t st) {
+  dim3 grid(cdiv(hB, CP_TBH) * cdiv(wB, CP_TBW), cdiv(hA, CP_TAH) * cdiv(wA, CP_TAW), B);
+#define CWT_CP4D(CI, CO)                                                                                         \
+  if (cin == CI && cout == CO) {                                                                                 \
+    hipLaunchKernelGGL((cp4d_layer_kernel<CI, CO>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, Wa, ba, Wb, bb, y); \
+    CWT_LAUNCH_CHECK();                                                                                          \
+    return 0;                                                                                                    \
+  }
+  CWT_CP4D(1, 10)
+  CWT_CP4D(2, 10)
+  CWT_CP4D(10, 10)
+  CWT_CP4D(10, 1)
+#undef CWT_CP4D
+  return fail(CWT_EARG, "cp4d layer: channels (1|2 -> 10, 10 -> 10, 10 -> 1) only");
+}
+
+int launch_to_channels_last(const float* x, int B, int C, long P, float* y, hipStream_t st) {
+  const long n = (long)B * C * P;
+  hipLaunchKernelGGL(to_channels_last_kernel, dim3((unsigned)std::min<long>(65536, cdiv(n, 256))), dim3(256), 0, st, x,
+                     B, C, P, y);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_add_inplace(float* y, const float* x, long n, hipStream_t st) {
+  hipLaunchKernelGGL(add_inplace_kernel, dim3((unsigned)std::min<long>(65536, cdiv(n, 256))), dim3(256), 0, st, y, x, n);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_match_softmax(const float* corr, int B, int NA, int NB, float temp, int ldp, float* P, hipStream_t st) {
+  hipLaunchKernelGGL(match_softmax_kernel, dim3(B * NA), dim3(256), 0, st, corr, NA, NB, temp, ldp, P);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_match_vt(const float* v, int B, int NB, int C, int ldp, float* vt, hipStream_t st) {
+  hipLaunchKernelGGL(match_vt_kernel, dim3(cdiv(ldp, 32), cdiv(C, 32), B), dim3(256), 0, st, v, NB, C, ldp, vt);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace cwt

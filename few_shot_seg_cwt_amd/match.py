@@ -1,0 +1,166 @@
+"""MatchNet, the 4-D matching head of the MMN / MatchNet variants, on
+HIP kernels (csrc/match.hip) behind the C ABI:
+
+  MutualMatching(corr4d)                      src/model/match.py:21-53
+  NeighConsensus(kernel_sizes, channels, ...)  src/model/match.py:56-85  (CenterPivotConv4d layers,
+                                               src/model/conv4d.py:11-62)
+  MatchNet(temp, cv_type, in_channel, ...)     src/model/match.py:88-163 (forward, corr_forward,
+                                               run_match_model)
+
+The modules keep the reference's parameter names (``NeighConsensus.conv.{0,2,4}.conv{1,2}.
+{weight,bias}``), so a reference state_dict loads as is.  Built: the default head of every MMN /
+MatchNet script -- CenterPivotConv4d ('red'), kernel sizes [3, 3, 3], channels [10, 10, 1],
+in_channel 1 or 2, symmetric or not -- forward only (inference).  Not built: the full Conv4d
+('cv4'), the spatial context encoder (sce), the cycle-consistency mask (cyc) and ig_mask.
+
+Parity is unpinned: the reference cannot be run here and holds no fixtures for
+this head; tests/test_gpu_match.py checks it against oracle/match_oracle.py, a float64
+restatement of the same modules.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from .heads import get_corr
+from .transformer import as_tokens
+
+
+def MutualMatching(corr4d: torch.Tensor) -> torch.Tensor:
+    """match.py:21-53: corr4d [B, C, ha, wa, hb, wb] -> same shape, each channel scaled by its
+    ratios to the max over the query positions and over the support positions."""
+    _lib.require(corr4d, "corr4d")
+    B, C, ha, wa, hb, wb = corr4d.shape
+    NA, NB = ha * wa, hb * wb
+    x = corr4d.reshape(B, C, NA, NB).permute(0, 2, 3, 1).contiguous()   # channels last
+    y = torch.empty_like(x)
+    _lib.check(_lib.lib().cwt_mutual_matching(_lib.ctx(x.device.index), _lib.ptr(x), B, NA, NB, C, _lib.ptr(y),
+                                              _lib.stream_ptr(x.device)), "cwt_mutual_matching")
+    return y.permute(0, 3, 1, 2).reshape(B, C, ha, wa, hb, wb)
+
+
+class CenterPivotConv4d(torch.nn.Module):
+    """conv4d.py:11-62 parameter holder (conv1 over the first position pair, conv2 over the
+    second), stride 1, kernel 3, padding 1; the layer runs inside NeighConsensus's fused path."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size=(3,) * 4, padding=(1,) * 4,
+                 stride=(1,) * 4, bias: bool = True, device=None):
+        super().__init__()
+        if tuple(kernel_size) != (3,) * 4 or tuple(padding) != (1,) * 4 or tuple(stride) != (1,) * 4 or not bias:
+            raise NotImplementedError("CenterPivotConv4d: kernel 3, padding 1, stride 1, bias only")
+        self.conv1 = torch.nn.Conv2d(in_channels, out_channels, 3, padding=1, bias=True, device=device)
+        self.conv2 = torch.nn.Conv2d(in_channels, out_channels, 3, padding=1, bias=True, device=device)
+
+
+class NeighConsensus(torch.nn.Module):
+    """match.py:56-85 with the default geometry: three CenterPivotConv4d + ReLU layers,
+    channels in_channel -> 10 -> 10 -> 1, symmetric mode conv(x) + conv(x^T)^T."""
+
+    def __init__(self, kernel_sizes=(3, 3, 3), channels=(10, 10, 1), symmetric_mode: bool = True, conv: str = "red",
+                 in_channel: int = 1, device=None):
+        super().__init__()
+        if conv != "red":
+            raise NotImplementedError("NeighConsensus: only the CenterPivotConv4d ('red') layers are built")
+        if tuple(kernel_sizes) != (3, 3, 3) or tuple(channels) != (10, 10, 1) or in_channel not in (1, 2):
+            raise NotImplementedError("NeighConsensus: kernel sizes [3,3,3], channels [10,10,1], in_channel 1 or 2")
+        self.symmetric_mode = symmetric_mode
+        self.kernel_sizes = list(kernel_sizes)
+        self.channels = list(channels)
+        self.in_channel = in_channel
+        mods = []
+        ch_in = in_channel
+        for ch_out in channels:
+            mods += [CenterPivotConv4d(ch_in, ch_out, device=device), torch.nn.ReLU(inplace=True)]
+            ch_in = ch_out
+        self.conv = torch.nn.Sequential(*mods)
+        self._packed, self._packed_key = None, None
+
+    def packed(self) -> torch.Tensor:
+        """The layers' parameters in cwt_match_corr_forward's order (cached per parameter version)."""
+        ps = []
+        for i in (0, 2, 4):
+            layer = self.conv[i]
+            ps += [layer.conv1.weight, layer.conv1.bias, layer.conv2.weight, layer.conv2.bias]
+        key = tuple((p.data_ptr(), p._version) for p in ps)
+        if self._packed is None or key != self._packed_key:
+            with torch.no_grad():
+                self._packed = torch.cat([p.detach().reshape(-1).float() for p in ps]).contiguous()
+            self._packed_key = key
+        return self._packed
+
+
+class MatchNet(torch.nn.Module):
+    """match.py:88-163.  forward(fq_fea, fs_fea, v) and corr_forward(corr4d, v, ret_attn) on the
+    device; v is the support feature map [B, Cv, h, w] (returned weighted_v has its shape)."""
+
+    def __init__(self, temp: float = 3.0, cv_type: str = "red", in_channel: int = 1, sce: bool = False,
+                 cyc: bool = False, sym_mode: bool = True, cv_kernels=(3, 3, 3), cv_channels=(10, 10, 1),
+                 device=None):
+        super().__init__()
+        if sce or cyc:
+            raise NotImplementedError("MatchNet: the spatial context encoder and the cycle mask are not built")
+        self.temp = temp
+        self.sce, self.cyc = sce, cyc
+        self.in_channel = in_channel
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.NeighConsensus = NeighConsensus(kernel_sizes=cv_kernels, channels=cv_channels, symmetric_mode=sym_mode,
+                                             conv=cv_type, in_channel=in_channel, device=dev)
+
+    def _run(self, corr: torch.Tensor, h: int, w: int, v: torch.Tensor | None):
+        """corr [B, L, hw, hw] contiguous -> (corr2d [B, hw, hw], weighted_v tokens or None)."""
+        _lib.require(corr, "corr")
+        B, L = corr.shape[0], corr.shape[1]
+        if L != self.in_channel:
+            raise ValueError("input corr channel inconsistent with in_channel of NCNet")
+        params = self.NeighConsensus.packed()
+        hw = h * w
+        corr2d = torch.empty((B, hw, hw), device=corr.device, dtype=torch.float32)
+        wv, vt, Cv = None, None, 0
+        if v is not None:
+            vt = as_tokens(v if v.dim() == 4 else v.reshape(v.shape[0], v.shape[1], h, w))
+            Cv = vt.shape[1]
+            wv = torch.empty((B, h, w, Cv), device=corr.device, dtype=torch.float32)
+        _lib.check(_lib.lib().cwt_match_corr_forward(
+            _lib.ctx(corr.device.index), _lib.ptr(corr), B, L, h, w, _lib.ptr(params),
+            1 if self.NeighConsensus.symmetric_mode else 0, float(self.temp),
+            _lib.ptr(vt) if vt is not None else None, Cv, _lib.ptr(corr2d), _lib.ptr(wv) if wv is not None else None,
+            _lib.stream_ptr(corr.device)), "cwt_match_corr_forward")
+        return corr2d, (wv.permute(0, 3, 1, 2) if wv is not None else None)
+
+    def run_match_model(self, corr4d: torch.Tensor) -> torch.Tensor:
+        """match.py:159-163: corr4d [B, L, h, w, h, w] -> [B, 1, h, w, h, w]."""
+        B, L, h, w = corr4d.shape[:4]
+        corr2d, _ = self._run(corr4d.reshape(B, L, h * w, h * w).contiguous(), h, w, None)
+        return corr2d.reshape(B, 1, h, w, h, w)
+
+    def corr_forward(self, corr4d: torch.Tensor, v: torch.Tensor, ret_attn: bool = False):
+        """match.py:142-157 (returns weighted_v [B, Cv, h, w]; with ret_attn (corr2d, weighted_v))."""
+        B, ch, h, w = corr4d.shape[:4]
+        assert ch == self.in_channel, "input corr channel inconsistent with in_channel of NCNet"
+        corr2d, wv = self._run(corr4d.reshape(B, ch, h * w, h * w).contiguous(), h, w, v)
+        return (corr2d, wv) if ret_attn else wv
+
+    def forward(self, fq_fea, fs_fea, v, s_mask=None, ig_mask=None, ret_corr=False, use_cyc=False, ret_cyc=False):
+        """match.py:103-140 without sce / cyc / ig_mask: normalised features -> get_corr ->
+        run_match_model -> softmax(temp * corr2d) -> v . attn^T."""
+        if ig_mask is not None or use_cyc or ret_cyc:
+            raise NotImplementedError("MatchNet.forward: ig_mask and the cycle mask are not built")
+        B, ch, h, w = fq_fea.shape
+        corr = get_corr(fq_fea, fs_fea)   # normalises both (the reference's F.normalize first is the same map)
+        corr2d, wv = self._run(corr.reshape(B, 1, h * w, h * w), h, w, v)
+        if ret_corr:
+            return wv, corr2d.reshape(B, h, w, h, w)
+        return wv
+
+
+def init_match_params(mod: torch.nn.Module, seed: int = 0) -> None:
+    """Deterministic parameters for tests / benchmarks (nn.Conv2d's default init bounds)."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, p in mod.named_parameters():
+            fan_in = p.shape[1] * 9 if p.dim() == 4 else 10
+            bound = 1.0 / math.sqrt(fan_in)
+            p.copy_((torch.rand(p.shape, generator=g, dtype=torch.float32) * 2 - 1) * bound)

@@ -324,6 +324,27 @@ int cwt_cos_classify_bwd(cwt_ctx* ctx, const float* x, int B, int P, int C, int 
 int cwt_corr(cwt_ctx* ctx, const float* q, const float* k, int B, int Pq, int Pk, int C, float* sim,
              void* stream);
 
+/* MutualMatching (src/model/match.py:21-53), per channel: x device [B][NA][NB][C] (channels
+ * last: x[b][a][j][c] = corr4d[b, c, a, j] with a, j the flattened query / support positions);
+ * y = x * ((x / (max_a x + 1e-5)) * (x / (max_j x + 1e-5))), the maxima per (b, c) over all
+ * query positions a (for each j) and all support positions j (for each a).  y may alias x.
+ * C <= 64. */
+int cwt_mutual_matching(cwt_ctx* ctx, const float* x, int B, int NA, int NB, int C, float* y, void* stream);
+
+/* MatchNet.corr_forward (src/model/match.py:142-163; NeighConsensus :56-85 with the default
+ * kernel sizes [3,3,3], channels [10,10,1] and CenterPivotConv4d layers, conv4d.py:11-62):
+ * corr device [B][L][h*w][h*w] (the torch [B, L, h, w, h, w] tensor, L = in_channel 1 or 2);
+ * nc_params device: per layer l = 0, 1, 2 (channels L -> 10 -> 10 -> 1) conv1.weight [co][ci][3][3],
+ * conv1.bias [co], conv2.weight [co][ci][3][3], conv2.bias [co], concatenated (the order of
+ * NeighConsensus.conv.{0,2,4}.{conv1,conv2}.{weight,bias} in its state_dict); symmetric = the
+ * sym_mode flag; temp the softmax temperature.  corr2d device [B][h*w][h*w] receives
+ * run_match_model's output (the ret_attn corr2d); with weighted_v non-NULL, v device
+ * [B][h*w][Cv] (NHWC tokens of the support feature) gives weighted_v device [B][h*w][Cv] =
+ * softmax(temp * corr2d, -1) . v (tokens of bmm(v, attn^T)).  Exact fp32. */
+int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
+                           int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
+                           void* stream);
+
 /* torch.optim.SGD(momentum, dampening 0, weight_decay, nesterov) step over one flat
  * fp32 parameter buffer (optimizer.py:8-15): buf = m*buf + (g + wd*p) (buf = g+wd*p on
  * the first step, first_step != 0); p -= lr * (nesterov ? g + wd*p + m*buf : buf). */

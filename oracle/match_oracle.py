@@ -1,0 +1,81 @@
+"""ORACLE — test infrastructure only.  CPU restatement of the reference's MatchNet head
+(the 4-D matching head of the MMN / MatchNet variants).
+
+Only ``tests/`` may import this module, and only as the checker.  The product path
+(``few_shot_seg_cwt_amd.match``) never imports it.
+
+Parity unpinned: the reference cannot be run in this container and holds no
+fixtures for this head, so this restatement is checked only by its own construction (each
+function cites the reference file:line whose algorithm it restates, written independently of
+it) and by tests/test_match_oracle.py's algebraic identities (symmetric-mode transpose
+equivariance, the separable CenterPivotConv4d against a dense 4-D convolution with the
+cross-shaped kernel).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+
+def mutual_matching(x: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    """match.py:21-53: x [B, C, ha, wa, hb, wb]; per channel, the ratio of each score to the
+    maximum over the query positions (for its support position) and to the maximum over the
+    support positions (for its query position): x * ((x / maxA) * (x / maxB))."""
+    B, C, ha, wa, hb, wb = x.shape
+    m = x.reshape(B, C, ha * wa, hb * wb)
+    max_over_q = m.amax(dim=2, keepdim=True)   # for every support position
+    max_over_s = m.amax(dim=3, keepdim=True)   # for every query position
+    r_s = m / (max_over_q + eps)
+    r_q = m / (max_over_s + eps)
+    return (m * (r_q * r_s)).reshape(B, C, ha, wa, hb, wb)
+
+
+def center_pivot_conv4d(x: torch.Tensor, w1, b1, w2, b2) -> torch.Tensor:
+    """conv4d.py:40-62 at stride 1, kernel 3, padding 1: a 2-D conv (w1, b1) over the first
+    position pair for every fixed second pair, plus one (w2, b2) over the second pair for every
+    fixed first pair."""
+    B, C, ha, wa, hb, wb = x.shape
+    O = w1.shape[0]
+    # over (ha, wa): fold (hb, wb) into the batch
+    xa = x.permute(0, 4, 5, 1, 2, 3).reshape(B * hb * wb, C, ha, wa)
+    ya = F.conv2d(xa, w1, b1, padding=1).reshape(B, hb, wb, O, ha, wa).permute(0, 3, 4, 5, 1, 2)
+    # over (hb, wb): fold (ha, wa) into the batch
+    xb = x.permute(0, 2, 3, 1, 4, 5).reshape(B * ha * wa, C, hb, wb)
+    yb = F.conv2d(xb, w2, b2, padding=1).reshape(B, ha, wa, O, hb, wb).permute(0, 3, 1, 2, 4, 5)
+    return ya + yb
+
+
+def neigh_consensus(x: torch.Tensor, layers, symmetric: bool = True) -> torch.Tensor:
+    """match.py:56-85: layers = [(w1, b1, w2, b2)] * 3, each CenterPivotConv4d then ReLU;
+    symmetric mode adds the stack applied to the pair-swapped tensor, swapped back."""
+    def stack(z):
+        for (w1, b1, w2, b2) in layers:
+            z = torch.relu(center_pivot_conv4d(z, w1, b1, w2, b2))
+        return z
+    y = stack(x)
+    if symmetric:
+        y = y + stack(x.permute(0, 1, 4, 5, 2, 3)).permute(0, 1, 4, 5, 2, 3)
+    return y
+
+
+def run_match_model(corr4d: torch.Tensor, layers, symmetric: bool = True) -> torch.Tensor:
+    """match.py:159-163."""
+    return mutual_matching(neigh_consensus(mutual_matching(corr4d), layers, symmetric))
+
+
+def corr_forward(corr4d: torch.Tensor, v: torch.Tensor, layers, temp: float, symmetric: bool = True):
+    """match.py:142-157: corr4d [B, L, h, w, h, w], v [B, Cv, h, w] ->
+    (corr2d [B, hw, hw], weighted_v [B, Cv, h, w])."""
+    B, L, h, w = corr4d.shape[:4]
+    corr2d = run_match_model(corr4d, layers, symmetric).reshape(B, h * w, h * w)
+    attn = torch.softmax(corr2d * temp, dim=-1)
+    wv = torch.bmm(v.reshape(B, v.shape[1], h * w), attn.transpose(1, 2)).reshape(B, v.shape[1], h, w)
+    return corr2d, wv
+
+
+def layers_from_state(sd, prefix: str = "NeighConsensus.conv.", dtype=torch.float64):
+    out = []
+    for i in (0, 2, 4):
+        p = f"{prefix}{i}."
+        out.append(tuple(sd[p + n].to(dtype) for n in ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias")))
+    return out

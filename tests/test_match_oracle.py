@@ -1,0 +1,67 @@
+"""CPU checks of oracle/match_oracle.py (the MatchNet restatement; parity unpinned: no
+reference fixture exists for this head).  The restatement is checked against
+independent formulations of the same maps: MutualMatching element by element, the separable
+CenterPivotConv4d against a dense 4-D correlation with its cross-shaped 3^4 kernel, and the
+symmetric NeighConsensus's equivariance under swapping the two position pairs."""
+import torch
+
+from oracle import match_oracle as M
+
+
+def _layers(L, seed):
+    g = torch.Generator().manual_seed(seed)
+    out, ci = [], L
+    for co in (10, 10, 1):
+        mk = lambda *s: (torch.rand(*s, generator=g, dtype=torch.float64) * 2 - 1) * 0.3  # noqa: E731
+        out.append((mk(co, ci, 3, 3), mk(co), mk(co, ci, 3, 3), mk(co)))
+        ci = co
+    return out
+
+
+def test_mutual_matching_elementwise():
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand(2, 2, 3, 4, 4, 3, generator=g, dtype=torch.float64)
+    y = M.mutual_matching(x)
+    B, C = 2, 2
+    m = x.reshape(B, C, 12, 12)
+    for b in range(B):
+        for c in range(C):
+            for i in range(12):
+                for j in range(12):
+                    v = m[b, c, i, j]
+                    ref = v * ((v / (m[b, c, i, :].max() + 1e-5)) * (v / (m[b, c, :, j].max() + 1e-5)))
+                    assert torch.allclose(y.reshape(B, C, 12, 12)[b, c, i, j], ref, rtol=1e-14, atol=0)
+
+
+def test_center_pivot_equals_dense_cross_kernel():
+    g = torch.Generator().manual_seed(2)
+    B, C, O, ha, wa, hb, wb = 1, 2, 3, 4, 5, 5, 3
+    x = torch.rand(B, C, ha, wa, hb, wb, generator=g, dtype=torch.float64)
+    w1, w2 = torch.rand(O, C, 3, 3, generator=g, dtype=torch.float64), torch.rand(O, C, 3, 3, generator=g, dtype=torch.float64)
+    b1, b2 = torch.rand(O, generator=g, dtype=torch.float64), torch.rand(O, generator=g, dtype=torch.float64)
+    y = M.center_pivot_conv4d(x, w1, b1, w2, b2)
+    xp = torch.nn.functional.pad(x, (1, 1, 1, 1, 1, 1, 1, 1))
+    ref = torch.zeros(B, O, ha, wa, hb, wb, dtype=torch.float64) + (b1 + b2).view(1, O, 1, 1, 1, 1)
+    for t1 in range(3):
+        for t2 in range(3):
+            for t3 in range(3):
+                for t4 in range(3):
+                    k = torch.zeros(O, C, dtype=torch.float64)
+                    if (t3, t4) == (1, 1):
+                        k = k + w1[:, :, t1, t2]
+                    if (t1, t2) == (1, 1):
+                        k = k + w2[:, :, t3, t4]
+                    if not k.abs().sum():
+                        continue
+                    sl = xp[:, :, t1:t1 + ha, t2:t2 + wa, t3:t3 + hb, t4:t4 + wb]
+                    ref = ref + torch.einsum("oc,bcijkl->boijkl", k, sl)
+    assert torch.allclose(y, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_symmetric_consensus_is_swap_equivariant():
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(1, 2, 5, 4, 5, 4, generator=g, dtype=torch.float64)
+    layers = _layers(2, 4)
+    y = M.neigh_consensus(x, layers, symmetric=True)
+    ys = M.neigh_consensus(x.permute(0, 1, 4, 5, 2, 3), layers, symmetric=True).permute(0, 1, 4, 5, 2, 3)
+    assert torch.allclose(y, ys, rtol=1e-12, atol=1e-12)
