@@ -61,6 +61,9 @@ SIGNATURES = {
     "cwt_corr": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "cwt_mutual_matching": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "cwt_match_corr_forward": (_I, [_P, _P, _I, _I, _I, _I, _P, _I, _F, _P, _I, _P, _P, _P]),
+    "cwt_weight_average": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cwt_mmn_blend": (_I, [_P, _P, _P, _I, _I64, _F, _P, _P, _P]),
+    "cwt_extract_features_mid": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "cwt_sgd_step": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _I, _I, _P]),
     "cwt_pretrain_create": (_I, [_P, _I, _I, _I, C.POINTER(C.c_char_p), C.POINTER(_P), C.POINTER(_I64), _F,
                                  C.POINTER(_P)]),

@@ -61,6 +61,8 @@ int launch_cos_cls_bwd(const float* x, long P, int B, int n, const float* w_eff,
                        const float* vnorm, float* dv, float* dg, float* db, float* dscale, hipStream_t st);
 int launch_corr(const float* q, const float* k, int B, int Pq, int Pk, int C, float* qn, float* kn, float* sim,
                 hipStream_t st);
+int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipStream_t st);
+int launch_widen_bf16(const __bf16* x, long n, float* y, hipStream_t st);
 int launch_gemm_abt(const float* A, const float* Bm, int B, int M, int N, int K, float* Cm, hipStream_t st);
 int launch_mutual_matching(const float* x, int B, int NA, int NB, int C, float* y, float* rowmax, float* colpart,
                            float* colmax, hipStream_t st);
@@ -70,6 +72,11 @@ int launch_to_channels_last(const float* x, int B, int C, long P, float* y, hipS
 int launch_add_inplace(float* y, const float* x, long n, hipStream_t st);
 int launch_match_softmax(const float* corr, int B, int NA, int NB, float temp, int ldp, float* P, hipStream_t st);
 int launch_match_vt(const float* v, int B, int NB, int C, int ldp, float* vt, hipStream_t st);
+int launch_wa_attn(const float* tpg, int N, int h, int w, int co, const float* bt, const float* bp, const float* bg,
+                   float* wavg, hipStream_t st);
+int launch_wa_residual(const float* x, const float* back, const float* b, long n, int C, float* out, hipStream_t st);
+int launch_mmn_blend(const float* fq_in, const float* att, int B, long n, float att_wt, float* att_mean, float* fq_out,
+                     hipStream_t st);
 int launch_seg_metrics(const float* logits, const int64_t* target, int B, int h, int w, int S, float* iut,
                        double* ce, unsigned* counts_ws, hipStream_t st, const float* logits2 = nullptr,
                        float* iut2 = nullptr);
@@ -518,8 +525,10 @@ struct TrainBn {
 // The whole extractor as a list of conv calls + byte kernels.  dry_run sizes the split-K workspace.
 // tb != null: every BN on batch statistics with running-statistic update, Dropout2d on the
 // bottleneck output (train.py:184 model.train() before the first support extraction).
+// mid (optional, eval mode only): fp32 NHWC copies of the outputs of layer2, layer3 and layer4
+// ([N][h][h][512 / 1024 / 2048]; get_feat_list's per-layer features, pspnet.py:272-287)
 static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N, int S, float* feat,
-                       hipStream_t st, const TrainBn* tb = nullptr) {
+                       hipStream_t st, const TrainBn* tb = nullptr, float* const* mid = nullptr) {
   // conv arithmetic / activation storage: plain bf16 (cwt_backbone_set_precision), else the
   // context's fp32-accurate mode (S-layout bf16x3 by default)
   const bool b16 = bb->precision == CWT_CONV_BF16;
@@ -583,6 +592,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   cc(&bb->stem[1], A, N, Hs, Hs, 64, B, 64, 0, nullptr, 0, 1);
   cc(&bb->stem[2], B, N, Hs, Hs, 64, A, 128, 0, nullptr, 0, 1);
   const size_t n_stem_calls = calls.size();
+  size_t last_of_layer[4] = {0, 0, 0, 0};  // call index of each layer's last block (mid features)
   float* cur = B;  // maxpool output
   float* other = A;
   int H = H1;
@@ -603,6 +613,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
         res_ld = blk.down.Co;
       }
       cc(&blk.c3, T2, N, Ho, Ho, blk.c3.Ci, other, blk.c3.Co, 0, res, res_ld, 1);
+      if (bi == nbk - 1) last_of_layer[li] = calls.size() - 1;
       std::swap(cur, other);
       H = Ho;
     }
@@ -770,8 +781,24 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
       return rc;
     p.end();
   }
-  for (size_t i = n_stem_calls; i < n_backbone_calls; ++i)
+  for (size_t i = n_stem_calls; i < n_backbone_calls; ++i) {
     if ((rc = run_call(i))) return rc;
+    for (int li = 1; li < 4 && mid; ++li) {  // layer2 .. layer4 outputs, before the buffer is reused
+      if (i != last_of_layer[li] || !mid[li - 1]) continue;
+      const ConvCall& c = calls[i];
+      const ConvArgs a = make_args(c);
+      const long P = (long)a.M;
+      if (layout == ACT_SPLIT)
+        rc = launch_unsplit_act((const __bf16*)c.y, P, a.Co, mid[li - 1], a.Co, st);
+      else if (layout == ACT_BF16)
+        rc = launch_widen_bf16((const __bf16*)c.y, P * a.Co, mid[li - 1], st);
+      else {
+        const hipError_t e = hipMemcpyAsync(mid[li - 1], c.y, (size_t)P * a.Co * 4, hipMemcpyDeviceToDevice, st);
+        rc = e == hipSuccess ? 0 : fail((int)e, "mid feature copy");
+      }
+      if (rc) return rc;
+    }
+  }
   {
     Prof p(ctx, st, "ppm_pool", 0.0, 4.0 * ((double)N * h * h * 2048 + (double)N * 50 * 2048));
     if ((rc = launch_ppm(L4, N, h, h, 2048, kBins, 4, COL, POOL, st, layout))) return rc;
@@ -936,6 +963,19 @@ int cwt_extract_features(cwt_ctx* ctx, const cwt_backbone* handle, const float* 
   CWT_CHECK(N >= 1 && S >= 9 && (S - 1) % 8 == 0, "need N >= 1 and (S-1) % 8 == 0 (pspnet.py:150)");
   CWT_HIP(hipSetDevice(ctx->device));
   return run_extract(ctx, bb, img, N, S, feat, (hipStream_t)stream);
+}
+
+int cwt_extract_features_mid(cwt_ctx* ctx, const cwt_backbone* handle, const float* img, int N, int S, float* feat,
+                             float* l2, float* l3, float* l4, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  const Backbone* bb = reinterpret_cast<const Backbone*>(handle);
+  if (!bb) return fail(CWT_ESTATE, "backbone is NULL (cwt_backbone_load)");
+  if (bb->device != ctx->device) return fail(CWT_EARG, "backbone and context are on different devices");
+  CWT_CHECK(img && feat, "null buffer");
+  CWT_CHECK(N >= 1 && S >= 9 && (S - 1) % 8 == 0, "need N >= 1 and (S-1) % 8 == 0 (pspnet.py:150)");
+  CWT_HIP(hipSetDevice(ctx->device));
+  float* const mid[3] = {l2, l3, l4};
+  return run_extract(ctx, bb, img, N, S, feat, (hipStream_t)stream, nullptr, mid);
 }
 
 int cwt_extract_features_train_bn(cwt_ctx* ctx, cwt_backbone* handle, const float* img, int N, int S, float* feat,
@@ -1291,6 +1331,41 @@ int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h,
   }
   p.end();
   return 0;
+}
+
+int cwt_weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C, const float* w_tpg,
+                       const float* b_theta, const float* b_phi, const float* b_g, const float* w_back,
+                       const float* b_back, float* out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && w_tpg && b_theta && b_phi && b_g && w_back && b_back && out && N >= 1 && h >= 1 && w >= 1,
+            "bad arguments");
+  CWT_CHECK(C == 512 || C == 1024 || C == 2048, "WeightAverage: c_in 512, 1024 or 2048");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int co = C / 2;
+  const long P = (long)N * h * w;
+  void *tpg, *wavg, *back;
+  int rc;
+  if ((rc = ensure_ws(ctx, "wa.tpg", (size_t)P * 3 * co * 4, &tpg)) ||
+      (rc = ensure_ws(ctx, "wa.avg", (size_t)P * co * 4, &wavg)) ||
+      (rc = ensure_ws(ctx, "wa.back", (size_t)P * C * 4, &back)))
+    return rc;
+  Prof p(ctx, st, "weight_average c" + std::to_string(C), 2.0 * P * C * co * 4, 4.0 * P * (2.0 * C + 5.0 * co));
+  // theta | phi | g of every pixel: one GEMM against the three stacked 1x1 weights [3co][C]
+  if ((rc = launch_gemm_abt(x, w_tpg, 1, (int)P, 3 * co, C, (float*)tpg, st))) return rc;
+  if ((rc = launch_wa_attn((const float*)tpg, N, h, w, co, b_theta, b_phi, b_g, (float*)wavg, st))) return rc;
+  if ((rc = launch_gemm_abt((const float*)wavg, w_back, 1, (int)P, C, co, (float*)back, st))) return rc;
+  if ((rc = launch_wa_residual(x, (const float*)back, b_back, P * C, C, out, st))) return rc;
+  p.end();
+  return 0;
+}
+
+int cwt_mmn_blend(cwt_ctx* ctx, const float* f_q, const float* att_fq, int B, int64_t n, float att_wt,
+                  float* att_mean, float* fq_out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(f_q && att_fq && att_mean && fq_out && B >= 1 && n >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_mmn_blend(f_q, att_fq, B, (long)n, att_wt, att_mean, fq_out, (hipStream_t)stream);
 }
 
 int cwt_seg_metrics(cwt_ctx* ctx, const float* logits, const int64_t* target, int B, int h, int w, int S,

@@ -536,6 +536,17 @@ __global__ void unsplit_act_kernel(const __bf16* s, long P, int C, float* out, i
   *(f32x4*)(out + p * ld + c + 4) = v1;
 }
 
+// plain bf16 -> fp32 (the bf16 stack's activations)
+__global__ void widen_bf16_kernel(const __bf16* x, long n, float* y) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = (float)x[i];
+}
+
+int launch_widen_bf16(const __bf16* x, long n, float* y, hipStream_t st) {
+  hipLaunchKernelGGL(widen_bf16_kernel, dim3((unsigned)std::min<long>(65536, (n + 255) / 256)), dim3(256), 0, st, x, n, y);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 int launch_split_act(const float* x, long P, int C, int ld, __bf16* out, hipStream_t st) {
   if (C % 32) return fail(CWT_EARG, "split_act: C % 32");
   const long n = P * (C / 8);

@@ -1,5 +1,6 @@
-// MatchNet's 4-D matching head (reference src/model/match.py:21-163,
-// src/model/conv4d.py:11-62): the run_match_model chain of corr_forward,
+// MatchNet's 4-D matching head and the MMN head around it (reference
+// src/model/match.py:21-163, src/model/conv4d.py:11-62, src/model/mmn.py:11-71,
+// src/model/msm/msm_func.py:50-104): the run_match_model chain of corr_forward,
 //   MutualMatching -> NeighConsensus (symmetric, three CenterPivotConv4d + ReLU) ->
 //   MutualMatching -> softmax(temp * corr2d) -> v . attn^T,
 // over a correlation of NA = hA*wA query positions by NB = hB*wB support positions.
@@ -104,10 +105,14 @@ __global__ __launch_bounds__(256) void cp4d_layer_kernel(const float* __restrict
                                                          const float* __restrict__ Wa, const float* __restrict__ ba,
                                                          const float* __restrict__ Wb, const float* __restrict__ bb,
                                                          float* __restrict__ y) {
-  __shared__ float xa[CP_HA][CP_NB][CIN];  // a halo box x b tile
-  __shared__ float xb[CP_NA][CP_HB][CIN];  // a tile x b halo box
-  __shared__ float wl[2][COUT][CIN * 9 + 1];
-  __shared__ float bl[COUT];
+  // a halo box x b tile, one float of padding per a-halo position (the wave's two a rows of a
+  // 32-lane group then fall on disjoint banks); b halo box at the tile's a positions
+  __shared__ float xa[CP_HA][CP_NB * CIN + 1];
+  __shared__ float xb[CP_NA][CP_HB][CIN];
+  // weights tap-major with the outputs innermost ([side][tap][c][o], o padded to a multiple of
+  // 4): one broadcast ds_read_b128 gives four outputs' weights for an input value
+  constexpr int CO4 = (COUT + 3) & ~3;
+  __shared__ __attribute__((aligned(16))) float wl[2][9][CIN][CO4];
   const int NA = hA * wA, NB = hB * wB;
   const int ntb = (wB + CP_TBW - 1) / CP_TBW;
   const int ta = blockIdx.y, tb = blockIdx.x;  // a tile, b tile
@@ -116,33 +121,49 @@ __global__ __launch_bounds__(256) void cp4d_layer_kernel(const float* __restrict
   const int hb0 = (tb / ntb) * CP_TBH, wb0 = (tb % ntb) * CP_TBW;
   const long xoff = (long)blockIdx.z * NA * NB * CIN;
   const int t = threadIdx.x;
-  for (int i = t; i < 2 * COUT * CIN * 9; i += 256) {
-    const int s = i / (COUT * CIN * 9), r = i - s * (COUT * CIN * 9);
-    const int o = r / (CIN * 9), k = r - o * (CIN * 9);
-    wl[s][o][k] = (s ? Wb : Wa)[r];
+  for (int i = threadIdx.x; i < 2 * 9 * CIN * CO4; i += 256) {
+    const int o = i % CO4, r = i / CO4;
+    const int c = r % CIN, r2 = r / CIN;
+    const int tap = r2 % 9, side = r2 / 9;
+    (&wl[0][0][0][0])[i] = o < COUT ? (side ? Wb : Wa)[(o * CIN + c) * 9 + tap] : 0.f;
   }
-  if (t < COUT) bl[t] = ba[t] + bb[t];
-  // a halo box at the tile's b positions
-  for (int i = t; i < CP_HA * CP_NB * CIN; i += 256) {
+  // both boxes: every load of the thread issued before the first LDS store (one round of
+  // memory latency per workgroup instead of one per element)
+  constexpr int EA = CP_HA * CP_NB * CIN, EB = CP_NA * CP_HB * CIN;
+  constexpr int IA = (EA + 255) / 256, IB = (EB + 255) / 256;
+  float ra[IA], rb[IB];
+#pragma unroll
+  for (int k = 0; k < IA; ++k) {  // a halo box at the tile's b positions
+    const int i = t + 256 * k;
     const int c = i % CIN, p = i / CIN;
     const int bi = p % CP_NB, ai = p / CP_NB;
     const int ha = ha0 - 1 + ai / (CP_TAW + 2), wa = wa0 - 1 + ai % (CP_TAW + 2);
     const int hb = hb0 + bi / CP_TBW, wb = wb0 + bi % CP_TBW;
-    float v = 0.f;
-    if ((unsigned)ha < (unsigned)hA && (unsigned)wa < (unsigned)wA && hb < hB && wb < wB)
-      v = x[xoff + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + c];
-    xa[ai][bi][c] = v;
+    const bool in = i < EA && (unsigned)ha < (unsigned)hA && (unsigned)wa < (unsigned)wA && hb < hB && wb < wB;
+    ra[k] = in ? x[xoff + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + c] : 0.f;
   }
-  // b halo box at the tile's a positions
-  for (int i = t; i < CP_NA * CP_HB * CIN; i += 256) {
+#pragma unroll
+  for (int k = 0; k < IB; ++k) {  // b halo box at the tile's a positions
+    const int i = t + 256 * k;
     const int c = i % CIN, p = i / CIN;
     const int bi = p % CP_HB, ai = p / CP_HB;
     const int ha = ha0 + ai / CP_TAW, wa = wa0 + ai % CP_TAW;
     const int hb = hb0 - 1 + bi / (CP_TBW + 2), wb = wb0 - 1 + bi % (CP_TBW + 2);
-    float v = 0.f;
-    if (ha < hA && wa < wA && (unsigned)hb < (unsigned)hB && (unsigned)wb < (unsigned)wB)
-      v = x[xoff + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + c];
-    xb[ai][bi][c] = v;
+    const bool in = i < EB && ha < hA && wa < wA && (unsigned)hb < (unsigned)hB && (unsigned)wb < (unsigned)wB;
+    rb[k] = in ? x[xoff + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + c] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < IA; ++k) {
+    const int i = t + 256 * k;
+    if (i < EA) {
+      const int c = i % CIN, p = i / CIN;
+      xa[p / CP_NB][(p % CP_NB) * CIN + c] = ra[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < IB; ++k) {
+    const int i = t + 256 * k;
+    if (i < EB) (&xb[0][0][0])[i] = rb[k];
   }
   __syncthreads();
   const int ai = t / CP_NB, bi = t % CP_NB;  // this thread's pair within the tile
@@ -150,13 +171,12 @@ __global__ __launch_bounds__(256) void cp4d_layer_kernel(const float* __restrict
   const int hb = hb0 + bi / CP_TBW, wb = wb0 + bi % CP_TBW;
   float acc[COUT];
 #pragma unroll
-  for (int o = 0; o < COUT; ++o) acc[o] = bl[o];
+  for (int o = 0; o < COUT; ++o) acc[o] = ba[o] + bb[o];
   const int aiy = ai / CP_TAW, aix = ai % CP_TAW, biy = bi / CP_TBW, bix = bi % CP_TBW;
-#pragma unroll
-  for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const float* pa = xa[(aiy + ky) * (CP_TAW + 2) + aix + kx][bi];
+#pragma unroll 1
+  for (int tap = 0; tap < 9; ++tap) {  // one tap's inputs and weights live at a time
+      const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+      const float* pa = &xa[(aiy + ky) * (CP_TAW + 2) + aix + kx][bi * CIN];
       const float* pb = xb[ai][(biy + ky) * (CP_TBW + 2) + bix + kx];
       float va[CIN], vb[CIN];
 #pragma unroll
@@ -165,12 +185,21 @@ __global__ __launch_bounds__(256) void cp4d_layer_kernel(const float* __restrict
         vb[c] = pb[c];
       }
 #pragma unroll
-      for (int o = 0; o < COUT; ++o)
+      for (int c = 0; c < CIN; ++c) {
+        const float* w0 = wl[0][tap][c];
+        const float* w1 = wl[1][tap][c];
 #pragma unroll
-        for (int c = 0; c < CIN; ++c) {
-          acc[o] = fmaf(wl[0][o][c * 9 + ky * 3 + kx], va[c], acc[o]);
-          acc[o] = fmaf(wl[1][o][c * 9 + ky * 3 + kx], vb[c], acc[o]);
+        for (int o4 = 0; o4 < CO4; o4 += 4) {
+          const f32x4 a4 = *(const f32x4*)(w0 + o4), b4 = *(const f32x4*)(w1 + o4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (o4 + q < COUT) {
+              acc[o4 + q] = fmaf(a4[q], va[c], acc[o4 + q]);
+              acc[o4 + q] = fmaf(b4[q], vb[c], acc[o4 + q]);
+            }
         }
+        if (c & 1) __builtin_amdgcn_sched_barrier(0);  // bounds the weight reads in flight (registers)
+      }
     }
   if (ha < hA && wa < wA && hb < hB && wb < wB) {
     float* yp = y + (long)blockIdx.z * NA * NB * COUT + ((long)(ha * wA + wa) * NB + hb * wB + wb) * COUT;
@@ -236,6 +265,133 @@ __global__ __launch_bounds__(256) void match_vt_kernel(const float* __restrict__
     const int c = c0 + r, j = j0 + tx;
     if (c < C && j < ldp) vt[((long)b * C + c) * ldp + j] = tile[tx][r];
   }
+}
+
+// ---- WeightAverage (src/model/msm/msm_func.py:50-104), R = 3 ----
+// tpg [N][P][3co]: theta | phi | g of every pixel (1x1 convs as one GEMM, biases not yet
+// added); per pixel: cos_r = CosineSimilarity(phi(x_r), theta(x)) over its 3x3 replicate-padded
+// neighbourhood r (torch: dot / (max(|phi|, 1e-8) max(|theta|, 1e-8))), softmax over the 9,
+// wavg = sum_r softmax_r g(x_r).  One workgroup per pixel, co / 256 channels per thread.
+template <int CPT>
+__global__ __launch_bounds__(256) void wa_attn_kernel(const float* __restrict__ tpg, int h, int w, int co,
+                                                      const float* __restrict__ bt, const float* __restrict__ bp,
+                                                      const float* __restrict__ bg, float* __restrict__ wavg) {
+  const long P = (long)h * w;
+  const long pix = blockIdx.x;  // n * P + p
+  const long n = pix / P;
+  const int p = (int)(pix - n * P), y = p / w, x = p - y * w;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const long ld = 3L * co;
+  __shared__ float red[4][19];
+  __shared__ float sm[9];
+  float th[CPT];
+  const float* tp = tpg + pix * ld;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) th[k] = tp[t + 256 * k] + bt[t + 256 * k];
+  float part[19];
+  part[18] = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) part[18] = fmaf(th[k], th[k], part[18]);
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    const int yy = min(max(y + r / 3 - 1, 0), h - 1), xx = min(max(x + r % 3 - 1, 0), w - 1);
+    const float* q = tpg + (n * P + (long)yy * w + xx) * ld + co;
+    float d = 0.f, nn = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const float ph = q[t + 256 * k] + bp[t + 256 * k];
+      d = fmaf(ph, th[k], d);
+      nn = fmaf(ph, ph, nn);
+    }
+    part[r] = d;
+    part[9 + r] = nn;
+  }
+#pragma unroll
+  for (int i = 0; i < 19; ++i) {
+    const float v = wave_sum_dpp(part[i]);
+    if (lane == 0) red[wv][i] = v;
+  }
+  __syncthreads();
+  if (t == 0) {
+    float tot[19];
+#pragma unroll
+    for (int i = 0; i < 19; ++i) tot[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    const float tn = fmaxf(sqrtf(tot[18]), 1e-8f);
+    float cs[9], m = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      cs[r] = tot[r] / (fmaxf(sqrtf(tot[9 + r]), 1e-8f) * tn);
+      m = fmaxf(m, cs[r]);
+    }
+    float se = 0.f;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      cs[r] = expf(cs[r] - m);
+      se += cs[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 9; ++r) sm[r] = cs[r] / se;
+  }
+  __syncthreads();
+  float acc[CPT];
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) acc[k] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    const int yy = min(max(y + r / 3 - 1, 0), h - 1), xx = min(max(x + r % 3 - 1, 0), w - 1);
+    const float* q = tpg + (n * P + (long)yy * w + xx) * ld + 2 * co;
+    const float a = sm[r];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) acc[k] = fmaf(a, q[t + 256 * k] + bg[t + 256 * k], acc[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) wavg[pix * co + t + 256 * k] = acc[k];
+}
+
+// out = x + (back + b): conv_back's bias and WeightAverage's residual (msm_func.py:99-104)
+__global__ void wa_residual_kernel(const float* __restrict__ x, const float* __restrict__ back,
+                                   const float* __restrict__ b, long n, int C, float* __restrict__ out) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    out[i] = x[i] + (back[i] + b[i % C]);
+}
+
+// MMN.forward's tail (mmn.py:65-67): att_mean = mean over the B support rows of att_fq;
+// fq = f_q * (1 - att_wt) + att_mean * att_wt.  Tokens [B][P][C] / [P][C].
+__global__ void mmn_blend_kernel(const float* __restrict__ fq_in, const float* __restrict__ att, int B, long n,
+                                 float att_wt, float* __restrict__ att_mean, float* __restrict__ fq_out) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += att[(long)b * n + i];
+    const float m = s / (float)B;
+    att_mean[i] = m;
+    fq_out[i] = fq_in[i] * (1.f - att_wt) + m * att_wt;
+  }
+}
+
+int launch_wa_attn(const float* tpg, int N, int h, int w, int co, const float* bt, const float* bp, const float* bg,
+                   float* wavg, hipStream_t st) {
+  const dim3 grid((unsigned)((long)N * h * w));
+  if (co == 256) hipLaunchKernelGGL((wa_attn_kernel<1>), grid, dim3(256), 0, st, tpg, h, w, co, bt, bp, bg, wavg);
+  else if (co == 512) hipLaunchKernelGGL((wa_attn_kernel<2>), grid, dim3(256), 0, st, tpg, h, w, co, bt, bp, bg, wavg);
+  else if (co == 1024) hipLaunchKernelGGL((wa_attn_kernel<4>), grid, dim3(256), 0, st, tpg, h, w, co, bt, bp, bg, wavg);
+  else return fail(CWT_EARG, "WeightAverage: c_in / 2 must be 256, 512 or 1024");
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_wa_residual(const float* x, const float* back, const float* b, long n, int C, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(wa_residual_kernel, dim3((unsigned)std::min<long>(65536, cdiv(n, 256))), dim3(256), 0, st, x,
+                     back, b, n, C, out);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_mmn_blend(const float* fq_in, const float* att, int B, long n, float att_wt, float* att_mean, float* fq_out,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(mmn_blend_kernel, dim3((unsigned)std::min<long>(65536, cdiv(n, 256))), dim3(256), 0, st, fq_in,
+                     att, B, n, att_wt, att_mean, fq_out);
+  CWT_LAUNCH_CHECK();
+  return 0;
 }
 
 int launch_mutual_matching(const float* x, int B, int NA, int NB, int C, float* y, float* rowmax, float* colpart,

@@ -6,12 +6,16 @@ HIP kernels (csrc/match.hip) behind the C ABI:
                                                src/model/conv4d.py:11-62)
   MatchNet(temp, cv_type, in_channel, ...)     src/model/match.py:88-163 (forward, corr_forward,
                                                run_match_model)
+  WeightAverage(c_in, args)                    src/model/msm/msm_func.py:50-104
+  MMN(args, agg, wa, red_dim)                  src/model/mmn.py:11-71 (forward)
 
 The modules keep the reference's parameter names (``NeighConsensus.conv.{0,2,4}.conv{1,2}.
 {weight,bias}``), so a reference state_dict loads as is.  Built: the default head of every MMN /
 MatchNet script -- CenterPivotConv4d ('red'), kernel sizes [3, 3, 3], channels [10, 10, 1],
-in_channel 1 or 2, symmetric or not -- forward only (inference).  Not built: the full Conv4d
-('cv4'), the spatial context encoder (sce), the cycle-consistency mask (cyc) and ig_mask.
+in_channel 1 or 2, symmetric or not -- and the MMN head of the mmn configs (rmid 'l34', all_lr
+'l', agg 'cat', wa True, red_dim False), forward only (inference).  Not built: the full Conv4d
+('cv4'), the spatial context encoder (sce), the cycle-consistency mask (cyc), ig_mask, agg 'sum',
+red_dim, forward_mmn (its MSBlock) and the MMN trainers' backward.
 
 Parity is unpinned: the reference cannot be run here and holds no fixtures for
 this head; tests/test_gpu_match.py checks it against oracle/match_oracle.py, a float64
@@ -161,6 +165,117 @@ def init_match_params(mod: torch.nn.Module, seed: int = 0) -> None:
     g = torch.Generator().manual_seed(seed)
     with torch.no_grad():
         for name, p in mod.named_parameters():
-            fan_in = p.shape[1] * 9 if p.dim() == 4 else 10
+            fan_in = p.shape[1] * p.shape[2] * p.shape[3] if p.dim() == 4 else 100
             bound = 1.0 / math.sqrt(fan_in)
             p.copy_((torch.rand(p.shape, generator=g, dtype=torch.float32) * 2 - 1) * bound)
+
+
+class WeightAverage(torch.nn.Module):
+    """msm_func.py:50-104 (R = 3): x + conv_back(softmax-weighted g over the 3x3 replicate-padded
+    neighbourhood, weights = cosine similarity of phi(neighbour) and theta(x)).  Parameter names
+    conv_theta / conv_phi / conv_g / conv_back as the reference."""
+
+    def __init__(self, c_in: int, args=None, R: int = 3, device=None):
+        super().__init__()
+        if R != 3:
+            raise NotImplementedError("WeightAverage: R = 3 only")
+        for k in ("att_drop", "proj_drop"):
+            p = (args.get(k, 0.0) if isinstance(args, dict) else getattr(args, k, 0.0)) if args is not None else 0.0
+            if p:
+                raise NotImplementedError("WeightAverage: att_drop / proj_drop are identities here (eval)")
+        c_out = c_in // 2
+        self.c_in, self.c_out, self.R = c_in, c_out, R
+        self.conv_theta = torch.nn.Conv2d(c_in, c_out, 1, device=device)
+        self.conv_phi = torch.nn.Conv2d(c_in, c_out, 1, device=device)
+        self.conv_g = torch.nn.Conv2d(c_in, c_out, 1, device=device)
+        self.conv_back = torch.nn.Conv2d(c_out, c_in, 1, device=device)
+        self._w, self._key = None, None
+
+    def _weights(self):
+        ps = [self.conv_theta.weight, self.conv_phi.weight, self.conv_g.weight, self.conv_back.weight]
+        key = tuple((p.data_ptr(), p._version) for p in ps)
+        if self._w is None or key != self._key:
+            with torch.no_grad():
+                tpg = torch.cat([p.detach().reshape(self.c_out, self.c_in) for p in ps[:3]]).contiguous()
+                back = ps[3].detach().reshape(self.c_in, self.c_out).contiguous()
+            self._w, self._key = (tpg, back), key
+        return self._w
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        _lib.require(x, "x")
+        N, C, h, w = x.shape
+        if C != self.c_in:
+            raise ValueError(f"expected {self.c_in} channels, got {C}")
+        xt = as_tokens(x)
+        tpg, back = self._weights()
+        out = torch.empty((N, C, h, w), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
+        _lib.check(_lib.lib().cwt_weight_average(
+            _lib.ctx(x.device.index), _lib.ptr(xt), N, h, w, C, _lib.ptr(tpg), _lib.ptr(self.conv_theta.bias),
+            _lib.ptr(self.conv_phi.bias), _lib.ptr(self.conv_g.bias), _lib.ptr(back), _lib.ptr(self.conv_back.bias),
+            _lib.ptr(out), _lib.stream_ptr(x.device)), "cwt_weight_average")
+        return out
+
+
+def _get(args, k, default=None):
+    if isinstance(args, dict):
+        return args.get(k, default)
+    return getattr(args, k, default)
+
+
+class MMN(torch.nn.Module):
+    """mmn.py:11-71: per-layer WeightAverage, the 4-D correlation of every (query, support)
+    layer feature pair stacked as channels, MatchNet.corr_forward over it with v = f_s, and the
+    blend fq = f_q * (1 - att_wt) + mean_shots(att_fq) * att_wt."""
+
+    def __init__(self, args, agg: str = "cat", wa: bool = False, red_dim=False, device=None):
+        super().__init__()
+        if agg != "cat":
+            raise NotImplementedError("MMN: agg 'cat' only")
+        if red_dim:
+            raise NotImplementedError("MMN: red_dim is not built")
+        self.args, self.agg, self.wa, self.red_dim = args, agg, wa, red_dim
+        rmid = str(_get(args, "rmid"))
+        self.bid_lst = [int(c) for c in rmid[1:]]
+        layers = int(_get(args, "layers", 50))
+        self.nbottlenecks = [3, 4, 6, 3] if layers == 50 else [3, 4, 23, 3]
+        self.feature_channels = [256, 512, 1024, 2048]
+        all_lr = str(_get(args, "all_lr", "l"))
+        if any(str(i) in all_lr for i in self.bid_lst):
+            raise NotImplementedError("MMN: every-bottleneck features (all_lr naming a layer) are not built")
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if wa:
+            for bid in self.bid_lst:
+                setattr(self, "wa_" + str(bid), WeightAverage(self.feature_channels[bid - 1], args, device=dev))
+        match_ch = len(self.bid_lst)
+        self.att_wt = float(_get(args, "att_wt", 0.2))
+        self.corr_net = MatchNet(temp=float(_get(args, "temp", 20.0)), cv_type=str(_get(args, "conv4d", "red")),
+                                 sce=False, cyc=False, sym_mode=True, in_channel=match_ch, device=dev)
+
+    def forward(self, fq_lst, fs_lst, f_q, f_s, ret_attn: bool = False):
+        """mmn.py:42-71: fq_lst / fs_lst {layer: [feature]} (extract_features with rmid),
+        f_q [1, C, h, w], f_s [B, C, h, w] -> (fq, att_fq) [or (attn, fq, att_fq)]."""
+        B, ch, h, w = f_s.shape
+        P = h * w
+        L = len(self.bid_lst)
+        corr4d = torch.empty((B, L, P, P), device=f_s.device, dtype=torch.float32)
+        for li, idx in enumerate(self.bid_lst[::-1]):
+            fq_fea, fs_fea = fq_lst[idx][0], fs_lst[idx][0]
+            if self.wa:
+                m = getattr(self, "wa_" + str(idx))
+                fq_fea, fs_fea = m(fq_fea), m(fs_fea)   # the query once: its B expanded copies are equal
+            for b in range(B):
+                qt, kt = as_tokens(fq_fea[:1] if fq_fea.shape[0] == 1 else fq_fea[b:b + 1]), as_tokens(fs_fea[b:b + 1])
+                C = qt.shape[1]
+                _lib.check(_lib.lib().cwt_corr(_lib.ctx(f_s.device.index), _lib.ptr(qt), _lib.ptr(kt), 1, P, P, C,
+                                               _lib.ptr(corr4d[b, li]), _lib.stream_ptr(f_s.device)), "cwt_corr")
+        attn, att = self.corr_net._run(corr4d, h, w, f_s)   # att [B, Cv, h, w] (channels_last)
+        att_t = as_tokens(att)
+        fqt = as_tokens(f_q)
+        att_fq = torch.empty((1, ch, h, w), device=f_s.device, dtype=torch.float32, memory_format=torch.channels_last)
+        fq = torch.empty_like(att_fq)
+        _lib.check(_lib.lib().cwt_mmn_blend(_lib.ctx(f_s.device.index), _lib.ptr(fqt), _lib.ptr(att_t), B, P * ch,
+                                            self.att_wt, _lib.ptr(att_fq), _lib.ptr(fq), _lib.stream_ptr(f_s.device)),
+                   "cwt_mmn_blend")
+        if ret_attn:
+            return attn, fq, att_fq
+        return fq, att_fq

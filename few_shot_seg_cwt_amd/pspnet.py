@@ -69,6 +69,14 @@ class PSPNet:
         self.conv_dtype = str(_arg(args, "conv_dtype", "fp32"))
         if self.conv_dtype not in self._PRECISION:
             raise ValueError(f"conv_dtype must be one of {sorted(self._PRECISION)}")
+        # per-layer features for the MMN / MatchNet variants (pspnet.py:172-181): returned when
+        # rmid names layers ('l34', 'mid3', ...); get_feat_list keeps each layer's last block
+        # (all_lr 'l'; every block of a named layer is not built)
+        self.rmid = _arg(args, "rmid", None)
+        self.all_lr = str(_arg(args, "all_lr", "l"))
+        self.mid_features = self.rmid is not None and ("l" in str(self.rmid) or "mid" in str(self.rmid))
+        if self.mid_features and any(ch.isdigit() for ch in self.all_lr):
+            raise NotImplementedError("all_lr naming layers (every bottleneck's features) is not built")
 
     _PRECISION = {"fp32": 0, "bf16": 1}  # CWT_CONV_FP32 / CWT_CONV_BF16 (include/cwt.h)
 
@@ -169,7 +177,8 @@ class PSPNet:
 
     # -- hot path ------------------------------------------------------------------------
     def extract_features(self, x: torch.Tensor, out: torch.Tensor | None = None):
-        """pspnet.py:172-181: returns (f [N,512,h,w] channels_last, [])."""
+        """pspnet.py:172-181: returns (f [N,512,h,w] channels_last, []), or with an rmid naming
+        layers (f, {2: [layer2], 3: [layer3], 4: [layer4]}) (channels_last, fp32)."""
         if self._state is None:
             raise RuntimeError("load_state_dict first")
         _lib.require(x, "x")
@@ -184,6 +193,8 @@ class PSPNet:
                               memory_format=torch.channels_last)
         if x.device != self.device:
             raise ValueError(f"x is on {x.device}, the backbone on {self.device}")
+        if self.training and self.mid_features:
+            raise NotImplementedError("per-layer features (rmid) are built for the eval-mode extractor only")
         if self.training:
             seed = dropout_seed()   # Dropout2d masks; the host RNG stream stays the reference's
             _lib.check(_lib.lib().cwt_extract_features_train_bn(
@@ -191,6 +202,13 @@ class PSPNet:
                 self.dropout_p, seed, _lib.stream_ptr(x.device)), "cwt_extract_features_train_bn")
             self._stats_moved = True
             return out, []
+        if self.mid_features:
+            mids = {lid: torch.empty((N, c, h, h), device=x.device, dtype=torch.float32,
+                                     memory_format=torch.channels_last) for lid, c in ((2, 512), (3, 1024), (4, 2048))}
+            _lib.check(_lib.lib().cwt_extract_features_mid(
+                _lib.ctx(x.device.index), self._handle, _lib.ptr(x), N, S, _lib.ptr(out), _lib.ptr(mids[2]),
+                _lib.ptr(mids[3]), _lib.ptr(mids[4]), _lib.stream_ptr(x.device)), "cwt_extract_features_mid")
+            return out, {lid: [t] for lid, t in mids.items()}
         _lib.check(_lib.lib().cwt_extract_features(_lib.ctx(x.device.index), self._handle, _lib.ptr(x), N, S,
                                                    _lib.ptr(out),
                                                    _lib.stream_ptr(x.device)), "cwt_extract_features")

@@ -107,6 +107,14 @@ int cwt_extract_features(cwt_ctx* ctx, const cwt_backbone* bb, const float* img,
  * N >= 2 (the PPM bin-1 BatchNorm sees N values; torch raises for 1).  Not thread-safe
  * against concurrent extractions with the same backbone.
  */
+/* extract_features with the per-layer features (pspnet.py:172-181 with an rmid of 'l..' /
+ * 'mid', get_feat_list :272-287 with all_lr 'l': the last block of each layer): as
+ * cwt_extract_features, plus fp32 NHWC copies of the outputs of layer2, layer3 and layer4
+ * ([N][h][h][512 / 1024 / 2048], h = the feature side) into l2 / l3 / l4 (each may be NULL).
+ * Eval-mode BN. */
+int cwt_extract_features_mid(cwt_ctx* ctx, const cwt_backbone* bb, const float* img, int N, int S, float* feat,
+                             float* l2, float* l3, float* l4, void* stream);
+
 int cwt_extract_features_train_bn(cwt_ctx* ctx, cwt_backbone* bb, const float* img, int N, int S,
                                   float* feat, float momentum, float dropout_p, uint64_t seed,
                                   void* stream);
@@ -344,6 +352,23 @@ int cwt_mutual_matching(cwt_ctx* ctx, const float* x, int B, int NA, int NB, int
 int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
                            int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
                            void* stream);
+
+/* WeightAverage (src/model/msm/msm_func.py:50-104, R = 3; the MMN head's wa_<layer> modules,
+ * mmn.py:27-34,53-55): x device [N][h][w][C] (NHWC tokens), C = c_in in {512, 1024, 2048};
+ * w_tpg device [3 C/2][C] = conv_theta.weight, conv_phi.weight, conv_g.weight stacked (each
+ * [C/2][C]); b_theta / b_phi / b_g device [C/2]; w_back device [C][C/2], b_back device [C].
+ * out device [N][h][w][C] = x + conv_back(sum_r softmax_r(cos(phi(x_r), theta(x))) g(x_r)) over
+ * the 3x3 replicate-padded neighbourhood r (CosineSimilarity: dot / (max|a| max|b|), eps 1e-8).
+ * Dropouts are identities (att_drop / proj_drop default 0, eval).  Exact fp32. */
+int cwt_weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C, const float* w_tpg,
+                       const float* b_theta, const float* b_phi, const float* b_g, const float* w_back,
+                       const float* b_back, float* out, void* stream);
+
+/* MMN.forward's tail (src/model/mmn.py:65-67): att_fq device [B][n] (the B support rows'
+ * weighted query features, n = h*w*C), f_q device [n]; att_mean device [n] = mean over B;
+ * fq_out device [n] = f_q * (1 - att_wt) + att_mean * att_wt. */
+int cwt_mmn_blend(cwt_ctx* ctx, const float* f_q, const float* att_fq, int B, int64_t n, float att_wt,
+                  float* att_mean, float* fq_out, void* stream);
 
 /* torch.optim.SGD(momentum, dampening 0, weight_decay, nesterov) step over one flat
  * fp32 parameter buffer (optimizer.py:8-15): buf = m*buf + (g + wd*p) (buf = g+wd*p on

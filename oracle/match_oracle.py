@@ -79,3 +79,57 @@ def layers_from_state(sd, prefix: str = "NeighConsensus.conv.", dtype=torch.floa
         p = f"{prefix}{i}."
         out.append(tuple(sd[p + n].to(dtype) for n in ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias")))
     return out
+
+
+def weight_average(x: torch.Tensor, p) -> torch.Tensor:
+    """msm_func.py:50-104 (R = 3, dropouts off): p = (w_theta, b_theta, w_phi, b_phi, w_g, b_g,
+    w_back, b_back) as nn.Conv2d 1x1 weights / biases."""
+    wt, bt, wp, bp, wg, bg, wb, bb = p
+    B, C, h, w = x.shape
+    xp = F.pad(x, (1, 1, 1, 1), mode="replicate")
+    theta = F.conv2d(x, wt, bt)
+    cos, gs = [], []
+    for dy in range(3):
+        for dx in range(3):
+            nb = xp[:, :, dy:dy + h, dx:dx + w]      # the neighbour at offset (dy - 1, dx - 1)
+            cos.append(F.cosine_similarity(F.conv2d(nb, wp, bp), theta, dim=1))
+            gs.append(F.conv2d(nb, wg, bg))
+    sm = torch.softmax(torch.stack(cos, 1), dim=1)            # [B, 9, h, w]
+    wavg = sum(sm[:, r:r + 1] * gs[r] for r in range(9))
+    return x + F.conv2d(wavg, wb, bb)
+
+
+def feat_list(x: torch.Tensor, sd, layers: int = 50):
+    """get_feat_list (pspnet.py:272-287) with all_lr 'l': {2, 3, 4: the layer's last block output}."""
+    from oracle.cwt_oracle import RESNET_BLOCKS, bottleneck, stem
+    x = stem(x, sd)
+    out = {}
+    for li, nblk in enumerate(RESNET_BLOCKS[layers], start=1):
+        for b in range(nblk):
+            x = bottleneck(x, sd, li, b)
+        if li >= 2:
+            out[li] = x
+    return out
+
+
+def mmn_forward(fq_lst, fs_lst, f_q, f_s, bid_lst, wa_params, layers, temp: float, att_wt: float):
+    """mmn.py:42-71 with agg 'cat', red_dim False: fq_lst / fs_lst {layer: feature}, wa_params
+    {layer: weight_average params} or None -> (fq, att_fq)."""
+    B, ch, h, w = f_s.shape
+    corrs = []
+    for idx in bid_lst[::-1]:
+        fq, fs = fq_lst[idx].expand(B, -1, -1, -1), fs_lst[idx]
+        if wa_params is not None:
+            fq, fs = weight_average(fq, wa_params[idx]), weight_average(fs, wa_params[idx])
+        bq = F.normalize(fq.reshape(B, fq.shape[1], h * w), dim=1)
+        bs = F.normalize(fs.reshape(B, fs.shape[1], h * w), dim=1)
+        corrs.append(torch.bmm(bq.transpose(1, 2), bs).reshape(B, 1, h, w, h, w))
+    _, att = corr_forward(torch.cat(corrs, 1), f_s, layers, temp, True)
+    att = att.mean(dim=0, keepdim=True)
+    return f_q * (1 - att_wt) + att * att_wt, att
+
+
+def wa_params_from_state(sd, prefix: str, dtype=torch.float64):
+    return tuple(sd[prefix + n].to(dtype) for n in ("conv_theta.weight", "conv_theta.bias", "conv_phi.weight",
+                                                     "conv_phi.bias", "conv_g.weight", "conv_g.bias",
+                                                     "conv_back.weight", "conv_back.bias"))

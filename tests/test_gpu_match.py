@@ -86,3 +86,71 @@ def test_forward_from_features_and_state_dict_keys(dev):
     e = rel(wv, wvo)
     print(f"MatchNet.forward: {e:.2e}")
     assert e < TOL
+
+
+@pytest.mark.parametrize("N,C,h,w", [(2, 512, 9, 11), (1, 2048, 7, 7), (1, 1024, 6, 5)])
+def test_weight_average(dev, N, C, h, w):
+    """msm_func.py:50-104 (R 3) against the float64 restatement."""
+    from few_shot_seg_cwt_amd.match import WeightAverage, init_match_params
+    from oracle import match_oracle as M
+    m = WeightAverage(C, {}, device=dev)
+    init_match_params(m, seed=C + h)
+    g = torch.Generator().manual_seed(C)
+    x = torch.rand(N, C, h, w, generator=g).to(dev)
+    y = m(x)
+    sd = {k: t.cpu() for k, t in m.state_dict().items()}
+    yo = M.weight_average(x.double().cpu(), M.wa_params_from_state(sd, ""))
+    e = rel(y, yo)
+    print(f"WeightAverage N={N} C={C} {h}x{w}: {e:.2e}")
+    assert e < TOL
+
+
+def test_mmn_forward(dev):
+    """mmn.py:42-71 (rmid l34, all_lr l, agg cat, wa True) on random layer features, 2 shots."""
+    from few_shot_seg_cwt_amd.match import MMN, init_match_params
+    from oracle import match_oracle as M
+    args = dict(rmid="l34", layers=50, all_lr="l", temp=20.0, att_wt=0.2, conv4d="red")
+    net = MMN(args, agg="cat", wa=True, red_dim=False, device=dev)
+    init_match_params(net, seed=5)
+    g = torch.Generator().manual_seed(23)
+    h = 8
+    fq_lst = {3: [torch.rand(1, 1024, h, h, generator=g).to(dev)], 4: [torch.rand(1, 2048, h, h, generator=g).to(dev)]}
+    fs_lst = {3: [torch.rand(2, 1024, h, h, generator=g).to(dev)], 4: [torch.rand(2, 2048, h, h, generator=g).to(dev)]}
+    f_q = torch.rand(1, 512, h, h, generator=g).to(dev)
+    f_s = torch.rand(2, 512, h, h, generator=g).to(dev)
+    fq, att_fq = net(fq_lst, fs_lst, f_q, f_s)
+    sd = {k: t.cpu() for k, t in net.state_dict().items()}
+    wa = {b: M.wa_params_from_state(sd, f"wa_{b}.") for b in (3, 4)}
+    layers = M.layers_from_state(sd, prefix="corr_net.NeighConsensus.conv.")
+    d = lambda t: t.double().cpu()  # noqa: E731
+    fqo, atto = M.mmn_forward({k: d(v[0]) for k, v in fq_lst.items()}, {k: d(v[0]) for k, v in fs_lst.items()},
+                              d(f_q), d(f_s), [3, 4], wa, layers, 20.0, 0.2)
+    errs = dict(fq=rel(fq, fqo), att_fq=rel(att_fq, atto))
+    print(f"MMN.forward: {errs}")
+    assert max(errs.values()) < TOL, errs
+
+
+def test_extract_mid_features(dev):
+    """extract_features with rmid 'l34' (pspnet.py:172-181): the layer2/3/4 outputs beside the
+    usual feature map, against the oracle's float64 backbone (bf16x3 convs: bar 1e-4)."""
+    from few_shot_seg_cwt_amd import PSPNet
+    from few_shot_seg_cwt_amd import synthetic as syn
+    from oracle import match_oracle as M
+    from oracle.cwt_oracle import to_torch_state
+    sd = syn.make_pspnet_state(50, 2021)
+    args = dict(layers=50, rmid="l34", all_lr="l")
+    net = PSPNet(args)
+    net.load_state_dict(sd)
+    x = torch.from_numpy(syn.normal(2021, "mid_img", (2, 3, 65, 65), 1.0)).to(dev)
+    f, lst = net.extract_features(x)
+    plain = PSPNet(dict(layers=50))
+    plain.load_state_dict(sd)
+    f0, empty = plain.extract_features(x)
+    torch.cuda.synchronize()
+    assert empty == [] and sorted(lst) == [2, 3, 4]
+    assert torch.equal(f, f0)
+    sd64 = {k: v.double() for k, v in to_torch_state(sd).items()}
+    ref = M.feat_list(x.double().cpu(), sd64, 50)
+    errs = {k: rel(lst[k][0], ref[k]) for k in (2, 3, 4)}
+    print(f"mid features: {errs}")
+    assert max(errs.values()) < 1e-4, errs
