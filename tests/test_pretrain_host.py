@@ -194,3 +194,47 @@ def test_pretrain_state_dict_keeps_reference_key_order(tmp_path):
         assert torch.equal(by_pos[k], back[k]), k
         if k != "gamma":
             assert torch.equal(by_name[k], back[k]), k
+
+
+@pytest.mark.parametrize("N,S,structured", [(4, 65, False), (16, 65, False), (8, 129, True)])
+def test_whole_step_gradient_is_ill_conditioned_in_the_reference_math(N, S, structured):
+    """Why the whole-step GPU test (test_gpu_pretrain.py) cannot hold every gradient to a flat
+    1e-3 / 1e-2: the reference's own computation (the oracle's torch autograd of pretrain.py:104-121)
+    in fp32 moves most parameter gradients of this network by more than 1e-2 against the same
+    computation in float64, for random batches, for larger batches (N = 16: BN over more values) and
+    for structured, learnable batches (class-coloured blocks, so the gradient is not pure noise
+    cancellation).  Training-mode BN backward (dx = g/sigma (dy - mean dy - xhat mean(dy xhat))) over
+    ~50 layers amplifies rounding.  The chain is therefore pinned stage by stage instead
+    (test_gpu_pretrain_chain.py: each stage recomputed in float64 from the HIP step's own inputs,
+    masks and upstream gradient, every gradient at 1e-4); the whole step is held to
+    max(1e-3, 8 x this spread) per tensor.  Measured here, fp32 vs float64 of the reference math:
+    the count of tensors whose spread exceeds 1e-2 is asserted to be a majority."""
+    from oracle.pretrain_oracle import pretrain_step
+    torch.set_num_threads(min(8, torch.get_num_threads()))
+    nc, layers = 16, 50
+    state = syn.make_pspnet_state(layers, 2021, num_classes_tr=nc)
+    sd32 = {k: torch.from_numpy(np.array(v, dtype=np.float32 if v.dtype != np.int64 else np.int64))
+            for k, v in state.items()}
+    sd64 = {k: (v.double() if v.dtype == torch.float32 else v) for k, v in sd32.items()}
+    if structured:
+        blk, g = 32, (S + 31) // 32
+        cls = (syn.uniform01(2021, "sb_cls", N * g * g) * nc).astype(np.int64).reshape(N, g, g)
+        t = np.repeat(np.repeat(cls, blk, 1), blk, 2)[:, :S, :S]
+        col = syn.normal(2021, "sb_col", (nc, 3), 1.0)
+        x = col[t].transpose(0, 3, 1, 2) + syn.normal(2021, "sb_noise", (N, 3, S, S), 0.1)
+        x, t = torch.from_numpy(x.astype(np.float32)), torch.from_numpy(t)
+    else:
+        x = torch.from_numpy(syn.normal(2021, "pt_img", (N, 3, S, S), 1.0))
+        t = torch.from_numpy((syn.uniform01(2021, "pt_lbl", N * S * S) * nc).astype(np.int64).reshape(N, S, S))
+    _, g32, _, _ = pretrain_step(sd32, x, t, nc, layers)
+    _, g64, _, _ = pretrain_step(sd64, x.double(), t, nc, layers)
+
+    def rel(a, b):
+        a, b = a.double().numpy(), b.double().numpy()
+        return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+    spread = np.array([rel(g32[k], g64[k]) for k in g64])
+    print(f"N={N} S={S} structured={structured}: reference-math fp32 vs fp64 gradient spread: "
+          f"{int((spread > 1e-2).sum())} of {spread.size} tensors above 1e-2, max {spread.max():.3g}, "
+          f"median {np.median(spread):.3g}")
+    assert (spread > 1e-2).sum() > spread.size // 2
