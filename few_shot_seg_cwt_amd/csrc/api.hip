@@ -1633,7 +1633,7 @@ int cwt_debug_adapt_spin_limit(cwt_ctx* ctx, int64_t limit) {
 
 int cwt_ctx_set_adapt_units(cwt_ctx* ctx, int units_per_workgroup) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
-  CWT_CHECK(units_per_workgroup >= 0 && units_per_workgroup <= 2, "units per workgroup must be 0 (automatic), 1 or 2");
+  CWT_CHECK(units_per_workgroup >= 0 && units_per_workgroup <= 3, "units per workgroup must be 0 (automatic), 1, 2 or 3");
   ctx->adapt_upw = units_per_workgroup;
   return 0;
 }

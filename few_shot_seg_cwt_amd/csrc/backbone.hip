@@ -7,6 +7,7 @@
 //    a separable interpolation of their per-tap products   (pspnet.py:19-38,124-128); the
 //    concat buffer of the reference (torch.cat) is never materialised
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.h"
@@ -135,11 +136,118 @@ __global__ __launch_bounds__(256) void stem_conv1_s_kernel(const float* __restri
   }
 }
 
+// The stem conv on the exact f32 matrix cores (round 3).  K = 27 taps (padded to 28) x 64
+// output channels x 16 pixels per wave step: D[16 ch][16 pix] = W[16 ch][4 k] . I[4 k][16 pix]
+// by v_mfma_f32_16x16x4_f32 (an fmaf chain per output, so plain fp32 arithmetic), 7 k-steps x
+// 4 channel blocks = 28 MFMAs per 16 pixels.  The 16 rows of channel block nb hold channels
+// chan(nb, r) = 32 (nb >> 1) + 8 (r >> 2) + 4 (nb & 1) + (r & 3), so D lane l (pixel l & 15,
+// rows 4 (l >> 4) .. +3) ends up with channels 8j .. 8j + 7 and 32 + 8j .. 32 + 8j + 7 (j = l >> 4):
+// two 16-B hi and two 16-B lo stores of the S-layout (or two of plain bf16) per lane, no
+// shuffle.  A lane's weights (28), BN scale / shift (16 + 16) stay in registers while the wave
+// walks its 16-pixel groups; the image reads are 4-B gathers from L2 (2.7 MB image per episode).
+// The VALU form above gave every (pixel, 8 channels) thread 216 FMAs behind 54 LDS weight reads
+// and ran at 26-33 us for 2 x 237^2 pixels, 6x its byte floor.
+template <bool BF16>
+__global__ __launch_bounds__(256) void stem_conv1_mfma_kernel(const float* __restrict__ img, int N, int S,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift,
+                                                              __bf16* __restrict__ out, int Ho, float floor_,
+                                                              int ngroups) {
+  const int lane = threadIdx.x & 63, j = lane >> 4, c16 = lane & 15;
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
+  // A operand: lane supplies W[row c16][k = 4s + j] of every channel block
+  float a[4][7];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const int ch = 32 * (nb >> 1) + 8 * (c16 >> 2) + 4 * (nb & 1) + (c16 & 3);
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const int k = 4 * s + j;
+      a[nb][s] = k < 27 ? w[k * 64 + ch] : 0.f;
+    }
+  }
+  // this lane's output channels: nb -> chan(nb, 4j + i)
+  float sc[4][4], sh[4][4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ch = 32 * (nb >> 1) + 8 * j + 4 * (nb & 1) + i;
+      sc[nb][i] = scale[ch];
+      sh[nb][i] = shift[ch];
+    }
+  const long hw = (long)Ho * Ho, total = (long)N * hw;
+  // the gathers of group grp + nwaves are issued before group grp's MFMAs (one group ahead)
+  auto gather = [&](int grp, float (&b)[7]) {
+    const long pix = (long)grp * 16 + c16;
+    const long pc = pix < total ? pix : total - 1;  // tail lanes compute a valid pixel, never stored
+    const int n = (int)(pc / hw);
+    const int rem = (int)(pc - (long)n * hw);
+    const int oh = rem / Ho, ow = rem - oh * Ho;
+    const float* ib = img + (long)n * 3 * S * S;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const int k = 4 * s + j;
+      const int ci = k / 9, t = k - 9 * ci, ky = t / 3, kx = t - 3 * ky;
+      const int ih = 2 * oh - 1 + ky, iw = 2 * ow - 1 + kx;
+      const bool ok = k < 27 && (unsigned)ih < (unsigned)S && (unsigned)iw < (unsigned)S;
+      b[s] = ok ? ib[((long)ci * S + ih) * S + iw] : 0.f;
+    }
+  };
+  float bn[7];
+  if (wave < ngroups) gather(wave, bn);
+  for (int grp = wave; grp < ngroups; grp += nwaves) {
+    const long pix = (long)grp * 16 + c16;
+    float b[7];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) b[s] = bn[s];
+    if (grp + nwaves < ngroups) gather(grp + nwaves, bn);
+    f32x4 acc[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 7; ++s) acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[nb][s], b[s], acc[nb], 0, 0, 0);
+    }
+    if (pix >= total) continue;
+    // channel block pair h = 0: channels 8j..8j+7 (nb 0, 1); h = 1: 32 + 8j .. (nb 2, 3)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 hi, lo;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int nb = 2 * h + (q >> 2), i = q & 3;
+        const float r = fmaxf(fmaf(acc[nb][i], sc[nb][i], sh[nb][i]), floor_);
+        hi[q] = (__bf16)r;
+        lo[q] = (__bf16)(r - (float)hi[q]);
+      }
+      if (BF16) {
+        *(bf16x8*)(out + pix * 64 + 32 * h + 8 * j) = hi;
+      } else {
+        __bf16* sp = out + pix * 128 + 64 * h + 8 * j;
+        *(bf16x8*)sp = hi;
+        *(bf16x8*)(sp + 32) = lo;
+      }
+    }
+  }
+}
+
 int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const float* scale,
                       const float* shift, float* out, int Ho, hipStream_t st, int layout, int relu) {
   long total = (long)N * Ho * Ho;
   const float floor_ = relu ? 0.f : -INFINITY;  // relu = 0: raw conv (training-mode BN follows)
-  if (layout == ACT_SPLIT)
+  static const bool valu = getenv("CWT_STEM_VALU") && atoi(getenv("CWT_STEM_VALU"));  // A/B switch
+  const int ngroups = (int)cdiv(total, 16);
+  const int grid = (int)std::min<long>(cdiv(ngroups, 4 * 4), 2048);  // ~4 groups per wave, 4 waves per block
+  if (layout == ACT_SPLIT && !valu)
+    hipLaunchKernelGGL(stem_conv1_mfma_kernel<false>, dim3(grid), dim3(256), 0, st, img, N, S, w27x64, scale, shift,
+                       (__bf16*)out, Ho, floor_, ngroups);
+  else if (layout == ACT_BF16 && !valu)
+    hipLaunchKernelGGL(stem_conv1_mfma_kernel<true>, dim3(grid), dim3(256), 0, st, img, N, S, w27x64, scale, shift,
+                       (__bf16*)out, Ho, floor_, ngroups);
+  else if (layout == ACT_SPLIT)
     hipLaunchKernelGGL(stem_conv1_s_kernel<false>, dim3(cdiv(total * 8, 256)), dim3(256), 0, st, img, N, S, w27x64,
                        scale, shift, (__bf16*)out, Ho, floor_);
   else if (layout == ACT_BF16)
@@ -230,8 +338,71 @@ __global__ void maxpool3s2_s_kernel(const __bf16* __restrict__ in, int N, int H,
   *(bf16x8*)(dp + 32) = lo;
 }
 
+// The same with two horizontally adjacent outputs per thread (round 3): their windows share
+// input column 2*ow+1, so 15 pixel loads (hi + lo each) make two outputs instead of 18 making
+// one; the channel group is the fastest index, so a wave still reads whole 128-B lines.
+__global__ void maxpool3s2_s2_kernel(const __bf16* __restrict__ in, int N, int H, int W, int C,
+                                     __bf16* __restrict__ out, int Ho, int Wo) {
+  const int g8 = C >> 3, Wp = (Wo + 1) >> 1;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)N * Ho * Wp * g8;
+  if (idx >= total) return;
+  const int g = (int)(idx % g8);
+  const long pp = idx / g8;
+  const int owp = (int)(pp % Wp);
+  const long nh = pp / Wp;
+  const int oh = (int)(nh % Ho);
+  const int n = (int)(nh / Ho);
+  const int ow = 2 * owp;
+  const int coff = (g >> 2) * 64 + (g & 3) * 8;
+  float m0[8], m1[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) m0[q] = m1[q] = -INFINITY;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int ih = oh * 2 - 1 + ky;
+    if ((unsigned)ih >= (unsigned)H) continue;
+    const __bf16* rp = in + ((long)n * H + ih) * W * (2L * C) + coff;
+#pragma unroll
+    for (int kx = 0; kx < 5; ++kx) {
+      const int iw = ow * 2 - 1 + kx;
+      if ((unsigned)iw >= (unsigned)W) continue;
+      const __bf16* sp = rp + (long)iw * (2L * C);
+      const bf16x8 hi = *(const bf16x8*)sp, lo = *(const bf16x8*)(sp + 32);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float v = (float)hi[q] + (float)lo[q];
+        if (kx < 3) m0[q] = fmaxf(m0[q], v);
+        if (kx >= 2) m1[q] = fmaxf(m1[q], v);
+      }
+    }
+  }
+  const long pix = ((long)n * Ho + oh) * Wo + ow;
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    if (ow + o >= Wo) break;
+    bf16x8 hi, lo;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float m = o ? m1[q] : m0[q];
+      hi[q] = (__bf16)m;
+      lo[q] = (__bf16)(m - (float)hi[q]);
+    }
+    __bf16* dp = out + (pix + o) * (2L * C) + coff;
+    *(bf16x8*)dp = hi;
+    *(bf16x8*)(dp + 32) = lo;
+  }
+}
+
 int launch_maxpool3s2_s(const __bf16* in, int N, int H, int W, int C, __bf16* out, int Ho, int Wo, hipStream_t st) {
   if (C % 32) return fail(CWT_EARG, "maxpool_s: C % 32");
+  static const bool one = getenv("CWT_MAXPOOL1") && atoi(getenv("CWT_MAXPOOL1"));  // A/B switch
+  if (!one) {
+    const long total = (long)N * Ho * ((Wo + 1) / 2) * (C / 8);
+    hipLaunchKernelGGL(maxpool3s2_s2_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, in, N, H, W, C, out, Ho, Wo);
+    CWT_LAUNCH_CHECK();
+    return 0;
+  }
   long total = (long)N * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(maxpool3s2_s_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, in, N, H, W, C, out, Ho, Wo);
   CWT_LAUNCH_CHECK();
@@ -361,6 +532,47 @@ __global__ void ppm_rowseg_kernel(const float* __restrict__ x, int N, int h, int
   rowseg[idx] = s;
 }
 
+// The same pass over the S-layout / bf16 map with 8 channels per thread (round 3): one 16-B hi
+// and one 16-B lo load per pixel (8 per pixel for bf16) instead of two 2-B loads per channel,
+// and two 16-B stores.  The per-channel sum runs over the segment's pixels in the same order as
+// the scalar form (identical result).
+template <int LAYOUT>
+__global__ void ppm_rowseg8_kernel(const __bf16* __restrict__ x, int N, int h, int w, int C, PPMSegs sx,
+                                   float* __restrict__ rowseg) {
+  constexpr bool SPLIT = LAYOUT == ACT_SPLIT;
+  const int C8 = C >> 3;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)N * h * sx.nseg * C8;
+  if (idx >= total) return;
+  const int c8 = (int)(idx % C8);
+  const long r = idx / C8;
+  const int xs = (int)(r % sx.nseg);
+  const long ny = r / sx.nseg;
+  const int x0 = sx.b[xs], len = sx.b[xs + 1] - x0;
+  const long pstride = SPLIT ? 2L * C : (long)C;
+  const __bf16* src = x + (ny * w + x0) * pstride + (SPLIT ? (c8 >> 2) * 64 + (c8 & 3) * 8 : c8 * 8);
+  float s[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s[q] = 0.f;
+  for (int u0 = 0; u0 < len; u0 += 8) {
+    bf16x8 hv[8], lv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long o = (long)min(u0 + u, len - 1) * pstride;
+      hv[u] = *(const bf16x8*)(src + o);
+      if (SPLIT) lv[u] = *(const bf16x8*)(src + o + 32);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u0 + u < len)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[q] += SPLIT ? (float)hv[u][q] + (float)lv[u][q] : (float)hv[u][q];
+  }
+  float* d = rowseg + idx * 8;
+  *(f32x4*)d = f32x4{s[0], s[1], s[2], s[3]};
+  *(f32x4*)(d + 4) = f32x4{s[4], s[5], s[6], s[7]};
+}
+
 __global__ void ppm_blk_kernel(const float* __restrict__ rowseg, int N, int h, int C, PPMSegs sx, PPMSegs sy,
                                float* __restrict__ blk) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -433,11 +645,11 @@ int launch_ppm(const float* x, int N, int h, int w, int ld, const int* bins, int
   float* blk = ws + (long)N * h * sx.nseg * C;
   const long t1 = (long)N * h * sx.nseg * C;
   if (layout == ACT_SPLIT)
-    hipLaunchKernelGGL(ppm_rowseg_kernel<ACT_SPLIT>, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx,
-                       rowseg);
+    hipLaunchKernelGGL(ppm_rowseg8_kernel<ACT_SPLIT>, dim3(cdiv(t1 / 8, 256)), dim3(256), 0, st, (const __bf16*)x, N,
+                       h, w, C, sx, rowseg);
   else if (layout == ACT_BF16)
-    hipLaunchKernelGGL(ppm_rowseg_kernel<ACT_BF16>, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx,
-                       rowseg);
+    hipLaunchKernelGGL(ppm_rowseg8_kernel<ACT_BF16>, dim3(cdiv(t1 / 8, 256)), dim3(256), 0, st, (const __bf16*)x, N,
+                       h, w, C, sx, rowseg);
   else
     hipLaunchKernelGGL(ppm_rowseg_kernel<ACT_F32>, dim3(cdiv(t1, 256)), dim3(256), 0, st, x, N, h, w, ld, C, sx,
                        rowseg);

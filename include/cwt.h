@@ -459,7 +459,7 @@ int cwt_pretrain_num_params(const cwt_pretrain* pt, int64_t* total, int64_t* bac
  */
 /*
  * Scheduling knob (no reference counterpart): how many 64-pixel units of the support map one
- * workgroup of the persistent inner loop holds (0 = automatic, 1 or 2).  2 halves the CUs the
+ * workgroup of the persistent inner loop holds (0 = automatic, 1, 2 or 3).  2 halves the CUs the
  * loop occupies, for contexts whose inner loops run beside another stream's extractor pass
  * (few_shot_seg_cwt_amd.episode.EpisodePipeline); results are the same either way.
  */
