@@ -63,6 +63,10 @@ SIGNATURES = {
     "cwt_match_corr_forward": (_I, [_P, _P, _I, _I, _I, _I, _P, _I, _F, _P, _I, _P, _P, _P]),
     "cwt_weight_average": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cwt_mmn_blend": (_I, [_P, _P, _P, _I, _I64, _F, _P, _P, _P]),
+    "cwt_linear": (_I, [_P, _P, _I64, _I, _P, _P, _I, _I, _I, _P, _P]),
+    "cwt_sine_pos_add": (_I, [_P, _P, _I, _I, _I, _I, _F, _I, _F, _F, _P, _P]),
+    "cwt_deform_attn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "cwt_norm_blend": (_I, [_P, _P, _P, _I64, _I, _F, _P, _P]),
     "cwt_extract_features_mid": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "cwt_sgd_step": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _I, _I, _P]),
     "cwt_pretrain_create": (_I, [_P, _I, _I, _I, C.POINTER(C.c_char_p), C.POINTER(_P), C.POINTER(_I64), _F,

@@ -75,6 +75,13 @@ int launch_match_vt(const float* v, int B, int NB, int C, int ldp, float* vt, hi
 int launch_wa_attn(const float* tpg, int N, int h, int w, int co, const float* bt, const float* bp, const float* bg,
                    float* wavg, hipStream_t st);
 int launch_wa_residual(const float* x, const float* back, const float* b, long n, int C, float* out, hipStream_t st);
+int launch_linear_epilogue(const float* tmp, const float* bias, const float* acc, long P, int N, int relu, float* out,
+                           hipStream_t st);
+int launch_sine_pos_add(const float* x, int B, int h, int w, int C, float temperature, int normalize, float scale,
+                        float eps, float* out, hipStream_t st);
+int launch_deform_attn(const float* value, const float* offsets, const float* logits, int B, int H, int W, int M,
+                       int P, int D, float* out, hipStream_t st);
+int launch_norm_blend(const float* a, const float* b, long T, int C, float wt, float* out, hipStream_t st);
 int launch_mmn_blend(const float* fq_in, const float* att, int B, long n, float att_wt, float* att_mean, float* fq_out,
                      hipStream_t st);
 int launch_seg_metrics(const float* logits, const int64_t* target, int B, int h, int w, int S, float* iut,
@@ -1366,6 +1373,55 @@ int cwt_mmn_blend(cwt_ctx* ctx, const float* f_q, const float* att_fq, int B, in
   CWT_CHECK(f_q && att_fq && att_mean && fq_out && B >= 1 && n >= 1, "bad arguments");
   CWT_HIP(hipSetDevice(ctx->device));
   return launch_mmn_blend(f_q, att_fq, B, (long)n, att_wt, att_mean, fq_out, (hipStream_t)stream);
+}
+
+int cwt_linear(cwt_ctx* ctx, const float* x, int64_t P, int K, const float* w, const float* bias, int N, int relu,
+               int accumulate, float* out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && w && out && P >= 1 && K >= 4 && K % 4 == 0 && N >= 1 && P <= (1L << 30), "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  void* tmp;
+  int rc;
+  if ((rc = ensure_ws(ctx, "linear.tmp", (size_t)P * N * 4, &tmp))) return rc;
+  Prof p(ctx, st, "linear " + std::to_string(K) + "x" + std::to_string(N), 2.0 * P * N * K,
+         4.0 * ((double)P * K + (double)N * K + (double)P * N));
+  if ((rc = launch_gemm_abt(x, w, 1, (int)P, N, K, (float*)tmp, st))) return rc;
+  if ((rc = launch_linear_epilogue((const float*)tmp, bias, accumulate ? out : nullptr, (long)P, N, relu, out, st)))
+    return rc;
+  p.end();
+  return 0;
+}
+
+int cwt_sine_pos_add(cwt_ctx* ctx, const float* x, int B, int h, int w, int C, float temperature, int normalize,
+                     float scale, float eps, float* out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && out && B >= 1 && h >= 1 && w >= 1 && C >= 2 && C % 2 == 0 && temperature > 0.f, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_sine_pos_add(x, B, h, w, C, temperature, normalize, scale, eps, out, (hipStream_t)stream);
+}
+
+int cwt_deform_attn(cwt_ctx* ctx, const float* value, const float* offsets, const float* logits, int B, int H, int W,
+                    int n_heads, int n_points, int d_head, float* out, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(value && offsets && logits && out && B >= 1 && H >= 1 && W >= 1 && n_heads >= 1 && n_points >= 1 &&
+                d_head >= 1,
+            "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  Prof p(ctx, st, "deform_attn", 2.0 * B * H * W * n_heads * n_points * d_head * 5,
+         4.0 * (double)B * H * W * n_heads * (d_head * 2 + n_points * 3));
+  int rc = launch_deform_attn(value, offsets, logits, B, H, W, n_heads, n_points, d_head, out, st);
+  p.end();
+  return rc;
+}
+
+int cwt_norm_blend(cwt_ctx* ctx, const float* a, const float* b, int64_t T, int C, float wt, float* out,
+                   void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(a && b && out && T >= 1 && C >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_norm_blend(a, b, (long)T, C, wt, out, (hipStream_t)stream);
 }
 
 int cwt_seg_metrics(cwt_ctx* ctx, const float* logits, const int64_t* target, int B, int h, int w, int S,

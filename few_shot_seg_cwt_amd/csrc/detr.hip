@@ -1,0 +1,162 @@
+// DeTr head of the transformer variants (src/model/detr.py:13-151),
+// forward only, on tokens [B][hw][C] (channels last):
+//  * linear epilogue: bias, ReLU and an accumulated second product after the exact-fp32 GEMM
+//    (launch_gemm_abt), for nn.Linear / 1x1 nn.Conv2d (detr.py:22, ms_deform_attn.py:56-59);
+//  * the sine position embedding of SinePositionalEncoding(256, normalize=True)
+//    (positional_encoding.py:44-74) added to the query tokens (detr.py:94);
+//  * the deformable attention core: per (query, head) a softmax over the n_points attention
+//    logits, sampling locations reference + offset / (W, H), and the bilinear grid_sample
+//    (align_corners False, zero padding) of the head's value channels at each of them, summed
+//    with the attention weights (ms_deform_attn.py:84-117, ms_deform_attn_func.py:41-61), one
+//    level (DeformAtt n_levels = 1, detr.py:32,78-110);
+//  * the blend F.normalize(a) + F.normalize(b) * att_wt (detr.py:41,45).
+#include "common.h"
+#include "kernels.h"
+
+namespace cwt {
+
+// out[p][n] = act(tmp[p][n] + bias[n] (+ acc[p][n]))
+__global__ void linear_epilogue_kernel(const float* __restrict__ tmp, const float* __restrict__ bias,
+                                       const float* __restrict__ acc, long total, int N, int relu,
+                                       float* __restrict__ out) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    float v = tmp[i];
+    if (acc) v = acc[i] + v;
+    if (bias) v += bias[i % N];
+    out[i] = relu ? fmaxf(v, 0.f) : v;
+  }
+}
+
+int launch_linear_epilogue(const float* tmp, const float* bias, const float* acc, long P, int N, int relu, float* out,
+                           hipStream_t st) {
+  const long total = P * N;
+  hipLaunchKernelGGL(linear_epilogue_kernel, dim3((unsigned)std::min<long>(4096, cdiv(total, 256))), dim3(256), 0, st,
+                     tmp, bias, acc, total, N, relu, out);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+// x + pos for SinePositionalEncoding(num_feats = C/2, temperature, normalize, scale, eps) of
+// the mask DeformAtt passes (detr.py:135: torch.zeros(...).long(), so ~mask is -1 everywhere):
+// y_embed = cumsum over rows of -1 = -(i + 1), x_embed = -(j + 1); normalize divides by the last
+// row / column plus eps, in fp32 as the reference does.  Channel c < C/2: the y part, k = c;
+// c >= C/2: the x part, k = c - C/2; dim_t[k] = temperature^(2 (k / 2) / num_feats); even k sin,
+// odd k cos (the stack + flatten interleave).  One thread per (token, channel).
+__global__ void sine_pos_add_kernel(const float* __restrict__ x, int B, int h, int w, int C, float temperature,
+                                    int normalize, float scale, float eps, float* __restrict__ out) {
+#pragma clang fp contract(off)
+  const int nf = C / 2;
+  const long total = (long)B * h * w * C;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % C);
+    const long pix = idx / C;
+    const int j = (int)(pix % w);
+    const int i = (int)((pix / w) % h);
+    const bool ypart = c < nf;
+    const int k = ypart ? c : c - nf;
+    float e = ypart ? -(float)(i + 1) : -(float)(j + 1);
+    if (normalize) {
+      const float last = ypart ? -(float)h : -(float)w;
+      e = e / (last + eps) * scale;
+    }
+    const float dt = powf(temperature, (2.f * (float)(k / 2)) / (float)nf);
+    const float a = e / dt;
+    const float pv = (k & 1) ? cosf(a) : sinf(a);
+    out[idx] = x[idx] + pv;
+  }
+}
+
+int launch_sine_pos_add(const float* x, int B, int h, int w, int C, float temperature, int normalize, float scale,
+                        float eps, float* out, hipStream_t st) {
+  const long total = (long)B * h * w * C;
+  hipLaunchKernelGGL(sine_pos_add_kernel, dim3((unsigned)std::min<long>(4096, cdiv(total, 256))), dim3(256), 0, st, x,
+                     B, h, w, C, temperature, normalize, scale, eps, out);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+// One wave per (batch, query, head); lane d < D holds value channel head*D + d.  The offsets and
+// logits of the (query, head) are wave-uniform loads.  grid_sample's source index (align_corners
+// False): ix = ((g + 1) W - 1) / 2 with g = 2 loc - 1, loc = ref + off / W, ref = (j + 0.5) / W,
+// evaluated in that order (fp contraction off); corners outside the map contribute 0.
+constexpr int DA_MAXP = 16;
+__global__ __launch_bounds__(256) void deform_attn_kernel(const float* __restrict__ value,
+                                                          const float* __restrict__ offsets,
+                                                          const float* __restrict__ logits, int B, int H, int W,
+                                                          int M, int P, int D, float* __restrict__ out) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const long L = (long)H * W;
+  const long nw = (long)B * L * M;
+  const long wid = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= nw) return;
+  const int m = (int)(wid % M);
+  const long bq = wid / M;
+  const int q = (int)(bq % L);
+  const int b = (int)(bq / L);
+  const int qy = q / W, qx = q - qy * W;
+  const float* lg = logits + (bq * M + m) * P;
+  const float* of = offsets + (bq * M + m) * P * 2;
+  float mx = -INFINITY;
+  for (int p = 0; p < P; ++p) mx = fmaxf(mx, lg[p]);
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += expf(lg[p] - mx);
+  const float ref_x = ((float)qx + 0.5f) / (float)W, ref_y = ((float)qy + 0.5f) / (float)H;
+  const float* vb = value + (long)b * L * (M * D) + m * D + lane;
+  const bool act = lane < D;
+  float acc = 0.f;
+  for (int p = 0; p < P; ++p) {
+    const float lx = ref_x + of[2 * p] / (float)W, ly = ref_y + of[2 * p + 1] / (float)H;
+    const float gx = 2.f * lx - 1.f, gy = 2.f * ly - 1.f;
+    const float ix = ((gx + 1.f) * (float)W - 1.f) / 2.f, iy = ((gy + 1.f) * (float)H - 1.f) / 2.f;
+    const float fx = floorf(ix), fy = floorf(iy);
+    const int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+    const float wx1 = ix - fx, wx0 = (fx + 1.f) - ix, wy1 = iy - fy, wy0 = (fy + 1.f) - iy;
+    const float w00 = wx0 * wy0, w01 = wx1 * wy0, w10 = wx0 * wy1, w11 = wx1 * wy1;  // nw, ne, sw, se
+    float v = 0.f;
+    if (act) {
+      if ((unsigned)y0 < (unsigned)H && (unsigned)x0 < (unsigned)W) v += vb[((long)y0 * W + x0) * (M * D)] * w00;
+      if ((unsigned)y0 < (unsigned)H && (unsigned)x1 < (unsigned)W) v += vb[((long)y0 * W + x1) * (M * D)] * w01;
+      if ((unsigned)y1 < (unsigned)H && (unsigned)x0 < (unsigned)W) v += vb[((long)y1 * W + x0) * (M * D)] * w10;
+      if ((unsigned)y1 < (unsigned)H && (unsigned)x1 < (unsigned)W) v += vb[((long)y1 * W + x1) * (M * D)] * w11;
+    }
+    acc += v * (expf(lg[p] - mx) / s);
+  }
+  if (act) out[bq * (M * D) + m * D + lane] = acc;
+}
+
+int launch_deform_attn(const float* value, const float* offsets, const float* logits, int B, int H, int W, int M,
+                       int P, int D, float* out, hipStream_t st) {
+  if (P > DA_MAXP || D > 64) return fail(CWT_EARG, "deform_attn: n_points <= 16 and d_model / n_heads <= 64");
+  const long nw = (long)B * H * W * M;
+  hipLaunchKernelGGL(deform_attn_kernel, dim3((unsigned)cdiv(nw, 4)), dim3(256), 0, st, value, offsets, logits, B, H,
+                     W, M, P, D, out);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+// out[t] = a[t] / max(|a[t]|, 1e-12) + b[t] / max(|b[t]|, 1e-12) * wt, one wave per token
+__global__ __launch_bounds__(256) void norm_blend_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                         long T, int C, float wt, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  for (long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6); r < T; r += (long)gridDim.x * 4) {
+    const float* ar = a + r * C;
+    const float* br = b + r * C;
+    float sa = 0.f, sb = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      sa = fmaf(ar[c], ar[c], sa);
+      sb = fmaf(br[c], br[c], sb);
+    }
+    const float na = fmaxf(sqrtf(wave_sum_dpp(sa)), 1e-12f), nb = fmaxf(sqrtf(wave_sum_dpp(sb)), 1e-12f);
+    for (int c = lane; c < C; c += 64) out[r * C + c] = ar[c] / na + br[c] / nb * wt;
+  }
+}
+
+int launch_norm_blend(const float* a, const float* b, long T, int C, float wt, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(norm_blend_kernel, dim3((unsigned)std::min<long>(2048, (T + 3) / 4)), dim3(256), 0, st, a, b, T, C,
+                     wt, out);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace cwt

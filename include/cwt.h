@@ -370,6 +370,38 @@ int cwt_weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C,
 int cwt_mmn_blend(cwt_ctx* ctx, const float* f_q, const float* att_fq, int B, int64_t n, float att_wt,
                   float* att_mean, float* fq_out, void* stream);
 
+/* ---- DeTr head (src/model/detr.py:13-151), forward only; tokens are [B][hw][C] (NHWC) ---- */
+
+/* nn.Linear / 1x1 nn.Conv2d over tokens (detr.py:22 adjust_feature, ms_deform_attn.py:56-59
+ * value_proj / sampling_offsets / attention_weights / output_proj): x device [P][K] (K % 4 == 0),
+ * w device [N][K] (the module's weight), bias device [N] or NULL; out device [P][N] =
+ * relu?(x w^T + bias (+ out when accumulate != 0: a second input segment of a channel concat,
+ * detr.py:56-59)).  Exact fp32 (f32 MFMA). */
+int cwt_linear(cwt_ctx* ctx, const float* x, int64_t P, int K, const float* w, const float* bias, int N, int relu,
+               int accumulate, float* out, void* stream);
+
+/* query + SinePositionalEncoding(C/2, temperature, normalize, scale, eps)(mask) with the mask
+ * DeformAtt.get_qry_flatten_input builds without a padding mask (detr.py:135: a zero LONG tensor,
+ * so ~mask = -1 and the cumulative embeddings run -1, -2, ...; positional_encoding.py:44-74):
+ * x, out device [B][h][w][C]. */
+int cwt_sine_pos_add(cwt_ctx* ctx, const float* x, int B, int h, int w, int C, float temperature, int normalize,
+                     float scale, float eps, float* out, void* stream);
+
+/* MSDeformAttn's core over one level (ms_deform_attn.py:84-117 with ms_deform_attn_core_pytorch,
+ * ms_deform_attn_func.py:41-61; DeformAtt's reference points, detr.py:98-110): value device
+ * [B][H*W][n_heads*d_head] (value_proj output), offsets device [B][H*W][n_heads][n_points][2]
+ * (sampling_offsets output, (x, y)), logits device [B][H*W][n_heads][n_points] (attention_weights
+ * output, before the softmax); out device [B][H*W][n_heads*d_head] = sum_p softmax_p(logits)
+ * grid_sample(value_head, 2 (ref + off / (W, H)) - 1) (bilinear, zeros, align_corners False).
+ * n_points <= 16, d_head <= 64. */
+int cwt_deform_attn(cwt_ctx* ctx, const float* value, const float* offsets, const float* logits, int B, int H, int W,
+                    int n_heads, int n_points, int d_head, float* out, void* stream);
+
+/* DeTr's blends (detr.py:41,45): out[t] = F.normalize(a[t]) + F.normalize(b[t]) * wt over T
+ * tokens of C channels (eps 1e-12); a, b, out device [T][C]. */
+int cwt_norm_blend(cwt_ctx* ctx, const float* a, const float* b, int64_t T, int C, float wt, float* out,
+                   void* stream);
+
 /* torch.optim.SGD(momentum, dampening 0, weight_decay, nesterov) step over one flat
  * fp32 parameter buffer (optimizer.py:8-15): buf = m*buf + (g + wd*p) (buf = g+wd*p on
  * the first step, first_step != 0); p -= lr * (nesterov ? g + wd*p + m*buf : buf). */
