@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Record of the round-3 A/B in profiles/r3/sweeps_rejected/splitk_inlaunch_*.  The in-launch combine was
+# slower and was removed afterwards, with its CWT_SPLITK_EPI switch.)
 # In-launch split-K combine of conv_x3s (the tile's last arriver sums the partials): per-plan
 # parity (every split-K plan), extraction parity, then A/B against the separate epilogue launch
 # (CWT_SPLITK_EPI=1): extractor per-launch sums and the default bench.
