@@ -62,3 +62,30 @@ def test_deform_core_matches_explicit_bilinear():
                 lx, ly = float(loc[0, q, m, 0, p, 0]), float(loc[0, q, m, 0, p, 1])
                 acc += _bilinear_zero(img, lx * W - 0.5, ly * H - 0.5) * float(aw[0, q, m, 0, p])
             assert torch.allclose(out[0, q, m * Dh:(m + 1) * Dh], acc, atol=1e-12)
+
+
+def test_detr_parameter_names_and_init_follow_the_reference():
+    """DeTr / DeformAtt / MSDeformAttn keep the reference's state_dict keys (detr.py:13-110,
+    ms_deform_attn.py:54-59) and MSDeformAttn's initialisation (ms_deform_attn.py:61-75); host
+    only (parameters on the CPU, no forward)."""
+    from few_shot_seg_cwt_amd.detr import DeTr, MSDeformAttn
+    cpu = torch.device("cpu")
+    net = DeTr(dict(rmid="l34", temp=20.0, att_wt=0.2), sf_att=True, cs_att=True, reduce_dim=512, device=cpu)
+    keys = set(net.state_dict().keys())
+    want = {"adjust_feature.0.weight", "self_trans.level_embed"}
+    for i in (0, 2, 4):
+        for c in ("conv1", "conv2"):
+            want |= {f"cross_trans.NeighConsensus.conv.{i}.{c}.weight", f"cross_trans.NeighConsensus.conv.{i}.{c}.bias"}
+    for m in ("sampling_offsets", "attention_weights", "value_proj", "output_proj"):
+        want |= {f"self_trans.self_trans.{m}.weight", f"self_trans.self_trans.{m}.bias"}
+    assert keys == want, sorted(keys ^ want)
+    assert tuple(net.adjust_feature[0].weight.shape) == (512, 3072, 1, 1)
+    m = MSDeformAttn(d_model=512, n_levels=1, n_heads=8, n_points=9, device=cpu)
+    assert torch.count_nonzero(m.sampling_offsets.weight) == 0 and torch.count_nonzero(m.attention_weights.weight) == 0
+    b = m.sampling_offsets.bias.view(8, 1, 9, 2)
+    for h in range(8):
+        th = h * 2 * math.pi / 8
+        d = torch.tensor([math.cos(th), math.sin(th)])
+        d = d / d.abs().max()
+        for p in range(9):
+            assert torch.allclose(b[h, 0, p], d * (p + 1), atol=1e-6)
