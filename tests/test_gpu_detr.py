@@ -115,13 +115,13 @@ def test_ms_deform_attn_reference_init(dev):
     assert e < 1e-5
 
 
-@pytest.mark.parametrize("cs,sf", [(True, False), (False, True), (True, True)])
-def test_detr_forward(dev, cs, sf):
+@pytest.mark.parametrize("cs,sf,h", [(True, False, 20), (False, True, 20), (True, True, 20), (True, True, 60)])
+def test_detr_forward(dev, cs, sf, h):
     from few_shot_seg_cwt_amd.detr import DeTr
     from few_shot_seg_cwt_amd.match import init_match_params
     from oracle import detr_oracle as D
     from oracle import match_oracle as MO
-    h = w = 20
+    w = h
     args = dict(rmid="l34", temp=20.0, att_wt=0.2)
     torch.manual_seed(1)
     net = DeTr(args, sf_att=sf, cs_att=cs, reduce_dim=512, device=dev)
@@ -147,5 +147,5 @@ def test_detr_forward(dev, cs, sf):
         errs["ca"] = rel(ca, rca)
     if sf:
         errs["sa"] = rel(sa, rsa)
-    print(f"DeTr cs={cs} sf={sf}: {errs}")
+    print(f"DeTr cs={cs} sf={sf} {h}x{w}: {errs}")
     assert all(v < 2e-5 for v in errs.values()), errs
