@@ -133,8 +133,11 @@ def pmc_traffic(dom_name: str):
             if "traffic_bytes" not in e:
                 continue
             if mt:
+                # kernel names carry <BM, BN, WAVES_M, WAVES_N, NSTG, STAGE, PF>
                 kind, bm, bn, stage = mt.group(1), mt.group(2), mt.group(3), mt.group(4)
-                hit = f"conv_igemm_{kind}<{bm}, {bn}, " in k and k.split(">(")[0].endswith(f", {stage}")
+                targs = k.split(">(")[0].split("<", 1)[-1].split(", ")
+                hit = (f"conv_igemm_{kind}<" in k and len(targs) >= 6 and targs[0] == bm and targs[1] == bn
+                       and targs[5] == stage)
             else:
                 hit = dom_name in k
             if hit:
