@@ -5,7 +5,9 @@
 //   mode 1: VGPRs by global_load_dwordx4 (no LDS), two register sets (tile t+1 in flight while
 //           tile t is summed);
 //   mode 2: VGPRs by global_load_dwordx4, then ds_write_b128 into a DEPTH-slot LDS ring, one
-//           barrier per tile (register-staged operand loads).
+//           barrier per tile (register-staged operand loads);
+//   mode 3: hybrid (round 3): half of each tile's pieces by LDS-DMA (issued DEPTH-1 tiles ahead),
+//           half by global_load_dwordx4 one tile ahead + ds_write_b128 into the same ring slot.
 // Every workgroup streams its own rotation of a shared 2 MB row set (L2-resident, like the
 // weight / activation rows of a conv tile).  Prints GB/s per CU for each form.
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/intake_bench.hip -o tools/intake_bench
@@ -74,6 +76,71 @@ __global__ __launch_bounds__(NW * 64) void intake(const char* __restrict__ buf, 
 #pragma unroll
       for (int j = 0; j < PW; ++j) acc += b[j][0] + b[j][3];
     }
+  } else if (MODE == 3) {
+    constexpr int PD = PW / 2;  // pieces per wave by LDS-DMA; the other PW - PD through registers
+    auto dma = [&](int t) {
+#pragma unroll
+      for (int j = 0; j < PD; ++j)
+        __builtin_amdgcn_global_load_lds((const GLBP void*)src_of(t, j),
+                                         (LDSP void*)(lds + (t % DEPTH) * TILE + (wv * PW + j) * 1024), 16, 0, 0);
+    };
+    f32x4 r[PW - PD];
+    for (int t = 0; t < DEPTH - 1 && t < iters; ++t) dma(t);
+#pragma unroll
+    for (int j = 0; j < PW - PD; ++j) r[j] = *(const f32x4*)src_of(0, PD + j);
+    for (int t = 0; t < iters; ++t) {
+      // tile t's register half (loaded one step ago, BEFORE that step's DMA) lands and goes to its
+      // slot; its DMA half was issued DEPTH-1 steps ago: only the youngest DMA may stay in flight
+      if (DEPTH >= 3 && t + DEPTH - 2 < iters && t > 0)
+        wait_vm<PD>();
+      else
+        wait_vm<0>();
+      char* slot = lds + (t % DEPTH) * TILE;
+#pragma unroll
+      for (int j = 0; j < PW - PD; ++j) *(f32x4*)(slot + (wv * PW + PD + j) * 1024 + lane * 16) = r[j];
+      __syncthreads();
+      if (t + 1 < iters) {
+#pragma unroll
+        for (int j = 0; j < PW - PD; ++j) r[j] = *(const f32x4*)src_of(t + 1, PD + j);
+      }
+      if (t + DEPTH - 1 < iters) dma(t + DEPTH - 1);
+      acc += *(const float*)(lds + (t % DEPTH) * TILE + threadIdx.x * 16);
+    }
+  } else if (MODE == 4) {
+    // half of each tile by LDS-DMA (DEPTH-slot ring), half straight into registers (two register
+    // sets, never written to LDS: an operand consumed from VGPRs, as a wave-private MFMA operand)
+    constexpr int PD = PW / 2, PR = PW - PD;
+    auto dma = [&](int t) {
+#pragma unroll
+      for (int j = 0; j < PD; ++j)
+        __builtin_amdgcn_global_load_lds((const GLBP void*)src_of(t, j),
+                                         (LDSP void*)(lds + (t % DEPTH) * TILE + (wv * PW + j) * 1024), 16, 0, 0);
+    };
+    f32x4 r0[PR], r1[PR];
+#pragma unroll
+    for (int j = 0; j < PR; ++j) r0[j] = *(const f32x4*)src_of(0, PD + j);
+    for (int t = 0; t < DEPTH - 1 && t < iters; ++t) dma(t);
+    for (int t = 0; t < iters; t += 2) {
+      // even step: r1 <- tile t+1 while r0 (tile t) is consumed; odd step the other way round
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int tt = t + half;
+        if (tt >= iters) break;
+        if (tt + DEPTH - 2 < iters && DEPTH >= 3)
+          wait_vm<PD + PR>();  // the youngest DMA and register set may stay in flight
+        else
+          wait_vm<0>();
+        __syncthreads();
+        if (tt + 1 < iters) {
+#pragma unroll
+          for (int j = 0; j < PR; ++j) (half ? r0 : r1)[j] = *(const f32x4*)src_of(tt + 1, PD + j);
+        }
+        if (tt + DEPTH - 1 < iters) dma(tt + DEPTH - 1);
+#pragma unroll
+        for (int j = 0; j < PR; ++j) acc += (half ? r1 : r0)[j][0] + (half ? r1 : r0)[j][3];
+        acc += *(const float*)(lds + (tt % DEPTH) * TILE + threadIdx.x * 16);
+      }
+    }
   } else {
     f32x4 a[PW];
 #pragma unroll
@@ -134,6 +201,12 @@ int main() {
     run<1, 16, 2>(buf, nrows, sink, grid, "regs    16 waves (2 sets)");
     run<2, 4, 2>(buf, nrows, sink, grid, "regs+ds_write 4 waves ring 2");
     run<2, 8, 2>(buf, nrows, sink, grid, "regs+ds_write 8 waves ring 2");
+    run<3, 4, 3>(buf, nrows, sink, grid, "hybrid dma+regs 4 waves ring 3");
+    run<3, 8, 3>(buf, nrows, sink, grid, "hybrid dma+regs 8 waves ring 3");
+    run<3, 4, 2>(buf, nrows, sink, grid, "hybrid dma+regs 4 waves ring 2");
+    run<4, 4, 3>(buf, nrows, sink, grid, "dma half + direct-regs half 4w ring 3");
+    run<4, 8, 3>(buf, nrows, sink, grid, "dma half + direct-regs half 8w ring 3");
+    run<4, 4, 2>(buf, nrows, sink, grid, "dma half + direct-regs half 4w ring 2");
   }
   hipError_t e = hipGetLastError();
   printf("status %s\n", hipGetErrorString(e));
