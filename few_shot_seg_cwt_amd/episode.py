@@ -232,12 +232,22 @@ class EpisodePipeline:
         # workgroup (59 instead of 118 CUs at 1-shot 473^2), leaving the rest to the extractor
         # passes beside it -- 466 against 443 episodes/s (same session); results are unchanged
         self.c_adapt = _lib.new_ctx()
-        upw = int(os.environ.get("CWT_PIPE_ADAPT_UNITS", "2"))   # (1 or 2: A/B of the geometry)
+        upw = int(os.environ.get("CWT_PIPE_ADAPT_UNITS", "2"))   # (1, 2 or 3: A/B of the geometry)
         _lib.check(_lib.lib().cwt_ctx_set_adapt_units(self.c_adapt, upw), "cwt_ctx_set_adapt_units")
         self.k = 0
+        # drain: submit(..., last=True) (the caller knows no episode follows before it reads the
+        # results back) runs that episode's inner loop and tail on a context with the automatic
+        # geometry (one unit per workgroup at 1-shot 473^2: 118 CUs, 1.05 instead of 1.4 ms), since
+        # no extractor pass runs beside it any more.  Same kernels, same inputs, same results.
+        # CWT_PIPE_DRAIN=0 turns it off (A/B).
+        self.drain = os.environ.get("CWT_PIPE_DRAIN", "1") != "0"
+        self.c_solo = None
 
     @torch.no_grad()
-    def submit(self, imgs: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor, W0: torch.Tensor) -> dict:
+    def submit(self, imgs: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor, W0: torch.Tensor,
+               last: bool = False) -> dict:
+        """Queue one episode; last=True: no episode follows before the caller reads the results
+        (its inner loop then takes the whole-chip geometry; the results are the same)."""
         eng = self.eng
         cur = torch.cuda.current_stream()
         shot = imgs.shape[0] - 1
@@ -254,7 +264,12 @@ class EpisodePipeline:
                     f_all, _ = eng.model.extract_features(imgs)
             done = torch.cuda.Event()
             done.record(s_ex)
-        with torch.cuda.stream(self.s_adapt), _lib.using_ctx(self.c_adapt):
+        c_ad = self.c_adapt
+        if last and self.drain:
+            if self.c_solo is None:
+                self.c_solo = _lib.new_ctx()   # automatic geometry (cwt_ctx_set_adapt_units 0)
+            c_ad = self.c_solo
+        with torch.cuda.stream(self.s_adapt), _lib.using_ctx(c_ad):
             self.s_adapt.wait_event(done)
             for t in (f_all, imgs, s_label, q_label, W0):
                 t.record_stream(self.s_adapt)
@@ -311,7 +326,7 @@ class EpisodePipeline:
             return
         for s in self.s_ext + [self.s_adapt]:
             s.synchronize()
-        for c in [c for c in self.c_ext if c is not None] + [self.c_adapt]:
+        for c in [c for c in self.c_ext if c is not None] + [self.c_adapt] + ([self.c_solo] if self.c_solo else []):
             _lib.destroy_ctx(c, self.device)
         self.closed = True
         for k, v in list(EpisodePipeline._shared.items()):
@@ -477,7 +492,9 @@ def validate_transformer(args, val_loader, model, transformer, episodes_out: lis
             imgs = torch.cat([spprt_imgs[0], qry_img], 0).to(dev, non_blocking=True)
             sl = s_label[0].to(dev, non_blocking=True)
             ql = q_label.to(dev, non_blocking=True)
-            r = pipe.submit(imgs, sl, ql, W0.to(dev)) if pipe is not None else engine.run(imgs, sl, ql, W0.to(dev))
+            last = e + world >= nb_episodes   # this rank's last episode of the run
+            r = (pipe.submit(imgs, sl, ql, W0.to(dev), last=last) if pipe is not None
+                 else engine.run(imgs, sl, ql, W0.to(dev)))
             pending.append((r, subcls))
             if len(pending) > (1 if pipe is not None else 0):
                 finish(*pending.pop(0))
