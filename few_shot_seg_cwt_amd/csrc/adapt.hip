@@ -1694,7 +1694,9 @@ __global__ __launch_bounds__(256) void seg_ce_kernel(SegCEArgs a) {
 __global__ void seg_ce_final_kernel(const AdaptScalars* sc, const double* loss_num, float* loss_out, float* dlogits,
                                     long n) {
   const double sumw = (double)sc->nbg + (double)sc->nfg * (double)sc->wfg;
-  const float inv = (float)(1.0 / sumw);
+  // every query pixel ignored (sumw = 0): loss 0/0 = NaN and zero gradients, as torch's
+  // CrossEntropyLoss(ignore_index=255) returns them (train.py:261-265)
+  const float inv = sumw > 0.0 ? (float)(1.0 / sumw) : 0.f;
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) loss_out[0] = (float)(loss_num[0] / sumw);
   for (; i < n; i += (long)gridDim.x * blockDim.x) dlogits[i] *= inv;

@@ -970,8 +970,9 @@ __global__ void seg_ce_final_kernel(const double* __restrict__ part, long nblk, 
     __syncthreads();
   }
   if (threadIdx.x == 0) {
+    // every pixel ignored: loss 0/0 = NaN and zero gradients, as torch's CE (ignore_index)
     loss[0] = (float)(s1[0] / s2[0]);
-    inv[0] = (float)(1.0 / s2[0]);
+    inv[0] = s2[0] > 0.0 ? (float)(1.0 / s2[0]) : 0.f;
   }
 }
 

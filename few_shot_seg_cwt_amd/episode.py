@@ -474,7 +474,9 @@ def validate_transformer(args, val_loader, model, transformer, episodes_out: lis
             iut0 = r["iut0"].cpu().numpy()[0]
             ce = r["ce"].cpu().numpy()[0]
             _lib.check_status()     # the readback synchronised: surface an inner-loop barrier timeout
-            loss_meter.update(float(ce[0] / max(ce[1], 1.0)))
+            # CE mean over the non-ignored pixels; a query with every pixel 255 gives NaN, as
+            # CrossEntropyLoss(ignore_index=255) does in the reference (test.py:222-224)
+            loss_meter.update(float(ce[0] / ce[1]) if ce[1] > 0 else float("nan"))
             for c in [int(x.item()) for x in subcls]:
                 cls_iu[c] += (iut[0, 1], iut[1, 1])       # FG only (test.py:227-228)
                 cls_iu0[c] += (iut0[0, 1], iut0[1, 1])

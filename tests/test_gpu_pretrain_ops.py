@@ -117,6 +117,24 @@ def test_smoothed_ce(dev, nc, S):
     assert rel(dl.cpu(), g.permute(0, 2, 3, 1)) < 1e-4
 
 
+def test_smoothed_ce_all_ignored(dev):
+    """Every target pixel 255: the reference's masked_select(...).mean() is NaN and its gradient
+    zero (pretrain.py:163-219), so the SGD step that follows sees a zero gradient."""
+    from oracle.pretrain_oracle import smoothed_ce
+    nc, S, N = 16, 33, 2
+    h = (S - 1) // 8 + 1
+    gen = torch.Generator().manual_seed(9)
+    lg = torch.randn(N, nc, h, h, generator=gen, dtype=torch.float64, requires_grad=True)
+    t = torch.full((N, S, S), 255, dtype=torch.int64)
+    loss = smoothed_ce(F.interpolate(lg, size=(S, S), mode="bilinear", align_corners=True), t, nc, True)
+    g, = torch.autograd.grad(loss, [lg])
+    dl, lo = torch.empty(N, h, h, nc, device=dev), torch.empty(1, device=dev)
+    op(2, [lg.detach().permute(0, 2, 3, 1).contiguous().float().to(dev), t.to(dev), dl, lo], [N, S, h, nc],
+       [0.9, 0.1 / (nc - 1)])
+    assert np.isnan(loss.item()) and np.isnan(float(lo))
+    assert float(g.abs().max()) == 0.0 and float(dl.abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("N,h", [(2, 17), (1, 60)])
 def test_ppm_field_fold_and_adjoint(dev, N, h):
     """The pretraining bottleneck's folded PPM branch (pretrain.hip pt_forward / pt_backward):
