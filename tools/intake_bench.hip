@@ -8,6 +8,13 @@
 //           barrier per tile (register-staged operand loads);
 //   mode 3: hybrid (round 3): half of each tile's pieces by LDS-DMA (issued DEPTH-1 tiles ahead),
 //           half by global_load_dwordx4 one tile ahead + ds_write_b128 into the same ring slot.
+//   mode 5: LDS-DMA with NO workgroup barrier: each wave streams its own pieces into its own part
+//           of the DEPTH-slot ring and reads only what it loaded (vmcnt wait only) -- the DMA
+//           path's own rate, to tell whether the per-tile barrier or the path sets the ceiling.
+//   mode 6: mode 0's shared tile (each wave loads 1/NW of it and reads another wave's piece) with
+//           the per-tile workgroup barrier replaced by LDS counters: FULL[slot] (each wave adds 1
+//           once its own pieces have landed; readers wait for NW per use of the slot) and
+//           FREE[slot] (each wave adds 1 after reading; a refill waits for NW per earlier use).
 // Every workgroup streams its own rotation of a shared 2 MB row set (L2-resident, like the
 // weight / activation rows of a conv tile).  Prints GB/s per CU for each form.
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/intake_bench.hip -o tools/intake_bench
@@ -105,6 +112,64 @@ __global__ __launch_bounds__(NW * 64) void intake(const char* __restrict__ buf, 
       }
       if (t + DEPTH - 1 < iters) dma(t + DEPTH - 1);
       acc += *(const float*)(lds + (t % DEPTH) * TILE + threadIdx.x * 16);
+    }
+  } else if (MODE == 5) {
+    for (int t = 0; t < DEPTH - 1 && t < iters; ++t)
+#pragma unroll
+      for (int j = 0; j < PW; ++j)
+        __builtin_amdgcn_global_load_lds((const GLBP void*)src_of(t, j),
+                                         (LDSP void*)(lds + (t % DEPTH) * TILE + (wv * PW + j) * 1024), 16, 0, 0);
+    for (int t = 0; t < iters; ++t) {
+      if (t + DEPTH - 1 < iters)
+        wait_vm<PW * (DEPTH - 2)>();
+      else
+        wait_vm<0>();
+      // this wave's own 1-KB pieces of tile t (no other wave's data is read)
+      acc += *(const float*)(lds + (t % DEPTH) * TILE + (wv * PW) * 1024 + lane * 16);
+      if (t + DEPTH - 1 < iters) {
+        const int tt = t + DEPTH - 1;
+        // the slot being refilled was read at step t - 1 by this wave only: its ds_read has
+        // returned (the add above consumed an LDS value issued after it)
+#pragma unroll
+        for (int j = 0; j < PW; ++j)
+          __builtin_amdgcn_global_load_lds((const GLBP void*)src_of(tt, j),
+                                           (LDSP void*)(lds + (tt % DEPTH) * TILE + (wv * PW + j) * 1024), 16, 0, 0);
+      }
+    }
+  } else if (MODE == 6) {
+    __shared__ int full[DEPTH], freec[DEPTH];
+    if (threadIdx.x < DEPTH) {
+      full[threadIdx.x] = 0;
+      freec[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    volatile LDSP int* vfull = (volatile LDSP int*)full;
+    volatile LDSP int* vfree = (volatile LDSP int*)freec;
+    auto issue = [&](int tt) {
+#pragma unroll
+      for (int j = 0; j < PW; ++j)
+        __builtin_amdgcn_global_load_lds((const GLBP void*)src_of(tt, j),
+                                         (LDSP void*)(lds + (tt % DEPTH) * TILE + (wv * PW + j) * 1024), 16, 0, 0);
+    };
+    for (int t = 0; t < DEPTH - 1 && t < iters; ++t) issue(t);
+    for (int t = 0; t < iters; ++t) {
+      const int slot = t % DEPTH, use = t / DEPTH;
+      if (t + DEPTH - 1 < iters)
+        wait_vm<PW * (DEPTH - 2)>();
+      else
+        wait_vm<0>();
+      if (lane == 0) __hip_atomic_fetch_add(&full[slot], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // refill the slot tile t-1 used once every wave has read it
+      if (t + DEPTH - 1 < iters) {
+        const int tt = t + DEPTH - 1, s2 = tt % DEPTH, prior = tt / DEPTH;
+        while (vfree[s2] < NW * prior) __builtin_amdgcn_s_sleep(0);
+        issue(tt);
+      }
+      while (vfull[slot] < NW * (use + 1)) __builtin_amdgcn_s_sleep(0);
+      acc += *(const float*)(lds + slot * TILE + (((wv + 1) % NW) * PW) * 1024 + lane * 16);
+      // the read above has returned (acc consumed it) before this wave releases the slot
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(&freec[slot], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   } else if (MODE == 4) {
     // half of each tile by LDS-DMA (DEPTH-slot ring), half straight into registers (two register
@@ -207,6 +272,14 @@ int main() {
     run<4, 4, 3>(buf, nrows, sink, grid, "dma half + direct-regs half 4w ring 3");
     run<4, 8, 3>(buf, nrows, sink, grid, "dma half + direct-regs half 8w ring 3");
     run<4, 4, 2>(buf, nrows, sink, grid, "dma half + direct-regs half 4w ring 2");
+    run<5, 4, 3>(buf, nrows, sink, grid, "lds-dma no barrier 4 waves ring 3");
+    run<5, 8, 3>(buf, nrows, sink, grid, "lds-dma no barrier 8 waves ring 3");
+    run<5, 4, 4>(buf, nrows, sink, grid, "lds-dma no barrier 4 waves ring 4");
+    run<5, 16, 2>(buf, nrows, sink, grid, "lds-dma no barrier 16 waves ring 2");
+    run<6, 4, 3>(buf, nrows, sink, grid, "lds-dma FULL/FREE 4 waves ring 3");
+    run<6, 8, 3>(buf, nrows, sink, grid, "lds-dma FULL/FREE 8 waves ring 3");
+    run<6, 4, 4>(buf, nrows, sink, grid, "lds-dma FULL/FREE 4 waves ring 4");
+    run<6, 8, 4>(buf, nrows, sink, grid, "lds-dma FULL/FREE 8 waves ring 4");
   }
   hipError_t e = hipGetLastError();
   printf("status %s\n", hipGetErrorString(e));
