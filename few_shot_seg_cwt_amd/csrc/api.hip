@@ -72,6 +72,8 @@ int launch_to_channels_last(const float* x, int B, int C, long P, float* y, hipS
 int launch_add_inplace(float* y, const float* x, long n, hipStream_t st);
 int launch_match_softmax(const float* corr, int B, int NA, int NB, float temp, int ldp, float* P, hipStream_t st);
 int launch_match_vt(const float* v, int B, int NB, int C, int ldp, float* vt, hipStream_t st);
+int launch_match_masks(float* corr, int B, int NA, int NB, const uint8_t* ig, const int64_t* s_mask, float* incons,
+                       int* q2k, float* pv, int* pi, hipStream_t st);
 int launch_wa_attn(const float* tpg, int N, int h, int w, int co, const float* bt, const float* bp, const float* bg,
                    float* wavg, hipStream_t st);
 int launch_wa_residual(const float* x, const float* back, const float* b, long n, int C, float* out, hipStream_t st);
@@ -1336,6 +1338,46 @@ int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h,
     if ((rc = launch_match_vt(v, B, (int)NB, Cv, ldp, (float*)vt, st))) return rc;
     if ((rc = launch_gemm_abt((const float*)pw, (const float*)vt, B, (int)NA, Cv, ldp, weighted_v, st))) return rc;
   }
+  p.end();
+  return 0;
+}
+
+int cwt_match_masks(cwt_ctx* ctx, float* corr2d, int B, int NA, int NB, const uint8_t* ig_mask,
+                    const int64_t* s_mask, float* inconsistent, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(corr2d && B >= 1 && NA >= 1 && NB >= 1, "bad arguments");
+  CWT_CHECK(!s_mask || inconsistent, "the cycle mask needs inconsistent");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  void *q2k = nullptr, *pv = nullptr, *pi = nullptr;
+  int rc;
+  if (s_mask && ((rc = ensure_ws(ctx, "match.q2k", (size_t)B * NA * 4, &q2k)) ||
+                 (rc = ensure_ws(ctx, "match.colv", (size_t)B * 16 * NB * 4, &pv)) ||
+                 (rc = ensure_ws(ctx, "match.coli", (size_t)B * 16 * NB * 4, &pi))))
+    return rc;
+  Prof p(ctx, st, "match_masks", 0.0, 4.0 * B * NA * NB * (s_mask ? 4 : 2));
+  if ((rc = launch_match_masks(corr2d, B, NA, NB, ig_mask, s_mask, inconsistent, (int*)q2k, (float*)pv, (int*)pi, st)))
+    return rc;
+  p.end();
+  return 0;
+}
+
+int cwt_match_readout(cwt_ctx* ctx, const float* corr2d, int B, int NA, int NB, float temp, const float* v, int Cv,
+                      float* weighted_v, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(corr2d && v && weighted_v && B >= 1 && NA >= 1 && NB >= 1 && Cv >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int ldp = (int)((NB + 3) & ~3L);
+  void *pw, *vt;
+  int rc;
+  if ((rc = ensure_ws(ctx, "match.attn", (size_t)B * NA * ldp * 4, &pw)) ||
+      (rc = ensure_ws(ctx, "match.vt", (size_t)B * Cv * ldp * 4, &vt)))
+    return rc;
+  Prof p(ctx, st, "match_readout", 2.0 * B * NA * (double)NB * Cv, 4.0 * B * ((double)NA * NB * 2 + (double)NB * Cv));
+  if ((rc = launch_match_softmax(corr2d, B, NA, NB, temp, ldp, (float*)pw, st))) return rc;
+  if ((rc = launch_match_vt(v, B, NB, Cv, ldp, (float*)vt, st))) return rc;
+  if ((rc = launch_gemm_abt((const float*)pw, (const float*)vt, B, NA, Cv, ldp, weighted_v, st))) return rc;
   p.end();
   return 0;
 }

@@ -267,6 +267,107 @@ __global__ __launch_bounds__(256) void match_vt_kernel(const float* __restrict__
   }
 }
 
+// ---- MatchNet's support masks (match.py:117-126, run_cyc match.py:165-182) ----
+// ig_mask [B][NB] (uint8, nullable): corr2d[b][a][j] = 1e-4 where ig_mask[b][j] (every query a).
+// The cycle mask: k2q[j] = argmax over a of corr2d[a][j], q2k[a] = argmax over j of corr2d[a][j]
+// (after the ig mask; first index on ties, as torch's max on the CPU), inconsistent[j] =
+// s_mask[j] != s_mask[q2k[k2q[j]]], and corr2d += inconsistent[j] * -1000 (Dropout(0.1) of the
+// mask is the identity in eval mode).
+__device__ __forceinline__ float masked_corr(const float* cr, const uint8_t* ig, int j) {
+  return (ig && ig[j]) ? 1e-4f : cr[j];
+}
+
+__device__ __forceinline__ void argmax_merge(float& v, int& i, float v2, int i2) {
+  if (v2 > v || (v2 == v && i2 < i)) {
+    v = v2;
+    i = i2;
+  }
+}
+
+// q2k: one workgroup per row (b, a)
+__global__ __launch_bounds__(256) void match_row_argmax_kernel(const float* __restrict__ corr, const uint8_t* ig,
+                                                               int NA, int NB, int* __restrict__ q2k) {
+  const long row = blockIdx.x;  // b * NA + a
+  const int b = (int)(row / NA);
+  const float* cr = corr + row * NB;
+  const uint8_t* igb = ig ? ig + (long)b * NB : nullptr;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  float v = -INFINITY;
+  int idx = 0x7fffffff;
+  for (int j = t; j < NB; j += 256) argmax_merge(v, idx, masked_corr(cr, igb, j), j);
+  for (int o = 32; o > 0; o >>= 1) argmax_merge(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+  __shared__ float rv[4];
+  __shared__ int ri[4];
+  if (lane == 0) {
+    rv[wv] = v;
+    ri[wv] = idx;
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int w = 1; w < 4; ++w) argmax_merge(v, idx, rv[w], ri[w]);
+    q2k[row] = (idx >= 0 && idx < NB) ? idx : 0;  // an all-NaN row: keep the index in range
+  }
+}
+
+// k2q partials: workgroup (column block of 64, row chunk, b); 4 waves stride the chunk's rows,
+// lanes own columns; partial (value, index) per (b, chunk, column)
+constexpr int MATCH_COL_CHUNKS = 16;
+__global__ __launch_bounds__(256) void match_col_argmax_kernel(const float* __restrict__ corr, const uint8_t* ig,
+                                                               int NA, int NB, float* __restrict__ pv,
+                                                               int* __restrict__ pi) {
+  const int b = blockIdx.z, chunk = blockIdx.y;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  const int per = (NA + MATCH_COL_CHUNKS - 1) / MATCH_COL_CHUNKS;
+  const int a0 = chunk * per, a1 = min(NA, a0 + per);
+  float v = -INFINITY;
+  int idx = 0x7fffffff;
+  const bool masked = ig && j < NB && ig[(long)b * NB + j];
+  if (j < NB)
+    for (int a = a0 + wv; a < a1; a += 4) argmax_merge(v, idx, masked ? 1e-4f : corr[((long)b * NA + a) * NB + j], a);
+  __shared__ float rv[4][64];
+  __shared__ int ri[4][64];
+  rv[wv][lane] = v;
+  ri[wv][lane] = idx;
+  __syncthreads();
+  if (wv == 0 && j < NB) {
+    for (int w = 1; w < 4; ++w) argmax_merge(v, idx, rv[w][lane], ri[w][lane]);
+    const long o = ((long)b * MATCH_COL_CHUNKS + chunk) * NB + j;
+    pv[o] = v;
+    pi[o] = idx;
+  }
+}
+
+// inconsistent[b][j] from the chunk partials, q2k and s_mask
+__global__ void match_cyc_kernel(const float* __restrict__ pv, const int* __restrict__ pi, const int* __restrict__ q2k,
+                                 const int64_t* __restrict__ s_mask, int B, int NA, int NB, float* __restrict__ incons) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)B * NB) return;
+  const int b = (int)(e / NB), j = (int)(e - (long)b * NB);
+  float v = -INFINITY;
+  int k2q = 0x7fffffff;
+  for (int c = 0; c < MATCH_COL_CHUNKS; ++c) {
+    const long o = ((long)b * MATCH_COL_CHUNKS + c) * NB + j;
+    argmax_merge(v, k2q, pv[o], pi[o]);
+  }
+  if (k2q < 0 || k2q >= NA) k2q = 0;  // an all-NaN column: torch would return some index; keep it in range
+  const int r = q2k[(long)b * NA + k2q];
+  incons[e] = s_mask[(long)b * NB + j] != s_mask[(long)b * NB + r] ? 1.f : 0.f;
+}
+
+__global__ void match_mask_apply_kernel(float* __restrict__ corr, const uint8_t* ig, const float* incons, int B, int NA,
+                                        int NB) {
+  const long total = (long)B * NA * NB;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(e % NB);
+    const int b = (int)(e / ((long)NA * NB));
+    float v = corr[e];
+    if (ig && ig[(long)b * NB + j]) v = 1e-4f;
+    if (incons) v = v + incons[(long)b * NB + j] * -1000.f;
+    corr[e] = v;
+  }
+}
+
 // ---- WeightAverage (src/model/msm/msm_func.py:50-104), R = 3 ----
 // tpg [N][P][3co]: theta | phi | g of every pixel (1x1 convs as one GEMM, biases not yet
 // added); per pixel: cos_r = CosineSimilarity(phi(x_r), theta(x)) over its 3x3 replicate-padded
@@ -449,6 +550,27 @@ int launch_match_softmax(const float* corr, int B, int NA, int NB, float temp, i
 int launch_match_vt(const float* v, int B, int NB, int C, int ldp, float* vt, hipStream_t st) {
   hipLaunchKernelGGL(match_vt_kernel, dim3(cdiv(ldp, 32), cdiv(C, 32), B), dim3(256), 0, st, v, NB, C, ldp, vt);
   CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_match_masks(float* corr, int B, int NA, int NB, const uint8_t* ig, const int64_t* s_mask, float* incons,
+                       int* q2k, float* pv, int* pi, hipStream_t st) {
+  if (s_mask) {
+    hipLaunchKernelGGL(match_row_argmax_kernel, dim3(B * NA), dim3(256), 0, st, (const float*)corr, ig, NA, NB, q2k);
+    CWT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(match_col_argmax_kernel, dim3(cdiv(NB, 64), MATCH_COL_CHUNKS, B), dim3(256), 0, st,
+                       (const float*)corr, ig, NA, NB, pv, pi);
+    CWT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(match_cyc_kernel, dim3(cdiv((long)B * NB, 256)), dim3(256), 0, st, (const float*)pv,
+                       (const int*)pi, (const int*)q2k, s_mask, B, NA, NB, incons);
+    CWT_LAUNCH_CHECK();
+  }
+  if (ig || s_mask) {
+    const long total = (long)B * NA * NB;
+    hipLaunchKernelGGL(match_mask_apply_kernel, dim3((unsigned)std::min<long>(65536, cdiv(total, 256))), dim3(256), 0,
+                       st, corr, ig, s_mask ? (const float*)incons : (const float*)nullptr, B, NA, NB);
+    CWT_LAUNCH_CHECK();
+  }
   return 0;
 }
 

@@ -13,9 +13,9 @@ The modules keep the reference's parameter names (``NeighConsensus.conv.{0,2,4}.
 {weight,bias}``), so a reference state_dict loads as is.  Built: the default head of every MMN /
 MatchNet script -- CenterPivotConv4d ('red'), kernel sizes [3, 3, 3], channels [10, 10, 1],
 in_channel 1 or 2, symmetric or not -- and the MMN head of the mmn configs (rmid 'l34', all_lr
-'l', agg 'cat', wa True, red_dim False), forward only (inference).  Not built: the full Conv4d
-('cv4'), the spatial context encoder (sce), the cycle-consistency mask (cyc), ig_mask, agg 'sum',
-red_dim, forward_mmn (its MSBlock) and the MMN trainers' backward.
+'l', agg 'cat', wa True, red_dim False), forward only (inference), with MatchNet.forward's ig_mask and (round 3) its
+cycle-consistency mask (cyc, eval mode).  Not built: the full Conv4d ('cv4'), the spatial context
+encoder (sce), agg 'sum', red_dim, forward_mmn (its MSBlock) and the MMN trainers' backward.
 
 Parity is unpinned: the reference cannot be run here and holds no fixtures for
 this head; tests/test_gpu_match.py checks it against oracle/match_oracle.py, a float64
@@ -104,8 +104,8 @@ class MatchNet(torch.nn.Module):
                  cyc: bool = False, sym_mode: bool = True, cv_kernels=(3, 3, 3), cv_channels=(10, 10, 1),
                  device=None):
         super().__init__()
-        if sce or cyc:
-            raise NotImplementedError("MatchNet: the spatial context encoder and the cycle mask are not built")
+        if sce:
+            raise NotImplementedError("MatchNet: the spatial context encoder (sce) is not built")
         self.temp = temp
         self.sce, self.cyc = sce, cyc
         self.in_channel = in_channel
@@ -148,16 +148,56 @@ class MatchNet(torch.nn.Module):
         return (corr2d, wv) if ret_attn else wv
 
     def forward(self, fq_fea, fs_fea, v, s_mask=None, ig_mask=None, ret_corr=False, use_cyc=False, ret_cyc=False):
-        """match.py:103-140 without sce / cyc / ig_mask: normalised features -> get_corr ->
-        run_match_model -> softmax(temp * corr2d) -> v . attn^T."""
-        if ig_mask is not None or use_cyc or ret_cyc:
-            raise NotImplementedError("MatchNet.forward: ig_mask and the cycle mask are not built")
+        """match.py:103-140 (without sce): normalised features -> get_corr -> run_match_model ->
+        the ig mask and, with ``cyc`` and ``use_cyc``, the cycle-consistency mask (run_cyc,
+        match.py:165-182; cwt_match_masks) -> softmax(temp * corr2d) -> v . attn^T
+        (cwt_match_readout).  Returns as the reference: weighted_v, plus corr2d [B, h, w, h, w]
+        with ret_corr, plus the inconsistent mask [B, 1, h*w] with ret_cyc."""
         B, ch, h, w = fq_fea.shape
+        hw = h * w
         corr = get_corr(fq_fea, fs_fea)   # normalises both (the reference's F.normalize first is the same map)
-        corr2d, wv = self._run(corr.reshape(B, 1, h * w, h * w), h, w, v)
+        cyc_on = bool(self.cyc and use_cyc)
+        if ig_mask is None and not cyc_on:
+            if ret_cyc:   # the reference reads an unbound inconsistent_mask here
+                raise UnboundLocalError("ret_cyc needs the cycle mask (cyc=True and use_cyc=True)")
+            corr2d, wv = self._run(corr.reshape(B, 1, hw, hw), h, w, v)
+            return (wv, corr2d.reshape(B, h, w, h, w)) if ret_corr else wv
+        if cyc_on and s_mask is None:   # run_cyc returns None and the reference fails on it
+            raise ValueError("the cycle mask needs s_mask")
+        if cyc_on and self.training:
+            raise NotImplementedError("the cycle mask's Dropout(0.1) in training mode is not built; call .eval()")
+        corr2d, _ = self._run(corr.reshape(B, 1, hw, hw), h, w, None)
+        dev = corr2d.device
+        ig = None
+        if ig_mask is not None:
+            if ig_mask.numel() != B * hw:
+                raise ValueError("ig_mask must hold B * h * w entries (ig_mask.view(B, -1, h*w))")
+            ig = ig_mask.reshape(B, hw).to(device=dev, dtype=torch.uint8).contiguous()
+        sm, inc = None, None
+        if cyc_on:
+            if s_mask.numel() != B * hw:
+                raise ValueError("s_mask must hold B * h * w entries (s_mask.view(B, n_s))")
+            sm = s_mask.reshape(B, hw).to(device=dev, dtype=torch.int64).contiguous()
+            inc = torch.empty((B, hw), device=dev, dtype=torch.float32)
+        _lib.check(_lib.lib().cwt_match_masks(
+            _lib.ctx(dev.index), _lib.ptr(corr2d), B, hw, hw, _lib.ptr(ig) if ig is not None else None,
+            _lib.ptr(sm) if sm is not None else None, _lib.ptr(inc) if inc is not None else None,
+            _lib.stream_ptr(dev)), "cwt_match_masks")
+        vt = as_tokens(v if v.dim() == 4 else v.reshape(v.shape[0], v.shape[1], h, w))
+        Cv = vt.shape[-1] if vt.dim() == 3 else vt.shape[1]
+        wv = torch.empty((B, h, w, Cv), device=dev, dtype=torch.float32)
+        _lib.check(_lib.lib().cwt_match_readout(
+            _lib.ctx(dev.index), _lib.ptr(corr2d), B, hw, hw, float(self.temp), _lib.ptr(vt), Cv, _lib.ptr(wv),
+            _lib.stream_ptr(dev)), "cwt_match_readout")
+        wv = wv.permute(0, 3, 1, 2)
+        out = [wv]
         if ret_corr:
-            return wv, corr2d.reshape(B, h, w, h, w)
-        return wv
+            out.append(corr2d.reshape(B, h, w, h, w))
+        if ret_cyc:
+            if inc is None:
+                raise UnboundLocalError("ret_cyc needs the cycle mask (cyc=True and use_cyc=True)")
+            out.append(inc.unsqueeze(1))
+        return out[0] if len(out) == 1 else tuple(out)
 
 
 def init_match_params(mod: torch.nn.Module, seed: int = 0) -> None:

@@ -353,6 +353,21 @@ int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h,
                            int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
                            void* stream);
 
+/* MatchNet.forward's support masks on corr2d device [B][NA][NB], in place (src/model/match.py:
+ * 117-126 and run_cyc, match.py:165-182).  ig_mask device [B][NB] uint8 (NULL: none) sets every
+ * query row's entry of a masked support position to 1e-4.  With s_mask device [B][NB] int64 (the
+ * support label map; NULL: no cycle mask), after the ig mask: k2q[j] = argmax over the queries,
+ * q2k[a] = argmax over the supports (first index on ties, as torch's CPU max), inconsistent
+ * device [B][NB] = s_mask[j] != s_mask[q2k[k2q[j]]] as 0 / 1, and corr2d += inconsistent * -1000.
+ * The reference's Dropout(0.1) on the mask is its eval-mode identity. */
+int cwt_match_masks(cwt_ctx* ctx, float* corr2d, int B, int NA, int NB, const uint8_t* ig_mask,
+                    const int64_t* s_mask, float* inconsistent, void* stream);
+
+/* MatchNet's readout (match.py:128-130): weighted_v device [B][NA][Cv] = softmax(temp * corr2d,
+ * -1) . v, v device [B][NB][Cv] (NHWC tokens).  Exact fp32. */
+int cwt_match_readout(cwt_ctx* ctx, const float* corr2d, int B, int NA, int NB, float temp, const float* v, int Cv,
+                      float* weighted_v, void* stream);
+
 /* WeightAverage (src/model/msm/msm_func.py:50-104, R = 3; the MMN head's wa_<layer> modules,
  * mmn.py:27-34,53-55): x device [N][h][w][C] (NHWC tokens), C = c_in in {512, 1024, 2048};
  * w_tpg device [3 C/2][C] = conv_theta.weight, conv_phi.weight, conv_g.weight stacked (each

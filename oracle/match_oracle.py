@@ -73,6 +73,26 @@ def corr_forward(corr4d: torch.Tensor, v: torch.Tensor, layers, temp: float, sym
     return corr2d, wv
 
 
+def support_masks(corr2d: torch.Tensor, ig_mask=None, s_mask=None):
+    """match.py:117-126 with run_cyc (match.py:165-182) in eval mode (Dropout identity):
+    corr2d [B, N_q, N_s] -> (masked corr2d, inconsistent [B, N_s] or None).  Not in place."""
+    B, nq, ns = corr2d.shape
+    c = corr2d.clone()
+    if ig_mask is not None:
+        m = ig_mask.reshape(B, 1, ns).expand(c.shape)
+        c[m == True] = 0.0001   # noqa: E712  (the reference's spelling)
+    inc = None
+    if s_mask is not None:
+        sm = s_mask.reshape(B, ns)
+        k2q = c.max(1)[1]
+        q2k = c.max(2)[1]
+        re_map_idx = torch.gather(q2k, 1, k2q)
+        re_map_mask = torch.gather(sm, 1, re_map_idx)
+        inc = (~(sm == re_map_mask)).to(c.dtype)
+        c = c + inc.unsqueeze(1) * (-1000.0)
+    return c, inc
+
+
 def layers_from_state(sd, prefix: str = "NeighConsensus.conv.", dtype=torch.float64):
     out = []
     for i in (0, 2, 4):

@@ -154,3 +154,54 @@ def test_extract_mid_features(dev):
     errs = {k: rel(lst[k][0], ref[k]) for k in (2, 3, 4)}
     print(f"mid features: {errs}")
     assert max(errs.values()) < 1e-4, errs
+
+
+@pytest.mark.parametrize("use_ig,use_cyc", [(True, False), (False, True), (True, True)])
+def test_forward_support_masks(dev, use_ig, use_cyc):
+    """MatchNet.forward's ig_mask and cycle mask (match.py:117-126, 165-182).  The masks are
+    checked on the device's own corr2d (argmax decisions on float64 values would differ only at
+    ties the fp32 rounding creates): the oracle applies support_masks to the unmasked corr2d the
+    device returns, the inconsistent mask must match exactly, the masked corr2d and weighted_v at
+    2e-5 (weighted_v against the float64 softmax readout of the oracle's masked corr2d)."""
+    from few_shot_seg_cwt_amd.match import MatchNet, init_match_params
+    from oracle import match_oracle as M
+    B, C, h, w, Cv = 2, 64, 9, 11, 48
+    g = torch.Generator().manual_seed(31)
+    fq = torch.rand(B, C, h, w, generator=g).to(dev)
+    fs = torch.rand(B, C, h, w, generator=g).to(dev)
+    v = torch.randn(B, Cv, h, w, generator=g).to(dev)
+    ig = (torch.rand(B, h * w, generator=g) < 0.2) if use_ig else None
+    # a support label map of two regions, so some cycles land on the other label
+    sm = (torch.rand(B, h, w, generator=g) < 0.4).long() if use_cyc else None
+    net = MatchNet(temp=20.0, cyc=use_cyc, device=dev).eval()
+    init_match_params(net, 5)
+    _, corr_plain = net(fq, fs, v, ret_corr=True)
+    out = net(fq, fs, v, s_mask=sm.to(dev) if use_cyc else None, ig_mask=ig.to(dev) if use_ig else None,
+              ret_corr=True, use_cyc=use_cyc, ret_cyc=use_cyc)
+    wv, corr = out[0], out[1]
+    c_ref, inc_ref = M.support_masks(corr_plain.reshape(B, h * w, h * w).double().cpu(),
+                                     ig if use_ig else None, sm if use_cyc else None)
+    if use_cyc:
+        inc = out[2]
+        assert tuple(inc.shape) == (B, 1, h * w)
+        assert torch.equal(inc[:, 0].cpu().double(), inc_ref), "inconsistent mask"
+        assert 0 < int(inc_ref.sum()) < B * h * w
+    e_c = rel(corr.reshape(B, h * w, h * w), c_ref)
+    attn = torch.softmax(c_ref * 20.0, dim=-1)
+    wv_ref = torch.bmm(v.double().cpu().reshape(B, Cv, h * w), attn.transpose(1, 2)).reshape(B, Cv, h, w)
+    e_v = rel(wv, wv_ref)
+    print(f"MatchNet masks ig={use_ig} cyc={use_cyc}: corr2d {e_c:.2e} weighted_v {e_v:.2e}")
+    assert e_c < 1e-6 and e_v < TOL
+
+
+def test_forward_masks_errors(dev):
+    from few_shot_seg_cwt_amd.match import MatchNet
+    net = MatchNet(temp=20.0, cyc=True, device=dev)
+    f = torch.rand(1, 8, 4, 4, device=dev)
+    with pytest.raises(NotImplementedError):   # Dropout(0.1) of the mask in training mode
+        net(f, f, f, s_mask=torch.zeros(1, 4, 4, dtype=torch.long, device=dev), use_cyc=True)
+    net.eval()
+    with pytest.raises(ValueError):
+        net(f, f, f, s_mask=None, use_cyc=True)
+    with pytest.raises(UnboundLocalError):
+        MatchNet(temp=20.0, device=dev).eval()(f, f, f, ret_cyc=True)

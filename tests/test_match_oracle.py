@@ -65,3 +65,25 @@ def test_symmetric_consensus_is_swap_equivariant():
     y = M.neigh_consensus(x, layers, symmetric=True)
     ys = M.neigh_consensus(x.permute(0, 1, 4, 5, 2, 3), layers, symmetric=True).permute(0, 1, 4, 5, 2, 3)
     assert torch.allclose(y, ys, rtol=1e-12, atol=1e-12)
+
+
+def test_support_masks_against_loops():
+    """oracle support_masks (match.py:117-126, run_cyc 165-182, eval mode) against explicit
+    loops: the ig columns set to 1e-4, k2q / q2k first-index argmaxes, the -1000 offsets."""
+    from oracle import match_oracle as M
+    g = torch.Generator().manual_seed(4)
+    B, n = 2, 12
+    c = torch.rand(B, n, n, generator=g, dtype=torch.float64)
+    ig = torch.rand(B, n, generator=g) < 0.25
+    sm = (torch.rand(B, n, generator=g) < 0.5).long()
+    out, inc = M.support_masks(c, ig, sm)
+    for b in range(B):
+        cm = [[1e-4 if bool(ig[b, j]) else float(c[b, i, j]) for j in range(n)] for i in range(n)]
+        for j in range(n):
+            col = [cm[i][j] for i in range(n)]
+            k2q = col.index(max(col))
+            q2k = cm[k2q].index(max(cm[k2q]))
+            bad = int(sm[b, j]) != int(sm[b, q2k])
+            assert float(inc[b, j]) == (1.0 if bad else 0.0)
+            for i in range(n):
+                assert float(out[b, i, j]) == cm[i][j] + (-1000.0 if bad else 0.0)
