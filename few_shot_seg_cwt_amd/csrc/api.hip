@@ -72,6 +72,8 @@ int launch_to_channels_last(const float* x, int B, int C, long P, float* y, hipS
 int launch_add_inplace(float* y, const float* x, long n, hipStream_t st);
 int launch_match_softmax(const float* corr, int B, int NA, int NB, float temp, int ldp, float* P, hipStream_t st);
 int launch_match_vt(const float* v, int B, int NB, int C, int ldp, float* vt, hipStream_t st);
+int launch_cv4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* W,
+                      const float* bias, int swap, float* y, hipStream_t st);
 int launch_match_masks(float* corr, int B, int NA, int NB, const uint8_t* ig, const int64_t* s_mask, float* incons,
                        int* q2k, float* pv, int* pi, hipStream_t st);
 int launch_wa_attn(const float* tpg, int N, int h, int w, int co, const float* bt, const float* bp, const float* bg,
@@ -1268,9 +1270,9 @@ int cwt_mutual_matching(cwt_ctx* ctx, const float* x, int B, int NA, int NB, int
   return launch_mutual_matching(x, B, NA, NB, C, y, rm, cp, cm, (hipStream_t)stream);
 }
 
-int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
-                           int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
-                           void* stream) {
+static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
+                              int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
+                              void* stream, bool cv4) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
   CWT_CHECK(corr && nc_params && corr2d && B >= 1 && (L == 1 || L == 2) && h >= 1 && w >= 1,
             "bad arguments (in_channel 1 or 2)");
@@ -1296,8 +1298,30 @@ int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h,
     if ((rc = launch_to_channels_last(corr, B, L, P, (float*)x0, st))) return rc;
     if ((rc = launch_mutual_matching((const float*)x0, B, (int)NA, (int)NB, L, (float*)x0, rm, cp, cm, st))) return rc;
   }
-  // parameters per layer: conv1.weight [co][ci][3][3], conv1.bias [co], conv2.weight, conv2.bias
   const int ch[4] = {L, 10, 10, 1};
+  if (cv4) {
+    // Conv4d layers (conv4d.py:64-138): per layer weight [3][co][ci][3][3][3] (the reference's
+    // pre-permuted filter), bias [co]; the symmetric branch is the same stack with each filter's
+    // position pairs exchanged (cv4d_layer_kernel swap)
+    const float* cw[3][2];
+    const float* q = nc_params;
+    for (int l = 0; l < 3; ++l) {
+      cw[l][0] = q;
+      q += 81 * ch[l] * ch[l + 1];
+      cw[l][1] = q;
+      q += ch[l + 1];
+    }
+    for (int br = 0; br < (symmetric ? 2 : 1); ++br) {
+      const float* in = (const float*)x0;
+      float* outs[3] = {(float*)x1, (float*)x2, br ? (float*)y2 : (float*)y1};
+      for (int l = 0; l < 3; ++l) {
+        if ((rc = launch_cv4d_layer(in, B, h, w, h, w, ch[l], ch[l + 1], cw[l][0], cw[l][1], br, outs[l], st)))
+          return rc;
+        in = outs[l];
+      }
+    }
+  } else {
+  // parameters per layer: conv1.weight [co][ci][3][3], conv1.bias [co], conv2.weight, conv2.bias
   const float* lw[3][4];
   {
     const float* q = nc_params;
@@ -1323,6 +1347,7 @@ int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h,
       in = outs[l];
     }
   }
+  }
   if (symmetric && (rc = launch_add_inplace((float*)y1, (const float*)y2, B * P, st))) return rc;
   if ((rc = mm_ws(ctx, B, (int)NA, (int)NB, 1, &rm, &cp, &cm))) return rc;
   if ((rc = launch_mutual_matching((const float*)y1, B, (int)NA, (int)NB, 1, corr2d, rm, cp, cm, st))) return rc;
@@ -1340,6 +1365,18 @@ int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h,
   }
   p.end();
   return 0;
+}
+
+int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
+                           int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
+                           void* stream) {
+  return match_corr_forward(ctx, corr, B, L, h, w, nc_params, symmetric, temp, v, Cv, corr2d, weighted_v, stream, false);
+}
+
+int cwt_match_corr_forward_cv4(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
+                               int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
+                               void* stream) {
+  return match_corr_forward(ctx, corr, B, L, h, w, nc_params, symmetric, temp, v, Cv, corr2d, weighted_v, stream, true);
 }
 
 int cwt_match_masks(cwt_ctx* ctx, float* corr2d, int B, int NA, int NB, const uint8_t* ig_mask,

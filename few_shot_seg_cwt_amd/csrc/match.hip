@@ -267,6 +267,68 @@ __global__ __launch_bounds__(256) void match_vt_kernel(const float* __restrict__
   }
 }
 
+// ---- Conv4d ('cv4', src/model/conv4d.py:64-138) + ReLU, one NeighConsensus layer ----
+// x, y channels last [B][hA wA][hB wB][C].  W is the reference's pre-permuted filter
+// [k0][co][ci][k1][k2][k3] (Conv4d permutes it in its constructor), kernel 3, zero padding 1:
+// y(i,j,k,l) = relu(bias + sum W[d0][co][ci][d1][d2][d3] x(i+d0-1, j+d1-1, k+d2-1, l+d3-1)), the
+// per-slice conv3d sum of conv_4d.  swap = 1 applies the filter with (d0,d1) and (d2,d3)
+// exchanged: conv(x^T)^T of the symmetric mode as one pass.  One thread per output position,
+// every output channel; the filter tap-major in LDS (uniform broadcast reads).  fp32 VALU.
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void cv4d_layer_kernel(const float* __restrict__ x, int B, int hA, int wA, int hB,
+                                                         int wB, const float* __restrict__ W,
+                                                         const float* __restrict__ bias, int swap,
+                                                         float* __restrict__ y) {
+  __shared__ float wl[81][CIN][COUT];
+  for (int e = threadIdx.x; e < 81 * CIN * COUT; e += 256) {
+    // e walks the stored layout [d0][co][ci][d1][d2][d3]
+    const int d3 = e % 3, d2 = (e / 3) % 3, d1 = (e / 9) % 3;
+    const int ci = (e / 27) % CIN, co = (e / (27 * CIN)) % COUT, d0 = e / (27 * CIN * COUT);
+    const int tap = swap ? ((d2 * 3 + d3) * 3 + d0) * 3 + d1 : ((d0 * 3 + d1) * 3 + d2) * 3 + d3;
+    wl[tap][ci][co] = W[e];
+  }
+  __syncthreads();
+  const long NB = (long)hB * wB, P = (long)hA * wA * NB, total = (long)B * P;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(q / P);
+    const long pos = q - (long)b * P;
+    const int l = (int)(pos % wB), k = (int)((pos / wB) % hB);
+    const long pa = pos / NB;
+    const int j = (int)(pa % wA), i = (int)(pa / wA);
+    float acc[COUT];
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) acc[co] = bias[co];
+    for (int d0 = 0; d0 < 3; ++d0) {
+      const int ii = i + d0 - 1;
+      if ((unsigned)ii >= (unsigned)hA) continue;
+      for (int d1 = 0; d1 < 3; ++d1) {
+        const int jj = j + d1 - 1;
+        if ((unsigned)jj >= (unsigned)wA) continue;
+        for (int d2 = 0; d2 < 3; ++d2) {
+          const int kk = k + d2 - 1;
+          if ((unsigned)kk >= (unsigned)hB) continue;
+#pragma unroll
+          for (int d3 = 0; d3 < 3; ++d3) {
+            const int ll = l + d3 - 1;
+            if ((unsigned)ll >= (unsigned)wB) continue;
+            const float* xp = x + ((long)b * P + ((long)ii * wA + jj) * NB + (long)kk * wB + ll) * CIN;
+            const int tap = ((d0 * 3 + d1) * 3 + d2) * 3 + d3;
+#pragma unroll
+            for (int ci = 0; ci < CIN; ++ci) {
+              const float xv = xp[ci];
+#pragma unroll
+              for (int co = 0; co < COUT; ++co) acc[co] = fmaf(wl[tap][ci][co], xv, acc[co]);
+            }
+          }
+        }
+      }
+    }
+    float* yp = y + q * COUT;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) yp[co] = fmaxf(acc[co], 0.f);
+  }
+}
+
 // ---- MatchNet's support masks (match.py:117-126, run_cyc match.py:165-182) ----
 // ig_mask [B][NB] (uint8, nullable): corr2d[b][a][j] = 1e-4 where ig_mask[b][j] (every query a).
 // The cycle mask: k2q[j] = argmax over a of corr2d[a][j], q2k[a] = argmax over j of corr2d[a][j]
@@ -572,6 +634,24 @@ int launch_match_masks(float* corr, int B, int NA, int NB, const uint8_t* ig, co
     CWT_LAUNCH_CHECK();
   }
   return 0;
+}
+
+int launch_cv4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* W,
+                      const float* bias, int swap, float* y, hipStream_t st) {
+  const long total = (long)B * hA * wA * hB * wB;
+  const dim3 grid((unsigned)std::min<long>(65536, cdiv(total, 256)));
+#define CWT_CV4D(CI, CO)                                                                                      \
+  if (cin == CI && cout == CO) {                                                                              \
+    hipLaunchKernelGGL((cv4d_layer_kernel<CI, CO>), grid, dim3(256), 0, st, x, B, hA, wA, hB, wB, W, bias, swap, y); \
+    CWT_LAUNCH_CHECK();                                                                                       \
+    return 0;                                                                                                 \
+  }
+  CWT_CV4D(1, 10)
+  CWT_CV4D(2, 10)
+  CWT_CV4D(10, 10)
+  CWT_CV4D(10, 1)
+#undef CWT_CV4D
+  return fail(CWT_EARG, "cv4d layer: channels (1|2 -> 10, 10 -> 10, 10 -> 1) only");
 }
 
 }  // namespace cwt

@@ -3,7 +3,8 @@ HIP kernels (csrc/match.hip) behind the C ABI:
 
   MutualMatching(corr4d)                      src/model/match.py:21-53
   NeighConsensus(kernel_sizes, channels, ...)  src/model/match.py:56-85  (CenterPivotConv4d layers,
-                                               src/model/conv4d.py:11-62)
+                                               src/model/conv4d.py:11-62, or Conv4d layers,
+                                               conv4d.py:64-138)
   MatchNet(temp, cv_type, in_channel, ...)     src/model/match.py:88-163 (forward, corr_forward,
                                                run_match_model)
   WeightAverage(c_in, args)                    src/model/msm/msm_func.py:50-104
@@ -14,8 +15,9 @@ The modules keep the reference's parameter names (``NeighConsensus.conv.{0,2,4}.
 MatchNet script -- CenterPivotConv4d ('red'), kernel sizes [3, 3, 3], channels [10, 10, 1],
 in_channel 1 or 2, symmetric or not -- and the MMN head of the mmn configs (rmid 'l34', all_lr
 'l', agg 'cat', wa True, red_dim False), forward only (inference), with MatchNet.forward's ig_mask and (round 3) its
-cycle-consistency mask (cyc, eval mode).  Not built: the full Conv4d ('cv4'), the spatial context
-encoder (sce), agg 'sum', red_dim, forward_mmn (its MSBlock) and the MMN trainers' backward.
+cycle-consistency mask (cyc, eval mode), and NeighConsensus over full Conv4d layers ('cv4',
+fp32 VALU).  Not built: the spatial context encoder (sce), agg 'sum', red_dim, forward_mmn (its
+MSBlock) and the MMN trainers' backward.
 
 Parity is unpinned: the reference cannot be run here and holds no fixtures for
 this head; tests/test_gpu_match.py checks it against oracle/match_oracle.py, a float64
@@ -59,6 +61,25 @@ class CenterPivotConv4d(torch.nn.Module):
         self.conv2 = torch.nn.Conv2d(in_channels, out_channels, 3, padding=1, bias=True, device=device)
 
 
+class Conv4d(torch.nn.Module):
+    """conv4d.py:101-138 parameter holder: ``weight`` in the reference's pre-permuted layout
+    [k0][co][ci][k1][k2][k3] (Conv4d permutes it in its constructor, so a reference state_dict
+    holds that layout), ``bias`` [co]; _ConvNd's default initialisation on [co][ci][3][3][3][3].
+    Kernel 3, padding 1, stride 1; the layer runs inside NeighConsensus's device path."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size=(3,) * 4, padding=(1,) * 4, bias: bool = True,
+                 pre_permuted_filters: bool = True, device=None):
+        super().__init__()
+        if tuple(kernel_size) != (3,) * 4 or tuple(padding) != (1,) * 4 or not bias or not pre_permuted_filters:
+            raise NotImplementedError("Conv4d: kernel 3, padding 1, bias, pre-permuted filters only")
+        w = torch.empty(out_channels, in_channels, 3, 3, 3, 3)
+        torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        bound = 1.0 / math.sqrt(in_channels * 81)
+        self.weight = torch.nn.Parameter(w.permute(2, 0, 1, 3, 4, 5).contiguous().to(device))
+        self.bias = torch.nn.Parameter(torch.empty(out_channels).uniform_(-bound, bound).to(device))
+        self.pre_permuted_filters = True
+
+
 class NeighConsensus(torch.nn.Module):
     """match.py:56-85 with the default geometry: three CenterPivotConv4d + ReLU layers,
     channels in_channel -> 10 -> 10 -> 1, symmetric mode conv(x) + conv(x^T)^T."""
@@ -66,8 +87,9 @@ class NeighConsensus(torch.nn.Module):
     def __init__(self, kernel_sizes=(3, 3, 3), channels=(10, 10, 1), symmetric_mode: bool = True, conv: str = "red",
                  in_channel: int = 1, device=None):
         super().__init__()
-        if conv != "red":
-            raise NotImplementedError("NeighConsensus: only the CenterPivotConv4d ('red') layers are built")
+        if conv not in ("red", "cv4"):
+            raise ValueError(f"NeighConsensus: conv must be 'red' or 'cv4' (match.py:15), got {conv!r}")
+        self.conv_type = conv
         if tuple(kernel_sizes) != (3, 3, 3) or tuple(channels) != (10, 10, 1) or in_channel not in (1, 2):
             raise NotImplementedError("NeighConsensus: kernel sizes [3,3,3], channels [10,10,1], in_channel 1 or 2")
         self.symmetric_mode = symmetric_mode
@@ -77,7 +99,9 @@ class NeighConsensus(torch.nn.Module):
         mods = []
         ch_in = in_channel
         for ch_out in channels:
-            mods += [CenterPivotConv4d(ch_in, ch_out, device=device), torch.nn.ReLU(inplace=True)]
+            layer = Conv4d(ch_in, ch_out, device=device) if conv == "cv4" else CenterPivotConv4d(ch_in, ch_out,
+                                                                                                  device=device)
+            mods += [layer, torch.nn.ReLU(inplace=True)]
             ch_in = ch_out
         self.conv = torch.nn.Sequential(*mods)
         self._packed, self._packed_key = None, None
@@ -87,7 +111,10 @@ class NeighConsensus(torch.nn.Module):
         ps = []
         for i in (0, 2, 4):
             layer = self.conv[i]
-            ps += [layer.conv1.weight, layer.conv1.bias, layer.conv2.weight, layer.conv2.bias]
+            if self.conv_type == "cv4":
+                ps += [layer.weight, layer.bias]
+            else:
+                ps += [layer.conv1.weight, layer.conv1.bias, layer.conv2.weight, layer.conv2.bias]
         key = tuple((p.data_ptr(), p._version) for p in ps)
         if self._packed is None or key != self._packed_key:
             with torch.no_grad():
@@ -127,11 +154,12 @@ class MatchNet(torch.nn.Module):
             vt = as_tokens(v if v.dim() == 4 else v.reshape(v.shape[0], v.shape[1], h, w))
             Cv = vt.shape[1]
             wv = torch.empty((B, h, w, Cv), device=corr.device, dtype=torch.float32)
-        _lib.check(_lib.lib().cwt_match_corr_forward(
+        entry = "cwt_match_corr_forward_cv4" if self.NeighConsensus.conv_type == "cv4" else "cwt_match_corr_forward"
+        _lib.check(getattr(_lib.lib(), entry)(
             _lib.ctx(corr.device.index), _lib.ptr(corr), B, L, h, w, _lib.ptr(params),
             1 if self.NeighConsensus.symmetric_mode else 0, float(self.temp),
             _lib.ptr(vt) if vt is not None else None, Cv, _lib.ptr(corr2d), _lib.ptr(wv) if wv is not None else None,
-            _lib.stream_ptr(corr.device)), "cwt_match_corr_forward")
+            _lib.stream_ptr(corr.device)), entry)
         return corr2d, (wv.permute(0, 3, 1, 2) if wv is not None else None)
 
     def run_match_model(self, corr4d: torch.Tensor) -> torch.Tensor:
@@ -205,7 +233,7 @@ def init_match_params(mod: torch.nn.Module, seed: int = 0) -> None:
     g = torch.Generator().manual_seed(seed)
     with torch.no_grad():
         for name, p in mod.named_parameters():
-            fan_in = p.shape[1] * p.shape[2] * p.shape[3] if p.dim() == 4 else 100
+            fan_in = p.shape[1] * p.shape[2] * p.shape[3] if p.dim() == 4 else (p.shape[2] * 81 if p.dim() == 6 else 100)
             bound = 1.0 / math.sqrt(fan_in)
             p.copy_((torch.rand(p.shape, generator=g, dtype=torch.float32) * 2 - 1) * bound)
 

@@ -353,6 +353,14 @@ int cwt_match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h,
                            int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
                            void* stream);
 
+/* cwt_match_corr_forward with NeighConsensus over full Conv4d layers (conv='cv4', src/model/
+ * conv4d.py:64-138; match.py:15,56-85): nc_params device = per layer (0, 2, 4) the reference's
+ * pre-permuted weight [3][co][ci][3][3][3] then its bias [co].  fp32 VALU (no MFMA path: every
+ * reference config uses 'red'). */
+int cwt_match_corr_forward_cv4(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
+                               int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
+                               void* stream);
+
 /* MatchNet.forward's support masks on corr2d device [B][NA][NB], in place (src/model/match.py:
  * 117-126 and run_cyc, match.py:165-182).  ig_mask device [B][NB] uint8 (NULL: none) sets every
  * query row's entry of a masked support position to 1e-4.  With s_mask device [B][NB] int64 (the

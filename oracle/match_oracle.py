@@ -45,6 +45,37 @@ def center_pivot_conv4d(x: torch.Tensor, w1, b1, w2, b2) -> torch.Tensor:
     return ya + yb
 
 
+def conv4d(x: torch.Tensor, w_perm, b) -> torch.Tensor:
+    """conv4d.py:64-98 (conv_4d) at kernel 3: w_perm is the pre-permuted filter [k0][co][ci][k1]
+    [k2][k3]; for each first-dimension slice i, conv3d of the zero-padded input slices i-1, i,
+    i+1 with the matching filter slices (the bias once, with the centre slice)."""
+    B, C, h, w, d, t = x.shape
+    xs = x.permute(2, 0, 1, 3, 4, 5)
+    pad = w_perm.shape[0] // 2
+    Z = torch.zeros((pad, B, C, w, d, t), dtype=x.dtype)
+    xp = torch.cat((Z, xs, Z), 0)
+    out = []
+    for i in range(h):
+        o = F.conv3d(xp[i + pad], w_perm[pad], bias=b, stride=1, padding=pad)
+        for p_ in range(1, pad + 1):
+            o = o + F.conv3d(xp[i + pad - p_], w_perm[pad - p_], bias=None, stride=1, padding=pad)
+            o = o + F.conv3d(xp[i + pad + p_], w_perm[pad + p_], bias=None, stride=1, padding=pad)
+        out.append(o)
+    return torch.stack(out, 0).permute(1, 2, 0, 3, 4, 5)
+
+
+def neigh_consensus_cv4(x: torch.Tensor, layers, symmetric: bool = True) -> torch.Tensor:
+    """match.py:56-85 with conv='cv4': layers = [(w_perm, b)] * 3, each Conv4d then ReLU."""
+    def stack(z):
+        for (wp, b) in layers:
+            z = torch.relu(conv4d(z, wp, b))
+        return z
+    y = stack(x)
+    if symmetric:
+        y = y + stack(x.permute(0, 1, 4, 5, 2, 3)).permute(0, 1, 4, 5, 2, 3)
+    return y
+
+
 def neigh_consensus(x: torch.Tensor, layers, symmetric: bool = True) -> torch.Tensor:
     """match.py:56-85: layers = [(w1, b1, w2, b2)] * 3, each CenterPivotConv4d then ReLU;
     symmetric mode adds the stack applied to the pair-swapped tensor, swapped back."""
@@ -59,8 +90,9 @@ def neigh_consensus(x: torch.Tensor, layers, symmetric: bool = True) -> torch.Te
 
 
 def run_match_model(corr4d: torch.Tensor, layers, symmetric: bool = True) -> torch.Tensor:
-    """match.py:159-163."""
-    return mutual_matching(neigh_consensus(mutual_matching(corr4d), layers, symmetric))
+    """match.py:159-163 (layers of 2 tensors: Conv4d 'cv4'; of 4: CenterPivotConv4d 'red')."""
+    nc = neigh_consensus_cv4 if len(layers[0]) == 2 else neigh_consensus
+    return mutual_matching(nc(mutual_matching(corr4d), layers, symmetric))
 
 
 def corr_forward(corr4d: torch.Tensor, v: torch.Tensor, layers, temp: float, symmetric: bool = True):
@@ -97,6 +129,9 @@ def layers_from_state(sd, prefix: str = "NeighConsensus.conv.", dtype=torch.floa
     out = []
     for i in (0, 2, 4):
         p = f"{prefix}{i}."
+        if p + "weight" in sd:   # Conv4d ('cv4')
+            out.append((sd[p + "weight"].to(dtype), sd[p + "bias"].to(dtype)))
+            continue
         out.append(tuple(sd[p + n].to(dtype) for n in ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias")))
     return out
 

@@ -205,3 +205,25 @@ def test_forward_masks_errors(dev):
         net(f, f, f, s_mask=None, use_cyc=True)
     with pytest.raises(UnboundLocalError):
         MatchNet(temp=20.0, device=dev).eval()(f, f, f, ret_cyc=True)
+
+
+@pytest.mark.parametrize("L,h,w,sym", [(1, 6, 7, True), (2, 5, 5, True), (1, 7, 4, False)])
+def test_corr_forward_cv4(dev, L, h, w, sym):
+    """NeighConsensus over full Conv4d layers (conv='cv4', conv4d.py:64-138) through
+    corr_forward, against the oracle's per-slice conv3d restatement in float64."""
+    from few_shot_seg_cwt_amd.match import MatchNet, init_match_params
+    from oracle import match_oracle as M
+    net = MatchNet(temp=20.0, cv_type="cv4", in_channel=L, sym_mode=sym, device=dev)
+    init_match_params(net, 13)
+    sd = {k: t.detach().double().cpu() for k, t in net.state_dict().items()}
+    assert tuple(sd["NeighConsensus.conv.0.weight"].shape) == (3, 10, L, 3, 3, 3)
+    assert set(sd) == {f"NeighConsensus.conv.{i}.{n}" for i in (0, 2, 4) for n in ("weight", "bias")}
+    B, Cv = 1, 24
+    corr = _corr(dev, B, L, h, w, 17)
+    g = torch.Generator().manual_seed(18)
+    v = torch.randn(B, Cv, h, w, generator=g).to(dev)
+    corr2d, wv = net.corr_forward(corr, v, ret_attn=True)
+    rc, rwv = M.corr_forward(corr.double().cpu(), v.double().cpu(), M.layers_from_state(sd), 20.0, sym)
+    e_c, e_v = rel(corr2d, rc), rel(wv, rwv)
+    print(f"corr_forward cv4 L={L} {h}x{w} sym={sym}: corr2d {e_c:.2e} weighted_v {e_v:.2e}")
+    assert e_c < TOL and e_v < TOL

@@ -87,3 +87,32 @@ def test_support_masks_against_loops():
             assert float(inc[b, j]) == (1.0 if bad else 0.0)
             for i in range(n):
                 assert float(out[b, i, j]) == cm[i][j] + (-1000.0 if bad else 0.0)
+
+
+def test_conv4d_against_direct_sum_and_swap():
+    """oracle conv4d (conv_4d's per-slice conv3d sum, conv4d.py:64-98, pre-permuted filter)
+    against the direct 4-D cross-correlation with zero padding; and the identity the device's
+    symmetric branch uses: conv(x^T)^T = conv(x) with the filter's position pairs exchanged."""
+    from oracle import match_oracle as M
+    g = torch.Generator().manual_seed(8)
+    B, C, O = 1, 2, 3
+    sh = (3, 4, 3, 2)
+    x = torch.rand(B, C, *sh, generator=g, dtype=torch.float64)
+    w = torch.rand(O, C, 3, 3, 3, 3, generator=g, dtype=torch.float64) - 0.5
+    b = torch.rand(O, generator=g, dtype=torch.float64)
+    wp = w.permute(2, 0, 1, 3, 4, 5).contiguous()
+    y = M.conv4d(x, wp, b)
+    xpad = torch.nn.functional.pad(x, (1, 1, 1, 1, 1, 1, 1, 1))
+    ref = torch.zeros(B, O, *sh, dtype=torch.float64)
+    for i in range(sh[0]):
+        for j in range(sh[1]):
+            for k in range(sh[2]):
+                for l in range(sh[3]):
+                    patch = xpad[0, :, i:i + 3, j:j + 3, k:k + 3, l:l + 3]
+                    ref[0, :, i, j, k, l] = (w * patch[None]).sum(dim=(1, 2, 3, 4, 5)) + b
+    assert torch.allclose(y, ref, atol=1e-12)
+    xs = torch.rand(B, C, 3, 4, 3, 4, generator=g, dtype=torch.float64)
+    lhs = M.conv4d(xs.permute(0, 1, 4, 5, 2, 3), wp, b).permute(0, 1, 4, 5, 2, 3)
+    w_sw = w.permute(0, 1, 4, 5, 2, 3)   # filter taps (u0, u1, u2, u3) <- (u2, u3, u0, u1)
+    rhs = M.conv4d(xs, w_sw.permute(2, 0, 1, 3, 4, 5).contiguous(), b)
+    assert torch.allclose(lhs, rhs, atol=1e-12)
