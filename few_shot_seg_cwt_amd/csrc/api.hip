@@ -74,6 +74,7 @@ int launch_match_softmax(const float* corr, int B, int NA, int NB, float temp, i
 int launch_match_vt(const float* v, int B, int NB, int C, int ldp, float* vt, hipStream_t st);
 int launch_cv4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* W,
                       const float* bias, int swap, float* y, hipStream_t st);
+int launch_sce_descriptor(const float* x, int B, int h, int w, int C, int k, int ldg, float* g, hipStream_t st);
 int launch_match_masks(float* corr, int B, int NA, int NB, const uint8_t* ig, const int64_t* s_mask, float* incons,
                        int* q2k, float* pv, int* pi, hipStream_t st);
 int launch_wa_attn(const float* tpg, int N, int h, int w, int co, const float* bt, const float* bp, const float* bg,
@@ -1377,6 +1378,19 @@ int cwt_match_corr_forward_cv4(cwt_ctx* ctx, const float* corr, int B, int L, in
                                int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
                                void* stream) {
   return match_corr_forward(ctx, corr, B, L, h, w, nc_params, symmetric, temp, v, Cv, corr2d, weighted_v, stream, true);
+}
+
+int cwt_sce_descriptor(cwt_ctx* ctx, const float* x, int B, int h, int w, int C, int k, int ldg, float* g,
+                       void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && g && B >= 1 && h >= 1 && w >= 1 && C >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  Prof p(ctx, st, "sce_descriptor", 2.0 * B * h * w * (double)k * k * C, 4.0 * B * h * w * ((double)C + ldg));
+  int rc;
+  if ((rc = launch_sce_descriptor(x, B, h, w, C, k, ldg, g, st))) return rc;
+  p.end();
+  return 0;
 }
 
 int cwt_match_masks(cwt_ctx* ctx, float* corr2d, int B, int NA, int NB, const uint8_t* ig_mask,

@@ -329,6 +329,47 @@ __global__ __launch_bounds__(256) void cv4d_layer_kernel(const float* __restrict
   }
 }
 
+// ---- Spatial context descriptor (src/model/base/spatial_context.py:13-65) ----
+// x tokens [B][h][w][C]; g [B][h w][ldg]: g[o] = <x(p), x(p + offset o)> over the k x k window
+// (zero outside the map), then featureL2Norm: g / sqrt(sum g^2 + 1e-6); columns k^2 .. ldg-1 zero.
+// One workgroup per pixel: the pixel's feature in LDS, each wave one window offset at a time
+// (lanes over channels, coalesced), the window in LDS for the norm.
+constexpr int SCE_MAXK2 = 32 * 32;
+__global__ __launch_bounds__(256) void sce_descriptor_kernel(const float* __restrict__ x, int h, int w, int C, int k,
+                                                             int ldg, float* __restrict__ g) {
+  extern __shared__ float sm_sce[];  // q [C], win [k*k]
+  float* q = sm_sce;
+  float* win = sm_sce + C;
+  const long pix = blockIdx.x;  // b * h * w + y * w + xx
+  const long hw = (long)h * w;
+  const int b = (int)(pix / hw);
+  const int yy = (int)((pix % hw) / w), xx = (int)(pix % w);
+  const float* xb = x + (long)b * hw * C;
+  for (int c = threadIdx.x; c < C; c += 256) q[c] = xb[((long)yy * w + xx) * C + c];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, pad = k / 2, k2 = k * k;
+  for (int o = wv; o < k2; o += 4) {
+    const int ny = yy + o / k - pad, nx = xx + o % k - pad;
+    float s = 0.f;
+    if ((unsigned)ny < (unsigned)h && (unsigned)nx < (unsigned)w) {
+      const float* xn = xb + ((long)ny * w + nx) * C;
+      for (int c = lane; c < C; c += 64) s = fmaf(q[c], xn[c], s);
+      s = wave_sum_dpp(s);
+    }
+    if (lane == 0) win[o] = s;
+  }
+  __syncthreads();
+  float ss = 0.f;
+  for (int o = threadIdx.x; o < k2; o += 256) ss = fmaf(win[o], win[o], ss);
+  ss = wave_sum_dpp(ss);
+  __shared__ float red[4];
+  if (lane == 0) red[wv] = ss;
+  __syncthreads();
+  const float inv = 1.f / sqrtf(((red[0] + red[1]) + (red[2] + red[3])) + 1e-6f);
+  float* gp = g + pix * ldg;
+  for (int o = threadIdx.x; o < ldg; o += 256) gp[o] = o < k2 ? win[o] * inv : 0.f;
+}
+
 // ---- MatchNet's support masks (match.py:117-126, run_cyc match.py:165-182) ----
 // ig_mask [B][NB] (uint8, nullable): corr2d[b][a][j] = 1e-4 where ig_mask[b][j] (every query a).
 // The cycle mask: k2q[j] = argmax over a of corr2d[a][j], q2k[a] = argmax over j of corr2d[a][j]
@@ -652,6 +693,15 @@ int launch_cv4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int
   CWT_CV4D(10, 1)
 #undef CWT_CV4D
   return fail(CWT_EARG, "cv4d layer: channels (1|2 -> 10, 10 -> 10, 10 -> 1) only");
+}
+
+int launch_sce_descriptor(const float* x, int B, int h, int w, int C, int k, int ldg, float* g, hipStream_t st) {
+  if (k < 1 || k % 2 == 0 || k * k > SCE_MAXK2 || ldg < k * k) return fail(CWT_EARG, "sce: odd kernel size, k*k <= 1024");
+  const size_t lds = (size_t)(C + k * k) * 4;
+  if (lds > 64 * 1024) return fail(CWT_EARG, "sce: C + k*k floats must fit 64 KB of LDS");
+  hipLaunchKernelGGL(sce_descriptor_kernel, dim3((unsigned)((long)B * h * w)), dim3(256), lds, st, x, h, w, C, k, ldg, g);
+  CWT_LAUNCH_CHECK();
+  return 0;
 }
 
 }  // namespace cwt

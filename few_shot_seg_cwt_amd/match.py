@@ -16,8 +16,8 @@ MatchNet script -- CenterPivotConv4d ('red'), kernel sizes [3, 3, 3], channels [
 in_channel 1 or 2, symmetric or not -- and the MMN head of the mmn configs (rmid 'l34', all_lr
 'l', agg 'cat', wa True, red_dim False), forward only (inference), with MatchNet.forward's ig_mask and (round 3) its
 cycle-consistency mask (cyc, eval mode), and NeighConsensus over full Conv4d layers ('cv4',
-fp32 VALU).  Not built: the spatial context encoder (sce), agg 'sum', red_dim, forward_mmn (its
-MSBlock) and the MMN trainers' backward.
+fp32 VALU), and the spatial context encoder (sce, spatial_context.py).  Not built: agg 'sum',
+red_dim, forward_mmn (its MSBlock) and the MMN trainers' backward.
 
 Parity is unpinned: the reference cannot be run here and holds no fixtures for
 this head; tests/test_gpu_match.py checks it against oracle/match_oracle.py, a float64
@@ -123,6 +123,52 @@ class NeighConsensus(torch.nn.Module):
         return self._packed
 
 
+class SpatialContextEncoder(torch.nn.Module):
+    """src/model/base/spatial_context.py:68-110: x [B, C, h, w] -> relu(conv1x1(cat(x,
+    featureL2Norm(generate_spatial_descriptor(x, k))))) [B, hidden, h, w].  The descriptor on
+    the device (cwt_sce_descriptor), the 1x1 conv as two accumulated f32-MFMA GEMMs over the
+    concatenation's two segments (detr.linear), the descriptor segment padded to a multiple of 4
+    columns with zero weights.  Keeps the reference's ``embeddingFea.0.{weight,bias}``."""
+
+    def __init__(self, kernel_size: int = 25, input_dim: int = 25 * 25 + 2048, hidden_dim: int = 2048, device=None):
+        super().__init__()
+        self.kernel_size = kernel_size
+        self.embeddingFea = torch.nn.Sequential(torch.nn.Conv2d(input_dim, hidden_dim, 1, padding=0, device=device),
+                                                torch.nn.ReLU(inplace=True))
+        self._wsplit, self._wkey = None, None
+
+    def _weights(self, C: int, ldg: int):
+        conv = self.embeddingFea[0]
+        key = (conv.weight.data_ptr(), conv.weight._version, C, ldg)
+        if self._wsplit is None or key != self._wkey:
+            with torch.no_grad():
+                W = conv.weight.detach().reshape(conv.weight.shape[0], -1).float()
+                k2 = self.kernel_size ** 2
+                if W.shape[1] != C + k2:
+                    raise ValueError(f"SpatialContextEncoder: input_dim {W.shape[1]} != C + k^2 = {C + k2}")
+                wg = torch.zeros((W.shape[0], ldg), device=W.device, dtype=torch.float32)
+                wg[:, :k2] = W[:, C:]
+                self._wsplit = (W[:, :C].contiguous(), wg.contiguous())
+            self._wkey = key
+        return self._wsplit
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from .detr import linear
+        xt = as_tokens(x)
+        B, C, h, w = xt.shape
+        k = self.kernel_size
+        ldg = (k * k + 3) & ~3
+        g = torch.empty((B * h * w, ldg), device=x.device, dtype=torch.float32)
+        _lib.check(_lib.lib().cwt_sce_descriptor(_lib.ctx(x.device.index), _lib.ptr(xt), B, h, w, C, k, ldg,
+                                                 _lib.ptr(g), _lib.stream_ptr(x.device)), "cwt_sce_descriptor")
+        wx, wg = self._weights(C, ldg)
+        tok = xt.permute(0, 2, 3, 1).reshape(B * h * w, C)   # a view of the NHWC storage
+        out = linear(tok, wx)
+        linear(g, wg, self.embeddingFea[0].bias, relu=True, out=out, accumulate=True)
+        return out.reshape(B, h, w, -1).permute(0, 3, 1, 2)
+
+
 class MatchNet(torch.nn.Module):
     """match.py:88-163.  forward(fq_fea, fs_fea, v) and corr_forward(corr4d, v, ret_attn) on the
     device; v is the support feature map [B, Cv, h, w] (returned weighted_v has its shape)."""
@@ -131,12 +177,13 @@ class MatchNet(torch.nn.Module):
                  cyc: bool = False, sym_mode: bool = True, cv_kernels=(3, 3, 3), cv_channels=(10, 10, 1),
                  device=None):
         super().__init__()
-        if sce:
-            raise NotImplementedError("MatchNet: the spatial context encoder (sce) is not built")
         self.temp = temp
         self.sce, self.cyc = sce, cyc
         self.in_channel = in_channel
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if sce:   # match.py:95-97
+            self.SpatialContextEncoder = SpatialContextEncoder(kernel_size=25, input_dim=25 * 25 + 2048, hidden_dim=2048,
+                                                               device=dev)
         self.NeighConsensus = NeighConsensus(kernel_sizes=cv_kernels, channels=cv_channels, symmetric_mode=sym_mode,
                                              conv=cv_type, in_channel=in_channel, device=dev)
 
@@ -176,13 +223,18 @@ class MatchNet(torch.nn.Module):
         return (corr2d, wv) if ret_attn else wv
 
     def forward(self, fq_fea, fs_fea, v, s_mask=None, ig_mask=None, ret_corr=False, use_cyc=False, ret_cyc=False):
-        """match.py:103-140 (without sce): normalised features -> get_corr -> run_match_model ->
+        """match.py:103-140: normalised features (-> the spatial context encoder with ``sce``) ->
+        get_corr -> run_match_model ->
         the ig mask and, with ``cyc`` and ``use_cyc``, the cycle-consistency mask (run_cyc,
         match.py:165-182; cwt_match_masks) -> softmax(temp * corr2d) -> v . attn^T
         (cwt_match_readout).  Returns as the reference: weighted_v, plus corr2d [B, h, w, h, w]
         with ret_corr, plus the inconsistent mask [B, 1, h*w] with ret_cyc."""
         B, ch, h, w = fq_fea.shape
         hw = h * w
+        if self.sce:   # match.py:108-113: F.normalize, then the encoder on both maps
+            from .detr import norm_blend
+            fq_fea = self.SpatialContextEncoder(norm_blend(fq_fea, fq_fea, 0.0))   # normalize(a) + normalize(a) * 0
+            fs_fea = self.SpatialContextEncoder(norm_blend(fs_fea, fs_fea, 0.0))
         corr = get_corr(fq_fea, fs_fea)   # normalises both (the reference's F.normalize first is the same map)
         cyc_on = bool(self.cyc and use_cyc)
         if ig_mask is None and not cyc_on:

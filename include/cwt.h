@@ -361,6 +361,14 @@ int cwt_match_corr_forward_cv4(cwt_ctx* ctx, const float* corr, int B, int L, in
                                int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
                                void* stream);
 
+/* The spatial context descriptor of MatchNet's sce option (src/model/base/spatial_context.py:
+ * 13-65, generate_spatial_descriptor + featureL2Norm): x device [B][h][w][C] (NHWC tokens), k odd
+ * (the reference uses 25), g device [B][h*w][ldg], ldg >= k*k: the dot products of each pixel's
+ * feature with its k x k window (zero padded), divided by sqrt(sum of squares + 1e-6); columns
+ * k*k .. ldg-1 are zero.  C + k*k floats must fit 64 KB.  Exact fp32. */
+int cwt_sce_descriptor(cwt_ctx* ctx, const float* x, int B, int h, int w, int C, int k, int ldg, float* g,
+                       void* stream);
+
 /* MatchNet.forward's support masks on corr2d device [B][NA][NB], in place (src/model/match.py:
  * 117-126 and run_cyc, match.py:165-182).  ig_mask device [B][NB] uint8 (NULL: none) sets every
  * query row's entry of a masked support position to 1e-4.  With s_mask device [B][NB] int64 (the

@@ -105,6 +105,23 @@ def corr_forward(corr4d: torch.Tensor, v: torch.Tensor, layers, temp: float, sym
     return corr2d, wv
 
 
+def spatial_descriptor(x: torch.Tensor, k: int) -> torch.Tensor:
+    """spatial_context.py:13-56 (generate_spatial_descriptor): x [B, C, h, w] -> [B, k*k, h, w],
+    the dot product of each pixel's feature with every position of its zero-padded k x k
+    window (row-major window order)."""
+    B, C, h, w = x.shape
+    pad = k // 2
+    patches = F.unfold(x, k, padding=pad).reshape(B, C, k * k, h * w)
+    return (patches * x.reshape(B, C, 1, h * w)).sum(1).reshape(B, k * k, h, w)
+
+
+def spatial_context_encoder(x: torch.Tensor, k: int, weight, bias) -> torch.Tensor:
+    """spatial_context.py:59-110: featureL2Norm (eps 1e-6 inside the root), cat, 1x1 conv, ReLU."""
+    g = spatial_descriptor(x, k)
+    g = g / torch.pow(torch.sum(g * g, 1) + 1e-6, 0.5).unsqueeze(1)
+    return torch.relu(F.conv2d(torch.cat([x, g], 1), weight, bias))
+
+
 def support_masks(corr2d: torch.Tensor, ig_mask=None, s_mask=None):
     """match.py:117-126 with run_cyc (match.py:165-182) in eval mode (Dropout identity):
     corr2d [B, N_q, N_s] -> (masked corr2d, inconsistent [B, N_s] or None).  Not in place."""

@@ -227,3 +227,51 @@ def test_corr_forward_cv4(dev, L, h, w, sym):
     e_c, e_v = rel(corr2d, rc), rel(wv, rwv)
     print(f"corr_forward cv4 L={L} {h}x{w} sym={sym}: corr2d {e_c:.2e} weighted_v {e_v:.2e}")
     assert e_c < TOL and e_v < TOL
+
+
+@pytest.mark.parametrize("C,h,w,k", [(2048, 13, 11, 25), (64, 9, 8, 5)])
+def test_spatial_context_encoder(dev, C, h, w, k):
+    """SpatialContextEncoder (spatial_context.py:13-110) against the float64 oracle: the
+    window descriptor, featureL2Norm, the concatenation and the 1x1 conv + ReLU."""
+    from few_shot_seg_cwt_amd.match import SpatialContextEncoder, init_match_params
+    from oracle import match_oracle as M
+    hidden = 2048 if C == 2048 else 96
+    enc = SpatialContextEncoder(kernel_size=k, input_dim=k * k + C, hidden_dim=hidden, device=dev)
+    init_match_params(enc, 21)
+    g = torch.Generator().manual_seed(22)
+    x = torch.nn.functional.normalize(torch.rand(2, C, h, w, generator=g), dim=1)
+    y = enc(x.to(dev))
+    sd = {n: t.detach().double().cpu() for n, t in enc.state_dict().items()}
+    assert set(sd) == {"embeddingFea.0.weight", "embeddingFea.0.bias"}
+    ref = M.spatial_context_encoder(x.double(), k, sd["embeddingFea.0.weight"], sd["embeddingFea.0.bias"])
+    e = rel(y, ref)
+    print(f"SpatialContextEncoder C={C} {h}x{w} k={k}: {e:.2e}")
+    assert e < 1e-5
+
+
+def test_matchnet_forward_sce(dev):
+    """MatchNet(sce=True).forward (match.py:95-97,108-113) against the oracle chain:
+    normalize -> encoder -> get_corr -> run_match_model -> softmax readout."""
+    from few_shot_seg_cwt_amd.match import MatchNet, init_match_params
+    from oracle import match_oracle as M
+    B, C, h, w, Cv = 1, 2048, 8, 9, 32
+    net = MatchNet(temp=20.0, sce=True, device=dev).eval()
+    init_match_params(net, 23)
+    g = torch.Generator().manual_seed(24)
+    fq, fs = torch.rand(B, C, h, w, generator=g), torch.rand(B, C, h, w, generator=g)
+    v = torch.randn(B, Cv, h, w, generator=g)
+    wv, corr = net(fq.to(dev), fs.to(dev), v.to(dev), ret_corr=True)
+    sd = {n: t.detach().double().cpu() for n, t in net.state_dict().items()}
+    W, b = sd["SpatialContextEncoder.embeddingFea.0.weight"], sd["SpatialContextEncoder.embeddingFea.0.bias"]
+    eq = M.spatial_context_encoder(torch.nn.functional.normalize(fq.double(), dim=1), 25, W, b)
+    es = M.spatial_context_encoder(torch.nn.functional.normalize(fs.double(), dim=1), 25, W, b)
+    nq = torch.nn.functional.normalize(eq, dim=1).reshape(B, -1, h * w)
+    ns = torch.nn.functional.normalize(es, dim=1).reshape(B, -1, h * w)
+    corr0 = torch.bmm(nq.transpose(1, 2), ns).reshape(B, 1, h, w, h, w)
+    rc, rwv = M.corr_forward(corr0, v.double(), M.layers_from_state(sd), 20.0, True)
+    e_c, e_v = rel(corr.reshape(B, h * w, h * w), rc), rel(wv, rwv)
+    print(f"MatchNet sce: corr2d {e_c:.2e} weighted_v {e_v:.2e}")
+    # the encoder's ReLU features are nearly parallel (cosines near 1), so corr2d carries the
+    # chain's fp32 rounding at ~1e-5 and the temp-20 softmax scales it by up to 20 in weighted_v
+    # (measured 6.8e-6 / 2.8e-5); each stage alone is within 1e-5 (tests above)
+    assert e_c < TOL and e_v < 5 * TOL

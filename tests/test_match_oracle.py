@@ -116,3 +116,21 @@ def test_conv4d_against_direct_sum_and_swap():
     w_sw = w.permute(0, 1, 4, 5, 2, 3)   # filter taps (u0, u1, u2, u3) <- (u2, u3, u0, u1)
     rhs = M.conv4d(xs, w_sw.permute(2, 0, 1, 3, 4, 5).contiguous(), b)
     assert torch.allclose(lhs, rhs, atol=1e-12)
+
+
+def test_spatial_descriptor_against_loops():
+    """oracle spatial_descriptor (unfold form) against generate_spatial_descriptor's per-pixel
+    window loop (spatial_context.py:13-56) on a small map."""
+    from oracle import match_oracle as M
+    g = torch.Generator().manual_seed(6)
+    B, C, h, w, k = 2, 5, 6, 7, 5
+    x = torch.rand(B, C, h, w, generator=g, dtype=torch.float64)
+    d = M.spatial_descriptor(x, k)
+    pad = k // 2
+    xp = torch.nn.functional.pad(x, (pad, pad, pad, pad))
+    for hi in range(h):
+        for wj in range(w):
+            q = x[:, :, hi, wj]
+            patch = xp[:, :, hi:hi + k, wj:wj + k].reshape(B, C, k * k)
+            ref = torch.bmm(q.unsqueeze(1), patch).squeeze(1)
+            assert torch.allclose(d[:, :, hi, wj], ref, atol=1e-12)
