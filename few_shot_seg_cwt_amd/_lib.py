@@ -63,6 +63,7 @@ SIGNATURES = {
     "cwt_match_corr_forward": (_I, [_P, _P, _I, _I, _I, _I, _P, _I, _F, _P, _I, _P, _P, _P]),
     "cwt_match_corr_forward_cv4": (_I, [_P, _P, _I, _I, _I, _I, _P, _I, _F, _P, _I, _P, _P, _P]),
     "cwt_match_masks": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
+    "cwt_channel_sum": (_I, [_P, _P, _I, _I, _I64, _P, _P]),
     "cwt_sce_descriptor": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "cwt_match_readout": (_I, [_P, _P, _I, _I, _I, _F, _P, _I, _P, _P]),
     "cwt_weight_average": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),

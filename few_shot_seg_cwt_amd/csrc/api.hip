@@ -75,6 +75,7 @@ int launch_match_vt(const float* v, int B, int NB, int C, int ldp, float* vt, hi
 int launch_cv4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* W,
                       const float* bias, int swap, float* y, hipStream_t st);
 int launch_sce_descriptor(const float* x, int B, int h, int w, int C, int k, int ldg, float* g, hipStream_t st);
+int launch_channel_sum(const float* x, int B, int L, long P, float* y, hipStream_t st);
 int launch_match_masks(float* corr, int B, int NA, int NB, const uint8_t* ig, const int64_t* s_mask, float* incons,
                        int* q2k, float* pv, int* pi, hipStream_t st);
 int launch_wa_attn(const float* tpg, int N, int h, int w, int co, const float* bt, const float* bp, const float* bg,
@@ -1389,6 +1390,18 @@ int cwt_sce_descriptor(cwt_ctx* ctx, const float* x, int B, int h, int w, int C,
   Prof p(ctx, st, "sce_descriptor", 2.0 * B * h * w * (double)k * k * C, 4.0 * B * h * w * ((double)C + ldg));
   int rc;
   if ((rc = launch_sce_descriptor(x, B, h, w, C, k, ldg, g, st))) return rc;
+  p.end();
+  return 0;
+}
+
+int cwt_channel_sum(cwt_ctx* ctx, const float* x, int B, int L, int64_t P, float* y, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && y && B >= 1 && L >= 1 && P >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  Prof p(ctx, st, "channel_sum", (double)B * L * P, 4.0 * B * P * (L + 1));
+  int rc;
+  if ((rc = launch_channel_sum(x, B, L, (long)P, y, st))) return rc;
   p.end();
   return 0;
 }

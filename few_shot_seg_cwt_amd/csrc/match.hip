@@ -370,6 +370,19 @@ __global__ __launch_bounds__(256) void sce_descriptor_kernel(const float* __rest
   for (int o = threadIdx.x; o < ldg; o += 256) gp[o] = o < k2 ? win[o] * inv : 0.f;
 }
 
+// ---- MMN agg 'sum' (mmn.py:62-63): y[b][p] = sum over l of x[b][l][p], l in order ----
+__global__ void channel_sum_kernel(const float* __restrict__ x, int B, int L, long P, float* __restrict__ y) {
+  const long total = (long)B * P;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(e / P);
+    const long p = e - (long)b * P;
+    const float* xb = x + (long)b * L * P + p;
+    float s = xb[0];
+    for (int l = 1; l < L; ++l) s += xb[(long)l * P];
+    y[e] = s;
+  }
+}
+
 // ---- MatchNet's support masks (match.py:117-126, run_cyc match.py:165-182) ----
 // ig_mask [B][NB] (uint8, nullable): corr2d[b][a][j] = 1e-4 where ig_mask[b][j] (every query a).
 // The cycle mask: k2q[j] = argmax over a of corr2d[a][j], q2k[a] = argmax over j of corr2d[a][j]
@@ -700,6 +713,14 @@ int launch_sce_descriptor(const float* x, int B, int h, int w, int C, int k, int
   const size_t lds = (size_t)(C + k * k) * 4;
   if (lds > 64 * 1024) return fail(CWT_EARG, "sce: C + k*k floats must fit 64 KB of LDS");
   hipLaunchKernelGGL(sce_descriptor_kernel, dim3((unsigned)((long)B * h * w)), dim3(256), lds, st, x, h, w, C, k, ldg, g);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_channel_sum(const float* x, int B, int L, long P, float* y, hipStream_t st) {
+  const long total = (long)B * P;
+  hipLaunchKernelGGL(channel_sum_kernel, dim3((unsigned)std::min<long>(65536, cdiv(total, 256))), dim3(256), 0, st, x, B,
+                     L, P, y);
   CWT_LAUNCH_CHECK();
   return 0;
 }

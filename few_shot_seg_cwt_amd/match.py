@@ -16,8 +16,8 @@ MatchNet script -- CenterPivotConv4d ('red'), kernel sizes [3, 3, 3], channels [
 in_channel 1 or 2, symmetric or not -- and the MMN head of the mmn configs (rmid 'l34', all_lr
 'l', agg 'cat', wa True, red_dim False), forward only (inference), with MatchNet.forward's ig_mask and (round 3) its
 cycle-consistency mask (cyc, eval mode), and NeighConsensus over full Conv4d layers ('cv4',
-fp32 VALU), and the spatial context encoder (sce, spatial_context.py).  Not built: agg 'sum',
-red_dim, forward_mmn (its MSBlock) and the MMN trainers' backward.
+fp32 VALU), the spatial context encoder (sce, spatial_context.py), and MMN's agg 'sum' and red_dim.
+Not built: forward_mmn (its MSBlock) and the MMN trainers' backward.
 
 Parity is unpinned: the reference cannot be run here and holds no fixtures for
 this head; tests/test_gpu_match.py checks it against oracle/match_oracle.py, a float64
@@ -349,10 +349,8 @@ class MMN(torch.nn.Module):
 
     def __init__(self, args, agg: str = "cat", wa: bool = False, red_dim=False, device=None):
         super().__init__()
-        if agg != "cat":
-            raise NotImplementedError("MMN: agg 'cat' only")
-        if red_dim:
-            raise NotImplementedError("MMN: red_dim is not built")
+        if agg not in ("cat", "sum"):
+            raise ValueError(f"MMN: agg must be 'cat' or 'sum', got {agg!r}")
         self.args, self.agg, self.wa, self.red_dim = args, agg, wa, red_dim
         rmid = str(_get(args, "rmid"))
         self.bid_lst = [int(c) for c in rmid[1:]]
@@ -363,13 +361,27 @@ class MMN(torch.nn.Module):
         if any(str(i) in all_lr for i in self.bid_lst):
             raise NotImplementedError("MMN: every-bottleneck features (all_lr naming a layer) are not built")
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        if wa:
+        if wa or red_dim:   # mmn.py:26-33: the wa_ modules exist whenever red_dim does
             for bid in self.bid_lst:
-                setattr(self, "wa_" + str(bid), WeightAverage(self.feature_channels[bid - 1], args, device=dev))
-        match_ch = len(self.bid_lst)
+                c_in = self.feature_channels[bid - 1]
+                if isinstance(red_dim, int) and not isinstance(red_dim, bool) and red_dim:
+                    setattr(self, "rd_" + str(bid),
+                            torch.nn.Sequential(torch.nn.Conv2d(c_in, red_dim, 1, bias=False, device=dev),
+                                                torch.nn.ReLU(inplace=True)))
+                    c_in = red_dim
+                setattr(self, "wa_" + str(bid), WeightAverage(c_in, args, device=dev))
+        match_ch = 1 if agg == "sum" else len(self.bid_lst)
         self.att_wt = float(_get(args, "att_wt", 0.2))
         self.corr_net = MatchNet(temp=float(_get(args, "temp", 20.0)), cv_type=str(_get(args, "conv4d", "red")),
                                  sce=False, cyc=False, sym_mode=True, in_channel=match_ch, device=dev)
+
+    def _reduce(self, idx: int, x: torch.Tensor) -> torch.Tensor:
+        from .detr import linear
+        conv = getattr(self, "rd_" + str(idx))[0]
+        xt = as_tokens(x)
+        N, C, h, w = xt.shape
+        y = linear(xt.permute(0, 2, 3, 1).reshape(N * h * w, C), conv.weight, None, relu=True)
+        return y.reshape(N, h, w, -1).permute(0, 3, 1, 2)
 
     def forward(self, fq_lst, fs_lst, f_q, f_s, ret_attn: bool = False):
         """mmn.py:42-71: fq_lst / fs_lst {layer: [feature]} (extract_features with rmid),
@@ -380,6 +392,8 @@ class MMN(torch.nn.Module):
         corr4d = torch.empty((B, L, P, P), device=f_s.device, dtype=torch.float32)
         for li, idx in enumerate(self.bid_lst[::-1]):
             fq_fea, fs_fea = fq_lst[idx][0], fs_lst[idx][0]
+            if self.red_dim:   # rd_<layer>: 1x1 conv (no bias) + ReLU on the device GEMM
+                fq_fea, fs_fea = self._reduce(idx, fq_fea), self._reduce(idx, fs_fea)
             if self.wa:
                 m = getattr(self, "wa_" + str(idx))
                 fq_fea, fs_fea = m(fq_fea), m(fs_fea)   # the query once: its B expanded copies are equal
@@ -388,6 +402,11 @@ class MMN(torch.nn.Module):
                 C = qt.shape[1]
                 _lib.check(_lib.lib().cwt_corr(_lib.ctx(f_s.device.index), _lib.ptr(qt), _lib.ptr(kt), 1, P, P, C,
                                                _lib.ptr(corr4d[b, li]), _lib.stream_ptr(f_s.device)), "cwt_corr")
+        if self.agg == "sum":   # mmn.py:62-63
+            summed = torch.empty((B, 1, P, P), device=f_s.device, dtype=torch.float32)
+            _lib.check(_lib.lib().cwt_channel_sum(_lib.ctx(f_s.device.index), _lib.ptr(corr4d), B, L, P * P,
+                                                  _lib.ptr(summed), _lib.stream_ptr(f_s.device)), "cwt_channel_sum")
+            corr4d = summed
         attn, att = self.corr_net._run(corr4d, h, w, f_s)   # att [B, Cv, h, w] (channels_last)
         att_t = as_tokens(att)
         fqt = as_tokens(f_q)

@@ -369,6 +369,10 @@ int cwt_match_corr_forward_cv4(cwt_ctx* ctx, const float* corr, int B, int L, in
 int cwt_sce_descriptor(cwt_ctx* ctx, const float* x, int B, int h, int w, int C, int k, int ldg, float* g,
                        void* stream);
 
+/* MMN's agg 'sum' (src/model/mmn.py:62-63, torch.sum(corr4d, dim=1, keepdim=True)): x device
+ * [B][L][P], y device [B][P] = the sum over l, in order of l. */
+int cwt_channel_sum(cwt_ctx* ctx, const float* x, int B, int L, int64_t P, float* y, void* stream);
+
 /* MatchNet.forward's support masks on corr2d device [B][NA][NB], in place (src/model/match.py:
  * 117-126 and run_cyc, match.py:165-182).  ig_mask device [B][NB] uint8 (NULL: none) sets every
  * query row's entry of a masked support position to 1e-4.  With s_mask device [B][NB] int64 (the

@@ -184,19 +184,26 @@ def feat_list(x: torch.Tensor, sd, layers: int = 50):
     return out
 
 
-def mmn_forward(fq_lst, fs_lst, f_q, f_s, bid_lst, wa_params, layers, temp: float, att_wt: float):
-    """mmn.py:42-71 with agg 'cat', red_dim False: fq_lst / fs_lst {layer: feature}, wa_params
-    {layer: weight_average params} or None -> (fq, att_fq)."""
+def mmn_forward(fq_lst, fs_lst, f_q, f_s, bid_lst, wa_params, layers, temp: float, att_wt: float,
+                agg: str = "cat", rd_weights=None):
+    """mmn.py:42-71: fq_lst / fs_lst {layer: feature}, wa_params {layer: weight_average params}
+    or None, rd_weights {layer: rd_<layer>.0.weight} (red_dim) or None, agg 'cat' or 'sum' ->
+    (fq, att_fq)."""
     B, ch, h, w = f_s.shape
     corrs = []
     for idx in bid_lst[::-1]:
         fq, fs = fq_lst[idx].expand(B, -1, -1, -1), fs_lst[idx]
+        if rd_weights is not None:
+            fq, fs = torch.relu(F.conv2d(fq, rd_weights[idx])), torch.relu(F.conv2d(fs, rd_weights[idx]))
         if wa_params is not None:
             fq, fs = weight_average(fq, wa_params[idx]), weight_average(fs, wa_params[idx])
         bq = F.normalize(fq.reshape(B, fq.shape[1], h * w), dim=1)
         bs = F.normalize(fs.reshape(B, fs.shape[1], h * w), dim=1)
         corrs.append(torch.bmm(bq.transpose(1, 2), bs).reshape(B, 1, h, w, h, w))
-    _, att = corr_forward(torch.cat(corrs, 1), f_s, layers, temp, True)
+    corr4d = torch.cat(corrs, 1)
+    if agg == "sum":
+        corr4d = torch.sum(corr4d, dim=1, keepdim=True)
+    _, att = corr_forward(corr4d, f_s, layers, temp, True)
     att = att.mean(dim=0, keepdim=True)
     return f_q * (1 - att_wt) + att * att_wt, att
 

@@ -275,3 +275,33 @@ def test_matchnet_forward_sce(dev):
     # chain's fp32 rounding at ~1e-5 and the temp-20 softmax scales it by up to 20 in weighted_v
     # (measured 6.8e-6 / 2.8e-5); each stage alone is within 1e-5 (tests above)
     assert e_c < TOL and e_v < 5 * TOL
+
+
+@pytest.mark.parametrize("agg,wa,red_dim", [("sum", True, False), ("cat", True, 512), ("sum", False, 256)])
+def test_mmn_forward_agg_red_dim(dev, agg, wa, red_dim):
+    """MMN with agg 'sum' (mmn.py:62-63) and red_dim (the rd_<layer> 1x1 conv + ReLU, mmn.py:
+    28-31,49-51; the wa_ modules exist whenever red_dim does) against the oracle chain."""
+    from few_shot_seg_cwt_amd.match import MMN, init_match_params
+    from oracle import match_oracle as M
+    args = dict(rmid="l34", layers=50, all_lr="l", temp=20.0, att_wt=0.2, conv4d="red")
+    net = MMN(args, agg=agg, wa=wa, red_dim=red_dim, device=dev)
+    init_match_params(net, seed=6)
+    sd = {k: t.cpu() for k, t in net.state_dict().items()}
+    if red_dim:
+        assert tuple(sd["rd_3.0.weight"].shape) == (red_dim, 1024, 1, 1) and "wa_4.conv_theta.weight" in sd
+    g = torch.Generator().manual_seed(25)
+    h = 8
+    fq_lst = {3: [torch.rand(1, 1024, h, h, generator=g).to(dev)], 4: [torch.rand(1, 2048, h, h, generator=g).to(dev)]}
+    fs_lst = {3: [torch.rand(2, 1024, h, h, generator=g).to(dev)], 4: [torch.rand(2, 2048, h, h, generator=g).to(dev)]}
+    f_q = torch.rand(1, 512, h, h, generator=g).to(dev)
+    f_s = torch.rand(2, 512, h, h, generator=g).to(dev)
+    fq, att_fq = net(fq_lst, fs_lst, f_q, f_s)
+    wap = {b: M.wa_params_from_state(sd, f"wa_{b}.") for b in (3, 4)} if wa else None
+    rdw = {b: sd[f"rd_{b}.0.weight"].double() for b in (3, 4)} if red_dim else None
+    layers = M.layers_from_state(sd, prefix="corr_net.NeighConsensus.conv.")
+    d = lambda t: t.double().cpu()  # noqa: E731
+    fqo, atto = M.mmn_forward({k: d(v[0]) for k, v in fq_lst.items()}, {k: d(v[0]) for k, v in fs_lst.items()},
+                              d(f_q), d(f_s), [3, 4], wap, layers, 20.0, 0.2, agg=agg, rd_weights=rdw)
+    errs = dict(fq=rel(fq, fqo), att_fq=rel(att_fq, atto))
+    print(f"MMN agg={agg} wa={wa} red_dim={red_dim}: {errs}")
+    assert max(errs.values()) < TOL, errs
