@@ -196,6 +196,33 @@ def conv_roofline(fine, peak_tflops):
                               "summed over the stack's conv launches (one episode, per-launch events)"}
 
 
+class adapt_leg:
+    """Launch the inner loops of a side leg (timing studies, the exact-fp32 leg) as their own
+    instantiation of the persistent kernel (CWT_ADAPT_DBG: 128 = the SIDE instantiation, code
+    identical to the product one; 64 = the latency-floor study), so rocprofv3's per-kernel
+    statistics of the timed kernel hold only the timed region's launches (and warm-up)."""
+
+    def __init__(self, flags: int):
+        self.flags = flags
+
+    def __enter__(self):
+        self.old = os.environ.get("CWT_ADAPT_DBG")
+        if self.flags:
+            os.environ["CWT_ADAPT_DBG"] = str(self.flags)
+        return self
+
+    def __exit__(self, *exc):
+        if self.flags:
+            if self.old is None:
+                os.environ.pop("CWT_ADAPT_DBG", None)
+            else:
+                os.environ["CWT_ADAPT_DBG"] = self.old
+        return False
+
+
+ADAPT_SIDE, ADAPT_FLOOR = 128, 64
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -358,8 +385,12 @@ def main():
     ap.add_argument("--batch", type=int, default=10, help="--pretrain: images per iteration (pascal_pretrain.yaml: 10)")
     ap.add_argument("--num-classes", type=int, default=16, help="--pretrain: num_classes_tr (16 PASCAL, 61 COCO)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--exact-steps", type=int, default=10,
-                    help="episodes of the exact-fp32 conv leg (cwt_ctx_set_conv_arith F32, sequential); 0 = skip")
+    ap.add_argument("--exact-steps", type=int, default=20,
+                    help="episodes of the exact-fp32 conv leg (cwt_ctx_set_conv_arith F32 on every extractor "
+                         "context; through the same episode pipeline as the headline, and sequential); 0 = skip")
+    ap.add_argument("--pair-steps", type=int, default=20,
+                    help="steps of the batched-pipeline leg (two episodes share one extractor pass, "
+                         "EpisodePipeline.submit_batch; reported beside the headline); 0 = skip")
     ap.add_argument("--profile-json", default=None, help="write per-launch records here (rank 0)")
     args = ap.parse_args()
 
@@ -486,6 +517,54 @@ def main():
                "note": "the same K steps one episode after the other on one stream (--pipeline 0)"}
         del seq_out
         pipe = pipe_saved
+    # ---- batched pipeline: two episodes per extractor pass (M = 4*h*w
+    # rows per conv at 1-shot), their inner loops in one persistent launch, tails batched; the
+    # same pipeline and streams.  A throughput form reported beside the headline, not in it ----
+    pairs = None
+    if pipe is not None and not args.train and E == 1 and args.pair_steps > 0:
+        EP = 2
+        pool2 = []
+        for i in range(2):
+            eps = [syn.make_episode(seed, rank * 1000 + 500 + i * EP + e, S, shot, classes) for e in range(EP)]
+            imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0] for ep in eps] + [ep["qry_img"] for ep in eps]))
+            sl = torch.from_numpy(np.stack([ep["s_label"][0] for ep in eps]))
+            ql = torch.from_numpy(np.concatenate([ep["q_label"] for ep in eps]))
+            pool2.append((imgs.to(dev), sl.to(dev), ql.to(dev)))
+        P = args.pair_steps
+        W02 = ((torch.rand((P + 2, EP, 2, 512), generator=g) * 2 - 1) * bound).to(dev)
+        with adapt_leg(ADAPT_SIDE):
+            for s_ in range(2):
+                im, sl_, ql_ = pool2[s_ % 2]
+                pipe.submit_batch(im, sl_, ql_, W02[s_].clone(), last=s_ == 1)
+            pipe.wait()
+            torch.cuda.synchronize()
+            _lib.profile_enable(1)
+            cdist.barrier()
+            torch.cuda.synchronize()
+            tp0 = time.perf_counter()
+            pouts = [pipe.submit_batch(pool2[s_ % 2][0], pool2[s_ % 2][1], pool2[s_ % 2][2], W02[2 + s_],
+                                       last=s_ == P - 1)["iut"] for s_ in range(P)]
+            pipe.wait()
+            torch.cuda.synchronize()
+            cdist.barrier()
+            dtp = cdist.all_reduce_max_scalar(time.perf_counter() - tp0)
+            precs = _lib.profile_records()
+            _lib.profile_enable(2)
+            model.extract_features(pool2[0][0])
+            torch.cuda.synchronize()
+            pfine = _lib.profile_records()
+            _lib.profile_enable(0)
+        pex = [r for r in precs if r[0].startswith("extract_features")]
+        pairs = {"value": round(world * P * EP / dtp, 3), "unit": "episodes/s", "steps": P, "episodes_per_step": EP,
+                 "ms_per_episode": round(dtp / (P * EP) * 1e3, 3),
+                 "mode": "EpisodePipeline.submit_batch: two episodes' support + query images in ONE extractor pass "
+                         f"({EP * (shot + 1)} images, conv GEMM rows M = {EP * (shot + 1)}*h*w), their inner loops "
+                         "in one persistent launch, the fused tails batched; exact per episode (eval-mode BN)",
+                 "extract_ms_per_step": round(sum(r[3] for r in pex) / P, 3),
+                 "conv_stack": {"note": f"one {EP * (shot + 1)}-image extractor pass alone, per-launch records",
+                                **conv_roofline(pfine, PEAK_BF16_MFMA_TFLOPS if args.conv_dtype == "bf16"
+                                                else round(PEAK_BF16_MFMA_TFLOPS / 3, 1))}}
+        del pouts
     iu = torch.cat(iuts).sum(0)
 
     def total(prefix):
@@ -493,8 +572,8 @@ def main():
         return len(sel), sum(r[1] for r in sel), sum(r[3] for r in sel)
 
     n_ex, ex_fl, ex_ms = total("extract_features")
-    n_ad, _, ad_ms = total("inner_adapt")
-    ad_bytes = sum(r[2] for r in recs if r[0].startswith("inner_adapt"))
+    n_ad, _, ad_ms = total("inner_adapt x")      # the phase bracket (label prep + setup + the loop)
+    ad_bytes = sum(r[2] for r in recs if r[0].startswith("inner_adapt x"))
     n_at, _, at_ms = total("attention")
     dom = [r for r in recs if r[0].startswith("conv_igemm")]     # the bottleneck conv (level 1 records only it)
     dom_name = dom[0][0].split(" ")[0] if dom else "n/a"
@@ -515,17 +594,20 @@ def main():
     # the instantiation the timed region ran (the record name carries it: "inner_adapt x200 [adapt_persist_kernel<2]");
     # with the pipeline's drain the burst's last loop runs the whole-chip geometry: the roofline
     # figures are over the launches of the named (majority) instantiation
-    ad_names = [r[0] for r in recs if r[0].startswith("inner_adapt") and "[" in r[0]]
+    # roofline: the persistent kernel's own launches ("inner_adapt_kernel [...]" records: the
+    # kernel alone, as rocprofv3 times it), else the phase bracket
+    kpref = "inner_adapt_kernel [" if any(r[0].startswith("inner_adapt_kernel [") for r in recs) else "inner_adapt x"
+    ad_names = [r[0] for r in recs if r[0].startswith(kpref) and "[" in r[0]]
     ad_kernel = (max(set(ad_names), key=ad_names.count).split("[", 1)[1].rstrip("]") if ad_names
                  else "adapt_persist_kernel<")
-    ad_sel = [r for r in recs if r[0].startswith("inner_adapt") and (not ad_names or ad_kernel + "]" in r[0])]
+    ad_sel = [r for r in recs if r[0].startswith(kpref) and (not ad_names or ad_kernel + "]" in r[0])]
     ad_launches = max(len(ad_sel), 1)
     ad_bytes_launch = sum(r[2] for r in ad_sel) / ad_launches
     ad_ms_launch = sum(r[3] for r in ad_sel) / ad_launches
     ad_achieved = ad_bytes_launch / (ad_ms_launch * 1e-3) / 1e9 if ad_ms_launch else 0.0
     seq_ad = None
     if seq_recs:
-        s_sel = [r for r in seq_recs if r[0].startswith("inner_adapt")]
+        s_sel = [r for r in seq_recs if r[0].startswith(kpref)]
         if s_sel:
             s_ms = sum(r[3] for r in s_sel) / len(s_sel)
             s_by = sum(r[2] for r in s_sel) / len(s_sel)
@@ -542,10 +624,11 @@ def main():
 
     # per-launch table from one extra (untimed) episode at profile level 2
     _lib.profile_enable(2)
-    step(0, W0[0].clone())
-    if pipe is not None:
-        pipe.wait()
-    torch.cuda.synchronize()
+    with adapt_leg(ADAPT_SIDE):
+        step(0, W0[0].clone())
+        if pipe is not None:
+            pipe.wait()
+        torch.cuda.synchronize()
     fine = _lib.profile_records()
     _lib.profile_enable(0)
     _lib.check_status()   # every launch so far has completed: surface an inner-loop barrier timeout
@@ -561,43 +644,35 @@ def main():
         from few_shot_seg_cwt_amd.episode import inner_adapt
 
         def time_loop(ctx_sel, dbg, reps=5):
-            old = os.environ.get("CWT_ADAPT_DBG")
-            if dbg:
-                os.environ["CWT_ADAPT_DBG"] = str(dbg)
-            try:
-                st = torch.cuda.current_stream()
-                evs = []
+            """median of the persistent kernel's own bracket (inner_adapt_kernel records, as the
+            timed region's roofline uses) over reps launches after one warm-up"""
+            with adapt_leg(dbg):
+                _lib.profile_enable(1)
                 for r in range(reps + 1):
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(st)
                     if ctx_sel is None:
                         inner_adapt(f_s0, sl0[0], W0[0, 0].clone(), cfg["cls_lr"], cfg["adapt_iter"])
                     else:
                         with _lib.using_ctx(ctx_sel):
                             inner_adapt(f_s0, sl0[0], W0[0, 0].clone(), cfg["cls_lr"], cfg["adapt_iter"])
-                    e1.record(st)
-                    evs.append((e0, e1))
                 torch.cuda.synchronize()
-            finally:
-                if dbg:
-                    if old is None:
-                        os.environ.pop("CWT_ADAPT_DBG", None)
-                    else:
-                        os.environ["CWT_ADAPT_DBG"] = old
-            return float(np.median([a.elapsed_time(b) for a, b in evs[1:]]))
+                ks = [r[3] for r in _lib.profile_records() if r[0].startswith(kpref)]
+                _lib.profile_enable(0)
+            return float(np.median(ks[1:]))
 
         geos = [("sequential_leg (default context)", None)]
         if pipe is not None:
             geos.insert(0, ("timed region's geometry (the pipeline's adapt context)", pipe.c_adapt))
-        latency_floor = {"basis": "the same persistent kernel at the same G, alone on the GPU, with every unit's "
-                                  "arithmetic and atomics skipped (CWT_ADAPT_DBG & 64): the per-step exchange "
+        latency_floor = {"basis": "the same persistent kernel at the same G, alone on the GPU (its own launch "
+                                  "bracket, as the timed roofline's), with every unit's "
+                                  "arithmetic and atomics skipped (CWT_ADAPT_DBG & 64, the FLOOR instantiation "
+                                  "adapt_persist_kernel<NRES, 2>; the 'alone' runs beside it are the SIDE "
+                                  "instantiation <NRES, 3>, code identical to the timed one): the per-step exchange "
                                   "(slot zeroing, arrival, poll, replica reads, W update) x adapt_iter -- the "
-                                  "loop's dependency-chain floor in this design; bracket includes the label prep "
-                                  "and setup kernels as the timed one does"}
+                                  "loop's dependency-chain floor in this design"}
         bytes_floor_ms = ad_bytes_launch / (PEAK_HBM_GBPS * 1e9) * 1e3
         for label, c in geos:
-            full = time_loop(c, 0)
-            floor = time_loop(c, 64)
+            full = time_loop(c, ADAPT_SIDE)
+            floor = time_loop(c, ADAPT_FLOOR)
             latency_floor[label.split(" ")[0]] = {"what": label, "floor_ms": round(floor, 4),
                                                   "alone_ms": round(full, 4),
                                                   "frac_alone_vs_floor": round(max(floor, bytes_floor_ms) / full, 4)}
@@ -614,41 +689,71 @@ def main():
     # priced against the 157.3 TF fp32 matrix peak ----
     exact_fp32 = None
     if not args.train and E == 1 and conv_x3 and args.exact_steps > 0:
-        c0 = _lib.ctx(dev.index)
-        _lib.check(_lib.lib().cwt_ctx_set_conv_arith(c0, 1), "cwt_ctx_set_conv_arith")
+        # every context that runs extractor passes: the default one, and the pipeline's other
+        # extractor streams' contexts
+        ext_ctxs = [_lib.ctx(dev.index)] + ([c for c in pipe.c_ext if c is not None] if pipe is not None else [])
+
+        def set_arith(v):
+            for c in ext_ctxs:
+                _lib.check(_lib.lib().cwt_ctx_set_conv_arith(c, v), "cwt_ctx_set_conv_arith")
+
+        nx = args.exact_steps
+        set_arith(1)
         try:
-            for s_ in range(2):
-                im, sl_, ql_ = pool[s_ % len(pool)]
-                engine.run(im, sl_[0], ql_, W0[s_, 0].clone())
-            torch.cuda.synchronize()
-            _lib.profile_enable(1)
-            cdist.barrier()
-            torch.cuda.synchronize()
-            tf0 = time.perf_counter()
-            for s_ in range(args.exact_steps):
-                im, sl_, ql_ = pool[s_ % len(pool)]
-                engine.run(im, sl_[0], ql_, W0[args.warmup + s_ % args.steps, 0].clone())
-            torch.cuda.synchronize()
-            cdist.barrier()
-            dtf = cdist.all_reduce_max_scalar(time.perf_counter() - tf0)
-            frecs = _lib.profile_records()
-            _lib.profile_enable(2)
-            engine.run(pool[0][0], pool[0][1][0], pool[0][2], W0[0, 0].clone())
-            torch.cuda.synchronize()
-            ffine = _lib.profile_records()
-            _lib.profile_enable(0)
+            with adapt_leg(ADAPT_SIDE):
+                # warm-up: the f32 plans' workspaces, both paths
+                for s_ in range(3):
+                    im, sl_, ql_ = pool[s_ % len(pool)]
+                    if pipe is not None:
+                        pipe.submit(im, sl_[0], ql_, W0[s_, 0].clone(), last=s_ == 2)
+                    else:
+                        engine.run(im, sl_[0], ql_, W0[s_, 0].clone())
+                if pipe is not None:
+                    pipe.wait()
+                torch.cuda.synchronize()
+                legs = {}
+                for mode in (("pipelined", "sequential") if pipe is not None else ("sequential",)):
+                    _lib.profile_enable(1)
+                    cdist.barrier()
+                    torch.cuda.synchronize()
+                    tf0 = time.perf_counter()
+                    outs = []
+                    for s_ in range(nx):
+                        im, sl_, ql_ = pool[s_ % len(pool)]
+                        w_ = W0[args.warmup + s_ % args.steps, 0].clone()
+                        if mode == "pipelined":
+                            outs.append(pipe.submit(im, sl_[0], ql_, w_, last=s_ == nx - 1)["iut"])
+                        else:
+                            outs.append(engine.run(im, sl_[0], ql_, w_)["iut"])
+                    if mode == "pipelined":
+                        pipe.wait()
+                    torch.cuda.synchronize()
+                    cdist.barrier()
+                    dtf = cdist.all_reduce_max_scalar(time.perf_counter() - tf0)
+                    legs[mode] = (dtf, _lib.profile_records())
+                    del outs
+                _lib.profile_enable(2)
+                engine.run(pool[0][0], pool[0][1][0], pool[0][2], W0[0, 0].clone())
+                torch.cuda.synchronize()
+                ffine = _lib.profile_records()
+                _lib.profile_enable(0)
         finally:
-            _lib.check(_lib.lib().cwt_ctx_set_conv_arith(c0, 0), "cwt_ctx_set_conv_arith")
+            set_arith(0)
+        head = "pipelined" if "pipelined" in legs else "sequential"
+        dtf, frecs = legs[head]
         fex = [r for r in frecs if r[0].startswith("extract_features")]
         fdom = [r for r in frecs if r[0].startswith("conv_igemm")]
         fex_fl, fex_ms = sum(r[1] for r in fex), sum(r[3] for r in fex)
         exact_fp32 = {
-            "value": round(world * args.exact_steps / dtf, 3), "unit": "episodes/s",
-            "ms_per_step": round(dtf / args.exact_steps * 1e3, 3), "steps": args.exact_steps,
-            "mode": "sequential (one episode after the other), conv stack on v_mfma_f32 (exact fp32, the "
-                    "reference's numerics without the bf16x3 split)",
+            "value": round(world * nx / dtf, 3), "unit": "episodes/s",
+            "ms_per_step": round(dtf / nx * 1e3, 3), "steps": nx,
+            "mode": (f"{head}: the same episodes through the same "
+                     + (f"episode pipeline ({args.pipeline} extractor streams) " if head == "pipelined" else "loop ")
+                     + "as the headline, conv stack on v_mfma_f32 (exact fp32, the reference's numerics "
+                       "without the bf16x3 split)"),
             "conv_stack": {"tflops": round(fex_fl / (fex_ms * 1e-3) / 1e12, 2),
-                           "ms_per_step": round(fex_ms / args.exact_steps, 3),
+                           "extract_ms_per_step": round(fex_ms / nx, 3),
+                           "note": "roofline_frac from one extra episode's per-launch records (level 2, alone)",
                            **conv_roofline(ffine, PEAK_FP32_MFMA_TFLOPS)},
             "conv_roofline": None if not fdom else {
                 "kernel": fdom[0][0].split(" ")[0] + " (bottleneck conv)",
@@ -656,6 +761,10 @@ def main():
                 "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(sum(r[1] for r in fdom) / (sum(r[3] for r in fdom) * 1e-3) / 1e12
                               / PEAK_FP32_MFMA_TFLOPS, 4)}}
+        if "sequential" in legs and head != "sequential":
+            dts_, _ = legs["sequential"]
+            exact_fp32["sequential"] = {"value": round(world * nx / dts_, 3),
+                                        "ms_per_step": round(dts_ / nx * 1e3, 3)}
         _lib.check_status()
 
     out = {
@@ -727,6 +836,7 @@ def main():
                           "note": "executed in the declared re-associated form (DESIGN.md §3, ~59 MFLOP of token work)"}},
         "iou_fg_timed": None if args.train else round(float((iu[0, 1] / iu[1, 1].clamp_min(1)).item()), 4),
         "sequential": seq,
+        "batched_pipeline": pairs,
         "exact_fp32": exact_fp32,
     }
     if rank == 0 and args.profile_json:

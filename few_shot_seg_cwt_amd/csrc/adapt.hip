@@ -654,9 +654,6 @@ struct PersistArgs {
   int uc;      // lo-res columns owned per unit (15 or 31)
   long spin_limit;   // polls per barrier before the grid gives up (PA_SPIN_LIMIT by default)
   unsigned* status;  // the context's mapped host status word (cwt_ctx_status), or null
-  int floor_only;    // timing study (CWT_ADAPT_DBG & 64): skip every unit's arithmetic and atomics --
-                     // what is left is the per-step exchange (slot zeroing, arrival, poll, replica
-                     // reads, W update): the loop's latency floor at this G (bench.py latency_floor)
 };
 
 struct PaUnit {
@@ -844,8 +841,16 @@ struct PaScrAlias {
 // every step, each wave's slice by LDS-DMA into its private 8 KB while the previous unit is
 // computed; 0: units streamed from L2 into registers (opt-in, slower).  Fewer workgroups make each step's barrier cheaper and leave CUs to the
 // next episode's extractor pass (EpisodePipeline).
-template <int NRES, bool STAMPS = false>
+// MODE only separates instantiations so that rocprofv3's per-kernel statistics attribute each
+// launch to the leg that made it: 0 the product kernel (every timed launch); 1 STAMPS (above);
+// 2 FLOOR, the latency-floor study (CWT_ADAPT_DBG & 64: every unit's arithmetic and atomics
+// skipped, what is left is the per-step exchange); 3 SIDE, code identical to 0, launched for
+// bench.py's side legs (CWT_ADAPT_DBG & 128: the loop timed alone, the exact-fp32 leg) so that
+// they do not mix into the timed kernel's rocprof average.
+template <int NRES, int MODE = 0>
 __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsigned long long* stamps = nullptr) {
+  constexpr bool STAMPS = MODE == 1;
+  constexpr bool FLOOR = MODE == 2;
   constexpr int C = 512;
   constexpr int EWK = (NRES >= 2) ? 2 : NRES == 1 ? 1 : PA_EW;  // episodes a workgroup's units may span
   constexpr bool LOCK = NRES == 2 || NRES == 4;  // units in lockstep, the second one's f in fl2
@@ -1283,7 +1288,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
                                  dsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     };
-    if (a.floor_only) {
+    if constexpr (FLOOR) {
       // timing study: no unit work (NRES 3 still drains its in-flight DMA)
       if (NRES == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if constexpr (NRES == 4) {
@@ -1489,10 +1494,6 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
   PersistArgs a;
   a.status = status;
   a.spin_limit = spin_limit > 0 ? spin_limit : PA_SPIN_LIMIT;
-  {
-    const char* fd = getenv("CWT_ADAPT_DBG");
-    a.floor_only = (fd && (atoi(fd) & 64)) ? 1 : 0;
-  }
   a.f = f;
   a.lbl = lbl_ws;
   a.sc = sc;
@@ -1515,7 +1516,11 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
   a.nrep = pr ? atoi(pr) : PA_R_DEFAULT;
   if (a.nrep != 2 && a.nrep != 4 && a.nrep != 8 && a.nrep != 16) a.nrep = PA_R_DEFAULT;
   const char* dbg = getenv("CWT_ADAPT_DBG");
-  if (dbg && (atoi(dbg) & 32)) {  // timing study (tools/persist_stamps.py)
+  const int dbgv = dbg ? atoi(dbg) : 0;
+  // MODE: 1 stamps (timing study), 2 latency floor (& 64), 3 side leg (& 128), 0 product
+  const int mode = (dbgv & 32) ? 1 : (dbgv & 64) ? 2 : (dbgv & 128) ? 3 : 0;
+  unsigned long long* stp = nullptr;
+  if (mode == 1) {  // timing study (tools/persist_stamps.py)
     const long n_st = ((long)iters + 1) * G * 10;
     if (n_st > g_adapt_stamps_n) {
       CWT_HIP(hipDeviceSynchronize());
@@ -1523,27 +1528,26 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
       CWT_HIP(hipMalloc(&g_adapt_stamps, n_st * sizeof(unsigned long long)));
       g_adapt_stamps_n = n_st;
     }
-    if (nres == 4)
-      hipLaunchKernelGGL((adapt_persist_kernel<4, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
-    else if (nres == 3)
-      hipLaunchKernelGGL((adapt_persist_kernel<3, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
-    else if (nres == 1)
-      hipLaunchKernelGGL((adapt_persist_kernel<1, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
-    else if (nres == 2)
-      hipLaunchKernelGGL((adapt_persist_kernel<2, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
-    else
-      hipLaunchKernelGGL((adapt_persist_kernel<0, true>), dim3(G), dim3(PA_T), 0, st, a, g_adapt_stamps);
-  } else if (nres == 4) {
-    hipLaunchKernelGGL((adapt_persist_kernel<4, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
-  } else if (nres == 3) {
-    hipLaunchKernelGGL((adapt_persist_kernel<3, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
-  } else if (nres == 1) {
-    hipLaunchKernelGGL((adapt_persist_kernel<1, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
-  } else if (nres == 2) {
-    hipLaunchKernelGGL((adapt_persist_kernel<2, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
-  } else {
-    hipLaunchKernelGGL((adapt_persist_kernel<0, false>), dim3(G), dim3(PA_T), 0, st, a, (unsigned long long*)nullptr);
+    stp = g_adapt_stamps;
   }
+#define CWT_PA_LAUNCH(NR, MD) \
+  hipLaunchKernelGGL((adapt_persist_kernel<NR, MD>), dim3(G), dim3(PA_T), 0, st, a, stp)
+#define CWT_PA_MODES(NR)                     \
+  switch (mode) {                            \
+    case 1: CWT_PA_LAUNCH(NR, 1); break;     \
+    case 2: CWT_PA_LAUNCH(NR, 2); break;     \
+    case 3: CWT_PA_LAUNCH(NR, 3); break;     \
+    default: CWT_PA_LAUNCH(NR, 0); break;    \
+  }
+  switch (nres) {
+    case 4: CWT_PA_MODES(4); break;
+    case 3: CWT_PA_MODES(3); break;
+    case 2: CWT_PA_MODES(2); break;
+    case 1: CWT_PA_MODES(1); break;
+    default: CWT_PA_MODES(0); break;
+  }
+#undef CWT_PA_MODES
+#undef CWT_PA_LAUNCH
   CWT_LAUNCH_CHECK();
   return 0;
 }
@@ -1581,7 +1585,8 @@ const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw) {
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
                  float* W, float* f_ws /*[E][n][h][w][512]*/, uint8_t* lbl_ws, AdaptScalars* sc /*[E] + partial counts*/,
                  float* acc3 /*[E][3][R][512]*/, float* wbuf /*[E][2][2][512]*/, AdaptDevArgs* dargs /*[E]*/,
-                 AdaptGraphCache* cache, int upw, unsigned* status, long spin_limit, hipStream_t st) {
+                 AdaptGraphCache* cache, int upw, unsigned* status, long spin_limit, hipStream_t st,
+                 hipEvent_t ev_k0, hipEvent_t ev_k1) {
   const long total = (long)n * S * S;  // labels per episode
   unsigned long long* part = (unsigned long long*)(sc + E);  // [E][PREP_MAXBLK][2] after the scalars
   const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
@@ -1599,9 +1604,14 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
                      persist ? cnt : (unsigned*)nullptr, persist ? PA_CNT_WORDS : 0);
   CWT_LAUNCH_CHECK();
   if (iters <= 0) return 0;
-  if (persist)  // one launch for all steps, f read in place (no copy, no graph)
-    return enqueue_adapt_persist(f, lbl_ws, sc, acc3, cnt, dargs, E, n, h, w, S, iters, pG, punits, pncb, pnres, puc,
-                                 status, spin_limit, st);
+  if (persist) {  // one launch for all steps, f read in place (no copy, no graph)
+    if (ev_k0) CWT_HIP(hipEventRecord(ev_k0, st));  // profile bracket of the kernel alone (optional)
+    const int r = enqueue_adapt_persist(f, lbl_ws, sc, acc3, cnt, dargs, E, n, h, w, S, iters, pG, punits, pncb, pnres,
+                                        puc, status, spin_limit, st);
+    if (ev_k1) CWT_HIP(hipEventRecord(ev_k1, st));
+    return r;
+  }
+  // (the step launches: the caller records the bracket around the whole call)
   // the step graph reads f from the library's buffer (fixed address, baked into the graph)
   if (f != f_ws)
     CWT_HIP(hipMemcpyAsync(f_ws, f, (size_t)E * n * h * w * 512 * sizeof(float), hipMemcpyDeviceToDevice, st));

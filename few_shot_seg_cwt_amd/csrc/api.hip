@@ -31,7 +31,7 @@ struct AdaptDevArgs;
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
                  float* W, float* f_ws, uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf,
                  AdaptDevArgs* dargs, AdaptGraphCache* cache, int upw, unsigned* status, long spin_limit,
-                 hipStream_t st);
+                 hipStream_t st, hipEvent_t ev_k0, hipEvent_t ev_k1);
 const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw);
 extern unsigned long long* g_adapt_stamps;
 extern long g_adapt_stamps_n;
@@ -211,6 +211,25 @@ struct Prof {
   void end() {
     if (idx >= 0) (void)hipEventRecord(c->recs[idx].e1, st);
     idx = -1;
+  }
+  // deferred form: the record's two events, for a callee to record around one launch
+  // (Prof(..., level, true)); recorded in place of the constructor / end() when used
+  hipEvent_t ev0() const { return idx >= 0 ? c->recs[idx].e0 : nullptr; }
+  hipEvent_t ev1() const { return idx >= 0 ? c->recs[idx].e1 : nullptr; }
+  Prof(cwt_ctx* ctx, hipStream_t s, const std::string& name, double flops, double bytes, int level, bool deferred)
+      : Prof(ctx, s, name, flops, bytes, deferred ? 1 << 30 : level) {
+    if (!deferred || c->prof_level < level) return;
+    hipEvent_t ev[2];
+    for (int k = 0; k < 2; ++k) {
+      if (c->ev_used == c->evpool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        c->evpool.push_back(e);
+      }
+      ev[k] = c->evpool[c->ev_used++];
+    }
+    c->recs.push_back({name, flops, bytes, ev[0], ev[1]});
+    idx = (int)c->recs.size() - 1;
   }
 };
 
@@ -1065,9 +1084,15 @@ int cwt_inner_adapt_batch(cwt_ctx* ctx, const float* f_s, const int64_t* s_label
              adapt_kernel_name(E, n, h, w, iters, ctx->adapt_upw) + "]",
          (double)E * iters * 2.0 * (4.0 * C * h * w * n), (double)E * iters * ((double)n * h * w * C * 4 + (double)n * S * S),
          1);
+  // the persistent kernel alone (no label prep / setup kernels): the launch rocprofv3 times
+  const char* kname = adapt_kernel_name(E, n, h, w, iters, ctx->adapt_upw);
+  const bool persist_k = strncmp(kname, "adapt_persist", 13) == 0;
+  Prof pk(ctx, (hipStream_t)stream, std::string("inner_adapt_kernel [") + kname + "]",
+          (double)E * iters * 2.0 * (4.0 * C * h * w * n), (double)E * iters * ((double)n * h * w * C * 4 + (double)n * S * S),
+          1, persist_k);
   rc = launch_adapt(f_s, s_label, E, n, h, w, S, lr, iters, W_inout, (float*)fws, (uint8_t*)lbl, (AdaptScalars*)sc,
                     (float*)acc, (float*)wb, (AdaptDevArgs*)dargs, ctx->use_graph ? &ctx->adapt_graphs : nullptr,
-                    ctx->adapt_upw, ctx->status_dev, ctx->adapt_spin_limit, (hipStream_t)stream);
+                    ctx->adapt_upw, ctx->status_dev, ctx->adapt_spin_limit, (hipStream_t)stream, pk.ev0(), pk.ev1());
   p.end();
   return rc;
 }

@@ -29,6 +29,8 @@ namespace cwt {
 
 // STAGE only names the instantiation (0 stem, 1-4 layer1-4, 5 PPM, 6 bottleneck) so that
 // rocprofv3's per-kernel statistics break the conv stack down by stage.
+// (256x128 tiles at one workgroup per CU were tried: they spill 60-76 VGPRs with the two
+// register sets of the prefetch.)
 template <int BM, int BN, int STAGE>
 __global__ __launch_bounds__(256, 2) void conv_igemm_f32(ConvArgs a) {
   constexpr int BK = 32;
@@ -221,10 +223,30 @@ __global__ void conv_splitk_epilogue(ConvArgs a, int nsplit) {
   *(f32x4*)(a.y + (long)m * a.y_ld + a.y_off + co) = v;
 }
 
+// Measured plans of the exact-fp32 conv (tools/conv_f32_sweep.py on the MI355X,
+// tools/gen_plan_table.py --f32): {M, Co, K, bm, bn, nsplit}
+struct MeasuredPlanF32 {
+  int M, Co, K, bm, bn, nsplit;
+};
+static const MeasuredPlanF32 kMeasuredPlansF32[] = {
+#include "conv_plans_f32.inc"
+    {0, 0, 0, 0, 0, 0}};
+
 // Choose tile + split-K for a conv so the grid covers the 256 CUs (SURVEY.md §8(d):
-// at batch 1-6 images, M is only 3600-43200 pixels at layer2-4).
+// at batch 1-6 images, M is only 3600-43200 pixels at layer2-4): the measured table first.
 ConvPlan plan_conv(int M, int Co, int K) {
   ConvPlan p;
+  {
+    const int ktiles = K / 32;
+    for (const MeasuredPlanF32& e : kMeasuredPlansF32)
+      if (e.M == M && e.Co == Co && e.K == K && e.bn > 0 && Co % e.bn == 0) {
+        p.bm = e.bm;
+        p.bn = e.bn;
+        p.kt_per_split = cdiv(ktiles, e.nsplit);
+        p.nsplit = cdiv(ktiles, p.kt_per_split);
+        return p;
+      }
+  }
   const int ktiles = K / 32;
   p.bn = (Co % 128 == 0) ? 128 : 64;
   p.bm = 128;

@@ -215,6 +215,14 @@ class StandardData:
         return t, lt
 
 
+def _draw_base_seed() -> None:
+    """iter(DataLoader) draws the iterator's base seed from the global torch RNG before the
+    sampler draws anything (torch/utils/data/dataloader.py, _BaseDataLoaderIter.__init__; the
+    reference's pretrain.py:105 and train.py:188 iterators): consume the same draw, so every later
+    torch RNG draw (the shuffle order, W0, dropout seeds) lines up with the reference's."""
+    torch.empty((), dtype=torch.int64).random_()
+
+
 class StandardLoader:
     """``torch.utils.data.DataLoader(StandardData, batch_size, shuffle, sampler, drop_last)``
     (dataset.py:61-68) in the calling process: batches stacked on the device, order from torch's
@@ -232,6 +240,7 @@ class StandardLoader:
 
     def __iter__(self):
         n = len(self.dataset)
+        _draw_base_seed()
         if self.sampler is not None:
             order = list(self.sampler)
         elif self.shuffle:
@@ -392,6 +401,7 @@ class EpisodeLoader:
 
     def __iter__(self):
         n = len(self.dataset)
+        _draw_base_seed()
         if self.sampler is not None:
             order = list(self.sampler)
         elif self.shuffle:

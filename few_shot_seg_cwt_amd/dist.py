@@ -75,6 +75,9 @@ def broadcast_params_(flat: torch.Tensor, src: int = 0) -> torch.Tensor:
             t = flat.detach().to(_reduce_device())
             dist.broadcast(t, src)
             flat.data.copy_(t)
+        # writes through .data do not bump the version counter that keys the transformer's
+        # folded inference weights (MultiHeadAttentionOne.params_version): bump it here
+        torch.autograd.graph.increment_version(flat)
     return flat
 
 

@@ -114,8 +114,11 @@ def cwt_tail(transformer, Wb: torch.Tensor, f_q: torch.Tensor):
     """test.py:190-204 after the inner loop: pred_q0 = W . f_q, f_hat = F.normalize(f_q),
     W' = CWT(W, f_hat, f_hat), pred_q = W' . f_hat.  4 heads: the fused form (one pass over the
     raw tokens, no normalised copy; cwt_attention_infer + cwt_classify_scaled); otherwise the
-    module-by-module kernels.  Returns (W', pred_q, pred_q0)."""
-    if transformer.n_head == 4:
+    module-by-module kernels.  Returns (W', pred_q, pred_q0).  The fused entry point takes
+    d_model 512, at most 16384 tokens and 4 queries per call (cwt_attention_infer); any other
+    shape takes the module path, as before it."""
+    B, Cc, h, w = f_q.shape
+    if transformer.n_head == 4 and transformer.d_model == 512 and Cc == 512 and h * w <= 16384 and B <= 4:
         if not f_q.is_contiguous(memory_format=torch.channels_last):
             f_q = f_q.contiguous(memory_format=torch.channels_last)
         W2, inv, pred_q0 = transformer.infer_raw(Wb, f_q)
@@ -277,6 +280,53 @@ class EpisodePipeline:
             W = inner_adapt(f_s, s_label, W0, eng.lr, eng.iters)
             Wb = W.view(1, 2, -1)
             W2, pred_q, pred_q0 = cwt_tail(eng.transformer, Wb, f_q)
+            iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
+            done_all = torch.cuda.Event()
+            done_all.record(self.s_adapt)
+        return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, done=done_all)
+
+    @torch.no_grad()
+    def submit_batch(self, imgs: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor, W0: torch.Tensor,
+                     last: bool = False) -> dict:
+        """Queue E independent episodes that share ONE extractor pass (``EpisodeEngine.run_batch``
+        in the pipeline): imgs [E*shot + E,3,S,S] (the supports episode-major, then the queries),
+        s_label [E,shot,S,S], q_label [E,S,S], W0 [E,2,512] (adapted in place).  Eval-mode BN makes
+        the shared pass exact, the E inner loops run in one persistent launch with per-episode W,
+        class weights and accumulators, the tails in groups of 4: every episode's outputs are the
+        ones ``run`` gives it alone (tests/test_gpu_batch.py).  A throughput form (bigger conv GEMMs,
+        M = E*(shot+1)*h*w), reported beside the one-episode pipeline, not in place of it."""
+        eng = self.eng
+        cur = torch.cuda.current_stream()
+        E = W0.shape[0]
+        shot = s_label.shape[1]
+        if imgs.shape[0] != E * (shot + 1) or E > 16:
+            raise ValueError("imgs must hold E*shot supports then E queries, E <= 16")
+        i = self.k % len(self.s_ext)
+        self.k += 1
+        s_ex = self.s_ext[i]
+        s_ex.wait_stream(cur)
+        self.s_adapt.wait_stream(cur)
+        with torch.cuda.stream(s_ex):
+            if self.c_ext[i] is None:
+                f_all, _ = eng.model.extract_features(imgs)
+            else:
+                with _lib.using_ctx(self.c_ext[i]):
+                    f_all, _ = eng.model.extract_features(imgs)
+            done = torch.cuda.Event()
+            done.record(s_ex)
+        c_ad = self.c_adapt
+        if last and self.drain:
+            if self.c_solo is None:
+                self.c_solo = _lib.new_ctx()
+            c_ad = self.c_solo
+        with torch.cuda.stream(self.s_adapt), _lib.using_ctx(c_ad):
+            self.s_adapt.wait_event(done)
+            for t in (f_all, imgs, s_label, q_label, W0):
+                t.record_stream(self.s_adapt)
+            f_s, f_q = f_all[:E * shot], f_all[E * shot:]
+            W = inner_adapt_batch(f_s, s_label, W0, eng.lr, eng.iters)
+            parts = [cwt_tail(eng.transformer, W[j:j + 4], f_q[j:j + 4]) for j in range(0, E, 4)]
+            W2, pred_q, pred_q0 = (torch.cat([p[j] for p in parts]) for j in range(3))
             iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
             done_all = torch.cuda.Event()
             done_all.record(self.s_adapt)

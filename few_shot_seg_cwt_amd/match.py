@@ -81,10 +81,12 @@ class Conv4d(torch.nn.Module):
 
 
 class NeighConsensus(torch.nn.Module):
-    """match.py:56-85 with the default geometry: three CenterPivotConv4d + ReLU layers,
-    channels in_channel -> 10 -> 10 -> 1, symmetric mode conv(x) + conv(x^T)^T."""
+    """match.py:56-85 with the default geometry: three 4-D conv + ReLU layers, channels
+    in_channel -> 10 -> 10 -> 1, symmetric mode conv(x) + conv(x^T)^T.  ``conv`` defaults to
+    'cv4' (full Conv4d) as the reference signature does (match.py:57); MatchNet passes its
+    config's cv_type ('red' = CenterPivotConv4d in every reference config)."""
 
-    def __init__(self, kernel_sizes=(3, 3, 3), channels=(10, 10, 1), symmetric_mode: bool = True, conv: str = "red",
+    def __init__(self, kernel_sizes=(3, 3, 3), channels=(10, 10, 1), symmetric_mode: bool = True, conv: str = "cv4",
                  in_channel: int = 1, device=None):
         super().__init__()
         if conv not in ("red", "cv4"):

@@ -341,6 +341,9 @@ def train_epoch(model: PretrainPSPNet, batches, epoch: int, iters_per_epoch: int
         # CosineAnnealingLR anneals every group from its own base lr to eta_min (optimizer.py:32)
         losses.append(model.train_step(images, gt, lr=cosine_lr(base_lr, it, total),
                                        lr_head=cosine_lr(base_lr * scale, it, total)))
+        # scheduler.step() follows every optimizer.step() (pretrain.py:118-121): the optimizer's
+        # state then holds the NEXT iteration's lr, which is what a checkpoint saves
+        model._group_lr = (cosine_lr(base_lr, it + 1, total), cosine_lr(base_lr * scale, it + 1, total))
     return torch.stack(losses).mean() if losses else torch.zeros(())
 
 

@@ -136,7 +136,10 @@ class MultiHeadAttentionOne(torch.nn.Module):
         return self
 
     def named_views(self):
-        return [(n, self.flat.data[off:off + k].view(shp)) for n, shp, off, k in self._layout]
+        # detach() (not .data) shares flat's version counter: an in-place write through a view
+        # bumps params_version(), so the folded inference weights cannot go stale
+        flat = self.flat.detach()
+        return [(n, flat[off:off + k].view(shp)) for n, shp, off, k in self._layout]
 
     # -- kernels --------------------------------------------------------------------------
     def _ptrs(self, t: torch.Tensor):

@@ -200,3 +200,52 @@ def test_standard_loader_end_to_end(dev, tmp_path):
             np.testing.assert_array_equal(gt[k].cpu().numpy(), reft)
         n += 1
     assert n == len(loader)
+
+
+class _Items:
+    """A stand-in dataset of n (tensor, tensor) items for the loaders' order logic."""
+    return_paths = False
+
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return torch.tensor([float(i)]), torch.tensor([i])
+
+
+@pytest.mark.parametrize("shuffle", [True, False])
+def test_standard_loader_rng_matches_torch_dataloader(shuffle):
+    """The loader's batch order and the global torch RNG stream after it equal
+    torch.utils.data.DataLoader's (the iterator's base-seed draw, then RandomSampler's seed):
+    pretrain.py:105 iterates a DataLoader, so every later draw lines up with the reference's."""
+    n, bs = 11, 3
+    torch.manual_seed(123)
+    ref = [b[1].view(-1).tolist() for b in torch.utils.data.DataLoader(_Items(n), batch_size=bs, shuffle=shuffle,
+                                                                       drop_last=True)]
+    after_ref = torch.rand(4)
+    torch.manual_seed(123)
+    got = [b[1].view(-1).tolist() for b in D.StandardLoader(_Items(n), bs, shuffle, drop_last=True)]
+    after = torch.rand(4)
+    assert got == ref
+    assert torch.equal(after, after_ref)
+
+
+def test_episode_loader_rng_matches_torch_dataloader():
+    """The episodic loader (batch 1, shuffled) consumes the global RNG like DataLoader too."""
+    n = 7
+    torch.manual_seed(5)
+    ref = [int(b[1]) for b in torch.utils.data.DataLoader(_Items(n), batch_size=1, shuffle=True)]
+    after_ref = torch.rand(3)
+    torch.manual_seed(5)
+
+    class _Ep(_Items):
+        def __getitem__(self, i):
+            t = torch.tensor([i])
+            return t, t, t, t, [i], "", ""
+    got = [int(b[1]) for b in D.EpisodeLoader(_Ep(n), shuffle=True)]
+    after = torch.rand(3)
+    assert got == ref
+    assert torch.equal(after, after_ref)

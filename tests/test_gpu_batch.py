@@ -101,6 +101,46 @@ def test_pipeline_equals_run(dev, streams):
     pipe.close()
 
 
+@pytest.mark.gpu
+def test_pipeline_batch_equals_run(dev):
+    """EpisodePipeline.submit_batch (two episodes sharing one extractor pass, their inner loops in
+    one persistent launch, the tails batched) gives every episode what EpisodeEngine.run gives it
+    alone, pair after pair through the pipeline's streams."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, get_model
+    from few_shot_seg_cwt_amd.episode import EpisodeEngine, EpisodePipeline
+    S, shot, n, E = 129, 1, 4, 2
+    cfg = syn.cfg_defaults(image_size=S)
+    m = get_model(cfg).load_state_dict(syn.make_pspnet_state(50, SEED))
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    eng = EpisodeEngine(m, t, cfg)
+    pipe = EpisodePipeline(eng, extract_streams=2)
+    eps = [syn.make_episode(SEED, 90 + e, S, shot) for e in range(n)]
+    W0 = torch.from_numpy(syn.normal(9, "wpb", (n, 2, 512), 0.04)).to(dev)
+    outs = []
+    for b in range(0, n, E):
+        grp = eps[b:b + E]
+        imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0] for ep in grp] + [ep["qry_img"] for ep in grp]))
+        sl = torch.from_numpy(np.stack([ep["s_label"][0] for ep in grp]))
+        ql = torch.from_numpy(np.concatenate([ep["q_label"] for ep in grp]))
+        outs.append(pipe.submit_batch(imgs.to(dev), sl.to(dev), ql.to(dev), W0[b:b + E].clone(), last=b + E >= n))
+    pipe.wait()
+    torch.cuda.synchronize()
+    for e, ep in enumerate(eps):
+        o = outs[e // E]
+        j = e % E
+        imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
+        r = eng.run(imgs, torch.from_numpy(ep["s_label"][0]).to(dev), torch.from_numpy(ep["q_label"]).to(dev),
+                    W0[e].clone())
+        torch.cuda.synchronize()
+        # the shared pass picks its conv plans for its own M (as run_batch): ~1e-5 after 200 steps
+        assert rel(o["W"][j], r["W"]) < TOL_RUN, e
+        assert rel(o["W2"][j], r["W2"][0]) < TOL_RUN, e
+        assert rel(o["pred_q"][j], r["pred_q"][0]) < TOL_RUN, e
+        assert float((o["iut"][j] - r["iut"][0]).abs().max()) <= 2, e
+    pipe.close()
+
+
 def test_validate_transformer_reuses_its_pipeline(dev):
     """validate_transformer runs every epoch: its EpisodePipeline (and the libcwt contexts it
     holds) is created once per device and reused, so repeated calls do not pile up contexts."""

@@ -217,3 +217,21 @@ def test_pretrain_checkpoint_resume(dev, tmp_path):
     got = r.state_dict()
     for k in ref:
         assert torch.equal(ref[k], got[k]), k
+
+
+@pytest.mark.gpu
+def test_pretrain_checkpoint_lr_is_post_step(dev):
+    """scheduler.step() follows every optimizer.step() (pretrain.py:118-121), so the reference's
+    checkpoint holds the NEXT iteration's lr: after train_epoch's last iteration of the last epoch
+    that is eta_min, per group."""
+    from few_shot_seg_cwt_amd.pretrain import PretrainPSPNet, cosine_lr, train_epoch
+    a = args()
+    m = PretrainPSPNet(a, syn.make_pspnet_state(50, SEED, num_classes_tr=16), dev)
+    batches = [tuple(t.to(dev) for t in make_batch(2, 33, 16, SEED + 21 + i)) for i in range(2)]
+    train_epoch(m, batches, epoch=0, iters_per_epoch=2, epochs=2, base_lr=a["lr"])
+    g = m.optimizer_state_dict()["param_groups"]
+    assert g[0]["lr"] == pytest.approx(cosine_lr(a["lr"], 2, 4))
+    assert g[5]["lr"] == pytest.approx(cosine_lr(a["lr"] * a["scale_lr"], 2, 4))
+    train_epoch(m, batches, epoch=1, iters_per_epoch=2, epochs=2, base_lr=a["lr"])
+    g = m.optimizer_state_dict()["param_groups"]
+    assert g[0]["lr"] == pytest.approx(1e-6) and g[7]["lr"] == pytest.approx(1e-6)
