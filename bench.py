@@ -574,7 +574,9 @@ def main():
     n_ex, ex_fl, ex_ms = total("extract_features")
     n_ad, _, ad_ms = total("inner_adapt x")      # the phase bracket (label prep + setup + the loop)
     ad_bytes = sum(r[2] for r in recs if r[0].startswith("inner_adapt x"))
-    n_at, _, at_ms = total("attention")
+    n_at, _, at_ms = total("attention")       # the module-by-module CWT (CWT_FUSED_TAIL=0)
+    n_tl, _, tl_ms = total("post_loop_tail")  # the one-launch tail (CWT + classifier + metrics)
+    n_tk, _, tk_ms = total("episode_tail_kernel")
     dom = [r for r in recs if r[0].startswith("conv_igemm")]     # the bottleneck conv (level 1 records only it)
     dom_name = dom[0][0].split(" ")[0] if dom else "n/a"
     dn, dfl, dms = len(dom), sum(r[1] for r in dom), sum(r[3] for r in dom)
@@ -824,7 +826,12 @@ def main():
                                "formulation counts the 4096-channel bottleneck conv as written",
                        **conv_roofline(fine, peak)},
         "phases_ms_per_step": {"extract": round(ex_ms / args.steps, 3), "inner_adapt": round(ad_ms / args.steps, 3),
-                               "attention": round(at_ms / args.steps, 3)},
+                               "attention": round(at_ms / args.steps, 3),
+                               "post_loop_tail": round(tl_ms / args.steps, 4),
+                               "post_loop_tail_kernel": round(tk_ms / max(n_tk, 1), 4),
+                               "post_loop_tail_note": "cwt_episode_tail: normalize + pred_q0 + CWT + classifier + "
+                                                      "upsample / argmax / IoU / CE of pred_q and pred_q0 in ONE "
+                                                      "launch (DESIGN.md §3); attention = the module path, 0 here"},
         "phases_roofline": {
             "inner_adapt": {"bound": "hbm", "achieved_GBps": round(ad_achieved, 1), "peak_GBps": PEAK_HBM_GBPS,
                             "frac": round(ad_achieved / PEAK_HBM_GBPS, 4),

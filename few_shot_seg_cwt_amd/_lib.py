@@ -51,6 +51,8 @@ SIGNATURES = {
     "cwt_classify": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_attention_infer": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
     "cwt_classify_scaled": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "cwt_episode_tail": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P,
+                              _P]),
     "cwt_seg_metrics": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "cwt_seg_metrics_pair": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "cwt_seg_ce_fwd_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
@@ -95,6 +97,8 @@ SIGNATURES = {
                               _P, _I, _I, _I, _P]),
     "cwt_debug_conv_b16": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _I,
                                 _P, _I, _I, _I, _P]),
+    "cwt_debug_conv_f32d": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _I,
+                                 _I, _I, _P]),
     "cwt_debug_census": (_I, [_P, _I, _P, _P]),
     "cwt_debug_pretrain_op": (_I, [_P, _I, C.POINTER(_P), C.POINTER(_I64), C.POINTER(_F), _P]),
     "cwt_debug_adapt_stamps": (_I, [_P, _P, _I64, C.POINTER(_I64)]),
@@ -238,6 +242,7 @@ def all_ctx(device: int | None = None):
 
 
 STATUS_ADAPT_BARRIER = 1   # CWT_STATUS_ADAPT_BARRIER (include/cwt.h)
+STATUS_TAIL_BARRIER = 2    # CWT_STATUS_TAIL_BARRIER
 
 
 def check_status(device: int | None = None, clear: bool = True) -> None:
@@ -248,6 +253,9 @@ def check_status(device: int | None = None, clear: bool = True) -> None:
     for c in all_ctx(device):
         check(lib().cwt_ctx_status(c, C.byref(w), int(clear)), "cwt_ctx_status")
         bad |= w.value
+    if bad & STATUS_TAIL_BARRIER:
+        raise CwtError("the fused episode tail's grid barrier timed out (its workgroups were not all co-resident): "
+                       "the CWT output, logits and IoU counts of an episode on this device are wrong")
     if bad & STATUS_ADAPT_BARRIER:
         raise CwtError("the persistent inner loop's grid barrier timed out (its workgroups were not all "
                        "co-resident): the adapted classifier W of an episode on this device is wrong")

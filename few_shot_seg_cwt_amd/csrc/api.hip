@@ -47,6 +47,13 @@ size_t attention_fold_floats(int C, int H);
 int attention_fold(const float* w_qkvs, const float* fc_w, int C, int H, float* fold, float* ws, size_t ws_floats,
                    hipStream_t st);
 size_t attention_infer_ws_floats(int B, int hw, int C, int H);
+size_t episode_tail_ws_floats(int B, int hw, int G);
+size_t episode_tail_cnt_words();
+unsigned episode_tail_max_epoch(int G);
+int launch_episode_tail(const float* q, const float* f, int B, int hw, int h, int w, int S, const int64_t* target,
+                        const float* fold, const float* fc_b, const float* ln_w, const float* ln_b, float* out,
+                        float* logits, float* logits0, float* iut, double* ce, float* iut0, float* ws,
+                        unsigned* cnt, unsigned epoch, int G, long spin_limit, unsigned* status, hipStream_t st);
 int attention_infer(const float* q, const float* f, int B, int hw, int C, int H, const float* fold, const float* fc_b,
                     const float* ln_w, const float* ln_b, float* out, float* inv_norm, float* logits0, float* ws,
                     hipStream_t st);
@@ -177,6 +184,9 @@ struct cwt_ctx {
   unsigned* status_host = nullptr;
   unsigned* status_dev = nullptr;
   long adapt_spin_limit = 0;  // 0: the persistent loop's default bound (cwt_debug_adapt_spin_limit)
+  // cwt_episode_tail's counters: this context's next launch number on them; ~0u = re-zero first
+  unsigned tail_epoch = ~0u;
+  int tail_G = 0;
   // folded CWT weights of cwt_attention_infer (M_h = W_h^T W_h, P = [fc_h W_h]) and the
   // parameter identity they were folded from (buffers + the caller's version counter)
   const float* fold_w = nullptr;
@@ -567,9 +577,14 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   // the training-mode BN pass (once per epoch) amplifies conv rounding ~100x through its
   // batch statistics: in fp32 precision it runs the exact-fp32 conv path
   const bool conv_split = ctx->conv_split && !(tb && !b16);
-  const bool s_path = b16 || conv_split;  // conv_x3s.hip kernels
+  const bool s_path = b16 || conv_split;  // S-layout / bf16 activations
   const int layout = b16 ? ACT_BF16 : conv_split ? ACT_SPLIT : ACT_F32;
-  const int prec = b16 ? 1 : 3;
+  // the exact-fp32 path (eval mode) runs on the same LDS-DMA conv body (conv_igemm_f32d: fp32
+  // NHWC activations, f32 MFMA); CWT_CONV_F32D=0 selects the register-staged conv_igemm_f32
+  static const bool f32d_env = !(getenv("CWT_CONV_F32D") && getenv("CWT_CONV_F32D")[0] == '0');
+  const bool f32d = !s_path && !tb && f32d_env;
+  const bool dma = s_path || f32d;  // conv_x3s.hip kernels
+  const int prec = b16 ? 1 : conv_split ? 3 : 0;
   const int Hs = down2(S), H1 = down2(Hs), h = down2(H1);
   const long sA = std::max({(long)N * Hs * Hs * 128, (long)N * H1 * H1 * 256, (long)N * h * h * 2048});
   const long sT1 = std::max((long)N * H1 * H1 * 128, (long)N * h * h * 512);
@@ -663,12 +678,12 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     ConvArgs a = make_args(c);
     if (b16 && !c.L->w_b) return fail(CWT_ESTATE, "bf16 conv weights missing (Ci % 64 != 0)");
     ConvPlan pl = b16 ? plan_conv_b16(a.M, a.Co, a.K) : conv_split ? plan_conv_x3s(a.M, a.Co, a.K)
-                                                                  : plan_conv(a.M, a.Co, a.K);
+                  : f32d ? plan_conv_f32d(a.M, a.Co, a.K) : plan_conv(a.M, a.Co, a.K);
     plans.push_back(pl);
     if (pl.nsplit > 1) part_floats = std::max(part_floats, (size_t)pl.nsplit * a.M * a.Co);
   }
   const __bf16* zero = nullptr;
-  if (s_path && (rc = zero_line(ctx, &zero))) return rc;
+  if (dma && (rc = zero_line(ctx, &zero))) return rc;
   float *BNPART = nullptr, *BNSC = nullptr;
   size_t bn_part_floats = 0;
   if (tb) {
@@ -729,7 +744,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     const double bytes = eb * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K) +
                          ob * ((double)a.M * a.Co + (a.res ? (double)a.M * a.Co : 0.0));
     Prof p(ctx, st,
-           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : "conv_igemm_f32<") +
+           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : f32d ? "conv_igemm_f32d<" : "conv_igemm_f32<") +
                std::to_string(pl.bm) + "," +
                std::to_string(pl.bn) + "," +
                std::to_string(calls[i].stage) + ">" +
@@ -738,16 +753,16 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
                std::to_string(a.stride) + "d" + std::to_string(a.dil) + "@" + std::to_string(a.Ho),
            flops, bytes, calls[i].stage == 6 ? 1 : 2);
     int r;
-    if (s_path) {
+    if (dma) {
       ConvSArgs sa;
       memset(&sa, 0, sizeof(sa));
       const ConvCall& c = calls[i];
-      sa.xs = (const __bf16*)c.x;
-      sa.ws = b16 ? c.L->w_b : c.L->w_s;
+      sa.xs = (const __bf16*)c.x;  // (f32d: the fp32 NHWC map, the same 128-B line geometry)
+      sa.ws = b16 ? c.L->w_b : f32d ? (const __bf16*)c.L->w : c.L->w_s;
       sa.zero = zero;
       sa.scale = a.scale;
       sa.shift = a.shift;
-      if (c.out_f32) {
+      if (c.out_f32 || f32d) {
         sa.y = c.y;
         sa.y_ld = c.y_ld;
         sa.y_off = c.y_off;
@@ -948,6 +963,7 @@ int cwt_ctx_status(cwt_ctx* ctx, uint32_t* status, int clear) {
   if (!ctx || !status) return fail(CWT_EARG, "null argument");
   volatile unsigned* w = ctx->status_host;
   *status = *w;
+  if (*status & CWT_STATUS_TAIL_BARRIER) ctx->tail_epoch = ~0u;  // its counters are re-zeroed before the next tail
   if (clear) *w = 0u;
   return 0;
 }
@@ -1196,6 +1212,55 @@ int cwt_attention_infer(cwt_ctx* ctx, const float* q, const float* f, int B, int
     ctx->fold_H = H;
   }
   rc = attention_infer(q, f, B, hw, C, H, (const float*)fold, fc_b, ln_w, ln_b, out, inv_norm, logits0, (float*)ws, st);
+  p.end();
+  return rc;
+}
+
+int cwt_episode_tail(cwt_ctx* ctx, const float* q, const float* f, int B, int h, int w, int S, const int64_t* q_label,
+                     const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b,
+                     int64_t params_version, float* out, float* logits, float* logits0, float* iut, double* ce,
+                     float* iut0, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(q && f && q_label && w_qkvs && fc_w && fc_b && ln_w && ln_b && out && logits && logits0 && iut && ce && iut0,
+            "null buffer");
+  const int hw = h * w;
+  CWT_CHECK(B >= 1 && B <= 4 && h >= 1 && w >= 1 && hw <= 512 * 32 && S - 1 == 8 * (h - 1) && S - 1 == 8 * (w - 1),
+            "need 1 <= B <= 4, h*w <= 16384, S - 1 == 8 (h - 1) == 8 (w - 1)");
+  CWT_HIP(hipSetDevice(ctx->device));
+  const hipStream_t st = (hipStream_t)stream;
+  constexpr int C = 512, H = 4;
+  int cu = 0;
+  CWT_HIP(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  // G co-resident 512-thread workgroups (one per CU by their LDS); CWT_TAIL_G for A/B
+  int G = std::min(64, cu);
+  if (const char* gs = getenv("CWT_TAIL_G")) G = std::max(1, std::min(atoi(gs), cu));
+  void *fold, *ws, *cnt;
+  int rc;
+  if ((rc = ensure_ws(ctx, "attn.fold", attention_fold_floats(C, H) * 4, &fold))) return rc;
+  if ((rc = ensure_ws(ctx, "tail.ws", std::max(episode_tail_ws_floats(B, hw, G), (size_t)4 << 20) * 4, &ws))) return rc;
+  if ((rc = ensure_ws(ctx, "tail.cnt", episode_tail_cnt_words() * 4, &cnt))) return rc;
+  // phase record (the fold when the parameters changed + the launch) and the kernel alone
+  Prof p(ctx, st, "post_loop_tail", (double)B * (2.0 * 2.0 * hw * C * C * H + 2.0 * 2.0 * H * 2.0 * hw * C),
+         4.0 * ((double)B * hw * C + 2.0 * H * C * C + 2.0 * C), 1);
+  Prof pk(ctx, st, "episode_tail_kernel", (double)B * (2.0 * 2.0 * hw * C * C * H + 2.0 * 2.0 * H * 2.0 * hw * C),
+          4.0 * ((double)B * hw * C * 2 + 2.0 * H * C * C) + 9.0 * B * S * S, 1, true);
+  if (ctx->fold_w != w_qkvs || ctx->fold_fc != fc_w || ctx->fold_ver != params_version || ctx->fold_H != H) {
+    if ((rc = attention_fold(w_qkvs, fc_w, C, H, (float*)fold, (float*)ws, (size_t)4 << 20, st))) return rc;
+    ctx->fold_w = w_qkvs;
+    ctx->fold_fc = fc_w;
+    ctx->fold_ver = params_version;
+    ctx->fold_H = H;
+  }
+  if (ctx->tail_epoch > episode_tail_max_epoch(G) || ctx->tail_G != G) {  // fresh, wrapped, aborted or re-sized
+    CWT_HIP(hipMemsetAsync(cnt, 0, episode_tail_cnt_words() * 4, st));
+    ctx->tail_epoch = 0;
+    ctx->tail_G = G;
+  }
+  if (pk.ev0()) CWT_HIP(hipEventRecord(pk.ev0(), st));
+  rc = launch_episode_tail(q, f, B, hw, h, w, S, q_label, (const float*)fold, fc_b, ln_w, ln_b, out, logits, logits0,
+                           iut, ce, iut0, (float*)ws, (unsigned*)cnt, ctx->tail_epoch++, G, ctx->adapt_spin_limit,
+                           ctx->status_dev, st);
+  if (pk.ev1()) CWT_HIP(hipEventRecord(pk.ev1(), st));
   p.end();
   return rc;
 }
@@ -1734,7 +1799,8 @@ static int debug_conv_s(cwt_ctx* ctx, int prec, const void* xs, int N, int Hi, i
   a.Wo = (Wi + 2 * pad - dil * (k - 1) - 1) / stride + 1;
   a.M = N * a.Ho * a.Wo;
   a.K = k * k * Ci;
-  ConvPlan p = prec == 1 ? plan_conv_b16(a.M, a.Co, a.K) : plan_conv_x3s(a.M, a.Co, a.K);
+  ConvPlan p = prec == 1 ? plan_conv_b16(a.M, a.Co, a.K) : prec == 0 ? plan_conv_f32d(a.M, a.Co, a.K)
+                                                         : plan_conv_x3s(a.M, a.Co, a.K);
   if (bm > 0) {
     const int var = bm / 1000;  // bm = 1000 * variant + rows (cwt_debug.h)
     bm %= 1000;
@@ -1770,6 +1836,14 @@ int cwt_debug_conv_s(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci
                      void* stream) {
   return debug_conv_s(ctx, 3, xs, N, Hi, Wi, Ci, ws, scale, shift, Co, k, stride, pad, dil, res, res_ld, res_s, relu, y,
                       y_ld, y_off, ys, bm, bn, nsplit, stream);
+}
+
+int cwt_debug_conv_f32d(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, const float* w_packed,
+                        const float* scale, const float* shift, int Co, int k, int stride, int pad, int dil,
+                        const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
+                        int nsplit, void* stream) {
+  return debug_conv_s(ctx, 0, x, N, Hi, Wi, Ci, w_packed, scale, shift, Co, k, stride, pad, dil, res, res_ld, nullptr,
+                      relu, y, y_ld, y_off, nullptr, bm, bn, nsplit, stream);
 }
 
 int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws, const float* scale,

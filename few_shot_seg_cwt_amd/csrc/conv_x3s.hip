@@ -153,7 +153,8 @@ __device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, co
 // addressing of the operand DMA (every production instantiation sets it).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF>
 __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
-  static_assert(PREC == 1 || PREC == 3, "PREC: 3 = bf16x3 over the S-layout, 1 = plain bf16");
+  static_assert(PREC == 0 || PREC == 1 || PREC == 3,
+                "PREC: 3 = bf16x3 over the S-layout, 1 = plain bf16, 0 = exact fp32 (f32 MFMA)");
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int FM = WM / 16, FN = WN / 16;
@@ -333,7 +334,17 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        if (PREC == 1) {  // "hi" / "lo" = first / second 32 k of the 64-deep tile
+        if (PREC == 0) {
+          // exact fp32: a 16-B chunk is 4 consecutive k of one row; lane (row fr, chunk fk)
+          // supplies k = 4 fk + s to MFMA s (A and B permuted alike: the k order of a sum is
+          // free), 16-B chunks fk and 4 + fk cover the 32-deep tile in 8 v_mfma_f32_16x16x4_f32
+          const f32x4 a0 = __builtin_bit_cast(f32x4, F.ah[i]), a1 = __builtin_bit_cast(f32x4, F.al[i]);
+          const f32x4 b0 = __builtin_bit_cast(f32x4, F.bh[j]), b1 = __builtin_bit_cast(f32x4, F.bl[j]);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], b0[s], acc[i][j], 0, 0, 0);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], b1[s], acc[i][j], 0, 0, 0);
+        } else if (PREC == 1) {  // "hi" / "lo" = first / second 32 k of the 64-deep tile
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.ah[i], F.bh[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.al[i], F.bl[j], acc[i][j], 0, 0, 0);
         } else {
@@ -456,6 +467,14 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x3s(ConvSArg
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_b16(ConvSArgs a) {
   conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 1, (PF | 8)>(a);
+}
+// Exact fp32 on the same LDS-DMA body: fp32 NHWC activations and the fp32 packed weights are
+// byte-for-byte the S-layout's geometry (one 128-B line = 32 fp32 channels of one pixel, or 32 k
+// of one packed weight row), so only the fragment arithmetic differs (v_mfma_f32_16x16x4_f32,
+// an fmaf chain per output: the reference's fp32 products without the bf16x3 split).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_f32d(ConvSArgs a) {
+  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 0, (PF | 8)>(a);
 }
 
 // Split-K reduction (fixed order, deterministic) + the same epilogue math.
@@ -609,6 +628,7 @@ int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipSt
   }
 CWT_TILE_LAUNCH(conv_igemm_x3s)
 CWT_TILE_LAUNCH(conv_igemm_b16)
+CWT_TILE_LAUNCH(conv_igemm_f32d)
 #undef CWT_TILE_LAUNCH
 
 struct MeasuredPlanS {
@@ -678,6 +698,27 @@ ConvPlan plan_conv_b16(int M, int Co, int K) {
   return plan_heuristic_s(M, Co, ktiles);
 }
 
+static const MeasuredPlanS kMeasuredPlansF32D[] = {
+#include "conv_plans_f32d.inc"
+    {0, 0, 0, 0, 0, 0, 0}};
+
+// Exact fp32 on the LDS-DMA body: 32-deep K-tiles; its own measured table
+// (conv_plans_f32d.inc, tools/conv_s_sweep.py --prec 0), else the heuristic.
+ConvPlan plan_conv_f32d(int M, int Co, int K) {
+  const int ktiles = K / 32;
+  for (const MeasuredPlanS& e : kMeasuredPlansF32D)
+    if (e.M == M && e.Co == Co && e.K == K && e.bn > 0 && Co % e.bn == 0) {
+      ConvPlan p;
+      p.bm = e.bm;
+      p.bn = e.bn;
+      p.var = e.var;
+      p.kt_per_split = cdiv(ktiles, e.nsplit);
+      p.nsplit = cdiv(ktiles, p.kt_per_split);
+      return p;
+    }
+  return plan_heuristic_s(M, Co, ktiles);
+}
+
 template <int PREC>
 static void launch_splitk_s(const ConvSArgs& a, int nsplit, hipStream_t st) {
   const long n = (long)a.M * (a.Co / 8);
@@ -695,7 +736,9 @@ static void launch_splitk_s(const ConvSArgs& a, int nsplit, hipStream_t st) {
 // 64-channel-block order, plan_conv_b16)
 int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,
                     hipStream_t st, int prec) {
-  if (prec != 1 && prec != 3) return fail(CWT_EARG, "conv precision must be 3 (bf16x3) or 1 (bf16)");
+  if (prec != 0 && prec != 1 && prec != 3)
+    return fail(CWT_EARG, "conv precision must be 3 (bf16x3), 1 (bf16) or 0 (exact fp32)");
+  if (prec == 0 && (a.ys || a.res_s || !a.y)) return fail(CWT_EARG, "exact-fp32 conv: fp32 output and residual only");
   if (!a.xs || !a.ws || !a.zero) return fail(CWT_ESTATE, "S-layout conv needs its input, weights and a zero line");
   const int kb = prec == 1 ? 64 : 32;
   if (a.Ci % kb || a.Co % 64 || a.Co % p.bn)
@@ -714,7 +757,17 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
     main.part = nullptr;
   }
   dim3 grid(cdiv(a.M, p.bm), a.Co / p.bn, nsplit);
-  if (prec == 1) {
+  if (prec == 0) {
+    switch (stage) {
+      case 0: launch_tiles_conv_igemm_f32d<0>(main, p, grid, st); break;
+      case 1: launch_tiles_conv_igemm_f32d<1>(main, p, grid, st); break;
+      case 2: launch_tiles_conv_igemm_f32d<2>(main, p, grid, st); break;
+      case 3: launch_tiles_conv_igemm_f32d<3>(main, p, grid, st); break;
+      case 4: launch_tiles_conv_igemm_f32d<4>(main, p, grid, st); break;
+      case 5: launch_tiles_conv_igemm_f32d<5>(main, p, grid, st); break;
+      default: launch_tiles_conv_igemm_f32d<6>(main, p, grid, st); break;
+    }
+  } else if (prec == 1) {
     switch (stage) {
       case 0: launch_tiles_conv_igemm_b16<0>(main, p, grid, st); break;
       case 1: launch_tiles_conv_igemm_b16<1>(main, p, grid, st); break;
@@ -740,6 +793,8 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
     main.part = part_ws;
     if (prec == 1)
       launch_splitk_s<1>(main, nsplit, st);
+    else if (prec == 0)
+      launch_splitk_s<0>(main, nsplit, st);
     else
       launch_splitk_s<3>(main, nsplit, st);
     CWT_LAUNCH_CHECK();

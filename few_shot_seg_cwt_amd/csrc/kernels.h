@@ -116,6 +116,7 @@ int launch_splitk_epilogue(const ConvArgs& a, int nsplit, hipStream_t st);
 // split-activation variant (conv_x3s.hip)
 ConvPlan plan_conv_x3s(int M, int Co, int K);
 ConvPlan plan_conv_b16(int M, int Co, int K);
+ConvPlan plan_conv_f32d(int M, int Co, int K);
 // prec 3: bf16x3 (S-layout operands); prec 1: plain bf16 (NHWC bf16 activations, [Co][K]
 // bf16 weights with K ordered (64-channel block, tap, channel): packed_k64)
 int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,

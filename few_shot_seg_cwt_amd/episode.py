@@ -128,6 +128,53 @@ def cwt_tail(transformer, Wb: torch.Tensor, f_q: torch.Tensor):
     return W2, classify(W2, fqn), pred_q0
 
 
+_FUSED_TAIL = os.environ.get("CWT_FUSED_TAIL", "1") != "0"   # 0: the module kernels (A/B)
+
+
+def fused_tail_ok(transformer, f_q: torch.Tensor) -> bool:
+    """The one-launch tail (cwt_episode_tail) takes 4 heads, d_model 512, <= 4 queries of
+    <= 16384 tokens (S - 1 == 8 (h - 1): the extractor's geometry)."""
+    B, Cc, h, w = f_q.shape
+    return (_FUSED_TAIL and transformer.n_head == 4 and Cc == 512 and h * w <= 16384 and B <= 4 and h == w)
+
+
+def episode_tail(transformer, Wb: torch.Tensor, f_q: torch.Tensor, q_label: torch.Tensor):
+    """test.py:190-224 after the inner loop in ONE launch (cwt_episode_tail): pred_q0 = W . f_q,
+    W' = CWT(W, F.normalize(f_q)), pred_q = W' . F.normalize(f_q), and the metrics of both
+    against q_label.  Returns (W', pred_q, pred_q0, iut, ce, iut0) as cwt_tail + seg_metrics_pair
+    do (the same function: tests/test_gpu_tail.py)."""
+    if not f_q.is_contiguous(memory_format=torch.channels_last):
+        f_q = f_q.contiguous(memory_format=torch.channels_last)
+    B, Cc, h, w = f_q.shape
+    S = q_label.shape[-1]
+    t = transformer
+    Wb = Wb.contiguous()
+    tg = q_label.reshape(B, S, S).contiguous()
+    dev = f_q.device
+    out = torch.empty((B, 2, Cc), device=dev, dtype=torch.float32)
+    logits = torch.empty((B, 2, h, w), device=dev, dtype=torch.float32)
+    logits0 = torch.empty_like(logits)
+    iut = torch.empty((B, 3, 2), device=dev, dtype=torch.float32)
+    iut0 = torch.empty_like(iut)
+    ce = torch.empty((B, 2), device=dev, dtype=torch.float64)
+    wq, fw, fb, lw, lb = t._ptrs(t.flat)
+    _lib.check(_lib.lib().cwt_episode_tail(_lib.ctx(dev.index), _lib.ptr(Wb), _lib.ptr(f_q), B, h, w, S, _lib.ptr(tg),
+                                           wq, fw, fb, lw, lb, t.params_version(), _lib.ptr(out), _lib.ptr(logits),
+                                           _lib.ptr(logits0), _lib.ptr(iut), _lib.ptr(ce), _lib.ptr(iut0),
+                                           _lib.stream_ptr(dev)), "cwt_episode_tail")
+    return out, logits, logits0, iut, ce, iut0
+
+
+def tail_and_metrics(transformer, Wb: torch.Tensor, f_q: torch.Tensor, q_label: torch.Tensor):
+    """(W', pred_q, pred_q0, iut, ce, iut0) of an episode group (B <= 4): the one-launch tail
+    where it applies, else cwt_tail + seg_metrics_pair."""
+    if fused_tail_ok(transformer, f_q):
+        return episode_tail(transformer, Wb, f_q, q_label)
+    W2, pred_q, pred_q0 = cwt_tail(transformer, Wb, f_q)
+    iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
+    return W2, pred_q, pred_q0, iut, ce, iut0
+
+
 def classify_bwd(dlogits: torch.Tensor, f: torch.Tensor, dW: torch.Tensor):
     B, Cc, h, w = f.shape
     dlogits = dlogits.contiguous()
@@ -170,8 +217,7 @@ class EpisodeEngine:
         f_s, f_q = f_all[:shot], f_all[shot:]
         W = inner_adapt(f_s, s_label, W0, self.lr, self.iters)
         Wb = W.view(1, 2, -1)
-        W2, pred_q, pred_q0 = cwt_tail(self.transformer, Wb, f_q)
-        iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
+        W2, pred_q, pred_q0, iut, ce, iut0 = tail_and_metrics(self.transformer, Wb, f_q, q_label)
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, f_s=f_s, f_q=f_q)
 
     @torch.no_grad()
@@ -189,9 +235,8 @@ class EpisodeEngine:
         f_all, _ = self.model.extract_features(imgs)
         f_s, f_q = f_all[:E * shot], f_all[E * shot:]
         W = inner_adapt_batch(f_s, s_label, W0, self.lr, self.iters)
-        parts = [cwt_tail(self.transformer, W[i:i + 4], f_q[i:i + 4]) for i in range(0, E, 4)]
-        W2, pred_q, pred_q0 = (torch.cat([p[j] for p in parts]) for j in range(3))
-        iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
+        parts = [tail_and_metrics(self.transformer, W[i:i + 4], f_q[i:i + 4], q_label[i:i + 4]) for i in range(0, E, 4)]
+        W2, pred_q, pred_q0, iut, ce, iut0 = (torch.cat([p[j] for p in parts]) for j in range(6))
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, f_s=f_s, f_q=f_q)
 
 
@@ -279,8 +324,7 @@ class EpisodePipeline:
             f_s, f_q = f_all[:shot], f_all[shot:]
             W = inner_adapt(f_s, s_label, W0, eng.lr, eng.iters)
             Wb = W.view(1, 2, -1)
-            W2, pred_q, pred_q0 = cwt_tail(eng.transformer, Wb, f_q)
-            iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
+            W2, pred_q, pred_q0, iut, ce, iut0 = tail_and_metrics(eng.transformer, Wb, f_q, q_label)
             done_all = torch.cuda.Event()
             done_all.record(self.s_adapt)
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, done=done_all)
@@ -325,9 +369,9 @@ class EpisodePipeline:
                 t.record_stream(self.s_adapt)
             f_s, f_q = f_all[:E * shot], f_all[E * shot:]
             W = inner_adapt_batch(f_s, s_label, W0, eng.lr, eng.iters)
-            parts = [cwt_tail(eng.transformer, W[j:j + 4], f_q[j:j + 4]) for j in range(0, E, 4)]
-            W2, pred_q, pred_q0 = (torch.cat([p[j] for p in parts]) for j in range(3))
-            iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
+            parts = [tail_and_metrics(eng.transformer, W[j:j + 4], f_q[j:j + 4], q_label[j:j + 4])
+                     for j in range(0, E, 4)]
+            W2, pred_q, pred_q0, iut, ce, iut0 = (torch.cat([p[j] for p in parts]) for j in range(6))
             done_all = torch.cuda.Event()
             done_all.record(self.s_adapt)
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, done=done_all)

@@ -37,6 +37,7 @@ extern "C" {
 
 /* Bits of the context's asynchronous status word (cwt_ctx_status). */
 #define CWT_STATUS_ADAPT_BARRIER 1u  /* the persistent inner loop's grid barrier timed out: W is wrong */
+#define CWT_STATUS_TAIL_BARRIER 2u   /* cwt_episode_tail's grid barrier timed out: its outputs are wrong */
 
 typedef struct cwt_ctx cwt_ctx;
 typedef struct cwt_backbone cwt_backbone;  /* one loaded (frozen) PSPNet extractor */
@@ -260,6 +261,24 @@ int cwt_classify_scaled(cwt_ctx* ctx, const float* W, const float* f, const floa
  * W: device [B,2,C]; f: NHWC [B,P,C]; logits: device [B,2,P] (NCHW [B,2,h,w]). */
 int cwt_classify(cwt_ctx* ctx, const float* W, const float* f, int B, int P, int C, float* logits,
                  void* stream);
+
+/*
+ * The inference episode's whole tail after the inner loop in ONE launch (test.py:190-224):
+ * pred_q0 = W . f_q, f_hat = F.normalize(f_q), W' = MultiHeadAttentionOne(4, 512, 512, 512).eval()
+ * (W, f_hat, f_hat), pred_q = W' . f_hat, and the upsample / argmax / intersection-union-target /
+ * CE of pred_q and pred_q0 against q_label (util.py:237-308) -- what cwt_attention_infer +
+ * cwt_classify_scaled + cwt_seg_metrics_pair compute in 8 launches, as one grid of co-resident
+ * workgroups with in-kernel grid barriers between the phases.  The folded weights
+ * follow (w_qkvs, fc_w, params_version) as in cwt_attention_infer.  C = 512, H = 4, B <= 4,
+ * hw = h*w <= 16384, S - 1 == 8 (h - 1).
+ * q [B,2,C] (the adapted W); f NHWC [B,hw,C] raw; q_label int64 [B,S,S]; out W' [B,2,C];
+ * logits / logits0 [B,2,hw]; iut / iut0 fp32 [B,3,2]; ce fp64 [B,2] (sum of -log p_y, count).
+ * A grid barrier that cannot complete sets CWT_STATUS_TAIL_BARRIER.
+ */
+int cwt_episode_tail(cwt_ctx* ctx, const float* q, const float* f, int B, int h, int w, int S, const int64_t* q_label,
+                     const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w, const float* ln_b,
+                     int64_t params_version, float* out, float* logits, float* logits0, float* iut, double* ce,
+                     float* iut0, void* stream);
 
 /*
  * Segmentation metrics of low-res logits against a full-res label:

@@ -53,6 +53,16 @@ int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int 
                        int dil, const float* res, int res_ld, const void* res_s, int relu, float* y,
                        int y_ld, int y_off, void* ys, int bm, int bn, int nsplit, void* stream);
 
+/* The exact-fp32 conv on the LDS-DMA body (conv_igemm_f32d, the eval-mode exact path of
+ * cwt_ctx_set_conv_arith(CWT_CONV_ARITH_F32)): x fp32 NHWC [N][Hi][Wi][Ci] (Ci % 32 == 0,
+ * pixel stride Ci), w_packed fp32 [Co][K] in the packed_k order (32-channel block, tap, channel),
+ * res fp32 [M][res_ld] or NULL, y fp32 [M][y_ld] at channel offset y_off.  bm / bn / nsplit as
+ * cwt_debug_conv_s (bm = 1000 * variant + rows; 0 = the library's plan). */
+int cwt_debug_conv_f32d(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, const float* w_packed,
+                        const float* scale, const float* shift, int Co, int k, int stride, int pad, int dil,
+                        const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
+                        int nsplit, void* stream);
+
 /* Timing-study hook of the inner loop: with CWT_ADAPT_DBG=32 in the environment, the inner
  * loop runs a separately compiled instantiation that records clock stamps per step and
  * workgroup (persistent loop: tools/persist_stamps.py; per-step launches with

@@ -211,3 +211,73 @@ def test_conv_b16_plans(case, plan):
     assert err < TOL_B16, err
     # the bf16 output is the round-to-nearest bf16 of the fp32 output
     assert torch.equal(yb, yf.to(torch.bfloat16).float())
+
+
+# ---------------------------------------------------------------- exact fp32 (conv_igemm_f32d)
+# the LDS-DMA body over fp32 NHWC operands with v_mfma_f32_16x16x4_f32 (fmaf chains): against a
+# float64 conv only the fp32 summation order differs
+TOL_F32D = 1e-5
+
+
+def pack_w_f32(w):
+    """[Co,Ci,k,k] fp32 -> fp32 [Co][K], K in packed_k order (32-channel block, tap, channel)."""
+    Co, Ci, k, _ = w.shape
+    return w.reshape(Co, Ci // 32, 32, k * k).permute(0, 1, 3, 2).contiguous()
+
+
+def run_conv_f32d(x, w, scale, shift, stride, pad, dil, res=None, relu=True, bm=0, bn=0, nsplit=0, y_pad=0, y_off=0):
+    L = _lib()
+    dev = torch.device("cuda", 0)
+    N, Ci, Hi, Wi = x.shape
+    Co, _, k, _ = w.shape
+    xd = x.permute(0, 2, 3, 1).contiguous().to(dev)
+    wd = pack_w_f32(w).to(dev)
+    Ho = (Hi + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    y_ld = Co + y_pad
+    y = torch.full((N, Ho, Ho, y_ld), float("nan"), device=dev)
+    rd = res.permute(0, 2, 3, 1).contiguous().to(dev) if res is not None else None
+    sc, sh = scale.to(dev), shift.to(dev)
+    rc = L.lib().cwt_debug_conv_f32d(L.ctx(0), L.ptr(xd), N, Hi, Wi, Ci, L.ptr(wd), L.ptr(sc), L.ptr(sh), Co, k,
+                                     stride, pad, dil, L.ptr(rd), Co, int(relu), L.ptr(y), y_ld, y_off, bm, bn,
+                                     nsplit, L.stream_ptr())
+    L.check(rc, "cwt_debug_conv_f32d")
+    torch.cuda.synchronize()
+    yc = y.cpu()
+    if y_pad:
+        untouched = torch.cat([yc[..., :y_off], yc[..., y_off + Co:]], -1)
+        assert torch.isnan(untouched).all(), "wrote outside its channel slice"
+    return yc[..., y_off:y_off + Co].permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("plan", PLANS, ids=lambda p: f"{p[0]}x{p[1]}s{p[2]}")
+def test_conv_f32d_plans(case, plan):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    N, Ci, Co, Hi, k, stride, dil, has_res = case
+    bm, bn, ns = plan
+    if bn and Co % bn:
+        pytest.skip("Co not a multiple of the tile")
+    tag = f"{N}_{Ci}_{Co}_{Hi}_{k}"
+    x = torch.from_numpy(syn.normal(1, "x" + tag, (N, Ci, Hi, Hi), 1.0))
+    w = torch.from_numpy(syn.normal(1, "w" + tag, (Co, Ci, k, k), (2.0 / (Ci * k * k)) ** 0.5))
+    scale = torch.from_numpy(syn.uniform(1, "s" + tag, (Co,), 0.5, 1.5))
+    shift = torch.from_numpy(syn.normal(1, "b" + tag, (Co,), 0.1))
+    pad = dil if k == 3 else 0
+    Ho = (Hi + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    res = torch.from_numpy(syn.normal(1, "r" + tag, (N, Co, Ho, Ho), 1.0)) if has_res else None
+    y = run_conv_f32d(x, w, scale, shift, stride, pad, dil, res, bm=bm, bn=bn, nsplit=ns)
+    ref = ref_conv(x, w, scale, shift, stride, pad, dil, res, True)
+    err = float((y.double() - ref).abs().max() / ref.abs().max())
+    assert err < TOL_F32D, err
+
+
+def test_conv_f32d_channel_strided_out():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    x = torch.from_numpy(syn.normal(2, "x", (2, 64, 11, 11), 1.0))
+    w = torch.from_numpy(syn.normal(2, "w", (128, 64, 3, 3), 0.06))
+    scale, shift = torch.ones(128), torch.zeros(128)
+    y = run_conv_f32d(x, w, scale, shift, 1, 1, 1, None, relu=False, y_pad=256, y_off=128)
+    ref = ref_conv(x, w, scale, shift, 1, 1, 1, None, False)
+    assert float((y.double() - ref).abs().max() / ref.abs().max()) < TOL_F32D

@@ -75,6 +75,42 @@ def test_extract_features_full_vs_oracle(dev):
     assert rel(f, ref) < TOL
 
 
+class exact_fp32:
+    """the default context's conv stack on the exact-fp32 path (cwt_ctx_set_conv_arith F32:
+    conv_igemm_f32d, the LDS-DMA body on v_mfma_f32_16x16x4_f32) for the duration"""
+
+    def __enter__(self):
+        from few_shot_seg_cwt_amd import _lib
+        _lib.check(_lib.lib().cwt_ctx_set_conv_arith(_lib.ctx(0), 1), "cwt_ctx_set_conv_arith")
+
+    def __exit__(self, *exc):
+        from few_shot_seg_cwt_amd import _lib
+        _lib.check(_lib.lib().cwt_ctx_set_conv_arith(_lib.ctx(0), 0), "cwt_ctx_set_conv_arith")
+        return False
+
+
+@pytest.mark.parametrize("layers", [50, 101])
+def test_extract_features_exact_fp32_small_vs_reference(dev, small, layers):
+    ep = syn.make_episode(SEED, 7, 33, 2)
+    x = torch.from_numpy(ep["spprt_imgs"][0]).to(dev)
+    with exact_fp32():
+        f, _ = model(layers).extract_features(x)
+        torch.cuda.synchronize()
+    # fp32 products, fp32 sums in another order: the reference's own arithmetic
+    assert rel(f, small[f"feat_r{layers}_S33"]) < 1e-5
+
+
+def test_extract_features_exact_fp32_full_vs_oracle(dev):
+    from oracle import cwt_oracle as O
+    ep = syn.make_episode(SEED, 0, 473, 1)
+    x = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]]))
+    with exact_fp32():
+        f, _ = model(50).extract_features(x.to(dev))
+        torch.cuda.synchronize()
+    ref = O.extract_features(x, O.to_torch_state(syn.make_pspnet_state(50, SEED)))
+    assert rel(f, ref) < 1e-5
+
+
 def test_extract_batch_independent(dev):
     # batching support + query in one pass must equal separate passes (eval-mode BN)
     ep = syn.make_episode(SEED, 3, 129, 2)
@@ -263,6 +299,34 @@ def test_episode_vs_reference(dev, golden_dir, name, layers, S, shot, n_ep):
         for key in ("pred_q", "pred_q0"):
             _, hard = flip_report(r[key][0], g[f"e{e}_{key}"], S, f"{name}:e{e}:{key}")
             assert hard == 0
+
+
+@pytest.mark.parametrize("name,layers,S,shot", [
+    ("episode_pascal_r50_1shot.npz", 50, 473, 1),
+    ("episode_coco_r101_1shot.npz", 101, 641, 1),
+])
+def test_episode_exact_fp32_vs_reference(dev, golden_dir, name, layers, S, shot):
+    """The exact-fp32 conv stack (bench.py's exact_fp32 leg) against the reference's episode
+    fixture: W, W', logits and IoU counts; no argmax flip above the margin."""
+    from few_shot_seg_cwt_amd.episode import EpisodeEngine
+    g = dict(np.load(os.path.join(golden_dir, name)))
+    cfg = syn.cfg_defaults(layers=layers, image_size=S, shot=shot)
+    eng = EpisodeEngine(model(layers), transformer(4), cfg)
+    classes = syn.coco_val_classes(0) if layers == 101 else None
+    ep = syn.make_episode(SEED, 0, S, shot, classes)
+    imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
+    W0 = torch.from_numpy(g["e0_W0"]).to(dev).contiguous()
+    with exact_fp32():
+        r = eng.run(imgs, torch.from_numpy(ep["s_label"][0]).to(dev), torch.from_numpy(ep["q_label"]).to(dev), W0)
+        torch.cuda.synchronize()
+    assert rel(r["W"], g["e0_W"]) < TOL
+    assert rel(r["W2"][0], g["e0_W2"]) < TOL
+    assert rel(r["pred_q"][0], g["e0_pred_q"]) < TOL
+    low = _low_margin(g["e0_pred_q"], S)
+    iu = r["iut"][0].cpu().numpy()
+    assert np.abs(iu - g["e0_iu"]).max() <= low
+    _, hard = flip_report(r["pred_q"][0], g["e0_pred_q"], S, f"{name}:exact_fp32")
+    assert hard == 0
 
 
 def test_validate_transformer_vs_reference(dev, golden_dir):

@@ -106,3 +106,51 @@ def test_fold_follows_parameter_changes(dev):
     t2 = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
     t2.load_state_dict(syn.make_transformer_state(4, 512, SEED + 2))
     assert rel(cwt_tail(t2, W, f)[0], _modules(t2, W, f)[0]) < TOL
+
+
+# ---------------------------------------------------------------- the one-launch tail
+def _labels(B, S, tag, p_ignore=0.05):
+    lab = (syn.uniform01(9, "tl" + tag, B * S * S) < 0.3).astype(np.int64).reshape(B, S, S)
+    lab[syn.uniform01(10, "ti" + tag, B * S * S).reshape(B, S, S) < p_ignore] = 255
+    return torch.from_numpy(lab)
+
+
+@pytest.mark.parametrize("B,h", [(1, 60), (1, 81), (2, 60), (4, 33), (3, 9), (1, 2), (2, 17)])
+def test_episode_tail_one_launch_equals_modules(dev, B, h):
+    """cwt_episode_tail (one launch, in-kernel grid barriers) against the module kernels it
+    replaces: cwt_attention_infer + cwt_classify_scaled + cwt_seg_metrics_pair (W', pred_q,
+    pred_q0 at fp32 rounding; integer counts equal except on pixels whose two upsampled logits
+    are within rounding of each other; the CE sums to double rounding)."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne
+    from few_shot_seg_cwt_amd.episode import cwt_tail, episode_tail
+    from few_shot_seg_cwt_amd.util import seg_metrics_pair
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    t.eval()
+    S = 8 * (h - 1) + 1
+    f, W = _inputs(dev, B, h, f"1l{B}_{h}")
+    ql = _labels(B, S, f"{B}_{h}").to(dev)
+    for rep in range(2):   # the second launch runs on the counters the first advanced
+        W2, pq, pq0, iut, ce, iut0 = episode_tail(t, W, f, ql)
+        W2r, pqr, pq0r = cwt_tail(t, W, f)
+        iutr, cer, iut0r = seg_metrics_pair(pqr, pq0r, ql)
+        torch.cuda.synchronize()
+        errs = dict(W2=rel(W2, W2r), pred_q=rel(pq, pqr), pred_q0=rel(pq0, pq0r))
+        print(f"one-launch tail B={B} h={h} rep={rep}: {errs}")
+        assert max(errs.values()) < TOL, errs
+        # pq / pqr differ at fp32 rounding: a pixel whose two upsampled logits tie within it may flip
+        assert float((iut - iutr).abs().max()) <= 2 and float((iut0 - iut0r).abs().max()) <= 2
+        assert float(ce[:, 1].sub(cer[:, 1]).abs().max()) == 0.0           # valid-pixel counts
+        assert float(((ce[:, 0] - cer[:, 0]).abs() / cer[:, 0].abs().clamp_min(1e-30)).max()) < 1e-5
+
+
+def test_episode_tail_status_clean(dev):
+    """No grid-barrier timeout on a normal launch (the context's status word stays clear)."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib
+    from few_shot_seg_cwt_amd.episode import episode_tail
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    f, W = _inputs(dev, 1, 60, "st")
+    episode_tail(t, W, f, _labels(1, 473, "st").to(dev))
+    torch.cuda.synchronize()
+    _lib.check_status()

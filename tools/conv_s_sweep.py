@@ -81,6 +81,9 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         if prec == 1:   # plain bf16 operands (K order inside a row does not matter for timing)
             xs = x.to(torch.bfloat16).contiguous()
             ws = w.reshape(Co, K).to(torch.bfloat16).contiguous()
+        elif prec == 0:  # exact fp32 (conv_igemm_f32d): fp32 NHWC and fp32 [Co][K] weights
+            xs = x
+            ws = w.reshape(Co, K).contiguous()
         else:
             xs = torch.empty(n_img * Hi * Hi * Ci * 2, dtype=torch.bfloat16, device=dev)
             ws = torch.empty(Co * K * 2, dtype=torch.bfloat16, device=dev)
@@ -90,7 +93,9 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         sh = torch.zeros(Co, device=dev)
         r = torch.randn(n_img, Ho, Ho, Co, device=dev) if has_res else None
         rs = None
-        if has_res and prec == 1:
+        if has_res and prec == 0:
+            rs = None
+        elif has_res and prec == 1:
             rs = r.to(torch.bfloat16).contiguous()
         elif has_res:
             rs = torch.empty(M * Co * 2, dtype=torch.bfloat16, device=dev)
@@ -102,6 +107,10 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         conv_fn = lib.cwt_debug_conv_b16 if prec == 1 else lib.cwt_debug_conv_s
 
         def new(bm, bn, ns):
+            if prec == 0:
+                return lambda: _lib.check(lib.cwt_debug_conv_f32d(
+                    ctx, _lib.ptr(xs), n_img, Hi, Hi, Ci, _lib.ptr(ws), _lib.ptr(sc), _lib.ptr(sh), Co, k, stride,
+                    pad, dil, _lib.ptr(r), Co, 1, _lib.ptr(y), Co, 0, bm, bn, ns, sp))
             return lambda: _lib.check(conv_fn(
                 ctx, _lib.ptr(xs), n_img, Hi, Hi, Ci, _lib.ptr(ws), _lib.ptr(sc), _lib.ptr(sh), Co, k, stride, pad,
                 dil, None, Co, _lib.ptr(rs), 1, None, Co, 0, _lib.ptr(ys), bm, bn, ns, sp))
@@ -151,7 +160,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--quick", action="store_true", help="old vs new automatic plan only")
     ap.add_argument("--out", default="conv_s_sweep.json")
-    ap.add_argument("--prec", type=int, default=3, choices=[1, 3], help="3 = bf16x3 (x3s), 1 = plain bf16 (b16)")
+    ap.add_argument("--prec", type=int, default=3, choices=[0, 1, 3],
+                    help="3 = bf16x3 (x3s), 1 = plain bf16 (b16), 0 = exact fp32 on the LDS-DMA body (f32d)")
     ap.add_argument("--vars", default="0,1,2,4", help="main-loop variants (0 base, 1 prefetch, 2 prefetch 8 waves, 4 128x128 two per CU; 8-11 timing study)")
     ap.add_argument("--only", default="", help="comma list of shape names (default: all)")
     args = ap.parse_args()
