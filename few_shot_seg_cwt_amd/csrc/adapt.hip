@@ -854,13 +854,16 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
   constexpr int C = 512;
   constexpr int EWK = (NRES >= 2) ? 2 : NRES == 1 ? 1 : PA_EW;  // episodes a workgroup's units may span
   constexpr bool LOCK = NRES == 2 || NRES == 4;  // units in lockstep, the second one's f in fl2
+  // NRES 5: two units in lockstep, both in registers (the second one in cur2, as NRES 4's third):
+  // no LDS reads of f in the z and dW passes
+  constexpr bool BREG = NRES == 5;
   __shared__ float fl2[LOCK ? PA_NW : 1][PA_CPW][LOCK ? 64 : 1];
   __shared__ __attribute__((aligned(16))) float fs3[NRES == 3 ? PA_NW * 64 * PA_CPW : 4];  // NRES 3: per-wave f slices
   __shared__ float dlw[PA_NW][EWK][PA_CPW];     // d = W1 - W0 of each wave's channels (wave-private)
   __shared__ float wlw[PA_NW][EWK][2][PA_CPW];  // W0, W1 of each wave's channels (wave-private)
   // NRES 2 runs its two units in lockstep (one set of LDS barriers, one butterfly and one set
   // of atomics per step when both units belong to one episode): the second unit's copies [1]
-  constexpr int NU = NRES == 2 ? 2 : NRES == 4 ? 3 : 1;
+  constexpr int NU = (NRES == 2 || NRES == 5) ? 2 : NRES == 4 ? 3 : 1;
   __shared__ std::conditional_t<NRES == 4, PaScrAlias<NU>, PaScrSep<NU>> scr;
   auto& zpart_u = scr.zpart;
   auto& P0_u = scr.P0;
@@ -924,7 +927,17 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
 #pragma unroll
     for (int j = 0; j < PA_CPW; ++j) fl2[wv][j][lane] = 0.f;
   }
-  PaTile cur2;  // NRES 4: the third unit (registers); zero when the workgroup has fewer
+  PaTile cur2;  // NRES 4: the third unit (registers); NRES 5: the second; zero when the workgroup has fewer
+  if (BREG) {
+    if (u1 - u0 > 1) {
+      pa_load(cur2, a, pa_unit(a, u0 + 1), wv, lane);
+    } else {
+#pragma unroll
+      for (int j = 0; j < PA_CPW; ++j) cur2.fr[j] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) cur2.y[k][0] = cur2.y[k][1] = 255;
+    }
+  }
   if (NRES == 4) {
     if (u1 - u0 > 2) {
       pa_load(cur2, a, pa_unit(a, u0 + 2), wv, lane);
@@ -948,7 +961,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
   }
   // NRES 4: the three units' labels one byte each (unit A's f stays in cur.fr)
   const unsigned yap = pack_y(cur.y), ycp = pack_y(cur2.y);
-  const unsigned y2p = pack_y(y2);
+  const unsigned y2p = BREG ? ycp : pack_y(y2);
   __syncthreads();
 
   const int i_row = wv >> 1;
@@ -1159,13 +1172,13 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
           const f32x4 db = *(const f32x4*)&dlw[wv][ewb][4 * j];
           float fb[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) fb[r] = fl2[wv][4 * j + r][lane];
+          for (int r = 0; r < 4; ++r) fb[r] = BREG ? cur2.fr[4 * j + r] : fl2[wv][4 * j + r][lane];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             sda = fmaf(da[r], cur.fr[4 * j + r], sda);
             sdb = fmaf(db[r], fb[r], sdb);
           }
-          if (j & 1) asm volatile("" ::: "memory");  // at most 8 of unit B's LDS reads in flight (registers)
+          if (!BREG && (j & 1)) asm volatile("" ::: "memory");  // at most 8 of unit B's LDS reads in flight (registers)
         }
         zpart_u[0][wv][lane] = sda;
         zpart_u[NU - 1][wv][lane] = sdb;
@@ -1189,7 +1202,22 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       }
       lds_barrier();
       stamp(2);
-      {
+      if constexpr (BREG) {
+        // both units in registers: each episode's dW formed on the fly inside the butterfly
+        // (channels j and j + 16 together, at most 16 values live beside the two units' f)
+        const float ga = gs_u[0][lane], gb = has_b ? gs_u[NU - 1][lane] : 0.f;
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+          const int e = pass ? qb.e : qa.e;
+          if (pass && qb.e == qa.e) break;
+          const float ma = qa.e == e ? ga : 0.f, mb = qb.e == e ? gb : 0.f;
+          const float dsum = pa_butterfly_fn([&](int j) { return fmaf(mb, cur2.fr[j], ma * cur.fr[j]); }, lane);
+          if ((lane & 1) == 0)
+            __hip_atomic_fetch_add(a.acc + (long)e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C + wv * PA_CPW +
+                                       (lane >> 1),
+                                   dsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
         float accd[PA_CPW];
         const float ga = gs_u[0][lane], gb = has_b ? gs_u[NU - 1][lane] : 0.f;
         if (qa.e == qb.e) {  // one butterfly and one set of atomics for both units
@@ -1199,10 +1227,10 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
           for (int j0 = 0; j0 < PA_CPW; j0 += 8) {
             float fb[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) fb[k] = fl2[wv][j0 + k][lane];
+            for (int k = 0; k < 8; ++k) fb[k] = BREG ? cur2.fr[j0 + k] : fl2[wv][j0 + k][lane];
 #pragma unroll
             for (int k = 0; k < 8; ++k) accd[j0 + k] = fmaf(gb, fb[k], accd[j0 + k]);
-            asm volatile("" ::: "memory");
+            if (!BREG) asm volatile("" ::: "memory");
           }
           pa_butterfly(accd, lane);
           if ((lane & 1) == 0)
@@ -1214,7 +1242,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
           for (int uu = 0; uu < 2; ++uu) {
             const PaUnit& q = uu ? qb : qa;
 #pragma unroll
-            for (int j = 0; j < PA_CPW; ++j) accd[j] = uu ? gb * fl2[wv][j][lane] : ga * cur.fr[j];
+            for (int j = 0; j < PA_CPW; ++j) accd[j] = uu ? gb * (BREG ? cur2.fr[j] : fl2[wv][j][lane]) : ga * cur.fr[j];
             pa_butterfly(accd, lane);
             if ((lane & 1) == 0)
               __hip_atomic_fetch_add(a.acc + (long)q.e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
@@ -1293,7 +1321,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       if (NRES == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if constexpr (NRES == 4) {
       triple_body(u1 - u0);
-    } else if constexpr (NRES == 2) {
+    } else if constexpr (NRES == 2 || NRES == 5) {
       const bool has_b = u1 - u0 == 2;
       pair_body(q, has_b ? pa_unit(a, u0 + 1) : q, has_b);
     } else
@@ -1469,7 +1497,10 @@ static int persist_geometry(int E, int n, int h, int w, int upw_pref, int* G_out
   // registers and one in LDS (nres 4); CWT_ADAPT_LOCK3=0 returns it to the step launches
   const char* l3s = getenv("CWT_ADAPT_LOCK3");
   const bool lock3 = !(l3s && l3s[0] == '0');
-  int nres = k == 1 ? 1 : (k == 2 && span <= 2) ? 2 : (k == 3 && span <= 2 && lock3) ? 4 : 0;
+  // k = 2: both units in registers (nres 5) unless CWT_ADAPT_BREG=0 (the second unit's f in LDS, nres 2)
+  const char* brs = getenv("CWT_ADAPT_BREG");
+  const bool breg = !(brs && brs[0] == '0');
+  int nres = k == 1 ? 1 : (k == 2 && span <= 2) ? (breg ? 5 : 2) : (k == 3 && span <= 2 && lock3) ? 4 : 0;
   if (nres == 0 && k >= stream_from && span <= 2) nres = 3;
   if (span > (nres >= 2 ? 2 : PA_EW)) return 1;
   // three units per workgroup: as few workgroups as that takes (5-shot 473^2: 197, not 256 with
@@ -1540,6 +1571,7 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
     default: CWT_PA_LAUNCH(NR, 0); break;    \
   }
   switch (nres) {
+    case 5: CWT_PA_MODES(5); break;
     case 4: CWT_PA_MODES(4); break;
     case 3: CWT_PA_MODES(3); break;
     case 2: CWT_PA_MODES(2); break;
@@ -1574,9 +1606,9 @@ const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw) {
   int pG = 0, punits = 0, pncb = 0, pnres = 0, puc = 0;
   const char* pe = getenv("CWT_ADAPT_PERSIST");
   if (iters > 0 && !(pe && pe[0] == '0') && persist_geometry(E, n, h, w, upw, &pG, &punits, &pncb, &pnres, &puc) == 0) {
-    static const char* names[5] = {"adapt_persist_kernel<0", "adapt_persist_kernel<1", "adapt_persist_kernel<2",
-                                   "adapt_persist_kernel<3", "adapt_persist_kernel<4"};
-    return names[pnres <= 4 ? pnres : 0];
+    static const char* names[6] = {"adapt_persist_kernel<0", "adapt_persist_kernel<1", "adapt_persist_kernel<2",
+                                   "adapt_persist_kernel<3", "adapt_persist_kernel<4", "adapt_persist_kernel<5"};
+    return names[pnres <= 5 ? pnres : 0];
   }
   return "adapt_step_kernel<";
 }

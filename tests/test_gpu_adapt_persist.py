@@ -29,10 +29,15 @@ def dev():
 
 def _run(persist, f, lbl, W0, iters, uc=None, upw=None, stream=None):
     """persist: "0" per-step launches, "2" the persistent loop also where units are streamed;
-    upw: units per workgroup ("1": f in registers; "2", the default: the second unit in LDS);
+    upw: units per workgroup ("1": f in registers; "2": two units in lockstep, both in registers
+    (adapt_persist_kernel<5>); "2lds": the same with the second unit's f in LDS (<2>));
     stream: "1" the LDS-streamed form from 3 units per workgroup, "0" never."""
     from few_shot_seg_cwt_amd.episode import inner_adapt_batch
-    env = {"CWT_ADAPT_PERSIST": persist, "CWT_ADAPT_UC": uc, "CWT_ADAPT_UPW": upw, "CWT_ADAPT_STREAM": stream}
+    breg = None
+    if upw == "2lds":
+        upw, breg = "2", "0"
+    env = {"CWT_ADAPT_PERSIST": persist, "CWT_ADAPT_UC": uc, "CWT_ADAPT_UPW": upw, "CWT_ADAPT_STREAM": stream,
+           "CWT_ADAPT_BREG": breg}
     old = {k: os.environ.get(k) for k in env}
     for k, v in env.items():
         if v is None:
@@ -63,7 +68,7 @@ def _run(persist, f, lbl, W0, iters, uc=None, upw=None, stream=None):
     (3, 2, 65, 20, None),
     (2, 1, 33, 5, None),
 ])
-@pytest.mark.parametrize("upw", ["1", "2"])
+@pytest.mark.parametrize("upw", ["1", "2", "2lds"])
 def test_persist_equals_step_launches(dev, E, n, S, iters, uc, upw):
     h = (S - 1) // 8 + 1
     f = torch.from_numpy(syn.normal(5, f"fp{E}{n}{S}", (E * n, 512, h, h), 0.1)).to(dev)

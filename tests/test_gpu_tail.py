@@ -154,3 +154,31 @@ def test_episode_tail_status_clean(dev):
     episode_tail(t, W, f, _labels(1, 473, "st").to(dev))
     torch.cuda.synchronize()
     _lib.check_status()
+
+
+def test_episode_tail_barrier_timeout_is_raised(dev):
+    """A tail whose grid barrier gives up (spin bound 1 through cwt_debug_adapt_spin_limit) drains
+    its grid, reports CWT_STATUS_TAIL_BARRIER and the host raises CwtError at its next check; the
+    check re-arms the context (its counters are re-zeroed before the next tail), after which the
+    same call is clean and equals the module kernels."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib
+    from few_shot_seg_cwt_amd.episode import cwt_tail, episode_tail
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    f, W = _inputs(dev, 1, 60, "to")
+    ql = _labels(1, 473, "to").to(dev)
+    _lib.check_status()
+    c = _lib.ctx(dev.index)
+    _lib.check(_lib.lib().cwt_debug_adapt_spin_limit(c, 1), "spin limit")
+    try:
+        episode_tail(t, W, f, ql)
+        torch.cuda.synchronize()
+        with pytest.raises(_lib.CwtError, match="episode tail's grid barrier timed out"):
+            _lib.check_status()
+    finally:
+        _lib.check(_lib.lib().cwt_debug_adapt_spin_limit(c, 0), "spin limit")
+    W2, pq, pq0, iut, ce, iut0 = episode_tail(t, W, f, ql)
+    torch.cuda.synchronize()
+    _lib.check_status()
+    W2r, pqr, _ = cwt_tail(t, W, f)
+    assert rel(W2, W2r) < TOL and rel(pq, pqr) < TOL
