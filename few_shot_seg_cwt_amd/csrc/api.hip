@@ -53,7 +53,8 @@ unsigned episode_tail_max_epoch(int G);
 int launch_episode_tail(const float* q, const float* f, int B, int hw, int h, int w, int S, const int64_t* target,
                         const float* fold, const float* fc_b, const float* ln_w, const float* ln_b, float* out,
                         float* logits, float* logits0, float* iut, double* ce, float* iut0, float* ws,
-                        unsigned* cnt, unsigned epoch, int G, long spin_limit, unsigned* status, hipStream_t st);
+                        unsigned* cnt, unsigned epoch, int G, long spin_limit, unsigned* status, hipStream_t st,
+                        unsigned long long* stamps);
 int attention_infer(const float* q, const float* f, int B, int hw, int C, int H, const float* fold, const float* fc_b,
                     const float* ln_w, const float* ln_b, float* out, float* inv_norm, float* logits0, float* ws,
                     hipStream_t st);
@@ -187,6 +188,7 @@ struct cwt_ctx {
   // cwt_episode_tail's counters: this context's next launch number on them; ~0u = re-zero first
   unsigned tail_epoch = ~0u;
   int tail_G = 0;
+  int tail_stamp_G = 0;  // workgroups of the last stamped tail launch (CWT_TAIL_STAMPS)
   // folded CWT weights of cwt_attention_infer (M_h = W_h^T W_h, P = [fc_h W_h]) and the
   // parameter identity they were folded from (buffers + the caller's version counter)
   const float* fold_w = nullptr;
@@ -1256,10 +1258,15 @@ int cwt_episode_tail(cwt_ctx* ctx, const float* q, const float* f, int B, int h,
     ctx->tail_epoch = 0;
     ctx->tail_G = G;
   }
+  void* stamps = nullptr;  // timing study (CWT_TAIL_STAMPS=1): per-workgroup phase stamps (cwt_debug_tail_stamps)
+  if (getenv("CWT_TAIL_STAMPS") && getenv("CWT_TAIL_STAMPS")[0] == '1' &&
+      (rc = ensure_ws(ctx, "tail.stamps", (size_t)G * 16 * 8, &stamps)))
+    return rc;
+  ctx->tail_stamp_G = stamps ? G : 0;
   if (pk.ev0()) CWT_HIP(hipEventRecord(pk.ev0(), st));
   rc = launch_episode_tail(q, f, B, hw, h, w, S, q_label, (const float*)fold, fc_b, ln_w, ln_b, out, logits, logits0,
                            iut, ce, iut0, (float*)ws, (unsigned*)cnt, ctx->tail_epoch++, G, ctx->adapt_spin_limit,
-                           ctx->status_dev, st);
+                           ctx->status_dev, st, (unsigned long long*)stamps);
   if (pk.ev1()) CWT_HIP(hipEventRecord(pk.ev1(), st));
   p.end();
   return rc;
@@ -1852,6 +1859,18 @@ int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int 
                        int nsplit, void* stream) {
   return debug_conv_s(ctx, 1, xs, N, Hi, Wi, Ci, ws, scale, shift, Co, k, stride, pad, dil, res, res_ld, res_s, relu, y,
                       y_ld, y_off, ys, bm, bn, nsplit, stream);
+}
+
+int cwt_debug_tail_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t max_count, int64_t* count) {
+  if (!ctx || !count) return fail(CWT_EARG, "null argument");
+  CWT_HIP(hipSetDevice(ctx->device));
+  auto it = ctx->ws.find("tail.stamps");
+  *count = (it == ctx->ws.end() || !ctx->tail_stamp_G) ? 0 : (int64_t)ctx->tail_stamp_G * 16;
+  if (host_out && *count > 0 && max_count > 0) {
+    CWT_HIP(hipDeviceSynchronize());
+    CWT_HIP(hipMemcpy(host_out, it->second.p, (size_t)std::min<int64_t>(max_count, *count) * 8, hipMemcpyDeviceToHost));
+  }
+  return 0;
 }
 
 int cwt_debug_adapt_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t max_count, int64_t* count) {

@@ -212,76 +212,79 @@ __global__ __launch_bounds__(256) void cp4d_layer_kernel(const float* __restrict
 
 // ---- the same layer on the f32 matrix cores (COUT = 10) and a register-blocked VALU form for
 // COUT = 1 (round 4; the scalar kernel above measured 16 % of the fp32 VALU peak at 60^2: bound
-// by its broadcast LDS weight reads, one per two FMAs) ----
+// by its broadcast LDS weight reads, one per two FMAs, and by 4-B staging loads) ----
 // Tile: a 4 x 4 patch of a positions by a 4 x 4 patch of b positions (256 pairs); staged in LDS
 // as the a halo box (6 x 6) at the tile's 16 b positions and the tile's 16 a positions at the b
-// halo box, channels padded to CP (zeros) and positions PS floats apart.
+// halo box, CIN floats per position (dense; 2 floats of padding at the end).
 constexpr int CM_T = 4, CM_H = CM_T + 2, CM_NH = CM_H * CM_H, CM_NT = CM_T * CM_T;  // 6 x 6 halo, 16 tile
+template <int CIN>
+struct CmLds {
+  static constexpr int EA = CM_NH * CM_NT * CIN, EB = CM_NT * CM_NH * CIN;  // floats
+};
 
-template <int CIN, int CP, int PS>
+// xa[ah][bt][c]: a halo position ah (6 x 6 around the a tile), tile b position bt; xb[at][bh][c]:
+// tile a position at, b halo position bh.  CIN even: 8-B loads (a position is CIN / 2 of them,
+// 8-B aligned); every load of the thread is issued before the first LDS store; positions off the
+// map read 0.
+template <int CIN>
 __device__ __forceinline__ void cm_stage(const float* __restrict__ x, int hA, int wA, int hB, int wB, int ha0, int wa0,
                                          int hb0, int wb0, long xoff, float* xa, float* xb) {
-  // xa[ah][bt][c]: a halo position ah (6 x 6 around the a tile), tile b position bt;
-  // xb[at][bh][c]: tile a position at, b halo position bh.  Every load of the thread is issued
-  // before the first LDS store; channels >= CIN and positions off the map read 0.
   const int NB = hB * wB;
-  constexpr int EA = CM_NH * CM_NT * CP, EB = CM_NT * CM_NH * CP;
-  constexpr int IA = (EA + 255) / 256, IB = (EB + 255) / 256;
+  constexpr int V = (CIN % 2 == 0) ? 2 : 1;  // floats per load
+  constexpr int VP = CIN / V;                // loads per position
+  constexpr int LA = CM_NH * CM_NT * VP, LB = CM_NT * CM_NH * VP;
+  constexpr int IA = (LA + 255) / 256, IB = (LB + 255) / 256;
+  typedef float vec_t __attribute__((ext_vector_type(V)));
   const int t = threadIdx.x;
-  float ra[IA], rb[IB];
+  vec_t ra[IA], rb[IB];
 #pragma unroll
   for (int k = 0; k < IA; ++k) {
     const int i = t + 256 * k;
-    const int c = i % CP, p = i / CP;
+    const int q = i % VP, p = i / VP;
     const int bt = p % CM_NT, ah = p / CM_NT;
     const int ha = ha0 - 1 + ah / CM_H, wa = wa0 - 1 + ah % CM_H;
     const int hb = hb0 + bt / CM_T, wb = wb0 + bt % CM_T;
-    const bool in = i < EA && c < CIN && (unsigned)ha < (unsigned)hA && (unsigned)wa < (unsigned)wA && hb < hB &&
-                    wb < wB;
-    ra[k] = in ? x[xoff + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + c] : 0.f;
+    const bool in = i < LA && (unsigned)ha < (unsigned)hA && (unsigned)wa < (unsigned)wA && hb < hB && wb < wB;
+    ra[k] = in ? *(const vec_t*)(x + xoff + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + q * V) : vec_t(0.f);
   }
 #pragma unroll
   for (int k = 0; k < IB; ++k) {
     const int i = t + 256 * k;
-    const int c = i % CP, p = i / CP;
+    const int q = i % VP, p = i / VP;
     const int bh = p % CM_NH, at = p / CM_NH;
     const int ha = ha0 + at / CM_T, wa = wa0 + at % CM_T;
     const int hb = hb0 - 1 + bh / CM_H, wb = wb0 - 1 + bh % CM_H;
-    const bool in = i < EB && c < CIN && ha < hA && wa < wA && (unsigned)hb < (unsigned)hB && (unsigned)wb < (unsigned)wB;
-    rb[k] = in ? x[xoff + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + c] : 0.f;
+    const bool in = i < LB && ha < hA && wa < wA && (unsigned)hb < (unsigned)hB && (unsigned)wb < (unsigned)wB;
+    rb[k] = in ? *(const vec_t*)(x + xoff + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + q * V) : vec_t(0.f);
   }
 #pragma unroll
   for (int k = 0; k < IA; ++k) {
     const int i = t + 256 * k;
-    if (i < EA) xa[(i / CP) * PS + i % CP] = ra[k];
+    if (i < LA) *(vec_t*)(xa + i * V) = ra[k];
   }
 #pragma unroll
   for (int k = 0; k < IB; ++k) {
     const int i = t + 256 * k;
-    if (i < EB) xb[(i / CP) * PS + i % CP] = rb[k];
+    if (i < LB) *(vec_t*)(xb + i * V) = rb[k];
   }
 }
 
 // COUT = 10 on v_mfma_f32_16x16x4_f32 (fp32 products, fp32 sums: an fmaf chain per output).
 // Output rows of one MFMA group: the 16 tile b positions of ONE tile a position (group G = the a
-// position); columns: the 10 output channels (16 wide, 6 unused).  K = (tap, channel): for CIN >=
-// 4 channels padded to CP = 4 k (zeros) so MFMA m covers tap m / (CP/4) and channels
-// 4 (m % (CP/4)) + lane/16 -- an LDS address of lane base + immediate; for CIN = 1, 2 the 9 CIN
-// (tap, channel) rows are dense.  Both 2-D convolutions (a plane, b plane) accumulate into the
-// same accumulators.  4 waves x 4 groups = the tile's 256 pairs.
+// position); columns: the 10 output channels (16 wide, 6 unused).  K = (tap, channel) dense,
+// 9 CIN rows padded to a multiple of 4 (zero weights): MFMA m, lane group g = lane / 16 takes
+// k = 4 m + g, read at the lane's per-k LDS offset.  Both 2-D convolutions (a plane, b plane)
+// accumulate into the same accumulators.  4 waves x 4 groups = the tile's 256 pairs.
 template <int CIN>
 __global__ __launch_bounds__(256) void cp4d_mfma_kernel(const float* __restrict__ x, int hA, int wA, int hB, int wB,
                                                         const float* __restrict__ Wa, const float* __restrict__ ba,
                                                         const float* __restrict__ Wb, const float* __restrict__ bb,
                                                         float* __restrict__ y) {
   constexpr int COUT = 10;
-  constexpr bool PADC = CIN >= 4;
-  constexpr int CP = PADC ? (CIN + 3) / 4 * 4 : CIN;
-  constexpr int PS = CP | 1;                 // odd position stride (fewer bank collisions)
-  constexpr int KT = 9 * CP;                 // K rows per branch
-  constexpr int NM = (KT + 3) / 4;           // MFMAs per branch and group
-  __shared__ float xa[CM_NH * CM_NT * PS];
-  __shared__ float xb[CM_NT * CM_NH * PS];
+  constexpr int KT = 9 * CIN;        // K rows per branch
+  constexpr int NM = (KT + 3) / 4;   // MFMAs per branch and group
+  __shared__ __attribute__((aligned(16))) float xa[CmLds<CIN>::EA + 2];
+  __shared__ __attribute__((aligned(16))) float xb[CmLds<CIN>::EB + 2];
   const int NA = hA * wA, NB = hB * wB;
   const int ntb = (wB + CM_T - 1) / CM_T, nta = (wA + CM_T - 1) / CM_T;
   const int ta = blockIdx.y, tb = blockIdx.x;
@@ -290,57 +293,42 @@ __global__ __launch_bounds__(256) void cp4d_mfma_kernel(const float* __restrict_
   const long xoff = (long)blockIdx.z * NA * NB * CIN;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int r = lane & 15, g4 = lane >> 4;
-  // this lane's weights (B operand: column r = output channel, k = 4 m + g4), both branches
+  cm_stage<CIN>(x, hA, wA, hB, wB, ha0, wa0, hb0, wb0, xoff, xa, xb);
+  // this lane's weights (B operand: column r = output channel, k = 4 m + g4) and the LDS offsets
+  // of its k's (tap, channel) in the two staged boxes
   float wra[NM], wrb[NM];
+  int offa[NM], offb[NM];
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
-    int tap, c;
-    bool kin;
-    if (PADC) {
-      tap = m / (CP / 4);
-      c = 4 * (m % (CP / 4)) + g4;
-      kin = c < CIN;
-    } else {
-      const int k = 4 * m + g4;
-      kin = k < 9 * CIN;
-      tap = kin ? k / CIN : 0;
-      c = kin ? k % CIN : 0;
-    }
+    const int k = 4 * m + g4;
+    const bool kin = k < KT;
+    const int tap = kin ? k / CIN : 0, c = kin ? k % CIN : 0;
+    const int ky = tap / 3, kx = tap - 3 * (tap / 3);
     const bool live = kin && r < COUT;
     wra[m] = live ? Wa[(r * CIN + c) * 9 + tap] : 0.f;
     wrb[m] = live ? Wb[(r * CIN + c) * 9 + tap] : 0.f;
+    offa[m] = (ky * CM_H + kx) * CM_NT * CIN + c;
+    offb[m] = (ky * CM_H + kx) * CIN + c;
   }
-  cm_stage<CIN, CP, PS>(x, hA, wA, hB, wB, ha0, wa0, hb0, wb0, xoff, xa, xb);
+  // row r of group G: a tile position G (ay, ax), b tile position r (by, bx)
+  const int by = r / CM_T, bx = r % CM_T;
+  const int base_b = (by * CM_H + bx) * CIN;
   __syncthreads();
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // row r of group G: a tile position G (ay, ax), b tile position r (by, bx)
-  const int by = r / CM_T, bx = r % CM_T;
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
-    int tap, c;
-    if (PADC) {
-      tap = m / (CP / 4);
-      c = 4 * (m % (CP / 4)) + g4;
-    } else {
-      const int k = 4 * m + g4;
-      tap = k < 9 * CIN ? k / CIN : 0;
-      c = k < 9 * CIN ? k % CIN : 0;
-    }
-    const int ky = tap / 3, kx = tap - 3 * (tap / 3);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int G = wv * 4 + j, ay = G / CM_T, ax = G % CM_T;
-      // a branch: a halo position (ay + ky, ax + kx), tile b position r
-      const float va = xa[(((ay + ky) * CM_H + ax + kx) * CM_NT + r) * PS + c];
+      const float va = xa[((ay * CM_H + ax) * CM_NT + r) * CIN + offa[m]];
       acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va, wra[m], acc[j], 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int G = wv * 4 + j;
-      // b branch: tile a position G, b halo position (by + ky, bx + kx)
-      const float vb = xb[(G * CM_NH + (by + ky) * CM_H + bx + kx) * PS + c];
+      const float vb = xb[G * CM_NH * CIN + base_b + offb[m]];
       acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vb, wrb[m], acc[j], 0, 0, 0);
     }
   }
@@ -365,17 +353,17 @@ __global__ __launch_bounds__(256) void cp4d_mfma_kernel(const float* __restrict_
 }
 
 // COUT = 1 (the consensus stack's last layer, CIN = 10): a thread per (a, b) pair of the same
-// staged tile, channels padded to 12 and read 4 at a time (ds_read_b128), the 2 x 9 x 12 weights
-// in LDS read as wave-uniform broadcasts, 4 independent partial sums per thread.
+// staged tile, its channels read 2 at a time (ds_read_b64), the 2 x 9 x CIN weights in LDS read
+// as wave-uniform broadcasts, two independent partial sums per thread.
 template <int CIN>
 __global__ __launch_bounds__(256) void cp4d_c1_kernel(const float* __restrict__ x, int hA, int wA, int hB, int wB,
                                                       const float* __restrict__ Wa, const float* __restrict__ ba,
                                                       const float* __restrict__ Wb, const float* __restrict__ bb,
                                                       float* __restrict__ y) {
-  constexpr int CP = (CIN + 3) / 4 * 4, PS = CP;
-  __shared__ __attribute__((aligned(16))) float xa[CM_NH * CM_NT * PS];
-  __shared__ __attribute__((aligned(16))) float xb[CM_NT * CM_NH * PS];
-  __shared__ __attribute__((aligned(16))) float wl[2][9][CP];
+  static_assert(CIN % 2 == 0, "pairs of channels");
+  __shared__ __attribute__((aligned(16))) float xa[CmLds<CIN>::EA + 2];
+  __shared__ __attribute__((aligned(16))) float xb[CmLds<CIN>::EB + 2];
+  __shared__ __attribute__((aligned(16))) float wl[2][9][CIN];
   const int NA = hA * wA, NB = hB * wB;
   const int ntb = (wB + CM_T - 1) / CM_T, nta = (wA + CM_T - 1) / CM_T;
   const int ta = blockIdx.y, tb = blockIdx.x;
@@ -383,35 +371,34 @@ __global__ __launch_bounds__(256) void cp4d_c1_kernel(const float* __restrict__ 
   const int hb0 = (tb / ntb) * CM_T, wb0 = (tb % ntb) * CM_T;
   const long xoff = (long)blockIdx.z * NA * NB * CIN;
   const int t = threadIdx.x;
-  if (t < 2 * 9 * CP) {
-    const int c = t % CP, tap = (t / CP) % 9, side = t / (9 * CP);
-    (&wl[0][0][0])[t] = c < CIN ? (side ? Wb : Wa)[c * 9 + tap] : 0.f;
+  if (t < 2 * 9 * CIN) {
+    const int c = t % CIN, tap = (t / CIN) % 9, side = t / (9 * CIN);
+    (&wl[0][0][0])[t] = (side ? Wb : Wa)[c * 9 + tap];
   }
-  cm_stage<CIN, CP, PS>(x, hA, wA, hB, wB, ha0, wa0, hb0, wb0, xoff, xa, xb);
+  cm_stage<CIN>(x, hA, wA, hB, wB, ha0, wa0, hb0, wb0, xoff, xa, xb);
   __syncthreads();
   const int at = t / CM_NT, bt = t % CM_NT;
   const int ay = at / CM_T, ax = at % CM_T, by = bt / CM_T, bx = bt % CM_T;
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  float s0 = 0.f, s1 = 0.f;
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int ky = tap / 3, kx = tap % 3;
-    const float* pa = &xa[(((ay + ky) * CM_H + ax + kx) * CM_NT + bt) * PS];
-    const float* pb = &xb[(at * CM_NH + (by + ky) * CM_H + bx + kx) * PS];
+    const float* pa = &xa[(((ay + ky) * CM_H + ax + kx) * CM_NT + bt) * CIN];
+    const float* pb = &xb[(at * CM_NH + (by + ky) * CM_H + bx + kx) * CIN];
 #pragma unroll
-    for (int c4 = 0; c4 < CP / 4; ++c4) {
-      const f32x4 va = *(const f32x4*)(pa + 4 * c4), vb = *(const f32x4*)(pb + 4 * c4);
-      const f32x4 wa = *(const f32x4*)&wl[0][tap][4 * c4], wb = *(const f32x4*)&wl[1][tap][4 * c4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        s[q] = fmaf(wa[q], va[q], s[q]);
-        s[q] = fmaf(wb[q], vb[q], s[q]);
-      }
+    for (int c2 = 0; c2 < CIN / 2; ++c2) {
+      const f32x2 va = *(const f32x2*)(pa + 2 * c2), vb = *(const f32x2*)(pb + 2 * c2);
+      const f32x2 wa = *(const f32x2*)&wl[0][tap][2 * c2], wb = *(const f32x2*)&wl[1][tap][2 * c2];
+      s0 = fmaf(wa[0], va[0], s0);
+      s1 = fmaf(wa[1], va[1], s1);
+      s0 = fmaf(wb[0], vb[0], s0);
+      s1 = fmaf(wb[1], vb[1], s1);
     }
   }
   const int ha = ha0 + ay, wa = wa0 + ax, hb = hb0 + by, wb = wb0 + bx;
   if (ha < hA && wa < wA && hb < hB && wb < wB)
-    y[(long)blockIdx.z * NA * NB + (long)(ha * wA + wa) * NB + hb * wB + wb] =
-        fmaxf(((s[0] + s[1]) + (s[2] + s[3])) + (ba[0] + bb[0]), 0.f);
+    y[(long)blockIdx.z * NA * NB + (long)(ha * wA + wa) * NB + hb * wB + wb] = fmaxf((s0 + s1) + (ba[0] + bb[0]), 0.f);
 }
 
 // x [B][C][P] (channel planes) -> y [B][P][C] (channels last)

@@ -74,7 +74,9 @@ struct TailArgs {
   unsigned tick_base;    // e * G
   long spin_limit;
   unsigned* status;      // the context's mapped host status word
+  unsigned long long* stamps;  // timing study (ST instantiation): [G][TL_NSTAMP] s_memtime per phase edge
 };
+constexpr int TL_NSTAMP = 16;
 
 __device__ __forceinline__ void st1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void st1(unsigned* p, unsigned v) {
@@ -160,6 +162,9 @@ struct TailMet {  // P5
   double fd[2][TL_T];
 };
 
+// ST: the timing-study instantiation (CWT_TAIL_STAMPS=1): thread 0 of every workgroup records
+// s_memtime at each phase edge (and s_memrealtime at entry / exit) into a.stamps; never the timed one.
+template <bool ST>
 __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
   constexpr int C = TL_C, H = TL_H, NR = TL_NR;
   __shared__ __attribute__((aligned(16))) char smem_raw[sizeof(TailTok)];
@@ -174,6 +179,12 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
     abort_flag = 0;
     last_flag = 0;
   }
+  unsigned long long* stp = (ST && t == 0) ? a.stamps + (long)gi * TL_NSTAMP : nullptr;
+  auto stamp = [&](int i) {
+    if (ST && stp) stp[i] = __builtin_amdgcn_s_memtime();
+  };
+  if (ST && stp) stp[14] = __builtin_amdgcn_s_memrealtime();
+  stamp(0);
   __syncthreads();
 
   // ---- P0: r[v][h*C + k] = M[h*C + k] . q[v] / sqrt(C) (rowdot_kernel<8>'s per-lane partition) ----
@@ -195,7 +206,9 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
       }
     }
   }
+  stamp(1);
   if (!tail_barrier(a, a.bar_base + (unsigned)G * 1, &abort_flag)) return;
+  stamp(2);
 
   // ---- P1: the token pass over this workgroup's chunks (attn_tokens_kernel) ----
   {
@@ -307,7 +320,9 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
       }
     }
   }
+  stamp(3);
   if (!tail_barrier(a, a.bar_base + (unsigned)G * 2, &abort_flag)) return;
+  stamp(4);
 
   // ---- P2: combine the chunk partials: g[b][rho][k] (items: b, rho, 64-channel block) ----
   {
@@ -351,7 +366,9 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
       }
     }
   }
+  stamp(5);
   if (!tail_barrier(a, a.bar_base + (unsigned)G * 3, &abort_flag)) return;
+  stamp(6);
 
   // ---- P3: y[v][j] = P[j] . g_v + fc_b[j] + q_v[j] (rowdot_kernel<32>'s per-lane partition) ----
   {
@@ -384,7 +401,9 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
       }
     }
   }
+  stamp(7);
   if (!tail_barrier(a, a.bar_base + (unsigned)G * 4, &abort_flag)) return;
+  stamp(8);
 
   // ---- P4: LayerNorm (each workgroup its own copy of W'), then pred_q over this workgroup's
   // token chunks: (W' . f_p) / ||f_p|| (classify_scaled_kernel) ----
@@ -444,18 +463,38 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
       }
     }
   }
+  stamp(9);
   if (!tail_barrier(a, a.bar_base + (unsigned)G * 5, &abort_flag)) return;
+  stamp(10);
 
   // ---- P5: upsample (align_corners) + argmax + counts + CE (seg_metrics_kernel's per-pixel
   // math) of pred_q and pred_q0; per-workgroup partials, summed by the last arriver ----
   {
     TailMet& L = *(TailMet*)smem_raw;
     const long npix = (long)a.S * a.S, plane = (long)a.h * a.w;
+    // the episode's four low-res planes (pred_q, pred_q0) staged in LDS once per workgroup when
+    // they fit beside the partials (473^2: 58 KB, 641^2: 105 KB): the per-pixel bilinear reads
+    // then hit LDS instead of sixteen sc1 loads from L2
+    float* lg = (float*)(smem_raw + sizeof(TailMet));
+    const bool in_lds = 4 * plane * (long)sizeof(float) <= (long)(sizeof(TailTok) - sizeof(TailMet));
     for (int b = 0; b < B; ++b) {
       const float* L0 = a.logits + (long)b * 2 * plane;
       const float* L1 = L0 + plane;
       const float* K0 = a.logits0 + (long)b * 2 * plane;
       const float* K1 = K0 + plane;
+      if (in_lds) {
+        __syncthreads();  // the previous episode's reads of lg are done
+        for (long i = t; i < 2 * plane; i += TL_T) {
+          lg[i] = ld1(a.logits + (long)b * 2 * plane + i);
+          lg[2 * plane + i] = ld1(a.logits0 + (long)b * 2 * plane + i);
+        }
+        __syncthreads();
+        L0 = lg;
+        L1 = lg + plane;
+        K0 = lg + 2 * plane;
+        K1 = lg + 3 * plane;
+      }
+      auto rd = [&](const float* pp, long o) { return in_lds ? pp[o] : ld1(pp + o); };
       unsigned c[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       double nll = 0.0;
       unsigned nvalid = 0;
@@ -464,14 +503,14 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
         const Lerp ly = lerp_coord(Y, a.h, a.sy), lx = lerp_coord(X, a.w, a.sx);
         const long o00 = ly.i0 * a.w + lx.i0, o01 = ly.i0 * a.w + lx.i1, o10 = ly.i1 * a.w + lx.i0,
                    o11 = ly.i1 * a.w + lx.i1;
-        const float l0 = ly.l0 * (lx.l0 * ld1(L0 + o00) + lx.l1 * ld1(L0 + o01)) +
-                         ly.l1 * (lx.l0 * ld1(L0 + o10) + lx.l1 * ld1(L0 + o11));
-        const float l1 = ly.l0 * (lx.l0 * ld1(L1 + o00) + lx.l1 * ld1(L1 + o01)) +
-                         ly.l1 * (lx.l0 * ld1(L1 + o10) + lx.l1 * ld1(L1 + o11));
-        const float k0 = ly.l0 * (lx.l0 * ld1(K0 + o00) + lx.l1 * ld1(K0 + o01)) +
-                         ly.l1 * (lx.l0 * ld1(K0 + o10) + lx.l1 * ld1(K0 + o11));
-        const float k1 = ly.l0 * (lx.l0 * ld1(K1 + o00) + lx.l1 * ld1(K1 + o01)) +
-                         ly.l1 * (lx.l0 * ld1(K1 + o10) + lx.l1 * ld1(K1 + o11));
+        const float l0 = ly.l0 * (lx.l0 * rd(L0, o00) + lx.l1 * rd(L0, o01)) +
+                         ly.l1 * (lx.l0 * rd(L0, o10) + lx.l1 * rd(L0, o11));
+        const float l1 = ly.l0 * (lx.l0 * rd(L1, o00) + lx.l1 * rd(L1, o01)) +
+                         ly.l1 * (lx.l0 * rd(L1, o10) + lx.l1 * rd(L1, o11));
+        const float k0 = ly.l0 * (lx.l0 * rd(K0, o00) + lx.l1 * rd(K0, o01)) +
+                         ly.l1 * (lx.l0 * rd(K0, o10) + lx.l1 * rd(K0, o11));
+        const float k1 = ly.l0 * (lx.l0 * rd(K1, o00) + lx.l1 * rd(K1, o01)) +
+                         ly.l1 * (lx.l0 * rd(K1, o10) + lx.l1 * rd(K1, o11));
         const int64_t tg = a.target[(long)b * npix + i];
         if (tg == 255) continue;
         const int pred = (l1 > l0) ? 1 : 0, pred0 = (k1 > k0) ? 1 : 0;  // torch.argmax: first index on ties
@@ -516,6 +555,8 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
       }
     }
     // ticket: the last workgroup to arrive sums the partials in workgroup order (deterministic)
+    stamp(11);
+    if (ST && stp) stp[15] = __builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
@@ -573,7 +614,8 @@ size_t episode_tail_cnt_words() { return (TL_REP + 2) * TL_STRIDE; }
 int launch_episode_tail(const float* q, const float* f, int B, int hw, int h, int w, int S, const int64_t* target,
                         const float* fold, const float* fc_b, const float* ln_w, const float* ln_b, float* out,
                         float* logits, float* logits0, float* iut, double* ce, float* iut0, float* ws,
-                        unsigned* cnt, unsigned epoch, int G, long spin_limit, unsigned* status, hipStream_t st) {
+                        unsigned* cnt, unsigned epoch, int G, long spin_limit, unsigned* status, hipStream_t st,
+                        unsigned long long* stamps) {
   if (B < 1 || B > TL_MAXB || hw < 1 || hw > TL_MAXCHUNK * TL_TPB || h * w != hw || G < 1 || G > TL_T)
     return fail(CWT_EARG, "episode_tail: need 1 <= B <= 4, hw = h*w <= 16384, 1 <= G <= 512");
   TailArgs a;
@@ -623,7 +665,11 @@ int launch_episode_tail(const float* q, const float* f, int B, int hw, int h, in
   a.tick_base = epoch * (unsigned)G;
   a.spin_limit = spin_limit > 0 ? spin_limit : 4000000;
   a.status = status;
-  hipLaunchKernelGGL(episode_tail_kernel, dim3(G), dim3(TL_T), 0, st, a);
+  a.stamps = stamps;
+  if (stamps)
+    hipLaunchKernelGGL((episode_tail_kernel<true>), dim3(G), dim3(TL_T), 0, st, a);
+  else
+    hipLaunchKernelGGL((episode_tail_kernel<false>), dim3(G), dim3(TL_T), 0, st, a);
   CWT_LAUNCH_CHECK();
   return 0;
 }

@@ -63,6 +63,13 @@ int cwt_debug_conv_f32d(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int
                         const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
                         int nsplit, void* stream);
 
+/* Timing-study hook of cwt_episode_tail: with CWT_TAIL_STAMPS=1 in the environment the tail runs a
+ * separately compiled instantiation whose workgroups record s_memtime at each phase edge
+ * ([G][16]: 0 entry, 2k-1 / 2k before / after grid barrier k, 11 the partials written, 14 / 15
+ * s_memrealtime at entry / before the ticket; tools/tail_stamps.py).  Copies up to max_count of
+ * the last stamped launch's values to host_out; *count = G * 16 (0 if none). */
+int cwt_debug_tail_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t max_count, int64_t* count);
+
 /* Timing-study hook of the inner loop: with CWT_ADAPT_DBG=32 in the environment, the inner
  * loop runs a separately compiled instantiation that records clock stamps per step and
  * workgroup (persistent loop: tools/persist_stamps.py; per-step launches with
