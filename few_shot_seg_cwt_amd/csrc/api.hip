@@ -1233,8 +1233,11 @@ int cwt_episode_tail(cwt_ctx* ctx, const float* q, const float* f, int B, int h,
   constexpr int C = 512, H = 4;
   int cu = 0;
   CWT_HIP(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-  // G co-resident 512-thread workgroups (one per CU by their LDS); CWT_TAIL_G for A/B
-  int G = std::min(64, cu);
+  // G co-resident 512-thread workgroups (~54 KB of LDS each): the whole chip (up to 256)
+  // on a context that runs alone; 64 on one whose inner loop shares the chip with another
+  // stream's extractor pass (cwt_ctx_set_adapt_units >= 2: EpisodePipeline's adapt context).
+  // CWT_TAIL_G for A/B
+  int G = std::min(ctx->adapt_upw >= 2 ? 64 : 256, cu);
   if (const char* gs = getenv("CWT_TAIL_G")) G = std::max(1, std::min(atoi(gs), cu));
   void *fold, *ws, *cnt;
   int rc;

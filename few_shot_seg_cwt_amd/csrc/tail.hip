@@ -19,8 +19,11 @@
 // Every value one workgroup hands to another is stored write-through (sc1) and loaded with sc1
 // loads (MI355X_MICROARCH.md, hand-off table, first row): no L2 write-back or invalidate.  The
 // arithmetic of every phase is the module kernels' (the same per-lane partitions and reduction
-// trees), except the chunk combine (8 waves take every 8th chunk instead of 4 every 4th) and the
-// order of the CE's double partial sums.
+// trees), except the chunk combine (8 waves take every 8th chunk instead of 4 every 4th), the
+// token pass's per-wave sums (added pairwise into two LDS slots: the phases' LDS is ~54 KB, so a
+// tail workgroup can share a CU with an extractor conv's workgroup in the episode pipeline) and
+// the order of the CE's double partial sums.  P5 gives each workgroup one contiguous pixel range
+// and stages the low-res rows it reads in LDS.
 // Counters are monotonic over launches: launch e's barrier k waits for G (e NBAR + k) arrivals,
 // its ticket's last arriver sees e G + G - 1 (the host bumps e per launch and re-zeroes the
 // counters before the 32-bit range would wrap, or after a launch aborted).
@@ -142,15 +145,18 @@ __device__ __forceinline__ float tl_dot8(f32x4 a0, f32x4 a1, f32x4 b0, f32x4 b1)
 // LDS of the phases (one object, carved per phase)
 struct TailTok {  // P1
   float rs[TL_NR + 2][TL_C];      // score rows, then W's two rows
-  float wg[TL_NW][TL_NR][TL_C];   // per-wave exp-weighted token sums
+  float wg[2][TL_NR][TL_C];       // exp-weighted token sums, rescaled to the chunk max: two slots,
+                                  // the waves adding into them two at a time (LDS ~54 KB, so a
+                                  // tail workgroup co-resides with an extractor conv's)
   float wml[TL_NW][TL_NR][2];
 };
 struct TailComb {  // P2
   float ms[TL_MAXCHUNK], ls[TL_MAXCHUNK];
   float sg[TL_NW][64], sl[TL_NW];
 };
+constexpr int TL_PV = 4;  // P3: score vectors staged per pass
 struct TailProj {  // P3
-  float gv[2 * TL_MAXB][TL_H * TL_C];
+  float gv[TL_PV][TL_H * TL_C];
 };
 struct TailCls {  // P4
   float w2[2 * TL_MAXB][TL_C];
@@ -289,27 +295,45 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
           ga[rho] += w * fa[tt];
           gb[rho] += w * fb[tt];
         }
-#pragma unroll
-      for (int rho = 0; rho < NR; ++rho) {
-        *(f32x4*)&L.wg[wv][rho][4 * lane] = ga[rho];
-        *(f32x4*)&L.wg[wv][rho][256 + 4 * lane] = gb[rho];
-      }
       if (lane < NR) {
         L.wml[wv][lane][0] = m;
         L.wml[wv][lane][1] = l;
       }
       __syncthreads();
+      // rescale this wave's sums to the chunk max of each rho, then add them into slot wv & 1,
+      // waves (0, 1) first, then (2, 3), ...: slot s = ((w_s + w_{s+2}) + w_{s+4}) + w_{s+6}
+      float sw[NR];
+#pragma unroll
+      for (int rho = 0; rho < NR; ++rho) {
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < TL_NW; ++w) M = fmaxf(M, L.wml[w][rho][0]);
+        sw[rho] = (L.wml[wv][rho][0] == -INFINITY) ? 0.f : __expf(L.wml[wv][rho][0] - M);
+      }
+      for (int r = 0; r < TL_NW / 2; ++r) {
+        if ((wv >> 1) == r) {
+          const int slot = wv & 1;
+#pragma unroll
+          for (int rho = 0; rho < NR; ++rho) {
+            f32x4* da = (f32x4*)&L.wg[slot][rho][4 * lane];
+            f32x4* db = (f32x4*)&L.wg[slot][rho][256 + 4 * lane];
+            const f32x4 xa = sw[rho] * ga[rho], xb = sw[rho] * gb[rho];
+            *da = r ? *da + xa : xa;
+            *db = r ? *db + xb : xb;
+          }
+        }
+        __syncthreads();
+      }
       for (int i = t; i < NR * (C / 4); i += TL_T) {
         const int rho = i / (C / 4), c4 = i - rho * (C / 4);
         float M = -INFINITY;
 #pragma unroll
         for (int w = 0; w < TL_NW; ++w) M = fmaxf(M, L.wml[w][rho][0]);
-        f32x4 Gs = f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 Gs = *(const f32x4*)&L.wg[0][rho][c4 * 4] + *(const f32x4*)&L.wg[1][rho][c4 * 4];
         float Ls = 0.f;
 #pragma unroll
         for (int w = 0; w < TL_NW; ++w) {
           const float s = (L.wml[w][rho][0] == -INFINITY) ? 0.f : __expf(L.wml[w][rho][0] - M);
-          Gs += s * *(const f32x4*)&L.wg[w][rho][c4 * 4];
           Ls = fmaf(s, L.wml[w][rho][1], Ls);
         }
         st1x4(a.part_g + (((long)b * nchunk + chunk) * NR + rho) * C + c4 * 4, Gs);
@@ -373,7 +397,10 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
   // ---- P3: y[v][j] = P[j] . g_v + fc_b[j] + q_v[j] (rowdot_kernel<32>'s per-lane partition) ----
   {
     TailProj& L = *(TailProj*)smem_raw;
-    for (int i = t; i < nv * H * C; i += TL_T) L.gv[i / (H * C)][i % (H * C)] = ld1(a.g + i);
+    for (int v0 = 0; v0 < nv; v0 += TL_PV) {
+    const int npv = min(TL_PV, nv - v0);
+    __syncthreads();  // the previous pass's reads are done
+    for (int i = t; i < npv * H * C; i += TL_T) L.gv[i / (H * C)][i % (H * C)] = ld1(a.g + (long)v0 * H * C + i);
     __syncthreads();
     for (int row = gi * TL_NW + wv; row < C; row += G * TL_NW) {
       float av[32];
@@ -386,11 +413,12 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
         av[4 * c + 2] = u[2];
         av[4 * c + 3] = u[3];
       }
-      for (int v = 0; v < nv; ++v) {
+      for (int vi = 0; vi < npv; ++vi) {
+        const int v = v0 + vi;
         float s = 0.f;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          const f32x4 u = *(const f32x4*)&L.gv[v][c * 256 + lane * 4];
+          const f32x4 u = *(const f32x4*)&L.gv[vi][c * 256 + lane * 4];
           s = fmaf(av[4 * c], u[0], s);
           s = fmaf(av[4 * c + 1], u[1], s);
           s = fmaf(av[4 * c + 2], u[2], s);
@@ -399,6 +427,7 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
         s = wave_sum(s);
         if (lane == 0) st1(a.y + (long)v * C + row, s + a.fc_b[row] + a.q[(long)v * C + row]);
       }
+    }
     }
   }
   stamp(7);
@@ -472,33 +501,42 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
   {
     TailMet& L = *(TailMet*)smem_raw;
     const long npix = (long)a.S * a.S, plane = (long)a.h * a.w;
-    // the episode's four low-res planes (pred_q, pred_q0) staged in LDS once per workgroup when
-    // they fit beside the partials (473^2: 58 KB, 641^2: 105 KB): the per-pixel bilinear reads
-    // then hit LDS instead of sixteen sc1 loads from L2
+    // this workgroup's pixels: one contiguous range of the S x S image per episode; the low-res
+    // rows its bilinear footprint touches (four planes: pred_q, pred_q0) are staged in LDS when
+    // they fit beside the partials -- the per-pixel reads then hit LDS, not sixteen sc1 loads
+    const long p0 = npix * gi / G, p1 = npix * (gi + 1) / G;
+    const int Y0 = (int)(p0 / a.S), Y1 = (int)((p1 > p0 ? p1 - 1 : p0) / a.S);
+    const int ylo = lerp_coord(Y0, a.h, a.sy).i0, yhi = lerp_coord(Y1, a.h, a.sy).i1;
+    const long nrow = (long)(yhi - ylo + 1) * a.w;  // staged floats per plane
     float* lg = (float*)(smem_raw + sizeof(TailMet));
-    const bool in_lds = 4 * plane * (long)sizeof(float) <= (long)(sizeof(TailTok) - sizeof(TailMet));
+    const bool in_lds = 4 * nrow * (long)sizeof(float) <= (long)(sizeof(TailTok) - sizeof(TailMet));
     for (int b = 0; b < B; ++b) {
       const float* L0 = a.logits + (long)b * 2 * plane;
       const float* L1 = L0 + plane;
       const float* K0 = a.logits0 + (long)b * 2 * plane;
       const float* K1 = K0 + plane;
+      long obase = 0;  // subtracted from every plane offset when staged
       if (in_lds) {
         __syncthreads();  // the previous episode's reads of lg are done
-        for (long i = t; i < 2 * plane; i += TL_T) {
-          lg[i] = ld1(a.logits + (long)b * 2 * plane + i);
-          lg[2 * plane + i] = ld1(a.logits0 + (long)b * 2 * plane + i);
+        const long r0 = (long)ylo * a.w;
+        for (long i = t; i < nrow; i += TL_T) {
+          lg[i] = ld1(L0 + r0 + i);
+          lg[nrow + i] = ld1(L1 + r0 + i);
+          lg[2 * nrow + i] = ld1(K0 + r0 + i);
+          lg[3 * nrow + i] = ld1(K1 + r0 + i);
         }
         __syncthreads();
         L0 = lg;
-        L1 = lg + plane;
-        K0 = lg + 2 * plane;
-        K1 = lg + 3 * plane;
+        L1 = lg + nrow;
+        K0 = lg + 2 * nrow;
+        K1 = lg + 3 * nrow;
+        obase = r0;
       }
-      auto rd = [&](const float* pp, long o) { return in_lds ? pp[o] : ld1(pp + o); };
+      auto rd = [&](const float* pp, long o) { return in_lds ? pp[o - obase] : ld1(pp + o); };
       unsigned c[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       double nll = 0.0;
       unsigned nvalid = 0;
-      for (long i = (long)gi * TL_T + t; i < npix; i += (long)G * TL_T) {
+      for (long i = p0 + t; i < p1; i += TL_T) {
         const int Y = (int)(i / a.S), X = (int)(i - (long)Y * a.S);
         const Lerp ly = lerp_coord(Y, a.h, a.sy), lx = lerp_coord(X, a.w, a.sx);
         const long o00 = ly.i0 * a.w + lx.i0, o01 = ly.i0 * a.w + lx.i1, o10 = ly.i1 * a.w + lx.i0,
