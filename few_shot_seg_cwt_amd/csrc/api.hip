@@ -275,6 +275,73 @@ static int zero_line(cwt_ctx* ctx, const __bf16** out) {
   return 0;
 }
 
+// C = A . Bm^T (+ bias[N]) (+ res, pixel stride res_ld) in exact fp32 on the LDS-DMA conv body:
+// conv_igemm_f32d as a 1x1 conv over M "pixels" (A's [M][K] rows) with the [N][K] weights Bm (a
+// 1x1 conv's fp32 packing is plain row-major [Co][Ci]); the epilogue is fmaf(acc, 1, bias) then
+// + res, the order of the separate bias / residual passes it replaces.  Shapes: K % 32 == 0,
+// N % 64 == 0, 16-B aligned operands (gemm_f32d_ok); the rest stay on corr_gemm_kernel.
+// CWT_GEMM_F32D=0 keeps every GEMM there (A/B).
+static bool gemm_f32d_ok(int M, int N, int K, const void* A, const void* Bm, const void* Cm, const void* res) {
+  static const bool on = !(getenv("CWT_GEMM_F32D") && getenv("CWT_GEMM_F32D")[0] == '0');
+  const uintptr_t al = (uintptr_t)A | (uintptr_t)Bm | (uintptr_t)Cm | (uintptr_t)res;
+  return on && M >= 1 && K % 32 == 0 && N % 64 == 0 && N <= 8192 && (al & 15) == 0;
+}
+static int zero_line(cwt_ctx* ctx, const __bf16** out);
+static int gemm_f32d(cwt_ctx* ctx, const float* A, const float* Bm, int M, int N, int K, float* Cm, const float* bias,
+                     const float* res, int res_ld, hipStream_t st, int relu = 0) {
+  const bool fresh = ctx->ws.find("gemm.one") == ctx->ws.end();
+  void *one, *zer, *part;
+  const __bf16* zero;
+  int rc;
+  if ((rc = ensure_ws(ctx, "gemm.one", 8192 * 4, &one)) || (rc = ensure_ws(ctx, "gemm.zero", 8192 * 4, &zer)) ||
+      (rc = zero_line(ctx, &zero)))
+    return rc;
+  if (fresh) {
+    CWT_HIP(hipMemsetD32((hipDeviceptr_t)one, 0x3f800000u, 8192));  // 1.0f
+    CWT_HIP(hipMemset(zer, 0, 8192 * 4));
+  }
+  const ConvPlan pl = plan_conv_f32d(M, N, K);
+  const size_t part_floats = pl.nsplit > 1 ? (size_t)pl.nsplit * M * N : 1;
+  if ((rc = ensure_ws(ctx, "gemm.part", part_floats * 4, &part))) return rc;
+  ConvSArgs a;
+  memset(&a, 0, sizeof(a));
+  a.xs = (const __bf16*)A;
+  a.ws = (const __bf16*)Bm;
+  a.zero = zero;
+  a.scale = (const float*)one;
+  a.shift = bias ? bias : (const float*)zer;
+  a.res = res;
+  a.res_ld = res_ld;
+  a.y = Cm;
+  a.y_ld = N;
+  a.N = 1;
+  a.Hi = M;
+  a.Wi = 1;
+  a.Ci = K;
+  a.Ho = M;
+  a.Wo = 1;
+  a.Co = N;
+  a.kh = a.kw = 1;
+  a.stride = 1;
+  a.dil = 1;
+  a.M = M;
+  a.K = K;
+  a.relu = relu;
+  return launch_conv_x3s(a, pl, 0, (float*)part, part_floats, st, 0);
+}
+
+// MatchNet's readout weighted_v[b] = attn[b] . v[b] as tokens [B][NA][Cv] = P[b] . vt[b]^T
+static int readout_gemm(cwt_ctx* ctx, const float* P, const float* vt, int B, int NA, int Cv, int ldp, float* out,
+                        hipStream_t st) {
+  if (!gemm_f32d_ok(NA, Cv, ldp, P, vt, out, nullptr)) return launch_gemm_abt(P, vt, B, NA, Cv, ldp, out, st);
+  for (int b = 0; b < B; ++b) {
+    int rc = gemm_f32d(ctx, P + (long)b * NA * ldp, vt + (long)b * Cv * ldp, NA, Cv, ldp, out + (long)b * NA * Cv,
+                       nullptr, nullptr, 0, st);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 struct HostParams {
   std::map<std::string, std::pair<const float*, int64_t>> m;
   const float* get(const std::string& k, int64_t numel, std::string* err) const {
@@ -1456,14 +1523,14 @@ static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int
   if (weighted_v) {
     // attn = softmax(temp * corr2d, dim=-1); weighted_v = bmm(v, attn^T) (match.py:151-153),
     // here as tokens [B][NA][Cv] = attn . v
-    const int ldp = (int)((NB + 3) & ~3L);
+    const int ldp = (int)((NB + 31) & ~31L);  // zero-padded to whole 32-deep K tiles (gemm_f32d)
     void *pw, *vt;
     if ((rc = ensure_ws(ctx, "match.attn", (size_t)B * NA * ldp * 4, &pw)) ||
         (rc = ensure_ws(ctx, "match.vt", (size_t)B * Cv * ldp * 4, &vt)))
       return rc;
     if ((rc = launch_match_softmax(corr2d, B, (int)NA, (int)NB, temp, ldp, (float*)pw, st))) return rc;
     if ((rc = launch_match_vt(v, B, (int)NB, Cv, ldp, (float*)vt, st))) return rc;
-    if ((rc = launch_gemm_abt((const float*)pw, (const float*)vt, B, (int)NA, Cv, ldp, weighted_v, st))) return rc;
+    if ((rc = readout_gemm(ctx, (const float*)pw, (const float*)vt, B, (int)NA, Cv, ldp, weighted_v, st))) return rc;
   }
   p.end();
   return 0;
@@ -1532,7 +1599,7 @@ int cwt_match_readout(cwt_ctx* ctx, const float* corr2d, int B, int NA, int NB, 
   CWT_CHECK(corr2d && v && weighted_v && B >= 1 && NA >= 1 && NB >= 1 && Cv >= 1, "bad arguments");
   CWT_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
-  const int ldp = (int)((NB + 3) & ~3L);
+  const int ldp = (int)((NB + 31) & ~31L);  // zero-padded to whole 32-deep K tiles (gemm_f32d)
   void *pw, *vt;
   int rc;
   if ((rc = ensure_ws(ctx, "match.attn", (size_t)B * NA * ldp * 4, &pw)) ||
@@ -1541,7 +1608,7 @@ int cwt_match_readout(cwt_ctx* ctx, const float* corr2d, int B, int NA, int NB, 
   Prof p(ctx, st, "match_readout", 2.0 * B * NA * (double)NB * Cv, 4.0 * B * ((double)NA * NB * 2 + (double)NB * Cv));
   if ((rc = launch_match_softmax(corr2d, B, NA, NB, temp, ldp, (float*)pw, st))) return rc;
   if ((rc = launch_match_vt(v, B, NB, Cv, ldp, (float*)vt, st))) return rc;
-  if ((rc = launch_gemm_abt((const float*)pw, (const float*)vt, B, NA, Cv, ldp, weighted_v, st))) return rc;
+  if ((rc = readout_gemm(ctx, (const float*)pw, (const float*)vt, B, NA, Cv, ldp, weighted_v, st))) return rc;
   p.end();
   return 0;
 }
@@ -1565,10 +1632,18 @@ int cwt_weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C,
     return rc;
   Prof p(ctx, st, "weight_average c" + std::to_string(C), 2.0 * P * C * co * 4, 4.0 * P * (2.0 * C + 5.0 * co));
   // theta | phi | g of every pixel: one GEMM against the three stacked 1x1 weights [3co][C]
-  if ((rc = launch_gemm_abt(x, w_tpg, 1, (int)P, 3 * co, C, (float*)tpg, st))) return rc;
+  if (gemm_f32d_ok((int)P, 3 * co, C, x, w_tpg, tpg, nullptr)) {
+    if ((rc = gemm_f32d(ctx, x, w_tpg, (int)P, 3 * co, C, (float*)tpg, nullptr, nullptr, 0, st))) return rc;
+  } else if ((rc = launch_gemm_abt(x, w_tpg, 1, (int)P, 3 * co, C, (float*)tpg, st))) {
+    return rc;
+  }
   if ((rc = launch_wa_attn((const float*)tpg, N, h, w, co, b_theta, b_phi, b_g, (float*)wavg, st))) return rc;
-  if ((rc = launch_gemm_abt((const float*)wavg, w_back, 1, (int)P, C, co, (float*)back, st))) return rc;
-  if ((rc = launch_wa_residual(x, (const float*)back, b_back, P * C, C, out, st))) return rc;
+  if (gemm_f32d_ok((int)P, C, co, wavg, w_back, out, x)) {  // conv_back + bias + residual in one epilogue
+    if ((rc = gemm_f32d(ctx, (const float*)wavg, w_back, (int)P, C, co, out, b_back, x, C, st))) return rc;
+  } else {
+    if ((rc = launch_gemm_abt((const float*)wavg, w_back, 1, (int)P, C, co, (float*)back, st))) return rc;
+    if ((rc = launch_wa_residual(x, (const float*)back, b_back, P * C, C, out, st))) return rc;
+  }
   p.end();
   return 0;
 }
@@ -1592,9 +1667,17 @@ int cwt_linear(cwt_ctx* ctx, const float* x, int64_t P, int K, const float* w, c
   if ((rc = ensure_ws(ctx, "linear.tmp", (size_t)P * N * 4, &tmp))) return rc;
   Prof p(ctx, st, "linear " + std::to_string(K) + "x" + std::to_string(N), 2.0 * P * N * K,
          4.0 * ((double)P * K + (double)N * K + (double)P * N));
-  if ((rc = launch_gemm_abt(x, w, 1, (int)P, N, K, (float*)tmp, st))) return rc;
-  if ((rc = launch_linear_epilogue((const float*)tmp, bias, accumulate ? out : nullptr, (long)P, N, relu, out, st)))
-    return rc;
+  if (!accumulate && gemm_f32d_ok((int)P, N, K, x, w, out, nullptr)) {  // (tmp + bias), relu: the epilogue's order
+    if ((rc = gemm_f32d(ctx, x, w, (int)P, N, K, out, bias, nullptr, 0, st, relu))) return rc;
+  } else {
+    if (gemm_f32d_ok((int)P, N, K, x, w, tmp, nullptr)) {
+      if ((rc = gemm_f32d(ctx, x, w, (int)P, N, K, (float*)tmp, nullptr, nullptr, 0, st))) return rc;
+    } else if ((rc = launch_gemm_abt(x, w, 1, (int)P, N, K, (float*)tmp, st))) {
+      return rc;
+    }
+    if ((rc = launch_linear_epilogue((const float*)tmp, bias, accumulate ? out : nullptr, (long)P, N, relu, out, st)))
+      return rc;
+  }
   p.end();
   return 0;
 }

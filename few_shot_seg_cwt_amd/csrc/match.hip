@@ -401,6 +401,321 @@ __global__ __launch_bounds__(256) void cp4d_c1_kernel(const float* __restrict__ 
     y[(long)blockIdx.z * NA * NB + (long)(ha * wA + wa) * NB + hb * wB + wb] = fmaxf((s0 + s1) + (ba[0] + bb[0]), 0.f);
 }
 
+// ---- persistent forms (round 4, second pass): the tile kernels above spent ~85 % of a wave's
+// life outside the matrix pipe (PMC: SQ_VALU_MFMA_BUSY 40 % of the 10 -> 10 layer's time, a wave
+// living 41 k cycles for 5.9 k of MFMA) -- each workgroup staged its tile, then loaded its weights
+// (46 scattered loads per lane), then computed, with nothing to overlap the loads but the two
+// other workgroups on the CU.  Here a workgroup stays resident over tiles t, t + G, t + 2G, ...:
+// weights and per-lane LDS offsets are formed once, and the next tile's staging loads are issued
+// into registers right after the current tile is stored to LDS, so they fly under its MFMAs.
+// Same staged layout, same per-output fmaf chains (the K order below only changes which MFMA
+// carries which (tap, channel) row: the f32 MFMA accumulates one product at a time, in K order,
+// so the sums differ from the tile kernels' only in that order).
+template <int CIN>
+struct CmRegs {
+  static constexpr int V = (CIN % 2 == 0) ? 2 : 1, VP = CIN / V;
+  static constexpr int LA = CM_NH * CM_NT * VP, LB = CM_NT * CM_NH * VP;
+  static constexpr int IA = (LA + 255) / 256, IB = (LB + 255) / 256;
+  typedef float vec_t __attribute__((ext_vector_type(V)));
+  vec_t ra[IA], rb[IB];
+};
+
+// tile t of the grid of (a tile, b tile, batch) -> its origin and input offset
+struct CmTile {
+  int ha0, wa0, hb0, wb0, z;
+};
+__device__ __forceinline__ CmTile cm_tile(int t, int nta, int ntb, int NTA, int NTB) {
+  const int per = NTA * NTB;
+  const int z = t / per, r = t - z * per;
+  const int ta = r / NTB, tb = r - ta * NTB;
+  return CmTile{(ta / nta) * CM_T, (ta % nta) * CM_T, (tb / ntb) * CM_T, (tb % ntb) * CM_T, z};
+}
+
+// Tile schedule of the persistent kernels.  order 0: workgroup w takes tiles w, w + G, ... of
+// the (batch, a tile, b tile) order, b fastest.  order 1: the same order cut into 8 contiguous
+// ranges, one per XCD (workgroup w runs on XCD w % 8 when G % 8 == 0), so the tiles that share
+// staged data share an L2.  order 2: as 1, with the tiles visited by rows of b tiles, a tiles
+// fastest within a row (the b-halo strip of a row is then streamed once per a tile, the a halo
+// slides along wa inside one L2).
+struct CmSched {
+  int cur, end, step;
+};
+__device__ __forceinline__ CmSched cm_sched(int ntiles, int order) {
+  if (order == 0 || (gridDim.x & 7)) return CmSched{(int)blockIdx.x, ntiles, (int)gridDim.x};
+  const int xcd = blockIdx.x & 7, per = (ntiles + 7) / 8;
+  return CmSched{xcd * per + (int)(blockIdx.x >> 3), min(ntiles, (xcd + 1) * per), (int)(gridDim.x >> 3)};
+}
+__device__ __forceinline__ int cm_order(int l, int order, int NTA, int NTB, int nbb) {
+  if (order < 2) return l;
+  const int per = NTA * NTB, z = l / per, r = l - z * per;
+  const int full = (NTB / nbb) * nbb;
+  int ta, tb;
+  if (r < NTA * full) {
+    const int blk = r / (NTA * nbb), rem = r - blk * NTA * nbb;
+    ta = rem / nbb;
+    tb = blk * nbb + rem % nbb;
+  } else {
+    const int r2 = r - NTA * full, nl = NTB - full;
+    ta = r2 / nl;
+    tb = full + r2 % nl;
+  }
+  return z * per + ta * NTB + tb;
+}
+
+template <int CIN>
+__device__ __forceinline__ void cm_load(CmRegs<CIN>& R, const float* __restrict__ x, int hA, int wA, int hB, int wB,
+                                        const CmTile& T) {
+  using Rg = CmRegs<CIN>;
+  typedef typename Rg::vec_t vec_t;
+  constexpr int V = Rg::V, VP = Rg::VP;
+  const int NB = hB * wB;
+  const float* xz = x + (long)T.z * hA * wA * NB * CIN;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < Rg::IA; ++k) {
+    int i = t + 256 * k;
+    asm volatile("" : "+v"(i));  // re-derive the indices per tile: hoisted, 24 loads' worth held ~120 VGPRs
+    const int q = i % VP, p = i / VP;
+    const int bt = p % CM_NT, ah = p / CM_NT;
+    const int ha = T.ha0 - 1 + ah / CM_H, wa = T.wa0 - 1 + ah % CM_H;
+    const int hb = T.hb0 + bt / CM_T, wb = T.wb0 + bt % CM_T;
+    const bool in = i < Rg::LA && (unsigned)ha < (unsigned)hA && (unsigned)wa < (unsigned)wA && hb < hB && wb < wB;
+    R.ra[k] = in ? *(const vec_t*)(xz + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + q * V) : vec_t(0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < Rg::IB; ++k) {
+    int i = t + 256 * k;
+    asm volatile("" : "+v"(i));
+    const int q = i % VP, p = i / VP;
+    const int bh = p % CM_NH, at = p / CM_NH;
+    const int ha = T.ha0 + at / CM_T, wa = T.wa0 + at % CM_T;
+    const int hb = T.hb0 - 1 + bh / CM_H, wb = T.wb0 - 1 + bh % CM_H;
+    const bool in = i < Rg::LB && ha < hA && wa < wA && (unsigned)hb < (unsigned)hB && (unsigned)wb < (unsigned)wB;
+    R.rb[k] = in ? *(const vec_t*)(xz + (((long)(ha * wA + wa) * NB) + hb * wB + wb) * CIN + q * V) : vec_t(0.f);
+  }
+}
+
+template <int CIN>
+__device__ __forceinline__ void cm_store(const CmRegs<CIN>& R, float* xa, float* xb) {
+  using Rg = CmRegs<CIN>;
+  typedef typename Rg::vec_t vec_t;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < Rg::IA; ++k) {
+    const int i = t + 256 * k;
+    if (i < Rg::LA) *(vec_t*)(xa + i * Rg::V) = R.ra[k];
+  }
+#pragma unroll
+  for (int k = 0; k < Rg::IB; ++k) {
+    const int i = t + 256 * k;
+    if (i < Rg::LB) *(vec_t*)(xb + i * Rg::V) = R.rb[k];
+  }
+}
+
+// K order of the persistent MFMA kernel (per branch): first the F = CIN / 4 full channel quads
+// of every tap (MFMA m < 9 F: tap m / F, channels 4 (m % F) + g4 -- the four lane groups share the
+// tap, so the LDS offset is the lane's base + an immediate), then the R = CIN % 4 leftover
+// channels of PER = 4 / R taps per MFMA (lane group g4: tap i PER + g4 / R, channel 4F + g4 % R;
+// offsets formed once into registers).  CIN = 10: 18 + 5 = 23 MFMAs (92 rows, as before).
+template <int CIN>
+struct CmK {
+  static constexpr int F = CIN / 4, R = CIN % 4;
+  static constexpr int PER = R ? 4 / R : 1;
+  static constexpr int NFULL = 9 * F;
+  // F even: the full quads of a tap go in MFMA pairs (2p, 2p + 1) whose lane group g4 takes the
+  // ADJACENT channels 8 q + 2 g4 and 8 q + 2 g4 + 1 -- one ds_read_b64 feeds both MFMAs
+  static constexpr bool PAIR = F % 2 == 0 && F > 0;
+  static constexpr int NMIX = R ? (9 + PER - 1) / PER : 0;
+  static constexpr int NM = NFULL + NMIX;
+};
+__device__ __forceinline__ constexpr int cm_toff(int tap) { return (tap / 3) * CM_H + tap % 3; }  // halo position
+
+template <int CIN>
+__global__ __launch_bounds__(256) void cp4d_mfma_persist_kernel(const float* __restrict__ x, int hA, int wA, int hB,
+                                                                int wB, int ntiles, const float* __restrict__ Wa,
+                                                                const float* __restrict__ ba,
+                                                                const float* __restrict__ Wb,
+                                                                const float* __restrict__ bb, float* __restrict__ y,
+                                                                int dbg, int order) {
+  constexpr int COUT = 10;
+  using K = CmK<CIN>;
+  constexpr int NM = K::NM, NMIX = K::NMIX;
+  __shared__ __attribute__((aligned(16))) float xa[CmLds<CIN>::EA + 2];
+  __shared__ __attribute__((aligned(16))) float xb[CmLds<CIN>::EB + 2];
+  const int NA = hA * wA, NB = hB * wB;
+  const int ntb = (wB + CM_T - 1) / CM_T, nta = (wA + CM_T - 1) / CM_T;
+  const int NTB = ntb * ((hB + CM_T - 1) / CM_T), NTA = nta * ((hA + CM_T - 1) / CM_T);
+  const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int r = lane & 15, g4 = lane >> 4;
+  CmSched sc = cm_sched(ntiles, order);
+  if (sc.cur >= sc.end) return;
+  int tile = cm_order(sc.cur, order, NTA, NTB, ntb);
+  CmRegs<CIN> R;
+  cm_load<CIN>(R, x, hA, wA, hB, wB, cm_tile(tile, nta, ntb, NTA, NTB));
+  // weights (B operand: column r = output channel) in this K order, and the mixed MFMAs' offsets
+  float wra[NM], wrb[NM];
+  int mixa[NMIX > 0 ? NMIX : 1], mixb[NMIX > 0 ? NMIX : 1];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    int tap, c;
+    bool kin;
+    if (m < K::NFULL && K::PAIR) {
+      const int pp = m / 2, h = m % 2;
+      tap = pp / (K::F / 2);
+      c = 8 * (pp % (K::F / 2)) + 2 * g4 + h;
+      kin = true;
+    } else if (m < K::NFULL) {
+      tap = m / K::F;
+      c = 4 * (m % K::F) + g4;
+      kin = true;
+    } else {
+      const int i = m - K::NFULL;
+      tap = i * K::PER + g4 / (K::R ? K::R : 1);
+      c = 4 * K::F + g4 % (K::R ? K::R : 1);
+      kin = g4 / (K::R ? K::R : 1) < K::PER && tap < 9;
+      if (!kin) tap = c = 0;
+      mixa[i] = cm_toff(tap) * CM_NT * CIN + c;
+      mixb[i] = cm_toff(tap) * CIN + c;
+    }
+    const bool live = kin && r < COUT;
+    wra[m] = live ? Wa[(r * CIN + c) * 9 + tap] : 0.f;
+    wrb[m] = live ? Wb[(r * CIN + c) * 9 + tap] : 0.f;
+  }
+  const float bias = r < COUT ? ba[r] + bb[r] : 0.f;
+  // row r of group j: a tile position (wv, j), b tile position r = (by, bx)
+  const int by = r / CM_T, bx = r % CM_T;
+  const float* pa = xa + (wv * CM_H * CM_NT + r) * CIN;                // + j CM_NT CIN + offsets
+  const float* pb = xb + (wv * CM_T * CM_NH + by * CM_H + bx) * CIN;   // + j CM_NH CIN + offsets
+  for (;;) {
+    const CmTile T = cm_tile(tile, nta, ntb, NTA, NTB);
+    sc.cur += sc.step;
+    const bool more = sc.cur < sc.end;
+    tile = cm_order(more ? sc.cur : 0, order, NTA, NTB, ntb);
+    __syncthreads();  // the previous tile's LDS reads are done
+    cm_store<CIN>(R, xa, xb);
+    __syncthreads();
+    if (more && !(dbg & 2)) cm_load<CIN>(R, x, hA, wA, hB, wB, cm_tile(tile, nta, ntb, NTA, NTB));
+    f32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int m = 0; m < (K::PAIR ? K::NFULL : 0); m += 2) {
+      if (dbg & 1) break;
+      const int pp = m / 2, tap = pp / (K::F / 2), q8 = 8 * (pp % (K::F / 2)) + 2 * g4;
+      const int oa = cm_toff(tap) * CM_NT * CIN + q8, ob = cm_toff(tap) * CIN + q8;
+      f32x2 va[4], vb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        va[j] = *(const f32x2*)(pa + j * CM_NT * CIN + oa);
+        vb[j] = *(const f32x2*)(pb + j * CM_NH * CIN + ob);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[j][h], wra[m + h], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[j][h], wrb[m + h], acc[j], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int m = K::PAIR ? K::NFULL : 0; m < NM; ++m) {
+      if (dbg & 1) break;  // timing study: staging only (CWT_CP4D_DBG=1); 2: compute only
+      int oa, ob;
+      if (m < K::NFULL) {
+        oa = cm_toff(m / K::F) * CM_NT * CIN + 4 * (m % K::F) + g4;
+        ob = cm_toff(m / K::F) * CIN + 4 * (m % K::F) + g4;
+      } else {
+        oa = mixa[m - K::NFULL];
+        ob = mixb[m - K::NFULL];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[j * CM_NT * CIN + oa], wra[m], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(pb[j * CM_NH * CIN + ob], wrb[m], acc[j], 0, 0, 0);
+    }
+    // D: lane (col o = r, rows 4 g4 + i) -> pair (a = (wv, j), b = 4 g4 + i), channel o
+    if (r < COUT) {
+      float* yz = y + (long)T.z * NA * NB * COUT;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ha = T.ha0 + wv, wa = T.wa0 + j;
+        if (ha >= hA || wa >= wA) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int hb = T.hb0 + g4, wb = T.wb0 + i;
+          if (hb < hB && wb < wB) yz[((long)(ha * wA + wa) * NB + hb * wB + wb) * COUT + r] = fmaxf(acc[j][i] + bias, 0.f);
+        }
+      }
+    }
+    if (!more) break;
+  }
+}
+
+// COUT = 1, persistent: cp4d_c1_kernel's per-pair arithmetic over the same staged tiles
+template <int CIN>
+__global__ __launch_bounds__(256) void cp4d_c1_persist_kernel(const float* __restrict__ x, int hA, int wA, int hB,
+                                                              int wB, int ntiles, const float* __restrict__ Wa,
+                                                              const float* __restrict__ ba,
+                                                              const float* __restrict__ Wb,
+                                                              const float* __restrict__ bb, float* __restrict__ y,
+                                                              int dbg, int order) {
+  static_assert(CIN % 2 == 0, "pairs of channels");
+  __shared__ __attribute__((aligned(16))) float xa[CmLds<CIN>::EA + 2];
+  __shared__ __attribute__((aligned(16))) float xb[CmLds<CIN>::EB + 2];
+  __shared__ __attribute__((aligned(16))) float wl[2][9][CIN];
+  const int NA = hA * wA, NB = hB * wB;
+  const int ntb = (wB + CM_T - 1) / CM_T, nta = (wA + CM_T - 1) / CM_T;
+  const int NTB = ntb * ((hB + CM_T - 1) / CM_T), NTA = nta * ((hA + CM_T - 1) / CM_T);
+  const int t = threadIdx.x;
+  CmSched sc = cm_sched(ntiles, order);
+  if (sc.cur >= sc.end) return;
+  int tile = cm_order(sc.cur, order, NTA, NTB, ntb);
+  CmRegs<CIN> R;
+  cm_load<CIN>(R, x, hA, wA, hB, wB, cm_tile(tile, nta, ntb, NTA, NTB));
+  if (t < 2 * 9 * CIN) {
+    const int c = t % CIN, tap = (t / CIN) % 9, side = t / (9 * CIN);
+    (&wl[0][0][0])[t] = (side ? Wb : Wa)[c * 9 + tap];
+  }
+  const float bias = ba[0] + bb[0];
+  const int at = t / CM_NT, bt = t % CM_NT;
+  const int ay = at / CM_T, ax = at % CM_T, by = bt / CM_T, bx = bt % CM_T;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  for (;;) {
+    const CmTile T = cm_tile(tile, nta, ntb, NTA, NTB);
+    sc.cur += sc.step;
+    const bool more = sc.cur < sc.end;
+    tile = cm_order(more ? sc.cur : 0, order, NTA, NTB, ntb);
+    __syncthreads();
+    cm_store<CIN>(R, xa, xb);
+    __syncthreads();
+    if (more && !(dbg & 2)) cm_load<CIN>(R, x, hA, wA, hB, wB, cm_tile(tile, nta, ntb, NTA, NTB));
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (dbg & 1) break;
+      const int ky = tap / 3, kx = tap % 3;
+      const float* pa = &xa[(((ay + ky) * CM_H + ax + kx) * CM_NT + bt) * CIN];
+      const float* pb = &xb[(at * CM_NH + (by + ky) * CM_H + bx + kx) * CIN];
+#pragma unroll
+      for (int c2 = 0; c2 < CIN / 2; ++c2) {
+        const f32x2 va = *(const f32x2*)(pa + 2 * c2), vb = *(const f32x2*)(pb + 2 * c2);
+        const f32x2 wa = *(const f32x2*)&wl[0][tap][2 * c2], wb = *(const f32x2*)&wl[1][tap][2 * c2];
+        s0 = fmaf(wa[0], va[0], s0);
+        s1 = fmaf(wa[1], va[1], s1);
+        s0 = fmaf(wb[0], vb[0], s0);
+        s1 = fmaf(wb[1], vb[1], s1);
+      }
+    }
+    const int ha = T.ha0 + ay, wa = T.wa0 + ax, hb = T.hb0 + by, wb = T.wb0 + bx;
+    if (ha < hA && wa < wA && hb < hB && wb < wB)
+      y[(long)T.z * NA * NB + (long)(ha * wA + wa) * NB + hb * wB + wb] = fmaxf((s0 + s1) + bias, 0.f);
+    if (!more) break;
+  }
+}
+
 // x [B][C][P] (channel planes) -> y [B][P][C] (channels last)
 __global__ void to_channels_last_kernel(const float* __restrict__ x, int B, int C, long P, float* __restrict__ y) {
   const long total = (long)B * C * P;
@@ -821,8 +1136,36 @@ int launch_mutual_matching(const float* x, int B, int NA, int NB, int C, float* 
 
 int launch_cp4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* Wa,
                       const float* ba, const float* Wb, const float* bb, float* y, hipStream_t st) {
-  // the matrix-core / register-blocked forms (round 4); CWT_CP4D_MFMA=0 selects the scalar kernel
+  // the matrix-core / register-blocked forms (round 4): persistent workgroups with the next
+  // tile's loads in flight (default), CWT_CP4D_PERSIST=0 the one-tile-per-workgroup kernels;
+  // CWT_CP4D_MFMA=0 selects the scalar kernel
   static const bool mfma = !(getenv("CWT_CP4D_MFMA") && getenv("CWT_CP4D_MFMA")[0] == '0');
+  static const bool persist = !(getenv("CWT_CP4D_PERSIST") && getenv("CWT_CP4D_PERSIST")[0] == '0');
+  if (mfma && persist) {
+    const int ntiles = cdiv(hB, CM_T) * cdiv(wB, CM_T) * cdiv(hA, CM_T) * cdiv(wA, CM_T) * B;
+    static const int dbg = getenv("CWT_CP4D_DBG") ? atoi(getenv("CWT_CP4D_DBG")) : 0;  // timing study only
+    static const int order = getenv("CWT_CP4D_ORDER") ? atoi(getenv("CWT_CP4D_ORDER")) : 2;  // cm_sched
+    int dev = 0, cu = 0;
+    CWT_HIP(hipGetDevice(&dev));
+    CWT_HIP(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev));
+#define CWT_CPP(CI, KERNEL)                                                                                  \
+  if (cin == CI) {                                                                                           \
+    static int occ = 0;                                                                                      \
+    if (!occ) CWT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (KERNEL<CI>), 256, 0));             \
+    const int G = std::max(1, std::min(ntiles, std::max(1, occ) * cu));  /* a multiple of 8 when cu is */      \
+    hipLaunchKernelGGL((KERNEL<CI>), dim3(G), dim3(256), 0, st, x, hA, wA, hB, wB, ntiles, Wa, ba, Wb, bb, y, dbg, order); \
+    CWT_LAUNCH_CHECK();                                                                                      \
+    return 0;                                                                                                \
+  }
+    if (cout == 10) {
+      CWT_CPP(1, cp4d_mfma_persist_kernel)
+      CWT_CPP(2, cp4d_mfma_persist_kernel)
+      CWT_CPP(10, cp4d_mfma_persist_kernel)
+    } else if (cout == 1) {
+      CWT_CPP(10, cp4d_c1_persist_kernel)
+    }
+#undef CWT_CPP
+  }
   if (mfma) {
     const dim3 g4(cdiv(hB, CM_T) * cdiv(wB, CM_T), cdiv(hA, CM_T) * cdiv(wA, CM_T), B);
 #define CWT_CPM(CI, KERNEL)                                                                             \

@@ -193,6 +193,28 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
   stamp(0);
   __syncthreads();
 
+  // this workgroup's first token chunk (f_q is an input): its loads fly under P0 and barrier 1;
+  // the registers of its LAST chunk stay live into P4 (the classifier reads the same tokens)
+  f32x4 fa[TL_TPW], fb[TL_TPW];
+  float invs[TL_TPW];
+  auto load_chunk = [&](int ci) {
+    const int b = ci / nchunk, chunk = ci - b * nchunk;
+    const int tok0 = chunk * TL_TPB + wv * TL_TPW;
+#pragma unroll
+    for (int tt = 0; tt < TL_TPW; ++tt) {
+      const int p = tok0 + tt;
+      if (p < hw) {
+        const float* src = a.f + ((long)b * hw + p) * C + 4 * lane;
+        fa[tt] = *(const f32x4*)src;
+        fb[tt] = *(const f32x4*)(src + 256);
+      } else {
+        fa[tt] = fb[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  const int last_ci = gi < B * nchunk ? gi + ((B * nchunk - 1 - gi) / G) * G : -1;
+  if (gi < B * nchunk) load_chunk(gi);
+
   // ---- P0: r[v][h*C + k] = M[h*C + k] . q[v] / sqrt(C) (rowdot_kernel<8>'s per-lane partition) ----
   {
     const float alpha = 1.0f / sqrtf((float)C);
@@ -231,18 +253,7 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
         b_loaded = b;
       }
       const int tok0 = chunk * TL_TPB + wv * TL_TPW;
-      f32x4 fa[TL_TPW], fb[TL_TPW];
-#pragma unroll
-      for (int tt = 0; tt < TL_TPW; ++tt) {
-        const int p = tok0 + tt;
-        if (p < hw) {
-          const float* src = a.f + ((long)b * hw + p) * C + 4 * lane;
-          fa[tt] = *(const f32x4*)src;
-          fb[tt] = *(const f32x4*)(src + 256);
-        } else {
-          fa[tt] = fb[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
+      if (ci != gi) load_chunk(ci);  // the first one was loaded before P0
       __syncthreads();
       float v[64];
 #pragma unroll
@@ -270,7 +281,9 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
       const bool valid = score_lane && p < hw;
       const float nrm2 = __shfl(red, 32 + my_t * 8, 64);
       const float inv = 1.0f / fmaxf(sqrtf(nrm2), 1e-12f);
-      if (valid && my_rho == 0) a.inv[(long)b * hw + p] = inv;  // read back by this workgroup only (P4)
+#pragma unroll
+      for (int tt = 0; tt < TL_TPW; ++tt) invs[tt] = __shfl(inv, tt * NR, 64);  // lane tt NR: token tt
+      if (ci != last_ci && valid && my_rho == 0) a.inv[(long)b * hw + p] = inv;  // read back by this workgroup only (P4)
       if (lane >= 32 && ((lane & 7) == 1 || (lane & 7) == 2)) {
         const int pt = tok0 + ((lane - 32) >> 3);
         if (pt < hw) st1(a.logits0 + ((long)b * 2 + (lane & 7) - 1) * hw + pt, red);
@@ -464,8 +477,9 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
       }
     }
     __syncthreads();
-    for (int ci = gi; ci < B * nchunk; ci += G) {
+    for (int ci = last_ci; ci >= 0; ci -= G) {  // the last token chunk first: its tokens are in registers
       const int b = ci / nchunk, chunk = ci - b * nchunk;
+      const bool regs = ci == last_ci;
       const f32x4 w0a = *(const f32x4*)&L.w2[2 * b][lane * 4], w0b = *(const f32x4*)&L.w2[2 * b][256 + lane * 4];
       const f32x4 w1a = *(const f32x4*)&L.w2[2 * b + 1][lane * 4], w1b = *(const f32x4*)&L.w2[2 * b + 1][256 + lane * 4];
 #pragma unroll
@@ -473,7 +487,7 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
         const int p = chunk * TL_TPB + wv * TL_TPW + tt;
         if (p >= hw) break;
         const float* src = a.f + ((long)b * hw + p) * C + lane * 4;
-        const f32x4 u = *(const f32x4*)src, vv = *(const f32x4*)(src + 256);
+        const f32x4 u = regs ? fa[tt] : *(const f32x4*)src, vv = regs ? fb[tt] : *(const f32x4*)(src + 256);
         float s0 = 0.f, s1 = 0.f;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
@@ -485,7 +499,7 @@ __global__ __launch_bounds__(TL_T) void episode_tail_kernel(TailArgs a) {
         s0 = wave_sum_dpp(s0);
         s1 = wave_sum_dpp(s1);
         if (lane == 0) {
-          const float iv = ld1(a.inv + (long)b * hw + p);
+          const float iv = regs ? invs[tt] : ld1(a.inv + (long)b * hw + p);
           st1(a.logits + (long)b * 2 * hw + p, s0 * iv);
           st1(a.logits + (long)b * 2 * hw + hw + p, s1 * iv);
         }
