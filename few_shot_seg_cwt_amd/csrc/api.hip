@@ -280,9 +280,15 @@ static int zero_line(cwt_ctx* ctx, const __bf16** out) {
 // 1x1 conv's fp32 packing is plain row-major [Co][Ci]); the epilogue is fmaf(acc, 1, bias) then
 // + res, the order of the separate bias / residual passes it replaces.  Shapes: K % 32 == 0,
 // N % 64 == 0, 16-B aligned operands (gemm_f32d_ok); the rest stay on corr_gemm_kernel.
-// CWT_GEMM_F32D=0 keeps every GEMM there (A/B).
+// Used for MatchNet's readout and cwt_linear; WeightAverage's two GEMMs measured slower on it
+// with the heuristic plans (0.72 against 0.66 ms for the layer-4 module, profiles/r4/run_i) and
+// stay on corr_gemm_kernel unless CWT_GEMM_F32D=2.  CWT_GEMM_F32D=0 keeps every GEMM there.
+static int gemm_f32d_mode() {
+  static const int m = getenv("CWT_GEMM_F32D") ? atoi(getenv("CWT_GEMM_F32D")) : 1;
+  return m;
+}
 static bool gemm_f32d_ok(int M, int N, int K, const void* A, const void* Bm, const void* Cm, const void* res) {
-  static const bool on = !(getenv("CWT_GEMM_F32D") && getenv("CWT_GEMM_F32D")[0] == '0');
+  const bool on = gemm_f32d_mode() != 0;
   const uintptr_t al = (uintptr_t)A | (uintptr_t)Bm | (uintptr_t)Cm | (uintptr_t)res;
   return on && M >= 1 && K % 32 == 0 && N % 64 == 0 && N <= 8192 && (al & 15) == 0;
 }
@@ -1632,13 +1638,14 @@ int cwt_weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C,
     return rc;
   Prof p(ctx, st, "weight_average c" + std::to_string(C), 2.0 * P * C * co * 4, 4.0 * P * (2.0 * C + 5.0 * co));
   // theta | phi | g of every pixel: one GEMM against the three stacked 1x1 weights [3co][C]
-  if (gemm_f32d_ok((int)P, 3 * co, C, x, w_tpg, tpg, nullptr)) {
+  const bool wa_f32d = gemm_f32d_mode() == 2;
+  if (wa_f32d && gemm_f32d_ok((int)P, 3 * co, C, x, w_tpg, tpg, nullptr)) {
     if ((rc = gemm_f32d(ctx, x, w_tpg, (int)P, 3 * co, C, (float*)tpg, nullptr, nullptr, 0, st))) return rc;
   } else if ((rc = launch_gemm_abt(x, w_tpg, 1, (int)P, 3 * co, C, (float*)tpg, st))) {
     return rc;
   }
   if ((rc = launch_wa_attn((const float*)tpg, N, h, w, co, b_theta, b_phi, b_g, (float*)wavg, st))) return rc;
-  if (gemm_f32d_ok((int)P, C, co, wavg, w_back, out, x)) {  // conv_back + bias + residual in one epilogue
+  if (wa_f32d && gemm_f32d_ok((int)P, C, co, wavg, w_back, out, x)) {  // conv_back + bias + residual in one epilogue
     if ((rc = gemm_f32d(ctx, (const float*)wavg, w_back, (int)P, C, co, out, b_back, x, C, st))) return rc;
   } else {
     if ((rc = launch_gemm_abt((const float*)wavg, w_back, 1, (int)P, C, co, (float*)back, st))) return rc;

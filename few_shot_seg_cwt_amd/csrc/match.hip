@@ -1136,15 +1136,19 @@ int launch_mutual_matching(const float* x, int B, int NA, int NB, int C, float* 
 
 int launch_cp4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* Wa,
                       const float* ba, const float* Wb, const float* bb, float* y, hipStream_t st) {
-  // the matrix-core / register-blocked forms (round 4): persistent workgroups with the next
-  // tile's loads in flight (default), CWT_CP4D_PERSIST=0 the one-tile-per-workgroup kernels;
+  // the matrix-core / register-blocked forms (round 4): for 10 -> 10 persistent workgroups with
+  // the next tile's loads in flight (1,169 against 1,207 us at 60^2; the 2 -> 10 and 10 -> 1
+  // layers measured slower that way: 331 / 605 against 297 / 471 us, profiles/r4/run_i), the
+  // rest one tile per workgroup; CWT_CP4D_PERSIST=0 / 2: none / all persistent (A/B);
   // CWT_CP4D_MFMA=0 selects the scalar kernel
   static const bool mfma = !(getenv("CWT_CP4D_MFMA") && getenv("CWT_CP4D_MFMA")[0] == '0');
-  static const bool persist = !(getenv("CWT_CP4D_PERSIST") && getenv("CWT_CP4D_PERSIST")[0] == '0');
+  static const int persist_mode = getenv("CWT_CP4D_PERSIST") ? atoi(getenv("CWT_CP4D_PERSIST")) : 1;
+  const bool persist = persist_mode == 2 || (persist_mode == 1 && cin == 10 && cout == 10);
   if (mfma && persist) {
     const int ntiles = cdiv(hB, CM_T) * cdiv(wB, CM_T) * cdiv(hA, CM_T) * cdiv(wA, CM_T) * B;
     static const int dbg = getenv("CWT_CP4D_DBG") ? atoi(getenv("CWT_CP4D_DBG")) : 0;  // timing study only
-    static const int order = getenv("CWT_CP4D_ORDER") ? atoi(getenv("CWT_CP4D_ORDER")) : 2;  // cm_sched
+    // cm_sched: order 1 cuts the 10 -> 10 layer's L2 misses 25 -> 15 M per launch at the same time
+    static const int order = getenv("CWT_CP4D_ORDER") ? atoi(getenv("CWT_CP4D_ORDER")) : 1;
     int dev = 0, cu = 0;
     CWT_HIP(hipGetDevice(&dev));
     CWT_HIP(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev));

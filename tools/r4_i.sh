@@ -21,4 +21,8 @@ done
 cd $R
 CWT_GEMM_F32D=0 timeout -k 10 200 python -u tools/time_match.py 1 5 > $O/time_gemm_old.json 2> $O/time_gemm_old.err || exit $?
 timeout -k 10 200 python -u tools/time_match.py 1 5 > $O/time_gemm_f32d.json 2> $O/time_gemm_f32d.err || exit $?
+for v in p0f1 p1f1 p0f0 p0f1 p1f1 p0f0; do
+  CWT_PIPE_ADAPT_PRIO=${v:1:1} CWT_FUSED_TAIL=${v:3:1} timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 \
+    --exact-steps 0 --pair-steps 0 --no-cpu-baseline >> $O/bench_$v.jsonl 2>> $O/bench_ab.err || exit $?
+done
 echo done
