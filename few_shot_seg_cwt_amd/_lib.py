@@ -70,6 +70,14 @@ SIGNATURES = {
     "cwt_match_readout": (_I, [_P, _P, _I, _I, _I, _F, _P, _I, _P, _P]),
     "cwt_weight_average": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cwt_mmn_blend": (_I, [_P, _P, _P, _I, _I64, _F, _P, _P, _P]),
+    "cwt_match_corr_saved_floats": (_I, [_I, _I, _I, _I, _I, _I, C.POINTER(_I64)]),
+    "cwt_match_corr_forward_train": (_I, [_P, _P, _I, _I, _I, _I, _P, _I, _F, _P, _I, _P, _P, _P, _P]),
+    "cwt_match_corr_backward": (_I, [_P, _P, _I, _I, _I, _I, _P, _I, _F, _P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "cwt_corr_backward": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _P]),
+    "cwt_weight_average_train": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cwt_weight_average_backward": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                         _P, _P, _P]),
+    "cwt_mmn_blend_backward": (_I, [_P, _P, _P, _I, _I64, _F, _P, _P, _P]),
     "cwt_linear": (_I, [_P, _P, _I64, _I, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_sine_pos_add": (_I, [_P, _P, _I, _I, _I, _I, _F, _I, _F, _F, _P, _P]),
     "cwt_deform_attn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),

@@ -1445,9 +1445,36 @@ int cwt_mutual_matching(cwt_ctx* ctx, const float* x, int B, int NA, int NB, int
   return launch_mutual_matching(x, B, NA, NB, C, y, rm, cp, cm, (hipStream_t)stream);
 }
 
+// the activations the corr_forward backward reads (cwt_match_corr_forward_train), carved from one
+// caller buffer: x0 = MutualMatching(corr) channels-last [E][L], o[branch][layer] the ReLU outputs
+// [E][10], [E][10], [E][1], y = o[0][2] + o[1][2] [E] (E = B NA NB), attn [B][NA][ld32(NB)]
+struct MatchSaved {
+  float* x0;
+  float* o[2][3];
+  float* y;
+  float* attn;
+};
+static size_t match_saved_layout(float* base, int B, int L, long NA, int symmetric, int readout, MatchSaved* s) {
+  const long E = (long)B * NA * NA, ldp = (NA + 31) & ~31L;
+  size_t off = 0;
+  auto take = [&](long n) {
+    float* p = base ? base + off : nullptr;
+    off += (size_t)n;
+    return p;
+  };
+  MatchSaved d;
+  d.x0 = take(E * L);
+  for (int br = 0; br < 2; ++br)
+    for (int l = 0; l < 3; ++l) d.o[br][l] = (br == 0 || symmetric) ? take(E * (l < 2 ? 10 : 1)) : nullptr;
+  d.y = take(E);
+  d.attn = readout ? take((long)B * NA * ldp) : nullptr;
+  if (s) *s = d;
+  return off;
+}
+
 static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
                               int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
-                              void* stream, bool cv4) {
+                              void* stream, bool cv4, float* saved = nullptr) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
   CWT_CHECK(corr && nc_params && corr2d && B >= 1 && (L == 1 || L == 2) && h >= 1 && w >= 1,
             "bad arguments (in_channel 1 or 2)");
@@ -1463,6 +1490,12 @@ static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int
       (rc = ensure_ws(ctx, "match.y1", (size_t)B * P * 4, &y1)) ||
       (rc = ensure_ws(ctx, "match.y2", (size_t)B * P * 4, &y2)))
     return rc;
+  MatchSaved S;
+  if (saved) {
+    CWT_CHECK(!cv4, "the training forward keeps CenterPivotConv4d ('red') activations only");
+    match_saved_layout(saved, B, L, NA, symmetric, weighted_v != nullptr, &S);
+    x0 = S.x0;
+  }
   float *rm, *cp, *cm;
   if ((rc = mm_ws(ctx, B, (int)NA, (int)NB, L, &rm, &cp, &cm))) return rc;
   Prof p(ctx, st, "match_corr_forward", 2.0 * B * P * 2 * (18.0 * L * 10 + 18.0 * 100 + 18.0 * 10), 4.0 * B * P * (L + 1));
@@ -1513,6 +1546,8 @@ static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int
   for (int br = 0; br < (symmetric ? 2 : 1); ++br) {
     const float* in = (const float*)x0;
     float* outs[3] = {(float*)x1, (float*)x2, br ? (float*)y2 : (float*)y1};
+    if (saved)
+      for (int l = 0; l < 3; ++l) outs[l] = S.o[br][l];
     for (int l = 0; l < 3; ++l) {
       const float* Wa = br ? lw[l][2] : lw[l][0];
       const float* ba = br ? lw[l][3] : lw[l][1];
@@ -1523,7 +1558,13 @@ static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int
     }
   }
   }
-  if (symmetric && (rc = launch_add_inplace((float*)y1, (const float*)y2, B * P, st))) return rc;
+  if (saved) {  // y = o[0][2] (+ o[1][2]) into its own slot: the ReLU outputs stay for the backward
+    CWT_HIP(hipMemcpyAsync(S.y, S.o[0][2], (size_t)B * P * 4, hipMemcpyDeviceToDevice, st));
+    if (symmetric && (rc = launch_add_inplace(S.y, (const float*)S.o[1][2], B * P, st))) return rc;
+    y1 = S.y;
+  } else if (symmetric && (rc = launch_add_inplace((float*)y1, (const float*)y2, B * P, st))) {
+    return rc;
+  }
   if ((rc = mm_ws(ctx, B, (int)NA, (int)NB, 1, &rm, &cp, &cm))) return rc;
   if ((rc = launch_mutual_matching((const float*)y1, B, (int)NA, (int)NB, 1, corr2d, rm, cp, cm, st))) return rc;
   if (weighted_v) {
@@ -1534,6 +1575,7 @@ static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int
     if ((rc = ensure_ws(ctx, "match.attn", (size_t)B * NA * ldp * 4, &pw)) ||
         (rc = ensure_ws(ctx, "match.vt", (size_t)B * Cv * ldp * 4, &vt)))
       return rc;
+    if (saved) pw = S.attn;
     if ((rc = launch_match_softmax(corr2d, B, (int)NA, (int)NB, temp, ldp, (float*)pw, st))) return rc;
     if ((rc = launch_match_vt(v, B, (int)NB, Cv, ldp, (float*)vt, st))) return rc;
     if ((rc = readout_gemm(ctx, (const float*)pw, (const float*)vt, B, (int)NA, Cv, ldp, weighted_v, st))) return rc;
@@ -1552,6 +1594,220 @@ int cwt_match_corr_forward_cv4(cwt_ctx* ctx, const float* corr, int B, int L, in
                                int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
                                void* stream) {
   return match_corr_forward(ctx, corr, B, L, h, w, nc_params, symmetric, temp, v, Cv, corr2d, weighted_v, stream, true);
+}
+
+// ---- MatchNet / MMN backward (match_bwd.hip) ----
+static inline long ld32(long n) { return (n + 31) & ~31L; }
+
+// C [M][N] = A [M][K] . W [N][K]^T (K % 4 == 0): the exact-fp32 conv body where its shape rules
+// allow (gemm_f32d), else corr_gemm_kernel
+static int gemm_nt(cwt_ctx* ctx, const float* A, const float* W, int M, int N, int K, float* C, hipStream_t st) {
+  if (gemm_f32d_ok(M, N, K, A, W, C, nullptr)) return gemm_f32d(ctx, A, W, M, N, K, C, nullptr, nullptr, 0, st);
+  if (K % 4) return fail(CWT_EARG, "gemm_nt: K % 4 != 0");
+  return launch_gemm_abt(A, W, 1, M, N, K, C, st);
+}
+
+static int mm_bwd_ws(cwt_ctx* ctx, int B, int NA, int NB, int C, MmBwdWs* w) {
+  const long nrb = cdiv(NA, 16), bc = (long)B * C;
+  const char* nm[8] = {"mb.rowmax", "mb.rowarg", "mb.colpv", "mb.colpi", "mb.colmax", "mb.colarg", "mb.srow", "mb.scol"};
+  const long sz[8] = {bc * NA, bc * NA, bc * nrb * NB, bc * nrb * NB, bc * NB, bc * NB, bc * NA, bc * NB};
+  void* p[8];
+  int rc;
+  for (int i = 0; i < 8; ++i)
+    if ((rc = ensure_ws(ctx, nm[i], (size_t)sz[i] * 4, &p[i]))) return rc;
+  w->rowmax = (float*)p[0];
+  w->rowarg = (int*)p[1];
+  w->colpv = (float*)p[2];
+  w->colpi = (int*)p[3];
+  w->colmax = (float*)p[4];
+  w->colarg = (int*)p[5];
+  w->srow = (float*)p[6];
+  w->scol = (float*)p[7];
+  return 0;
+}
+
+int cwt_match_corr_saved_floats(int B, int L, int h, int w, int symmetric, int readout, int64_t* n) {
+  if (!n || B < 1 || (L != 1 && L != 2) || h < 1 || w < 1) return fail(CWT_EARG, "bad arguments");
+  *n = (int64_t)match_saved_layout(nullptr, B, L, (long)h * w, symmetric, readout, nullptr);
+  return 0;
+}
+
+int cwt_match_corr_forward_train(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
+                                 int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
+                                 float* saved, void* stream) {
+  if (!saved) return fail(CWT_EARG, "saved is NULL");
+  return match_corr_forward(ctx, corr, B, L, h, w, nc_params, symmetric, temp, v, Cv, corr2d, weighted_v, stream, false,
+                            saved);
+}
+
+int cwt_match_corr_backward(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
+                            int symmetric, float temp, const float* v, int Cv, const float* saved,
+                            const float* d_corr2d, const float* d_weighted_v, float* d_corr, float* d_params,
+                            float* d_v, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(corr && nc_params && saved && d_params && B >= 1 && (L == 1 || L == 2) && h >= 1 && w >= 1,
+            "bad arguments (in_channel 1 or 2)");
+  CWT_CHECK(!d_weighted_v || (v && Cv >= 4 && Cv % 4 == 0), "d_weighted_v needs v and Cv % 4 == 0");
+  CWT_CHECK(!d_v || d_weighted_v, "d_v needs d_weighted_v");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  const long NA = (long)h * w, NB = NA, P = NA * NB, E = (long)B * P, ldp = ld32(NB);
+  MatchSaved S;
+  match_saved_layout((float*)saved, B, L, NA, symmetric, d_weighted_v != nullptr, &S);
+  const int ch[4] = {L, 10, 10, 1};
+  const float* lw[3][4];
+  float* dlw[3][4];
+  long np = 0;
+  for (int l = 0; l < 3; ++l) {
+    const long n = (long)ch[l + 1] * ch[l] * 9;
+    const long off[4] = {np, np + n, np + n + ch[l + 1], np + 2 * n + ch[l + 1]};
+    for (int q = 0; q < 4; ++q) {
+      lw[l][q] = nc_params + off[q];
+      dlw[l][q] = d_params + off[q];
+    }
+    np += 2 * (n + ch[l + 1]);
+  }
+  const size_t part_floats = (size_t)cp4d_wgrad_part_floats(10, 10);
+  void *g2d, *dy, *gA, *gm, *dx0, *part;
+  int rc;
+  if ((rc = ensure_ws(ctx, "mb.g2d", (size_t)E * 4, &g2d)) || (rc = ensure_ws(ctx, "mb.dy", (size_t)E * 4, &dy)) ||
+      (rc = ensure_ws(ctx, "mb.gA", (size_t)E * 10 * 4, &gA)) || (rc = ensure_ws(ctx, "mb.gm", (size_t)E * 10 * 4, &gm)) ||
+      (rc = ensure_ws(ctx, "mb.dx0", (size_t)E * L * 4, &dx0)) || (rc = ensure_ws(ctx, "mb.part", part_floats * 4, &part)))
+    return rc;
+  MmBwdWs mw;
+  if ((rc = mm_bwd_ws(ctx, B, (int)NA, (int)NB, L, &mw))) return rc;
+  Prof p(ctx, st, "match_corr_backward", 2.0 * 2.0 * B * P * 2 * (18.0 * L * 10 + 18.0 * 100 + 18.0 * 10),
+         4.0 * B * P * (L + 44));
+  CWT_HIP(hipMemsetAsync(d_params, 0, (size_t)np * 4, st));
+  // the gradient at corr2d: the caller's, plus the softmax readout's (match.py:151-153)
+  if (d_corr2d)
+    CWT_HIP(hipMemcpyAsync(g2d, d_corr2d, (size_t)E * 4, hipMemcpyDeviceToDevice, st));
+  else
+    CWT_HIP(hipMemsetAsync(g2d, 0, (size_t)E * 4, st));
+  if (d_weighted_v) {
+    void* dA;
+    if ((rc = ensure_ws(ctx, "mb.dA", (size_t)E * 4, &dA))) return rc;
+    for (int b = 0; b < B; ++b)  // dA = d_wv . v^T
+      if ((rc = gemm_nt(ctx, d_weighted_v + (long)b * NA * Cv, v + (long)b * NB * Cv, (int)NA, (int)NB, Cv,
+                        (float*)dA + (long)b * NA * NB, st)))
+        return rc;
+    if ((rc = launch_match_softmax_bwd(S.attn, (int)ldp, (const float*)dA, (int)(B * NA), (int)NB, temp, 1,
+                                       (float*)g2d, st)))
+      return rc;
+    if (d_v) {  // d_v[b] = attn[b]^T . d_wv[b]
+      const long lda = ld32(NA);
+      void *pt, *dwt;
+      if ((rc = ensure_ws(ctx, "mb.PT", (size_t)B * ldp * lda * 4, &pt)) ||
+          (rc = ensure_ws(ctx, "mb.dwvT", (size_t)B * Cv * lda * 4, &dwt)))
+        return rc;
+      if ((rc = launch_match_vt(S.attn, B, (int)NA, (int)ldp, (int)lda, (float*)pt, st)) ||
+          (rc = launch_match_vt(d_weighted_v, B, (int)NA, Cv, (int)lda, (float*)dwt, st)))
+        return rc;
+      for (int b = 0; b < B; ++b)
+        if ((rc = gemm_nt(ctx, (const float*)pt + (long)b * ldp * lda, (const float*)dwt + (long)b * Cv * lda, (int)NB, Cv,
+                          (int)lda, d_v + (long)b * NB * Cv, st)))
+          return rc;
+    }
+  }
+  // the second MutualMatching (match.py:162)
+  if ((rc = launch_mutual_matching_bwd(S.y, (const float*)g2d, B, (int)NA, (int)NB, 1, (float*)dy, mw, st))) return rc;
+  // NeighConsensus: both branches see the same output gradient (y = branch 0 + branch 1); branch 1
+  // applied conv2's filter over the a plane and conv1's over the b plane (match.py:75-80)
+  for (int br = 0; br < (symmetric ? 2 : 1); ++br) {
+    const float* gcur = (const float*)dy;
+    for (int l = 2; l >= 0; --l) {
+      const int cin = ch[l], cout = ch[l + 1];
+      const float* out = S.o[br][l];
+      const float* in = l ? S.o[br][l - 1] : S.x0;
+      if ((rc = launch_relu_mask(gcur, out, E * cout, (float*)gm, st))) return rc;
+      const float* Wa = br ? lw[l][2] : lw[l][0];
+      const float* Wb = br ? lw[l][0] : lw[l][2];
+      float* dWa = br ? dlw[l][2] : dlw[l][0];
+      float* dWb = br ? dlw[l][0] : dlw[l][2];
+      if ((rc = launch_cp4d_wgrad(in, (const float*)gm, B, h, w, h, w, cin, cout, (float*)part, part_floats, dWa, dWb,
+                                  dlw[l][1], dlw[l][3], st)))
+        return rc;
+      if (l > 0) {
+        if ((rc = launch_cp4d_dgrad((const float*)gm, B, h, w, h, w, cout, cin, Wa, Wb, (float*)gA, 0, st))) return rc;
+        gcur = (const float*)gA;
+      } else if (d_corr) {
+        if ((rc = launch_cp4d_dgrad((const float*)gm, B, h, w, h, w, cout, cin, Wa, Wb, (float*)dx0, br, st))) return rc;
+      }
+    }
+  }
+  // the first MutualMatching (match.py:160), back to the caller's channel-first layout
+  if (d_corr) {
+    if (L == 1) {
+      if ((rc = launch_mutual_matching_bwd(corr, (const float*)dx0, B, (int)NA, (int)NB, 1, d_corr, mw, st))) return rc;
+    } else {
+      void *xcl, *dxcl;
+      if ((rc = ensure_ws(ctx, "mb.xcl", (size_t)E * L * 4, &xcl)) || (rc = ensure_ws(ctx, "mb.dxcl", (size_t)E * L * 4, &dxcl)))
+        return rc;
+      if ((rc = launch_to_channels_last(corr, B, L, P, (float*)xcl, st)) ||
+          (rc = launch_mutual_matching_bwd((const float*)xcl, (const float*)dx0, B, (int)NA, (int)NB, L, (float*)dxcl, mw,
+                                           st)) ||
+          (rc = launch_to_channels_first((const float*)dxcl, B, L, P, d_corr, st)))
+        return rc;
+    }
+  }
+  p.end();
+  return 0;
+}
+
+int cwt_corr_backward(cwt_ctx* ctx, const float* q, const float* k, int B, int Pq, int Pk, int C, const float* d_sim,
+                      float* dq, float* dk, int accum_q, int accum_k, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(q && k && d_sim && B >= 1 && Pq >= 1 && Pk >= 1 && C >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  const float eps = 1e-12f;
+  void *qn, *qr, *kn, *kr;
+  int rc;
+  if ((rc = ensure_ws(ctx, "cb.qn", (size_t)B * Pq * C * 4, &qn)) || (rc = ensure_ws(ctx, "cb.qr", (size_t)B * Pq * 4, &qr)) ||
+      (rc = ensure_ws(ctx, "cb.kn", (size_t)B * Pk * C * 4, &kn)) || (rc = ensure_ws(ctx, "cb.kr", (size_t)B * Pk * 4, &kr)))
+    return rc;
+  Prof p(ctx, st, "corr_backward", 2.0 * 2.0 * B * (double)Pq * Pk * C, 4.0 * B * ((double)Pq * Pk + 2.0 * (Pq + Pk) * C));
+  if ((rc = launch_token_norm(q, (long)B * Pq, C, eps, (float*)qn, (float*)qr, st)) ||
+      (rc = launch_token_norm(k, (long)B * Pk, C, eps, (float*)kn, (float*)kr, st)))
+    return rc;
+  if (dq) {  // d qn = d_sim . kn
+    const long ldk = ld32(Pk);
+    void *dsp, *knt, *dqn;
+    if ((rc = ensure_ws(ctx, "cb.dsp", (size_t)B * Pq * ldk * 4, &dsp)) ||
+        (rc = ensure_ws(ctx, "cb.knT", (size_t)B * C * ldk * 4, &knt)) ||
+        (rc = ensure_ws(ctx, "cb.dqn", (size_t)B * Pq * C * 4, &dqn)))
+      return rc;
+    if ((rc = launch_copy_pad(d_sim, (long)B * Pq, Pk, (int)ldk, (float*)dsp, st)) ||
+        (rc = launch_match_vt((const float*)kn, B, Pk, C, (int)ldk, (float*)knt, st)))
+      return rc;
+    for (int b = 0; b < B; ++b)
+      if ((rc = gemm_nt(ctx, (const float*)dsp + (long)b * Pq * ldk, (const float*)knt + (long)b * C * ldk, Pq, C, (int)ldk,
+                        (float*)dqn + (long)b * Pq * C, st)))
+        return rc;
+    if ((rc = launch_token_norm_bwd((const float*)qn, (const float*)qr, (const float*)dqn, (long)B * Pq, C, C, eps, accum_q,
+                                    dq, st)))
+      return rc;
+  }
+  if (dk) {  // d kn = d_sim^T . qn
+    const long ldq = ld32(Pq);
+    void *dst, *qnt, *dkn;
+    if ((rc = ensure_ws(ctx, "cb.dsT", (size_t)B * Pk * ldq * 4, &dst)) ||
+        (rc = ensure_ws(ctx, "cb.qnT", (size_t)B * C * ldq * 4, &qnt)) ||
+        (rc = ensure_ws(ctx, "cb.dkn", (size_t)B * Pk * C * 4, &dkn)))
+      return rc;
+    if ((rc = launch_match_vt(d_sim, B, Pq, Pk, (int)ldq, (float*)dst, st)) ||
+        (rc = launch_match_vt((const float*)qn, B, Pq, C, (int)ldq, (float*)qnt, st)))
+      return rc;
+    for (int b = 0; b < B; ++b)
+      if ((rc = gemm_nt(ctx, (const float*)dst + (long)b * Pk * ldq, (const float*)qnt + (long)b * C * ldq, Pk, C, (int)ldq,
+                        (float*)dkn + (long)b * Pk * C, st)))
+        return rc;
+    if ((rc = launch_token_norm_bwd((const float*)kn, (const float*)kr, (const float*)dkn, (long)B * Pk, C, C, eps, accum_k,
+                                    dk, st)))
+      return rc;
+  }
+  p.end();
+  return 0;
 }
 
 int cwt_sce_descriptor(cwt_ctx* ctx, const float* x, int B, int h, int w, int C, int k, int ldg, float* g,
@@ -1619,9 +1875,9 @@ int cwt_match_readout(cwt_ctx* ctx, const float* corr2d, int B, int NA, int NB, 
   return 0;
 }
 
-int cwt_weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C, const float* w_tpg,
-                       const float* b_theta, const float* b_phi, const float* b_g, const float* w_back,
-                       const float* b_back, float* out, void* stream) {
+static int weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C, const float* w_tpg,
+                          const float* b_theta, const float* b_phi, const float* b_g, const float* w_back,
+                          const float* b_back, float* out, void* stream, float* tpg_keep, float* wavg_keep) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
   CWT_CHECK(x && w_tpg && b_theta && b_phi && b_g && w_back && b_back && out && N >= 1 && h >= 1 && w >= 1,
             "bad arguments");
@@ -1636,6 +1892,8 @@ int cwt_weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C,
       (rc = ensure_ws(ctx, "wa.avg", (size_t)P * co * 4, &wavg)) ||
       (rc = ensure_ws(ctx, "wa.back", (size_t)P * C * 4, &back)))
     return rc;
+  if (tpg_keep) tpg = tpg_keep;
+  if (wavg_keep) wavg = wavg_keep;
   Prof p(ctx, st, "weight_average c" + std::to_string(C), 2.0 * P * C * co * 4, 4.0 * P * (2.0 * C + 5.0 * co));
   // theta | phi | g of every pixel: one GEMM against the three stacked 1x1 weights [3co][C]
   const bool wa_f32d = gemm_f32d_mode() == 2;
@@ -1653,6 +1911,86 @@ int cwt_weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C,
   }
   p.end();
   return 0;
+}
+
+int cwt_weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C, const float* w_tpg,
+                       const float* b_theta, const float* b_phi, const float* b_g, const float* w_back,
+                       const float* b_back, float* out, void* stream) {
+  return weight_average(ctx, x, N, h, w, C, w_tpg, b_theta, b_phi, b_g, w_back, b_back, out, stream, nullptr, nullptr);
+}
+
+int cwt_weight_average_train(cwt_ctx* ctx, const float* x, int N, int h, int w, int C, const float* w_tpg,
+                             const float* b_theta, const float* b_phi, const float* b_g, const float* w_back,
+                             const float* b_back, float* out, float* tpg, float* wavg, void* stream) {
+  if (!tpg || !wavg) return fail(CWT_EARG, "tpg / wavg is NULL");
+  return weight_average(ctx, x, N, h, w, C, w_tpg, b_theta, b_phi, b_g, w_back, b_back, out, stream, tpg, wavg);
+}
+
+int cwt_weight_average_backward(cwt_ctx* ctx, const float* x, int N, int h, int w, int C, const float* w_tpg,
+                                const float* b_theta, const float* b_phi, const float* b_g, const float* w_back,
+                                const float* tpg, const float* wavg, const float* d_out, float* d_x,
+                                float* d_w_tpg, float* d_b_theta, float* d_b_phi, float* d_b_g, float* d_w_back,
+                                float* d_b_back, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && w_tpg && b_theta && b_phi && b_g && w_back && tpg && wavg && d_out && d_w_tpg && d_b_theta &&
+                d_b_phi && d_b_g && d_w_back && d_b_back && N >= 1 && h >= 1 && w >= 1,
+            "bad arguments");
+  CWT_CHECK(C == 512 || C == 1024 || C == 2048, "WeightAverage: c_in 512, 1024 or 2048");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int co = C / 2;
+  const long P = (long)N * h * w, ldP = ld32(P);
+  void *wbt, *dwavg, *coef, *dtpg, *dot, *wvt, *dtt, *xt;
+  int rc;
+  if ((rc = ensure_ws(ctx, "wab.wbT", (size_t)co * C * 4, &wbt)) || (rc = ensure_ws(ctx, "wab.dwavg", (size_t)P * co * 4, &dwavg)) ||
+      (rc = ensure_ws(ctx, "wab.coef", (size_t)P * 27 * 4, &coef)) ||
+      (rc = ensure_ws(ctx, "wab.dtpg", (size_t)P * 3 * co * 4, &dtpg)) ||
+      (rc = ensure_ws(ctx, "wab.doT", (size_t)C * ldP * 4, &dot)) || (rc = ensure_ws(ctx, "wab.wvT", (size_t)co * ldP * 4, &wvt)) ||
+      (rc = ensure_ws(ctx, "wab.dtT", (size_t)3 * co * ldP * 4, &dtt)) || (rc = ensure_ws(ctx, "wab.xT", (size_t)C * ldP * 4, &xt)))
+    return rc;
+  Prof p(ctx, st, "weight_average_backward c" + std::to_string(C), 2.0 * P * C * co * 8, 4.0 * P * (4.0 * C + 8.0 * co));
+  // d wavg = d_out . w_back  (conv_back, msm_func.py:99)
+  if ((rc = launch_match_vt(w_back, 1, C, co, C, (float*)wbt, st)) ||
+      (rc = gemm_nt(ctx, d_out, (const float*)wbt, (int)P, co, C, (float*)dwavg, st)))
+    return rc;
+  // softmax-weighted neighbourhood and the cosine similarities (msm_func.py:66-97)
+  if ((rc = launch_wa_bwd(tpg, N, h, w, co, b_theta, b_phi, b_g, (const float*)dwavg, (float*)coef, (float*)dtpg, st)))
+    return rc;
+  // biases: column sums in row order
+  if ((rc = launch_colsum((const float*)dtpg, P, co, 3L * co, 0, d_b_theta, st)) ||
+      (rc = launch_colsum((const float*)dtpg + co, P, co, 3L * co, 0, d_b_phi, st)) ||
+      (rc = launch_colsum((const float*)dtpg + 2 * co, P, co, 3L * co, 0, d_b_g, st)) ||
+      (rc = launch_colsum(d_out, P, C, C, 0, d_b_back, st)))
+    return rc;
+  // d w_back = d_out^T . wavg, d w_tpg = d tpg^T . x (reductions over the pixels, zero-padded to 32)
+  if ((rc = launch_match_vt(d_out, 1, (int)P, C, (int)ldP, (float*)dot, st)) ||
+      (rc = launch_match_vt(wavg, 1, (int)P, co, (int)ldP, (float*)wvt, st)) ||
+      (rc = gemm_nt(ctx, (const float*)dot, (const float*)wvt, C, co, (int)ldP, d_w_back, st)) ||
+      (rc = launch_match_vt((const float*)dtpg, 1, (int)P, 3 * co, (int)ldP, (float*)dtt, st)) ||
+      (rc = launch_match_vt(x, 1, (int)P, C, (int)ldP, (float*)xt, st)) ||
+      (rc = gemm_nt(ctx, (const float*)dtt, (const float*)xt, 3 * co, C, (int)ldP, d_w_tpg, st)))
+    return rc;
+  if (d_x) {  // d x = d_out (the residual) + d tpg . w_tpg
+    void* wtt;
+    if ((rc = ensure_ws(ctx, "wab.wtT", (size_t)C * 3 * co * 4, &wtt))) return rc;
+    if ((rc = launch_match_vt(w_tpg, 1, 3 * co, C, 3 * co, (float*)wtt, st))) return rc;
+    if (gemm_f32d_ok((int)P, C, 3 * co, dtpg, wtt, d_x, d_out)) {
+      if ((rc = gemm_f32d(ctx, (const float*)dtpg, (const float*)wtt, (int)P, C, 3 * co, d_x, nullptr, d_out, C, st))) return rc;
+    } else if ((rc = gemm_nt(ctx, (const float*)dtpg, (const float*)wtt, (int)P, C, 3 * co, d_x, st)) ||
+               (rc = launch_add_inplace(d_x, d_out, P * C, st))) {
+      return rc;
+    }
+  }
+  p.end();
+  return 0;
+}
+
+int cwt_mmn_blend_backward(cwt_ctx* ctx, const float* d_fq, const float* d_att_mean, int B, int64_t n, float att_wt,
+                           float* d_att, float* d_fq_in, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(d_att && B >= 1 && n >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_mmn_blend_bwd(d_fq, d_att_mean, B, (long)n, att_wt, d_att, d_fq_in, (hipStream_t)stream);
 }
 
 int cwt_mmn_blend(cwt_ctx* ctx, const float* f_q, const float* att_fq, int B, int64_t n, float att_wt,

@@ -194,4 +194,36 @@ int launch_ppm_field(const float* Q, int N, int h, int w, const int* bins, float
 // its adjoint: dQ [cells][9 * 512] from dF [N][h][w][512] (dR: R's shape, scratch)
 int launch_ppm_field_bwd(const float* dF, int N, int h, int w, const int* bins, float* dR, float* dQ, hipStream_t st);
 
+// ---- MatchNet / MMN backward (match_bwd.hip; launch_cp4d_dgrad in match.hip) ----
+struct MmBwdWs {  // MutualMatching backward scratch, per (b, c): rows NA, columns NB, row blocks of 16
+  float* rowmax;
+  int* rowarg;
+  float* colpv;  // [B*C][nrb][NB] column partial maxima, then the partial column sums
+  int* colpi;
+  float* colmax;
+  int* colarg;
+  float* srow;
+  float* scol;
+};
+int launch_mutual_matching_bwd(const float* x, const float* dy, int B, int NA, int NB, int C, float* dx,
+                               const MmBwdWs& ws, hipStream_t st);
+int launch_relu_mask(const float* g, const float* out, long n, float* gm, hipStream_t st);
+int cp4d_wgrad_part_floats(int cin, int cout);
+int launch_cp4d_wgrad(const float* x, const float* gm, int B, int hA, int wA, int hB, int wB, int cin, int cout,
+                      float* part, size_t part_floats, float* dWa, float* dWb, float* db1, float* db2, hipStream_t st);
+int launch_cp4d_dgrad(const float* g, int B, int hA, int wA, int hB, int wB, int gin, int gout, const float* Wa,
+                      const float* Wb, float* dx, int accum, hipStream_t st);
+int launch_match_softmax_bwd(const float* P, int ldp, const float* dA, int rows, int NB, float temp, int accum,
+                             float* g, hipStream_t st);
+int launch_token_norm(const float* x, long T, int C, float eps, float* xn, float* nrm, hipStream_t st);
+int launch_token_norm_bwd(const float* xn, const float* nrm, const float* dxn, long T, int C, int ld_d, float eps,
+                          int accum, float* dx, hipStream_t st);
+int launch_wa_bwd(const float* tpg, int N, int h, int w, int co, const float* bt, const float* bp, const float* bg,
+                  const float* dwavg, float* coef, float* dtpg, hipStream_t st);
+int launch_colsum(const float* X, long R, int Cc, long ld, int accum, float* out, hipStream_t st);
+int launch_to_channels_first(const float* x, int B, int C, long P, float* y, hipStream_t st);
+int launch_copy_pad(const float* X, long R, int Cc, int ld, float* out, hipStream_t st);
+int launch_mmn_blend_bwd(const float* d_fq, const float* d_mean, int B, long n, float att_wt, float* d_att,
+                         float* d_fq_in, hipStream_t st);
+
 }  // namespace cwt

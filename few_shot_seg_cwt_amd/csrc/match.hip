@@ -102,11 +102,14 @@ __global__ __launch_bounds__(256) void mm_apply_kernel(const float* x, long tota
 constexpr int CP_TAH = 2, CP_TAW = 8, CP_TBH = 2, CP_TBW = 8;
 constexpr int CP_NA = CP_TAH * CP_TAW, CP_NB = CP_TBH * CP_TBW;             // 16 x 16 = 256 pairs
 constexpr int CP_HA = (CP_TAH + 2) * (CP_TAW + 2), CP_HB = (CP_TBH + 2) * (CP_TBW + 2);  // 40 halo positions
-template <int CIN, int COUT>
+// MODE 1 (backward, match_bwd.hip): the input gradient of a layer -- the same cross-shaped
+// convolution of the output gradient with each filter transposed (in / out channels exchanged)
+// and flipped (tap 8 - t), no bias, no ReLU; accum adds into y (the symmetric branches' sum).
+template <int CIN, int COUT, int MODE>
 __global__ __launch_bounds__(256) void cp4d_layer_kernel(const float* __restrict__ x, int hA, int wA, int hB, int wB,
                                                          const float* __restrict__ Wa, const float* __restrict__ ba,
                                                          const float* __restrict__ Wb, const float* __restrict__ bb,
-                                                         float* __restrict__ y) {
+                                                         float* __restrict__ y, int accum) {
   // a halo box x b tile, one float of padding per a-halo position (the wave's two a rows of a
   // 32-lane group then fall on disjoint banks); b halo box at the tile's a positions
   __shared__ float xa[CP_HA][CP_NB * CIN + 1];
@@ -127,7 +130,8 @@ __global__ __launch_bounds__(256) void cp4d_layer_kernel(const float* __restrict
     const int o = i % CO4, r = i / CO4;
     const int c = r % CIN, r2 = r / CIN;
     const int tap = r2 % 9, side = r2 / 9;
-    (&wl[0][0][0][0])[i] = o < COUT ? (side ? Wb : Wa)[(o * CIN + c) * 9 + tap] : 0.f;
+    const float* W = side ? Wb : Wa;
+    (&wl[0][0][0][0])[i] = o >= COUT ? 0.f : MODE == 0 ? W[(o * CIN + c) * 9 + tap] : W[(c * COUT + o) * 9 + 8 - tap];
   }
   // both boxes: every load of the thread issued before the first LDS store (one round of
   // memory latency per workgroup instead of one per element)
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(256) void cp4d_layer_kernel(const float* __restrict
   const int hb = hb0 + bi / CP_TBW, wb = wb0 + bi % CP_TBW;
   float acc[COUT];
 #pragma unroll
-  for (int o = 0; o < COUT; ++o) acc[o] = ba[o] + bb[o];
+  for (int o = 0; o < COUT; ++o) acc[o] = MODE == 0 ? ba[o] + bb[o] : 0.f;
   const int aiy = ai / CP_TAW, aix = ai % CP_TAW, biy = bi / CP_TBW, bix = bi % CP_TBW;
 #pragma unroll 1
   for (int tap = 0; tap < 9; ++tap) {  // one tap's inputs and weights live at a time
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(256) void cp4d_layer_kernel(const float* __restrict
   if (ha < hA && wa < wA && hb < hB && wb < wB) {
     float* yp = y + (long)blockIdx.z * NA * NB * COUT + ((long)(ha * wA + wa) * NB + hb * wB + wb) * COUT;
 #pragma unroll
-    for (int o = 0; o < COUT; ++o) yp[o] = fmaxf(acc[o], 0.f);
+    for (int o = 0; o < COUT; ++o) yp[o] = MODE == 0 ? fmaxf(acc[o], 0.f) : accum ? yp[o] + acc[o] : acc[o];
   }
 }
 
@@ -1190,7 +1194,7 @@ int launch_cp4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int
   dim3 grid(cdiv(hB, CP_TBH) * cdiv(wB, CP_TBW), cdiv(hA, CP_TAH) * cdiv(wA, CP_TAW), B);
 #define CWT_CP4D(CI, CO)                                                                                         \
   if (cin == CI && cout == CO) {                                                                                 \
-    hipLaunchKernelGGL((cp4d_layer_kernel<CI, CO>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, Wa, ba, Wb, bb, y); \
+    hipLaunchKernelGGL((cp4d_layer_kernel<CI, CO, 0>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, Wa, ba, Wb, bb, y, 0); \
     CWT_LAUNCH_CHECK();                                                                                          \
     return 0;                                                                                                    \
   }
@@ -1200,6 +1204,27 @@ int launch_cp4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int
   CWT_CP4D(10, 1)
 #undef CWT_CP4D
   return fail(CWT_EARG, "cp4d layer: channels (1|2 -> 10, 10 -> 10, 10 -> 1) only");
+}
+
+// the input gradient of one CenterPivotConv4d layer (cp4d_layer_kernel MODE 1): g [B][NA][NB][gin]
+// is the layer's ReLU-masked output gradient, dx [B][NA][NB][gout] (gout = the layer's input
+// channels), Wa / Wb the a-plane / b-plane filters the forward applied ([gin][gout][3][3])
+int launch_cp4d_dgrad(const float* g, int B, int hA, int wA, int hB, int wB, int gin, int gout, const float* Wa,
+                      const float* Wb, float* dx, int accum, hipStream_t st) {
+  dim3 grid(cdiv(hB, CP_TBH) * cdiv(wB, CP_TBW), cdiv(hA, CP_TAH) * cdiv(wA, CP_TAW), B);
+#define CWT_CPD(CI, CO)                                                                                     \
+  if (gin == CI && gout == CO) {                                                                            \
+    hipLaunchKernelGGL((cp4d_layer_kernel<CI, CO, 1>), grid, dim3(256), 0, st, g, hA, wA, hB, wB, Wa,       \
+                       (const float*)nullptr, Wb, (const float*)nullptr, dx, accum);                        \
+    CWT_LAUNCH_CHECK();                                                                                     \
+    return 0;                                                                                               \
+  }
+  CWT_CPD(1, 10)
+  CWT_CPD(10, 10)
+  CWT_CPD(10, 1)
+  CWT_CPD(10, 2)
+#undef CWT_CPD
+  return fail(CWT_EARG, "cp4d input gradient: channels (1 -> 10, 10 -> 10, 10 -> 1|2) only");
 }
 
 int launch_to_channels_last(const float* x, int B, int C, long P, float* y, hipStream_t st) {

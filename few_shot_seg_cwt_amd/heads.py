@@ -127,17 +127,50 @@ def get_classifier(args, num_classes=None):
     raise NotImplementedError(f"dist {dist!r}: only the cosine heads are built here")
 
 
+class _CorrFn(torch.autograd.Function):
+    """get_corr under autograd: the backward is cwt_corr_backward (normalize's Jacobian around
+    two f32-MFMA GEMMs, d_sim . k_hat and d_sim^T . q_hat)."""
+
+    @staticmethod
+    def forward(ctx, qt, kt):
+        ctx.save_for_backward(qt, kt)
+        return _corr_tokens(qt, kt)
+
+    @staticmethod
+    def backward(ctx, d_sim):
+        qt, kt = ctx.saved_tensors
+        bs, ch, h, w = qt.shape
+        Pq, Pk = h * w, kt.shape[2] * kt.shape[3]
+        dq = torch.empty_like(qt) if ctx.needs_input_grad[0] else None
+        dk = torch.empty_like(kt) if ctx.needs_input_grad[1] else None
+        if dq is None and dk is None:
+            return None, None
+        d = d_sim.contiguous()
+        _lib.check(_lib.lib().cwt_corr_backward(_lib.ctx(qt.device.index), _lib.ptr(qt), _lib.ptr(kt), bs, Pq, Pk, ch,
+                                                _lib.ptr(d), _lib.ptr(dq), _lib.ptr(dk), 0, 0,
+                                                _lib.stream_ptr(qt.device)), "cwt_corr_backward")
+        return dq, dk
+
+
+def _corr_tokens(qt: torch.Tensor, kt: torch.Tensor) -> torch.Tensor:
+    bs, ch, h, w = qt.shape
+    Pq, Pk = h * w, kt.shape[2] * kt.shape[3]
+    sim = torch.empty((bs, Pq, Pk), device=qt.device, dtype=torch.float32)
+    _lib.check(_lib.lib().cwt_corr(_lib.ctx(qt.device.index), _lib.ptr(qt), _lib.ptr(kt), bs, Pq, Pk, ch, _lib.ptr(sim),
+                                   _lib.stream_ptr(qt.device)), "cwt_corr")
+    return sim
+
+
 def get_corr(q: torch.Tensor, k: torch.Tensor) -> torch.Tensor:
     """model_util.py:101-109: q, k [bs, ch, h, w] -> sim [bs, h*w, h*w] (q tokens x k tokens),
-    cosine similarity of every pair (F.normalize eps 1e-12), exact fp32 on the matrix cores."""
+    cosine similarity of every pair (F.normalize eps 1e-12), exact fp32 on the matrix cores.
+    Differentiable (cwt_corr_backward) when either input requires grad."""
     _lib.require(q, "q")
     _lib.require(k, "k")
     bs, ch, h, w = q.shape
     if k.shape[0] != bs or k.shape[1] != ch:
         raise ValueError("q and k must share batch and channels")
     qt, kt = as_tokens(q), as_tokens(k)
-    Pq, Pk = h * w, k.shape[2] * k.shape[3]
-    sim = torch.empty((bs, Pq, Pk), device=q.device, dtype=torch.float32)
-    _lib.check(_lib.lib().cwt_corr(_lib.ctx(q.device.index), _lib.ptr(qt), _lib.ptr(kt), bs, Pq, Pk, ch, _lib.ptr(sim),
-                                   _lib.stream_ptr(q.device)), "cwt_corr")
-    return sim
+    if torch.is_grad_enabled() and (qt.requires_grad or kt.requires_grad):
+        return _CorrFn.apply(qt, kt)
+    return _corr_tokens(qt, kt)

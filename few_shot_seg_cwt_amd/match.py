@@ -10,6 +10,15 @@ HIP kernels (csrc/match.hip) behind the C ABI:
   WeightAverage(c_in, args)                    src/model/msm/msm_func.py:50-104
   MMN(args, agg, wa, red_dim)                  src/model/mmn.py:11-71 (forward)
 
+Training (round 4): under autograd (grad enabled and a parameter or input
+requiring grad) MatchNet.corr_forward / forward ('red' layers), get_corr, WeightAverage and the
+MMN head (agg 'cat', red_dim False: every MMN config) run their backward on the device --
+cwt_match_corr_backward (softmax readout, both MutualMatchings with torch.max's single-index
+gradient routing, the CenterPivotConv4d layers' input / weight / bias gradients over both
+symmetric branches), cwt_corr_backward, cwt_weight_average_backward, cwt_mmn_blend_backward
+(csrc/match_bwd.hip) -- so the MMN trainers (train_cca.py:101-196, train_aug.py:102) and DeTr's
+cross attention (train_trans.py:100) can train this head.
+
 The modules keep the reference's parameter names (``NeighConsensus.conv.{0,2,4}.conv{1,2}.
 {weight,bias}``), so a reference state_dict loads as is.  Built: the default head of every MMN /
 MatchNet script -- CenterPivotConv4d ('red'), kernel sizes [3, 3, 3], channels [10, 10, 1],
@@ -25,6 +34,7 @@ restatement of the same modules.
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 
 import torch
@@ -108,6 +118,17 @@ class NeighConsensus(torch.nn.Module):
         self.conv = torch.nn.Sequential(*mods)
         self._packed, self._packed_key = None, None
 
+    def param_list(self):
+        """The layers' parameters in cwt_match_corr_forward's order."""
+        ps = []
+        for i in (0, 2, 4):
+            layer = self.conv[i]
+            if self.conv_type == "cv4":
+                ps += [layer.weight, layer.bias]
+            else:
+                ps += [layer.conv1.weight, layer.conv1.bias, layer.conv2.weight, layer.conv2.bias]
+        return ps
+
     def packed(self) -> torch.Tensor:
         """The layers' parameters in cwt_match_corr_forward's order (cached per parameter version)."""
         ps = []
@@ -171,6 +192,59 @@ class SpatialContextEncoder(torch.nn.Module):
         return out.reshape(B, h, w, -1).permute(0, 3, 1, 2)
 
 
+class _MatchCorrFn(torch.autograd.Function):
+    """MatchNet.corr_forward ('red' layers) under autograd: cwt_match_corr_forward_train keeps the
+    activations, cwt_match_corr_backward runs the whole chain's backward on the device."""
+
+    @staticmethod
+    def forward(ctx, corr, vt, symmetric, temp, h, w, *params):
+        # corr [B, L, hw, hw] contiguous; vt [B, Cv, h, w] token-contiguous (channels_last) or None
+        B, L = corr.shape[0], corr.shape[1]
+        hw, dev = h * w, corr.device
+        with torch.no_grad():
+            packed = torch.cat([p.detach().reshape(-1).float() for p in params]).contiguous()
+        n = C.c_int64()
+        _lib.check(_lib.lib().cwt_match_corr_saved_floats(B, L, h, w, int(symmetric), int(vt is not None), C.byref(n)),
+                   "cwt_match_corr_saved_floats")
+        saved = torch.empty(n.value, device=dev, dtype=torch.float32)
+        corr2d = torch.empty((B, hw, hw), device=dev, dtype=torch.float32)
+        Cv = vt.shape[1] if vt is not None else 0
+        wv = torch.empty((B, h, w, Cv), device=dev, dtype=torch.float32) if vt is not None else None
+        _lib.check(_lib.lib().cwt_match_corr_forward_train(
+            _lib.ctx(dev.index), _lib.ptr(corr), B, L, h, w, _lib.ptr(packed), int(symmetric), float(temp),
+            _lib.ptr(vt), Cv, _lib.ptr(corr2d), _lib.ptr(wv), _lib.ptr(saved), _lib.stream_ptr(dev)),
+            "cwt_match_corr_forward_train")
+        ctx.save_for_backward(corr, vt if vt is not None else corr.new_empty(0), packed, saved)
+        ctx.meta = (h, w, int(symmetric), float(temp), vt is not None)
+        ctx.shapes = [p.shape for p in params]
+        return corr2d, (wv.permute(0, 3, 1, 2) if wv is not None else corr.new_empty(0))
+
+    @staticmethod
+    def backward(ctx, g_corr2d, g_wv):
+        corr, vt, packed, saved = ctx.saved_tensors
+        h, w, sym, temp, has_v = ctx.meta
+        B, L = corr.shape[0], corr.shape[1]
+        dev = corr.device
+        gw = g_wv.permute(0, 2, 3, 1).contiguous() if (has_v and g_wv is not None and g_wv.numel()) else None
+        Cv = vt.shape[1] if has_v else 0
+        d_corr = torch.empty_like(corr) if ctx.needs_input_grad[0] else None
+        d_v = (torch.empty((B, h, w, Cv), device=dev, dtype=torch.float32)
+               if (has_v and gw is not None and ctx.needs_input_grad[1]) else None)
+        d_params = torch.empty_like(packed)
+        gc = g_corr2d.contiguous() if g_corr2d is not None else None
+        _lib.check(_lib.lib().cwt_match_corr_backward(
+            _lib.ctx(dev.index), _lib.ptr(corr), B, L, h, w, _lib.ptr(packed), sym, temp,
+            _lib.ptr(vt) if has_v else None, Cv, _lib.ptr(saved), _lib.ptr(gc), _lib.ptr(gw), _lib.ptr(d_corr),
+            _lib.ptr(d_params), _lib.ptr(d_v), _lib.stream_ptr(dev)), "cwt_match_corr_backward")
+        sizes = [math.prod(s) for s in ctx.shapes]
+        grads = [g.reshape(s) for g, s in zip(torch.split(d_params, sizes), ctx.shapes)]
+        return (d_corr, d_v.permute(0, 3, 1, 2) if d_v is not None else None, None, None, None, None, *grads)
+
+
+def _needs_grad(*ts) -> bool:
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
 class MatchNet(torch.nn.Module):
     """match.py:88-163.  forward(fq_fea, fs_fea, v) and corr_forward(corr4d, v, ret_attn) on the
     device; v is the support feature map [B, Cv, h, w] (returned weighted_v has its shape)."""
@@ -195,8 +269,16 @@ class MatchNet(torch.nn.Module):
         B, L = corr.shape[0], corr.shape[1]
         if L != self.in_channel:
             raise ValueError("input corr channel inconsistent with in_channel of NCNet")
-        params = self.NeighConsensus.packed()
         hw = h * w
+        nc = self.NeighConsensus
+        # the backward is built for CenterPivotConv4d ('red') layers, the layers every config trains;
+        # 'cv4' runs the inference kernels and its outputs carry no gradient
+        if nc.conv_type == "red" and _needs_grad(corr, v, *nc.param_list()):
+            vt = as_tokens(v if v.dim() == 4 else v.reshape(v.shape[0], v.shape[1], h, w)) if v is not None else None
+            corr2d, wv = _MatchCorrFn.apply(corr.contiguous(), vt, nc.symmetric_mode, float(self.temp), h, w,
+                                            *nc.param_list())
+            return corr2d, (wv if v is not None else None)
+        params = nc.packed()
         corr2d = torch.empty((B, hw, hw), device=corr.device, dtype=torch.float32)
         wv, vt, Cv = None, None, 0
         if v is not None:
@@ -244,6 +326,8 @@ class MatchNet(torch.nn.Module):
                 raise UnboundLocalError("ret_cyc needs the cycle mask (cyc=True and use_cyc=True)")
             corr2d, wv = self._run(corr.reshape(B, 1, hw, hw), h, w, v)
             return (wv, corr2d.reshape(B, h, w, h, w)) if ret_corr else wv
+        if corr.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError("MatchNet backward with ig_mask / the cycle mask is not built (no trainer uses it)")
         if cyc_on and s_mask is None:   # run_cyc returns None and the reference fails on it
             raise ValueError("the cycle mask needs s_mask")
         if cyc_on and self.training:
@@ -329,6 +413,10 @@ class WeightAverage(torch.nn.Module):
         if C != self.c_in:
             raise ValueError(f"expected {self.c_in} channels, got {C}")
         xt = as_tokens(x)
+        ps = [self.conv_theta.weight, self.conv_theta.bias, self.conv_phi.weight, self.conv_phi.bias,
+              self.conv_g.weight, self.conv_g.bias, self.conv_back.weight, self.conv_back.bias]
+        if _needs_grad(xt, *ps):
+            return _WeightAverageFn.apply(xt, *ps)
         tpg, back = self._weights()
         out = torch.empty((N, C, h, w), device=x.device, dtype=torch.float32, memory_format=torch.channels_last)
         _lib.check(_lib.lib().cwt_weight_average(
@@ -336,6 +424,128 @@ class WeightAverage(torch.nn.Module):
             _lib.ptr(self.conv_phi.bias), _lib.ptr(self.conv_g.bias), _lib.ptr(back), _lib.ptr(self.conv_back.bias),
             _lib.ptr(out), _lib.stream_ptr(x.device)), "cwt_weight_average")
         return out
+
+
+class _WeightAverageFn(torch.autograd.Function):
+    """WeightAverage under autograd: cwt_weight_average_train keeps theta | phi | g and the
+    weighted average, cwt_weight_average_backward forms every gradient on the device."""
+
+    @staticmethod
+    def forward(ctx, xt, wt, bt, wp, bp, wg, bg, wb, bb):
+        N, Cc, h, w = xt.shape
+        co = Cc // 2
+        dev = xt.device
+        with torch.no_grad():
+            tpg_w = torch.cat([p.detach().reshape(co, Cc) for p in (wt, wp, wg)]).contiguous()
+            back = wb.detach().reshape(Cc, co).contiguous()
+        out = torch.empty((N, Cc, h, w), device=dev, dtype=torch.float32, memory_format=torch.channels_last)
+        tpg = torch.empty((N * h * w, 3 * co), device=dev, dtype=torch.float32)
+        wavg = torch.empty((N * h * w, co), device=dev, dtype=torch.float32)
+        _lib.check(_lib.lib().cwt_weight_average_train(
+            _lib.ctx(dev.index), _lib.ptr(xt), N, h, w, Cc, _lib.ptr(tpg_w), _lib.ptr(bt), _lib.ptr(bp), _lib.ptr(bg),
+            _lib.ptr(back), _lib.ptr(bb), _lib.ptr(out), _lib.ptr(tpg), _lib.ptr(wavg), _lib.stream_ptr(dev)),
+            "cwt_weight_average_train")
+        ctx.save_for_backward(xt, tpg_w, bt, bp, bg, back, tpg, wavg)
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        xt, tpg_w, bt, bp, bg, back, tpg, wavg = ctx.saved_tensors
+        N, Cc, h, w = xt.shape
+        co = Cc // 2
+        dev = xt.device
+        d = as_tokens(d_out)
+        dx = torch.empty_like(xt) if ctx.needs_input_grad[0] else None
+        f = dict(device=dev, dtype=torch.float32)
+        d_wtpg, d_bt, d_bp, d_bg = torch.empty((3 * co, Cc), **f), torch.empty(co, **f), torch.empty(co, **f), \
+            torch.empty(co, **f)
+        d_wb, d_bb = torch.empty((Cc, co), **f), torch.empty(Cc, **f)
+        _lib.check(_lib.lib().cwt_weight_average_backward(
+            _lib.ctx(dev.index), _lib.ptr(xt), N, h, w, Cc, _lib.ptr(tpg_w), _lib.ptr(bt), _lib.ptr(bp), _lib.ptr(bg),
+            _lib.ptr(back), _lib.ptr(tpg), _lib.ptr(wavg), _lib.ptr(d), _lib.ptr(dx), _lib.ptr(d_wtpg), _lib.ptr(d_bt),
+            _lib.ptr(d_bp), _lib.ptr(d_bg), _lib.ptr(d_wb), _lib.ptr(d_bb), _lib.stream_ptr(dev)),
+            "cwt_weight_average_backward")
+        wshape = (co, Cc, 1, 1)
+        return (dx, d_wtpg[:co].reshape(wshape), d_bt, d_wtpg[co:2 * co].reshape(wshape), d_bp,
+                d_wtpg[2 * co:].reshape(wshape), d_bg, d_wb.reshape(Cc, co, 1, 1), d_bb)
+
+
+class _MMNCorrFn(torch.autograd.Function):
+    """MMN's stacked correlations (mmn.py:44-58, agg 'cat') under autograd: corr4d[b, l] =
+    get_corr(fq_l[b or 0], fs_l[b]); the backward is cwt_corr_backward per (b, l), a query feature
+    shared by the B support rows (fq expanded, mmn.py:50) accumulating its B gradients in order."""
+
+    @staticmethod
+    def forward(ctx, B, L, *feats):
+        h, w = feats[0].shape[2], feats[0].shape[3]
+        P = h * w
+        dev = feats[0].device
+        corr4d = torch.empty((B, L, P, P), device=dev, dtype=torch.float32)
+        for li in range(L):
+            q, k = feats[2 * li], feats[2 * li + 1]
+            for b in range(B):
+                qb = q[:1] if q.shape[0] == 1 else q[b:b + 1]
+                _lib.check(_lib.lib().cwt_corr(_lib.ctx(dev.index), _lib.ptr(qb), _lib.ptr(k[b:b + 1]), 1, P, P,
+                                               q.shape[1], _lib.ptr(corr4d[b, li]), _lib.stream_ptr(dev)), "cwt_corr")
+        ctx.save_for_backward(*feats)
+        ctx.BL = (B, L)
+        return corr4d
+
+    @staticmethod
+    def backward(ctx, g):
+        feats = ctx.saved_tensors
+        B, L = ctx.BL
+        g = g.contiguous()
+        h, w = feats[0].shape[2], feats[0].shape[3]
+        P = h * w
+        dev = feats[0].device
+        grads = []
+        for li in range(L):
+            q, k = feats[2 * li], feats[2 * li + 1]
+            nq, nk = ctx.needs_input_grad[2 + 2 * li], ctx.needs_input_grad[3 + 2 * li]
+            dq = torch.empty_like(q) if nq else None
+            dk = torch.empty_like(k) if nk else None
+            if nq or nk:
+                for b in range(B):
+                    shared = q.shape[0] == 1
+                    qi = 0 if shared else b
+                    _lib.check(_lib.lib().cwt_corr_backward(
+                        _lib.ctx(dev.index), _lib.ptr(q[qi:qi + 1]), _lib.ptr(k[b:b + 1]), 1, P, P, q.shape[1],
+                        _lib.ptr(g[b, li]), _lib.ptr(dq[qi:qi + 1]) if nq else None,
+                        _lib.ptr(dk[b:b + 1]) if nk else None, int(shared and b > 0), 0, _lib.stream_ptr(dev)),
+                        "cwt_corr_backward")
+            grads += [dq, dk]
+        return (None, None, *grads)
+
+
+class _MMNBlendFn(torch.autograd.Function):
+    """mmn.py:65-67 under autograd (cwt_mmn_blend / cwt_mmn_blend_backward)."""
+
+    @staticmethod
+    def forward(ctx, fqt, att_t, att_wt):
+        B = att_t.shape[0]
+        dev = fqt.device
+        att_fq = torch.empty(fqt.shape, device=dev, dtype=torch.float32, memory_format=torch.channels_last)
+        fq = torch.empty_like(att_fq)
+        _lib.check(_lib.lib().cwt_mmn_blend(_lib.ctx(dev.index), _lib.ptr(fqt), _lib.ptr(att_t), B, fqt.numel(),
+                                            float(att_wt), _lib.ptr(att_fq), _lib.ptr(fq), _lib.stream_ptr(dev)),
+                   "cwt_mmn_blend")
+        ctx.meta = (B, float(att_wt), tuple(att_t.shape))
+        return fq, att_fq
+
+    @staticmethod
+    def backward(ctx, d_fq, d_att_fq):
+        B, att_wt, ashape = ctx.meta
+        dfq = as_tokens(d_fq) if d_fq is not None else None
+        dm = as_tokens(d_att_fq) if d_att_fq is not None else None
+        ref = dfq if dfq is not None else dm
+        dev = ref.device
+        d_att = torch.empty(ashape, device=dev, dtype=torch.float32, memory_format=torch.channels_last)
+        d_in = torch.empty_like(ref) if (ctx.needs_input_grad[0] and dfq is not None) else None
+        _lib.check(_lib.lib().cwt_mmn_blend_backward(_lib.ctx(dev.index), _lib.ptr(dfq), _lib.ptr(dm), B, ref.numel(),
+                                                     att_wt, _lib.ptr(d_att), _lib.ptr(d_in), _lib.stream_ptr(dev)),
+                   "cwt_mmn_blend_backward")
+        return d_in, d_att, None
 
 
 def _get(args, k, default=None):
@@ -385,9 +595,32 @@ class MMN(torch.nn.Module):
         y = linear(xt.permute(0, 2, 3, 1).reshape(N * h * w, C), conv.weight, None, relu=True)
         return y.reshape(N, h, w, -1).permute(0, 3, 1, 2)
 
+    def _forward_train(self, fq_lst, fs_lst, f_q, f_s, ret_attn: bool):
+        """forward under autograd: WeightAverage, the stacked correlations, corr_forward and the
+        blend as differentiable device ops (agg 'cat', red_dim False: every MMN config)."""
+        if self.red_dim or self.agg != "cat":
+            raise NotImplementedError("MMN backward: agg 'cat' without red_dim only (every reference MMN config)")
+        B, ch, h, w = f_s.shape
+        L = len(self.bid_lst)
+        feats = []
+        for idx in self.bid_lst[::-1]:
+            fq_fea, fs_fea = fq_lst[idx][0], fs_lst[idx][0]
+            if self.wa:
+                m = getattr(self, "wa_" + str(idx))
+                fq_fea, fs_fea = m(fq_fea), m(fs_fea)
+            feats += [as_tokens(fq_fea), as_tokens(fs_fea)]
+        corr4d = _MMNCorrFn.apply(B, L, *feats)
+        attn, att = self.corr_net._run(corr4d, h, w, f_s)
+        fq, att_fq = _MMNBlendFn.apply(as_tokens(f_q), as_tokens(att), self.att_wt)
+        return (attn, fq, att_fq) if ret_attn else (fq, att_fq)
+
     def forward(self, fq_lst, fs_lst, f_q, f_s, ret_attn: bool = False):
         """mmn.py:42-71: fq_lst / fs_lst {layer: [feature]} (extract_features with rmid),
-        f_q [1, C, h, w], f_s [B, C, h, w] -> (fq, att_fq) [or (attn, fq, att_fq)]."""
+        f_q [1, C, h, w], f_s [B, C, h, w] -> (fq, att_fq) [or (attn, fq, att_fq)].  Under
+        autograd (a parameter or an input requiring grad) the backward runs on the device."""
+        feats_in = [t for lst in (fq_lst, fs_lst) for idx in self.bid_lst for t in lst[idx][:1]]
+        if _needs_grad(f_q, f_s, *feats_in, *self.parameters()):
+            return self._forward_train(fq_lst, fs_lst, f_q, f_s, ret_attn)
         B, ch, h, w = f_s.shape
         P = h * w
         L = len(self.bid_lst)

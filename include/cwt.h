@@ -424,6 +424,59 @@ int cwt_weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int C,
 int cwt_mmn_blend(cwt_ctx* ctx, const float* f_q, const float* att_fq, int B, int64_t n, float att_wt,
                   float* att_mean, float* fq_out, void* stream);
 
+/* ---- MatchNet / MMN training: the backward the reference's autograd runs through the head ----
+ * (MMN trained end to end by src/train_cca.py:101-196 and src/train_aug.py:102; DeTr's MatchNet
+ * cross attention by src/train_trans.py:100).  Every gradient is exact fp32 with fixed-order
+ * reductions (deterministic); outputs are overwritten unless an accumulate flag says otherwise. */
+
+/* Floats of the activations cwt_match_corr_forward_train keeps for the backward (CenterPivotConv4d
+ * layers): the MutualMatching output, each branch's three ReLU outputs, their sum and, with
+ * readout != 0, the attention [B][h*w][ld] (ld = h*w rounded up to 32). */
+int cwt_match_corr_saved_floats(int B, int L, int h, int w, int symmetric, int readout, int64_t* n);
+
+/* cwt_match_corr_forward (match.py:142-163, 'red' layers) keeping its activations in saved
+ * device [cwt_match_corr_saved_floats]: the forward of MatchNet.corr_forward under autograd. */
+int cwt_match_corr_forward_train(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w,
+                                 const float* nc_params, int symmetric, float temp, const float* v, int Cv,
+                                 float* corr2d, float* weighted_v, float* saved, void* stream);
+
+/* Its backward: d_corr2d device [B][h*w][h*w] (the gradient at corr2d, or NULL) and d_weighted_v
+ * device [B][h*w][Cv] (at weighted_v, or NULL) -> d_corr device [B][L][h*w][h*w] (or NULL), d_params
+ * device (nc_params' layout: every conv1 / conv2 weight and bias of the three layers, both branches
+ * summed), d_v device [B][h*w][Cv] (or NULL).  MutualMatching's maxima route their gradient to the
+ * first maximal position (torch.max's single index); Cv % 4 == 0. */
+int cwt_match_corr_backward(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
+                            int symmetric, float temp, const float* v, int Cv, const float* saved,
+                            const float* d_corr2d, const float* d_weighted_v, float* d_corr, float* d_params,
+                            float* d_v, void* stream);
+
+/* get_corr's backward (src/model/model_util.py:101-109: sim = normalize(q) . normalize(k)^T,
+ * F.normalize eps 1e-12): q device [B][Pq][C], k device [B][Pk][C] (tokens), d_sim device
+ * [B][Pq][Pk] -> dq device [B][Pq][C] and dk device [B][Pk][C] (either may be NULL), added into
+ * when accum_q / accum_k != 0 (a query feature shared by the B support rows, mmn.py:50). */
+int cwt_corr_backward(cwt_ctx* ctx, const float* q, const float* k, int B, int Pq, int Pk, int C, const float* d_sim,
+                      float* dq, float* dk, int accum_q, int accum_k, void* stream);
+
+/* cwt_weight_average keeping tpg device [N*h*w][3 C/2] (theta | phi | g before their biases) and
+ * wavg device [N*h*w][C/2] (the softmax-weighted g) for the backward. */
+int cwt_weight_average_train(cwt_ctx* ctx, const float* x, int N, int h, int w, int C, const float* w_tpg,
+                             const float* b_theta, const float* b_phi, const float* b_g, const float* w_back,
+                             const float* b_back, float* out, float* tpg, float* wavg, void* stream);
+
+/* WeightAverage's backward (msm_func.py:66-104): d_out device [N][h][w][C] -> d_x device
+ * [N][h][w][C] (or NULL), d_w_tpg device [3 C/2][C], d_b_theta / d_b_phi / d_b_g [C/2], d_w_back
+ * [C][C/2], d_b_back [C]; tpg / wavg from cwt_weight_average_train. */
+int cwt_weight_average_backward(cwt_ctx* ctx, const float* x, int N, int h, int w, int C, const float* w_tpg,
+                                const float* b_theta, const float* b_phi, const float* b_g, const float* w_back,
+                                const float* tpg, const float* wavg, const float* d_out, float* d_x,
+                                float* d_w_tpg, float* d_b_theta, float* d_b_phi, float* d_b_g, float* d_w_back,
+                                float* d_b_back, void* stream);
+
+/* cwt_mmn_blend's backward: d_fq device [n] (at fq_out, or NULL), d_att_mean device [n] (at
+ * att_mean, or NULL) -> d_att device [B][n], d_fq_in device [n] (or NULL). */
+int cwt_mmn_blend_backward(cwt_ctx* ctx, const float* d_fq, const float* d_att_mean, int B, int64_t n, float att_wt,
+                           float* d_att, float* d_fq_in, void* stream);
+
 /* ---- DeTr head (src/model/detr.py:13-151), forward only; tokens are [B][hw][C] (NHWC) ---- */
 
 /* nn.Linear / 1x1 nn.Conv2d over tokens (detr.py:22 adjust_feature, ms_deform_attn.py:56-59

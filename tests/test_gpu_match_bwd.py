@@ -1,0 +1,187 @@
+"""Backward of the MatchNet / MMN head on the device (csrc/match_bwd.hip: cwt_match_corr_backward,
+cwt_corr_backward, cwt_weight_average_backward, cwt_mmn_blend_backward) against float64
+autograd through oracle/match_oracle.py, the restatement of match.py:21-163, conv4d.py:40-62,
+msm_func.py:50-104, model_util.py:101-109 and mmn.py:42-71.  Parity unpinned (the reference holds
+no fixture for this head): these check the device gradients against autograd of
+the same float64 restatement the forward tests use.
+
+Bar: every gradient within 1e-4 of float64 autograd, measured per tensor as
+max|HIP - oracle| / max|oracle|, printed per case.  The loss is a fixed random linear functional
+of the outputs, so every output element carries gradient."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def _rand(shape, seed, lo=0.0, hi=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(*shape, generator=g, dtype=torch.float64) * (hi - lo) + lo
+
+
+@pytest.mark.parametrize("B,Pq,Pk,C", [(2, 36, 36, 64), (1, 25, 49, 512), (1, 64, 64, 1024)])
+def test_corr_backward(dev, B, Pq, Pk, C):
+    """get_corr (model_util.py:101-109): dq, dk of <G, normalize(q) normalize(k)^T>."""
+    from few_shot_seg_cwt_amd.heads import get_corr
+    q0, k0 = _rand((B, C, Pq, 1), 1) - 0.3, _rand((B, C, Pk, 1), 2) - 0.3
+    G = _rand((B, Pq, Pk), 3, -1, 1)
+    q = q0.float().to(dev).requires_grad_(True)
+    k = k0.float().to(dev).requires_grad_(True)
+    sim = get_corr(q, k)
+    (sim * G.float().to(dev)).sum().backward()
+    qo, ko = q0.clone().requires_grad_(True), k0.clone().requires_grad_(True)
+    so = torch.bmm(torch.nn.functional.normalize(qo.reshape(B, C, Pq), dim=1).transpose(1, 2),
+                   torch.nn.functional.normalize(ko.reshape(B, C, Pk), dim=1))
+    (so * G).sum().backward()
+    errs = dict(sim=rel(sim, so), dq=rel(q.grad, qo.grad), dk=rel(k.grad, ko.grad))
+    print(f"corr backward B={B} {Pq}x{Pk} C={C}: {errs}")
+    assert max(errs.values()) < TOL, errs
+
+
+@pytest.mark.parametrize("N,C,h,w", [(2, 512, 6, 7), (1, 1024, 5, 5), (1, 2048, 4, 6)])
+def test_weight_average_backward(dev, N, C, h, w):
+    """msm_func.py:50-104: d x and every parameter gradient of WeightAverage."""
+    from few_shot_seg_cwt_amd.match import WeightAverage, init_match_params
+    from oracle import match_oracle as M
+    m = WeightAverage(C, {}, device=dev)
+    init_match_params(m, seed=C + h)
+    x0 = _rand((N, C, h, w), C)
+    G = _rand((N, C, h, w), C + 1, -1, 1)
+    x = x0.float().to(dev).requires_grad_(True)
+    y = m(x)
+    (y * G.float().to(dev)).sum().backward()
+    names = ["conv_theta.weight", "conv_theta.bias", "conv_phi.weight", "conv_phi.bias", "conv_g.weight",
+             "conv_g.bias", "conv_back.weight", "conv_back.bias"]
+    sd = {k: t.detach().cpu().double().requires_grad_(True) for k, t in m.state_dict().items()}
+    xo = x0.clone().requires_grad_(True)
+    yo = M.weight_average(xo, tuple(sd[n] for n in names))
+    (yo * G).sum().backward()
+    params = dict(m.named_parameters())
+    errs = dict(y=rel(y, yo), dx=rel(x.grad, xo.grad))
+    for n in names:
+        errs[n] = rel(params[n].grad, sd[n].grad)
+    print(f"WeightAverage backward N={N} C={C} {h}x{w}: " + ", ".join(f"{k} {v:.1e}" for k, v in errs.items()))
+    assert max(errs.values()) < TOL, errs
+
+
+def _net(dev, L, sym, temp, seed):
+    from few_shot_seg_cwt_amd.match import MatchNet, init_match_params
+    net = MatchNet(temp=temp, in_channel=L, sym_mode=sym, device=dev)
+    init_match_params(net, seed)
+    with torch.no_grad():   # keep the one-channel last layer's ReLU open somewhere (a live gradient)
+        net.NeighConsensus.conv[4].conv1.bias.add_(0.2)
+    return net
+
+
+@pytest.mark.parametrize("B,L,h,w,sym", [(1, 1, 6, 6, True), (2, 2, 5, 7, True), (1, 1, 7, 5, False),
+                                         (1, 2, 12, 12, True)])
+def test_corr_forward_backward(dev, B, L, h, w, sym):
+    """match.py:142-163: gradients of <G1, corr2d> + <G2, weighted_v> with respect to the input
+    correlation, the NeighConsensus parameters and v."""
+    from oracle import match_oracle as M
+    temp = 20.0
+    net = _net(dev, L, sym, temp, seed=11 + L + h)
+    c0 = _rand((B, L, h, w, h, w), 5 * h + w, -0.2, 1.0)
+    v0 = _rand((B, 64, h, w), 13)
+    G1 = _rand((B, h * w, h * w), 17, -1, 1)
+    G2 = _rand((B, 64, h, w), 19, -1, 1)
+    corr = c0.float().to(dev).requires_grad_(True)
+    v = v0.float().to(dev).requires_grad_(True)
+    corr2d, wv = net.corr_forward(corr, v, ret_attn=True)
+    ((corr2d * G1.float().to(dev)).sum() + (wv * G2.float().to(dev)).sum()).backward()
+    names = [f"NeighConsensus.conv.{i}.{c}.{p}" for i in (0, 2, 4) for c in ("conv1", "conv2") for p in ("weight", "bias")]
+    sd = {k: t.detach().cpu().double().requires_grad_(True) for k, t in net.state_dict().items()}
+    layers = M.layers_from_state(sd)
+    co, vo = c0.clone().requires_grad_(True), v0.clone().requires_grad_(True)
+    c2o, wvo = M.corr_forward(co, vo, layers, temp, sym)
+    ((c2o * G1).sum() + (wvo * G2).sum()).backward()
+    params = dict(net.named_parameters())
+    assert float(co.grad.abs().max()) > 0 and float(sd[names[-1]].grad.abs().max()) > 0   # not a dead stack
+    errs = dict(corr2d=rel(corr2d, c2o), wv=rel(wv, wvo), d_corr=rel(corr.grad, co.grad), d_v=rel(v.grad, vo.grad))
+    for n in names:
+        errs[n.replace("NeighConsensus.conv.", "")] = rel(params[n].grad, sd[n].grad)
+    print(f"corr_forward backward B={B} L={L} {h}x{w} sym={sym}: " + ", ".join(f"{k} {e:.1e}" for k, e in errs.items()))
+    assert max(errs.values()) < TOL, errs
+
+
+def test_corr_backward_deterministic(dev):
+    """Fixed-order reductions: two backward passes give bit-identical gradients."""
+    net = _net(dev, 2, True, 20.0, seed=3)
+    c = _rand((1, 2, 8, 8, 8, 8), 4, -0.2, 1.0).float().to(dev)
+    v = _rand((1, 64, 8, 8), 5).float().to(dev)
+    G = _rand((1, 64, 8, 8), 6, -1, 1).float().to(dev)
+    grads = []
+    for _ in range(2):
+        net.zero_grad()
+        x = c.clone().requires_grad_(True)
+        _, wv = net.corr_forward(x, v, ret_attn=True)
+        (wv * G).sum().backward()
+        grads.append([x.grad.clone()] + [p.grad.clone() for p in net.parameters()])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
+def test_mmn_backward(dev):
+    """mmn.py:42-71 (rmid l34, all_lr l, agg cat, wa True, two shots): gradients of a linear
+    functional of (fq, att_fq) with respect to every MMN parameter (WeightAverage of both layers,
+    the NeighConsensus layers) and the layer features."""
+    from few_shot_seg_cwt_amd.match import MMN, init_match_params
+    from oracle import match_oracle as M
+    args = dict(rmid="l34", layers=50, all_lr="l", temp=20.0, att_wt=0.3, conv4d="red")
+    net = MMN(args, agg="cat", wa=True, red_dim=False, device=dev)
+    init_match_params(net, seed=9)
+    h, B = 6, 2
+    fq0 = {3: _rand((1, 1024, h, h), 31), 4: _rand((1, 2048, h, h), 32)}
+    fs0 = {3: _rand((B, 1024, h, h), 33), 4: _rand((B, 2048, h, h), 34)}
+    fq_in, fs_in = _rand((1, 512, h, h), 35), _rand((B, 512, h, h), 36)
+    G1, G2 = _rand((1, 512, h, h), 37, -1, 1), _rand((1, 512, h, h), 38, -1, 1)
+    fq_d = {k: [t.float().to(dev).requires_grad_(True)] for k, t in fq0.items()}
+    fs_d = {k: [t.float().to(dev).requires_grad_(True)] for k, t in fs0.items()}
+    fq, att_fq = net(fq_d, fs_d, fq_in.float().to(dev), fs_in.float().to(dev))
+    ((fq * G1.float().to(dev)).sum() + (att_fq * G2.float().to(dev)).sum()).backward()
+    sd = {k: t.detach().cpu().double().requires_grad_(True) for k, t in net.state_dict().items()}
+    wa = {b: M.wa_params_from_state(sd, f"wa_{b}.") for b in (3, 4)}
+    layers = M.layers_from_state(sd, prefix="corr_net.NeighConsensus.conv.")
+    fq_o = {k: t.clone().requires_grad_(True) for k, t in fq0.items()}
+    fs_o = {k: t.clone().requires_grad_(True) for k, t in fs0.items()}
+    fqo, atto = M.mmn_forward(fq_o, fs_o, fq_in, fs_in, [3, 4], wa, layers, 20.0, 0.3)
+    ((fqo * G1).sum() + (atto * G2).sum()).backward()
+    errs = dict(fq=rel(fq, fqo), att_fq=rel(att_fq, atto))
+    for k in (3, 4):
+        errs[f"d_fq{k}"] = rel(fq_d[k][0].grad, fq_o[k].grad)
+        errs[f"d_fs{k}"] = rel(fs_d[k][0].grad, fs_o[k].grad)
+    for n, p in net.named_parameters():
+        errs[n] = rel(p.grad, sd[n].grad)
+    print("MMN backward: " + ", ".join(f"{k} {e:.1e}" for k, e in errs.items()))
+    assert max(errs.values()) < TOL, errs
+
+
+def test_mmn_no_grad_matches_train_path(dev):
+    """The inference path (no_grad) and the autograd path give the same forward values."""
+    from few_shot_seg_cwt_amd.match import MMN, init_match_params
+    args = dict(rmid="l34", layers=50, all_lr="l", temp=20.0, att_wt=0.3, conv4d="red")
+    net = MMN(args, agg="cat", wa=True, red_dim=False, device=dev)
+    init_match_params(net, seed=2)
+    h = 8
+    fq = {3: [_rand((1, 1024, h, h), 1).float().to(dev)], 4: [_rand((1, 2048, h, h), 2).float().to(dev)]}
+    fs = {3: [_rand((1, 1024, h, h), 3).float().to(dev)], 4: [_rand((1, 2048, h, h), 4).float().to(dev)]}
+    f_q, f_s = _rand((1, 512, h, h), 5).float().to(dev), _rand((1, 512, h, h), 6).float().to(dev)
+    with torch.no_grad():
+        a = net(fq, fs, f_q, f_s)
+    b = net(fq, fs, f_q, f_s)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y.detach())

@@ -42,8 +42,20 @@ def timed(fn):
     return round(ts[len(ts) // 2], 3)
 
 
-out = {"h": h, "shots": shots,
-       "mmn_forward_ms": timed(lambda: net(fq_lst, fs_lst, f_q, f_s)),
-       "corr_forward_ms": timed(lambda: net.corr_net._run(corr, h, h, f_s)),
-       "weight_average_l4_ms": timed(lambda: net.wa_4(fq_lst[4][0]))}
+G = torch.rand(1, 512, h, h, generator=g).to(dev)
+
+
+def train_step():
+    """the head's forward + backward as the MMN trainers run it (train_cca.py:158-196)"""
+    net.zero_grad(set_to_none=True)
+    fq, att_fq = net(fq_lst, fs_lst, f_q, f_s)
+    (att_fq * G).sum().backward()
+
+
+with torch.no_grad():
+    out = {"h": h, "shots": shots,
+           "mmn_forward_ms": timed(lambda: net(fq_lst, fs_lst, f_q, f_s)),
+           "corr_forward_ms": timed(lambda: net.corr_net._run(corr, h, h, f_s)),
+           "weight_average_l4_ms": timed(lambda: net.wa_4(fq_lst[4][0]))}
+out["mmn_forward_backward_ms"] = timed(train_step)
 print(json.dumps(out))
