@@ -78,6 +78,9 @@ SIGNATURES = {
     "cwt_weight_average_backward": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                          _P, _P, _P]),
     "cwt_mmn_blend_backward": (_I, [_P, _P, _P, _I, _I64, _F, _P, _P, _P]),
+    "cwt_linear_backward": (_I, [_P, _P, _I64, _I, _P, _I, _P, _P, _P, _P, _I, _P, _P]),
+    "cwt_deform_attn_backward": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "cwt_norm_blend_backward": (_I, [_P, _P, _P, _I64, _I, _F, _P, _P, _P, _P]),
     "cwt_linear": (_I, [_P, _P, _I64, _I, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_sine_pos_add": (_I, [_P, _P, _I, _I, _I, _I, _F, _I, _F, _F, _P, _P]),
     "cwt_deform_attn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),

@@ -2058,6 +2058,83 @@ int cwt_norm_blend(cwt_ctx* ctx, const float* a, const float* b, int64_t T, int 
   return launch_norm_blend(a, b, (long)T, C, wt, out, (hipStream_t)stream);
 }
 
+// ---- DeTr head backward (train_trans.py:100): linear / 1x1 conv, deformable attention, blend ----
+int cwt_linear_backward(cwt_ctx* ctx, const float* x, int64_t P, int K, const float* w, int N, const float* out,
+                        const float* d_out, float* d_x, float* d_w, int ldw, float* d_b, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && w && d_out && P >= 1 && K >= 1 && N >= 1 && P <= (1L << 30) && (!d_w || ldw >= K), "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  const long ldN = ld32(N), ldP = ld32(P);
+  void *gm, *wt, *gt, *xt, *dw;
+  int rc;
+  if ((rc = ensure_ws(ctx, "lb.gm", (size_t)P * ldN * 4, &gm))) return rc;
+  Prof p(ctx, st, "linear_backward " + std::to_string(K) + "x" + std::to_string(N), 4.0 * P * N * K,
+         4.0 * ((double)P * K * 2 + (double)N * K * 2 + (double)P * N * 2));
+  // the output gradient through the ReLU (out > 0) when out is given
+  const float* g = d_out;
+  if (out) {
+    if ((rc = launch_relu_mask(d_out, out, P * N, (float*)gm, st))) return rc;
+    g = (const float*)gm;
+  }
+  if (d_b && (rc = launch_colsum(g, P, N, N, 0, d_b, st))) return rc;
+  if (d_x) {  // d x = g . w   (A = g [P][ldN], B^T = w^T [K][ldN])
+    const float* gp = g;
+    if (ldN != N) {
+      void* gpad;
+      if ((rc = ensure_ws(ctx, "lb.gpad", (size_t)P * ldN * 4, &gpad)) ||
+          (rc = launch_copy_pad(g, P, N, (int)ldN, (float*)gpad, st)))
+        return rc;
+      gp = (const float*)gpad;
+    }
+    if ((rc = ensure_ws(ctx, "lb.wT", (size_t)K * ldN * 4, &wt)) ||
+        (rc = launch_match_vt(w, 1, N, K, (int)ldN, (float*)wt, st)) ||
+        (rc = gemm_nt(ctx, gp, (const float*)wt, (int)P, K, (int)ldN, d_x, st)))
+      return rc;
+  }
+  if (d_w) {  // d w = g^T . x   (A = g^T [N][ldP], B^T = x^T [K][ldP])
+    if ((rc = ensure_ws(ctx, "lb.gT", (size_t)N * ldP * 4, &gt)) || (rc = ensure_ws(ctx, "lb.xT", (size_t)K * ldP * 4, &xt)) ||
+        (rc = launch_match_vt(g, 1, (int)P, N, (int)ldP, (float*)gt, st)) ||
+        (rc = launch_match_vt(x, 1, (int)P, K, (int)ldP, (float*)xt, st)))
+      return rc;
+    float* dst = d_w;
+    if (ldw != K) {
+      if ((rc = ensure_ws(ctx, "lb.dw", (size_t)N * K * 4, &dw))) return rc;
+      dst = (float*)dw;
+    }
+    if ((rc = gemm_nt(ctx, (const float*)gt, (const float*)xt, N, K, (int)ldP, dst, st))) return rc;
+    if (ldw != K && (rc = launch_copy_2d(dst, N, K, K, d_w, ldw, st))) return rc;
+  }
+  p.end();
+  return 0;
+}
+
+int cwt_deform_attn_backward(cwt_ctx* ctx, const float* value, const float* offsets, const float* logits, int B, int H,
+                             int W, int n_heads, int n_points, int d_head, const float* d_out, float* d_value,
+                             float* d_offsets, float* d_logits, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(value && offsets && logits && d_out && d_value && d_offsets && d_logits && B >= 1 && H >= 1 && W >= 1 &&
+                n_heads >= 1 && n_points >= 1 && d_head >= 1,
+            "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  Prof p(ctx, st, "deform_attn_backward", 2.0 * B * H * W * n_heads * n_points * d_head * 12,
+         4.0 * (double)B * H * W * n_heads * (d_head * 7 + n_points * 6));
+  CWT_HIP(hipMemsetAsync(d_value, 0, (size_t)B * H * W * n_heads * d_head * 4, st));
+  int rc = launch_deform_attn_bwd(value, offsets, logits, B, H, W, n_heads, n_points, d_head, d_out, d_value, d_offsets,
+                                  d_logits, st);
+  p.end();
+  return rc;
+}
+
+int cwt_norm_blend_backward(cwt_ctx* ctx, const float* a, const float* b, int64_t T, int C, float wt, const float* d_out,
+                            float* d_a, float* d_b, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(a && b && d_out && T >= 1 && C >= 1, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_norm_blend_bwd(a, b, d_out, (long)T, C, wt, d_a, d_b, (hipStream_t)stream);
+}
+
 int cwt_seg_metrics(cwt_ctx* ctx, const float* logits, const int64_t* target, int B, int h, int w, int S,
                     float* iut_out, double* ce_out, void* stream) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");

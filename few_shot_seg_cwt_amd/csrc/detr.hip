@@ -135,6 +135,153 @@ int launch_deform_attn(const float* value, const float* offsets, const float* lo
   return 0;
 }
 
+// Backward of deform_attn_kernel (ms_deform_attn.py:99-117 under autograd; the reference's CUDA
+// op backpropagates the same quantities), one wave per (batch, query, head) as the forward:
+//   v_p = bilinear(value, ix_p, iy_p), a = softmax(logits), out = sum_p a_p v_p;
+//   d a_p = <d_out, v_p>, d logits_p = a_p (d a_p - sum_q a_q d a_q),
+//   d offset_p = a_p <d_out, dv_p / d(ix, iy)> (ix = loc W - 1/2 and loc = ref + off / W, so
+//   d ix / d off_x = 1; zero-padded corners carry no value and no slope),
+//   d value[corner] += w_corner a_p d_out (float atomics: one value position is sampled by many
+//   queries, as in the reference's CUDA backward; d_value must be zeroed first).
+__global__ __launch_bounds__(256) void deform_attn_bwd_kernel(const float* __restrict__ value,
+                                                              const float* __restrict__ offsets,
+                                                              const float* __restrict__ logits, int B, int H, int W,
+                                                              int M, int P, int D, const float* __restrict__ d_out,
+                                                              float* d_value, float* __restrict__ d_offsets,
+                                                              float* __restrict__ d_logits) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const long L = (long)H * W;
+  const long nw = (long)B * L * M;
+  const long wid = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= nw) return;
+  const int m = (int)(wid % M);
+  const long bq = wid / M;
+  const int q = (int)(bq % L);
+  const int b = (int)(bq / L);
+  const int qy = q / W, qx = q - qy * W;
+  const float* lg = logits + (bq * M + m) * P;
+  const float* of = offsets + (bq * M + m) * P * 2;
+  float mx = -INFINITY;
+  for (int p = 0; p < P; ++p) mx = fmaxf(mx, lg[p]);
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += expf(lg[p] - mx);
+  const float ref_x = ((float)qx + 0.5f) / (float)W, ref_y = ((float)qy + 0.5f) / (float)H;
+  const long vs = (long)M * D;
+  const float* vb = value + (long)b * L * vs + m * D + lane;
+  float* dvb = d_value + (long)b * L * vs + m * D + lane;
+  const bool act = lane < D;
+  const float g = act ? d_out[bq * vs + m * D + lane] : 0.f;
+  float da[DA_MAXP], dox[DA_MAXP], doy[DA_MAXP], ap[DA_MAXP];
+  float sad = 0.f;
+  for (int p = 0; p < P; ++p) {
+    const float a = expf(lg[p] - mx) / s;
+    const float lx = ref_x + of[2 * p] / (float)W, ly = ref_y + of[2 * p + 1] / (float)H;
+    const float gx = 2.f * lx - 1.f, gy = 2.f * ly - 1.f;
+    const float ix = ((gx + 1.f) * (float)W - 1.f) / 2.f, iy = ((gy + 1.f) * (float)H - 1.f) / 2.f;
+    const float fx = floorf(ix), fy = floorf(iy);
+    const int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+    const float wx1 = ix - fx, wx0 = (fx + 1.f) - ix, wy1 = iy - fy, wy0 = (fy + 1.f) - iy;
+    const float w00 = wx0 * wy0, w01 = wx1 * wy0, w10 = wx0 * wy1, w11 = wx1 * wy1;
+    const bool i00 = act && (unsigned)y0 < (unsigned)H && (unsigned)x0 < (unsigned)W;
+    const bool i01 = act && (unsigned)y0 < (unsigned)H && (unsigned)x1 < (unsigned)W;
+    const bool i10 = act && (unsigned)y1 < (unsigned)H && (unsigned)x0 < (unsigned)W;
+    const bool i11 = act && (unsigned)y1 < (unsigned)H && (unsigned)x1 < (unsigned)W;
+    const float v00 = i00 ? vb[((long)y0 * W + x0) * vs] : 0.f, v01 = i01 ? vb[((long)y0 * W + x1) * vs] : 0.f;
+    const float v10 = i10 ? vb[((long)y1 * W + x0) * vs] : 0.f, v11 = i11 ? vb[((long)y1 * W + x1) * vs] : 0.f;
+    float v = 0.f;
+    v += v00 * w00;
+    v += v01 * w01;
+    v += v10 * w10;
+    v += v11 * w11;
+    const float dvx = wy0 * (v01 - v00) + wy1 * (v11 - v10), dvy = wx0 * (v10 - v00) + wx1 * (v11 - v01);
+    da[p] = wave_sum_dpp(g * v);
+    dox[p] = a * wave_sum_dpp(g * dvx);
+    doy[p] = a * wave_sum_dpp(g * dvy);
+    ap[p] = a;
+    sad += a * da[p];
+    const float gv = a * g;
+    if (i00) atomicAdd(&dvb[((long)y0 * W + x0) * vs], w00 * gv);
+    if (i01) atomicAdd(&dvb[((long)y0 * W + x1) * vs], w01 * gv);
+    if (i10) atomicAdd(&dvb[((long)y1 * W + x0) * vs], w10 * gv);
+    if (i11) atomicAdd(&dvb[((long)y1 * W + x1) * vs], w11 * gv);
+  }
+  if (lane == 0) {
+    float* dl = d_logits + (bq * M + m) * P;
+    float* dof = d_offsets + (bq * M + m) * P * 2;
+    for (int p = 0; p < P; ++p) {
+      dl[p] = ap[p] * (da[p] - sad);
+      dof[2 * p] = dox[p];
+      dof[2 * p + 1] = doy[p];
+    }
+  }
+}
+
+int launch_deform_attn_bwd(const float* value, const float* offsets, const float* logits, int B, int H, int W, int M,
+                           int P, int D, const float* d_out, float* d_value, float* d_offsets, float* d_logits,
+                           hipStream_t st) {
+  if (P > DA_MAXP || D > 64) return fail(CWT_EARG, "deform_attn: n_points <= 16 and d_model / n_heads <= 64");
+  const long nw = (long)B * H * W * M;
+  hipLaunchKernelGGL(deform_attn_bwd_kernel, dim3((unsigned)cdiv(nw, 4)), dim3(256), 0, st, value, offsets, logits, B, H,
+                     W, M, P, D, d_out, d_value, d_offsets, d_logits);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+// norm_blend's backward: d_a = (d - a_hat (a_hat . d)) / |a| (d / eps where |a| <= eps), d_b the
+// same for b scaled by wt; one wave per token
+__global__ __launch_bounds__(256) void norm_blend_bwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                             const float* __restrict__ d, long T, int C, float wt,
+                                                             float* __restrict__ d_a, float* __restrict__ d_b) {
+  const float eps = 1e-12f;
+  const int lane = threadIdx.x & 63;
+  for (long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6); r < T; r += (long)gridDim.x * 4) {
+    const float* ar = a + r * C;
+    const float* br = b + r * C;
+    const float* dr = d + r * C;
+    float sa = 0.f, sb = 0.f, pa = 0.f, pb = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      sa = fmaf(ar[c], ar[c], sa);
+      sb = fmaf(br[c], br[c], sb);
+      pa = fmaf(ar[c], dr[c], pa);
+      pb = fmaf(br[c], dr[c], pb);
+    }
+    const float na = sqrtf(wave_sum_dpp(sa)), nb = sqrtf(wave_sum_dpp(sb));
+    pa = wave_sum_dpp(pa);
+    pb = wave_sum_dpp(pb);
+    for (int c = lane; c < C; c += 64) {
+      if (d_a) d_a[r * C + c] = na > eps ? (dr[c] - (ar[c] / na) * (pa / na)) / na : dr[c] / eps;
+      if (d_b) d_b[r * C + c] = wt * (nb > eps ? (dr[c] - (br[c] / nb) * (pb / nb)) / nb : dr[c] / eps);
+    }
+  }
+}
+
+int launch_norm_blend_bwd(const float* a, const float* b, const float* d, long T, int C, float wt, float* d_a,
+                          float* d_b, hipStream_t st) {
+  hipLaunchKernelGGL(norm_blend_bwd_kernel, dim3((unsigned)std::min<long>(2048, (T + 3) / 4)), dim3(256), 0, st, a, b, d,
+                     T, C, wt, d_a, d_b);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+// dst[r][c] = src[r][c] (row strides lds / ldd)
+__global__ void copy_2d_kernel(const float* __restrict__ src, long R, int Cc, long lds, float* __restrict__ dst,
+                               long ldd) {
+  const long total = R * Cc;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / Cc;
+    const int c = (int)(i - r * Cc);
+    dst[r * ldd + c] = src[r * lds + c];
+  }
+}
+
+int launch_copy_2d(const float* src, long R, int Cc, long lds, float* dst, long ldd, hipStream_t st) {
+  hipLaunchKernelGGL(copy_2d_kernel, dim3((unsigned)std::min<long>(65536, cdiv(R * Cc, 256))), dim3(256), 0, st, src, R,
+                     Cc, lds, dst, ldd);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 // out[t] = a[t] / max(|a[t]|, 1e-12) + b[t] / max(|b[t]|, 1e-12) * wt, one wave per token
 __global__ __launch_bounds__(256) void norm_blend_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                          long T, int C, float wt, float* __restrict__ out) {

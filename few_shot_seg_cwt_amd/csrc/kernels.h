@@ -223,6 +223,12 @@ int launch_wa_bwd(const float* tpg, int N, int h, int w, int co, const float* bt
 int launch_colsum(const float* X, long R, int Cc, long ld, int accum, float* out, hipStream_t st);
 int launch_to_channels_first(const float* x, int B, int C, long P, float* y, hipStream_t st);
 int launch_copy_pad(const float* X, long R, int Cc, int ld, float* out, hipStream_t st);
+int launch_deform_attn_bwd(const float* value, const float* offsets, const float* logits, int B, int H, int W, int M,
+                           int P, int D, const float* d_out, float* d_value, float* d_offsets, float* d_logits,
+                           hipStream_t st);
+int launch_norm_blend_bwd(const float* a, const float* b, const float* d, long T, int C, float wt, float* d_a,
+                          float* d_b, hipStream_t st);
+int launch_copy_2d(const float* src, long R, int Cc, long lds, float* dst, long ldd, hipStream_t st);
 int launch_mmn_blend_bwd(const float* d_fq, const float* d_mean, int B, long n, float att_wt, float* d_att,
                          float* d_fq_in, hipStream_t st);
 

@@ -1,6 +1,6 @@
 """DeTr, the transformer head of the train_trans / train_tp_trans variants,
 on HIP kernels (csrc/detr.hip, the f32-MFMA GEMM of csrc/heads.hip, MatchNet of csrc/match.hip)
-behind the C ABI, forward only:
+behind the C ABI:
 
   SinePositionalEncoding(num_feats, ...)          src/model/positional_encoding.py:7-74
   MSDeformAttn(d_model, n_levels, n_heads, ...)   src/model/ops/modules/ms_deform_attn.py:30-117
@@ -22,6 +22,12 @@ the entries, which does not match what this repo's reference PSPNet.get_feat_lis
 ``rmid`` names the layers as in_fea_dim_lookup does ('l34' = layer3 + layer4, 1024 + 2048
 channels, detr.py:10), and fq_lst / fs_lst may be that dict (of features or one-element lists) or
 a list indexed by layer - 2.
+
+Training (round 4): under autograd every op of the head has its device
+backward -- cwt_linear_backward (adjust_feature's segments, the four MSDeformAttn projections),
+cwt_deform_attn_backward (softmax over the points, bilinear sampling: values, offsets, logits),
+cwt_norm_blend_backward, the position embedding's identity gradient, and MatchNet's
+(match.py) -- so DeTr trains as train_trans.py:100 runs it.
 
 Parity is unpinned: the reference cannot be run here and holds no fixtures for this
 head; tests/test_gpu_detr.py checks it against oracle/detr_oracle.py (float64, torch's own
@@ -66,15 +72,79 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     return out
 
 
+def _needs_grad(*ts) -> bool:
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
+class _LinearFn(torch.autograd.Function):
+    """linear under autograd; the backward is cwt_linear_backward (ReLU mask from the output)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu):
+        out = linear(x, weight, bias, relu)
+        ctx.save_for_backward(x, weight, out if relu else None)
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, d):
+        x, weight, out = ctx.saved_tensors
+        w = weight.detach().reshape(weight.shape[0], -1).contiguous()
+        N, K = w.shape
+        P = x.shape[0]
+        d = d.contiguous()
+        f = dict(device=x.device, dtype=torch.float32)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty((N, K), **f) if ctx.needs_input_grad[1] else None
+        db = torch.empty(N, **f) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        _lib.check(_lib.lib().cwt_linear_backward(_lib.ctx(x.device.index), _lib.ptr(x), P, K, _lib.ptr(w), N,
+                                                  _lib.ptr(out), _lib.ptr(d), _lib.ptr(dx), _lib.ptr(dw), K,
+                                                  _lib.ptr(db), _lib.stream_ptr(x.device)), "cwt_linear_backward")
+        return dx, (dw.reshape(weight.shape) if dw is not None else None), db, None
+
+
+def linear_t(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, relu: bool = False):
+    """linear, differentiable when x or the parameters require grad."""
+    if _needs_grad(x, weight, bias):
+        return _LinearFn.apply(x, weight, bias, relu)
+    return linear(x, weight, bias, relu)
+
+
+class _NormBlendFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, at, bt, wt):
+        ctx.save_for_backward(at, bt)
+        ctx.wt = float(wt)
+        return _norm_blend_tokens(at, bt, wt)
+
+    @staticmethod
+    def backward(ctx, d):
+        at, bt = ctx.saved_tensors
+        B, C, h, w = at.shape
+        dt = as_tokens(d)
+        da = torch.empty_like(at) if ctx.needs_input_grad[0] else None
+        db = torch.empty_like(bt) if ctx.needs_input_grad[1] else None
+        _lib.check(_lib.lib().cwt_norm_blend_backward(_lib.ctx(at.device.index), _lib.ptr(at), _lib.ptr(bt), B * h * w,
+                                                      C, ctx.wt, _lib.ptr(dt), _lib.ptr(da), _lib.ptr(db),
+                                                      _lib.stream_ptr(at.device)), "cwt_norm_blend_backward")
+        return da, db, None
+
+
+def _norm_blend_tokens(at, bt, wt):
+    B, C, h, w = at.shape
+    out = torch.empty((B, C, h, w), device=at.device, dtype=torch.float32, memory_format=torch.channels_last)
+    _lib.check(_lib.lib().cwt_norm_blend(_lib.ctx(at.device.index), _lib.ptr(at), _lib.ptr(bt), B * h * w, C, float(wt),
+                                         _lib.ptr(out), _lib.stream_ptr(at.device)), "cwt_norm_blend")
+    return out
+
+
 def norm_blend(a: torch.Tensor, b: torch.Tensor, wt: float) -> torch.Tensor:
     """F.normalize(a, dim=1) + F.normalize(b, dim=1) * wt for [B, C, h, w] maps (detr.py:41,45);
-    returns a channels_last [B, C, h, w] map."""
+    returns a channels_last [B, C, h, w] map (differentiable: cwt_norm_blend_backward)."""
     at, bt = as_tokens(a), as_tokens(b)
-    B, C, h, w = at.shape
-    out = torch.empty((B, C, h, w), device=a.device, dtype=torch.float32, memory_format=torch.channels_last)
-    _lib.check(_lib.lib().cwt_norm_blend(_lib.ctx(a.device.index), _lib.ptr(at), _lib.ptr(bt), B * h * w, C, float(wt),
-                                         _lib.ptr(out), _lib.stream_ptr(a.device)), "cwt_norm_blend")
-    return out
+    if _needs_grad(at, bt):
+        return _NormBlendFn.apply(at, bt, wt)
+    return _norm_blend_tokens(at, bt, wt)
 
 
 class SinePositionalEncoding(torch.nn.Module):
@@ -90,17 +160,65 @@ class SinePositionalEncoding(torch.nn.Module):
                                                                                   scale, eps)
 
     def add_to(self, x: torch.Tensor) -> torch.Tensor:
-        """x [B, C, h, w] with C = 2 num_feats -> x + pos (channels_last)."""
+        """x [B, C, h, w] with C = 2 num_feats -> x + pos (channels_last); the gradient with respect
+        to x is the identity (pos is a constant of the shape)."""
         xt = as_tokens(x)
         B, C, h, w = xt.shape
         if C != 2 * self.num_feats:
             raise ValueError(f"expected {2 * self.num_feats} channels, got {C}")
+        if _needs_grad(xt):
+            return _AddPosFn.apply(xt, self)
+        return self._add(xt)
+
+    def _add(self, xt: torch.Tensor) -> torch.Tensor:
+        B, C, h, w = xt.shape
         out = torch.empty_like(xt)
-        _lib.check(_lib.lib().cwt_sine_pos_add(_lib.ctx(x.device.index), _lib.ptr(xt), B, h, w, C,
+        _lib.check(_lib.lib().cwt_sine_pos_add(_lib.ctx(xt.device.index), _lib.ptr(xt), B, h, w, C,
                                                float(self.temperature), int(self.normalize), float(self.scale),
-                                               float(self.eps), _lib.ptr(out), _lib.stream_ptr(x.device)),
+                                               float(self.eps), _lib.ptr(out), _lib.stream_ptr(xt.device)),
                    "cwt_sine_pos_add")
         return out
+
+
+class _AddPosFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xt, mod):
+        return mod._add(xt)
+
+    @staticmethod
+    def backward(ctx, d):
+        return d, None
+
+
+def _deform_core(value, offs, logits, N, H, W, M, P, D):
+    core = torch.empty((N * H * W, M * D), device=value.device, dtype=torch.float32)
+    _lib.check(_lib.lib().cwt_deform_attn(_lib.ctx(value.device.index), _lib.ptr(value), _lib.ptr(offs),
+                                          _lib.ptr(logits), N, H, W, M, P, D, _lib.ptr(core),
+                                          _lib.stream_ptr(value.device)), "cwt_deform_attn")
+    return core
+
+
+class _DeformCoreFn(torch.autograd.Function):
+    """The deformable-attention core under autograd (cwt_deform_attn / cwt_deform_attn_backward)."""
+
+    @staticmethod
+    def forward(ctx, value, offs, logits, N, H, W, M, P, D):
+        core = _deform_core(value, offs, logits, N, H, W, M, P, D)
+        ctx.save_for_backward(value, offs, logits)
+        ctx.meta = (N, H, W, M, P, D)
+        return core
+
+    @staticmethod
+    def backward(ctx, d):
+        value, offs, logits = ctx.saved_tensors
+        N, H, W, M, P, D = ctx.meta
+        d = d.contiguous()
+        dv, do, dl = torch.empty_like(value), torch.empty_like(offs), torch.empty_like(logits)
+        _lib.check(_lib.lib().cwt_deform_attn_backward(_lib.ctx(value.device.index), _lib.ptr(value), _lib.ptr(offs),
+                                                       _lib.ptr(logits), N, H, W, M, P, D, _lib.ptr(d), _lib.ptr(dv),
+                                                       _lib.ptr(do), _lib.ptr(dl), _lib.stream_ptr(value.device)),
+                   "cwt_deform_attn_backward")
+        return dv, do, dl, None, None, None, None, None, None
 
 
 class MSDeformAttn(torch.nn.Module):
@@ -154,15 +272,15 @@ class MSDeformAttn(torch.nn.Module):
             raise ValueError("MSDeformAttn: queries must be the H*W pixel centres of the single level")
         q = query.reshape(N * Lq, C).contiguous()
         v_in = input_flatten.reshape(N * Lq, C).contiguous()
-        value = linear(v_in, self.value_proj.weight, self.value_proj.bias)
-        offs = linear(q, self.sampling_offsets.weight, self.sampling_offsets.bias)
-        logits = linear(q, self.attention_weights.weight, self.attention_weights.bias)
-        core = torch.empty((N * Lq, C), device=query.device, dtype=torch.float32)
-        _lib.check(_lib.lib().cwt_deform_attn(_lib.ctx(query.device.index), _lib.ptr(value), _lib.ptr(offs),
-                                              _lib.ptr(logits), N, H, W, self.n_heads, self.n_points,
-                                              C // self.n_heads, _lib.ptr(core), _lib.stream_ptr(query.device)),
-                   "cwt_deform_attn")
-        return linear(core, self.output_proj.weight, self.output_proj.bias).reshape(N, Lq, C)
+        value = linear_t(v_in, self.value_proj.weight, self.value_proj.bias)
+        offs = linear_t(q, self.sampling_offsets.weight, self.sampling_offsets.bias)
+        logits = linear_t(q, self.attention_weights.weight, self.attention_weights.bias)
+        M, P = self.n_heads, self.n_points
+        if _needs_grad(value, offs, logits):
+            core = _DeformCoreFn.apply(value, offs, logits, N, H, W, M, P, C // M)
+        else:
+            core = _deform_core(value, offs, logits, N, H, W, M, P, C // M)
+        return linear_t(core, self.output_proj.weight, self.output_proj.bias).reshape(N, Lq, C)
 
 
 class DeformAtt(torch.nn.Module):
@@ -194,6 +312,44 @@ class DeformAtt(torch.nn.Module):
         vt = as_tokens(f_q).permute(0, 2, 3, 1).reshape(B, h * w, C)
         out = self.self_trans(qt, None, vt, [[h, w]])
         return out.reshape(B, h, w, C).permute(0, 3, 1, 2)
+
+
+class _AdjustFn(torch.autograd.Function):
+    """adjust_feature (detr.py:22,58-59) under autograd: d x_l = g . W_l and the weight gradient's
+    column segment l = g^T . x_l, with g the output gradient through the ReLU."""
+
+    @staticmethod
+    def forward(ctx, mod, weight, *feats):
+        out = mod._adjust(list(feats))
+        ctx.mod = mod
+        ctx.save_for_backward(out, *feats)
+        return out
+
+    @staticmethod
+    def backward(ctx, d):
+        out, *feats = ctx.saved_tensors
+        mod = ctx.mod
+        B, N, h, w = out.shape
+        P = B * h * w
+        dt = as_tokens(d).permute(0, 2, 3, 1).reshape(P, N)
+        o2 = out.permute(0, 2, 3, 1).reshape(P, N)
+        segs = mod._weight_segments([f.shape[1] for f in feats])
+        Ktot = sum(f.shape[1] for f in feats)
+        dev = out.device
+        dW = torch.empty((N, Ktot), device=dev, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        grads, off = [], 0
+        for i, (f, wseg) in enumerate(zip(feats, segs)):
+            K = f.shape[1]
+            ft = f.permute(0, 2, 3, 1).reshape(P, K)
+            dx = torch.empty_like(f) if ctx.needs_input_grad[2 + i] else None
+            dxt = dx.permute(0, 2, 3, 1).reshape(P, K) if dx is not None else None
+            _lib.check(_lib.lib().cwt_linear_backward(
+                _lib.ctx(dev.index), _lib.ptr(ft), P, K, _lib.ptr(wseg), N, _lib.ptr(o2), _lib.ptr(dt), _lib.ptr(dxt),
+                _lib.ptr(dW[:, off:]) if dW is not None else None, Ktot, None, _lib.stream_ptr(dev)),
+                "cwt_linear_backward")
+            grads.append(dx)
+            off += K
+        return (None, dW.reshape(mod.adjust_feature[0].weight.shape) if dW is not None else None, *grads)
 
 
 class DeTr(torch.nn.Module):
@@ -246,25 +402,33 @@ class DeTr(torch.nn.Module):
             f = lst[lid - 2]
         return f[0] if isinstance(f, (list, tuple)) else f
 
+    def _adjust(self, feats):
+        """relu(sum_l x_l . W_l^T) over the layer segments (the concatenation never materialised)."""
+        B, _, h, w = feats[0].shape
+        segs = self._weight_segments([f.shape[1] for f in feats])
+        out = torch.empty((B, self.reduce_dim, h, w), device=feats[0].device, dtype=torch.float32,
+                          memory_format=torch.channels_last)
+        o2 = out.permute(0, 2, 3, 1).reshape(B * h * w, self.reduce_dim)
+        for i, (f, wseg) in enumerate(zip(feats, segs)):
+            ft = as_tokens(f).permute(0, 2, 3, 1).reshape(B * h * w, f.shape[1])
+            last = i == len(feats) - 1
+            linear(ft, wseg, None, relu=last, out=o2, accumulate=i > 0)
+        return out
+
     def compute_feat(self, fq_lst, fs_lst):
         """detr.py:49-61: relu(conv1x1(cat(layer features))) for the query and the support maps,
-        the concatenation never materialised (one product per layer segment, accumulated)."""
+        the concatenation never materialised (one product per layer segment, accumulated);
+        differentiable (cwt_linear_backward per segment) under autograd."""
         outs = []
+        weight = self.adjust_feature[0].weight
         for lst in (fq_lst, fs_lst):
-            feats = [self._layer(lst, lid) for lid in self.layers_used]
-            B, _, h, w = feats[0].shape
-            segs = self._weight_segments([f.shape[1] for f in feats])
-            out = torch.empty((B, self.reduce_dim, h, w), device=feats[0].device, dtype=torch.float32,
-                              memory_format=torch.channels_last)
-            o2 = out.permute(0, 2, 3, 1).reshape(B * h * w, self.reduce_dim)
-            for i, (f, wseg) in enumerate(zip(feats, segs)):
-                ft = as_tokens(f).permute(0, 2, 3, 1).reshape(B * h * w, f.shape[1])
-                last = i == len(feats) - 1
-                linear(ft, wseg, None, relu=last, out=o2, accumulate=i > 0)
-            outs.append(out)
+            feats = [as_tokens(self._layer(lst, lid)) for lid in self.layers_used]
+            if _needs_grad(weight, *feats):
+                outs.append(_AdjustFn.apply(self, weight, *feats))
+            else:
+                outs.append(self._adjust(feats))
         return outs[0], outs[1]
 
-    @torch.no_grad()
     def forward(self, fq_lst, fs_lst, f_q, f_s, padding_mask=None, s_padding_mask=None):
         if padding_mask is not None or s_padding_mask is not None:
             raise NotImplementedError("DeTr: padding masks are not built (train_trans.py passes None)")

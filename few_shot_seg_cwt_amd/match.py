@@ -12,7 +12,7 @@ HIP kernels (csrc/match.hip) behind the C ABI:
 
 Training (round 4): under autograd (grad enabled and a parameter or input
 requiring grad) MatchNet.corr_forward / forward ('red' layers), get_corr, WeightAverage and the
-MMN head (agg 'cat', red_dim False: every MMN config) run their backward on the device --
+MMN head (agg 'cat' or 'sum', red_dim) run their backward on the device --
 cwt_match_corr_backward (softmax readout, both MutualMatchings with torch.max's single-index
 gradient routing, the CenterPivotConv4d layers' input / weight / bias gradients over both
 symmetric branches), cwt_corr_backward, cwt_weight_average_backward, cwt_mmn_blend_backward
@@ -476,7 +476,7 @@ class _MMNCorrFn(torch.autograd.Function):
     shared by the B support rows (fq expanded, mmn.py:50) accumulating its B gradients in order."""
 
     @staticmethod
-    def forward(ctx, B, L, *feats):
+    def forward(ctx, B, L, agg_sum, *feats):
         h, w = feats[0].shape[2], feats[0].shape[3]
         P = h * w
         dev = feats[0].device
@@ -488,21 +488,26 @@ class _MMNCorrFn(torch.autograd.Function):
                 _lib.check(_lib.lib().cwt_corr(_lib.ctx(dev.index), _lib.ptr(qb), _lib.ptr(k[b:b + 1]), 1, P, P,
                                                q.shape[1], _lib.ptr(corr4d[b, li]), _lib.stream_ptr(dev)), "cwt_corr")
         ctx.save_for_backward(*feats)
-        ctx.BL = (B, L)
+        ctx.BL = (B, L, agg_sum)
+        if agg_sum:   # mmn.py:62-63: the layers' correlations summed into one channel
+            summed = torch.empty((B, 1, P, P), device=dev, dtype=torch.float32)
+            _lib.check(_lib.lib().cwt_channel_sum(_lib.ctx(dev.index), _lib.ptr(corr4d), B, L, P * P, _lib.ptr(summed),
+                                                  _lib.stream_ptr(dev)), "cwt_channel_sum")
+            return summed
         return corr4d
 
     @staticmethod
     def backward(ctx, g):
         feats = ctx.saved_tensors
-        B, L = ctx.BL
-        g = g.contiguous()
+        B, L, agg_sum = ctx.BL
+        g = g.contiguous()   # agg 'sum': every layer's correlation receives the summed channel's gradient
         h, w = feats[0].shape[2], feats[0].shape[3]
         P = h * w
         dev = feats[0].device
         grads = []
         for li in range(L):
             q, k = feats[2 * li], feats[2 * li + 1]
-            nq, nk = ctx.needs_input_grad[2 + 2 * li], ctx.needs_input_grad[3 + 2 * li]
+            nq, nk = ctx.needs_input_grad[3 + 2 * li], ctx.needs_input_grad[4 + 2 * li]
             dq = torch.empty_like(q) if nq else None
             dk = torch.empty_like(k) if nk else None
             if nq or nk:
@@ -511,11 +516,11 @@ class _MMNCorrFn(torch.autograd.Function):
                     qi = 0 if shared else b
                     _lib.check(_lib.lib().cwt_corr_backward(
                         _lib.ctx(dev.index), _lib.ptr(q[qi:qi + 1]), _lib.ptr(k[b:b + 1]), 1, P, P, q.shape[1],
-                        _lib.ptr(g[b, li]), _lib.ptr(dq[qi:qi + 1]) if nq else None,
+                        _lib.ptr(g[b, 0 if agg_sum else li]), _lib.ptr(dq[qi:qi + 1]) if nq else None,
                         _lib.ptr(dk[b:b + 1]) if nk else None, int(shared and b > 0), 0, _lib.stream_ptr(dev)),
                         "cwt_corr_backward")
             grads += [dq, dk]
-        return (None, None, *grads)
+        return (None, None, None, *grads)
 
 
 class _MMNBlendFn(torch.autograd.Function):
@@ -588,28 +593,29 @@ class MMN(torch.nn.Module):
                                  sce=False, cyc=False, sym_mode=True, in_channel=match_ch, device=dev)
 
     def _reduce(self, idx: int, x: torch.Tensor) -> torch.Tensor:
-        from .detr import linear
+        """rd_<layer>: 1x1 conv (no bias) + ReLU on the f32-MFMA GEMM (differentiable: linear_t)."""
+        from .detr import linear_t
         conv = getattr(self, "rd_" + str(idx))[0]
         xt = as_tokens(x)
         N, C, h, w = xt.shape
-        y = linear(xt.permute(0, 2, 3, 1).reshape(N * h * w, C), conv.weight, None, relu=True)
+        y = linear_t(xt.permute(0, 2, 3, 1).reshape(N * h * w, C), conv.weight, None, relu=True)
         return y.reshape(N, h, w, -1).permute(0, 3, 1, 2)
 
     def _forward_train(self, fq_lst, fs_lst, f_q, f_s, ret_attn: bool):
-        """forward under autograd: WeightAverage, the stacked correlations, corr_forward and the
-        blend as differentiable device ops (agg 'cat', red_dim False: every MMN config)."""
-        if self.red_dim or self.agg != "cat":
-            raise NotImplementedError("MMN backward: agg 'cat' without red_dim only (every reference MMN config)")
+        """forward under autograd: red_dim's 1x1 conv + ReLU, WeightAverage, the stacked (or, agg
+        'sum', summed) correlations, corr_forward and the blend as differentiable device ops."""
         B, ch, h, w = f_s.shape
         L = len(self.bid_lst)
         feats = []
         for idx in self.bid_lst[::-1]:
             fq_fea, fs_fea = fq_lst[idx][0], fs_lst[idx][0]
+            if self.red_dim:
+                fq_fea, fs_fea = self._reduce(idx, fq_fea), self._reduce(idx, fs_fea)
             if self.wa:
                 m = getattr(self, "wa_" + str(idx))
                 fq_fea, fs_fea = m(fq_fea), m(fs_fea)
             feats += [as_tokens(fq_fea), as_tokens(fs_fea)]
-        corr4d = _MMNCorrFn.apply(B, L, *feats)
+        corr4d = _MMNCorrFn.apply(B, L, self.agg == "sum", *feats)
         attn, att = self.corr_net._run(corr4d, h, w, f_s)
         fq, att_fq = _MMNBlendFn.apply(as_tokens(f_q), as_tokens(att), self.att_wt)
         return (attn, fq, att_fq) if ret_attn else (fq, att_fq)

@@ -477,6 +477,27 @@ int cwt_weight_average_backward(cwt_ctx* ctx, const float* x, int N, int h, int 
 int cwt_mmn_blend_backward(cwt_ctx* ctx, const float* d_fq, const float* d_att_mean, int B, int64_t n, float att_wt,
                            float* d_att, float* d_fq_in, void* stream);
 
+/* cwt_linear's backward (nn.Linear / the 1x1 nn.Conv2d of detr.py:22, ms_deform_attn.py:56-59):
+ * x device [P][K], w device [N][K], out device [P][N] the forward's output when it ended in a ReLU
+ * (its > 0 mask gates d_out) or NULL, d_out device [P][N] -> d_x device [P][K], d_w device [N][ldw]
+ * (a column slice of a wider weight when ldw > K: adjust_feature's per-layer segments), d_b device
+ * [N]; each may be NULL. */
+int cwt_linear_backward(cwt_ctx* ctx, const float* x, int64_t P, int K, const float* w, int N, const float* out,
+                        const float* d_out, float* d_x, float* d_w, int ldw, float* d_b, void* stream);
+
+/* cwt_deform_attn's backward (ms_deform_attn.py:99-117, ms_deform_attn_func.py:41-61 under autograd;
+ * one level, DeTr's pixel-centre reference points): d_out device [B][H*W][n_heads*d_head] ->
+ * d_value (same shape, accumulated with float atomics as the reference CUDA op does),
+ * d_offsets device [B][H*W][n_heads][n_points][2], d_logits device [B][H*W][n_heads][n_points]. */
+int cwt_deform_attn_backward(cwt_ctx* ctx, const float* value, const float* offsets, const float* logits, int B, int H,
+                             int W, int n_heads, int n_points, int d_head, const float* d_out, float* d_value,
+                             float* d_offsets, float* d_logits, void* stream);
+
+/* cwt_norm_blend's backward (detr.py:41,45): d_out device [T][C] -> d_a, d_b device [T][C] (either
+ * may be NULL). */
+int cwt_norm_blend_backward(cwt_ctx* ctx, const float* a, const float* b, int64_t T, int C, float wt, const float* d_out,
+                            float* d_a, float* d_b, void* stream);
+
 /* ---- DeTr head (src/model/detr.py:13-151), forward only; tokens are [B][hw][C] (NHWC) ---- */
 
 /* nn.Linear / 1x1 nn.Conv2d over tokens (detr.py:22 adjust_feature, ms_deform_attn.py:56-59

@@ -185,3 +185,39 @@ def test_mmn_no_grad_matches_train_path(dev):
     b = net(fq, fs, f_q, f_s)
     for x, y in zip(a, b):
         assert torch.equal(x, y.detach())
+
+
+@pytest.mark.parametrize("agg,red_dim", [("sum", False), ("cat", 512)])
+def test_mmn_backward_agg_red_dim(dev, agg, red_dim):
+    """MMN with agg 'sum' (mmn.py:62-63) and with red_dim (rd_<layer> 1x1 conv + ReLU, mmn.py:28-31,
+    49-51): parameter and feature gradients against the oracle chain."""
+    from few_shot_seg_cwt_amd.match import MMN, init_match_params
+    from oracle import match_oracle as M
+    args = dict(rmid="l34", layers=50, all_lr="l", temp=20.0, att_wt=0.3, conv4d="red")
+    net = MMN(args, agg=agg, wa=True, red_dim=red_dim, device=dev)
+    init_match_params(net, seed=12)
+    h, B = 6, 2
+    fq0 = {3: _rand((1, 1024, h, h), 41), 4: _rand((1, 2048, h, h), 42)}
+    fs0 = {3: _rand((B, 1024, h, h), 43), 4: _rand((B, 2048, h, h), 44)}
+    fq_in, fs_in = _rand((1, 512, h, h), 45), _rand((B, 512, h, h), 46)
+    G = _rand((1, 512, h, h), 47, -1, 1)
+    fq_d = {k: [t.float().to(dev).requires_grad_(True)] for k, t in fq0.items()}
+    fs_d = {k: [t.float().to(dev).requires_grad_(True)] for k, t in fs0.items()}
+    _, att_fq = net(fq_d, fs_d, fq_in.float().to(dev), fs_in.float().to(dev))
+    (att_fq * G.float().to(dev)).sum().backward()
+    sd = {k: t.detach().cpu().double().requires_grad_(True) for k, t in net.state_dict().items()}
+    wa = {b: M.wa_params_from_state(sd, f"wa_{b}.") for b in (3, 4)}
+    rdw = {b: sd[f"rd_{b}.0.weight"] for b in (3, 4)} if red_dim else None
+    layers = M.layers_from_state(sd, prefix="corr_net.NeighConsensus.conv.")
+    fq_o = {k: t.clone().requires_grad_(True) for k, t in fq0.items()}
+    fs_o = {k: t.clone().requires_grad_(True) for k, t in fs0.items()}
+    _, atto = M.mmn_forward(fq_o, fs_o, fq_in, fs_in, [3, 4], wa, layers, 20.0, 0.3, agg=agg, rd_weights=rdw)
+    (atto * G).sum().backward()
+    errs = dict(att_fq=rel(att_fq, atto))
+    for k in (3, 4):
+        errs[f"d_fq{k}"] = rel(fq_d[k][0].grad, fq_o[k].grad)
+        errs[f"d_fs{k}"] = rel(fs_d[k][0].grad, fs_o[k].grad)
+    for n, p in net.named_parameters():
+        errs[n] = rel(p.grad, sd[n].grad)
+    print(f"MMN backward agg={agg} red_dim={red_dim}: " + ", ".join(f"{k} {e:.1e}" for k, e in errs.items()))
+    assert max(errs.values()) < TOL, errs
