@@ -1956,11 +1956,14 @@ int cwt_weight_average_backward(cwt_ctx* ctx, const float* x, int N, int h, int 
   // softmax-weighted neighbourhood and the cosine similarities (msm_func.py:66-97)
   if ((rc = launch_wa_bwd(tpg, N, h, w, co, b_theta, b_phi, b_g, (const float*)dwavg, (float*)coef, (float*)dtpg, st)))
     return rc;
-  // biases: column sums in row order
-  if ((rc = launch_colsum((const float*)dtpg, P, co, 3L * co, 0, d_b_theta, st)) ||
-      (rc = launch_colsum((const float*)dtpg + co, P, co, 3L * co, 0, d_b_phi, st)) ||
-      (rc = launch_colsum((const float*)dtpg + 2 * co, P, co, 3L * co, 0, d_b_g, st)) ||
-      (rc = launch_colsum(d_out, P, C, C, 0, d_b_back, st)))
+  // biases: column sums in a fixed order
+  void* csw;
+  const size_t csn = colsum_ws_floats(P, C);
+  if ((rc = ensure_ws(ctx, "colsum", csn * 4, &csw))) return rc;
+  if ((rc = launch_colsum((const float*)dtpg, P, co, 3L * co, 0, d_b_theta, (float*)csw, csn, st)) ||
+      (rc = launch_colsum((const float*)dtpg + co, P, co, 3L * co, 0, d_b_phi, (float*)csw, csn, st)) ||
+      (rc = launch_colsum((const float*)dtpg + 2 * co, P, co, 3L * co, 0, d_b_g, (float*)csw, csn, st)) ||
+      (rc = launch_colsum(d_out, P, C, C, 0, d_b_back, (float*)csw, csn, st)))
     return rc;
   // d w_back = d_out^T . wavg, d w_tpg = d tpg^T . x (reductions over the pixels, zero-padded to 32)
   if ((rc = launch_match_vt(d_out, 1, (int)P, C, (int)ldP, (float*)dot, st)) ||
@@ -2077,7 +2080,12 @@ int cwt_linear_backward(cwt_ctx* ctx, const float* x, int64_t P, int K, const fl
     if ((rc = launch_relu_mask(d_out, out, P * N, (float*)gm, st))) return rc;
     g = (const float*)gm;
   }
-  if (d_b && (rc = launch_colsum(g, P, N, N, 0, d_b, st))) return rc;
+  if (d_b) {
+    void* csw;
+    const size_t csn = colsum_ws_floats(P, N);
+    if ((rc = ensure_ws(ctx, "colsum", csn * 4, &csw)) || (rc = launch_colsum(g, P, N, N, 0, d_b, (float*)csw, csn, st)))
+      return rc;
+  }
   if (d_x) {  // d x = g . w   (A = g [P][ldN], B^T = w^T [K][ldN])
     const float* gp = g;
     if (ldN != N) {

@@ -209,6 +209,8 @@ int launch_mutual_matching_bwd(const float* x, const float* dy, int B, int NA, i
                                const MmBwdWs& ws, hipStream_t st);
 int launch_relu_mask(const float* g, const float* out, long n, float* gm, hipStream_t st);
 int cp4d_wgrad_part_floats(int cin, int cout);
+int launch_cp4d_wgrad_mfma(const float* x, const float* gm, int B, int hA, int wA, int hB, int wB, int cin, int cout,
+                           int G, float* part, hipStream_t st);
 int launch_cp4d_wgrad(const float* x, const float* gm, int B, int hA, int wA, int hB, int wB, int cin, int cout,
                       float* part, size_t part_floats, float* dWa, float* dWb, float* db1, float* db2, hipStream_t st);
 int launch_cp4d_dgrad(const float* g, int B, int hA, int wA, int hB, int wB, int gin, int gout, const float* Wa,
@@ -220,7 +222,9 @@ int launch_token_norm_bwd(const float* xn, const float* nrm, const float* dxn, l
                           int accum, float* dx, hipStream_t st);
 int launch_wa_bwd(const float* tpg, int N, int h, int w, int co, const float* bt, const float* bp, const float* bg,
                   const float* dwavg, float* coef, float* dtpg, hipStream_t st);
-int launch_colsum(const float* X, long R, int Cc, long ld, int accum, float* out, hipStream_t st);
+size_t colsum_ws_floats(long R, int Cc);
+int launch_colsum(const float* X, long R, int Cc, long ld, int accum, float* out, float* ws, size_t ws_floats,
+                  hipStream_t st);
 int launch_to_channels_first(const float* x, int B, int C, long P, float* y, hipStream_t st);
 int launch_copy_pad(const float* X, long R, int Cc, int ld, float* out, hipStream_t st);
 int launch_deform_attn_bwd(const float* value, const float* offsets, const float* logits, int B, int H, int W, int M,

@@ -279,11 +279,14 @@ __device__ __forceinline__ void cm_stage(const float* __restrict__ x, int hA, in
 // 9 CIN rows padded to a multiple of 4 (zero weights): MFMA m, lane group g = lane / 16 takes
 // k = 4 m + g, read at the lane's per-k LDS offset.  Both 2-D convolutions (a plane, b plane)
 // accumulate into the same accumulators.  4 waves x 4 groups = the tile's 256 pairs.
-template <int CIN>
+// MODE 1: the input gradient of a layer with 10 input channels (the backward, launch_cp4d_dgrad):
+// transposed, flipped filters (W[(c COUT + o) 9 + 8 - tap]), no bias, no ReLU, y accumulated when
+// accum != 0.
+template <int CIN, int MODE = 0>
 __global__ __launch_bounds__(256) void cp4d_mfma_kernel(const float* __restrict__ x, int hA, int wA, int hB, int wB,
                                                         const float* __restrict__ Wa, const float* __restrict__ ba,
                                                         const float* __restrict__ Wb, const float* __restrict__ bb,
-                                                        float* __restrict__ y) {
+                                                        float* __restrict__ y, int accum = 0) {
   constexpr int COUT = 10;
   constexpr int KT = 9 * CIN;        // K rows per branch
   constexpr int NM = (KT + 3) / 4;   // MFMAs per branch and group
@@ -309,8 +312,9 @@ __global__ __launch_bounds__(256) void cp4d_mfma_kernel(const float* __restrict_
     const int tap = kin ? k / CIN : 0, c = kin ? k % CIN : 0;
     const int ky = tap / 3, kx = tap - 3 * (tap / 3);
     const bool live = kin && r < COUT;
-    wra[m] = live ? Wa[(r * CIN + c) * 9 + tap] : 0.f;
-    wrb[m] = live ? Wb[(r * CIN + c) * 9 + tap] : 0.f;
+    const int wi = MODE == 0 ? (r * CIN + c) * 9 + tap : (c * COUT + r) * 9 + 8 - tap;
+    wra[m] = live ? Wa[wi] : 0.f;
+    wrb[m] = live ? Wb[wi] : 0.f;
     offa[m] = (ky * CM_H + kx) * CM_NT * CIN + c;
     offb[m] = (ky * CM_H + kx) * CIN + c;
   }
@@ -338,7 +342,7 @@ __global__ __launch_bounds__(256) void cp4d_mfma_kernel(const float* __restrict_
   }
   // D: lane (col o = r, rows 4 g4 + i) -> pair (a = G, b = 4 g4 + i), channel o
   if (r < COUT) {
-    const float bias = ba[r] + bb[r];
+    const float bias = MODE == 0 ? ba[r] + bb[r] : 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int G = wv * 4 + j;
@@ -348,12 +352,123 @@ __global__ __launch_bounds__(256) void cp4d_mfma_kernel(const float* __restrict_
       for (int i = 0; i < 4; ++i) {
         const int bt = 4 * g4 + i;
         const int hb = hb0 + bt / CM_T, wb = wb0 + bt % CM_T;
-        if (hb < hB && wb < wB)
-          y[(long)blockIdx.z * NA * NB * COUT + ((long)(ha * wA + wa) * NB + hb * wB + wb) * COUT + r] =
-              fmaxf(acc[j][i] + bias, 0.f);
+        if (hb < hB && wb < wB) {
+          float* yp = y + (long)blockIdx.z * NA * NB * COUT + ((long)(ha * wA + wa) * NB + hb * wB + wb) * COUT + r;
+          *yp = MODE == 0 ? fmaxf(acc[j][i] + bias, 0.f) : accum ? *yp + acc[j][i] : acc[j][i];
+        }
       }
     }
   }
+}
+
+// Weight and bias gradients of one CenterPivotConv4d layer (the backward, match_bwd.hip) on the
+// same matrix cores: dW[(side, tap, c)][o] = sum over pairs p of X_side,tap[p][c] G[p][o] is the
+// transpose of the forward GEMM -- rows the 18 CIN (side, tap, channel) entries plus one row of
+// ones (whose result is the bias gradient sum_p G[p][o]), columns the COUT output channels, K the
+// pairs.  Workgroups stride over the forward's 4x4 (a) by 4x4 (b) tiles, staged as cm_stage does,
+// with the tile's (ReLU-masked) output gradient beside them; MFMA k-step s takes pairs 4 s .. 4 s
+// + 3 (lane group g4 = pair within the step), wave w the row blocks w, w + 4, ...; the sums stay
+// in the accumulators across tiles and land in part[workgroup] ([(side, tap, o)][c], then the
+// bias), summed in workgroup order by cp4d_wgrad_reduce_kernel.
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void cp4d_wgrad_mfma_kernel(const float* __restrict__ x, const float* __restrict__ gm,
+                                                              int B, int hA, int wA, int hB, int wB,
+                                                              float* __restrict__ part) {
+  constexpr int KE = 18 * CIN;              // (side, tap, c) rows; row KE = ones (the bias)
+  constexpr int MB = (KE + 1 + 15) / 16;    // 16-row blocks
+  constexpr int MW = (MB + 3) / 4;          // blocks per wave
+  constexpr int EA = CmLds<CIN>::EA, EB = CmLds<CIN>::EB;
+  constexpr int NE = 18 * COUT;
+  __shared__ __attribute__((aligned(16))) float xs[EA + EB + 2];
+  __shared__ float gl[CM_NT * CM_NT][COUT];
+  float* xa = xs;
+  float* xb = xs + EA;
+  const int NA = hA * wA, NB = hB * wB;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int i16 = lane & 15, g4 = lane >> 4;
+  // this lane's A rows: kind 0 data (LDS offset off[], box b[]), 1 the ones row, 2 padding
+  int off[MW], kind[MW];
+  bool inb[MW];
+#pragma unroll
+  for (int mw = 0; mw < MW; ++mw) {
+    const int kk = 16 * (wv + 4 * mw) + i16;
+    kind[mw] = kk < KE ? 0 : kk == KE ? 1 : 2;
+    const int k2 = kk < KE ? kk : 0;
+    const int side = k2 / (9 * CIN), tap = (k2 / CIN) % 9, c = k2 % CIN;
+    const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+    inb[mw] = side != 0;
+    off[mw] = side == 0 ? (ky * CM_H + kx) * CM_NT * CIN + c : EA + (ky * CM_H + kx) * CIN + c;
+  }
+  f32x4 acc[MW];
+#pragma unroll
+  for (int mw = 0; mw < MW; ++mw) acc[mw] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ntbw = (wB + CM_T - 1) / CM_T, ntaw = (wA + CM_T - 1) / CM_T;
+  const long ntb = (long)((hB + CM_T - 1) / CM_T) * ntbw, nta = (long)((hA + CM_T - 1) / CM_T) * ntaw;
+  const long ntiles = (long)B * nta * ntb;
+  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const long tb = tile % ntb, rest = tile / ntb;
+    const long ta = rest % nta, bz = rest / nta;
+    const int ha0 = (int)(ta / ntaw) * CM_T, wa0 = (int)(ta % ntaw) * CM_T;
+    const int hb0 = (int)(tb / ntbw) * CM_T, wb0 = (int)(tb % ntbw) * CM_T;
+    __syncthreads();  // the previous tile's LDS reads are done
+    cm_stage<CIN>(x, hA, wA, hB, wB, ha0, wa0, hb0, wb0, bz * NA * NB * CIN, xa, xb);
+    for (int e = t; e < CM_NT * CM_NT * COUT; e += 256) {
+      const int o = e % COUT, p = e / COUT;
+      const int at = p / CM_NT, bt = p % CM_NT;
+      const int ha = ha0 + at / CM_T, wa = wa0 + at % CM_T, hb = hb0 + bt / CM_T, wb = wb0 + bt % CM_T;
+      const bool in = ha < hA && wa < wA && hb < hB && wb < wB;
+      (&gl[0][0])[e] = in ? gm[(bz * NA * NB + (long)(ha * wA + wa) * NB + hb * wB + wb) * COUT + o] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int st = 0; st < CM_NT * CM_NT / 4; ++st) {
+      const int p = 4 * st + g4, at = p / CM_NT, bt = p % CM_NT;
+      const int terma = (((at / CM_T) * CM_H + at % CM_T) * CM_NT + bt) * CIN;
+      const int termb = (at * CM_NH + (bt / CM_T) * CM_H + bt % CM_T) * CIN;
+      const float bv = i16 < COUT ? gl[p][i16 < COUT ? i16 : 0] : 0.f;
+#pragma unroll
+      for (int mw = 0; mw < MW; ++mw) {
+        if (wv + 4 * mw >= MB) continue;
+        const float av = kind[mw] == 0 ? xs[(inb[mw] ? termb : terma) + off[mw]] : kind[mw] == 1 ? 1.f : 0.f;
+        acc[mw] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[mw], 0, 0, 0);
+      }
+    }
+  }
+  // D: lane (column o = i16, rows 4 g4 + r of block m)
+  float* pw = part + (long)blockIdx.x * (NE * CIN + COUT);
+  if (i16 < COUT) {
+#pragma unroll
+    for (int mw = 0; mw < MW; ++mw) {
+      const int m = wv + 4 * mw;
+      if (m >= MB) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kk = 16 * m + 4 * g4 + r;
+        if (kk < KE) {
+          const int side = kk / (9 * CIN), tap = (kk / CIN) % 9, c = kk % CIN;
+          pw[((side * 9 + tap) * COUT + i16) * CIN + c] = acc[mw][r];
+        } else if (kk == KE) {
+          pw[NE * CIN + i16] = acc[mw][r];
+        }
+      }
+    }
+  }
+}
+
+int launch_cp4d_wgrad_mfma(const float* x, const float* gm, int B, int hA, int wA, int hB, int wB, int cin, int cout,
+                           int G, float* part, hipStream_t st) {
+#define CWT_WGM(CI, CO)                                                                                            \
+  if (cin == CI && cout == CO) {                                                                                   \
+    hipLaunchKernelGGL((cp4d_wgrad_mfma_kernel<CI, CO>), dim3(G), dim3(256), 0, st, x, gm, B, hA, wA, hB, wB, part); \
+    CWT_LAUNCH_CHECK();                                                                                            \
+    return 0;                                                                                                      \
+  }
+  CWT_WGM(1, 10)
+  CWT_WGM(2, 10)
+  CWT_WGM(10, 10)
+  CWT_WGM(10, 1)
+#undef CWT_WGM
+  return fail(CWT_EARG, "cp4d wgrad: channels (1|2 -> 10, 10 -> 10, 10 -> 1) only");
 }
 
 // COUT = 1 (the consensus stack's last layer, CIN = 10): a thread per (a, b) pair of the same
@@ -1211,6 +1326,18 @@ int launch_cp4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int
 // channels), Wa / Wb the a-plane / b-plane filters the forward applied ([gin][gout][3][3])
 int launch_cp4d_dgrad(const float* g, int B, int hA, int wA, int hB, int wB, int gin, int gout, const float* Wa,
                       const float* Wb, float* dx, int accum, hipStream_t st) {
+  static const bool scalar = getenv("CWT_DGRAD_SCALAR") && getenv("CWT_DGRAD_SCALAR")[0] == '1';  // A/B only
+  if (gout == 10 && (gin == 1 || gin == 10) && !scalar) {  // 10 output channels: the matrix-core form
+    const dim3 g4(cdiv(hB, CM_T) * cdiv(wB, CM_T), cdiv(hA, CM_T) * cdiv(wA, CM_T), B);
+    if (gin == 1)
+      hipLaunchKernelGGL((cp4d_mfma_kernel<1, 1>), g4, dim3(256), 0, st, g, hA, wA, hB, wB, Wa, (const float*)nullptr,
+                         Wb, (const float*)nullptr, dx, accum);
+    else
+      hipLaunchKernelGGL((cp4d_mfma_kernel<10, 1>), g4, dim3(256), 0, st, g, hA, wA, hB, wB, Wa, (const float*)nullptr,
+                         Wb, (const float*)nullptr, dx, accum);
+    CWT_LAUNCH_CHECK();
+    return 0;
+  }
   dim3 grid(cdiv(hB, CP_TBH) * cdiv(wB, CP_TBW), cdiv(hA, CP_TAH) * cdiv(wA, CP_TAW), B);
 #define CWT_CPD(CI, CO)                                                                                     \
   if (gin == CI && gout == CO) {                                                                            \

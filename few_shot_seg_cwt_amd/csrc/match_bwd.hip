@@ -338,26 +338,39 @@ __global__ void cp4d_wgrad_reduce_kernel(const float* __restrict__ part, int G, 
   }
 }
 
-int cp4d_wgrad_part_floats(int cin, int cout) { return 256 * (18 * cout * cin + cout); }
+// workgroups of the weight-gradient pass: 512 for the 10 -> 10 layer (two per CU by LDS), 2048 for
+// the thinner layers (less LDS each; measured 0.52 against 1.26 ms for 2 -> 10 at 60^2)
+static int wgrad_grid(int cin, int cout) { return cin * cout >= 100 ? 512 : 2048; }
+int cp4d_wgrad_part_floats(int cin, int cout) {
+  (void)cin;
+  (void)cout;
+  return std::max(512 * (18 * 10 * 10 + 10), 2048 * (18 * 10 * 2 + 10));  // the largest of the four layers
+}
 
 int launch_cp4d_wgrad(const float* x, const float* gm, int B, int hA, int wA, int hB, int wB, int cin, int cout,
                       float* part, size_t part_floats, float* dWa, float* dWb, float* db1, float* db2,
                       hipStream_t st) {
   const long ntiles = (long)B * cdiv(hA, WG_TAH) * cdiv(wA, WG_TAW) * cdiv(hB, WG_TBH) * cdiv(wB, WG_TBW);
-  const int G = (int)std::min<long>(256, ntiles);
+  const int G = (int)std::min<long>(wgrad_grid(cin, cout), ntiles);
   const int n = 18 * cout * cin + cout;
   if ((size_t)G * n > part_floats) return fail(CWT_ESTATE, "cp4d wgrad: partial workspace too small");
+  static const bool scalar = getenv("CWT_WGRAD_SCALAR") && getenv("CWT_WGRAD_SCALAR")[0] == '1';  // A/B only
+  if (!scalar) {
+    int rc = launch_cp4d_wgrad_mfma(x, gm, B, hA, wA, hB, wB, cin, cout, G, part, st);
+    if (rc) return rc;
+  } else {
 #define CWT_WG(CI, CO)                                                                                        \
   if (cin == CI && cout == CO) {                                                                              \
     hipLaunchKernelGGL((cp4d_wgrad_kernel<CI, CO>), dim3(G), dim3(256), 0, st, x, gm, B, hA, wA, hB, wB, part); \
     CWT_LAUNCH_CHECK();                                                                                       \
   } else
-  CWT_WG(1, 10)
-  CWT_WG(2, 10)
-  CWT_WG(10, 10)
-  CWT_WG(10, 1)
-  return fail(CWT_EARG, "cp4d wgrad: channels (1|2 -> 10, 10 -> 10, 10 -> 1) only");
+    CWT_WG(1, 10)
+    CWT_WG(2, 10)
+    CWT_WG(10, 10)
+    CWT_WG(10, 1)
+    return fail(CWT_EARG, "cp4d wgrad: channels (1|2 -> 10, 10 -> 10, 10 -> 1) only");
 #undef CWT_WG
+  }
   hipLaunchKernelGGL(cp4d_wgrad_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, (const float*)part, G, cin, cout,
                      dWa, dWb, db1, db2);
   CWT_LAUNCH_CHECK();
@@ -622,17 +635,43 @@ int launch_wa_bwd(const float* tpg, int N, int h, int w, int co, const float* bt
 }
 
 // ---- small helpers ----
-// out[c] (+)= sum_r X[r][c] (row stride ld), rows in order: the bias gradients
-__global__ void colsum_kernel(const float* __restrict__ X, long R, int Cc, long ld, int accum, float* __restrict__ out) {
+// out[c] (+)= sum_r X[r][c] (row stride ld): the bias gradients.  Two fixed-order stages: chunks
+// of CS_ROWS rows summed per (64-column block, chunk) workgroup, 4 row lanes of 64 columns each
+// combined in lane order; then the chunk partials summed in chunk order.
+constexpr int CS_ROWS = 64;
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ X, long R, int Cc, long ld,
+                                                          float* __restrict__ part) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
+  const long r0 = (long)blockIdx.y * CS_ROWS;
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (c < Cc)
+    for (int i = rl; i < CS_ROWS && r0 + i < R; i += 4) s += X[(r0 + i) * ld + c];
+  red[rl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rl == 0 && c < Cc) {
+    const int l = threadIdx.x & 63;
+    part[(long)blockIdx.y * Cc + c] = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+  }
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ part, int nch, int Cc, int accum, float* __restrict__ out) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= Cc) return;
   float s = 0.f;
-  for (long r = 0; r < R; ++r) s += X[r * ld + c];
+  for (int k = 0; k < nch; ++k) s += part[(long)k * Cc + c];
   out[c] = accum ? out[c] + s : s;
 }
 
-int launch_colsum(const float* X, long R, int Cc, long ld, int accum, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_kernel, dim3(cdiv(Cc, 256)), dim3(256), 0, st, X, R, Cc, ld, accum, out);
+size_t colsum_ws_floats(long R, int Cc) { return (size_t)cdiv(R, CS_ROWS) * Cc; }
+
+int launch_colsum(const float* X, long R, int Cc, long ld, int accum, float* out, float* ws, size_t ws_floats,
+                  hipStream_t st) {
+  const int nch = cdiv(R, CS_ROWS);
+  if (!ws || ws_floats < colsum_ws_floats(R, Cc)) return fail(CWT_ESTATE, "colsum: workspace too small");
+  hipLaunchKernelGGL(colsum_part_kernel, dim3(cdiv(Cc, 64), nch), dim3(256), 0, st, X, R, Cc, ld, ws);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(Cc, 256)), dim3(256), 0, st, (const float*)ws, nch, Cc, accum, out);
   CWT_LAUNCH_CHECK();
   return 0;
 }
