@@ -280,9 +280,11 @@ static int zero_line(cwt_ctx* ctx, const __bf16** out) {
 // 1x1 conv's fp32 packing is plain row-major [Co][Ci]); the epilogue is fmaf(acc, 1, bias) then
 // + res, the order of the separate bias / residual passes it replaces.  Shapes: K % 32 == 0,
 // N % 64 == 0, 16-B aligned operands (gemm_f32d_ok); the rest stay on corr_gemm_kernel.
-// Used for MatchNet's readout and cwt_linear; WeightAverage's two GEMMs measured slower on it
-// with the heuristic plans (0.72 against 0.66 ms for the layer-4 module, profiles/r4/run_i) and
-// stay on corr_gemm_kernel unless CWT_GEMM_F32D=2.  CWT_GEMM_F32D=0 keeps every GEMM there.
+// Used for MatchNet's readout, cwt_linear and (with the measured plans of the heads' GEMM shapes,
+// conv_plans_f32d.inc from tools/conv_s_sweep.py --configs 0:60:1, profiles/r4/sweeps) the
+// WeightAverage GEMMs -- with the heuristic plans those measured slower than corr_gemm_kernel
+// (0.72 against 0.66 ms for the layer-4 module, profiles/r4/run_i).  CWT_GEMM_F32D=0 keeps
+// every GEMM on corr_gemm_kernel.
 static int gemm_f32d_mode() {
   static const int m = getenv("CWT_GEMM_F32D") ? atoi(getenv("CWT_GEMM_F32D")) : 1;
   return m;
@@ -1896,7 +1898,7 @@ static int weight_average(cwt_ctx* ctx, const float* x, int N, int h, int w, int
   if (wavg_keep) wavg = wavg_keep;
   Prof p(ctx, st, "weight_average c" + std::to_string(C), 2.0 * P * C * co * 4, 4.0 * P * (2.0 * C + 5.0 * co));
   // theta | phi | g of every pixel: one GEMM against the three stacked 1x1 weights [3co][C]
-  const bool wa_f32d = gemm_f32d_mode() == 2;
+  const bool wa_f32d = gemm_f32d_mode() != 0;
   if (wa_f32d && gemm_f32d_ok((int)P, 3 * co, C, x, w_tpg, tpg, nullptr)) {
     if ((rc = gemm_f32d(ctx, x, w_tpg, (int)P, 3 * co, C, (float*)tpg, nullptr, nullptr, 0, st))) return rc;
   } else if ((rc = launch_gemm_abt(x, w_tpg, 1, (int)P, 3 * co, C, (float*)tpg, st))) {

@@ -21,6 +21,12 @@ def shapes(layers, S, N):
     """(name, count, Ci, Co, Hi, k, stride, dil, res) of the implicit-GEMM convs of one
     extractor pass (api.hip run_extract; resnet.py:57-96 blocks with pspnet.py:124-129's
     dilation surgery, the PPM-folded bottleneck conv), identical shapes merged."""
+    if layers == 0:   # the variant heads' GEMMs as 1x1 convs over an S x S map (MMN WeightAverage
+        # theta|phi|g and conv_back, forward and the backward's row-major products; config 0:60:1)
+        return [("wa4_tpg", 1, 2048, 3072, S, 1, 1, 1, False), ("wa4_back", 1, 1024, 2048, S, 1, 1, 1, True),
+                ("wa3_tpg", 1, 1024, 1536, S, 1, 1, 1, False), ("wa3_back", 1, 512, 1024, S, 1, 1, 1, True),
+                ("wa4_dwavg", 1, 2048, 1024, S, 1, 1, 1, False), ("wa4_dx", 1, 3072, 2048, S, 1, 1, 1, True),
+                ("wa3_dwavg", 1, 1024, 512, S, 1, 1, 1, False), ("wa3_dx", 1, 1536, 1024, S, 1, 1, 1, True)]
     d2 = lambda x: (x - 1) // 2 + 1  # noqa: E731
     Hs = d2(S)
     H1 = d2(Hs)
