@@ -4,7 +4,7 @@
 # other operating points (configs #3-#5).
 set -u
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-O=gpurun_out/r4final
+O=${O:-gpurun_out/r4final}
 mkdir -p $O
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --profile-json $O/per_launch.json > $O/bench.json 2> $O/bench.err || exit $?
 cd /tmp && R=$GRAFT_REPO_ROOT
