@@ -857,8 +857,13 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
   // NRES 5: two units in lockstep, both in registers (the second one in cur2, as NRES 4's third):
   // no LDS reads of f in the z and dW passes
   constexpr bool BREG = NRES == 5;
+  // NRES 6: NRES 3 with the workgroup's first unit resident in registers (res): its f is never
+  // streamed, the DMA ring carries only the units after it (5-shot 641^2: 4-5 units per workgroup,
+  // about a fifth of the per-step stream)
+  constexpr bool STREAM = NRES == 3 || NRES == 6;
+  constexpr bool RES1 = NRES == 6;
   __shared__ float fl2[LOCK ? PA_NW : 1][PA_CPW][LOCK ? 64 : 1];
-  __shared__ __attribute__((aligned(16))) float fs3[NRES == 3 ? PA_NW * 64 * PA_CPW : 4];  // NRES 3: per-wave f slices
+  __shared__ __attribute__((aligned(16))) float fs3[(NRES == 3 || NRES == 6) ? PA_NW * 64 * PA_CPW : 4];  // NRES 3, 6: per-wave f slices
   __shared__ float dlw[PA_NW][EWK][PA_CPW];     // d = W1 - W0 of each wave's channels (wave-private)
   __shared__ float wlw[PA_NW][EWK][2][PA_CPW];  // W0, W1 of each wave's channels (wave-private)
   // NRES 2 runs its two units in lockstep (one set of LDS barriers, one butterfly and one set
@@ -914,9 +919,17 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
   }
   PaTile cur;
   PaUnit q = pa_unit(a, u0);
-  float* fw = fs3 + (NRES == 3 ? wv * 64 * PA_CPW : 0);
-  int ynx[2][2];  // NRES 3: labels of the unit whose f is in flight
-  if (NRES == 3) {
+  float* fw = fs3 + (STREAM ? wv * 64 * PA_CPW : 0);
+  int ynx[2][2] = {{255, 255}, {255, 255}};  // NRES 3, 6: labels of the unit whose f is in flight
+  PaTile res;  // NRES 6: the resident first unit
+  if (RES1) {
+    pa_load(res, a, q, wv, lane);
+    if (u1 - u0 > 1) {
+      const PaUnit qn = pa_unit(a, u0 + 1);
+      pa_issue_f(a, qn, wv, lane, fw);
+      pa_labels(ynx, a, qn, wv, lane);
+    }
+  } else if (STREAM) {
     pa_issue_f(a, q, wv, lane, fw);
     pa_labels(ynx, a, q, wv, lane);
   } else {
@@ -993,7 +1006,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
         }
       }
     };
-    if (NRES != 3) zero_share();
+    if (!STREAM) zero_share();
     // NRES 3: each unit's dW is reduced over the wave by the butterfly as usual, and the one
     // value a lane then holds (channel lane >> 1) is summed over the step's units of one episode
     // in a register; one atomic per episode and step (none in flight at the next unit's DMA wait)
@@ -1090,10 +1103,14 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       {
         float accd[PA_CPW];
         const float gp = gs[lane];
+        if constexpr (RES1) {  // the products formed on the fly (at most 16 live beside res and cur)
+          accd[0] = pa_butterfly_fn([&](int j) { return gp * fget(j); }, lane);
+        } else {
 #pragma unroll
-        for (int j = 0; j < PA_CPW; ++j) accd[j] = gp * fget(j);
-        pa_butterfly(accd, lane);  // lane L: channel (L >> 1) of the wave's slice, summed over 64 lanes
-        if (NRES == 3) {  // summed over the step's units of the episode, flushed on a change of episode
+          for (int j = 0; j < PA_CPW; ++j) accd[j] = gp * fget(j);
+          pa_butterfly(accd, lane);  // lane L: channel (L >> 1) of the wave's slice, summed over 64 lanes
+        }
+        if (STREAM) {  // summed over the step's units of the episode, flushed on a change of episode
           if (q.e != dsum3_e) {
             flush3();
             dsum3_e = q.e;
@@ -1318,7 +1335,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
     };
     if constexpr (FLOOR) {
       // timing study: no unit work (NRES 3 still drains its in-flight DMA)
-      if (NRES == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (STREAM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if constexpr (NRES == 4) {
       triple_body(u1 - u0);
     } else if constexpr (NRES == 2 || NRES == 5) {
@@ -1326,8 +1343,12 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       pair_body(q, has_b ? pa_unit(a, u0 + 1) : q, has_b);
     } else
     for (int u = u0; u < u1; ++u) {
-      if (NRES == 3) {  // this wave's slice of unit u landed (nothing younger is in flight), then
-                        // the next unit's DMA goes out while unit u is computed
+      if (RES1 && u == u0) {  // the resident unit, computed while the next unit's DMA is in flight
+        unit_body(pa_unit(a, u0), u0, [&](int jj) { return res.fr[jj]; }, res.y);
+        continue;
+      }
+      if (STREAM) {  // this wave's slice of unit u landed (nothing younger is in flight), then
+                     // the next unit's DMA goes out while unit u is computed
         const PaUnit qu = pa_unit(a, u);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         pa_read_f(cur.fr, fw, lane);
@@ -1357,7 +1378,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       }
       unit_body(q, u, [&](int jj) { return cur.fr[jj]; }, cur.y);
     }
-    if (NRES == 3) {
+    if (STREAM) {
       flush3();
       zero_share();
     }
@@ -1368,9 +1389,10 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
     stamp(4);
     if (STAMPS && stp) stp[8] = __builtin_amdgcn_s_memrealtime();
     if (t == 0) __hip_atomic_fetch_add(a.cnt + rep * PA_CNT_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (NRES == 3 && s + 1 < a.iters) {  // next step's first unit: W-independent, lands during the wait
-      pa_issue_f(a, pa_unit(a, u0), wv, lane, fw);
-      pa_labels(ynx, a, pa_unit(a, u0), wv, lane);
+    if (STREAM && s + 1 < a.iters && u0 + (RES1 ? 1 : 0) < u1) {  // next step's first streamed unit:
+      const PaUnit qn = pa_unit(a, u0 + (RES1 ? 1 : 0));               // W-independent, lands during the wait
+      pa_issue_f(a, qn, wv, lane, fw);
+      pa_labels(ynx, a, qn, wv, lane);
     }
     if (NRES == 0 && s + 1 < a.iters) {  // next step's first unit: W-independent, lands during the wait
       q = pa_unit(a, u0);
@@ -1502,6 +1524,12 @@ static int persist_geometry(int E, int n, int h, int w, int upw_pref, int* G_out
   const bool breg = !(brs && brs[0] == '0');
   int nres = k == 1 ? 1 : (k == 2 && span <= 2) ? (breg ? 5 : 2) : (k == 3 && span <= 2 && lock3) ? 4 : 0;
   if (nres == 0 && k >= stream_from && span <= 2) nres = 3;
+  // the streamed form with the first unit resident in registers (nres 6): opt in with
+  // CWT_ADAPT_RES1=1 -- measured slower (5-shot 641^2 alone: 6.77 against 5.87 ms; the resident f
+  // does not fit beside the streamed unit at 1,024 threads and 25 VGPRs spill to scratch, whose
+  // per-step reloads cost more than the fifth of the stream they save; profiles/r4/run_n)
+  const char* r1s = getenv("CWT_ADAPT_RES1");
+  if (nres == 3 && r1s && r1s[0] == '1') nres = 6;
   if (span > (nres >= 2 ? 2 : PA_EW)) return 1;
   // three units per workgroup: as few workgroups as that takes (5-shot 473^2: 197, not 256 with
   // two or three units each -- the step waits for the three-unit ones either way, and fewer
@@ -1571,6 +1599,7 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
     default: CWT_PA_LAUNCH(NR, 0); break;    \
   }
   switch (nres) {
+    case 6: CWT_PA_MODES(6); break;
     case 5: CWT_PA_MODES(5); break;
     case 4: CWT_PA_MODES(4); break;
     case 3: CWT_PA_MODES(3); break;
@@ -1606,9 +1635,10 @@ const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw) {
   int pG = 0, punits = 0, pncb = 0, pnres = 0, puc = 0;
   const char* pe = getenv("CWT_ADAPT_PERSIST");
   if (iters > 0 && !(pe && pe[0] == '0') && persist_geometry(E, n, h, w, upw, &pG, &punits, &pncb, &pnres, &puc) == 0) {
-    static const char* names[6] = {"adapt_persist_kernel<0", "adapt_persist_kernel<1", "adapt_persist_kernel<2",
-                                   "adapt_persist_kernel<3", "adapt_persist_kernel<4", "adapt_persist_kernel<5"};
-    return names[pnres <= 5 ? pnres : 0];
+    static const char* names[7] = {"adapt_persist_kernel<0", "adapt_persist_kernel<1", "adapt_persist_kernel<2",
+                                   "adapt_persist_kernel<3", "adapt_persist_kernel<4", "adapt_persist_kernel<5",
+                                   "adapt_persist_kernel<6"};
+    return names[pnres <= 6 ? pnres : 0];
   }
   return "adapt_step_kernel<";
 }

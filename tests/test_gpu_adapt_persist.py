@@ -27,17 +27,18 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def _run(persist, f, lbl, W0, iters, uc=None, upw=None, stream=None):
+def _run(persist, f, lbl, W0, iters, uc=None, upw=None, stream=None, res1=None):
     """persist: "0" per-step launches, "2" the persistent loop also where units are streamed;
     upw: units per workgroup ("1": f in registers; "2": two units in lockstep, both in registers
     (adapt_persist_kernel<5>); "2lds": the same with the second unit's f in LDS (<2>));
-    stream: "1" the LDS-streamed form from 3 units per workgroup, "0" never."""
+    stream: "1" the LDS-streamed form from 3 units per workgroup, "0" never; res1: "1" the first
+    unit of each workgroup resident in registers (<6>, opt-in), default every unit streamed (<3>)."""
     from few_shot_seg_cwt_amd.episode import inner_adapt_batch
     breg = None
     if upw == "2lds":
         upw, breg = "2", "0"
     env = {"CWT_ADAPT_PERSIST": persist, "CWT_ADAPT_UC": uc, "CWT_ADAPT_UPW": upw, "CWT_ADAPT_STREAM": stream,
-           "CWT_ADAPT_BREG": breg}
+           "CWT_ADAPT_BREG": breg, "CWT_ADAPT_RES1": res1}
     old = {k: os.environ.get(k) for k in env}
     for k, v in env.items():
         if v is None:
@@ -89,20 +90,22 @@ def test_persist_equals_step_launches(dev, E, n, S, iters, uc, upw):
     (2, 3, 129, 20),   # workgroups spanning two episodes
     (6, 1, 65, 10),
 ])
-def test_lds_streamed_units_equal_step_launches(dev, E, n, S, iters):
+@pytest.mark.parametrize("res1", ["0", "1"])
+def test_lds_streamed_units_equal_step_launches(dev, E, n, S, iters, res1):
     """The LDS-streamed form (each wave DMAs its 32-channel slice of the next unit into its own
     LDS while the current unit is computed; per-episode register sums of the butterfly results)
-    forced on from 3 units per workgroup."""
+    forced on from 3 units per workgroup; res1 "1": the first unit of each workgroup resident in
+    registers (adapt_persist_kernel<6>), "0": every unit streamed (<3>)."""
     h = (S - 1) // 8 + 1
     f = torch.from_numpy(syn.normal(7, f"fs{E}{n}{S}", (E * n, 512, h, h), 0.1)).to(dev)
     f = f.contiguous(memory_format=torch.channels_last)
     lbl = torch.stack([torch.from_numpy(syn.make_episode(SEED, 90 + e, S, n)["s_label"][0]) for e in range(E)]).to(dev)
     W0 = torch.from_numpy(syn.normal(8, f"ws{E}{n}{S}", (E, 2, 512), 0.04)).to(dev)
     Wp = _run("2", f, lbl, W0, iters, upw="1" if E * n * ((h - 1) * ((h - 2) // 31 + 1)) > 256 else "2",
-              stream="1")
+              stream="1", res1=res1)
     Ws = _run("0", f, lbl, W0, iters)
     errs = [rel(Wp[e], Ws[e]) for e in range(E)]
-    print(f"stream E={E} n={n} S={S}: max rel {max(errs):.2e}")
+    print(f"stream E={E} n={n} S={S} res1={res1}: max rel {max(errs):.2e}")
     assert max(errs) < 1e-4, errs
 
 
