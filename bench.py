@@ -746,6 +746,7 @@ def main():
         fex = [r for r in frecs if r[0].startswith("extract_features")]
         fdom = [r for r in frecs if r[0].startswith("conv_igemm")]
         fex_fl, fex_ms = sum(r[1] for r in fex), sum(r[3] for r in fex)
+        f_traffic, f_traffic_src = pmc_traffic(fdom[0][0].split(" ")[0].split("+")[0]) if fdom else (None, None)
         exact_fp32 = {
             "value": round(world * nx / dtf, 3), "unit": "episodes/s",
             "ms_per_step": round(dtf / nx * 1e3, 3), "steps": nx,
@@ -762,7 +763,9 @@ def main():
                 "achieved": round(sum(r[1] for r in fdom) / (sum(r[3] for r in fdom) * 1e-3) / 1e12, 2),
                 "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(sum(r[1] for r in fdom) / (sum(r[3] for r in fdom) * 1e-3) / 1e12
-                              / PEAK_FP32_MFMA_TFLOPS, 4)}}
+                              / PEAK_FP32_MFMA_TFLOPS, 4),
+                "traffic": f_traffic, "traffic_unit": "bytes/launch", "traffic_source": f_traffic_src,
+                "algorithmic_bytes_per_launch": round(fdom[0][2]) if len(fdom[0]) > 2 else None}}
         if "sequential" in legs and head != "sequential":
             dts_, _ = legs["sequential"]
             exact_fp32["sequential"] = {"value": round(world * nx / dts_, 3),
