@@ -491,6 +491,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     iuts = [step(s, W0[args.warmup + s], last=s == args.steps - 1) for s in range(args.steps)]
+    t_sub = time.perf_counter()   # the host has enqueued every step (a diagnostic of host-boundness)
     if pipe is not None:
         pipe.wait()
     torch.cuda.synchronize()
@@ -846,6 +847,7 @@ def main():
                           "note": "executed in the declared re-associated form (DESIGN.md §3, ~59 MFLOP of token work)"}},
         "iou_fg_timed": None if args.train else round(float((iu[0, 1] / iu[1, 1].clamp_min(1)).item()), 4),
         "sequential": seq,
+        "host_submit_ms_per_step": round((t_sub - t0) / args.steps * 1e3, 3),
         "batched_pipeline": pairs,
         "exact_fp32": exact_fp32,
     }

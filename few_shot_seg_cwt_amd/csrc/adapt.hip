@@ -1629,6 +1629,16 @@ size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lb
   return 0;
 }
 
+// Workgroups of the persistent inner loop launch_adapt will use for this geometry (each holds a
+// whole CU for the whole loop), 0 when it will use the per-step launches
+int adapt_persist_workgroups(int E, int n, int h, int w, int iters, int upw) {
+  int pG = 0, punits = 0, pncb = 0, pnres = 0, puc = 0;
+  const char* pe = getenv("CWT_ADAPT_PERSIST");
+  if (iters > 0 && !(pe && pe[0] == '0') && persist_geometry(E, n, h, w, upw, &pG, &punits, &pncb, &pnres, &puc) == 0)
+    return pG;
+  return 0;
+}
+
 // Which inner-loop kernel launch_adapt will use for this geometry (profile record names):
 // "adapt_persist_kernel<NRES" or "adapt_step_kernel<"
 const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw) {

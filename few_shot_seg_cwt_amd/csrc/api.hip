@@ -33,6 +33,7 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
                  AdaptDevArgs* dargs, AdaptGraphCache* cache, int upw, unsigned* status, long spin_limit,
                  hipStream_t st, hipEvent_t ev_k0, hipEvent_t ev_k1);
 const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw);
+int adapt_persist_workgroups(int E, int n, int h, int w, int iters, int upw);
 extern unsigned long long* g_adapt_stamps;
 extern long g_adapt_stamps_n;
 size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lbl, size_t* sc, size_t* acc,
@@ -2461,6 +2462,13 @@ int cwt_profile_record(cwt_ctx* ctx, int i, char* name, int name_len, double* fl
     CWT_HIP(hipEventSynchronize(r.e1));
     CWT_HIP(hipEventElapsedTime(ms, r.e0, r.e1));
   }
+  return 0;
+}
+
+int cwt_adapt_workgroups(cwt_ctx* ctx, int E, int n, int h, int w, int iters, int* G) {
+  if (!ctx || !G || E < 1 || n < 1 || h < 2 || w < 2) return fail(CWT_EARG, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  *G = adapt_persist_workgroups(E, n, h, w, iters, ctx->adapt_upw);
   return 0;
 }
 

@@ -14,6 +14,7 @@ Everything stays on the device; the host reads back per-episode IoU counts only.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import time
 from collections import defaultdict
@@ -293,6 +294,26 @@ class EpisodePipeline:
         # CWT_PIPE_DRAIN=0 turns it off (A/B).
         self.drain = os.environ.get("CWT_PIPE_DRAIN", "1") != "0"
         self.c_solo = None
+        # Opt-in (CWT_PIPE_DRAIN_OVERLAP=1): that loop on a stream of its own beside the previous
+        # episode's loop and tail (instead of after them) whenever the two persistent grids fit on
+        # the chip together (1-shot 473^2: 59 + 118 of 256 CUs; not 5-shot: 197 + 197), its tail
+        # then following on the adapt stream.  Measured no faster at the driver's 20 steps
+        # (470.5 vs 472.2 episodes/s, 3 interleaved pairs, profiles/r4/run_r), so off.
+        self.drain_overlap = os.environ.get("CWT_PIPE_DRAIN_OVERLAP", "0") == "1"
+        self.s_drain = None
+        self._fits = {}
+
+    def _drain_fits(self, shot: int, h: int, w: int, iters: int) -> bool:
+        key = (shot, h, w, iters)
+        if key not in self._fits:
+            gs = []
+            for c in (self.c_adapt, self.c_solo):
+                g = ctypes.c_int(0)
+                _lib.check(_lib.lib().cwt_adapt_workgroups(c, 1, shot, h, w, iters, ctypes.byref(g)),
+                           "cwt_adapt_workgroups")
+                gs.append(g.value)
+            self._fits[key] = min(gs) > 0 and sum(gs) <= _lib.cu_count(self.device)
+        return self._fits[key]
 
     @torch.no_grad()
     def submit(self, imgs: torch.Tensor, s_label: torch.Tensor, q_label: torch.Tensor, W0: torch.Tensor,
@@ -320,6 +341,28 @@ class EpisodePipeline:
             if self.c_solo is None:
                 self.c_solo = _lib.new_ctx()   # automatic geometry (cwt_ctx_set_adapt_units 0)
             c_ad = self.c_solo
+            if self.drain_overlap and self._drain_fits(shot, f_all.shape[2], f_all.shape[3], eng.iters):
+                if self.s_drain is None:
+                    self.s_drain = torch.cuda.Stream()
+                self.s_drain.wait_stream(cur)
+                with torch.cuda.stream(self.s_drain), _lib.using_ctx(self.c_solo):
+                    self.s_drain.wait_event(done)
+                    for t in (f_all, imgs, s_label, q_label, W0):
+                        t.record_stream(self.s_drain)
+                    W = inner_adapt(f_all[:shot], s_label, W0, eng.lr, eng.iters)
+                    looped = torch.cuda.Event()
+                    looped.record(self.s_drain)
+                with torch.cuda.stream(self.s_adapt), _lib.using_ctx(self.c_adapt):
+                    self.s_adapt.wait_event(looped)
+                    for t in (f_all, q_label, W):
+                        t.record_stream(self.s_adapt)
+                    W2, pred_q, pred_q0, iut, ce, iut0 = tail_and_metrics(eng.transformer, W.view(1, 2, -1),
+                                                                          f_all[shot:], q_label)
+                    done_all = torch.cuda.Event()
+                    done_all.record(self.s_adapt)
+                return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, done=done_all)
+        if c_ad is self.c_solo and self.s_drain is not None:
+            self.s_adapt.wait_stream(self.s_drain)     # c_solo's workspaces: one stream at a time
         with torch.cuda.stream(self.s_adapt), _lib.using_ctx(c_ad):
             self.s_adapt.wait_event(done)
             for t in (f_all, imgs, s_label, q_label, W0):
@@ -366,6 +409,8 @@ class EpisodePipeline:
             if self.c_solo is None:
                 self.c_solo = _lib.new_ctx()
             c_ad = self.c_solo
+        if c_ad is self.c_solo and self.s_drain is not None:
+            self.s_adapt.wait_stream(self.s_drain)     # c_solo's workspaces: one stream at a time
         with torch.cuda.stream(self.s_adapt), _lib.using_ctx(c_ad):
             self.s_adapt.wait_event(done)
             for t in (f_all, imgs, s_label, q_label, W0):
@@ -415,13 +460,15 @@ class EpisodePipeline:
         cur = torch.cuda.current_stream()
         for s in self.s_ext:
             cur.wait_stream(s)
+        if self.s_drain is not None:
+            cur.wait_stream(self.s_drain)
         cur.wait_stream(self.s_adapt)
 
     def close(self):
         """Synchronise the pipeline's streams and destroy its libcwt contexts."""
         if self.closed:
             return
-        for s in self.s_ext + [self.s_adapt]:
+        for s in self.s_ext + [self.s_adapt] + ([self.s_drain] if self.s_drain is not None else []):
             s.synchronize()
         for c in [c for c in self.c_ext if c is not None] + [self.c_adapt] + ([self.c_solo] if self.c_solo else []):
             _lib.destroy_ctx(c, self.device)

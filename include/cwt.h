@@ -429,6 +429,13 @@ int cwt_mmn_blend(cwt_ctx* ctx, const float* f_q, const float* att_fq, int B, in
  * cross attention by src/train_trans.py:100).  Every gradient is exact fp32 with fixed-order
  * reductions (deterministic); outputs are overwritten unless an accumulate flag says otherwise. */
 
+/* Scheduling query of the episode pipeline (no reference counterpart; test.py:164-187 is the loop
+ * it sizes): the number of workgroups -- each holding one whole CU for the whole loop -- of the
+ * persistent inner loop cwt_inner_adapt_batch would launch on this context for E episodes of n
+ * shots with h x w features (0: it would use the per-step launches).  EpisodePipeline runs a
+ * burst's last two loops side by side only when the two grids fit on the chip together. */
+int cwt_adapt_workgroups(cwt_ctx* ctx, int E, int n, int h, int w, int iters, int* G);
+
 /* Floats of the activations cwt_match_corr_forward_train keeps for the backward (CenterPivotConv4d
  * layers): the MutualMatching output, each branch's three ReLU outputs, their sum and, with
  * readout != 0, the attention [B][h*w][ld] (ld = h*w rounded up to 32). */

@@ -70,10 +70,12 @@ def test_run_batch_equals_run(dev, E):
         assert float((rb["iut"][e] - r["iut"][0]).abs().max()) <= 2
 
 
-@pytest.mark.parametrize("streams", [1, 2])
-def test_pipeline_equals_run(dev, streams):
+@pytest.mark.parametrize("streams,overlap", [(1, True), (2, True), (2, False)])
+def test_pipeline_equals_run(dev, streams, overlap):
     """EpisodePipeline (extractor of episode i+1 on one stream beside episode i's inner loop and
-    CWT on another) gives every episode what EpisodeEngine.run gives it alone."""
+    CWT on another) gives every episode what EpisodeEngine.run gives it alone -- the burst's last
+    episode through the drain (its loop on the whole-chip context; overlap: on a stream of its own
+    beside the previous episode's loop and tail)."""
     from few_shot_seg_cwt_amd import MultiHeadAttentionOne, get_model
     from few_shot_seg_cwt_amd.episode import EpisodeEngine, EpisodePipeline
     S, shot, n = 129, 1, 4
@@ -83,15 +85,18 @@ def test_pipeline_equals_run(dev, streams):
     t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
     eng = EpisodeEngine(m, t, cfg)
     pipe = EpisodePipeline(eng, extract_streams=streams)
+    pipe.drain_overlap = overlap
     eps = [syn.make_episode(SEED, 80 + e, S, shot) for e in range(n)]
     W0 = torch.from_numpy(syn.normal(8, "wpl", (n, 2, 512), 0.04)).to(dev)
     ins = []
     for ep in eps:
         imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
         ins.append((imgs, torch.from_numpy(ep["s_label"][0]).to(dev), torch.from_numpy(ep["q_label"]).to(dev)))
-    outs = [pipe.submit(i, s, q, W0[e].clone()) for e, (i, s, q) in enumerate(ins)]
+    outs = [pipe.submit(i, s, q, W0[e].clone(), last=e == n - 1) for e, (i, s, q) in enumerate(ins)]
     pipe.wait()
     torch.cuda.synchronize()
+    if overlap:
+        assert pipe.s_drain is not None   # the 17x17 grids fit beside each other
     for e, (i, s, q) in enumerate(ins):
         r = eng.run(i, s, q, W0[e].clone())
         torch.cuda.synchronize()
