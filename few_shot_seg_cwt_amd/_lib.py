@@ -109,6 +109,7 @@ SIGNATURES = {
                               _P, _I, _I, _I, _P]),
     "cwt_debug_conv_b16": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I, _I,
                                 _P, _I, _I, _I, _P]),
+    "cwt_debug_cp4d_layer": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P]),
     "cwt_debug_conv_f32d": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _I,
                                  _I, _I, _P]),
     "cwt_debug_census": (_I, [_P, _I, _P, _P]),

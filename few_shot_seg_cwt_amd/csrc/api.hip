@@ -77,6 +77,9 @@ int launch_mutual_matching(const float* x, int B, int NA, int NB, int C, float* 
                            float* colmax, hipStream_t st);
 int launch_cp4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* Wa,
                       const float* ba, const float* Wb, const float* bb, float* y, hipStream_t st);
+int launch_cp4d_layer_variant(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout,
+                              const float* Wa, const float* ba, const float* Wb, const float* bb, float* y, int variant,
+                              hipStream_t st);
 int launch_to_channels_last(const float* x, int B, int C, long P, float* y, hipStream_t st);
 int launch_add_inplace(float* y, const float* x, long n, hipStream_t st);
 int launch_match_softmax(const float* corr, int B, int NA, int NB, float temp, int ldp, float* P, hipStream_t st);
@@ -2378,6 +2381,16 @@ int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int 
                        int nsplit, void* stream) {
   return debug_conv_s(ctx, 1, xs, N, Hi, Wi, Ci, ws, scale, shift, Co, k, stride, pad, dil, res, res_ld, res_s, relu, y,
                       y_ld, y_off, ys, bm, bn, nsplit, stream);
+}
+
+// one CenterPivotConv4d layer (+ ReLU) on [B][NA][NB][cin] -> [B][NA][NB][cout] (launch_cp4d_layer);
+// variant 0 the automatic kernel choice, 1 never the rolling-window form, 2 only it
+int cwt_debug_cp4d_layer(cwt_ctx* ctx, const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout,
+                         const float* Wa, const float* ba, const float* Wb, const float* bb, float* y, int variant,
+                         void* stream) {
+  if (!ctx || !x || !Wa || !ba || !Wb || !bb || !y) return fail(CWT_EARG, "null argument");
+  if (B < 1 || hA < 1 || wA < 1 || hB < 1 || wB < 1) return fail(CWT_EARG, "bad shape");
+  return launch_cp4d_layer_variant(x, B, hA, wA, hB, wB, cin, cout, Wa, ba, Wb, bb, y, variant, (hipStream_t)stream);
 }
 
 int cwt_debug_tail_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t max_count, int64_t* count) {

@@ -835,6 +835,385 @@ __global__ __launch_bounds__(256) void cp4d_c1_persist_kernel(const float* __res
   }
 }
 
+// ---- rolling-window form (round 4, third pass): the tile kernels above stage a cross-shaped
+// box per 4x4-by-4x4 tile and so read every input 4.5 times (2.33 GB per 10 -> 10 layer at 60^2,
+// 2.0 GB of it past the L2s: staging-bound).  Here a workgroup owns a 4 x 12 tile of
+// b positions and a strip of 4 a rows, and walks the strip's a columns left to right: the window
+// holds the 6 a rows (strip + halo) x 3 a columns of the b box (the tile + its 1-position ring,
+// 6 x 14), so each step loads ONE new a column -- the a-plane convolution reads an input
+// (4 + 2) / 4 times, the b-plane convolution only the ring around the tile (the tile itself is
+// already in the window): ~2.2 reads per input.  The new column's loads are issued into
+// registers before the current column's MFMAs and stored after them.  MFMA layout and K order
+// as cp4d_mfma_persist_kernel (rows: 16 b positions of one a position; columns: the 10 outputs;
+// CmK's K order); wave w takes a row w of the strip, its three groups the tile's 48 b positions.
+// MODE 1: the input gradient (launch_cp4d_dgrad), as cp4d_mfma_kernel's MODE 1.
+constexpr int RL_BH = 4, RL_BW = 12, RL_XH = RL_BH + 2, RL_XW = RL_BW + 2;
+constexpr int RL_NT = RL_BH * RL_BW, RL_NX = RL_XH * RL_XW, RL_RA = 4, RL_ROWS = RL_RA + 2;
+static_assert(RL_NT == 48, "three 16-row MFMA groups per a position");
+
+// NS column slots per a row: 3 (two barriers per step: after the new column's store, and
+// before the next store overwrites the slot just read) or 4 (one barrier per step: the column
+// stored in step wa is read from step wa + 1 on, into the slot last read in step wa - 1)
+template <int CIN, int NS>
+struct RlWin {
+  static constexpr int V = (CIN % 2 == 0) ? 2 : 1, VP = CIN / V;
+  static constexpr int SLOT = RL_NX * CIN;        // floats of one (a row, column slot): the b box
+  static constexpr int ROW = NS * SLOT;           // NS column slots per a row
+  static constexpr int FLOATS = RL_ROWS * ROW;
+  static constexpr int L = RL_ROWS * RL_NX * VP;  // loads per window column
+  static constexpr int IL = (L + 255) / 256;
+  static constexpr int LDS = FLOATS + (IL * 256 - L) * V + 4;  // + a dummy tail for the spare lanes
+  typedef float vec_t __attribute__((ext_vector_type(V)));
+};
+constexpr int RL_OOR = 0x40000000;  // a buffer offset past every num_records: loads read 0, stores drop
+
+// The window column's loads, branch-free: a buffer resource based at the column (num_records 0
+// off the map), per-lane byte offsets out of range where the position is off the map or unused.
+template <int CIN, int V, int IL, typename vec_t>
+__device__ __forceinline__ void rl_load(vec_t (&rg)[IL], const int (&goff)[IL], const float* xz, int col, int wA,
+                                        int NA, int NB) {
+  const bool colin = (unsigned)col < (unsigned)wA;
+  const float* base = xz + (colin ? (long)col * NB * CIN : 0L);
+  const int nrec = colin ? (int)((long)(NA - col) * NB * CIN * 4) : 0;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000);
+#pragma unroll
+  for (int k = 0; k < IL; ++k) {
+    if constexpr (V == 2) {
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, goff[k], 0, 0);
+      rg[k] = __builtin_bit_cast(vec_t, v);
+    } else {
+      rg[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, goff[k], 0, 0));
+    }
+  }
+}
+
+template <int CIN, int MODE, int NS>
+__global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict__ x, int hA, int wA, int hB, int wB,
+                                                        int nsa, int wc, const float* __restrict__ Wa,
+                                                        const float* __restrict__ ba, const float* __restrict__ Wb,
+                                                        const float* __restrict__ bb, float* __restrict__ y,
+                                                        int accum) {
+  constexpr int COUT = 10;
+  using K = CmK<CIN>;
+  using Wn = RlWin<CIN, NS>;
+  typedef typename Wn::vec_t vec_t;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  constexpr int NM = K::NM, NMIX = K::NMIX, V = Wn::V, VP = Wn::VP;
+  __shared__ __attribute__((aligned(16))) float win[Wn::LDS];
+  const int NA = hA * wA, NB = hB * wB;
+  const int ntbw = (wB + RL_BW - 1) / RL_BW;
+  const int hb0 = ((int)blockIdx.x / ntbw) * RL_BH, wb0 = ((int)blockIdx.x % ntbw) * RL_BW;
+  const int c0 = blockIdx.y * wc, c1 = min(wA, c0 + wc);
+  const int z = blockIdx.z / nsa, ha0 = (blockIdx.z % nsa) * RL_RA;
+  const float* xz = x + (long)z * NA * NB * CIN;
+  float* yz = y + (long)z * NA * NB * COUT;
+  const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int r = lane & 15, g4 = lane >> 4;
+  // this thread's share of a window column: global offset at a column 0 (+ col NB CIN), -1 when
+  // off the map or not needed (the ring of the two halo rows), and its LDS offset in a slot
+  int goff[Wn::IL], loff[Wn::IL];
+#pragma unroll
+  for (int k = 0; k < Wn::IL; ++k) {
+    const int i = t + 256 * k;
+    const int q = i % VP, p = i / VP;
+    const int pos = p % RL_NX, row = p / RL_NX;
+    const int py = pos / RL_XW, px = pos % RL_XW;
+    const int ha = ha0 - 1 + row, hb = hb0 - 1 + py, wb = wb0 - 1 + px;
+    const bool ring = py == 0 || py == RL_XH - 1 || px == 0 || px == RL_XW - 1;
+    const bool in = i < Wn::L && (!ring || (row >= 1 && row <= RL_RA)) && (unsigned)ha < (unsigned)hA &&
+                    (unsigned)hb < (unsigned)hB && (unsigned)wb < (unsigned)wB;
+    goff[k] = in ? (((ha * wA) * NB + hb * wB + wb) * CIN + q * V) * 4 : RL_OOR;
+    loff[k] = i < Wn::L ? row * Wn::ROW + pos * CIN + q * V : Wn::FLOATS + (i - Wn::L) * V;
+  }
+  vec_t rg[Wn::IL];
+  auto load = [&](int col) { rl_load<CIN, Wn::V, Wn::IL>(rg, goff, xz, col, wA, NA, NB); };
+  auto store = [&](int slot) {
+#pragma unroll
+    for (int k = 0; k < Wn::IL; ++k) *(vec_t*)(win + (k < Wn::IL - 1 || loff[k] < Wn::FLOATS ? slot * Wn::SLOT : 0) + loff[k]) = rg[k];
+  };
+  load(c0 - 1);
+  // weights (B operand: column r = output channel) in CmK's K order; the mixed MFMAs' offsets:
+  // a plane (ky ROW + c) * 4 + kx (the column slot picked per step), b plane the box offset
+  float wra[NM], wrb[NM];
+  int mixa[NMIX > 0 ? NMIX : 1], mixb[NMIX > 0 ? NMIX : 1];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    int tap, c;
+    bool kin;
+    if (m < K::NFULL && K::PAIR) {
+      const int pp = m / 2, h = m % 2;
+      tap = pp / (K::F / 2);
+      c = 8 * (pp % (K::F / 2)) + 2 * g4 + h;
+      kin = true;
+    } else if (m < K::NFULL) {
+      tap = m / K::F;
+      c = 4 * (m % K::F) + g4;
+      kin = true;
+    } else {
+      const int i = m - K::NFULL;
+      tap = i * K::PER + g4 / (K::R ? K::R : 1);
+      c = 4 * K::F + g4 % (K::R ? K::R : 1);
+      kin = g4 / (K::R ? K::R : 1) < K::PER && tap < 9;
+      if (!kin) tap = c = 0;
+      mixa[i] = ((tap / 3) * Wn::ROW + c) * 4 + tap % 3;
+      mixb[i] = ((tap / 3 - 1) * RL_XW + tap % 3 - 1) * CIN + c;
+    }
+    const bool live = kin && r < COUT;
+    const int wi = MODE == 0 ? (r * CIN + c) * 9 + tap : (c * COUT + r) * 9 + 8 - tap;
+    wra[m] = live ? Wa[wi] : 0.f;
+    wrb[m] = live ? Wb[wi] : 0.f;
+  }
+  const float bias = (MODE == 0 && r < COUT) ? ba[r] + bb[r] : 0.f;
+  // group j's row r: tile b position 16 j + r -> its box position (times CIN)
+  int pbj[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int tp = 16 * j + r;
+    pbj[j] = ((tp / RL_BW + 1) * RL_XW + tp % RL_BW + 1) * CIN;
+  }
+  const float* wwin = win + wv * Wn::ROW;  // a row wv of the strip: window rows wv .. wv + 2
+  const int ha = ha0 + wv;
+  int yoff[3][4];  // byte offsets of this lane's outputs from column wa's base
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int tp = 16 * j + 4 * g4 + i;
+      const int hb = hb0 + tp / RL_BW, wb = wb0 + tp % RL_BW;
+      yoff[j][i] = (r < COUT && ha < hA && hb < hB && wb < wB) ? ((ha * wA * NB + hb * wB + wb) * COUT + r) * 4 : RL_OOR;
+    }
+  store(0);
+  load(c0);
+  store(1);
+  load(c0 + 1);
+  if (NS == 4) {
+    store(2);
+    if (c0 + 2 <= c1) load(c0 + 2);
+  }
+  for (int wa = c0; wa < c1; ++wa) {
+    const int s = (wa - c0) % NS;  // slot of column wa - 1
+    if (NS == 3) {
+      store((s + 2) % 3);  // column wa + 1
+      __syncthreads();
+      if (wa + 1 < c1) load(wa + 2);  // in flight under this column's MFMAs
+    } else {
+      __syncthreads();  // column wa + 1 stored; every read of column wa - 2 done
+      if (wa + 2 <= c1) store((s + 3) & 3);  // column wa + 2
+      if (wa + 3 <= c1) load(wa + 3);
+    }
+    const int cb0 = s * Wn::SLOT, cb1 = ((s + 1) % NS) * Wn::SLOT, cb2 = ((s + 2) % NS) * Wn::SLOT;
+    f32x4 acc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < (K::PAIR ? K::NFULL : 0); m += 2) {
+      const int pp = m / 2, tap = pp / (K::F / 2), q8 = 8 * (pp % (K::F / 2)) + 2 * g4;
+      const int ky = tap / 3, kx = tap % 3;
+      const int oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + q8;
+      const int ob = Wn::ROW + cb1 + ((ky - 1) * RL_XW + kx - 1) * CIN + q8;
+      f32x2 va[3], vb[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        va[j] = *(const f32x2*)(wwin + oa + pbj[j]);
+        vb[j] = *(const f32x2*)(wwin + ob + pbj[j]);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[j][h], wra[m + h], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[j][h], wrb[m + h], acc[j], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int m = K::PAIR ? K::NFULL : 0; m < NM; ++m) {
+      int oa, ob;
+      if (m < K::NFULL) {
+        const int tap = m / K::F, ky = tap / 3, kx = tap % 3, c = 4 * (m % K::F) + g4;
+        oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + c;
+        ob = Wn::ROW + cb1 + ((ky - 1) * RL_XW + kx - 1) * CIN + c;
+      } else {
+        const int ma = mixa[m - K::NFULL], kx = ma & 3;
+        oa = (ma >> 2) + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2);
+        ob = Wn::ROW + cb1 + mixb[m - K::NFULL];
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wwin[oa + pbj[j]], wra[m], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wwin[ob + pbj[j]], wrb[m], acc[j], 0, 0, 0);
+    }
+    // D: lane (col o = r, rows 4 g4 + i) -> pair (a = (ha, wa), b = tile position 16 j + 4 g4 + i),
+    // stored through a resource based at column wa (off-map pairs and dead columns: offset RL_OOR)
+    {
+      const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(yz + (long)wa * NB * COUT), (short)0, (int)((long)(NA - wa) * NB * COUT * 4), 0x00020000);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = MODE == 0 ? fmaxf(acc[j][i] + bias, 0.f) : acc[j][i];
+          if (MODE == 1 && accum)
+            v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff[j][i], 0, 0));
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, yoff[j][i], 0, 0);
+        }
+      }
+    }
+    if (NS == 3) __syncthreads();  // this column's reads of slot s are done before the next store
+  }
+}
+
+// COUT = 1 on the same rolling window (VALU: cp4d_c1_kernel's per-pair fmaf chains, the two
+// branches' even / odd channels in two partial sums); thread t < 192 takes strip row t / 48 and
+// tile b position t % 48, the filters are broadcast from LDS.
+template <int CIN, int NS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void cp4d_c1_roll_kernel(const float* __restrict__ x, int hA, int wA, int hB, int wB,
+                                                           int nsa, int wc, const float* __restrict__ Wa,
+                                                           const float* __restrict__ ba,
+                                                           const float* __restrict__ Wb,
+                                                           const float* __restrict__ bb, float* __restrict__ y) {
+  static_assert(CIN % 2 == 0, "pairs of channels");
+  using Wn = RlWin<CIN, NS>;
+  typedef typename Wn::vec_t vec_t;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  constexpr int V = Wn::V, VP = Wn::VP;
+  __shared__ __attribute__((aligned(16))) float win[Wn::LDS];
+  __shared__ __attribute__((aligned(16))) float wl[2][9][CIN];
+  const int NA = hA * wA, NB = hB * wB;
+  const int ntbw = (wB + RL_BW - 1) / RL_BW;
+  const int hb0 = ((int)blockIdx.x / ntbw) * RL_BH, wb0 = ((int)blockIdx.x % ntbw) * RL_BW;
+  const int c0 = blockIdx.y * wc, c1 = min(wA, c0 + wc);
+  const int z = blockIdx.z / nsa, ha0 = (blockIdx.z % nsa) * RL_RA;
+  const float* xz = x + (long)z * NA * NB * CIN;
+  float* yz = y + (long)z * NA * NB;
+  const int t = threadIdx.x;
+  int goff[Wn::IL], loff[Wn::IL];
+#pragma unroll
+  for (int k = 0; k < Wn::IL; ++k) {
+    const int i = t + 256 * k;
+    const int q = i % VP, p = i / VP;
+    const int pos = p % RL_NX, row = p / RL_NX;
+    const int py = pos / RL_XW, px = pos % RL_XW;
+    const int ha = ha0 - 1 + row, hb = hb0 - 1 + py, wb = wb0 - 1 + px;
+    const bool ring = py == 0 || py == RL_XH - 1 || px == 0 || px == RL_XW - 1;
+    const bool in = i < Wn::L && (!ring || (row >= 1 && row <= RL_RA)) && (unsigned)ha < (unsigned)hA &&
+                    (unsigned)hb < (unsigned)hB && (unsigned)wb < (unsigned)wB;
+    goff[k] = in ? (((ha * wA) * NB + hb * wB + wb) * CIN + q * V) * 4 : RL_OOR;
+    loff[k] = i < Wn::L ? row * Wn::ROW + pos * CIN + q * V : Wn::FLOATS + (i - Wn::L) * V;
+  }
+  vec_t rg[Wn::IL];
+  auto load = [&](int col) { rl_load<CIN, Wn::V, Wn::IL>(rg, goff, xz, col, wA, NA, NB); };
+  auto store = [&](int slot) {
+#pragma unroll
+    for (int k = 0; k < Wn::IL; ++k) *(vec_t*)(win + (k < Wn::IL - 1 || loff[k] < Wn::FLOATS ? slot * Wn::SLOT : 0) + loff[k]) = rg[k];
+  };
+  load(c0 - 1);
+  if (t < 2 * 9 * CIN) {
+    const int c = t % CIN, tap = (t / CIN) % 9, side = t / (9 * CIN);
+    (&wl[0][0][0])[t] = (side ? Wb : Wa)[c * 9 + tap];
+  }
+  const float bias = ba[0] + bb[0];
+  const bool act = t < RL_RA * RL_NT;
+  const int ai = act ? t / RL_NT : 0, tp = act ? t % RL_NT : 0;
+  const int pb = ((tp / RL_BW + 1) * RL_XW + tp % RL_BW + 1) * CIN;
+  const int ha = ha0 + ai, hb = hb0 + tp / RL_BW, wb = wb0 + tp % RL_BW;
+  const bool outp = act && ha < hA && hb < hB && wb < wB;
+  const int yoff = outp ? (ha * wA * NB + hb * wB + wb) * 4 : RL_OOR;  // from column wa's base
+  const float* wwin = win + ai * Wn::ROW + pb;
+  store(0);
+  load(c0);
+  store(1);
+  load(c0 + 1);
+  if (NS == 4) {
+    store(2);
+    if (c0 + 2 <= c1) load(c0 + 2);
+  }
+#pragma unroll 1
+  for (int wa = c0; wa < c1; ++wa) {
+    const int s = (wa - c0) % NS;
+    if (NS == 3) {
+      store((s + 2) % 3);
+      __syncthreads();
+      if (wa + 1 < c1) load(wa + 2);
+    } else {
+      __syncthreads();
+      if (wa + 2 <= c1) store((s + 3) & 3);
+      if (wa + 3 <= c1) load(wa + 3);
+    }
+    const int cb[3] = {s * Wn::SLOT, ((s + 1) % NS) * Wn::SLOT, ((s + 2) % NS) * Wn::SLOT};
+    int wz = 0;
+    asm volatile("" : "+v"(wz));  // the filters re-read from LDS per step (hoisted: 180 VGPRs)
+    const float* wlp = &wl[0][0][0] + wz;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll 3
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap % 3;
+      const float* pa = wwin + ky * Wn::ROW + (kx == 0 ? cb[0] : kx == 1 ? cb[1] : cb[2]);
+      const float* pbb = wwin + Wn::ROW + cb[1] + ((ky - 1) * RL_XW + kx - 1) * CIN;
+#pragma unroll
+      for (int c2 = 0; c2 < CIN / 2; ++c2) {
+        const f32x2 va = *(const f32x2*)(pa + 2 * c2), vb = *(const f32x2*)(pbb + 2 * c2);
+        const f32x2 w0 = *(const f32x2*)(wlp + tap * CIN + 2 * c2);
+        const f32x2 w1 = *(const f32x2*)(wlp + (9 + tap) * CIN + 2 * c2);
+        s0 = fmaf(w0[0], va[0], s0);
+        s1 = fmaf(w0[1], va[1], s1);
+        s0 = fmaf(w1[0], vb[0], s0);
+        s1 = fmaf(w1[1], vb[1], s1);
+      }
+    }
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(yz + (long)wa * NB), (short)0, (int)((long)(NA - wa) * NB * 4), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, fmaxf((s0 + s1) + bias, 0.f)), ry, yoff, 0, 0);
+    if (NS == 3) __syncthreads();
+  }
+}
+
+// the rolling-window launch (cp4d_roll_kernel); returns 1 when the shape is not taken (index range)
+// mode 0: COUT = 10 forward, 1: COUT = 10 input gradient, 2: COUT = 1 forward
+static int launch_cp4d_roll(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int mode, const float* Wa,
+                            const float* ba, const float* Wb, const float* bb, float* y, int accum, hipStream_t st) {
+  if ((long)hA * wA * hB * wB * 10 * 4 > RL_OOR) return 1;  // byte offsets within one batch entry below RL_OOR
+  static const int wc_env = getenv("CWT_CP4D_WC") ? atoi(getenv("CWT_CP4D_WC")) : 30;
+  const int wc = std::max(1, std::min(wA, wc_env));
+  static const int ns = getenv("CWT_CP4D_NS") && atoi(getenv("CWT_CP4D_NS")) == 3 ? 3 : 4;
+  const int nsa = cdiv(hA, RL_RA);
+  const dim3 grid(cdiv(hB, RL_BH) * cdiv(wB, RL_BW), cdiv(wA, wc), B * nsa);
+#define CWT_RL(CI, MD)                                                                                       \
+  if (cin == CI && mode == MD) {                                                                             \
+    if (ns == 3)                                                                                             \
+      hipLaunchKernelGGL((cp4d_roll_kernel<CI, MD, 3>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, \
+                         Wb, bb, y, accum);                                                                  \
+    else                                                                                                     \
+      hipLaunchKernelGGL((cp4d_roll_kernel<CI, MD, 4>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, \
+                         Wb, bb, y, accum);                                                                  \
+    CWT_LAUNCH_CHECK();                                                                                      \
+    return 0;                                                                                                \
+  }
+  CWT_RL(1, 0)
+  CWT_RL(2, 0)
+  CWT_RL(10, 0)
+  CWT_RL(1, 1)
+  CWT_RL(10, 1)
+#undef CWT_RL
+  if (cin == 10 && mode == 2) {  // COUT = 1
+    if (ns == 3)
+      hipLaunchKernelGGL((cp4d_c1_roll_kernel<10, 3>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, Wb,
+                         bb, y);
+    else
+      hipLaunchKernelGGL((cp4d_c1_roll_kernel<10, 4>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, Wb,
+                         bb, y);
+    CWT_LAUNCH_CHECK();
+    return 0;
+  }
+  return 1;
+}
+// CWT_CP4D_ROLL: 0 never, 1 (default) the COUT = 10 layers, 2 also COUT = 1 (A/B: the VALU
+// COUT = 1 form measured slower than the tile kernel, 552 against 480 us at 60^2)
+static int cp4d_roll_mode() {
+  static const int m = getenv("CWT_CP4D_ROLL") ? atoi(getenv("CWT_CP4D_ROLL")) : 1;
+  return m;
+}
+
 // x [B][C][P] (channel planes) -> y [B][P][C] (channels last)
 __global__ void to_channels_last_kernel(const float* __restrict__ x, int B, int C, long P, float* __restrict__ y) {
   const long total = (long)B * C * P;
@@ -1253,14 +1632,28 @@ int launch_mutual_matching(const float* x, int B, int NA, int NB, int C, float* 
   return 0;
 }
 
+// variant (cwt_debug_cp4d_layer): 0 the automatic choice, 1 never the rolling-window form, 2 only it
+int launch_cp4d_layer_variant(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout,
+                              const float* Wa, const float* ba, const float* Wb, const float* bb, float* y, int variant,
+                              hipStream_t st);
 int launch_cp4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* Wa,
                       const float* ba, const float* Wb, const float* bb, float* y, hipStream_t st) {
+  return launch_cp4d_layer_variant(x, B, hA, wA, hB, wB, cin, cout, Wa, ba, Wb, bb, y, 0, st);
+}
+int launch_cp4d_layer_variant(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout,
+                              const float* Wa, const float* ba, const float* Wb, const float* bb, float* y, int variant,
+                              hipStream_t st) {
   // the matrix-core / register-blocked forms (round 4): for 10 -> 10 persistent workgroups with
   // the next tile's loads in flight (1,169 against 1,207 us at 60^2; the 2 -> 10 and 10 -> 1
   // layers measured slower that way: 331 / 605 against 297 / 471 us, profiles/r4/run_i), the
   // rest one tile per workgroup; CWT_CP4D_PERSIST=0 / 2: none / all persistent (A/B);
   // CWT_CP4D_MFMA=0 selects the scalar kernel
   static const bool mfma = !(getenv("CWT_CP4D_MFMA") && getenv("CWT_CP4D_MFMA")[0] == '0');
+  if (((mfma && variant == 0 && (cp4d_roll_mode() == 2 || (cp4d_roll_mode() == 1 && cout == 10))) || variant == 2) &&
+      (cout == 10 || cout == 1) &&
+      launch_cp4d_roll(x, B, hA, wA, hB, wB, cin, cout == 10 ? 0 : 2, Wa, ba, Wb, bb, y, 0, st) == 0)
+    return 0;
+  if (variant == 2) return fail(CWT_EARG, "cp4d layer: no rolling-window form for this shape");
   static const int persist_mode = getenv("CWT_CP4D_PERSIST") ? atoi(getenv("CWT_CP4D_PERSIST")) : 1;
   const bool persist = persist_mode == 2 || (persist_mode == 1 && cin == 10 && cout == 10);
   if (mfma && persist) {
@@ -1328,6 +1721,9 @@ int launch_cp4d_dgrad(const float* g, int B, int hA, int wA, int hB, int wB, int
                       const float* Wb, float* dx, int accum, hipStream_t st) {
   static const bool scalar = getenv("CWT_DGRAD_SCALAR") && getenv("CWT_DGRAD_SCALAR")[0] == '1';  // A/B only
   if (gout == 10 && (gin == 1 || gin == 10) && !scalar) {  // 10 output channels: the matrix-core form
+    if (cp4d_roll_mode() != 0 &&
+        launch_cp4d_roll(g, B, hA, wA, hB, wB, gin, 1, Wa, nullptr, Wb, nullptr, dx, accum, st) == 0)
+      return 0;
     const dim3 g4(cdiv(hB, CM_T) * cdiv(wB, CM_T), cdiv(hA, CM_T) * cdiv(wA, CM_T), B);
     if (gin == 1)
       hipLaunchKernelGGL((cp4d_mfma_kernel<1, 1>), g4, dim3(256), 0, st, g, hA, wA, hB, wB, Wa, (const float*)nullptr,

@@ -63,6 +63,14 @@ int cwt_debug_conv_f32d(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int
                         const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
                         int nsplit, void* stream);
 
+/* One CenterPivotConv4d layer + ReLU (src/model/conv4d.py:40-62) on the channels-last 4-D
+ * tensor x [B][hA*wA][hB*wB][cin] -> y [B][hA*wA][hB*wB][cout]: Wa / Wb [cout][cin][3][3] the
+ * a-plane / b-plane filters, ba / bb their biases.  variant 0: the library's kernel choice, 1:
+ * never the rolling-window kernel (cp4d_roll_kernel), 2: only it (CWT_EARG where it has no form). */
+int cwt_debug_cp4d_layer(cwt_ctx* ctx, const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout,
+                         const float* Wa, const float* ba, const float* Wb, const float* bb, float* y, int variant,
+                         void* stream);
+
 /* Timing-study hook of cwt_episode_tail: with CWT_TAIL_STAMPS=1 in the environment the tail runs a
  * separately compiled instantiation whose workgroups record s_memtime at each phase edge
  * ([G][16]: 0 entry, 2k-1 / 2k before / after grid barrier k, 11 the partials written, 14 / 15
