@@ -851,11 +851,12 @@ constexpr int RL_BH = 4, RL_BW = 12, RL_XH = RL_BH + 2, RL_XW = RL_BW + 2;
 constexpr int RL_NT = RL_BH * RL_BW, RL_NX = RL_XH * RL_XW, RL_RA = 4, RL_ROWS = RL_RA + 2;
 static_assert(RL_NT == 48, "three 16-row MFMA groups per a position");
 
-// NS column slots per a row: 3 (two barriers per step: after the new column's store, and
-// before the next store overwrites the slot just read) or 4 (one barrier per step: the column
-// stored in step wa is read from step wa + 1 on, into the slot last read in step wa - 1)
-template <int CIN, int NS>
+// four column slots per a row (one barrier per step: the column stored in step wa is read from
+// step wa + 1 on, into the slot last read in step wa - 1; three slots need a second barrier and
+// measured 3 % slower)
+template <int CIN>
 struct RlWin {
+  static constexpr int NS = 4;
   static constexpr int V = (CIN % 2 == 0) ? 2 : 1, VP = CIN / V;
   static constexpr int SLOT = RL_NX * CIN;        // floats of one (a row, column slot): the b box
   static constexpr int ROW = NS * SLOT;           // NS column slots per a row
@@ -888,7 +889,7 @@ __device__ __forceinline__ void rl_load(vec_t (&rg)[IL], const int (&goff)[IL], 
   }
 }
 
-template <int CIN, int MODE, int NS>
+template <int CIN, int MODE, int PF>
 __global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict__ x, int hA, int wA, int hB, int wB,
                                                         int nsa, int wc, const float* __restrict__ Wa,
                                                         const float* __restrict__ ba, const float* __restrict__ Wb,
@@ -896,7 +897,7 @@ __global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict_
                                                         int accum) {
   constexpr int COUT = 10;
   using K = CmK<CIN>;
-  using Wn = RlWin<CIN, NS>;
+  using Wn = RlWin<CIN>;
   typedef typename Wn::vec_t vec_t;
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   constexpr int NM = K::NM, NMIX = K::NMIX, V = Wn::V, VP = Wn::VP;
@@ -983,97 +984,102 @@ __global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict_
       const int hb = hb0 + tp / RL_BW, wb = wb0 + tp % RL_BW;
       yoff[j][i] = (r < COUT && ha < hA && hb < hB && wb < wB) ? ((ha * wA * NB + hb * wB + wb) * COUT + r) * 4 : RL_OOR;
     }
+  vec_t rg2[Wn::IL];
+  auto load2 = [&](int col) { rl_load<CIN, Wn::V, Wn::IL>(rg2, goff, xz, col, wA, NA, NB); };
+  auto store2 = [&](int slot) {
+#pragma unroll
+    for (int k = 0; k < Wn::IL; ++k) *(vec_t*)(win + (k < Wn::IL - 1 || loff[k] < Wn::FLOATS ? slot * Wn::SLOT : 0) + loff[k]) = rg2[k];
+  };
+  // step wa: publish column wa + 1 (barrier), store column wa + 2 into the slot of column wa - 2,
+  // issue the loads of column wa + 1 + PF (PF = 2: two register sets, even / odd steps), compute
+  // column wa from the slots of columns wa - 1, wa, wa + 1
+  auto step = [&](int wa, auto&& st, auto&& ld) {
+    const int s = (wa - c0) & 3;  // slot of column wa - 1
+    __syncthreads();
+    if (wa + 2 <= c1) st((s + 3) & 3);
+    if (wa + 2 + PF <= c1) ld(wa + 2 + PF);
+      const int cb0 = s * Wn::SLOT, cb1 = ((s + 1) & 3) * Wn::SLOT, cb2 = ((s + 2) & 3) * Wn::SLOT;
+      f32x4 acc[3];
+  #pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+      for (int m = 0; m < (K::PAIR ? K::NFULL : 0); m += 2) {
+        const int pp = m / 2, tap = pp / (K::F / 2), q8 = 8 * (pp % (K::F / 2)) + 2 * g4;
+        const int ky = tap / 3, kx = tap % 3;
+        const int oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + q8;
+        const int ob = Wn::ROW + cb1 + ((ky - 1) * RL_XW + kx - 1) * CIN + q8;
+        f32x2 va[3], vb[3];
+  #pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          va[j] = *(const f32x2*)(wwin + oa + pbj[j]);
+          vb[j] = *(const f32x2*)(wwin + ob + pbj[j]);
+        }
+  #pragma unroll
+        for (int h = 0; h < 2; ++h) {
+  #pragma unroll
+          for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[j][h], wra[m + h], acc[j], 0, 0, 0);
+  #pragma unroll
+          for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[j][h], wrb[m + h], acc[j], 0, 0, 0);
+        }
+      }
+  #pragma unroll
+      for (int m = K::PAIR ? K::NFULL : 0; m < NM; ++m) {
+        int oa, ob;
+        if (m < K::NFULL) {
+          const int tap = m / K::F, ky = tap / 3, kx = tap % 3, c = 4 * (m % K::F) + g4;
+          oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + c;
+          ob = Wn::ROW + cb1 + ((ky - 1) * RL_XW + kx - 1) * CIN + c;
+        } else {
+          const int ma = mixa[m - K::NFULL], kx = ma & 3;
+          oa = (ma >> 2) + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2);
+          ob = Wn::ROW + cb1 + mixb[m - K::NFULL];
+        }
+  #pragma unroll
+        for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wwin[oa + pbj[j]], wra[m], acc[j], 0, 0, 0);
+  #pragma unroll
+        for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wwin[ob + pbj[j]], wrb[m], acc[j], 0, 0, 0);
+      }
+      // D: lane (col o = r, rows 4 g4 + i) -> pair (a = (ha, wa), b = tile position 16 j + 4 g4 + i),
+      // stored through a resource based at column wa (off-map pairs and dead columns: offset RL_OOR)
+      {
+        const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(yz + (long)wa * NB * COUT), (short)0, (int)((long)(NA - wa) * NB * COUT * 4), 0x00020000);
+  #pragma unroll
+        for (int j = 0; j < 3; ++j) {
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float v = MODE == 0 ? fmaxf(acc[j][i] + bias, 0.f) : acc[j][i];
+            if (MODE == 1 && accum)
+              v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff[j][i], 0, 0));
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, yoff[j][i], 0, 0);
+          }
+        }
+      }
+  };
   store(0);
   load(c0);
   store(1);
   load(c0 + 1);
-  if (NS == 4) {
-    store(2);
-    if (c0 + 2 <= c1) load(c0 + 2);
-  }
-  for (int wa = c0; wa < c1; ++wa) {
-    const int s = (wa - c0) % NS;  // slot of column wa - 1
-    if (NS == 3) {
-      store((s + 2) % 3);  // column wa + 1
-      __syncthreads();
-      if (wa + 1 < c1) load(wa + 2);  // in flight under this column's MFMAs
-    } else {
-      __syncthreads();  // column wa + 1 stored; every read of column wa - 2 done
-      if (wa + 2 <= c1) store((s + 3) & 3);  // column wa + 2
-      if (wa + 3 <= c1) load(wa + 3);
-    }
-    const int cb0 = s * Wn::SLOT, cb1 = ((s + 1) % NS) * Wn::SLOT, cb2 = ((s + 2) % NS) * Wn::SLOT;
-    f32x4 acc[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int m = 0; m < (K::PAIR ? K::NFULL : 0); m += 2) {
-      const int pp = m / 2, tap = pp / (K::F / 2), q8 = 8 * (pp % (K::F / 2)) + 2 * g4;
-      const int ky = tap / 3, kx = tap % 3;
-      const int oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + q8;
-      const int ob = Wn::ROW + cb1 + ((ky - 1) * RL_XW + kx - 1) * CIN + q8;
-      f32x2 va[3], vb[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        va[j] = *(const f32x2*)(wwin + oa + pbj[j]);
-        vb[j] = *(const f32x2*)(wwin + ob + pbj[j]);
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[j][h], wra[m + h], acc[j], 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[j][h], wrb[m + h], acc[j], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int m = K::PAIR ? K::NFULL : 0; m < NM; ++m) {
-      int oa, ob;
-      if (m < K::NFULL) {
-        const int tap = m / K::F, ky = tap / 3, kx = tap % 3, c = 4 * (m % K::F) + g4;
-        oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + c;
-        ob = Wn::ROW + cb1 + ((ky - 1) * RL_XW + kx - 1) * CIN + c;
-      } else {
-        const int ma = mixa[m - K::NFULL], kx = ma & 3;
-        oa = (ma >> 2) + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2);
-        ob = Wn::ROW + cb1 + mixb[m - K::NFULL];
-      }
-#pragma unroll
-      for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wwin[oa + pbj[j]], wra[m], acc[j], 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wwin[ob + pbj[j]], wrb[m], acc[j], 0, 0, 0);
-    }
-    // D: lane (col o = r, rows 4 g4 + i) -> pair (a = (ha, wa), b = tile position 16 j + 4 g4 + i),
-    // stored through a resource based at column wa (off-map pairs and dead columns: offset RL_OOR)
-    {
-      const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(yz + (long)wa * NB * COUT), (short)0, (int)((long)(NA - wa) * NB * COUT * 4), 0x00020000);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float v = MODE == 0 ? fmaxf(acc[j][i] + bias, 0.f) : acc[j][i];
-          if (MODE == 1 && accum)
-            v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff[j][i], 0, 0));
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, yoff[j][i], 0, 0);
-        }
-      }
-    }
-    if (NS == 3) __syncthreads();  // this column's reads of slot s are done before the next store
+  store(2);
+  if (c0 + 2 <= c1) load(c0 + 2);
+  if (PF == 2 && c0 + 3 <= c1) load2(c0 + 3);
+  for (int wa = c0; wa < c1; wa += PF) {
+    step(wa, store, load);
+    if (PF == 2 && wa + 1 < c1) step(wa + 1, store2, load2);
   }
 }
 
 // COUT = 1 on the same rolling window (VALU: cp4d_c1_kernel's per-pair fmaf chains, the two
 // branches' even / odd channels in two partial sums); thread t < 192 takes strip row t / 48 and
 // tile b position t % 48, the filters are broadcast from LDS.
-template <int CIN, int NS>
+template <int CIN, int PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void cp4d_c1_roll_kernel(const float* __restrict__ x, int hA, int wA, int hB, int wB,
                                                            int nsa, int wc, const float* __restrict__ Wa,
                                                            const float* __restrict__ ba,
                                                            const float* __restrict__ Wb,
                                                            const float* __restrict__ bb, float* __restrict__ y) {
   static_assert(CIN % 2 == 0, "pairs of channels");
-  using Wn = RlWin<CIN, NS>;
+  using Wn = RlWin<CIN>;
   typedef typename Wn::vec_t vec_t;
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   constexpr int V = Wn::V, VP = Wn::VP;
@@ -1120,51 +1126,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const bool outp = act && ha < hA && hb < hB && wb < wB;
   const int yoff = outp ? (ha * wA * NB + hb * wB + wb) * 4 : RL_OOR;  // from column wa's base
   const float* wwin = win + ai * Wn::ROW + pb;
+  vec_t rg2[Wn::IL];
+  auto load2 = [&](int col) { rl_load<CIN, Wn::V, Wn::IL>(rg2, goff, xz, col, wA, NA, NB); };
+  auto store2 = [&](int slot) {
+#pragma unroll
+    for (int k = 0; k < Wn::IL; ++k) *(vec_t*)(win + (k < Wn::IL - 1 || loff[k] < Wn::FLOATS ? slot * Wn::SLOT : 0) + loff[k]) = rg2[k];
+  };
+  auto step = [&](int wa, auto&& st, auto&& ld) {  // as cp4d_roll_kernel's
+    const int s = (wa - c0) & 3;
+    __syncthreads();
+    if (wa + 2 <= c1) st((s + 3) & 3);
+    if (wa + 2 + PF <= c1) ld(wa + 2 + PF);
+      const int cb[3] = {s * Wn::SLOT, ((s + 1) & 3) * Wn::SLOT, ((s + 2) & 3) * Wn::SLOT};
+      int wz = 0;
+      asm volatile("" : "+v"(wz));  // the filters re-read from LDS per step (hoisted: 180 VGPRs)
+      const float* wlp = &wl[0][0][0] + wz;
+      float s0 = 0.f, s1 = 0.f;
+  #pragma unroll 3
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap % 3;
+        const float* pa = wwin + ky * Wn::ROW + (kx == 0 ? cb[0] : kx == 1 ? cb[1] : cb[2]);
+        const float* pbb = wwin + Wn::ROW + cb[1] + ((ky - 1) * RL_XW + kx - 1) * CIN;
+  #pragma unroll
+        for (int c2 = 0; c2 < CIN / 2; ++c2) {
+          const f32x2 va = *(const f32x2*)(pa + 2 * c2), vb = *(const f32x2*)(pbb + 2 * c2);
+          const f32x2 w0 = *(const f32x2*)(wlp + tap * CIN + 2 * c2);
+          const f32x2 w1 = *(const f32x2*)(wlp + (9 + tap) * CIN + 2 * c2);
+          s0 = fmaf(w0[0], va[0], s0);
+          s1 = fmaf(w0[1], va[1], s1);
+          s0 = fmaf(w1[0], vb[0], s0);
+          s1 = fmaf(w1[1], vb[1], s1);
+        }
+      }
+      const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(yz + (long)wa * NB), (short)0, (int)((long)(NA - wa) * NB * 4), 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, fmaxf((s0 + s1) + bias, 0.f)), ry, yoff, 0, 0);
+  };
   store(0);
   load(c0);
   store(1);
   load(c0 + 1);
-  if (NS == 4) {
-    store(2);
-    if (c0 + 2 <= c1) load(c0 + 2);
-  }
+  store(2);
+  if (c0 + 2 <= c1) load(c0 + 2);
+  if (PF == 2 && c0 + 3 <= c1) load2(c0 + 3);
 #pragma unroll 1
-  for (int wa = c0; wa < c1; ++wa) {
-    const int s = (wa - c0) % NS;
-    if (NS == 3) {
-      store((s + 2) % 3);
-      __syncthreads();
-      if (wa + 1 < c1) load(wa + 2);
-    } else {
-      __syncthreads();
-      if (wa + 2 <= c1) store((s + 3) & 3);
-      if (wa + 3 <= c1) load(wa + 3);
-    }
-    const int cb[3] = {s * Wn::SLOT, ((s + 1) % NS) * Wn::SLOT, ((s + 2) % NS) * Wn::SLOT};
-    int wz = 0;
-    asm volatile("" : "+v"(wz));  // the filters re-read from LDS per step (hoisted: 180 VGPRs)
-    const float* wlp = &wl[0][0][0] + wz;
-    float s0 = 0.f, s1 = 0.f;
-#pragma unroll 3
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap % 3;
-      const float* pa = wwin + ky * Wn::ROW + (kx == 0 ? cb[0] : kx == 1 ? cb[1] : cb[2]);
-      const float* pbb = wwin + Wn::ROW + cb[1] + ((ky - 1) * RL_XW + kx - 1) * CIN;
-#pragma unroll
-      for (int c2 = 0; c2 < CIN / 2; ++c2) {
-        const f32x2 va = *(const f32x2*)(pa + 2 * c2), vb = *(const f32x2*)(pbb + 2 * c2);
-        const f32x2 w0 = *(const f32x2*)(wlp + tap * CIN + 2 * c2);
-        const f32x2 w1 = *(const f32x2*)(wlp + (9 + tap) * CIN + 2 * c2);
-        s0 = fmaf(w0[0], va[0], s0);
-        s1 = fmaf(w0[1], va[1], s1);
-        s0 = fmaf(w1[0], vb[0], s0);
-        s1 = fmaf(w1[1], vb[1], s1);
-      }
-    }
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(yz + (long)wa * NB), (short)0, (int)((long)(NA - wa) * NB * 4), 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, fmaxf((s0 + s1) + bias, 0.f)), ry, yoff, 0, 0);
-    if (NS == 3) __syncthreads();
+  for (int wa = c0; wa < c1; wa += PF) {
+    step(wa, store, load);
+    if (PF == 2 && wa + 1 < c1) step(wa + 1, store2, load2);
   }
 }
 
@@ -1175,16 +1183,16 @@ static int launch_cp4d_roll(const float* x, int B, int hA, int wA, int hB, int w
   if ((long)hA * wA * hB * wB * 10 * 4 > RL_OOR) return 1;  // byte offsets within one batch entry below RL_OOR
   static const int wc_env = getenv("CWT_CP4D_WC") ? atoi(getenv("CWT_CP4D_WC")) : 30;
   const int wc = std::max(1, std::min(wA, wc_env));
-  static const int ns = getenv("CWT_CP4D_NS") && atoi(getenv("CWT_CP4D_NS")) == 3 ? 3 : 4;
+  static const int pf = getenv("CWT_CP4D_PF") && atoi(getenv("CWT_CP4D_PF")) == 1 ? 1 : 2;  // prefetch depth
   const int nsa = cdiv(hA, RL_RA);
   const dim3 grid(cdiv(hB, RL_BH) * cdiv(wB, RL_BW), cdiv(wA, wc), B * nsa);
 #define CWT_RL(CI, MD)                                                                                       \
   if (cin == CI && mode == MD) {                                                                             \
-    if (ns == 3)                                                                                             \
-      hipLaunchKernelGGL((cp4d_roll_kernel<CI, MD, 3>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, \
+    if (pf == 1)                                                                                             \
+      hipLaunchKernelGGL((cp4d_roll_kernel<CI, MD, 1>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, \
                          Wb, bb, y, accum);                                                                  \
     else                                                                                                     \
-      hipLaunchKernelGGL((cp4d_roll_kernel<CI, MD, 4>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, \
+      hipLaunchKernelGGL((cp4d_roll_kernel<CI, MD, 2>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, \
                          Wb, bb, y, accum);                                                                  \
     CWT_LAUNCH_CHECK();                                                                                      \
     return 0;                                                                                                \
@@ -1196,11 +1204,11 @@ static int launch_cp4d_roll(const float* x, int B, int hA, int wA, int hB, int w
   CWT_RL(10, 1)
 #undef CWT_RL
   if (cin == 10 && mode == 2) {  // COUT = 1
-    if (ns == 3)
-      hipLaunchKernelGGL((cp4d_c1_roll_kernel<10, 3>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, Wb,
+    if (pf == 1)
+      hipLaunchKernelGGL((cp4d_c1_roll_kernel<10, 1>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, Wb,
                          bb, y);
     else
-      hipLaunchKernelGGL((cp4d_c1_roll_kernel<10, 4>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, Wb,
+      hipLaunchKernelGGL((cp4d_c1_roll_kernel<10, 2>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, Wb,
                          bb, y);
     CWT_LAUNCH_CHECK();
     return 0;

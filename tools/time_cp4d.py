@@ -14,7 +14,7 @@ from few_shot_seg_cwt_amd import _lib  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 dev = torch.device("cuda", 0)
 h = 60
-out = {"wc": os.environ.get("CWT_CP4D_WC", "20")}
+out = {"wc": os.environ.get("CWT_CP4D_WC", "30")}
 for cin, cout in ((2, 10), (10, 10), (10, 1)):
     x = torch.rand(1, h * h, h * h, cin, device=dev)
     y = torch.empty(1, h * h, h * h, cout, device=dev)
