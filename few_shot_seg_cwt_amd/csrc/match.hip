@@ -894,7 +894,7 @@ __global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict_
                                                         int nsa, int wc, const float* __restrict__ Wa,
                                                         const float* __restrict__ ba, const float* __restrict__ Wb,
                                                         const float* __restrict__ bb, float* __restrict__ y,
-                                                        int accum) {
+                                                        int accum, int dbg) {
   constexpr int COUT = 10;
   using K = CmK<CIN>;
   using Wn = RlWin<CIN>;
@@ -966,11 +966,13 @@ __global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict_
     wrb[m] = live ? Wb[wi] : 0.f;
   }
   const float bias = (MODE == 0 && r < COUT) ? ba[r] + bb[r] : 0.f;
-  // group j's row r: tile b position 16 j + r -> its box position (times CIN)
+  // group j's row r: tile b position 16 j + 4 (r % 4) + r / 4 -> its box position (times CIN); the
+  // D rows 4 g4 + i of a lane are then the positions 16 j + 4 i + g4, so each of its stores covers
+  // 4 consecutive b positions (160 contiguous bytes) instead of 4 positions 4 apart
   int pbj[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const int tp = 16 * j + r;
+    const int tp = 16 * j + 4 * (r & 3) + (r >> 2);  // D row 4 g4 + i <-> tile position 16 j + 4 i + g4
     pbj[j] = ((tp / RL_BW + 1) * RL_XW + tp % RL_BW + 1) * CIN;
   }
   const float* wwin = win + wv * Wn::ROW;  // a row wv of the strip: window rows wv .. wv + 2
@@ -980,7 +982,7 @@ __global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict_
   for (int j = 0; j < 3; ++j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int tp = 16 * j + 4 * g4 + i;
+      const int tp = 16 * j + 4 * i + g4;  // one store instruction: 4 consecutive b positions x 10 outputs
       const int hb = hb0 + tp / RL_BW, wb = wb0 + tp % RL_BW;
       yoff[j][i] = (r < COUT && ha < hA && hb < hB && wb < wB) ? ((ha * wA * NB + hb * wB + wb) * COUT + r) * 4 : RL_OOR;
     }
@@ -997,13 +999,14 @@ __global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict_
     const int s = (wa - c0) & 3;  // slot of column wa - 1
     __syncthreads();
     if (wa + 2 <= c1) st((s + 3) & 3);
-    if (wa + 2 + PF <= c1) ld(wa + 2 + PF);
+    if (wa + 2 + PF <= c1 && !(dbg & 2)) ld(wa + 2 + PF);  // dbg (timing study): 2 no loads, 1 no arithmetic
       const int cb0 = s * Wn::SLOT, cb1 = ((s + 1) & 3) * Wn::SLOT, cb2 = ((s + 2) & 3) * Wn::SLOT;
       f32x4 acc[3];
   #pragma unroll
       for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   #pragma unroll
       for (int m = 0; m < (K::PAIR ? K::NFULL : 0); m += 2) {
+        if (dbg & 1) break;
         const int pp = m / 2, tap = pp / (K::F / 2), q8 = 8 * (pp % (K::F / 2)) + 2 * g4;
         const int ky = tap / 3, kx = tap % 3;
         const int oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + q8;
@@ -1024,6 +1027,7 @@ __global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict_
       }
   #pragma unroll
       for (int m = K::PAIR ? K::NFULL : 0; m < NM; ++m) {
+        if (dbg & 1) break;
         int oa, ob;
         if (m < K::NFULL) {
           const int tap = m / K::F, ky = tap / 3, kx = tap % 3, c = 4 * (m % K::F) + g4;
@@ -1077,7 +1081,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                                                            int nsa, int wc, const float* __restrict__ Wa,
                                                            const float* __restrict__ ba,
                                                            const float* __restrict__ Wb,
-                                                           const float* __restrict__ bb, float* __restrict__ y) {
+                                                           const float* __restrict__ bb, float* __restrict__ y,
+                                                           int dbg) {
   static_assert(CIN % 2 == 0, "pairs of channels");
   using Wn = RlWin<CIN>;
   typedef typename Wn::vec_t vec_t;
@@ -1136,22 +1141,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int s = (wa - c0) & 3;
     __syncthreads();
     if (wa + 2 <= c1) st((s + 3) & 3);
-    if (wa + 2 + PF <= c1) ld(wa + 2 + PF);
+    if (wa + 2 + PF <= c1 && !(dbg & 2)) ld(wa + 2 + PF);  // dbg (timing study): 2 no loads, 1 no arithmetic
       const int cb[3] = {s * Wn::SLOT, ((s + 1) & 3) * Wn::SLOT, ((s + 2) & 3) * Wn::SLOT};
       int wz = 0;
-      asm volatile("" : "+v"(wz));  // the filters re-read from LDS per step (hoisted: 180 VGPRs)
-      const float* wlp = &wl[0][0][0] + wz;
+      asm volatile("" : "+s"(wz));  // the filters re-read per step as scalar loads (hoisted: 180 registers)
+      const float* wga = Wa + wz;
+      const float* wgb = Wb + wz;
       float s0 = 0.f, s1 = 0.f;
   #pragma unroll 3
       for (int tap = 0; tap < 9; ++tap) {
+        if (dbg & 1) break;
         const int ky = tap / 3, kx = tap % 3;
         const float* pa = wwin + ky * Wn::ROW + (kx == 0 ? cb[0] : kx == 1 ? cb[1] : cb[2]);
         const float* pbb = wwin + Wn::ROW + cb[1] + ((ky - 1) * RL_XW + kx - 1) * CIN;
   #pragma unroll
         for (int c2 = 0; c2 < CIN / 2; ++c2) {
           const f32x2 va = *(const f32x2*)(pa + 2 * c2), vb = *(const f32x2*)(pbb + 2 * c2);
-          const f32x2 w0 = *(const f32x2*)(wlp + tap * CIN + 2 * c2);
-          const f32x2 w1 = *(const f32x2*)(wlp + (9 + tap) * CIN + 2 * c2);
+          const f32x2 w0 = {wga[(2 * c2) * 9 + tap], wga[(2 * c2 + 1) * 9 + tap]};
+          const f32x2 w1 = {wgb[(2 * c2) * 9 + tap], wgb[(2 * c2 + 1) * 9 + tap]};
           s0 = fmaf(w0[0], va[0], s0);
           s1 = fmaf(w0[1], va[1], s1);
           s0 = fmaf(w1[0], vb[0], s0);
@@ -1183,6 +1190,7 @@ static int launch_cp4d_roll(const float* x, int B, int hA, int wA, int hB, int w
   if ((long)hA * wA * hB * wB * 10 * 4 > RL_OOR) return 1;  // byte offsets within one batch entry below RL_OOR
   static const int wc_env = getenv("CWT_CP4D_WC") ? atoi(getenv("CWT_CP4D_WC")) : 30;
   const int wc = std::max(1, std::min(wA, wc_env));
+  static const int dbg = getenv("CWT_CP4D_RDBG") ? atoi(getenv("CWT_CP4D_RDBG")) : 0;  // timing study only
   static const int pf = getenv("CWT_CP4D_PF") && atoi(getenv("CWT_CP4D_PF")) == 1 ? 1 : 2;  // prefetch depth
   const int nsa = cdiv(hA, RL_RA);
   const dim3 grid(cdiv(hB, RL_BH) * cdiv(wB, RL_BW), cdiv(wA, wc), B * nsa);
@@ -1190,10 +1198,10 @@ static int launch_cp4d_roll(const float* x, int B, int hA, int wA, int hB, int w
   if (cin == CI && mode == MD) {                                                                             \
     if (pf == 1)                                                                                             \
       hipLaunchKernelGGL((cp4d_roll_kernel<CI, MD, 1>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, \
-                         Wb, bb, y, accum);                                                                  \
+                         Wb, bb, y, accum, dbg);                                                             \
     else                                                                                                     \
       hipLaunchKernelGGL((cp4d_roll_kernel<CI, MD, 2>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, \
-                         Wb, bb, y, accum);                                                                  \
+                         Wb, bb, y, accum, dbg);                                                             \
     CWT_LAUNCH_CHECK();                                                                                      \
     return 0;                                                                                                \
   }
@@ -1206,19 +1214,19 @@ static int launch_cp4d_roll(const float* x, int B, int hA, int wA, int hB, int w
   if (cin == 10 && mode == 2) {  // COUT = 1
     if (pf == 1)
       hipLaunchKernelGGL((cp4d_c1_roll_kernel<10, 1>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, Wb,
-                         bb, y);
+                         bb, y, dbg);
     else
       hipLaunchKernelGGL((cp4d_c1_roll_kernel<10, 2>), grid, dim3(256), 0, st, x, hA, wA, hB, wB, nsa, wc, Wa, ba, Wb,
-                         bb, y);
+                         bb, y, dbg);
     CWT_LAUNCH_CHECK();
     return 0;
   }
   return 1;
 }
-// CWT_CP4D_ROLL: 0 never, 1 (default) the COUT = 10 layers, 2 also COUT = 1 (A/B: the VALU
-// COUT = 1 form measured slower than the tile kernel, 552 against 480 us at 60^2)
+// CWT_CP4D_ROLL: 0 never, 1 the COUT = 10 layers only, 2 (default) also COUT = 1 (its VALU form
+// with the filters from scalar loads: 355 against the tile kernel's 482 us at 60^2)
 static int cp4d_roll_mode() {
-  static const int m = getenv("CWT_CP4D_ROLL") ? atoi(getenv("CWT_CP4D_ROLL")) : 1;
+  static const int m = getenv("CWT_CP4D_ROLL") ? atoi(getenv("CWT_CP4D_ROLL")) : 2;
   return m;
 }
 
