@@ -1000,65 +1000,65 @@ __global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict_
     __syncthreads();
     if (wa + 2 <= c1) st((s + 3) & 3);
     if (wa + 2 + PF <= c1 && !(dbg & 2)) ld(wa + 2 + PF);  // dbg (timing study): 2 no loads, 1 no arithmetic
-      const int cb0 = s * Wn::SLOT, cb1 = ((s + 1) & 3) * Wn::SLOT, cb2 = ((s + 2) & 3) * Wn::SLOT;
-      f32x4 acc[3];
-  #pragma unroll
-      for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  #pragma unroll
-      for (int m = 0; m < (K::PAIR ? K::NFULL : 0); m += 2) {
-        if (dbg & 1) break;
-        const int pp = m / 2, tap = pp / (K::F / 2), q8 = 8 * (pp % (K::F / 2)) + 2 * g4;
-        const int ky = tap / 3, kx = tap % 3;
-        const int oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + q8;
-        const int ob = Wn::ROW + cb1 + ((ky - 1) * RL_XW + kx - 1) * CIN + q8;
-        f32x2 va[3], vb[3];
-  #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          va[j] = *(const f32x2*)(wwin + oa + pbj[j]);
-          vb[j] = *(const f32x2*)(wwin + ob + pbj[j]);
-        }
-  #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-  #pragma unroll
-          for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[j][h], wra[m + h], acc[j], 0, 0, 0);
-  #pragma unroll
-          for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[j][h], wrb[m + h], acc[j], 0, 0, 0);
+    const int cb0 = s * Wn::SLOT, cb1 = ((s + 1) & 3) * Wn::SLOT, cb2 = ((s + 2) & 3) * Wn::SLOT;
+    f32x4 acc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < (K::PAIR ? K::NFULL : 0); m += 2) {
+      if (dbg & 1) break;
+      const int pp = m / 2, tap = pp / (K::F / 2), q8 = 8 * (pp % (K::F / 2)) + 2 * g4;
+      const int ky = tap / 3, kx = tap % 3;
+      const int oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + q8;
+      const int ob = Wn::ROW + cb1 + ((ky - 1) * RL_XW + kx - 1) * CIN + q8;
+      f32x2 va[3], vb[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        va[j] = *(const f32x2*)(wwin + oa + pbj[j]);
+        vb[j] = *(const f32x2*)(wwin + ob + pbj[j]);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[j][h], wra[m + h], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[j][h], wrb[m + h], acc[j], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int m = K::PAIR ? K::NFULL : 0; m < NM; ++m) {
+      if (dbg & 1) break;
+      int oa, ob;
+      if (m < K::NFULL) {
+        const int tap = m / K::F, ky = tap / 3, kx = tap % 3, c = 4 * (m % K::F) + g4;
+        oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + c;
+        ob = Wn::ROW + cb1 + ((ky - 1) * RL_XW + kx - 1) * CIN + c;
+      } else {
+        const int ma = mixa[m - K::NFULL], kx = ma & 3;
+        oa = (ma >> 2) + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2);
+        ob = Wn::ROW + cb1 + mixb[m - K::NFULL];
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wwin[oa + pbj[j]], wra[m], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wwin[ob + pbj[j]], wrb[m], acc[j], 0, 0, 0);
+    }
+    // D: lane (col o = r, rows 4 g4 + i) -> pair (a = (ha, wa), b = tile position 16 j + 4 g4 + i),
+    // stored through a resource based at column wa (off-map pairs and dead columns: offset RL_OOR)
+    {
+      const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(yz + (long)wa * NB * COUT), (short)0, (int)((long)(NA - wa) * NB * COUT * 4), 0x00020000);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = MODE == 0 ? fmaxf(acc[j][i] + bias, 0.f) : acc[j][i];
+          if (MODE == 1 && accum)
+            v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff[j][i], 0, 0));
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, yoff[j][i], 0, 0);
         }
       }
-  #pragma unroll
-      for (int m = K::PAIR ? K::NFULL : 0; m < NM; ++m) {
-        if (dbg & 1) break;
-        int oa, ob;
-        if (m < K::NFULL) {
-          const int tap = m / K::F, ky = tap / 3, kx = tap % 3, c = 4 * (m % K::F) + g4;
-          oa = ky * Wn::ROW + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2) + c;
-          ob = Wn::ROW + cb1 + ((ky - 1) * RL_XW + kx - 1) * CIN + c;
-        } else {
-          const int ma = mixa[m - K::NFULL], kx = ma & 3;
-          oa = (ma >> 2) + (kx == 0 ? cb0 : kx == 1 ? cb1 : cb2);
-          ob = Wn::ROW + cb1 + mixb[m - K::NFULL];
-        }
-  #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wwin[oa + pbj[j]], wra[m], acc[j], 0, 0, 0);
-  #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wwin[ob + pbj[j]], wrb[m], acc[j], 0, 0, 0);
-      }
-      // D: lane (col o = r, rows 4 g4 + i) -> pair (a = (ha, wa), b = tile position 16 j + 4 g4 + i),
-      // stored through a resource based at column wa (off-map pairs and dead columns: offset RL_OOR)
-      {
-        const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(yz + (long)wa * NB * COUT), (short)0, (int)((long)(NA - wa) * NB * COUT * 4), 0x00020000);
-  #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-  #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float v = MODE == 0 ? fmaxf(acc[j][i] + bias, 0.f) : acc[j][i];
-            if (MODE == 1 && accum)
-              v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff[j][i], 0, 0));
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ry, yoff[j][i], 0, 0);
-          }
-        }
-      }
+    }
   };
   store(0);
   load(c0);
@@ -1075,7 +1075,8 @@ __global__ __launch_bounds__(256) void cp4d_roll_kernel(const float* __restrict_
 
 // COUT = 1 on the same rolling window (VALU: cp4d_c1_kernel's per-pair fmaf chains, the two
 // branches' even / odd channels in two partial sums); thread t < 192 takes strip row t / 48 and
-// tile b position t % 48, the filters are broadcast from LDS.
+// tile b position t % 48; the filters are wave-uniform scalar loads (broadcast from LDS they made
+// the kernel LDS-bound: 497 against 355 us at 60^2).
 template <int CIN, int PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void cp4d_c1_roll_kernel(const float* __restrict__ x, int hA, int wA, int hB, int wB,
                                                            int nsa, int wc, const float* __restrict__ Wa,
@@ -1089,7 +1090,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   constexpr int V = Wn::V, VP = Wn::VP;
   __shared__ __attribute__((aligned(16))) float win[Wn::LDS];
-  __shared__ __attribute__((aligned(16))) float wl[2][9][CIN];
   const int NA = hA * wA, NB = hB * wB;
   const int ntbw = (wB + RL_BW - 1) / RL_BW;
   const int hb0 = ((int)blockIdx.x / ntbw) * RL_BH, wb0 = ((int)blockIdx.x % ntbw) * RL_BW;
@@ -1119,10 +1119,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int k = 0; k < Wn::IL; ++k) *(vec_t*)(win + (k < Wn::IL - 1 || loff[k] < Wn::FLOATS ? slot * Wn::SLOT : 0) + loff[k]) = rg[k];
   };
   load(c0 - 1);
-  if (t < 2 * 9 * CIN) {
-    const int c = t % CIN, tap = (t / CIN) % 9, side = t / (9 * CIN);
-    (&wl[0][0][0])[t] = (side ? Wb : Wa)[c * 9 + tap];
-  }
   const float bias = ba[0] + bb[0];
   const bool act = t < RL_RA * RL_NT;
   const int ai = act ? t / RL_NT : 0, tp = act ? t % RL_NT : 0;
@@ -1142,32 +1138,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __syncthreads();
     if (wa + 2 <= c1) st((s + 3) & 3);
     if (wa + 2 + PF <= c1 && !(dbg & 2)) ld(wa + 2 + PF);  // dbg (timing study): 2 no loads, 1 no arithmetic
-      const int cb[3] = {s * Wn::SLOT, ((s + 1) & 3) * Wn::SLOT, ((s + 2) & 3) * Wn::SLOT};
-      int wz = 0;
-      asm volatile("" : "+s"(wz));  // the filters re-read per step as scalar loads (hoisted: 180 registers)
-      const float* wga = Wa + wz;
-      const float* wgb = Wb + wz;
-      float s0 = 0.f, s1 = 0.f;
-  #pragma unroll 3
-      for (int tap = 0; tap < 9; ++tap) {
-        if (dbg & 1) break;
-        const int ky = tap / 3, kx = tap % 3;
-        const float* pa = wwin + ky * Wn::ROW + (kx == 0 ? cb[0] : kx == 1 ? cb[1] : cb[2]);
-        const float* pbb = wwin + Wn::ROW + cb[1] + ((ky - 1) * RL_XW + kx - 1) * CIN;
-  #pragma unroll
-        for (int c2 = 0; c2 < CIN / 2; ++c2) {
-          const f32x2 va = *(const f32x2*)(pa + 2 * c2), vb = *(const f32x2*)(pbb + 2 * c2);
-          const f32x2 w0 = {wga[(2 * c2) * 9 + tap], wga[(2 * c2 + 1) * 9 + tap]};
-          const f32x2 w1 = {wgb[(2 * c2) * 9 + tap], wgb[(2 * c2 + 1) * 9 + tap]};
-          s0 = fmaf(w0[0], va[0], s0);
-          s1 = fmaf(w0[1], va[1], s1);
-          s0 = fmaf(w1[0], vb[0], s0);
-          s1 = fmaf(w1[1], vb[1], s1);
-        }
+    const int cb[3] = {s * Wn::SLOT, ((s + 1) & 3) * Wn::SLOT, ((s + 2) & 3) * Wn::SLOT};
+    int wz = 0;
+    asm volatile("" : "+s"(wz));  // the filters re-read per step as scalar loads (hoisted: 180 registers)
+    const float* wga = Wa + wz;
+    const float* wgb = Wb + wz;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll 3
+    for (int tap = 0; tap < 9; ++tap) {
+      if (dbg & 1) break;
+      const int ky = tap / 3, kx = tap % 3;
+      const float* pa = wwin + ky * Wn::ROW + (kx == 0 ? cb[0] : kx == 1 ? cb[1] : cb[2]);
+      const float* pbb = wwin + Wn::ROW + cb[1] + ((ky - 1) * RL_XW + kx - 1) * CIN;
+#pragma unroll
+      for (int c2 = 0; c2 < CIN / 2; ++c2) {
+        const f32x2 va = *(const f32x2*)(pa + 2 * c2), vb = *(const f32x2*)(pbb + 2 * c2);
+        const f32x2 w0 = {wga[(2 * c2) * 9 + tap], wga[(2 * c2 + 1) * 9 + tap]};
+        const f32x2 w1 = {wgb[(2 * c2) * 9 + tap], wgb[(2 * c2 + 1) * 9 + tap]};
+        s0 = fmaf(w0[0], va[0], s0);
+        s1 = fmaf(w0[1], va[1], s1);
+        s0 = fmaf(w1[0], vb[0], s0);
+        s1 = fmaf(w1[1], vb[1], s1);
       }
-      const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(yz + (long)wa * NB), (short)0, (int)((long)(NA - wa) * NB * 4), 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, fmaxf((s0 + s1) + bias, 0.f)), ry, yoff, 0, 0);
+    }
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(yz + (long)wa * NB), (short)0, (int)((long)(NA - wa) * NB * 4), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, fmaxf((s0 + s1) + bias, 0.f)), ry, yoff, 0, 0);
   };
   store(0);
   load(c0);
