@@ -199,6 +199,10 @@ struct cwt_ctx {
   const float* fold_fc = nullptr;
   int64_t fold_ver = -1;
   int fold_H = 0;
+  // a second stream for independent work inside one call (the symmetric NeighConsensus
+  // branches), forked from and joined back into the caller's stream by events
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace cwt {
@@ -1036,6 +1040,9 @@ int cwt_ctx_destroy(cwt_ctx* ctx) {
   for (auto& kv : ctx->ws)
     if (kv.second.p) (void)hipFree(kv.second.p);
   if (ctx->status_host) (void)hipHostFree(ctx->status_host);
+  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   delete ctx;
   return 0;
 }
@@ -1548,10 +1555,28 @@ static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int
     }
   }
   // branch 0: conv(x) (conv1 over the query positions a, conv2 over the support positions b);
-  // branch 1 (symmetric mode): conv(x^T)^T = the same stack with the two roles swapped
+  // branch 1 (symmetric mode): conv(x^T)^T = the same stack with the two roles swapped.  The two
+  // branches are independent until their sum: branch 1 runs on the context's second stream
+  // (its own intermediate buffers), so one branch's store-bound layers overlap the other's
+  // MFMA-bound ones (CWT_MATCH_BRANCH_STREAMS=0: one after the other on the caller's stream)
+  static const bool two_streams = !(getenv("CWT_MATCH_BRANCH_STREAMS") && getenv("CWT_MATCH_BRANCH_STREAMS")[0] == '0');
+  const bool fork = symmetric && two_streams;
+  void *x1b = x1, *x2b = x2;
+  if (fork) {
+    if (!saved && ((rc = ensure_ws(ctx, "match.x1b", (size_t)B * P * 10 * 4, &x1b)) ||
+                   (rc = ensure_ws(ctx, "match.x2b", (size_t)B * P * 10 * 4, &x2b))))
+      return rc;
+    if (!ctx->aux) CWT_HIP(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+    if (!ctx->ev_fork) CWT_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    if (!ctx->ev_join) CWT_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    CWT_HIP(hipEventRecord(ctx->ev_fork, st));
+    CWT_HIP(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
+  }
   for (int br = 0; br < (symmetric ? 2 : 1); ++br) {
     const float* in = (const float*)x0;
-    float* outs[3] = {(float*)x1, (float*)x2, br ? (float*)y2 : (float*)y1};
+    const hipStream_t bst = (fork && br == 1) ? ctx->aux : st;
+    float* outs[3] = {br && fork ? (float*)x1b : (float*)x1, br && fork ? (float*)x2b : (float*)x2,
+                      br ? (float*)y2 : (float*)y1};
     if (saved)
       for (int l = 0; l < 3; ++l) outs[l] = S.o[br][l];
     for (int l = 0; l < 3; ++l) {
@@ -1559,9 +1584,13 @@ static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int
       const float* ba = br ? lw[l][3] : lw[l][1];
       const float* Wb = br ? lw[l][0] : lw[l][2];
       const float* bb = br ? lw[l][1] : lw[l][3];
-      if ((rc = launch_cp4d_layer(in, B, h, w, h, w, ch[l], ch[l + 1], Wa, ba, Wb, bb, outs[l], st))) return rc;
+      if ((rc = launch_cp4d_layer(in, B, h, w, h, w, ch[l], ch[l + 1], Wa, ba, Wb, bb, outs[l], bst))) return rc;
       in = outs[l];
     }
+  }
+  if (fork) {
+    CWT_HIP(hipEventRecord(ctx->ev_join, ctx->aux));
+    CWT_HIP(hipStreamWaitEvent(st, ctx->ev_join, 0));
   }
   }
   if (saved) {  // y = o[0][2] (+ o[1][2]) into its own slot: the ReLU outputs stay for the backward
