@@ -75,6 +75,10 @@ int launch_widen_bf16(const __bf16* x, long n, float* y, hipStream_t st);
 int launch_gemm_abt(const float* A, const float* Bm, int B, int M, int N, int K, float* Cm, hipStream_t st);
 int launch_mutual_matching(const float* x, int B, int NA, int NB, int C, float* y, float* rowmax, float* colpart,
                            float* colmax, hipStream_t st);
+int launch_mutual_matching_sum(const float* x, const float* x2, int B, int NA, int NB, float* y, float* rowmax,
+                               float* colpart, float* colmax, hipStream_t st);
+int launch_mutual_matching_planar2(const float* x, int B, int NA, int NB, float* y, float* rowmax, float* colpart,
+                                   float* colmax, hipStream_t st);
 int launch_cp4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout, const float* Wa,
                       const float* ba, const float* Wb, const float* bb, float* y, hipStream_t st);
 int launch_cp4d_layer_variant(const float* x, int B, int hA, int wA, int hB, int wB, int cin, int cout,
@@ -1437,7 +1441,7 @@ int cwt_corr(cwt_ctx* ctx, const float* q, const float* k, int B, int Pq, int Pk
 static int mm_ws(cwt_ctx* ctx, int B, int NA, int NB, int C, float** rowmax, float** colpart, float** colmax) {
   void *r, *p, *c;
   int rc;
-  const long nrb = cdiv(NA, 16);
+  const long nrb = cdiv(NA, 8);  // row blocks of launch_mutual_matching (8 rows: vector forms; 16: scalar)
   if ((rc = ensure_ws(ctx, "match.rowmax", (size_t)B * C * NA * 4, &r)) ||
       (rc = ensure_ws(ctx, "match.colpart", (size_t)B * C * nrb * NB * 4, &p)) ||
       (rc = ensure_ws(ctx, "match.colmax", (size_t)B * C * NB * 4, &c)))
@@ -1485,6 +1489,13 @@ static size_t match_saved_layout(float* base, int B, int L, long NA, int symmetr
   return off;
 }
 
+// CWT_MM_FUSE=1: the 2-channel correlation's transposition folded into MutualMatching's passes
+// and the symmetric branches' sum into the second MutualMatching (fewer passes over the 4-D map)
+static bool mm_fuse() {
+  static const bool on = getenv("CWT_MM_FUSE") && getenv("CWT_MM_FUSE")[0] == '1';
+  return on;
+}
+
 static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int h, int w, const float* nc_params,
                               int symmetric, float temp, const float* v, int Cv, float* corr2d, float* weighted_v,
                               void* stream, bool cv4, float* saved = nullptr) {
@@ -1516,8 +1527,13 @@ static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int
   if (L == 1) {
     if ((rc = launch_mutual_matching(corr, B, (int)NA, (int)NB, 1, (float*)x0, rm, cp, cm, st))) return rc;
   } else {
-    if ((rc = launch_to_channels_last(corr, B, L, P, (float*)x0, st))) return rc;
-    if ((rc = launch_mutual_matching((const float*)x0, B, (int)NA, (int)NB, L, (float*)x0, rm, cp, cm, st))) return rc;
+    if (mm_fuse()) {
+      if ((rc = launch_mutual_matching_planar2(corr, B, (int)NA, (int)NB, (float*)x0, rm, cp, cm, st))) return rc;
+    } else {
+      if ((rc = launch_to_channels_last(corr, B, L, P, (float*)x0, st))) return rc;
+      if ((rc = launch_mutual_matching((const float*)x0, B, (int)NA, (int)NB, L, (float*)x0, rm, cp, cm, st)))
+        return rc;
+    }
   }
   const int ch[4] = {L, 10, 10, 1};
   if (cv4) {
@@ -1597,11 +1613,17 @@ static int match_corr_forward(cwt_ctx* ctx, const float* corr, int B, int L, int
     CWT_HIP(hipMemcpyAsync(S.y, S.o[0][2], (size_t)B * P * 4, hipMemcpyDeviceToDevice, st));
     if (symmetric && (rc = launch_add_inplace(S.y, (const float*)S.o[1][2], B * P, st))) return rc;
     y1 = S.y;
-  } else if (symmetric && (rc = launch_add_inplace((float*)y1, (const float*)y2, B * P, st))) {
+  } else if (symmetric && !mm_fuse() && (rc = launch_add_inplace((float*)y1, (const float*)y2, B * P, st))) {
     return rc;
   }
   if ((rc = mm_ws(ctx, B, (int)NA, (int)NB, 1, &rm, &cp, &cm))) return rc;
-  if ((rc = launch_mutual_matching((const float*)y1, B, (int)NA, (int)NB, 1, corr2d, rm, cp, cm, st))) return rc;
+  if (!saved && symmetric && mm_fuse()) {  // MutualMatching of y1 + y2 (the sum folded into its two passes)
+    if ((rc = launch_mutual_matching_sum((const float*)y1, (const float*)y2, B, (int)NA, (int)NB, corr2d, rm, cp, cm,
+                                         st)))
+      return rc;
+  } else if ((rc = launch_mutual_matching((const float*)y1, B, (int)NA, (int)NB, 1, corr2d, rm, cp, cm, st))) {
+    return rc;
+  }
   if (weighted_v) {
     // attn = softmax(temp * corr2d, dim=-1); weighted_v = bmm(v, attn^T) (match.py:151-153),
     // here as tokens [B][NA][Cv] = attn . v

@@ -26,10 +26,149 @@
 
 namespace cwt {
 
-// ---- MutualMatching (match.py:34-53), per channel of x[B][NA][NB][C] ----
-// row maxima (over b for each a) and per-row-block partial column maxima
-constexpr int MM_RB = 16;  // rows of a per block
-__global__ __launch_bounds__(256) void mm_rowcol_kernel(const float* __restrict__ x, int NA, int NB, int C,
+// ---- MutualMatching (match.py:34-53), per channel of x[B][NA][NB][C] (C = 1 or 2) ----
+// row maxima (over b for each a) and per-row-block partial column maxima; a thread reads the C
+// channels of a pair as one vector (both channels of a 128-B line in the same block)
+constexpr int MM_RB = 16;  // rows of a per block (the scalar form)
+constexpr int MM_RBV = 8;  // rows per block of the vector forms (450 workgroups at 60^2)
+// PLANAR: x is the torch layout [B][C][NA][NB] (channel planes) instead of channels-last
+template <int C, int RB = MM_RBV, bool PLANAR = false>
+__global__ __launch_bounds__(256) void mm_rowcol_kernel(const float* __restrict__ x, int NA, int NB,
+                                                        float* __restrict__ rowmax, float* __restrict__ colpart,
+                                                        const float* __restrict__ x2 = nullptr) {
+  // grid: (cdiv(NA, RB), B); rowmax [B*C][NA], colpart [B*C][cdiv(NA,RB)][NB]
+  typedef float vec_t __attribute__((ext_vector_type(C)));
+  const int b = blockIdx.y;
+  const int a0 = blockIdx.x * RB;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const vec_t* xb = (const vec_t*)(x + (long)b * NA * NB * C);
+  __shared__ float rm[4][RB][C];
+  float rmax[RB][C];
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int c = 0; c < C; ++c) rmax[r][c] = -INFINITY;
+  for (int j = t; j < NB; j += 256) {
+    float cm[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) cm[c] = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int a = a0 + r;
+      if (a < NA) {
+        vec_t v;
+        if (PLANAR) {
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            const float pv = x[((long)(b * C + c) * NA + a) * NB + j];
+            if (C == 1) v[0] = pv; else v[c] = pv;
+          }
+        } else {
+          v = xb[(long)a * NB + j];
+          if (C == 1 && x2) v[0] = v[0] + x2[(long)b * NA * NB + (long)a * NB + j];  // the symmetric branches' sum
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const float vc = C == 1 ? v[0] : v[c];
+          cm[c] = fmaxf(cm[c], vc);
+          rmax[r][c] = fmaxf(rmax[r][c], vc);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) colpart[((long)(b * C + c) * gridDim.x + blockIdx.x) * NB + j] = cm[c];
+  }
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      float v = rmax[r][c];
+      for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+      if (lane == 0) rm[wv][r][c] = v;
+    }
+  __syncthreads();
+  if (t < RB * C) {
+    const int r = t / C, c = t % C;
+    if (a0 + r < NA)
+      rowmax[(long)(b * C + c) * NA + a0 + r] = fmaxf(fmaxf(rm[0][r][c], rm[1][r][c]), fmaxf(rm[2][r][c], rm[3][r][c]));
+  }
+}
+
+// column maxima from the row blocks' partials: block = 64 columns x 4 slices of the row blocks
+// (the one-column-per-thread form ran 225 dependent loads per thread on 30 workgroups)
+__global__ __launch_bounds__(256) void mm_colmax_kernel(const float* __restrict__ colpart, int nrb, int NB,
+                                                        float* __restrict__ colmax) {
+  __shared__ float part[4][64];
+  const int bc = blockIdx.y;
+  const int jl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + jl;
+  float m = -INFINITY;
+  if (j < NB)
+    for (int rb = sl; rb < nrb; rb += 4) m = fmaxf(m, colpart[((long)bc * nrb + rb) * NB + j]);
+  part[sl][jl] = m;
+  __syncthreads();
+  if (sl == 0 && j < NB) colmax[(long)bc * NB + j] = fmaxf(fmaxf(part[0][jl], part[1][jl]), fmaxf(part[2][jl], part[3][jl]));
+}
+
+// y = x * ((x / (rowmax + eps)) * (x / (colmax + eps))); x, y [B][NA][NB][C] (y may alias x).
+// grid (NA, B): block (a, b) walks the row's NB pairs (C channels each as one vector)
+template <int C, bool PLANAR = false>  // PLANAR: x channel planes [B][C][NA][NB], y channels-last
+__global__ __launch_bounds__(256) void mm_apply_kernel(const float* x, int NA, int NB,
+                                                       const float* __restrict__ rowmax,
+                                                       const float* __restrict__ colmax, float* y,
+                                                       const float* __restrict__ x2 = nullptr) {
+  typedef float vec_t __attribute__((ext_vector_type(C)));
+  const float eps = 1e-5f;
+  const int a = blockIdx.x, b = blockIdx.y;
+  const long row = ((long)b * NA + a) * NB;
+  const vec_t* xr = (const vec_t*)x + row;
+  vec_t* yr = (vec_t*)y + row;
+  float ra[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) ra[c] = rowmax[(long)(b * C + c) * NA + a] + eps;
+  for (int j = threadIdx.x; j < NB; j += 256) {
+    vec_t v;
+    if (PLANAR) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float pv = x[((long)(b * C + c) * NA + a) * NB + j];
+        if (C == 1) v[0] = pv; else v[c] = pv;
+      }
+    } else {
+      v = xr[j];
+      if (C == 1 && x2) v[0] = v[0] + x2[row + j];
+    }
+    vec_t o;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float vc = C == 1 ? v[0] : v[c];
+      const float vb = vc / (colmax[(long)(b * C + c) * NB + j] + eps);  // corr4d_B: max over the A positions
+      const float va = vc / ra[c];                                       // corr4d_A: max over the B positions
+      if (C == 1) o[0] = vc * (va * vb); else o[c] = vc * (va * vb);
+    }
+    yr[j] = o;
+  }
+}
+
+// any C (cwt_mutual_matching takes up to 64): the scalar forms
+__global__ __launch_bounds__(256) void mm_apply_any_kernel(const float* x, long total, int NA, int NB, int C,
+                                                       const float* __restrict__ rowmax,
+                                                       const float* __restrict__ colmax, float* y) {
+  const float eps = 1e-5f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long p = i / C;
+    const int j = (int)(p % NB);
+    const long ab = p / NB;
+    const int a = (int)(ab % NA), b = (int)(ab / NA);
+    const int bc = b * C + c;
+    const float v = x[i];
+    const float vb = v / (colmax[(long)bc * NB + j] + eps);  // corr4d_B: max over the A positions
+    const float va = v / (rowmax[(long)bc * NA + a] + eps);  // corr4d_A: max over the B positions
+    y[i] = v * (va * vb);
+  }
+}
+__global__ __launch_bounds__(256) void mm_rowcol_any_kernel(const float* __restrict__ x, int NA, int NB, int C,
                                                         float* __restrict__ rowmax, float* __restrict__ colpart) {
   // grid: (cdiv(NA, MM_RB), B * C); rowmax [B*C][NA], colpart [B*C][cdiv(NA,MM_RB)][NB]
   const int bc = blockIdx.y, b = bc / C, c = bc - b * C;
@@ -62,35 +201,6 @@ __global__ __launch_bounds__(256) void mm_rowcol_kernel(const float* __restrict_
   __syncthreads();
   if (t < MM_RB && a0 + t < NA)
     rowmax[(long)bc * NA + a0 + t] = fmaxf(fmaxf(rm[0][t], rm[1][t]), fmaxf(rm[2][t], rm[3][t]));
-}
-
-__global__ __launch_bounds__(256) void mm_colmax_kernel(const float* __restrict__ colpart, int nrb, int NB,
-                                                        float* __restrict__ colmax) {
-  const int bc = blockIdx.y;
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= NB) return;
-  float m = -INFINITY;
-  for (int rb = 0; rb < nrb; ++rb) m = fmaxf(m, colpart[((long)bc * nrb + rb) * NB + j]);
-  colmax[(long)bc * NB + j] = m;
-}
-
-// y = x * ((x / (rowmax + eps)) * (x / (colmax + eps))); x, y [B][NA][NB][C] (y may alias x)
-__global__ __launch_bounds__(256) void mm_apply_kernel(const float* x, long total, int NA, int NB, int C,
-                                                       const float* __restrict__ rowmax,
-                                                       const float* __restrict__ colmax, float* y) {
-  const float eps = 1e-5f;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int c = (int)(i % C);
-    const long p = i / C;
-    const int j = (int)(p % NB);
-    const long ab = p / NB;
-    const int a = (int)(ab % NA), b = (int)(ab / NA);
-    const int bc = b * C + c;
-    const float v = x[i];
-    const float vb = v / (colmax[(long)bc * NB + j] + eps);  // corr4d_B: max over the A positions
-    const float va = v / (rowmax[(long)bc * NA + a] + eps);  // corr4d_A: max over the B positions
-    y[i] = v * (va * vb);
-  }
 }
 
 // ---- one CenterPivotConv4d layer (+ ReLU) on x[B][NA][NB][CIN] -> y[B][NA][NB][COUT] ----
@@ -1629,17 +1739,68 @@ int launch_mmn_blend(const float* fq_in, const float* att, int B, long n, float 
   return 0;
 }
 
+// the same on the torch layout x [B][2][NA][NB] (channel planes), y channels-last [B][NA][NB][2]: the
+// transposition folded into the two passes over x (MatchNet's in_channel 2 correlation)
+int launch_mutual_matching_planar2(const float* x, int B, int NA, int NB, float* y, float* rowmax, float* colpart,
+                                   float* colmax, hipStream_t st) {
+  const int nrbv = cdiv(NA, MM_RBV);
+  hipLaunchKernelGGL((mm_rowcol_kernel<2, MM_RBV, true>), dim3(nrbv, B), dim3(256), 0, st, x, NA, NB, rowmax, colpart);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mm_colmax_kernel, dim3(cdiv(NB, 64), B * 2), dim3(256), 0, st, (const float*)colpart, nrbv, NB,
+                     colmax);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL((mm_apply_kernel<2, true>), dim3(NA, B), dim3(256), 0, st, x, NA, NB, (const float*)rowmax,
+                     (const float*)colmax, y);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
+// one channel, on the sum x + x2 of two [B][NA][NB] tensors (NeighConsensus' symmetric branches;
+// the add the separate pass did, in the same order)
+int launch_mutual_matching_sum(const float* x, const float* x2, int B, int NA, int NB, float* y, float* rowmax,
+                               float* colpart, float* colmax, hipStream_t st) {
+  const int nrbv = cdiv(NA, MM_RBV);
+  hipLaunchKernelGGL((mm_rowcol_kernel<1>), dim3(nrbv, B), dim3(256), 0, st, x, NA, NB, rowmax, colpart, x2);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mm_colmax_kernel, dim3(cdiv(NB, 64), B), dim3(256), 0, st, (const float*)colpart, nrbv, NB,
+                     colmax);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL((mm_apply_kernel<1>), dim3(NA, B), dim3(256), 0, st, x, NA, NB, (const float*)rowmax,
+                     (const float*)colmax, y, x2);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 int launch_mutual_matching(const float* x, int B, int NA, int NB, int C, float* y, float* rowmax, float* colpart,
                            float* colmax, hipStream_t st) {
   const int nrb = cdiv(NA, MM_RB);
-  hipLaunchKernelGGL(mm_rowcol_kernel, dim3(nrb, B * C), dim3(256), 0, st, x, NA, NB, C, rowmax, colpart);
+  if (C != 1 && C != 2) {  // the scalar forms
+    hipLaunchKernelGGL(mm_rowcol_any_kernel, dim3(nrb, B * C), dim3(256), 0, st, x, NA, NB, C, rowmax, colpart);
+    CWT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(mm_colmax_kernel, dim3(cdiv(NB, 64), B * C), dim3(256), 0, st, (const float*)colpart, nrb,
+                       NB, colmax);
+    CWT_LAUNCH_CHECK();
+    const long total = (long)B * NA * NB * C;
+    hipLaunchKernelGGL(mm_apply_any_kernel, dim3((unsigned)std::min<long>(65536, cdiv(total, 256))), dim3(256), 0, st,
+                       x, total, NA, NB, C, (const float*)rowmax, (const float*)colmax, y);
+    CWT_LAUNCH_CHECK();
+    return 0;
+  }
+  const int nrbv = cdiv(NA, MM_RBV);
+  if (C == 1)
+    hipLaunchKernelGGL((mm_rowcol_kernel<1>), dim3(nrbv, B), dim3(256), 0, st, x, NA, NB, rowmax, colpart);
+  else
+    hipLaunchKernelGGL((mm_rowcol_kernel<2>), dim3(nrbv, B), dim3(256), 0, st, x, NA, NB, rowmax, colpart);
   CWT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(mm_colmax_kernel, dim3(cdiv(NB, 256), B * C), dim3(256), 0, st, (const float*)colpart, nrb, NB,
+  hipLaunchKernelGGL(mm_colmax_kernel, dim3(cdiv(NB, 64), B * C), dim3(256), 0, st, (const float*)colpart, nrbv, NB,
                      colmax);
   CWT_LAUNCH_CHECK();
-  const long total = (long)B * NA * NB * C;
-  hipLaunchKernelGGL(mm_apply_kernel, dim3((unsigned)std::min<long>(65536, cdiv(total, 256))), dim3(256), 0, st, x,
-                     total, NA, NB, C, (const float*)rowmax, (const float*)colmax, y);
+  if (C == 1)
+    hipLaunchKernelGGL(mm_apply_kernel<1>, dim3(NA, B), dim3(256), 0, st, x, NA, NB, (const float*)rowmax,
+                       (const float*)colmax, y);
+  else
+    hipLaunchKernelGGL(mm_apply_kernel<2>, dim3(NA, B), dim3(256), 0, st, x, NA, NB, (const float*)rowmax,
+                       (const float*)colmax, y);
   CWT_LAUNCH_CHECK();
   return 0;
 }

@@ -37,14 +37,15 @@ def _corr(dev, B, L, h, w, seed):
     return c.to(dev)
 
 
-def test_mutual_matching(dev):
+@pytest.mark.parametrize("C", [1, 2, 3])  # 1 / 2: the vector kernels; 3: the scalar forms
+def test_mutual_matching(dev, C):
     from few_shot_seg_cwt_amd.match import MutualMatching
     from oracle import match_oracle as M
     g = torch.Generator().manual_seed(7)
-    x = (torch.rand(2, 3, 5, 7, 6, 4, generator=g) * 2 - 1).to(dev)
+    x = (torch.rand(2, C, 5, 7, 6, 4, generator=g) * 2 - 1).to(dev)
     y = MutualMatching(x)
     e = rel(y, M.mutual_matching(x.double().cpu()))
-    print(f"MutualMatching: {e:.2e}")
+    print(f"MutualMatching C={C}: {e:.2e}")
     assert e < 1e-6
 
 
