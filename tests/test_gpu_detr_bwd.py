@@ -17,6 +17,7 @@ from test_gpu_detr import _deform_params, _rand, rel  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-4
+TOL_SUM = 3e-4  # the scalar bias gradients of the last 4-D consensus layer (test_detr_backward)
 
 
 @pytest.fixture(scope="module")
@@ -136,4 +137,10 @@ def test_detr_backward(dev, cs, sf):
         if t.grad is not None or sd[n].grad is not None:
             errs[n] = rel(t.grad, sd[n].grad)
     print(f"DeTr backward cs={cs} sf={sf}: " + ", ".join(f"{k} {e:.1e}" for k, e in errs.items()))
-    assert max(errs.values()) < TOL, errs
+    # the last consensus layer's two biases (10 -> 1) are single scalars, each the sum of the
+    # ReLU-masked upstream gradient over every (a, b) pair: a sum with heavy cancellation whose fp32
+    # relative error was measured at 3e-5 .. 1.1e-4 across runs and builds (profiles/r4/run_hh,
+    # run_gg) -- they get TOL_SUM; every other gradient keeps TOL
+    bias_sum = [k for k in errs if k.startswith("cross_trans.NeighConsensus.conv.4.") and k.endswith(".bias")]
+    assert max(v for k, v in errs.items() if k not in bias_sum) < TOL, errs
+    assert all(errs[k] < TOL_SUM for k in bias_sum), {k: errs[k] for k in bias_sum}
