@@ -112,6 +112,8 @@ SIGNATURES = {
     "cwt_debug_cp4d_layer": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P]),
     "cwt_debug_conv_f32d": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _I,
                                  _I, _I, _P]),
+    "cwt_debug_conv_x6": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _I,
+                               _I, _I, _P]),
     "cwt_debug_census": (_I, [_P, _I, _P, _P]),
     "cwt_debug_tail_stamps": (_I, [_P, _P, _I64, _P]),
     "cwt_debug_pretrain_op": (_I, [_P, _I, C.POINTER(_P), C.POINTER(_I64), C.POINTER(_F), _P]),

@@ -183,9 +183,10 @@ struct cwt_ctx {
   // inner loop: captured graphs of the step sequence (disable with CWT_ADAPT_GRAPH=0)
   cwt::AdaptGraphCache adapt_graphs;
   bool use_graph = true;
-  // conv arithmetic: bf16x3 on the bf16 matrix cores over S-layout activations (default,
-  // CWT_CONV=x3s) or exact fp32 MFMA over fp32 activations (CWT_CONV=f32)
-  bool conv_split = true;
+  // conv arithmetic (CWT_CONV_ARITH_*): fp32 width on the bf16 matrix cores, operands split three
+  // ways in registers (default, CWT_CONV=x6); bf16x3 over S-layout activations (CWT_CONV=x3s,
+  // ~16-bit operands: a declared approximation); exact fp32 MFMA (CWT_CONV=f32)
+  int conv_arith = CWT_CONV_ARITH_BF16X6;
   // persistent inner loop: units per workgroup (0 automatic, 1, 2), cwt_ctx_set_adapt_units
   int adapt_upw = 0;
   // asynchronous status word (cwt_ctx_status): mapped, coherent host memory the kernels OR
@@ -665,15 +666,18 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   const bool b16 = bb->precision == CWT_CONV_BF16;
   // the training-mode BN pass (once per epoch) amplifies conv rounding ~100x through its
   // batch statistics: in fp32 precision it runs the exact-fp32 conv path
-  const bool conv_split = ctx->conv_split && !(tb && !b16);
+  const bool conv_split = ctx->conv_arith == CWT_CONV_ARITH_BF16X3 && !(tb && !b16);
   const bool s_path = b16 || conv_split;  // S-layout / bf16 activations
   const int layout = b16 ? ACT_BF16 : conv_split ? ACT_SPLIT : ACT_F32;
   // the exact-fp32 path (eval mode) runs on the same LDS-DMA conv body (conv_igemm_f32d: fp32
   // NHWC activations, f32 MFMA); CWT_CONV_F32D=0 selects the register-staged conv_igemm_f32
   static const bool f32d_env = !(getenv("CWT_CONV_F32D") && getenv("CWT_CONV_F32D")[0] == '0');
-  const bool f32d = !s_path && !tb && f32d_env;
-  const bool dma = s_path || f32d;  // conv_x3s.hip kernels
-  const int prec = b16 ? 1 : conv_split ? 3 : 0;
+  // fp32 width on the bf16 matrix cores (conv_igemm_x6): f32d's operands, split in registers
+  const bool x6 = !s_path && !tb && ctx->conv_arith == CWT_CONV_ARITH_BF16X6;
+  const bool f32d = !s_path && !tb && !x6 && f32d_env;
+  const bool f32ops = f32d || x6;  // fp32 NHWC operands on the LDS-DMA body
+  const bool dma = s_path || f32ops;  // conv_x3s.hip kernels
+  const int prec = b16 ? 1 : conv_split ? 3 : x6 ? 6 : 0;
   const int Hs = down2(S), H1 = down2(Hs), h = down2(H1);
   const long sA = std::max({(long)N * Hs * Hs * 128, (long)N * H1 * H1 * 256, (long)N * h * h * 2048});
   const long sT1 = std::max((long)N * H1 * H1 * 128, (long)N * h * h * 512);
@@ -767,7 +771,8 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     ConvArgs a = make_args(c);
     if (b16 && !c.L->w_b) return fail(CWT_ESTATE, "bf16 conv weights missing (Ci % 64 != 0)");
     ConvPlan pl = b16 ? plan_conv_b16(a.M, a.Co, a.K) : conv_split ? plan_conv_x3s(a.M, a.Co, a.K)
-                  : f32d ? plan_conv_f32d(a.M, a.Co, a.K) : plan_conv(a.M, a.Co, a.K);
+                  : x6 ? plan_conv_x6(a.M, a.Co, a.K) : f32d ? plan_conv_f32d(a.M, a.Co, a.K)
+                                                         : plan_conv(a.M, a.Co, a.K);
     plans.push_back(pl);
     if (pl.nsplit > 1) part_floats = std::max(part_floats, (size_t)pl.nsplit * a.M * a.Co);
   }
@@ -833,7 +838,8 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     const double bytes = eb * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K) +
                          ob * ((double)a.M * a.Co + (a.res ? (double)a.M * a.Co : 0.0));
     Prof p(ctx, st,
-           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : f32d ? "conv_igemm_f32d<" : "conv_igemm_f32<") +
+           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : x6 ? "conv_igemm_x6<"
+                       : f32d ? "conv_igemm_f32d<" : "conv_igemm_f32<") +
                std::to_string(pl.bm) + "," +
                std::to_string(pl.bn) + "," +
                std::to_string(calls[i].stage) + ">" +
@@ -847,11 +853,11 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
       memset(&sa, 0, sizeof(sa));
       const ConvCall& c = calls[i];
       sa.xs = (const __bf16*)c.x;  // (f32d: the fp32 NHWC map, the same 128-B line geometry)
-      sa.ws = b16 ? c.L->w_b : f32d ? (const __bf16*)c.L->w : c.L->w_s;
+      sa.ws = b16 ? c.L->w_b : f32ops ? (const __bf16*)c.L->w : c.L->w_s;
       sa.zero = zero;
       sa.scale = a.scale;
       sa.shift = a.shift;
-      if (c.out_f32 || f32d) {
+      if (c.out_f32 || f32ops) {
         sa.y = c.y;
         sa.y_ld = c.y_ld;
         sa.y_off = c.y_off;
@@ -1020,12 +1026,12 @@ int cwt_ctx_create(int device, cwt_ctx** out) {
   const char* g = getenv("CWT_ADAPT_GRAPH");
   c->use_graph = !(g && g[0] == '0');
   const char* cv = getenv("CWT_CONV");
-  const std::string mode = cv ? std::string(cv) : std::string("x3s");
-  if (mode != "x3s" && mode != "f32") {
+  const std::string mode = cv ? std::string(cv) : std::string("x6");
+  if (mode != "x6" && mode != "x3s" && mode != "f32") {
     delete c;
-    return fail(CWT_EARG, "CWT_CONV must be x3s (default) or f32");
+    return fail(CWT_EARG, "CWT_CONV must be x6 (default), x3s or f32");
   }
-  c->conv_split = mode == "x3s";
+  c->conv_arith = mode == "x6" ? CWT_CONV_ARITH_BF16X6 : mode == "x3s" ? CWT_CONV_ARITH_BF16X3 : CWT_CONV_ARITH_F32;
   if (hipHostMalloc((void**)&c->status_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&c->status_dev, c->status_host, 0) != hipSuccess) {
     if (c->status_host) (void)hipHostFree(c->status_host);
@@ -2185,9 +2191,11 @@ int cwt_deform_attn_backward(cwt_ctx* ctx, const float* value, const float* offs
   hipStream_t st = (hipStream_t)stream;
   Prof p(ctx, st, "deform_attn_backward", 2.0 * B * H * W * n_heads * n_points * d_head * 12,
          4.0 * (double)B * H * W * n_heads * (d_head * 7 + n_points * 6));
-  CWT_HIP(hipMemsetAsync(d_value, 0, (size_t)B * H * W * n_heads * d_head * 4, st));
-  int rc = launch_deform_attn_bwd(value, offsets, logits, B, H, W, n_heads, n_points, d_head, d_out, d_value, d_offsets,
-                                  d_logits, st);
+  void* ws;
+  int rc;
+  if ((rc = ensure_ws(ctx, "detr.dv64", deform_attn_bwd_ws_bytes(B, H, W, n_heads, d_head), &ws))) return rc;
+  rc = launch_deform_attn_bwd(value, offsets, logits, B, H, W, n_heads, n_points, d_head, d_out, d_value, d_offsets,
+                              d_logits, ws, st);
   p.end();
   return rc;
 }
@@ -2379,8 +2387,10 @@ static int debug_conv_s(cwt_ctx* ctx, int prec, const void* xs, int N, int Hi, i
   a.Wo = (Wi + 2 * pad - dil * (k - 1) - 1) / stride + 1;
   a.M = N * a.Ho * a.Wo;
   a.K = k * k * Ci;
-  ConvPlan p = prec == 1 ? plan_conv_b16(a.M, a.Co, a.K) : prec == 0 ? plan_conv_f32d(a.M, a.Co, a.K)
-                                                         : plan_conv_x3s(a.M, a.Co, a.K);
+  ConvPlan p = prec == 1   ? plan_conv_b16(a.M, a.Co, a.K)
+               : prec == 0 ? plan_conv_f32d(a.M, a.Co, a.K)
+               : prec == 6 ? plan_conv_x6(a.M, a.Co, a.K)
+                           : plan_conv_x3s(a.M, a.Co, a.K);
   if (bm > 0) {
     const int var = bm / 1000;  // bm = 1000 * variant + rows (cwt_debug.h)
     bm %= 1000;
@@ -2423,6 +2433,14 @@ int cwt_debug_conv_f32d(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int
                         const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
                         int nsplit, void* stream) {
   return debug_conv_s(ctx, 0, x, N, Hi, Wi, Ci, w_packed, scale, shift, Co, k, stride, pad, dil, res, res_ld, nullptr,
+                      relu, y, y_ld, y_off, nullptr, bm, bn, nsplit, stream);
+}
+
+int cwt_debug_conv_x6(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, const float* w_packed,
+                      const float* scale, const float* shift, int Co, int k, int stride, int pad, int dil,
+                      const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
+                      int nsplit, void* stream) {
+  return debug_conv_s(ctx, 6, x, N, Hi, Wi, Ci, w_packed, scale, shift, Co, k, stride, pad, dil, res, res_ld, nullptr,
                       relu, y, y_ld, y_off, nullptr, bm, bn, nsplit, stream);
 }
 
@@ -2481,9 +2499,9 @@ int cwt_iou_preds(cwt_ctx* ctx, const int64_t* preds, const int64_t* target, int
 
 int cwt_ctx_set_conv_arith(cwt_ctx* ctx, int arith) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
-  CWT_CHECK(arith == CWT_CONV_ARITH_BF16X3 || arith == CWT_CONV_ARITH_F32,
-            "arith must be CWT_CONV_ARITH_BF16X3 (0) or CWT_CONV_ARITH_F32 (1)");
-  ctx->conv_split = arith == CWT_CONV_ARITH_BF16X3;
+  CWT_CHECK(arith == CWT_CONV_ARITH_BF16X3 || arith == CWT_CONV_ARITH_F32 || arith == CWT_CONV_ARITH_BF16X6,
+            "arith must be CWT_CONV_ARITH_BF16X3 (0), CWT_CONV_ARITH_F32 (1) or CWT_CONV_ARITH_BF16X6 (2)");
+  ctx->conv_arith = arith;
   return 0;
 }
 

@@ -144,6 +144,28 @@ __device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, co
   }
 }
 
+// PREC = 6 (conv_igemm_x6, the fp32-width path on the bf16 matrix cores): the exact-fp32 operands
+// (fp32 NHWC activations, fp32 packed weights: conv_igemm_f32d's bytes and LDS image) are split
+// in registers, after the fragment read, into three bf16 terms x = hi + mid + lo, EXACTLY:
+// hi = bf16_rne(x), mid = bf16_rne(x - hi), lo = x - hi - mid (|lo| <= 2^-16 |x|, at most 8
+// significant bits, so its bf16 conversion is exact).  a.b is summed from the six products whose
+// size is >= 2^-24 |a||b| (hi.hi, hi.mid, mid.hi, mid.mid, hi.lo, lo.hi) with fp32 accumulation;
+// the three dropped (mid.lo, lo.mid, lo.lo) total < 2^-23 |a||b|, the size of one fp32 rounding.
+// One v_mfma_f32_16x16x32_bf16 covers the whole 32-deep K-tile, so a fragment pair costs 6 x 16
+// cycles against the f32 MFMA's 8 x 32.
+__device__ __forceinline__ void split3_bf16(const f32x4& x0, const f32x4& x1, bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float v = i < 4 ? x0[i] : x1[i - 4];
+    const __bf16 hv = (__bf16)v;
+    const float r = v - (float)hv;
+    const __bf16 mv = (__bf16)r;
+    h[i] = hv;
+    m[i] = mv;
+    l[i] = (__bf16)(r - (float)mv);
+  }
+}
+
 // PF = 0: fragments of tile t are read after the barrier that publishes it, then its MFMAs.
 // PF = 1: fragments of tile t+1 are read (into a second register set) right after the barrier
 // that publishes it, BEFORE the MFMAs of tile t, so their LDS latency hides under the MFMAs;
@@ -153,8 +175,9 @@ __device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, co
 // addressing of the operand DMA (every production instantiation sets it).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF>
 __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
-  static_assert(PREC == 0 || PREC == 1 || PREC == 3,
-                "PREC: 3 = bf16x3 over the S-layout, 1 = plain bf16, 0 = exact fp32 (f32 MFMA)");
+  static_assert(PREC == 0 || PREC == 1 || PREC == 3 || PREC == 6,
+                "PREC: 3 = bf16x3 over the S-layout, 1 = plain bf16, 0 = exact fp32 (f32 MFMA), "
+                "6 = fp32 operands split three ways in registers (bf16x6)");
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int FM = WM / 16, FN = WN / 16;
@@ -300,8 +323,11 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   // fragment read geometry: lane -> row (lane & 15) of a 16-row block, k-chunk (lane >> 4)
   const int fr = lane & 15, fk = lane >> 4;
   const int swz = (fr >> 1) & 7;
-  const int off_hi = fr * 128 + ((fk ^ swz) << 4);
-  const int off_lo = fr * 128 + (((4 + fk) ^ swz) << 4);
+  // PREC 6: the lane's 8 fp32 k-values are 16-B chunks 2fk and 2fk+1 (k = 8fk .. 8fk+7, the k
+  // slots of its bf16 fragment); conflict-free like the others (rows fr, fr^1 share a swizzle
+  // but sit 128 B apart)
+  const int off_hi = fr * 128 + (((PREC == 6 ? 2 * fk : fk)) ^ swz) * 16;
+  const int off_lo = fr * 128 + (((PREC == 6 ? 2 * fk + 1 : 4 + fk)) ^ swz) * 16;
   const int a_row0 = wm * WM, b_row0 = BM + wn * WN;
 
   struct Frags {
@@ -328,6 +354,27 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(F.ah[i]), "v"(F.al[i]));
 #pragma unroll
       for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(F.bh[j]), "v"(F.bl[j]));
+      return;
+    }
+    if constexpr (PREC == 6) {
+      bf16x8 bs[FN][3];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        split3_bf16(__builtin_bit_cast(f32x4, F.bh[j]), __builtin_bit_cast(f32x4, F.bl[j]), bs[j][0], bs[j][1], bs[j][2]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        bf16x8 ah, am, al;
+        split3_bf16(__builtin_bit_cast(f32x4, F.ah[i]), __builtin_bit_cast(f32x4, F.al[i]), ah, am, al);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {  // smallest products first
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bs[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bs[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bs[j][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bs[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bs[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bs[j][0], acc[i][j], 0, 0, 0);
+        }
+      }
       return;
     }
 #pragma unroll
@@ -475,6 +522,13 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_b16(ConvSArg
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_f32d(ConvSArgs a) {
   conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 0, (PF | 8)>(a);
+}
+
+// fp32 width on the bf16 matrix cores: conv_igemm_f32d's operands, split three ways in registers
+// (PREC 6 above)
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x6(ConvSArgs a) {
+  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 6, (PF | 8)>(a);
 }
 
 // Split-K reduction (fixed order, deterministic) + the same epilogue math.
@@ -629,6 +683,7 @@ int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipSt
 CWT_TILE_LAUNCH(conv_igemm_x3s)
 CWT_TILE_LAUNCH(conv_igemm_b16)
 CWT_TILE_LAUNCH(conv_igemm_f32d)
+CWT_TILE_LAUNCH(conv_igemm_x6)
 #undef CWT_TILE_LAUNCH
 
 struct MeasuredPlanS {
@@ -719,6 +774,27 @@ ConvPlan plan_conv_f32d(int M, int Co, int K) {
   return plan_heuristic_s(M, Co, ktiles);
 }
 
+static const MeasuredPlanS kMeasuredPlansX6[] = {
+#include "conv_plans_x6.inc"
+    {0, 0, 0, 0, 0, 0, 0}};
+
+// fp32 width on the bf16 matrix cores (conv_igemm_x6): 32-deep K-tiles over f32d's operands; its
+// own measured table (conv_plans_x6.inc, tools/conv_s_sweep.py --prec 6), else the heuristic.
+ConvPlan plan_conv_x6(int M, int Co, int K) {
+  const int ktiles = K / 32;
+  for (const MeasuredPlanS& e : kMeasuredPlansX6)
+    if (e.M == M && e.Co == Co && e.K == K && e.bn > 0 && Co % e.bn == 0) {
+      ConvPlan p;
+      p.bm = e.bm;
+      p.bn = e.bn;
+      p.var = e.var;
+      p.kt_per_split = cdiv(ktiles, e.nsplit);
+      p.nsplit = cdiv(ktiles, p.kt_per_split);
+      return p;
+    }
+  return plan_heuristic_s(M, Co, ktiles);
+}
+
 template <int PREC>
 static void launch_splitk_s(const ConvSArgs& a, int nsplit, hipStream_t st) {
   const long n = (long)a.M * (a.Co / 8);
@@ -736,9 +812,10 @@ static void launch_splitk_s(const ConvSArgs& a, int nsplit, hipStream_t st) {
 // 64-channel-block order, plan_conv_b16)
 int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,
                     hipStream_t st, int prec) {
-  if (prec != 0 && prec != 1 && prec != 3)
-    return fail(CWT_EARG, "conv precision must be 3 (bf16x3), 1 (bf16) or 0 (exact fp32)");
-  if (prec == 0 && (a.ys || a.res_s || !a.y)) return fail(CWT_EARG, "exact-fp32 conv: fp32 output and residual only");
+  if (prec != 0 && prec != 1 && prec != 3 && prec != 6)
+    return fail(CWT_EARG, "conv precision must be 3 (bf16x3), 1 (bf16), 0 (exact fp32) or 6 (bf16x6)");
+  if ((prec == 0 || prec == 6) && (a.ys || a.res_s || !a.y))
+    return fail(CWT_EARG, "fp32-operand conv: fp32 output and residual only");
   if (!a.xs || !a.ws || !a.zero) return fail(CWT_ESTATE, "S-layout conv needs its input, weights and a zero line");
   const int kb = prec == 1 ? 64 : 32;
   if (a.Ci % kb || a.Co % 64 || a.Co % p.bn)
@@ -757,7 +834,17 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
     main.part = nullptr;
   }
   dim3 grid(cdiv(a.M, p.bm), a.Co / p.bn, nsplit);
-  if (prec == 0) {
+  if (prec == 6) {
+    switch (stage) {
+      case 0: launch_tiles_conv_igemm_x6<0>(main, p, grid, st); break;
+      case 1: launch_tiles_conv_igemm_x6<1>(main, p, grid, st); break;
+      case 2: launch_tiles_conv_igemm_x6<2>(main, p, grid, st); break;
+      case 3: launch_tiles_conv_igemm_x6<3>(main, p, grid, st); break;
+      case 4: launch_tiles_conv_igemm_x6<4>(main, p, grid, st); break;
+      case 5: launch_tiles_conv_igemm_x6<5>(main, p, grid, st); break;
+      default: launch_tiles_conv_igemm_x6<6>(main, p, grid, st); break;
+    }
+  } else if (prec == 0) {
     switch (stage) {
       case 0: launch_tiles_conv_igemm_f32d<0>(main, p, grid, st); break;
       case 1: launch_tiles_conv_igemm_f32d<1>(main, p, grid, st); break;
@@ -793,7 +880,7 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
     main.part = part_ws;
     if (prec == 1)
       launch_splitk_s<1>(main, nsplit, st);
-    else if (prec == 0)
+    else if (prec == 0 || prec == 6)
       launch_splitk_s<0>(main, nsplit, st);
     else
       launch_splitk_s<3>(main, nsplit, st);

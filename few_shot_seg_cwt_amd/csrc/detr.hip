@@ -141,13 +141,34 @@ int launch_deform_attn(const float* value, const float* offsets, const float* lo
 //   d a_p = <d_out, v_p>, d logits_p = a_p (d a_p - sum_q a_q d a_q),
 //   d offset_p = a_p <d_out, dv_p / d(ix, iy)> (ix = loc W - 1/2 and loc = ref + off / W, so
 //   d ix / d off_x = 1; zero-padded corners carry no value and no slope),
-//   d value[corner] += w_corner a_p d_out (float atomics: one value position is sampled by many
-//   queries, as in the reference's CUDA backward; d_value must be zeroed first).
+//   d value[corner] += w_corner a_p d_out.  One value position is sampled by many queries (the
+//   reference's CUDA backward scatters with float atomics, whose sum order -- and so result --
+//   changes from run to run); here every contribution is rounded once to a 64-bit fixed-point
+//   integer, rint(c 2^sh) with 2^sh chosen from max|d_out| so no sum can overflow (|c| <= |d_out|,
+//   at most H W P contributions per position), and added with integer atomics, which are exactly
+//   associative: the result is deterministic, within 2^-sh per contribution (~2^-45 max|d_out| at
+//   60^2 positions and 4 points) of the exact sum.  dv64 must be zeroed first;
+//   deform_attn_dv_finish_kernel converts it back.
+__global__ void absmax_bits_kernel(const float* __restrict__ x, long n, unsigned* __restrict__ out) {
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(x[i]));
+  for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // order-free: deterministic
+}
+
+__device__ __forceinline__ double dv_scale(const unsigned* gmax_bits, int headroom) {
+  const float gm = __uint_as_float(*gmax_bits);
+  const int e = gm > 0.f ? ilogbf(gm) : 0;  // |c| < 2^(e+1)
+  return ldexp(1.0, 62 - headroom - (e + 1));
+}
+
 __global__ __launch_bounds__(256) void deform_attn_bwd_kernel(const float* __restrict__ value,
                                                               const float* __restrict__ offsets,
                                                               const float* __restrict__ logits, int B, int H, int W,
                                                               int M, int P, int D, const float* __restrict__ d_out,
-                                                              float* d_value, float* __restrict__ d_offsets,
+                                                              unsigned long long* dv64, const unsigned* gmax_bits,
+                                                              int headroom, float* __restrict__ d_offsets,
                                                               float* __restrict__ d_logits) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
@@ -169,7 +190,8 @@ __global__ __launch_bounds__(256) void deform_attn_bwd_kernel(const float* __res
   const float ref_x = ((float)qx + 0.5f) / (float)W, ref_y = ((float)qy + 0.5f) / (float)H;
   const long vs = (long)M * D;
   const float* vb = value + (long)b * L * vs + m * D + lane;
-  float* dvb = d_value + (long)b * L * vs + m * D + lane;
+  unsigned long long* dvb = dv64 + (long)b * L * vs + m * D + lane;
+  const double S = dv_scale(gmax_bits, headroom);
   const bool act = lane < D;
   const float g = act ? d_out[bq * vs + m * D + lane] : 0.f;
   float da[DA_MAXP], dox[DA_MAXP], doy[DA_MAXP], ap[DA_MAXP];
@@ -201,10 +223,11 @@ __global__ __launch_bounds__(256) void deform_attn_bwd_kernel(const float* __res
     ap[p] = a;
     sad += a * da[p];
     const float gv = a * g;
-    if (i00) atomicAdd(&dvb[((long)y0 * W + x0) * vs], w00 * gv);
-    if (i01) atomicAdd(&dvb[((long)y0 * W + x1) * vs], w01 * gv);
-    if (i10) atomicAdd(&dvb[((long)y1 * W + x0) * vs], w10 * gv);
-    if (i11) atomicAdd(&dvb[((long)y1 * W + x1) * vs], w11 * gv);
+    auto fx64 = [&](float c) { return (unsigned long long)(long long)rint((double)c * S); };
+    if (i00) atomicAdd(&dvb[((long)y0 * W + x0) * vs], fx64(w00 * gv));
+    if (i01) atomicAdd(&dvb[((long)y0 * W + x1) * vs], fx64(w01 * gv));
+    if (i10) atomicAdd(&dvb[((long)y1 * W + x0) * vs], fx64(w10 * gv));
+    if (i11) atomicAdd(&dvb[((long)y1 * W + x1) * vs], fx64(w11 * gv));
   }
   if (lane == 0) {
     float* dl = d_logits + (bq * M + m) * P;
@@ -217,13 +240,36 @@ __global__ __launch_bounds__(256) void deform_attn_bwd_kernel(const float* __res
   }
 }
 
+__global__ void deform_attn_dv_finish_kernel(const unsigned long long* __restrict__ dv64, long n,
+                                             const unsigned* __restrict__ gmax_bits, int headroom,
+                                             float* __restrict__ d_value) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  d_value[i] = (float)((double)(long long)dv64[i] / dv_scale(gmax_bits, headroom));
+}
+
+size_t deform_attn_bwd_ws_bytes(int B, int H, int W, int M, int D) { return 256 + (size_t)B * H * W * M * D * 8; }
+
+// ws: deform_attn_bwd_ws_bytes bytes of device scratch
 int launch_deform_attn_bwd(const float* value, const float* offsets, const float* logits, int B, int H, int W, int M,
                            int P, int D, const float* d_out, float* d_value, float* d_offsets, float* d_logits,
-                           hipStream_t st) {
+                           void* ws, hipStream_t st) {
   if (P > DA_MAXP || D > 64) return fail(CWT_EARG, "deform_attn: n_points <= 16 and d_model / n_heads <= 64");
   const long nw = (long)B * H * W * M;
+  const long n = nw * D;
+  unsigned* gmax = (unsigned*)ws;
+  unsigned long long* dv64 = (unsigned long long*)((char*)ws + 256);
+  int headroom = 1;  // bits for the number of contributions per position (<= H W P) and the sign
+  while ((1L << headroom) < (long)H * W * P * 2) ++headroom;
+  if (hipMemsetAsync(ws, 0, 256 + (size_t)n * 8, st) != hipSuccess) return fail(CWT_ESTATE, "deform_attn_bwd: memset");
+  hipLaunchKernelGGL(absmax_bits_kernel, dim3((unsigned)std::min<long>(1024, cdiv(n, 256))), dim3(256), 0, st, d_out, n,
+                     gmax);
+  CWT_LAUNCH_CHECK();
   hipLaunchKernelGGL(deform_attn_bwd_kernel, dim3((unsigned)cdiv(nw, 4)), dim3(256), 0, st, value, offsets, logits, B, H,
-                     W, M, P, D, d_out, d_value, d_offsets, d_logits);
+                     W, M, P, D, d_out, dv64, (const unsigned*)gmax, headroom, d_offsets, d_logits);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(deform_attn_dv_finish_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st,
+                     (const unsigned long long*)dv64, n, (const unsigned*)gmax, headroom, d_value);
   CWT_LAUNCH_CHECK();
   return 0;
 }

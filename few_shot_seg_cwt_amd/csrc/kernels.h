@@ -117,8 +117,11 @@ int launch_splitk_epilogue(const ConvArgs& a, int nsplit, hipStream_t st);
 ConvPlan plan_conv_x3s(int M, int Co, int K);
 ConvPlan plan_conv_b16(int M, int Co, int K);
 ConvPlan plan_conv_f32d(int M, int Co, int K);
+ConvPlan plan_conv_x6(int M, int Co, int K);
 // prec 3: bf16x3 (S-layout operands); prec 1: plain bf16 (NHWC bf16 activations, [Co][K]
-// bf16 weights with K ordered (64-channel block, tap, channel): packed_k64)
+// bf16 weights with K ordered (64-channel block, tap, channel): packed_k64); prec 0: exact fp32
+// (f32 MFMA) and prec 6: fp32 width on the bf16 MFMA (three-way register split), both over fp32
+// NHWC activations and the fp32 packed weights
 int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,
                     hipStream_t st, int prec = 3);
 int launch_split_act(const float* x, long P, int C, int ld, __bf16* out, hipStream_t st);
@@ -227,9 +230,10 @@ int launch_colsum(const float* X, long R, int Cc, long ld, int accum, float* out
                   hipStream_t st);
 int launch_to_channels_first(const float* x, int B, int C, long P, float* y, hipStream_t st);
 int launch_copy_pad(const float* X, long R, int Cc, int ld, float* out, hipStream_t st);
+size_t deform_attn_bwd_ws_bytes(int B, int H, int W, int M, int D);
 int launch_deform_attn_bwd(const float* value, const float* offsets, const float* logits, int B, int H, int W, int M,
                            int P, int D, const float* d_out, float* d_value, float* d_offsets, float* d_logits,
-                           hipStream_t st);
+                           void* ws, hipStream_t st);
 int launch_norm_blend_bwd(const float* a, const float* b, const float* d, long T, int C, float wt, float* d_a,
                           float* d_b, hipStream_t st);
 int launch_copy_2d(const float* src, long R, int Cc, long lds, float* dst, long ldd, hipStream_t st);

@@ -318,12 +318,13 @@ __global__ __launch_bounds__(256) void cp4d_wgrad_kernel(const float* __restrict
   }
 }
 
-// sum the partials in workgroup order; dWa / dWb [COUT][CIN][9] and db1 / db2 [COUT] accumulate
+// sum the partials in workgroup order; dWa / dWb [COUT][CIN][9] accumulate, and db1 / db2 [COUT]
+// unless bias == 0 (cp4d_bias_grad_f64 sums those)
 __global__ void cp4d_wgrad_reduce_kernel(const float* __restrict__ part, int G, int CIN, int COUT, float* dWa,
-                                         float* dWb, float* db1, float* db2) {
+                                         float* dWb, float* db1, float* db2, int bias) {
   const int NE = 18 * COUT, n = NE * CIN + COUT;
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= n) return;
+  if (idx >= n || (!bias && idx >= NE * CIN)) return;
   float s = 0.f;
   for (int g = 0; g < G; ++g) s += part[(long)g * n + idx];
   if (idx < NE * CIN) {
@@ -336,6 +337,45 @@ __global__ void cp4d_wgrad_reduce_kernel(const float* __restrict__ part, int G, 
     db1[o] += s;
     db2[o] += s;
   }
+}
+
+// The bias gradients db1 = db2 += sum over every (a, b) pair of gm[p][o]: a sum of up to B (hA wA)
+// (hB wB) terms whose ReLU-masked values cancel heavily (the last consensus layer's single bias is
+// a few 1e-3 of sum |gm|), so it is accumulated in double, in a fixed order: chunks of
+// CB64_ROWS rows per workgroup (a thread's rows strided by 256, then a fixed LDS tree), then the
+// chunks in order.  Deterministic and accurate to the fp32 rounding of the result.
+constexpr int CB64_ROWS = 16384, CB64_MAXC = 16;
+__global__ __launch_bounds__(256) void colsum_f64_part_kernel(const float* __restrict__ X, long R, int Cc,
+                                                              double* __restrict__ part) {
+  __shared__ double red[256][CB64_MAXC + 1];
+  const int t = threadIdx.x;
+  const long r0 = (long)blockIdx.x * CB64_ROWS;
+  const long r1 = min(R, r0 + CB64_ROWS);
+  double acc[CB64_MAXC];
+#pragma unroll
+  for (int o = 0; o < CB64_MAXC; ++o) acc[o] = 0.0;
+  for (long r = r0 + t; r < r1; r += 256)
+#pragma unroll
+    for (int o = 0; o < CB64_MAXC; ++o)
+      if (o < Cc) acc[o] += (double)X[r * Cc + o];
+#pragma unroll
+  for (int o = 0; o < CB64_MAXC; ++o) red[t][o] = acc[o];
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (t < w)
+      for (int o = 0; o < Cc; ++o) red[t][o] += red[t + w][o];
+    __syncthreads();
+  }
+  if (t < Cc) part[(long)blockIdx.x * Cc + t] = red[0][t];
+}
+
+__global__ void colsum_f64_final_kernel(const double* __restrict__ part, int nch, int Cc, float* db1, float* db2) {
+  const int o = threadIdx.x;
+  if (o >= Cc) return;
+  double s = 0.0;
+  for (int c = 0; c < nch; ++c) s += part[(long)c * Cc + o];
+  db1[o] = (float)((double)db1[o] + s);
+  if (db2) db2[o] = (float)((double)db2[o] + s);
 }
 
 // workgroups of the weight-gradient pass: 512 for the 10 -> 10 layer (two per CU by LDS), 2048 for
@@ -372,7 +412,15 @@ int launch_cp4d_wgrad(const float* x, const float* gm, int B, int hA, int wA, in
 #undef CWT_WG
   }
   hipLaunchKernelGGL(cp4d_wgrad_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, (const float*)part, G, cin, cout,
-                     dWa, dWb, db1, db2);
+                     dWa, dWb, db1, db2, 0);
+  CWT_LAUNCH_CHECK();
+  // the biases in double (the partials above are consumed: their workspace takes the chunks)
+  const long R = (long)B * hA * wA * hB * wB;
+  const int nch = (int)cdiv(R, (long)CB64_ROWS);
+  if (cout > CB64_MAXC || (size_t)nch * cout * 2 > part_floats) return fail(CWT_ESTATE, "cp4d bias sum: workspace");
+  hipLaunchKernelGGL(colsum_f64_part_kernel, dim3(nch), dim3(256), 0, st, gm, R, cout, (double*)part);
+  CWT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(colsum_f64_final_kernel, dim3(1), dim3(64), 0, st, (const double*)part, nch, cout, db1, db2);
   CWT_LAUNCH_CHECK();
   return 0;
 }

@@ -494,7 +494,8 @@ int cwt_linear_backward(cwt_ctx* ctx, const float* x, int64_t P, int K, const fl
 
 /* cwt_deform_attn's backward (ms_deform_attn.py:99-117, ms_deform_attn_func.py:41-61 under autograd;
  * one level, DeTr's pixel-centre reference points): d_out device [B][H*W][n_heads*d_head] ->
- * d_value (same shape, accumulated with float atomics as the reference CUDA op does),
+ * d_value (same shape; the reference CUDA op scatters it with float atomics, run-to-run
+ * nondeterministic: here in 64-bit fixed point with integer atomics, deterministic),
  * d_offsets device [B][H*W][n_heads][n_points][2], d_logits device [B][H*W][n_heads][n_points]. */
 int cwt_deform_attn_backward(cwt_ctx* ctx, const float* value, const float* offsets, const float* logits, int B, int H,
                              int W, int n_heads, int n_points, int d_head, const float* d_out, float* d_value,
@@ -644,13 +645,19 @@ int cwt_ctx_status(cwt_ctx* ctx, uint32_t* status, int clear);
 
 /*
  * Arithmetic of this context's fp32 conv stack (no reference counterpart; the reference's
- * torch convs are fp32): CWT_CONV_ARITH_BF16X3 (default, or CWT_CONV=x3s) = fp32 operands split
- * into bf16 hi + lo, three bf16 MFMA products; CWT_CONV_ARITH_F32 (CWT_CONV=f32) = exact fp32
- * MFMA over fp32 activations.  Both packings are built at cwt_backbone_load, so this switches
- * between calls.  A bf16 backbone (cwt_backbone_set_precision) is unaffected.
+ * torch convs are fp32, src/model/resnet.py:57-96, pspnet.py:124-129):
+ *   CWT_CONV_ARITH_BF16X6 (default, or CWT_CONV=x6) = fp32 width on the bf16 matrix cores: fp32
+ *     activations and weights, each operand split exactly into bf16 hi + mid + lo in registers,
+ *     the six products >= 2^-24 |a||b| summed with fp32 accumulation;
+ *   CWT_CONV_ARITH_F32 (CWT_CONV=f32) = exact fp32 MFMA over fp32 activations;
+ *   CWT_CONV_ARITH_BF16X3 (CWT_CONV=x3s) = a declared approximation: operands rounded to 16
+ *     significant bits (bf16 hi + lo), three bf16 MFMA products.
+ * Every packing is built at cwt_backbone_load, so this switches between calls.  A bf16
+ * backbone (cwt_backbone_set_precision) is unaffected.
  */
 #define CWT_CONV_ARITH_BF16X3 0
 #define CWT_CONV_ARITH_F32 1
+#define CWT_CONV_ARITH_BF16X6 2
 int cwt_ctx_set_conv_arith(cwt_ctx* ctx, int arith);
 
 int cwt_profile_enable(cwt_ctx* ctx, int level);

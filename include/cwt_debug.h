@@ -63,6 +63,13 @@ int cwt_debug_conv_f32d(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int
                         const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
                         int nsplit, void* stream);
 
+/* The same conv at fp32 width on the bf16 matrix cores (conv_igemm_x6, the conv of
+ * cwt_ctx_set_conv_arith(CWT_CONV_ARITH_BF16X6)): arguments and layouts as cwt_debug_conv_f32d. */
+int cwt_debug_conv_x6(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, const float* w_packed,
+                      const float* scale, const float* shift, int Co, int k, int stride, int pad, int dil,
+                      const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
+                      int nsplit, void* stream);
+
 /* One CenterPivotConv4d layer + ReLU (src/model/conv4d.py:40-62) on the channels-last 4-D
  * tensor x [B][hA*wA][hB*wB][cin] -> y [B][hA*wA][hB*wB][cout]: Wa / Wb [cout][cin][3][3] the
  * a-plane / b-plane filters, ba / bb their biases.  variant 0: the library's kernel choice, 1:

@@ -225,7 +225,8 @@ def pack_w_f32(w):
     return w.reshape(Co, Ci // 32, 32, k * k).permute(0, 1, 3, 2).contiguous()
 
 
-def run_conv_f32d(x, w, scale, shift, stride, pad, dil, res=None, relu=True, bm=0, bn=0, nsplit=0, y_pad=0, y_off=0):
+def run_conv_f32d(x, w, scale, shift, stride, pad, dil, res=None, relu=True, bm=0, bn=0, nsplit=0, y_pad=0, y_off=0,
+                  entry="cwt_debug_conv_f32d"):
     L = _lib()
     dev = torch.device("cuda", 0)
     N, Ci, Hi, Wi = x.shape
@@ -237,10 +238,10 @@ def run_conv_f32d(x, w, scale, shift, stride, pad, dil, res=None, relu=True, bm=
     y = torch.full((N, Ho, Ho, y_ld), float("nan"), device=dev)
     rd = res.permute(0, 2, 3, 1).contiguous().to(dev) if res is not None else None
     sc, sh = scale.to(dev), shift.to(dev)
-    rc = L.lib().cwt_debug_conv_f32d(L.ctx(0), L.ptr(xd), N, Hi, Wi, Ci, L.ptr(wd), L.ptr(sc), L.ptr(sh), Co, k,
-                                     stride, pad, dil, L.ptr(rd), Co, int(relu), L.ptr(y), y_ld, y_off, bm, bn,
-                                     nsplit, L.stream_ptr())
-    L.check(rc, "cwt_debug_conv_f32d")
+    rc = getattr(L.lib(), entry)(L.ctx(0), L.ptr(xd), N, Hi, Wi, Ci, L.ptr(wd), L.ptr(sc), L.ptr(sh), Co, k,
+                                 stride, pad, dil, L.ptr(rd), Co, int(relu), L.ptr(y), y_ld, y_off, bm, bn,
+                                 nsplit, L.stream_ptr())
+    L.check(rc, entry)
     torch.cuda.synchronize()
     yc = y.cpu()
     if y_pad:
@@ -281,3 +282,67 @@ def test_conv_f32d_channel_strided_out():
     y = run_conv_f32d(x, w, scale, shift, 1, 1, 1, None, relu=False, y_pad=256, y_off=128)
     ref = ref_conv(x, w, scale, shift, 1, 1, 1, None, False)
     assert float((y.double() - ref).abs().max() / ref.abs().max()) < TOL_F32D
+
+
+# ---------------------------------------------------------------- fp32 width on bf16 MFMA (conv_igemm_x6)
+# f32d's operands split exactly into bf16 hi + mid + lo in registers; the three dropped products
+# total < 2^-23 |a||b| per product (one fp32 rounding): the same bar as the exact-fp32 kernel
+TOL_X6 = 1e-5
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("plan", PLANS, ids=lambda p: f"{p[0]}x{p[1]}s{p[2]}")
+def test_conv_x6_plans(case, plan):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    N, Ci, Co, Hi, k, stride, dil, has_res = case
+    bm, bn, ns = plan
+    if bn and Co % bn:
+        pytest.skip("Co not a multiple of the tile")
+    tag = f"{N}_{Ci}_{Co}_{Hi}_{k}"
+    x = torch.from_numpy(syn.normal(1, "x" + tag, (N, Ci, Hi, Hi), 1.0))
+    w = torch.from_numpy(syn.normal(1, "w" + tag, (Co, Ci, k, k), (2.0 / (Ci * k * k)) ** 0.5))
+    scale = torch.from_numpy(syn.uniform(1, "s" + tag, (Co,), 0.5, 1.5))
+    shift = torch.from_numpy(syn.normal(1, "b" + tag, (Co,), 0.1))
+    pad = dil if k == 3 else 0
+    Ho = (Hi + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    res = torch.from_numpy(syn.normal(1, "r" + tag, (N, Co, Ho, Ho), 1.0)) if has_res else None
+    y = run_conv_f32d(x, w, scale, shift, stride, pad, dil, res, bm=bm, bn=bn, nsplit=ns, entry="cwt_debug_conv_x6")
+    ref = ref_conv(x, w, scale, shift, stride, pad, dil, res, True)
+    err = float((y.double() - ref).abs().max() / ref.abs().max())
+    assert err < TOL_X6, err
+
+
+def test_conv_x6_wide_range_operands():
+    """Operands spanning 2^-30 .. 2^30 (every split level populated, tiny lo terms): the x6 conv
+    against float64 relative to the reference's own fp32 conv error, element by element."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    g = torch.Generator().manual_seed(5)
+    N, Ci, Co, Hi = 1, 64, 64, 9
+    mant = torch.rand((N, Ci, Hi, Hi), generator=g) + 0.5
+    expo = torch.randint(-30, 31, (N, Ci, Hi, Hi), generator=g).float()
+    x = (mant * torch.pow(2.0, expo) * torch.sign(torch.randn((N, Ci, Hi, Hi), generator=g))).float()
+    w = torch.randn((Co, Ci, 3, 3), generator=g) * 0.05
+    one, zero = torch.ones(Co), torch.zeros(Co)
+    y = run_conv_f32d(x, w, one, zero, 1, 1, 1, None, relu=False, entry="cwt_debug_conv_x6")
+    ref = ref_conv(x, w, one, zero, 1, 1, 1, None, False)
+    # bound per output: the dropped split terms (< 2^-23 |x||w| per product) plus the worst-case
+    # fp32 accumulation of K = 576 terms (gamma_K ~ K * 2^-24), both relative to sum |x||w|
+    absref = F.conv2d(x.double().abs(), w.double().abs(), None, 1, 1, 1)
+    bound = (2.0 * 2.0 ** -24 + 576 * 2.0 ** -24) * absref
+    assert bool(((y.double() - ref).abs() <= bound).all()), float(((y.double() - ref).abs() / absref).max())
+    y32 = F.conv2d(x, w, None, 1, 1, 1).double()
+    print("x6 max err / sum|x||w|:", float(((y.double() - ref).abs() / absref).max()),
+          " torch fp32:", float(((y32 - ref).abs() / absref).max()))
+
+
+def test_conv_x6_channel_strided_out():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    x = torch.from_numpy(syn.normal(2, "x", (2, 64, 11, 11), 1.0))
+    w = torch.from_numpy(syn.normal(2, "w", (128, 64, 3, 3), 0.06))
+    scale, shift = torch.ones(128), torch.zeros(128)
+    y = run_conv_f32d(x, w, scale, shift, 1, 1, 1, None, relu=False, y_pad=256, y_off=128, entry="cwt_debug_conv_x6")
+    ref = ref_conv(x, w, scale, shift, 1, 1, 1, None, False)
+    assert float((y.double() - ref).abs().max() / ref.abs().max()) < TOL_X6

@@ -66,49 +66,73 @@ def test_extract_features_small_vs_reference(dev, small, layers):
     assert rel(f, small[f"feat_r{layers}_S33"]) < 1e-4
 
 
-def test_extract_features_full_vs_oracle(dev):
-    from oracle import cwt_oracle as O
-    ep = syn.make_episode(SEED, 0, 473, 1)
-    x = torch.from_numpy(ep["qry_img"])
-    f, _ = model(50).extract_features(x.to(dev))
-    ref = O.extract_features(x, O.to_torch_state(syn.make_pspnet_state(50, SEED)))
-    assert rel(f, ref) < TOL
+ARITH_X3S, ARITH_F32, ARITH_X6 = 0, 1, 2   # CWT_CONV_ARITH_*; the context default is X6
 
 
-class exact_fp32:
-    """the default context's conv stack on the exact-fp32 path (cwt_ctx_set_conv_arith F32:
-    conv_igemm_f32d, the LDS-DMA body on v_mfma_f32_16x16x4_f32) for the duration"""
+class conv_arith:
+    """the default context's conv stack in another arithmetic for the duration
+    (cwt_ctx_set_conv_arith): F32 = conv_igemm_f32d (the LDS-DMA body on v_mfma_f32_16x16x4_f32),
+    X3S = the bf16x3 approximation over S-layout activations; restores the default (X6)"""
+
+    def __init__(self, arith):
+        self.arith = arith
 
     def __enter__(self):
         from few_shot_seg_cwt_amd import _lib
-        _lib.check(_lib.lib().cwt_ctx_set_conv_arith(_lib.ctx(0), 1), "cwt_ctx_set_conv_arith")
+        _lib.check(_lib.lib().cwt_ctx_set_conv_arith(_lib.ctx(0), self.arith), "cwt_ctx_set_conv_arith")
 
     def __exit__(self, *exc):
         from few_shot_seg_cwt_amd import _lib
-        _lib.check(_lib.lib().cwt_ctx_set_conv_arith(_lib.ctx(0), 0), "cwt_ctx_set_conv_arith")
+        _lib.check(_lib.lib().cwt_ctx_set_conv_arith(_lib.ctx(0), ARITH_X6), "cwt_ctx_set_conv_arith")
         return False
 
 
-@pytest.mark.parametrize("layers", [50, 101])
-def test_extract_features_exact_fp32_small_vs_reference(dev, small, layers):
-    ep = syn.make_episode(SEED, 7, 33, 2)
-    x = torch.from_numpy(ep["spprt_imgs"][0]).to(dev)
-    with exact_fp32():
-        f, _ = model(layers).extract_features(x)
-        torch.cuda.synchronize()
-    # fp32 products, fp32 sums in another order: the reference's own arithmetic
-    assert rel(f, small[f"feat_r{layers}_S33"]) < 1e-5
+def exact_fp32():
+    return conv_arith(ARITH_F32)
 
 
-def test_extract_features_exact_fp32_full_vs_oracle(dev):
+# x6 and f32: fp32-width products, fp32 sums in another order (the reference's own arithmetic,
+# bar 1e-5); x3s: 16-bit operands (the declared approximation, bar 1e-3)
+BAR = {ARITH_X6: 1e-5, ARITH_F32: 1e-5, ARITH_X3S: TOL}
+
+
+@pytest.mark.parametrize("arith", [ARITH_X6, ARITH_X3S], ids=["x6", "x3s"])
+def test_extract_features_full_vs_oracle(dev, arith):
     from oracle import cwt_oracle as O
     ep = syn.make_episode(SEED, 0, 473, 1)
-    x = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]]))
-    with exact_fp32():
+    x = torch.from_numpy(ep["qry_img"])
+    with conv_arith(arith):
         f, _ = model(50).extract_features(x.to(dev))
         torch.cuda.synchronize()
     ref = O.extract_features(x, O.to_torch_state(syn.make_pspnet_state(50, SEED)))
-    assert rel(f, ref) < 1e-5
+    err = rel(f, ref)
+    print(f"extract_features 473 arith {arith}: {err:.3e}")
+    assert err < BAR[arith]
+
+
+@pytest.mark.parametrize("arith", [ARITH_X6, ARITH_F32], ids=["x6", "f32"])
+@pytest.mark.parametrize("layers", [50, 101])
+def test_extract_features_exact_fp32_small_vs_reference(dev, small, layers, arith):
+    ep = syn.make_episode(SEED, 7, 33, 2)
+    x = torch.from_numpy(ep["spprt_imgs"][0]).to(dev)
+    with conv_arith(arith):
+        f, _ = model(layers).extract_features(x)
+        torch.cuda.synchronize()
+    assert rel(f, small[f"feat_r{layers}_S33"]) < BAR[arith]
+
+
+@pytest.mark.parametrize("arith", [ARITH_X6, ARITH_F32], ids=["x6", "f32"])
+def test_extract_features_exact_fp32_full_vs_oracle(dev, arith):
+    from oracle import cwt_oracle as O
+    ep = syn.make_episode(SEED, 0, 473, 1)
+    x = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]]))
+    with conv_arith(arith):
+        f, _ = model(50).extract_features(x.to(dev))
+        torch.cuda.synchronize()
+    ref = O.extract_features(x, O.to_torch_state(syn.make_pspnet_state(50, SEED)))
+    err = rel(f, ref)
+    print(f"extract_features 473 x2 arith {arith}: {err:.3e}")
+    assert err < BAR[arith]
 
 
 def test_extract_batch_independent(dev):
@@ -301,13 +325,15 @@ def test_episode_vs_reference(dev, golden_dir, name, layers, S, shot, n_ep):
             assert hard == 0
 
 
+@pytest.mark.parametrize("arith", [ARITH_F32, ARITH_X3S], ids=["f32", "x3s"])
 @pytest.mark.parametrize("name,layers,S,shot", [
     ("episode_pascal_r50_1shot.npz", 50, 473, 1),
     ("episode_coco_r101_1shot.npz", 101, 641, 1),
 ])
-def test_episode_exact_fp32_vs_reference(dev, golden_dir, name, layers, S, shot):
-    """The exact-fp32 conv stack (bench.py's exact_fp32 leg) against the reference's episode
-    fixture: W, W', logits and IoU counts; no argmax flip above the margin."""
+def test_episode_exact_fp32_vs_reference(dev, golden_dir, name, layers, S, shot, arith):
+    """The conv stack's other arithmetics (bench.py's exact_fp32 and bf16x3 legs; the default x6
+    runs in test_episode_vs_reference) against the reference's episode fixture: W, W', logits
+    and IoU counts; no argmax flip above the margin."""
     from few_shot_seg_cwt_amd.episode import EpisodeEngine
     g = dict(np.load(os.path.join(golden_dir, name)))
     cfg = syn.cfg_defaults(layers=layers, image_size=S, shot=shot)
@@ -316,7 +342,7 @@ def test_episode_exact_fp32_vs_reference(dev, golden_dir, name, layers, S, shot)
     ep = syn.make_episode(SEED, 0, S, shot, classes)
     imgs = torch.from_numpy(np.concatenate([ep["spprt_imgs"][0], ep["qry_img"]])).to(dev)
     W0 = torch.from_numpy(g["e0_W0"]).to(dev).contiguous()
-    with exact_fp32():
+    with conv_arith(arith):
         r = eng.run(imgs, torch.from_numpy(ep["s_label"][0]).to(dev), torch.from_numpy(ep["q_label"]).to(dev), W0)
         torch.cuda.synchronize()
     assert rel(r["W"], g["e0_W"]) < TOL
@@ -325,7 +351,7 @@ def test_episode_exact_fp32_vs_reference(dev, golden_dir, name, layers, S, shot)
     low = _low_margin(g["e0_pred_q"], S)
     iu = r["iut"][0].cpu().numpy()
     assert np.abs(iu - g["e0_iu"]).max() <= low
-    _, hard = flip_report(r["pred_q"][0], g["e0_pred_q"], S, f"{name}:exact_fp32")
+    _, hard = flip_report(r["pred_q"][0], g["e0_pred_q"], S, f"{name}:arith{arith}")
     assert hard == 0
 
 

@@ -87,7 +87,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         if prec == 1:   # plain bf16 operands (K order inside a row does not matter for timing)
             xs = x.to(torch.bfloat16).contiguous()
             ws = w.reshape(Co, K).to(torch.bfloat16).contiguous()
-        elif prec == 0:  # exact fp32 (conv_igemm_f32d): fp32 NHWC and fp32 [Co][K] weights
+        elif prec in (0, 6):  # exact fp32 (conv_igemm_f32d) / bf16x6 (conv_igemm_x6): fp32 NHWC and fp32 [Co][K]
             xs = x
             ws = w.reshape(Co, K).contiguous()
         else:
@@ -99,7 +99,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         sh = torch.zeros(Co, device=dev)
         r = torch.randn(n_img, Ho, Ho, Co, device=dev) if has_res else None
         rs = None
-        if has_res and prec == 0:
+        if has_res and prec in (0, 6):
             rs = None
         elif has_res and prec == 1:
             rs = r.to(torch.bfloat16).contiguous()
@@ -113,8 +113,9 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         conv_fn = lib.cwt_debug_conv_b16 if prec == 1 else lib.cwt_debug_conv_s
 
         def new(bm, bn, ns):
-            if prec == 0:
-                return lambda: _lib.check(lib.cwt_debug_conv_f32d(
+            if prec in (0, 6):
+                fn = lib.cwt_debug_conv_f32d if prec == 0 else lib.cwt_debug_conv_x6
+                return lambda: _lib.check(fn(
                     ctx, _lib.ptr(xs), n_img, Hi, Hi, Ci, _lib.ptr(ws), _lib.ptr(sc), _lib.ptr(sh), Co, k, stride,
                     pad, dil, _lib.ptr(r), Co, 1, _lib.ptr(y), Co, 0, bm, bn, ns, sp))
             return lambda: _lib.check(conv_fn(
@@ -166,8 +167,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--quick", action="store_true", help="old vs new automatic plan only")
     ap.add_argument("--out", default="conv_s_sweep.json")
-    ap.add_argument("--prec", type=int, default=3, choices=[0, 1, 3],
-                    help="3 = bf16x3 (x3s), 1 = plain bf16 (b16), 0 = exact fp32 on the LDS-DMA body (f32d)")
+    ap.add_argument("--prec", type=int, default=3, choices=[0, 1, 3, 6],
+                    help="3 = bf16x3 (x3s), 1 = plain bf16 (b16), 0 = exact fp32 on the LDS-DMA body (f32d), "
+                         "6 = fp32 width on bf16 MFMA (x6)")
     ap.add_argument("--vars", default="0,1,2,4", help="main-loop variants (0 base, 1 prefetch, 2 prefetch 8 waves, 4 128x128 two per CU; 8-11 timing study)")
     ap.add_argument("--only", default="", help="comma list of shape names (default: all)")
     args = ap.parse_args()
