@@ -129,6 +129,7 @@ struct ConvLayer {
   int Ci = 0, Co = 0, k = 1, stride = 1, pad = 0, dil = 1;
   float* w = nullptr;  // device, packed [Co][k][k][Ci] (stem conv1: [ci][ky][kx][co])
   __bf16* w_s = nullptr;   // S-layout [Co][K/32][hi 32 | lo 32] of the same split (conv_x3s.hip)
+  __bf16* w_l = nullptr;   // x6: the third term w - hi - lo, [Co][K/32][32] (exact in bf16)
   __bf16* w_b = nullptr;   // plain bf16 [Co][K], K in packed_k64 order (bf16 conv stack; Ci % 64 == 0)
   float* scale = nullptr;
   float* shift = nullptr;
@@ -455,11 +456,13 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
   int rc;
   if ((rc = upload(bb, packed, &L->w))) return rc;
   if (!stem1) {  // bf16x3 operands: hi = bf16_rne(w), lo = bf16_rne(w - hi)
-    std::vector<uint16_t> hi(packed.size()), lo(packed.size());
+    std::vector<uint16_t> hi(packed.size()), lo(packed.size()), lo3(packed.size());
     for (size_t i = 0; i < packed.size(); ++i) {
       const float v = packed[i];
       hi[i] = bf16_rne(v);
-      lo[i] = bf16_rne(v - bf16_to_float(hi[i]));
+      const float r = v - bf16_to_float(hi[i]);
+      lo[i] = bf16_rne(r);
+      lo3[i] = bf16_rne(r - bf16_to_float(lo[i]));  // exact: at most 8 significant bits remain
     }
     std::vector<uint16_t> sl(2 * packed.size());
     for (size_t r = 0; r < (size_t)Co; ++r)
@@ -470,6 +473,7 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
           sl[dst + 32] = lo[src];
         }
     if ((rc = upload_u16(bb, sl, &L->w_s))) return rc;
+    if (K % 32 == 0 && (rc = upload_u16(bb, lo3, &L->w_l))) return rc;  // [Co][K] = [Co][K/32][32]
     if (Ci % 64 == 0) {  // plain bf16 operand of the bf16 conv stack, K in packed_k64 order
       std::vector<uint16_t> b16(packed.size());
       for (int co = 0; co < Co; ++co)
@@ -853,7 +857,8 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
       memset(&sa, 0, sizeof(sa));
       const ConvCall& c = calls[i];
       sa.xs = (const __bf16*)c.x;  // (f32d: the fp32 NHWC map, the same 128-B line geometry)
-      sa.ws = b16 ? c.L->w_b : f32ops ? (const __bf16*)c.L->w : c.L->w_s;
+      sa.ws = b16 ? c.L->w_b : f32d ? (const __bf16*)c.L->w : c.L->w_s;  // x6: hi | mid (+ ws_lo)
+      sa.ws_lo = x6 ? c.L->w_l : nullptr;
       sa.zero = zero;
       sa.scale = a.scale;
       sa.shift = a.shift;
@@ -2411,6 +2416,15 @@ static int debug_conv_s(cwt_ctx* ctx, int prec, const void* xs, int N, int Hi, i
     const int kt = a.K / kb;
     p.kt_per_split = cdiv(kt, nsplit);
     p.nsplit = cdiv(kt, p.kt_per_split);
+  }
+  if (prec == 6) {  // the fp32 packed weights -> the x6 kernel's hi | mid line and lo plane
+    void *w3s, *w3l;
+    if ((rc = ensure_ws(ctx, "dbg.w3s", (size_t)Co * a.K * 4, &w3s)) ||
+        (rc = ensure_ws(ctx, "dbg.w3l", (size_t)Co * a.K * 2, &w3l)))
+      return rc;
+    if ((rc = launch_split_w3((const float*)ws, Co, a.K, (__bf16*)w3s, (__bf16*)w3l, (hipStream_t)stream))) return rc;
+    a.ws = (const __bf16*)w3s;
+    a.ws_lo = (const __bf16*)w3l;
   }
   void* part = nullptr;
   const size_t pf = (size_t)p.nsplit * a.M * a.Co;

@@ -144,15 +144,17 @@ __device__ __forceinline__ void store_out8(const ConvSArgs& a, int m, int co, co
   }
 }
 
-// PREC = 6 (conv_igemm_x6, the fp32-width path on the bf16 matrix cores): the exact-fp32 operands
-// (fp32 NHWC activations, fp32 packed weights: conv_igemm_f32d's bytes and LDS image) are split
-// in registers, after the fragment read, into three bf16 terms x = hi + mid + lo, EXACTLY:
-// hi = bf16_rne(x), mid = bf16_rne(x - hi), lo = x - hi - mid (|lo| <= 2^-16 |x|, at most 8
-// significant bits, so its bf16 conversion is exact).  a.b is summed from the six products whose
-// size is >= 2^-24 |a||b| (hi.hi, hi.mid, mid.hi, mid.mid, hi.lo, lo.hi) with fp32 accumulation;
-// the three dropped (mid.lo, lo.mid, lo.lo) total < 2^-23 |a||b|, the size of one fp32 rounding.
-// One v_mfma_f32_16x16x32_bf16 covers the whole 32-deep K-tile, so a fragment pair costs 6 x 16
-// cycles against the f32 MFMA's 8 x 32.
+// PREC = 6 (conv_igemm_x6, the fp32-width path on the bf16 matrix cores): every fp32 operand is
+// split EXACTLY into three bf16 terms x = hi + mid + lo: hi = bf16_rne(x), mid = bf16_rne(x - hi),
+// lo = x - hi - mid (|lo| <= 2^-16 |x|, at most 8 significant bits, so its bf16 conversion is
+// exact).  a.b is summed from the six products whose size is >= 2^-24 |a||b| (hi.hi, hi.mid,
+// mid.hi, mid.mid, hi.lo, lo.hi) with fp32 accumulation; the three dropped (mid.lo, lo.mid, lo.lo)
+// total < 2^-23 |a||b|, the size of one fp32 rounding.  One v_mfma_f32_16x16x32_bf16 covers the
+// whole 32-deep K-tile, so a fragment pair costs 6 x 16 cycles against the f32 MFMA's 8 x 32.
+// The activations stay fp32 NHWC (conv_igemm_f32d's bytes) and are split in registers after the
+// fragment read; the weights, static, are split once at load: the S-layout line [32 hi | 32 mid]
+// (the bf16x3 kernel's own packed weights) plus a lo plane [Co][K/32][32 lo] (64-B rows), both
+// moved to LDS by LDS-DMA, so the main loop's VALU splits only the A fragments.
 __device__ __forceinline__ void split3_bf16(const f32x4& x0, const f32x4& x1, bf16x8& h, bf16x8& m, bf16x8& l) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -182,8 +184,14 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int FM = WM / 16, FN = WN / 16;
   constexpr int LA = BM / (8 * NW), LB = BN / (8 * NW);  // LDS-DMA pieces (8 rows x 128 B) per wave per tile
-  constexpr int LPT = LA + LB;
-  constexpr int STG_BYTES = (BM + BN) * 128;
+  // PREC 6: the weights' lo plane, pieces of 16 rows x 64 B; with fewer pieces than waves the
+  // surplus waves repeat one (identical bytes to the same LDS slot), so every wave issues the same
+  // count per tile (the vmcnt accounting)
+  constexpr int NLO = PREC == 6 ? BN / 16 : 0;
+  constexpr int LBL = PREC == 6 ? (NLO + NW - 1) / NW : 0;
+  constexpr int LPT = LA + LB + LBL;
+  constexpr int LO_OFF = (BM + BN) * 128;  // the lo plane's place in a stage
+  constexpr int STG_BYTES = (BM + BN) * 128 + (PREC == 6 ? BN * 64 : 0);
   static_assert(LA * 8 * NW == BM && LB * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
   static_assert(NSTG >= 2 && NSTG <= 6, "ring depth");
   constexpr int EP_ROWS = WM < 32 ? WM : 32;
@@ -250,8 +258,8 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   // a row past M gets an offset past the buffer's end, which the hardware reads as zeros (no zero
   // line, no 64-bit address math, no exec-masked branch per piece).  The weights' K offset goes in
   // the uniform soffset.
-  __amdgpu_buffer_rsrc_t rsA, rsB;
-  int a_roff[LA], b_voff[LB];
+  __amdgpu_buffer_rsrc_t rsA, rsB, rsL;
+  int a_roff[LA], b_voff[LB], l_voff[LBL > 0 ? LBL : 1];
 #if defined(__HIP_DEVICE_COMPILE__)  // the buffer builtins exist for the device pass only
   if constexpr ((PF & 8) != 0) {
     const int cbl = a.Ci >> (PREC == 1 ? 6 : 5);
@@ -262,6 +270,18 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
     for (int j = 0; j < LA; ++j) a_roff[j] = (a_pix0[j] * cbl * 64 + a_ch[j]) * 2;
 #pragma unroll
     for (int j = 0; j < LB; ++j) b_voff[j] = b_off[j] * 2;
+    if constexpr (PREC == 6) {
+      // lo plane: piece q covers tile rows 16 q .. 16 q + 15; lane -> (row lane >> 2, LDS slot lane & 3)
+      // holding 16-B chunk slot ^ ((row >> 2) & 3) (conflict-free fragment reads, see read_frags)
+      rsL = __builtin_amdgcn_make_buffer_rsrc((void*)a.ws_lo, (short)0, (int)((long)a.Co * a.ktiles_total * 64),
+                                              0x00020000);
+#pragma unroll
+      for (int j = 0; j < LBL; ++j) {
+        const int q = (wv * LBL + j) % NLO;
+        const int r = q * 16 + (lane >> 2);
+        l_voff[j] = (n0 + r) * a.ktiles_total * 64 + (((lane & 3) ^ ((r >> 2) & 3)) << 4);
+      }
+    }
   }
 #endif
   auto issue = [&](int stg) {
@@ -282,6 +302,12 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       for (int j = 0; j < LB; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (CWT_LDS void*)(sb + BM * 128 + (wv * LB + j) * 1024), 16,
                                                  b_voff[j], i_kt * 128, 0, 0);
+      if constexpr (PREC == 6) {
+#pragma unroll
+        for (int j = 0; j < LBL; ++j)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsL, (CWT_LDS void*)(sb + LO_OFF + ((wv * LBL + j) % NLO) * 1024), 16,
+                                                   l_voff[j], i_kt * 64, 0, 0);
+      }
       ++i_kt;
       if (++i_kx == a.kw) {
         i_kx = 0;
@@ -323,15 +349,20 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   // fragment read geometry: lane -> row (lane & 15) of a 16-row block, k-chunk (lane >> 4)
   const int fr = lane & 15, fk = lane >> 4;
   const int swz = (fr >> 1) & 7;
-  // PREC 6: the lane's 8 fp32 k-values are 16-B chunks 2fk and 2fk+1 (k = 8fk .. 8fk+7, the k
-  // slots of its bf16 fragment); conflict-free like the others (rows fr, fr^1 share a swizzle
-  // but sit 128 B apart)
-  const int off_hi = fr * 128 + (((PREC == 6 ? 2 * fk : fk)) ^ swz) * 16;
-  const int off_lo = fr * 128 + (((PREC == 6 ? 2 * fk + 1 : 4 + fk)) ^ swz) * 16;
+  const int off_hi = fr * 128 + ((fk ^ swz) << 4);
+  const int off_lo = fr * 128 + (((4 + fk) ^ swz) << 4);
+  // PREC 6: an A lane's 8 fp32 k-values are 16-B chunks 2fk and 2fk+1 (k = 8fk .. 8fk+7, the k slots
+  // of its bf16 fragment and of the weights' hi / mid chunks fk, 4 + fk); conflict-free like the
+  // others (rows fr, fr^1 share a swizzle but sit 128 B apart).  The lo plane's 64-B rows: chunk fk
+  // of row fr sits in slot fk ^ ((fr >> 2) & 3), so a 16-lane group reads 16 distinct 16-B slots
+  const int off_a0 = PREC == 6 ? fr * 128 + (((2 * fk) ^ swz) << 4) : off_hi;
+  const int off_a1 = PREC == 6 ? fr * 128 + (((2 * fk + 1) ^ swz) << 4) : off_lo;
+  const int off_l = fr * 64 + ((fk ^ ((fr >> 2) & 3)) << 4);
   const int a_row0 = wm * WM, b_row0 = BM + wn * WN;
 
   struct Frags {
     bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+    bf16x8 bo[PREC == 6 ? FN : 1];  // PREC 6: the weights' lo term
   };
   auto read_frags = [&](Frags& F, int stg) {
     const char* sb = smem + stg * STG_BYTES;
@@ -344,8 +375,12 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const char* p = sb + (a_row0 + i * 16) * 128;
-      F.ah[i] = *(const bf16x8*)(p + off_hi);
-      F.al[i] = *(const bf16x8*)(p + off_lo);
+      F.ah[i] = *(const bf16x8*)(p + off_a0);
+      F.al[i] = *(const bf16x8*)(p + off_a1);
+    }
+    if constexpr (PREC == 6) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) F.bo[j] = *(const bf16x8*)(sb + LO_OFF + (wn * WN + j * 16) * 64 + off_l);
     }
   };
   auto mfmas = [&](const Frags& F) {
@@ -353,26 +388,22 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(F.ah[i]), "v"(F.al[i]));
 #pragma unroll
-      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(F.bh[j]), "v"(F.bl[j]));
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(F.bh[j]), "v"(F.bl[j]), "v"(F.bo[j < (PREC == 6 ? FN : 1) ? j : 0]));
       return;
     }
-    if constexpr (PREC == 6) {
-      bf16x8 bs[FN][3];
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        split3_bf16(__builtin_bit_cast(f32x4, F.bh[j]), __builtin_bit_cast(f32x4, F.bl[j]), bs[j][0], bs[j][1], bs[j][2]);
+    if constexpr (PREC == 6) {  // B: hi = bh, mid = bl, lo = bo (pre-split); A split here
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         bf16x8 ah, am, al;
         split3_bf16(__builtin_bit_cast(f32x4, F.ah[i]), __builtin_bit_cast(f32x4, F.al[i]), ah, am, al);
 #pragma unroll
         for (int j = 0; j < FN; ++j) {  // smallest products first
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bs[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bs[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bs[j][2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bs[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bs[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bs[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, F.bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, F.bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, F.bo[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, F.bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, F.bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, F.bh[j], acc[i][j], 0, 0, 0);
         }
       }
       return;
@@ -528,7 +559,11 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_f32d(ConvSAr
 // (PREC 6 above)
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x6(ConvSArgs a) {
-  conv_s_body<BM, BN, WAVES_M, WAVES_N, NSTG, 6, (PF | 8)>(a);
+  // a stage also holds the weights' lo plane: rings that would overflow the 160 KB of LDS lose a stage
+  constexpr int STG = (BM + BN) * 128 + BN * 64;
+  constexpr int NS = NSTG * STG <= 163840 ? NSTG : 163840 / STG;
+  static_assert(NS >= 2, "x6: a two-stage ring must fit in LDS");
+  conv_s_body<BM, BN, WAVES_M, WAVES_N, NS, 6, (PF | 8)>(a);
 }
 
 // Split-K reduction (fixed order, deterministic) + the same epilogue math.
@@ -588,6 +623,32 @@ __global__ void split_act_kernel(const float* x, long P, int C, int ld, __bf16* 
   __bf16* sp = out + (p * (C >> 5) + (c >> 5)) * 64 + (c & 31);
   *(bf16x8*)sp = hi;
   *(bf16x8*)(sp + 32) = lo;
+}
+
+// fp32 packed weights [R][K] (K % 32 == 0) -> the x6 kernel's two weight planes: the S-layout
+// line [R][K/32][32 hi | 32 mid] and the lo plane [R][K/32][32 lo] (hi = bf16_rne(w), mid =
+// bf16_rne(w - hi), lo = w - hi - mid, exact)
+__global__ void split_w3_kernel(const float* w, long n8, int K, __bf16* ws, __bf16* wl) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n8) return;
+  const long e = idx * 8;  // 8 consecutive k of one row
+  const long r = e / K;
+  const int k = (int)(e - r * K);
+  const f32x4 v0 = *(const f32x4*)(w + e), v1 = *(const f32x4*)(w + e + 4);
+  bf16x8 h, m, l;
+  split3_bf16(v0, v1, h, m, l);
+  __bf16* sp = ws + (r * (K >> 5) + (k >> 5)) * 64 + (k & 31);
+  *(bf16x8*)sp = h;
+  *(bf16x8*)(sp + 32) = m;
+  *(bf16x8*)(wl + (r * (K >> 5) + (k >> 5)) * 32 + (k & 31)) = l;
+}
+
+int launch_split_w3(const float* w, long R, int K, __bf16* ws, __bf16* wl, hipStream_t st) {
+  if (K % 32) return fail(CWT_EARG, "split_w3: K % 32");
+  const long n8 = R * K / 8;
+  hipLaunchKernelGGL(split_w3_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st, w, n8, K, ws, wl);
+  CWT_LAUNCH_CHECK();
+  return 0;
 }
 
 // S-layout -> fp32 (hi + lo), pixel stride ld
@@ -816,6 +877,7 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
     return fail(CWT_EARG, "conv precision must be 3 (bf16x3), 1 (bf16), 0 (exact fp32) or 6 (bf16x6)");
   if ((prec == 0 || prec == 6) && (a.ys || a.res_s || !a.y))
     return fail(CWT_EARG, "fp32-operand conv: fp32 output and residual only");
+  if (prec == 6 && !a.ws_lo) return fail(CWT_ESTATE, "x6 conv: the weights' lo plane is missing");
   if (!a.xs || !a.ws || !a.zero) return fail(CWT_ESTATE, "S-layout conv needs its input, weights and a zero line");
   const int kb = prec == 1 ? 64 : 32;
   if (a.Ci % kb || a.Co % 64 || a.Co % p.bn)

@@ -26,6 +26,7 @@ struct ConvArgs {
 struct ConvSArgs {
   const __bf16* xs;     // input, S-layout [N*Hi*Wi][Ci/32][64]
   const __bf16* ws;     // weights, S-layout [Co][K/32][64] (K in packed_k order)
+  const __bf16* ws_lo;  // x6 (prec 6): the weights' lo plane [Co][K/32][32] (ws holds hi | mid)
   const __bf16* zero;   // >= 128 B of zeros (padding taps, rows past M)
   const float* scale;   // [Co] folded BN scale
   const float* shift;   // [Co] folded BN shift
@@ -125,6 +126,7 @@ ConvPlan plan_conv_x6(int M, int Co, int K);
 int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, size_t part_ws_floats,
                     hipStream_t st, int prec = 3);
 int launch_split_act(const float* x, long P, int C, int ld, __bf16* out, hipStream_t st);
+int launch_split_w3(const float* w, long R, int K, __bf16* ws, __bf16* wl, hipStream_t st);
 int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipStream_t st);
 
 // inner loop (adapt.hip): cache of instantiated graphs of the 200-step launch sequence
