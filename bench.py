@@ -362,6 +362,84 @@ def main_pretrain(args, dev, rank, world, cdist):
         torch.distributed.destroy_process_group()
 
 
+def make_after(flat, opt, cdist, on_step=None):
+    """The training step's exchange point, run after each episode's CWT backward (SURVEY.md
+    §8(e); train.py:248-251 under DDP): the mean all-reduce of the flat gradient bucket over the
+    ranks, the identical SGD step everywhere, the gradient cleared.  on_step(flat) observes the
+    replica after each step (the CPU stand-in's digest)."""
+    def after():
+        cdist.all_reduce_mean_(flat.grad)
+        opt.step()
+        flat.grad.zero_()
+        if on_step is not None:
+            on_step(flat)
+    return after
+
+
+def timed_region(run_steps, sync, cdist):
+    """barrier + sync on both sides of the K timed steps; the max over ranks of the wall time."""
+    cdist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    out = run_steps()
+    sync()
+    cdist.barrier()
+    return cdist.all_reduce_max_scalar(time.perf_counter() - t0), out
+
+
+class CpuStandinTrainEngine:
+    """Test hook (CWT_BENCH_CPU_STANDIN=1, tests/test_bench_launch.py): the --train step's episode
+    replaced by a seeded CPU stand-in, so bench.py's own multi-rank path (process group, per-rank
+    episodes, make_after's all-reduce + SGD, timed_region's max-over-ranks clock, the JSON line)
+    runs under gloo without a device.  The stand-in's gradient depends on the rank's episode and
+    on the current parameters, as the real CWT gradient does."""
+
+    def __init__(self, flat: torch.Tensor):
+        self.flat = flat
+
+    def step(self, seed: int):
+        g = torch.Generator().manual_seed(seed)
+        noise = torch.randn(self.flat.shape, generator=g)
+        with torch.no_grad():
+            self.flat.grad = 0.01 * self.flat.detach() + noise
+        return {"loss": torch.tensor(float(noise[:64].square().mean()))}
+
+
+def main_cpu_standin(args, rank, world, cdist):
+    """bench.py --train on the CPU stand-in episode (see CpuStandinTrainEngine)."""
+    import hashlib
+    if not args.train:
+        raise SystemExit("CWT_BENCH_CPU_STANDIN covers --train only")
+    n = 4 * 512 * 512 + 4 * 512 + 2 * 512   # a CWT-sized flat bucket (w_qkvs + layer norm + fc, H = 4)
+    flat = torch.zeros(n).uniform_(-0.05, 0.05, generator=torch.Generator().manual_seed(2021 + rank))
+    flat.requires_grad_(True)
+    cdist.broadcast_params_(flat)                 # DDP's start-of-training broadcast
+    opt = torch.optim.SGD([flat], lr=0.0025, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    digests = []
+    after = make_after(flat, opt, cdist, lambda f: digests.append(
+        hashlib.sha256(f.detach().numpy().tobytes()).hexdigest()[:16]))
+    eng = CpuStandinTrainEngine(flat)
+
+    def step(i):
+        r = eng.step(rank * 1000 + i)   # each rank its own episodes
+        after()
+        return r["loss"]
+
+    for i in range(args.warmup):
+        step(i)
+    dt, losses = timed_region(lambda: [step(args.warmup + i) for i in range(args.steps)], lambda: None, cdist)
+    print(json.dumps({"rank": rank, "digests": digests, "dt_max": dt}), flush=True)
+    if rank == 0:
+        print(json.dumps({"metric": f"training episodes/sec ({args.size}x{args.size}, {args.shot}-shot, "
+                                    f"R{args.layers}) [CPU stand-in episode]",
+                          "value": round(world * args.steps / dt, 6), "unit": "training episodes/s",
+                          "n_gpus": cdist.rank_world()[1], "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(dt / args.steps * 1e3, 6), "data": "cpu stand-in (test hook)",
+                          "loss_last": float(losses[-1])}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -413,6 +491,8 @@ def main():
     rank, local, world = cdist.init_from_env()
     if world != args.gpus:
         raise SystemExit(f"process group has {world} ranks, --gpus asks for {args.gpus}")
+    if os.environ.get("CWT_BENCH_CPU_STANDIN") == "1":   # multi-rank path without a device (tests)
+        return main_cpu_standin(args, rank, world, cdist)
     if os.environ.get("CWT_BENCH_DRYRUN"):   # launch check without a device (tests/test_bench_launch.py)
         tot = cdist.all_reduce_sum_np(np.array([1.0]))[0]
         print(json.dumps({"rank": rank, "world": world, "ranks_seen": int(tot)}), flush=True)
@@ -469,10 +549,7 @@ def main():
     def step(i: int, Wbuf, last: bool = False):
         imgs, sl, ql = pool[i % len(pool)]
         if args.train:   # do_epoch iteration (train.py:188-267 + the all-reduce point of SURVEY §8(e))
-            def after():
-                cdist.all_reduce_mean_(trans.flat.grad)
-                opt.step()
-                trans.flat.grad.zero_()
+            after = make_after(trans.flat, opt, cdist)
             if pipe is not None:
                 r = pipe.submit_train(tengine, imgs, sl[0], ql, Wbuf[0], after)
             else:
@@ -493,17 +570,18 @@ def main():
     torch.cuda.synchronize()
 
     _lib.profile_enable(1)   # coarse: phases + bottleneck conv (no per-launch event gaps)
-    cdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    iuts = [step(s, W0[args.warmup + s], last=s == args.steps - 1) for s in range(args.steps)]
-    t_sub = time.perf_counter()   # the host has enqueued every step (a diagnostic of host-boundness)
-    if pipe is not None:
-        pipe.wait()
-    torch.cuda.synchronize()
-    cdist.barrier()
-    t1 = time.perf_counter()
-    dt = cdist.all_reduce_max_scalar(t1 - t0)
+    t_marks = {}
+
+    def run_steps():
+        t_marks["t0"] = time.perf_counter()
+        out = [step(s, W0[args.warmup + s], last=s == args.steps - 1) for s in range(args.steps)]
+        t_marks["sub"] = time.perf_counter()   # the host has enqueued every step (host-boundness diagnostic)
+        if pipe is not None:
+            pipe.wait()
+        return out
+
+    dt, iuts = timed_region(run_steps, torch.cuda.synchronize, cdist)
+    t0, t_sub = t_marks["t0"], t_marks["sub"]
     value = world * args.steps * E / dt
     seq = None
     recs = _lib.profile_records()
@@ -584,6 +662,7 @@ def main():
     n_at, _, at_ms = total("attention")       # the module-by-module CWT (CWT_FUSED_TAIL=0)
     n_tl, _, tl_ms = total("post_loop_tail")  # the one-launch tail (CWT + classifier + metrics)
     n_tk, _, tk_ms = total("episode_tail_kernel")
+    tk_sel = [r for r in recs if r[0].startswith("episode_tail_kernel")]
     dom = [r for r in recs if r[0].startswith("conv_igemm")]     # the bottleneck conv (level 1 records only it)
     dom_name = dom[0][0].split(" ")[0] if dom else "n/a"
     dn, dfl, dms = len(dom), sum(r[1] for r in dom), sum(r[3] for r in dom)
@@ -695,6 +774,36 @@ def main():
                                       "close the measured loop is to ITS floor (the byte frac above prices it as "
                                       "a bandwidth kernel, which it is not)")
         _lib.check_status()
+
+    # ---- the post-loop tail: normalize + pred_q0 + CWT + classifier + both
+    # metrics in one launch, priced as the HBM pass it is (algorithmic bytes: f_q read for the
+    # norms and again for the CWT / classifier, the CWT weights once, labels + 8-B IoU traffic per
+    # pixel) beside the reference formulation's FLOPs (transformer.py:54-83 as written) ----
+    tail_roofline = None
+    if tk_sel:
+        tk_launch_ms = sum(r[3] for r in tk_sel) / len(tk_sel)
+        tk_bytes = sum(r[2] for r in tk_sel) / len(tk_sel)
+        hw_ = h_feat * h_feat
+        exec_fl = E * (2.0 * 2 * 4 * hw_ * 512 * 2 + 2.0 * 2 * hw_ * 512 * 2)   # scores + A.f per head, 2 classifiers
+        ref_fl = reference_cwt_flops(hw_) * E
+        tk_traffic, tk_traffic_src = pmc_traffic("episode_tail_kernel")
+        tail_roofline = {
+            "bound": "hbm", "kernel": "episode_tail_kernel (cwt_episode_tail, one launch per episode)",
+            "avg_launch_ms": round(tk_launch_ms, 4), "launches": len(tk_sel),
+            "algorithmic_bytes_per_launch": round(tk_bytes),
+            "achieved": round(tk_bytes / (tk_launch_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+            "frac": round(tk_bytes / (tk_launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+            "traffic": tk_traffic, "traffic_unit": "bytes/launch", "traffic_source": tk_traffic_src,
+            "executed_flops_per_launch": exec_fl,
+            "reference_formulation_flops_per_launch": ref_fl,
+            "reference_formulation_tflops": round(ref_fl / (tk_launch_ms * 1e-3) / 1e12, 2),
+            "reference_formulation_frac_of_fp32_mfma": round(ref_fl / (tk_launch_ms * 1e-3) / 1e12
+                                                             / PEAK_FP32_MFMA_TFLOPS, 4),
+            "measured_in": "the timed region (pipelined: launched on the adapt stream while the next episodes' "
+                           "extractor passes hold most CUs)",
+            "note": "the CWT runs re-associated (DESIGN.md §3): scores = f . (W_k^T q') and W_v (sum_j a_j f_j) -- "
+                    "token work of ~59 MFLOP instead of projecting every token (15.1 GFLOP as written); the kernel "
+                    "is latency-bound (grid barriers between its phases), so both fractions are small"}
 
     # ---- other conv arithmetics through the same episodes and pipeline (cwt_ctx_set_conv_arith on
     # every extractor context): exact_fp32 = v_mfma_f32 (157.3 TF roof), bf16x3 = the declared
@@ -862,6 +971,7 @@ def main():
             "attention": {"ms_per_step": round(at_ms / args.steps, 3),
                           "gflop_reference_formulation_per_step": round(reference_cwt_flops(h_feat * h_feat) * E / 1e9, 2),
                           "note": "executed in the declared re-associated form (DESIGN.md §3, ~59 MFLOP of token work)"}},
+        "tail_roofline": tail_roofline,
         "iou_fg_timed": None if args.train else round(float((iu[0, 1] / iu[1, 1].clamp_min(1)).item()), 4),
         "sequential": seq,
         "host_submit_ms_per_step": round((t_sub - t0) / args.steps * 1e3, 3),
