@@ -130,6 +130,10 @@ struct ConvLayer {
   float* w = nullptr;  // device, packed [Co][k][k][Ci] (stem conv1: [ci][ky][kx][co])
   __bf16* w_s = nullptr;   // S-layout [Co][K/32][hi 32 | lo 32] of the same split (conv_x3s.hip)
   __bf16* w_l = nullptr;   // x6: the third term w - hi - lo, [Co][K/32][32] (exact in bf16)
+  // x6 Winograd F(2x2,3x3) (stride-1 3x3, Ci >= 256; wino.hip): U = G g G^T per transformed
+  // position, [16][Co][Ci] split like w_s / w_l
+  __bf16* wino_s = nullptr;
+  __bf16* wino_l = nullptr;
   __bf16* w_b = nullptr;   // plain bf16 [Co][K], K in packed_k64 order (bf16 conv stack; Ci % 64 == 0)
   float* scale = nullptr;
   float* shift = nullptr;
@@ -474,6 +478,26 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
         }
     if ((rc = upload_u16(bb, sl, &L->w_s))) return rc;
     if (K % 32 == 0 && (rc = upload_u16(bb, lo3, &L->w_l))) return rc;  // [Co][K] = [Co][K/32][32]
+    // the Winograd form's transformed weights: stride-1 3x3 layers with Ci >= 256 (at Ci = 128 the
+    // 16 thin GEMMs and the transforms measured slower than the direct conv: 35.9 vs 29.1 us,
+    // profiles/r5/sweeps)
+    if (k == 3 && stride == 1 && Ci >= 256 && Ci % 32 == 0) {
+      const size_t n = (size_t)16 * Co * Ci;
+      void *U = nullptr, *us = nullptr, *ul = nullptr;
+      CWT_HIP(hipMalloc(&us, n * 4));
+      bb->allocs.push_back(us);
+      CWT_HIP(hipMalloc(&ul, n * 2));
+      bb->allocs.push_back(ul);
+      CWT_HIP(hipMalloc(&U, n * 4));
+      rc = launch_wino_weights(L->w, Co, Ci, (float*)U, nullptr);
+      if (!rc) rc = launch_split_w3((const float*)U, 16L * Co, Ci, (__bf16*)us, (__bf16*)ul, nullptr);
+      const hipError_t e = hipDeviceSynchronize();
+      (void)hipFree(U);
+      if (rc) return rc;
+      if (e != hipSuccess) return fail((int)e, "winograd weight transform");
+      L->wino_s = (__bf16*)us;
+      L->wino_l = (__bf16*)ul;
+    }
     if (Ci % 64 == 0) {  // plain bf16 operand of the bf16 conv stack, K in packed_k64 order
       std::vector<uint16_t> b16(packed.size());
       for (int co = 0; co < Co; ++co)
@@ -652,6 +676,59 @@ static ConvArgs make_args(const ConvCall& c) {
   return a;
 }
 
+// One stride-1 3x3 conv (dilation d = padding) in the Winograd form on the x6 matrix-core
+// arithmetic (wino.hip): input transform -> 16 batched GEMMs (conv_igemm_x6, batch 16) -> output
+// transform with the conv's BN / residual / ReLU.  us / ul: the layer's wino_s / wino_l; bm > 0
+// overrides the GEMMs' tile (bm = 1000 * variant + rows, as cwt_debug_conv_s).
+static int run_wino_conv(cwt_ctx* ctx, const float* x, int N, int H, int W, int Ci, int Co, int d, const __bf16* us,
+                         const __bf16* ul, const float* scale, const float* shift, const float* res, int res_ld,
+                         int relu, float* y, int y_ld, int y_off, int stage, hipStream_t st, int bm = 0, int bn = 0) {
+  const WinoGeom g = wino_geom(N, H, W, d);
+  if (g.T * Ci * 4 >= (1L << 31) || g.T * Co * 4 >= (1L << 31)) return fail(CWT_EARG, "winograd: plane too large");
+  void *V, *Mb;
+  const __bf16* zero = nullptr;
+  int rc;
+  if ((rc = ensure_ws(ctx, "wino.V", (size_t)16 * g.T * Ci * 4, &V)) ||
+      (rc = ensure_ws(ctx, "wino.M", (size_t)16 * g.T * Co * 4, &Mb)) || (rc = zero_line(ctx, &zero)))
+    return rc;
+  if ((rc = launch_wino_in(x, g, Ci, (float*)V, st))) return rc;
+  ConvSArgs a;
+  memset(&a, 0, sizeof(a));
+  a.xs = (const __bf16*)V;
+  a.ws = us;
+  a.ws_lo = ul;
+  a.zero = zero;
+  a.scale = scale;
+  a.shift = shift;
+  a.N = 1;
+  a.Hi = (int)g.T;
+  a.Wi = 1;
+  a.Ci = Ci;
+  a.Ho = (int)g.T;
+  a.Wo = 1;
+  a.Co = Co;
+  a.kh = a.kw = 1;
+  a.stride = 1;
+  a.pad = 0;
+  a.dil = 1;
+  a.M = (int)g.T;
+  a.K = Ci;
+  a.part = (float*)Mb;
+  a.batch = 16;
+  a.xs_bstride = g.T * Ci * 4;
+  a.ws_bstride = (long)Co * Ci * 2;
+  a.wl_bstride = (long)Co * Ci;
+  ConvPlan p = plan_conv_x6_batched(a.M, Co, Ci, 16);
+  if (bm > 0) {
+    p.var = bm / 1000;
+    p.bm = bm % 1000;
+    p.bn = bn;
+    if (Co % p.bn) return fail(CWT_EARG, "winograd GEMM tile: Co % bn");
+  }
+  if ((rc = launch_conv_x3s(a, p, stage, nullptr, 0, st, 6))) return rc;
+  return launch_wino_out((const float*)Mb, g, Co, scale, shift, res, res_ld, relu, y, y_ld, y_off, st);
+}
+
 // Training-mode BN of one extraction (cwt_extract_features_train_bn; bn_train.hip)
 struct TrainBn {
   float momentum, drop_p;
@@ -823,6 +900,11 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     if ((rc = ensure_ws(ctx, "bb.PART", part_floats * 4, &p))) return rc;
     PART = (float*)p;
   }
+  // the Winograd form: stride-1 3x3 layers whose transformed weights were built at load, on
+  // images of a pixel stride equal to their channels
+  auto c_wino = [&](const ConvCall& c) {
+    return c.L->wino_s && c.L->k == 3 && c.L->stride == 1 && c.L->pad == c.L->dil && c.x_ld == c.L->Ci;
+  };
   auto run_call = [&](size_t i) -> int {
     ConvArgs a = make_args(calls[i]);
     // training-mode BN: raw conv (scale 1, shift 0); the bottleneck keeps its residual (the
@@ -834,7 +916,11 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
       a.relu = 0;
       if (!keep_res) a.res = nullptr;
     }
-    const ConvPlan& pl = plans[i];
+    static const bool wino_env = !(getenv("CWT_WINO") && getenv("CWT_WINO")[0] == '0');  // A/B: 0 = direct
+    const bool wino = x6 && wino_env && c_wino(calls[i]);
+    // the Winograd form's record names its batched GEMM's plan; its FLOPs stay the direct conv's
+    // (algorithmic: the roofline prices the conv, not the form that computes it)
+    const ConvPlan pl = wino ? plan_conv_x6_batched((int)wino_geom(a.N, a.Hi, a.Wi, a.dil).T, a.Co, a.Ci, 16) : plans[i];
     const double flops = 2.0 * a.M * a.Co * a.K;
     // algorithmic bytes: every operand once; 4 B per element (fp32 or the bf16x3 S-layout),
     // 2 B for the bf16 stack's activations and weights (its fp32 bottleneck output: 4 B)
@@ -842,8 +928,8 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     const double bytes = eb * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K) +
                          ob * ((double)a.M * a.Co + (a.res ? (double)a.M * a.Co : 0.0));
     Prof p(ctx, st,
-           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : x6 ? "conv_igemm_x6<"
-                       : f32d ? "conv_igemm_f32d<" : "conv_igemm_f32<") +
+           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : wino ? "conv_igemm_x6w<"
+                       : x6 ? "conv_igemm_x6<" : f32d ? "conv_igemm_f32d<" : "conv_igemm_f32<") +
                std::to_string(pl.bm) + "," +
                std::to_string(pl.bn) + "," +
                std::to_string(calls[i].stage) + ">" +
@@ -852,7 +938,11 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
                std::to_string(a.stride) + "d" + std::to_string(a.dil) + "@" + std::to_string(a.Ho),
            flops, bytes, calls[i].stage == 6 ? 1 : 2);
     int r;
-    if (dma) {
+    if (wino) {
+      const ConvCall& c = calls[i];
+      r = run_wino_conv(ctx, c.x, a.N, a.Hi, a.Wi, a.Ci, a.Co, a.dil, c.L->wino_s, c.L->wino_l, a.scale, a.shift,
+                        a.res, c.res_ld, a.relu, c.y, c.y_ld, c.y_off, c.stage, st);
+    } else if (dma) {
       ConvSArgs sa;
       memset(&sa, 0, sizeof(sa));
       const ConvCall& c = calls[i];
@@ -2456,6 +2546,33 @@ int cwt_debug_conv_x6(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int C
                       int nsplit, void* stream) {
   return debug_conv_s(ctx, 6, x, N, Hi, Wi, Ci, w_packed, scale, shift, Co, k, stride, pad, dil, res, res_ld, nullptr,
                       relu, y, y_ld, y_off, nullptr, bm, bn, nsplit, stream);
+}
+
+int cwt_debug_conv_x6w(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, const float* w_packed,
+                       const float* scale, const float* shift, int Co, int k, int stride, int pad, int dil,
+                       const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
+                       int nsplit, void* stream) {
+  (void)nsplit;
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(x && w_packed && scale && shift && y, "null buffer");
+  CWT_CHECK(k == 3 && stride == 1 && pad == dil && dil >= 1, "winograd form: 3x3, stride 1, padding = dilation");
+  CWT_CHECK(Ci % 32 == 0 && Co % 64 == 0 && N >= 1 && Hi >= 1 && Wi >= 1, "need Ci % 32 == 0, Co % 64 == 0");
+  CWT_CHECK(y_ld >= y_off + Co && y_ld % 4 == 0 && y_off % 4 == 0 && (!res || res_ld % 4 == 0), "bad strides");
+  CWT_CHECK(bm == 0 || ((bm % 1000 == 256 || bm % 1000 == 128 || bm % 1000 == 64) && (bn == 256 || bn == 128 || bn == 64)),
+            "bad tile");
+  CWT_HIP(hipSetDevice(ctx->device));
+  const hipStream_t st = (hipStream_t)stream;
+  const size_t n = (size_t)16 * Co * Ci;
+  void *U, *us, *ul;
+  int rc;
+  if ((rc = ensure_ws(ctx, "dbg.wU", n * 4, &U)) || (rc = ensure_ws(ctx, "dbg.wUs", n * 4, &us)) ||
+      (rc = ensure_ws(ctx, "dbg.wUl", n * 2, &ul)))
+    return rc;
+  if ((rc = launch_wino_weights(w_packed, Co, Ci, (float*)U, st)) ||
+      (rc = launch_split_w3((const float*)U, 16L * Co, Ci, (__bf16*)us, (__bf16*)ul, st)))
+    return rc;
+  return run_wino_conv(ctx, x, N, Hi, Wi, Ci, Co, dil, (const __bf16*)us, (const __bf16*)ul, scale, shift, res, res_ld,
+                       relu, y, y_ld, y_off, 0, st, bm, bn);
 }
 
 int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws, const float* scale,

@@ -206,6 +206,14 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   const int wm = wv / WAVES_N, wn = wv % WAVES_N;
   int mt, nt, ks;
   conv_tile_coords(mt, nt, ks);
+  // batched GEMMs (PREC 6, the Winograd products): grid.z = batch, one whole K range each
+  const bool batched = PREC == 6 && a.batch > 1;
+  const int bidx = batched ? ks : 0;
+  if (batched) ks = 0;
+  const char* xs_b = (const char*)a.xs + (batched ? bidx * a.xs_bstride : 0L);
+  const __bf16* ws_b = a.ws + (batched ? bidx * a.ws_bstride : 0L);
+  const __bf16* wl_b = a.ws_lo + (batched ? bidx * a.wl_bstride : 0L);
+  float* part_b = a.part + (batched ? (long)bidx * a.M * a.Co : 0L);
   const int m0 = mt * BM, n0 = nt * BN;
   const int kt_begin = ks * a.kt_per_split;
   const int kt_end = min(a.ktiles, kt_begin + a.kt_per_split);
@@ -264,8 +272,8 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   if constexpr ((PF & 8) != 0) {
     const int cbl = a.Ci >> (PREC == 1 ? 6 : 5);
     const long a_bytes = (long)a.N * a.Hi * a.Wi * cbl * 128;
-    rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.xs, (short)0, (int)a_bytes, 0x00020000);
-    rsB = __builtin_amdgcn_make_buffer_rsrc((void*)a.ws, (short)0, (int)((long)a.Co * a.ktiles_total * 128), 0x00020000);
+    rsA = __builtin_amdgcn_make_buffer_rsrc((void*)xs_b, (short)0, (int)a_bytes, 0x00020000);
+    rsB = __builtin_amdgcn_make_buffer_rsrc((void*)ws_b, (short)0, (int)((long)a.Co * a.ktiles_total * 128), 0x00020000);
 #pragma unroll
     for (int j = 0; j < LA; ++j) a_roff[j] = (a_pix0[j] * cbl * 64 + a_ch[j]) * 2;
 #pragma unroll
@@ -273,7 +281,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
     if constexpr (PREC == 6) {
       // lo plane: piece q covers tile rows 16 q .. 16 q + 15; lane -> (row lane >> 2, LDS slot lane & 3)
       // holding 16-B chunk slot ^ ((row >> 2) & 3) (conflict-free fragment reads, see read_frags)
-      rsL = __builtin_amdgcn_make_buffer_rsrc((void*)a.ws_lo, (short)0, (int)((long)a.Co * a.ktiles_total * 64),
+      rsL = __builtin_amdgcn_make_buffer_rsrc((void*)wl_b, (short)0, (int)((long)a.Co * a.ktiles_total * 64),
                                               0x00020000);
 #pragma unroll
       for (int j = 0; j < LBL; ++j) {
@@ -524,7 +532,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       const int m = mrow + pass * EP_ROWS + rr * RPR;
       if (m < a.M) {
         if (!fused) {
-          f32x4* pp = (f32x4*)(a.part + ((long)ks * a.M + m) * a.Co + co);
+          f32x4* pp = (f32x4*)(part_b + ((long)ks * a.M + m) * a.Co + co);
           pp[0] = v0[rr];
           pp[1] = v1[rr];
         } else {
@@ -856,6 +864,36 @@ ConvPlan plan_conv_x6(int M, int Co, int K) {
   return plan_heuristic_s(M, Co, ktiles);
 }
 
+// The Winograd path's 16 batched GEMMs [M = tiles][K = Ci] x [Ci][Co]: the measured table (keyed
+// like the direct convs; tile counts M never collide with them), else the largest tile giving
+// >= 200 workgroups over the whole batch, no split-K
+ConvPlan plan_conv_x6_batched(int M, int Co, int K, int batch) {
+  const int ktiles = K / 32;
+  for (const MeasuredPlanS& e : kMeasuredPlansX6)
+    if (e.M == M && e.Co == Co && e.K == K && e.bn > 0 && Co % e.bn == 0 && e.nsplit == 1) {
+      ConvPlan p;
+      p.bm = e.bm;
+      p.bn = e.bn;
+      p.var = e.var;
+      p.kt_per_split = ktiles;
+      p.nsplit = 1;
+      return p;
+    }
+  static const int cand[7][2] = {{256, 256}, {256, 128}, {128, 256}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  ConvPlan best;
+  for (auto& c : cand) {
+    if (Co % c[1] != 0) continue;
+    ConvPlan p;
+    p.bm = c[0];
+    p.bn = c[1];
+    p.kt_per_split = ktiles;
+    p.nsplit = 1;
+    best = p;
+    if ((long)cdiv(M, c[0]) * (Co / c[1]) * batch >= 200) return p;
+  }
+  return best;
+}
+
 template <int PREC>
 static void launch_splitk_s(const ConvSArgs& a, int nsplit, hipStream_t st) {
   const long n = (long)a.M * (a.Co / 8);
@@ -875,8 +913,11 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
                     hipStream_t st, int prec) {
   if (prec != 0 && prec != 1 && prec != 3 && prec != 6)
     return fail(CWT_EARG, "conv precision must be 3 (bf16x3), 1 (bf16), 0 (exact fp32) or 6 (bf16x6)");
-  if ((prec == 0 || prec == 6) && (a.ys || a.res_s || !a.y))
+  const bool batched = prec == 6 && a.batch > 1;
+  if ((prec == 0 || prec == 6) && (a.ys || a.res_s || (!a.y && !batched)))
     return fail(CWT_EARG, "fp32-operand conv: fp32 output and residual only");
+  if (batched && (p.nsplit != 1 || !a.part || a.kh != 1 || a.kw != 1))
+    return fail(CWT_EARG, "batched x6 GEMMs: 1x1, no split-K, raw output to part");
   if (prec == 6 && !a.ws_lo) return fail(CWT_ESTATE, "x6 conv: the weights' lo plane is missing");
   if (!a.xs || !a.ws || !a.zero) return fail(CWT_ESTATE, "S-layout conv needs its input, weights and a zero line");
   const int kb = prec == 1 ? 64 : 32;
@@ -889,13 +930,15 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
   const int nsplit = p.nsplit;
   if (nsplit < 1 || (long)p.kt_per_split * nsplit < a.ktiles) return fail(CWT_EARG, "conv plan does not cover K");
   ConvSArgs main = a;
-  if (nsplit > 1) {
+  if (batched) {
+    // main.part: the caller's [batch][M][Co] output
+  } else if (nsplit > 1) {
     if ((size_t)nsplit * a.M * a.Co > part_ws_floats) return fail(CWT_ESTATE, "split-K workspace too small");
     main.part = part_ws;
   } else {
     main.part = nullptr;
   }
-  dim3 grid(cdiv(a.M, p.bm), a.Co / p.bn, nsplit);
+  dim3 grid(cdiv(a.M, p.bm), a.Co / p.bn, nsplit * (batched ? a.batch : 1));
   if (prec == 6) {
     switch (stage) {
       case 0: launch_tiles_conv_igemm_x6<0>(main, p, grid, st); break;
@@ -938,7 +981,7 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
     }
   }
   CWT_LAUNCH_CHECK();
-  if (nsplit > 1) {
+  if (nsplit > 1 && !batched) {
     main.part = part_ws;
     if (prec == 1)
       launch_splitk_s<1>(main, nsplit, st);

@@ -40,6 +40,11 @@ struct ConvSArgs {
   int M, K, ktiles, ktiles_total, kt_per_split;
   int y_ld, y_off, res_ld;
   int relu;
+  // batched GEMMs (x6 only; the Winograd path's 16 products): grid.z = batch, GEMM b reads
+  // xs + b * xs_bstride BYTES, ws / ws_lo + b * ws_bstride / wl_bstride elements and writes its raw
+  // sums to part + b * M * Co (no epilogue); batch <= 1: off
+  int batch;
+  long xs_bstride, ws_bstride, wl_bstride;
 };
 
 // Conv weights are packed [Co][K] with K ordered (32-channel block, tap, channel in block):
@@ -119,6 +124,18 @@ ConvPlan plan_conv_x3s(int M, int Co, int K);
 ConvPlan plan_conv_b16(int M, int Co, int K);
 ConvPlan plan_conv_f32d(int M, int Co, int K);
 ConvPlan plan_conv_x6(int M, int Co, int K);
+ConvPlan plan_conv_x6_batched(int M, int Co, int K, int batch);
+// Winograd F(2x2, 3x3) for the x6 path's stride-1 3x3 convs (wino.hip)
+struct WinoGeom {
+  int N, H, W, d;  // image, dilation (= padding)
+  int TY, TX;      // 2x2 output tiles per dilation sub-grid
+  long T;          // N * d * d * TY * TX
+};
+WinoGeom wino_geom(int N, int H, int W, int d);
+int launch_wino_weights(const float* w_packed, int Co, int Ci, float* U, hipStream_t st);
+int launch_wino_in(const float* x, const WinoGeom& g, int Ci, float* V, hipStream_t st);
+int launch_wino_out(const float* Mb, const WinoGeom& g, int Co, const float* scale, const float* shift, const float* res,
+                    int res_ld, int relu, float* y, int y_ld, int y_off, hipStream_t st);
 // prec 3: bf16x3 (S-layout operands); prec 1: plain bf16 (NHWC bf16 activations, [Co][K]
 // bf16 weights with K ordered (64-channel block, tap, channel): packed_k64); prec 0: exact fp32
 // (f32 MFMA) and prec 6: fp32 width on the bf16 MFMA (three-way register split), both over fp32

@@ -70,6 +70,15 @@ int cwt_debug_conv_x6(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int C
                       const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
                       int nsplit, void* stream);
 
+/* The same conv in the Winograd F(2x2, 3x3) form on the x6 arithmetic (wino.hip; the form the
+ * x6 stack takes for stride-1 3x3 layers with Ci >= 256): k == 3, stride 1, pad == dil; the weights
+ * are transformed and split on the device each call; bm / bn pick the 16 batched GEMMs' tile
+ * (nsplit ignored: the batch fills the chip). */
+int cwt_debug_conv_x6w(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int Ci, const float* w_packed,
+                       const float* scale, const float* shift, int Co, int k, int stride, int pad, int dil,
+                       const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
+                       int nsplit, void* stream);
+
 /* One CenterPivotConv4d layer + ReLU (src/model/conv4d.py:40-62) on the channels-last 4-D
  * tensor x [B][hA*wA][hB*wB][cin] -> y [B][hA*wA][hB*wB][cout]: Wa / Wb [cout][cin][3][3] the
  * a-plane / b-plane filters, ba / bb their biases.  variant 0: the library's kernel choice, 1:

@@ -346,3 +346,51 @@ def test_conv_x6_channel_strided_out():
     y = run_conv_f32d(x, w, scale, shift, 1, 1, 1, None, relu=False, y_pad=256, y_off=128, entry="cwt_debug_conv_x6")
     ref = ref_conv(x, w, scale, shift, 1, 1, 1, None, False)
     assert float((y.double() - ref).abs().max() / ref.abs().max()) < TOL_X6
+
+
+# ---------------------------------------------------------------- x6 Winograd F(2x2, 3x3) (wino.hip)
+# the x6 stack's form for stride-1 3x3 convs: transforms in fp32 (+-1 coefficients; G g G^T in
+# double, rounded once), 16 batched x6 GEMMs; against float64 at the same bar as the direct x6
+WINO_CASES = [  # N, Ci, Co, Hi, dil, residual
+    (2, 64, 64, 37, 1, False),
+    (2, 128, 128, 15, 1, True),
+    (1, 128, 64, 13, 2, False),     # H not a multiple of 2d: ragged sub-grids (7 and 6 rows)
+    (2, 256, 256, 15, 2, True),
+    (1, 512, 128, 13, 4, False),
+    (1, 256, 64, 9, 4, True),       # sub-grids of 3 and 2 rows: half-empty edge tiles
+    (1, 64, 512, 19, 1, True),
+]
+WINO_TILES = [(0, 0), (256, 256), (256, 128), (128, 256), (128, 128), (128, 64), (64, 128), (64, 64), (4128, 128),
+              (1064, 64), (2128, 128)]
+
+
+@pytest.mark.parametrize("case", WINO_CASES, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("tile", WINO_TILES, ids=lambda p: f"{p[0]}x{p[1]}")
+def test_conv_x6_winograd(case, tile):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    N, Ci, Co, Hi, dil, has_res = case
+    bm, bn = tile
+    if bn and Co % bn:
+        pytest.skip("Co not a multiple of the tile")
+    tag = f"w{N}_{Ci}_{Co}_{Hi}_{dil}"
+    x = torch.from_numpy(syn.normal(1, "x" + tag, (N, Ci, Hi, Hi), 1.0))
+    w = torch.from_numpy(syn.normal(1, "w" + tag, (Co, Ci, 3, 3), (2.0 / (Ci * 9)) ** 0.5))
+    scale = torch.from_numpy(syn.uniform(1, "s" + tag, (Co,), 0.5, 1.5))
+    shift = torch.from_numpy(syn.normal(1, "b" + tag, (Co,), 0.1))
+    res = torch.from_numpy(syn.normal(1, "r" + tag, (N, Co, Hi, Hi), 1.0)) if has_res else None
+    y = run_conv_f32d(x, w, scale, shift, 1, dil, dil, res, bm=bm, bn=bn, entry="cwt_debug_conv_x6w")
+    ref = ref_conv(x, w, scale, shift, 1, dil, dil, res, True)
+    err = float((y.double() - ref).abs().max() / ref.abs().max())
+    assert err < TOL_X6, err
+
+
+def test_conv_x6_winograd_channel_strided_out():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    x = torch.from_numpy(syn.normal(2, "xw", (2, 128, 11, 11), 1.0))
+    w = torch.from_numpy(syn.normal(2, "ww", (128, 128, 3, 3), 0.04))
+    scale, shift = torch.ones(128), torch.zeros(128)
+    y = run_conv_f32d(x, w, scale, shift, 1, 2, 2, None, relu=False, y_pad=256, y_off=128, entry="cwt_debug_conv_x6w")
+    ref = ref_conv(x, w, scale, shift, 1, 2, 2, None, False)
+    assert float((y.double() - ref).abs().max() / ref.abs().max()) < TOL_X6

@@ -78,6 +78,8 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
     for name, cnt, Ci, Co, Hi, k, stride, dil, has_res in shapes(layers, size, n_img):
         if only and name not in only:
             continue
+        if prec == 7 and (k != 3 or stride != 1 or Ci < 128):
+            continue   # the Winograd form's candidates: stride-1 3x3 layers with Ci >= 128 (used at >= 256)
         pad = dil if k == 3 else 0
         Ho = (Hi + 2 * pad - dil * (k - 1) - 1) // stride + 1
         M, K = n_img * Ho * Ho, Ci * k * k
@@ -87,7 +89,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         if prec == 1:   # plain bf16 operands (K order inside a row does not matter for timing)
             xs = x.to(torch.bfloat16).contiguous()
             ws = w.reshape(Co, K).to(torch.bfloat16).contiguous()
-        elif prec in (0, 6):  # exact fp32 (conv_igemm_f32d) / bf16x6 (conv_igemm_x6): fp32 NHWC and fp32 [Co][K]
+        elif prec in (0, 6, 7):  # exact fp32 (f32d) / bf16x6 (x6, x6 Winograd): fp32 NHWC and fp32 [Co][K]
             xs = x
             ws = w.reshape(Co, K).contiguous()
         else:
@@ -99,7 +101,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         sh = torch.zeros(Co, device=dev)
         r = torch.randn(n_img, Ho, Ho, Co, device=dev) if has_res else None
         rs = None
-        if has_res and prec in (0, 6):
+        if has_res and prec in (0, 6, 7):
             rs = None
         elif has_res and prec == 1:
             rs = r.to(torch.bfloat16).contiguous()
@@ -113,8 +115,8 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         conv_fn = lib.cwt_debug_conv_b16 if prec == 1 else lib.cwt_debug_conv_s
 
         def new(bm, bn, ns):
-            if prec in (0, 6):
-                fn = lib.cwt_debug_conv_f32d if prec == 0 else lib.cwt_debug_conv_x6
+            if prec in (0, 6, 7):
+                fn = {0: lib.cwt_debug_conv_f32d, 6: lib.cwt_debug_conv_x6, 7: lib.cwt_debug_conv_x6w}[prec]
                 return lambda: _lib.check(fn(
                     ctx, _lib.ptr(xs), n_img, Hi, Hi, Ci, _lib.ptr(ws), _lib.ptr(sc), _lib.ptr(sh), Co, k, stride,
                     pad, dil, _lib.ptr(r), Co, 1, _lib.ptr(y), Co, 0, bm, bn, ns, sp))
@@ -139,7 +141,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
                     if var >= 2 and (bm == 256 or bn == 256):
                         continue   # 8-wave form only for the 128/64 tiles
                     for ns in (1, 2, 4, 8):
-                        if ns > 1 and ((K // (64 if prec == 1 else 32)) // ns < 4 or tiles * ns > 4096):
+                        if ns > 1 and (prec == 7 or (K // (64 if prec == 1 else 32)) // ns < 4 or tiles * ns > 4096):
                             continue
                         us = timed(new(1000 * var + bm, bn, ns), reps)
                         rows.append({"bm": bm, "bn": bn, "ns": ns, "var": var, "us": round(us, 2),
@@ -152,6 +154,10 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
               f"auto {t_auto:7.1f} ({flops / t_auto / 1e6:6.1f} TF)  best "
               f"{best['bm']}x{best['bn']}s{best['ns']}v{best['var']} {best['us']:7.1f} ({best['tflops']:6.1f} TF)",
               flush=True)
+        if prec == 7:   # the plan table keys the batched GEMMs by (tiles, Co, Ci)
+            d_ = dil
+            TY = (-(-Ho // d_) + 1) // 2
+            M, K = n_img * d_ * d_ * TY * TY, Ci
         res_all.append({"cfg": f"{layers}:{size}:{n_img}", "prec": prec, "name": name, "count": cnt, "Ci": Ci, "Co": Co, "k": k,
                         "Ho": Ho, "M": M, "K": K, "stride": stride, "dil": dil, "res": has_res,
                         "auto_us": round(t_auto, 2), "plans": rows})
@@ -167,9 +173,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--quick", action="store_true", help="old vs new automatic plan only")
     ap.add_argument("--out", default="conv_s_sweep.json")
-    ap.add_argument("--prec", type=int, default=3, choices=[0, 1, 3, 6],
+    ap.add_argument("--prec", type=int, default=3, choices=[0, 1, 3, 6, 7],
                     help="3 = bf16x3 (x3s), 1 = plain bf16 (b16), 0 = exact fp32 on the LDS-DMA body (f32d), "
-                         "6 = fp32 width on bf16 MFMA (x6)")
+                         "6 = fp32 width on bf16 MFMA (x6), 7 = x6 in the Winograd F(2x2,3x3) form (x6w)")
     ap.add_argument("--vars", default="0,1,2,4", help="main-loop variants (0 base, 1 prefetch, 2 prefetch 8 waves, 4 128x128 two per CU; 8-11 timing study)")
     ap.add_argument("--only", default="", help="comma list of shape names (default: all)")
     args = ap.parse_args()
