@@ -68,6 +68,8 @@ SIGNATURES = {
     "cwt_channel_sum": (_I, [_P, _P, _I, _I, _I64, _P, _P]),
     "cwt_sce_descriptor": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "cwt_match_readout": (_I, [_P, _P, _I, _I, _I, _F, _P, _I, _P, _P]),
+    "cwt_match_masks_train": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _F, C.c_uint64, _P]),
+    "cwt_match_readout_backward": (_I, [_P, _P, _I, _I, _I, _F, _P, _I, _P, _P, _P, _P, _P]),
     "cwt_weight_average": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "cwt_mmn_blend": (_I, [_P, _P, _P, _I, _I64, _F, _P, _P, _P]),
     "cwt_match_corr_saved_floats": (_I, [_I, _I, _I, _I, _I, _I, C.POINTER(_I64)]),

@@ -93,7 +93,8 @@ int launch_cv4d_layer(const float* x, int B, int hA, int wA, int hB, int wB, int
 int launch_sce_descriptor(const float* x, int B, int h, int w, int C, int k, int ldg, float* g, hipStream_t st);
 int launch_channel_sum(const float* x, int B, int L, long P, float* y, hipStream_t st);
 int launch_match_masks(float* corr, int B, int NA, int NB, const uint8_t* ig, const int64_t* s_mask, float* incons,
-                       int* q2k, float* pv, int* pi, hipStream_t st);
+                       int* q2k, float* pv, int* pi, hipStream_t st, float drop_p = 0.f, unsigned long long seed = 0);
+int launch_match_zero_ig_cols(float* g, const uint8_t* ig, int B, int NA, int NB, hipStream_t st);
 int launch_wa_attn(const float* tpg, int N, int h, int w, int co, const float* bt, const float* bp, const float* bg,
                    float* wavg, hipStream_t st);
 int launch_wa_residual(const float* x, const float* back, const float* b, long n, int C, float* out, hipStream_t st);
@@ -1995,8 +1996,13 @@ int cwt_channel_sum(cwt_ctx* ctx, const float* x, int B, int L, int64_t P, float
 
 int cwt_match_masks(cwt_ctx* ctx, float* corr2d, int B, int NA, int NB, const uint8_t* ig_mask,
                     const int64_t* s_mask, float* inconsistent, void* stream) {
+  return cwt_match_masks_train(ctx, corr2d, B, NA, NB, ig_mask, s_mask, inconsistent, 0.f, 0, stream);
+}
+
+int cwt_match_masks_train(cwt_ctx* ctx, float* corr2d, int B, int NA, int NB, const uint8_t* ig_mask,
+                          const int64_t* s_mask, float* inconsistent, float drop_p, uint64_t seed, void* stream) {
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
-  CWT_CHECK(corr2d && B >= 1 && NA >= 1 && NB >= 1, "bad arguments");
+  CWT_CHECK(corr2d && B >= 1 && NA >= 1 && NB >= 1 && drop_p >= 0.f && drop_p < 1.f, "bad arguments");
   CWT_CHECK(!s_mask || inconsistent, "the cycle mask needs inconsistent");
   CWT_HIP(hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
@@ -2007,7 +2013,8 @@ int cwt_match_masks(cwt_ctx* ctx, float* corr2d, int B, int NA, int NB, const ui
                  (rc = ensure_ws(ctx, "match.coli", (size_t)B * 16 * NB * 4, &pi))))
     return rc;
   Prof p(ctx, st, "match_masks", 0.0, 4.0 * B * NA * NB * (s_mask ? 4 : 2));
-  if ((rc = launch_match_masks(corr2d, B, NA, NB, ig_mask, s_mask, inconsistent, (int*)q2k, (float*)pv, (int*)pi, st)))
+  if ((rc = launch_match_masks(corr2d, B, NA, NB, ig_mask, s_mask, inconsistent, (int*)q2k, (float*)pv, (int*)pi, st,
+                               drop_p, (unsigned long long)seed)))
     return rc;
   p.end();
   return 0;
@@ -2029,6 +2036,54 @@ int cwt_match_readout(cwt_ctx* ctx, const float* corr2d, int B, int NA, int NB, 
   if ((rc = launch_match_softmax(corr2d, B, NA, NB, temp, ldp, (float*)pw, st))) return rc;
   if ((rc = launch_match_vt(v, B, NB, Cv, ldp, (float*)vt, st))) return rc;
   if ((rc = readout_gemm(ctx, (const float*)pw, (const float*)vt, B, NA, Cv, ldp, weighted_v, st))) return rc;
+  p.end();
+  return 0;
+}
+
+int cwt_match_readout_backward(cwt_ctx* ctx, const float* corr2d, int B, int NA, int NB, float temp, const float* v,
+                               int Cv, const float* d_weighted_v, const uint8_t* ig_mask, float* d_corr2d, float* d_v,
+                               void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(corr2d && d_corr2d && B >= 1 && NA >= 1 && NB >= 1, "bad arguments");
+  CWT_CHECK(!d_weighted_v || (v && Cv >= 4 && Cv % 4 == 0), "d_weighted_v needs v and Cv % 4 == 0");
+  CWT_CHECK(!d_v || d_weighted_v, "d_v needs d_weighted_v");
+  CWT_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int ldp = (int)((NB + 31) & ~31L);
+  const long E = (long)B * NA * NB;
+  void *pw, *dA;
+  int rc;
+  if ((rc = ensure_ws(ctx, "match.attn", (size_t)B * NA * ldp * 4, &pw)) ||
+      (rc = ensure_ws(ctx, "mb.dA", (size_t)E * 4, &dA)))
+    return rc;
+  Prof p(ctx, st, "match_readout_backward", 2.0 * 2.0 * B * NA * (double)NB * Cv,
+         4.0 * B * ((double)NA * NB * 4 + (double)(NA + NB) * Cv * 2));
+  if (d_weighted_v) {
+    // attn = softmax(temp corr2d) again (the forward's masked corr2d), dA = d_wv . v^T
+    if ((rc = launch_match_softmax(corr2d, B, NA, NB, temp, ldp, (float*)pw, st))) return rc;
+    for (int b = 0; b < B; ++b)
+      if ((rc = gemm_nt(ctx, d_weighted_v + (long)b * NA * Cv, v + (long)b * NB * Cv, NA, NB, Cv,
+                        (float*)dA + (long)b * NA * NB, st)))
+        return rc;
+    // d corr2d += temp P (dA - <P, dA>) (accumulating into the caller's gradient at corr2d)
+    if ((rc = launch_match_softmax_bwd((const float*)pw, ldp, (const float*)dA, B * NA, NB, temp, 1, d_corr2d, st)))
+      return rc;
+  }
+  if (ig_mask && (rc = launch_match_zero_ig_cols(d_corr2d, ig_mask, B, NA, NB, st))) return rc;
+  if (d_v) {  // d_v[b] = attn[b]^T . d_wv[b]
+    const long lda = ld32(NA);
+    void *pt, *dwt;
+    if ((rc = ensure_ws(ctx, "mb.PT", (size_t)B * ldp * lda * 4, &pt)) ||
+        (rc = ensure_ws(ctx, "mb.dwvT", (size_t)B * Cv * lda * 4, &dwt)))
+      return rc;
+    if ((rc = launch_match_vt((const float*)pw, B, NA, ldp, (int)lda, (float*)pt, st)) ||
+        (rc = launch_match_vt(d_weighted_v, B, NA, Cv, (int)lda, (float*)dwt, st)))
+      return rc;
+    for (int b = 0; b < B; ++b)
+      if ((rc = gemm_nt(ctx, (const float*)pt + (long)b * ldp * lda, (const float*)dwt + (long)b * Cv * lda, NB, Cv,
+                        (int)lda, d_v + (long)b * NB * Cv, st)))
+        return rc;
+  }
   p.end();
   return 0;
 }

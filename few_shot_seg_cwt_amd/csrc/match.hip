@@ -1612,6 +1612,34 @@ __global__ void match_mask_apply_kernel(float* __restrict__ corr, const uint8_t*
   }
 }
 
+// Train-mode Dropout(0.1) of the cycle mask (match.py:97 ass_drop, applied in run_cyc
+// match.py:181): inconsistent[b][j] *= dropout_scale(p, seed, stream 5, b NB + j) -- kept entries
+// become 1 / (1 - p), as nn.Dropout scales them; the mask is constant under autograd (argmax
+// indices), so no gradient passes through it.
+__global__ void match_cyc_dropout_kernel(float* __restrict__ incons, long n, float p, unsigned long long seed) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) incons[i] *= dropout_scale(p, seed, 5u, (unsigned long long)i);
+}
+
+// d corr2d[b][i][j] = 0 where ig_mask[b][j]: the masked entries were overwritten with the constant
+// 1e-4 (match.py:117-119), so nothing flows back through them
+__global__ void match_zero_ig_cols_kernel(float* __restrict__ g, const uint8_t* __restrict__ ig, int B, int NA, int NB) {
+  const long total = (long)B * NA * NB;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(e % NB);
+    const int b = (int)(e / ((long)NA * NB));
+    if (ig[(long)b * NB + j]) g[e] = 0.f;
+  }
+}
+
+int launch_match_zero_ig_cols(float* g, const uint8_t* ig, int B, int NA, int NB, hipStream_t st) {
+  const long total = (long)B * NA * NB;
+  hipLaunchKernelGGL(match_zero_ig_cols_kernel, dim3((unsigned)std::min<long>(65536, cdiv(total, 256))), dim3(256), 0, st,
+                     g, ig, B, NA, NB);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 // ---- WeightAverage (src/model/msm/msm_func.py:50-104), R = 3 ----
 // tpg [N][P][3co]: theta | phi | g of every pixel (1x1 convs as one GEMM, biases not yet
 // added); per pixel: cos_r = CosineSimilarity(phi(x_r), theta(x)) over its 3x3 replicate-padded
@@ -1950,7 +1978,7 @@ int launch_match_vt(const float* v, int B, int NB, int C, int ldp, float* vt, hi
 }
 
 int launch_match_masks(float* corr, int B, int NA, int NB, const uint8_t* ig, const int64_t* s_mask, float* incons,
-                       int* q2k, float* pv, int* pi, hipStream_t st) {
+                       int* q2k, float* pv, int* pi, hipStream_t st, float drop_p, unsigned long long seed) {
   if (s_mask) {
     hipLaunchKernelGGL(match_row_argmax_kernel, dim3(B * NA), dim3(256), 0, st, (const float*)corr, ig, NA, NB, q2k);
     CWT_LAUNCH_CHECK();
@@ -1960,6 +1988,11 @@ int launch_match_masks(float* corr, int B, int NA, int NB, const uint8_t* ig, co
     hipLaunchKernelGGL(match_cyc_kernel, dim3(cdiv((long)B * NB, 256)), dim3(256), 0, st, (const float*)pv,
                        (const int*)pi, (const int*)q2k, s_mask, B, NA, NB, incons);
     CWT_LAUNCH_CHECK();
+    if (drop_p > 0.f) {
+      hipLaunchKernelGGL(match_cyc_dropout_kernel, dim3(cdiv((long)B * NB, 256)), dim3(256), 0, st, incons, (long)B * NB,
+                         drop_p, seed);
+      CWT_LAUNCH_CHECK();
+    }
   }
   if (ig || s_mask) {
     const long total = (long)B * NA * NB;

@@ -17,14 +17,17 @@ cwt_match_corr_backward (softmax readout, both MutualMatchings with torch.max's 
 gradient routing, the CenterPivotConv4d layers' input / weight / bias gradients over both
 symmetric branches), cwt_corr_backward, cwt_weight_average_backward, cwt_mmn_blend_backward
 (csrc/match_bwd.hip) -- so the MMN trainers (train_cca.py:101-196, train_aug.py:102) and DeTr's
-cross attention (train_trans.py:100) can train this head.
+cross attention (train_trans.py:100) can train this head.  Round 5: MatchNet.forward's backward
+with ig_mask and the cycle mask (train_tp_match.py:188, train_match.py:164 use_cyc; the mask's
+train-mode Dropout(0.1) drawn on the device), cwt_match_readout_backward, and the spatial context
+encoder's weight / bias gradients (train_match.py:104 sce=args.sce).
 
 The modules keep the reference's parameter names (``NeighConsensus.conv.{0,2,4}.conv{1,2}.
 {weight,bias}``), so a reference state_dict loads as is.  Built: the default head of every MMN /
 MatchNet script -- CenterPivotConv4d ('red'), kernel sizes [3, 3, 3], channels [10, 10, 1],
 in_channel 1 or 2, symmetric or not -- and the MMN head of the mmn configs (rmid 'l34', all_lr
 'l', agg 'cat', wa True, red_dim False), forward only (inference), with MatchNet.forward's ig_mask and (round 3) its
-cycle-consistency mask (cyc, eval mode), and NeighConsensus over full Conv4d layers ('cv4',
+cycle-consistency mask (cyc; training mode since round 5), and NeighConsensus over full Conv4d layers ('cv4',
 fp32 VALU), the spatial context encoder (sce, spatial_context.py), and MMN's agg 'sum' and red_dim.
 Not built: forward_mmn (its MSBlock) and the MMN trainers' backward.
 
@@ -175,21 +178,73 @@ class SpatialContextEncoder(torch.nn.Module):
             self._wkey = key
         return self._wsplit
 
-    @torch.no_grad()
+    def _descriptor(self, xt: torch.Tensor, ldg: int) -> torch.Tensor:
+        B, C, h, w = xt.shape
+        g = torch.empty((B * h * w, ldg), device=xt.device, dtype=torch.float32)
+        _lib.check(_lib.lib().cwt_sce_descriptor(_lib.ctx(xt.device.index), _lib.ptr(xt), B, h, w, C, self.kernel_size,
+                                                 ldg, _lib.ptr(g), _lib.stream_ptr(xt.device)), "cwt_sce_descriptor")
+        return g
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         from .detr import linear
+        conv = self.embeddingFea[0]
+        if torch.is_grad_enabled() and x.requires_grad:
+            # the reference writes the descriptor into a leaf Variable created with x's requires_grad
+            # (spatial_context.py:32-53): torch refuses that in-place write, so the encoder has no
+            # gradient path into x there either
+            raise RuntimeError("SpatialContextEncoder: x requiring grad (the reference's generate_spatial_descriptor "
+                               "cannot run on it)")
         xt = as_tokens(x)
+        if _needs_grad(conv.weight, conv.bias):   # train_match.py with sce: the embedding trains
+            return _SceFn.apply(xt, conv.weight, conv.bias, self)
+        with torch.no_grad():
+            B, C, h, w = xt.shape
+            ldg = (self.kernel_size ** 2 + 3) & ~3
+            g = self._descriptor(xt, ldg)
+            wx, wg = self._weights(C, ldg)
+            tok = xt.permute(0, 2, 3, 1).reshape(B * h * w, C)   # a view of the NHWC storage
+            out = linear(tok, wx)
+            linear(g, wg, conv.bias, relu=True, out=out, accumulate=True)
+            return out.reshape(B, h, w, -1).permute(0, 3, 1, 2)
+
+
+class _SceFn(torch.autograd.Function):
+    """SpatialContextEncoder under autograd (the 1x1 conv's weight and bias train; the input and
+    its descriptor carry no gradient, as in the reference): out = relu([x | g] W^T + b); backward
+    by cwt_linear_backward over the two segments of the concatenation, the ReLU mask from out."""
+
+    @staticmethod
+    def forward(ctx, xt, weight, bias, enc):
+        from .detr import linear
         B, C, h, w = xt.shape
-        k = self.kernel_size
-        ldg = (k * k + 3) & ~3
-        g = torch.empty((B * h * w, ldg), device=x.device, dtype=torch.float32)
-        _lib.check(_lib.lib().cwt_sce_descriptor(_lib.ctx(x.device.index), _lib.ptr(xt), B, h, w, C, k, ldg,
-                                                 _lib.ptr(g), _lib.stream_ptr(x.device)), "cwt_sce_descriptor")
-        wx, wg = self._weights(C, ldg)
-        tok = xt.permute(0, 2, 3, 1).reshape(B * h * w, C)   # a view of the NHWC storage
+        ldg = (enc.kernel_size ** 2 + 3) & ~3
+        g = enc._descriptor(xt, ldg)
+        wx, wg = enc._weights(C, ldg)
+        tok = xt.permute(0, 2, 3, 1).reshape(B * h * w, C)
         out = linear(tok, wx)
-        linear(g, wg, self.embeddingFea[0].bias, relu=True, out=out, accumulate=True)
+        linear(g, wg, bias, relu=True, out=out, accumulate=True)
+        ctx.save_for_backward(tok, g, wx, wg, out)
+        ctx.meta = (weight.shape, enc.kernel_size ** 2, bias is not None)
         return out.reshape(B, h, w, -1).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, d):
+        tok, g, wx, wg, out = ctx.saved_tensors
+        wshape, k2, has_b = ctx.meta
+        P, C = tok.shape
+        N, ldg = wg.shape
+        dt = d.permute(0, 2, 3, 1).reshape(P, N).contiguous()
+        dev = tok.device
+        dwx = torch.empty((N, C), device=dev, dtype=torch.float32)
+        dwg = torch.empty((N, ldg), device=dev, dtype=torch.float32)
+        db = torch.empty(N, device=dev, dtype=torch.float32) if has_b else None
+        L, cx, st = _lib.lib(), _lib.ctx(dev.index), _lib.stream_ptr(dev)
+        _lib.check(L.cwt_linear_backward(cx, _lib.ptr(tok), P, C, _lib.ptr(wx), N, _lib.ptr(out), _lib.ptr(dt), None,
+                                         _lib.ptr(dwx), C, None, st), "cwt_linear_backward")
+        _lib.check(L.cwt_linear_backward(cx, _lib.ptr(g), P, ldg, _lib.ptr(wg), N, _lib.ptr(out), _lib.ptr(dt), None,
+                                         _lib.ptr(dwg), ldg, _lib.ptr(db), st), "cwt_linear_backward")
+        dw = torch.cat([dwx, dwg[:, :k2]], 1).reshape(wshape)
+        return None, dw, db, None
 
 
 class _MatchCorrFn(torch.autograd.Function):
@@ -243,6 +298,74 @@ class _MatchCorrFn(torch.autograd.Function):
 
 def _needs_grad(*ts) -> bool:
     return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
+class _MatchMaskedFn(torch.autograd.Function):
+    """MatchNet.forward with the support masks (match.py:103-130: ig_mask and, with cyc, the cycle
+    mask) under autograd ('red' layers).  Forward: cwt_match_corr_forward_train (the chain,
+    activations kept) -> cwt_match_masks_train on a copy of corr2d -> cwt_match_readout.  Backward:
+    cwt_match_readout_backward (softmax readout, then the ig-masked columns zeroed: the reference
+    overwrote them with a constant) -> cwt_match_corr_backward through both MutualMatchings and the
+    NeighConsensus layers.  The cycle mask is constant under autograd (argmax indices; its train-mode
+    Dropout(0.1) draws one scale per support position, stream 5 of the counter-based draw)."""
+
+    @staticmethod
+    def forward(ctx, corr, vt, ig, sm, symmetric, temp, h, w, drop_p, seed, *params):
+        B, L = corr.shape[0], corr.shape[1]
+        hw, dev = h * w, corr.device
+        Lb, cx, st = _lib.lib(), _lib.ctx(dev.index), _lib.stream_ptr(dev)
+        with torch.no_grad():
+            packed = torch.cat([p.detach().reshape(-1).float() for p in params]).contiguous()
+        n = C.c_int64()
+        _lib.check(Lb.cwt_match_corr_saved_floats(B, L, h, w, int(symmetric), 0, C.byref(n)),
+                   "cwt_match_corr_saved_floats")
+        saved = torch.empty(n.value, device=dev, dtype=torch.float32)
+        corr2d = torch.empty((B, hw, hw), device=dev, dtype=torch.float32)
+        _lib.check(Lb.cwt_match_corr_forward_train(cx, _lib.ptr(corr), B, L, h, w, _lib.ptr(packed), int(symmetric),
+                                                   float(temp), None, 0, _lib.ptr(corr2d), None, _lib.ptr(saved), st),
+                   "cwt_match_corr_forward_train")
+        inc = torch.empty((B, hw), device=dev, dtype=torch.float32) if sm is not None else None
+        _lib.check(Lb.cwt_match_masks_train(cx, _lib.ptr(corr2d), B, hw, hw, _lib.ptr(ig) if ig is not None else None,
+                                            _lib.ptr(sm) if sm is not None else None,
+                                            _lib.ptr(inc) if inc is not None else None, float(drop_p), int(seed), st),
+                   "cwt_match_masks_train")
+        Cv = vt.shape[1]
+        wv = torch.empty((B, h, w, Cv), device=dev, dtype=torch.float32)
+        _lib.check(Lb.cwt_match_readout(cx, _lib.ptr(corr2d), B, hw, hw, float(temp), _lib.ptr(vt), Cv, _lib.ptr(wv), st),
+                   "cwt_match_readout")
+        ctx.save_for_backward(corr, vt, packed, saved, corr2d, ig if ig is not None else corr.new_empty(0))
+        ctx.meta = (h, w, int(symmetric), float(temp), ig is not None)
+        ctx.shapes = [p.shape for p in params]
+        if inc is None:
+            inc = corr.new_empty(0)
+        ctx.mark_non_differentiable(inc)
+        return wv.permute(0, 3, 1, 2), corr2d, inc
+
+    @staticmethod
+    def backward(ctx, g_wv, g_corr2d, g_inc):
+        corr, vt, packed, saved, corr2d, ig = ctx.saved_tensors
+        h, w, sym, temp, has_ig = ctx.meta
+        B, L = corr.shape[0], corr.shape[1]
+        hw, dev = h * w, corr.device
+        Lb, cx, st = _lib.lib(), _lib.ctx(dev.index), _lib.stream_ptr(dev)
+        d2 = g_corr2d.contiguous().clone() if g_corr2d is not None else torch.zeros((B, hw, hw), device=dev)
+        gw = g_wv.permute(0, 2, 3, 1).contiguous() if g_wv is not None else None
+        Cv = vt.shape[1]
+        d_v = (torch.empty((B, h, w, Cv), device=dev, dtype=torch.float32)
+               if (gw is not None and ctx.needs_input_grad[1]) else None)
+        if gw is not None or has_ig:
+            _lib.check(Lb.cwt_match_readout_backward(cx, _lib.ptr(corr2d), B, hw, hw, temp, _lib.ptr(vt), Cv,
+                                                     _lib.ptr(gw), _lib.ptr(ig) if has_ig else None, _lib.ptr(d2),
+                                                     _lib.ptr(d_v), st), "cwt_match_readout_backward")
+        d_corr = torch.empty_like(corr) if ctx.needs_input_grad[0] else None
+        d_params = torch.empty_like(packed)
+        _lib.check(Lb.cwt_match_corr_backward(cx, _lib.ptr(corr), B, L, h, w, _lib.ptr(packed), sym, temp, None, 0,
+                                              _lib.ptr(saved), _lib.ptr(d2), None, _lib.ptr(d_corr),
+                                              _lib.ptr(d_params), None, st), "cwt_match_corr_backward")
+        sizes = [math.prod(s) for s in ctx.shapes]
+        grads = [g.reshape(s) for g, s in zip(torch.split(d_params, sizes), ctx.shapes)]
+        return (d_corr, d_v.permute(0, 3, 1, 2) if d_v is not None else None, None, None, None, None, None, None,
+                None, None, *grads)
 
 
 class MatchNet(torch.nn.Module):
@@ -326,14 +449,13 @@ class MatchNet(torch.nn.Module):
                 raise UnboundLocalError("ret_cyc needs the cycle mask (cyc=True and use_cyc=True)")
             corr2d, wv = self._run(corr.reshape(B, 1, hw, hw), h, w, v)
             return (wv, corr2d.reshape(B, h, w, h, w)) if ret_corr else wv
-        if corr.requires_grad and torch.is_grad_enabled():
-            raise NotImplementedError("MatchNet backward with ig_mask / the cycle mask is not built (no trainer uses it)")
         if cyc_on and s_mask is None:   # run_cyc returns None and the reference fails on it
             raise ValueError("the cycle mask needs s_mask")
-        if cyc_on and self.training:
-            raise NotImplementedError("the cycle mask's Dropout(0.1) in training mode is not built; call .eval()")
-        corr2d, _ = self._run(corr.reshape(B, 1, hw, hw), h, w, None)
-        dev = corr2d.device
+        # train mode: run_cyc's ass_drop = nn.Dropout(0.1) on the mask (match.py:97,181), one draw per
+        # call from torch's generator (the reference's own draw cannot be reproduced: its RNG stream)
+        drop_p = 0.1 if (cyc_on and self.training) else 0.0
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0 else 0
+        dev = corr.device
         ig = None
         if ig_mask is not None:
             if ig_mask.numel() != B * hw:
@@ -344,12 +466,27 @@ class MatchNet(torch.nn.Module):
             if s_mask.numel() != B * hw:
                 raise ValueError("s_mask must hold B * h * w entries (s_mask.view(B, n_s))")
             sm = s_mask.reshape(B, hw).to(device=dev, dtype=torch.int64).contiguous()
-            inc = torch.empty((B, hw), device=dev, dtype=torch.float32)
-        _lib.check(_lib.lib().cwt_match_masks(
-            _lib.ctx(dev.index), _lib.ptr(corr2d), B, hw, hw, _lib.ptr(ig) if ig is not None else None,
-            _lib.ptr(sm) if sm is not None else None, _lib.ptr(inc) if inc is not None else None,
-            _lib.stream_ptr(dev)), "cwt_match_masks")
+        nc = self.NeighConsensus
         vt = as_tokens(v if v.dim() == 4 else v.reshape(v.shape[0], v.shape[1], h, w))
+        if nc.conv_type == "red" and _needs_grad(corr, vt, *nc.param_list()):
+            wv, corr2d, inc = _MatchMaskedFn.apply(corr.reshape(B, 1, hw, hw).contiguous(), vt, ig, sm,
+                                                   nc.symmetric_mode, float(self.temp), h, w, drop_p, seed,
+                                                   *nc.param_list())
+            out = [wv]
+            if ret_corr:
+                out.append(corr2d.reshape(B, h, w, h, w))
+            if ret_cyc:
+                if sm is None:
+                    raise UnboundLocalError("ret_cyc needs the cycle mask (cyc=True and use_cyc=True)")
+                out.append(inc.unsqueeze(1))
+            return out[0] if len(out) == 1 else tuple(out)
+        corr2d, _ = self._run(corr.reshape(B, 1, hw, hw), h, w, None)
+        if cyc_on:
+            inc = torch.empty((B, hw), device=dev, dtype=torch.float32)
+        _lib.check(_lib.lib().cwt_match_masks_train(
+            _lib.ctx(dev.index), _lib.ptr(corr2d), B, hw, hw, _lib.ptr(ig) if ig is not None else None,
+            _lib.ptr(sm) if sm is not None else None, _lib.ptr(inc) if inc is not None else None, float(drop_p), seed,
+            _lib.stream_ptr(dev)), "cwt_match_masks_train")
         Cv = vt.shape[-1] if vt.dim() == 3 else vt.shape[1]
         wv = torch.empty((B, h, w, Cv), device=dev, dtype=torch.float32)
         _lib.check(_lib.lib().cwt_match_readout(

@@ -401,11 +401,25 @@ int cwt_channel_sum(cwt_ctx* ctx, const float* x, int B, int L, int64_t P, float
  * The reference's Dropout(0.1) on the mask is its eval-mode identity. */
 int cwt_match_masks(cwt_ctx* ctx, float* corr2d, int B, int NA, int NB, const uint8_t* ig_mask,
                     const int64_t* s_mask, float* inconsistent, void* stream);
+/* The same in training mode (match.py:97,181 ass_drop = nn.Dropout(0.1) on the cycle mask):
+ * inconsistent[b][j] is scaled by the counter-based dropout draw (common.h dropout_scale, stream 5,
+ * index b NB + j; kept entries 1 / (1 - drop_p)) before corr2d += inconsistent * -1000. */
+int cwt_match_masks_train(cwt_ctx* ctx, float* corr2d, int B, int NA, int NB, const uint8_t* ig_mask,
+                          const int64_t* s_mask, float* inconsistent, float drop_p, uint64_t seed, void* stream);
 
 /* MatchNet's readout (match.py:128-130): weighted_v device [B][NA][Cv] = softmax(temp * corr2d,
  * -1) . v, v device [B][NB][Cv] (NHWC tokens).  Exact fp32. */
 int cwt_match_readout(cwt_ctx* ctx, const float* corr2d, int B, int NA, int NB, float temp, const float* v, int Cv,
                       float* weighted_v, void* stream);
+/* Its backward (MatchNet.forward under autograd with the support masks, match.py:117-130):
+ * corr2d the masked corr2d the readout saw, d_weighted_v device [B][NA][Cv] -> d_corr2d device
+ * [B][NA][NB] += the softmax readout's gradient, then zeroed on the ig-masked support columns
+ * (those entries were overwritten by a constant; the -1000 * inconsistent shift passes the
+ * gradient unchanged); d_v device [B][NB][Cv] = attn^T . d_weighted_v (NULL: skipped).  Cv % 4 == 0.
+ * d_weighted_v NULL: only the ig columns of d_corr2d are zeroed. */
+int cwt_match_readout_backward(cwt_ctx* ctx, const float* corr2d, int B, int NA, int NB, float temp, const float* v,
+                               int Cv, const float* d_weighted_v, const uint8_t* ig_mask, float* d_corr2d, float* d_v,
+                               void* stream);
 
 /* WeightAverage (src/model/msm/msm_func.py:50-104, R = 3; the MMN head's wa_<layer> modules,
  * mmn.py:27-34,53-55): x device [N][h][w][C] (NHWC tokens), C = c_in in {512, 1024, 2048};

@@ -199,8 +199,10 @@ def test_forward_masks_errors(dev):
     from few_shot_seg_cwt_amd.match import MatchNet
     net = MatchNet(temp=20.0, cyc=True, device=dev)
     f = torch.rand(1, 8, 4, 4, device=dev)
-    with pytest.raises(NotImplementedError):   # Dropout(0.1) of the mask in training mode
-        net(f, f, f, s_mask=torch.zeros(1, 4, 4, dtype=torch.long, device=dev), use_cyc=True)
+    # training mode: Dropout(0.1) of the cycle mask (built since round 5): entries 0 or 1 / 0.9
+    _, inc = net(f, f, f, s_mask=(torch.rand(1, 4, 4, device=dev) < 0.5).long(), use_cyc=True, ret_cyc=True)
+    vals = set(round(float(x), 5) for x in inc.flatten().cpu())
+    assert vals <= {0.0, round(1 / 0.9, 5)}, vals
     net.eval()
     with pytest.raises(ValueError):
         net(f, f, f, s_mask=None, use_cyc=True)

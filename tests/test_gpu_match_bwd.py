@@ -221,3 +221,98 @@ def test_mmn_backward_agg_red_dim(dev, agg, red_dim):
         errs[n] = rel(p.grad, sd[n].grad)
     print(f"MMN backward agg={agg} red_dim={red_dim}: " + ", ".join(f"{k} {e:.1e}" for k, e in errs.items()))
     assert max(errs.values()) < TOL, errs
+
+
+def _get_corr64(fq, fs):
+    """heads.get_corr in float64: cosine similarity of every query / support pixel pair."""
+    B, C, h, w = fq.shape
+    nq = torch.nn.functional.normalize(fq, dim=1).reshape(B, C, h * w)
+    ns = torch.nn.functional.normalize(fs, dim=1).reshape(B, C, h * w)
+    return torch.bmm(nq.transpose(1, 2), ns).reshape(B, 1, h, w, h, w)
+
+
+@pytest.mark.parametrize("use_ig,use_cyc,train", [(True, False, False), (False, True, False), (True, True, True)])
+def test_forward_masks_backward(dev, use_ig, use_cyc, train):
+    """MatchNet.forward with ig_mask and / or the cycle mask under autograd (match.py:103-130,
+    165-182; train_tp_match.py:188, train_match.py:164): gradients of <G1, weighted_v> +
+    <G2, masked corr2d> with respect to v and every NeighConsensus parameter, against float64
+    autograd through the oracle chain.  The cycle mask (argmax decisions, and in training mode its
+    Dropout draw) is the device's own, a constant under autograd in both."""
+    from oracle import match_oracle as M
+    B, C, h, w, Cv, temp = 2, 64, 7, 8, 48, 20.0
+    net = _net(dev, 1, True, temp, seed=41)
+    net.cyc = use_cyc
+    net.train(train)
+    g = torch.Generator().manual_seed(42)
+    fq0, fs0 = torch.rand(B, C, h, w, generator=g).double(), torch.rand(B, C, h, w, generator=g).double()
+    v0 = torch.randn(B, Cv, h, w, generator=g).double()
+    ig = (torch.rand(B, h * w, generator=g) < 0.25) if use_ig else None
+    sm = (torch.rand(B, h, w, generator=g) < 0.4).long() if use_cyc else None
+    G1, G2 = _rand((B, Cv, h, w), 43, -1, 1), _rand((B, h * w, h * w), 44, -1, 1)
+    v = v0.float().to(dev).requires_grad_(True)
+    out = net(fq0.float().to(dev), fs0.float().to(dev), v, s_mask=sm.to(dev) if use_cyc else None,
+              ig_mask=ig.to(dev) if use_ig else None, ret_corr=True, use_cyc=use_cyc, ret_cyc=use_cyc)
+    wv, corr = out[0], out[1]
+    ((wv * G1.float().to(dev)).sum() + (corr.reshape(B, h * w, h * w) * G2.float().to(dev)).sum()).backward()
+    names = [f"NeighConsensus.conv.{i}.{c}.{p}" for i in (0, 2, 4) for c in ("conv1", "conv2") for p in ("weight", "bias")]
+    sd = {k: t.detach().cpu().double().requires_grad_(True) for k, t in net.state_dict().items()}
+    vo = v0.clone().requires_grad_(True)
+    c2 = M.run_match_model(_get_corr64(fq0, fs0), M.layers_from_state(sd), True).reshape(B, h * w, h * w)
+    if use_ig:
+        c2 = c2.masked_fill(ig.reshape(B, 1, h * w).expand(c2.shape), 0.0001)
+    if use_cyc:
+        inc = out[2][:, 0].detach().cpu().double()
+        c2 = c2 + inc.unsqueeze(1) * (-1000.0)
+        if train:
+            assert set(torch.unique(inc).tolist()) <= {0.0, float(torch.tensor(1 / 0.9, dtype=torch.float32))}
+    attn = torch.softmax(c2 * temp, dim=-1)
+    wvo = torch.bmm(vo.reshape(B, Cv, h * w), attn.transpose(1, 2)).reshape(B, Cv, h, w)
+    ((wvo * G1).sum() + (c2 * G2).sum()).backward()
+    params = dict(net.named_parameters())
+    errs = dict(wv=rel(wv, wvo), corr2d=rel(corr.reshape(B, h * w, h * w), c2), d_v=rel(v.grad, vo.grad))
+    for n in names:
+        errs[n.replace("NeighConsensus.conv.", "")] = rel(params[n].grad, sd[n].grad)
+    print(f"MatchNet masks backward ig={use_ig} cyc={use_cyc} train={train}: "
+          + ", ".join(f"{k} {e:.1e}" for k, e in errs.items()))
+    assert float(sd[names[0]].grad.abs().max()) > 0
+    assert max(errs.values()) < TOL, errs
+
+
+def test_sce_backward(dev):
+    """MatchNet(sce=True) training (train_match.py:104 sce=args.sce): the spatial context encoder's
+    1x1 conv weight and bias (spatial_context.py:84-87), the NeighConsensus parameters and v get
+    their gradients; the frozen features carry none (the reference cannot differentiate its
+    descriptor).  Against float64 autograd through the oracle chain."""
+    from few_shot_seg_cwt_amd.match import MatchNet, init_match_params
+    from oracle import match_oracle as M
+    B, C, h, w, Cv, temp = 1, 2048, 6, 7, 32, 20.0
+    net = MatchNet(temp=temp, sce=True, device=dev)
+    init_match_params(net, 51)
+    with torch.no_grad():
+        net.NeighConsensus.conv[4].conv1.bias.add_(0.2)
+    g = torch.Generator().manual_seed(52)
+    # zero-mean features: with all-positive ones the encoder's outputs are nearly parallel (cosines
+    # near 1), and the last consensus layer's two scalar bias gradients -- sums over every pair with
+    # heavy cancellation -- inherit the fp32 rounding of corr2d amplified (8e-4 measured); the
+    # gradient code is the same either way
+    fq0, fs0 = torch.randn(B, C, h, w, generator=g).double(), torch.randn(B, C, h, w, generator=g).double()
+    v0 = torch.randn(B, Cv, h, w, generator=g).double()
+    G = _rand((B, Cv, h, w), 53, -1, 1)
+    v = v0.float().to(dev).requires_grad_(True)
+    wv = net(fq0.float().to(dev), fs0.float().to(dev), v)
+    (wv * G.float().to(dev)).sum().backward()
+    sd = {k: t.detach().cpu().double().requires_grad_(True) for k, t in net.state_dict().items()}
+    W, b = sd["SpatialContextEncoder.embeddingFea.0.weight"], sd["SpatialContextEncoder.embeddingFea.0.bias"]
+    eq = M.spatial_context_encoder(torch.nn.functional.normalize(fq0, dim=1), 25, W, b)
+    es = M.spatial_context_encoder(torch.nn.functional.normalize(fs0, dim=1), 25, W, b)
+    vo = v0.clone().requires_grad_(True)
+    _, wvo = M.corr_forward(_get_corr64(eq, es), vo, M.layers_from_state(sd), temp, True)
+    (wvo * G).sum().backward()
+    params = dict(net.named_parameters())
+    errs = dict(wv=rel(wv, wvo), d_v=rel(v.grad, vo.grad))
+    for n in ["SpatialContextEncoder.embeddingFea.0.weight", "SpatialContextEncoder.embeddingFea.0.bias"] + \
+            [f"NeighConsensus.conv.{i}.{c}.{p}" for i in (0, 2, 4) for c in ("conv1", "conv2") for p in ("weight", "bias")]:
+        errs[n.split(".", 1)[1] if n.startswith("NeighConsensus") else n.split(".")[-1]] = rel(params[n].grad, sd[n].grad)
+    print("MatchNet sce backward: " + ", ".join(f"{k} {e:.1e}" for k, e in errs.items()))
+    assert float(W.grad.abs().max()) > 0
+    assert max(errs.values()) < TOL, errs
