@@ -1134,7 +1134,7 @@ int cwt_ctx_create(int device, cwt_ctx** out) {
     delete c;
     return fail(CWT_ESTATE, "cwt_ctx_create: mapped status word");
   }
-  *(volatile unsigned*)c->status_host = 0u;
+  for (int i = 0; i < 16; ++i) ((volatile unsigned*)c->status_host)[i] = 0u;
   *out = c;
   return 0;
 }
@@ -1155,10 +1155,16 @@ int cwt_ctx_destroy(cwt_ctx* ctx) {
 
 int cwt_ctx_status(cwt_ctx* ctx, uint32_t* status, int clear) {
   if (!ctx || !status) return fail(CWT_EARG, "null argument");
+  // one word per failure source (plain stores from the kernels, no PCIe atomics): word 0 the inner
+  // loop, word 1 the post-loop tail; the caller sees their OR
   volatile unsigned* w = ctx->status_host;
-  *status = *w;
-  if (*status & CWT_STATUS_TAIL_BARRIER) ctx->tail_epoch = ~0u;  // its counters are re-zeroed before the next tail
-  if (clear) *w = 0u;
+  const unsigned w0 = w[0], w1 = w[1];
+  *status = w0 | w1;
+  if (w1) ctx->tail_epoch = ~0u;  // the tail aborted: its counters are re-zeroed before the next tail
+  if (clear) {
+    w[0] = 0u;
+    w[1] = 0u;
+  }
   return 0;
 }
 
@@ -1461,7 +1467,7 @@ int cwt_episode_tail(cwt_ctx* ctx, const float* q, const float* f, int B, int h,
   if (pk.ev0()) CWT_HIP(hipEventRecord(pk.ev0(), st));
   rc = launch_episode_tail(q, f, B, hw, h, w, S, q_label, (const float*)fold, fc_b, ln_w, ln_b, out, logits, logits0,
                            iut, ce, iut0, (float*)ws, (unsigned*)cnt, ctx->tail_epoch++, G, ctx->adapt_spin_limit,
-                           ctx->status_dev, st, (unsigned long long*)stamps);
+                           ctx->status_dev + 1, st, (unsigned long long*)stamps);  // the tail's status word
   if (pk.ev1()) CWT_HIP(hipEventRecord(pk.ev1(), st));
   p.end();
   return rc;

@@ -76,7 +76,7 @@ struct TailArgs {
   unsigned bar_base;     // e * G * NBAR
   unsigned tick_base;    // e * G
   long spin_limit;
-  unsigned* status;      // the context's mapped host status word
+  unsigned* status;      // the tail's word of the context's mapped host status (word 1; the loop owns word 0)
   unsigned long long* stamps;  // timing study (ST instantiation): [G][TL_NSTAMP] s_memtime per phase edge
 };
 constexpr int TL_NSTAMP = 16;

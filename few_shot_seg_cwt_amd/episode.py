@@ -132,11 +132,13 @@ def cwt_tail(transformer, Wb: torch.Tensor, f_q: torch.Tensor):
 _FUSED_TAIL = os.environ.get("CWT_FUSED_TAIL", "1") != "0"   # 0: the module kernels (A/B)
 
 
-def fused_tail_ok(transformer, f_q: torch.Tensor) -> bool:
+def fused_tail_ok(transformer, f_q: torch.Tensor, S: int) -> bool:
     """The one-launch tail (cwt_episode_tail) takes 4 heads, d_model 512, <= 4 queries of
-    <= 16384 tokens (S - 1 == 8 (h - 1): the extractor's geometry)."""
+    <= 16384 tokens and labels of side S with S - 1 == 8 (h - 1) (the extractor's geometry);
+    anything else takes the module path (cwt_tail + seg_metrics_pair, any S)."""
     B, Cc, h, w = f_q.shape
-    return (_FUSED_TAIL and transformer.n_head == 4 and Cc == 512 and h * w <= 16384 and B <= 4 and h == w)
+    return (_FUSED_TAIL and transformer.n_head == 4 and Cc == 512 and h * w <= 16384 and B <= 4 and h == w
+            and S - 1 == 8 * (h - 1))
 
 
 def episode_tail(transformer, Wb: torch.Tensor, f_q: torch.Tensor, q_label: torch.Tensor):
@@ -169,7 +171,7 @@ def episode_tail(transformer, Wb: torch.Tensor, f_q: torch.Tensor, q_label: torc
 def tail_and_metrics(transformer, Wb: torch.Tensor, f_q: torch.Tensor, q_label: torch.Tensor):
     """(W', pred_q, pred_q0, iut, ce, iut0) of an episode group (B <= 4): the one-launch tail
     where it applies, else cwt_tail + seg_metrics_pair."""
-    if fused_tail_ok(transformer, f_q):
+    if fused_tail_ok(transformer, f_q, q_label.shape[-1]):
         return episode_tail(transformer, Wb, f_q, q_label)
     W2, pred_q, pred_q0 = cwt_tail(transformer, Wb, f_q)
     iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
@@ -312,7 +314,10 @@ class EpisodePipeline:
                 _lib.check(_lib.lib().cwt_adapt_workgroups(c, 1, shot, h, w, iters, ctypes.byref(g)),
                            "cwt_adapt_workgroups")
                 gs.append(g.value)
-            self._fits[key] = min(gs) > 0 and sum(gs) <= _lib.cu_count(self.device)
+            # the adapt context's fused tail (a 64-workgroup co-resident grid, cwt_episode_tail on a
+            # context with cwt_ctx_set_adapt_units >= 2) may run beside the drain loop as well
+            tail_g = min(64, _lib.cu_count(self.device))
+            self._fits[key] = min(gs) > 0 and sum(gs) + tail_g <= _lib.cu_count(self.device)
         return self._fits[key]
 
     @torch.no_grad()
