@@ -726,7 +726,8 @@ static int run_wino_conv(cwt_ctx* ctx, const float* x, int N, int H, int W, int 
     p.bn = bn;
     if (Co % p.bn) return fail(CWT_EARG, "winograd GEMM tile: Co % bn");
   }
-  if ((rc = launch_conv_x3s(a, p, stage, nullptr, 0, st, 6))) return rc;
+  (void)stage;  // the batched GEMMs are the stage-7 instantiations (their own rocprofv3 statistics)
+  if ((rc = launch_conv_x3s(a, p, 7, nullptr, 0, st, 6))) return rc;
   return launch_wino_out((const float*)Mb, g, Co, scale, shift, res, res_ld, relu, y, y_ld, y_off, st);
 }
 
@@ -2553,8 +2554,10 @@ static int debug_conv_s(cwt_ctx* ctx, int prec, const void* xs, int N, int Hi, i
     CWT_CHECK((bm == 256 && (bn == 256 || bn == 128)) || (bm == 128 && (bn == 256 || bn == 128 || bn == 64)) ||
                   (bm == 64 && (bn == 128 || bn == 64)),
               "tile must be one of 256x256, 256x128, 128x256, 128x128, 128x64, 64x128, 64x64");
-    CWT_CHECK((var >= 0 && var <= 2) || (var == 4 && bm == 128 && bn == 128) || (var >= 8 && var <= 11),
-              "variant must be 0, 1, 2, 4 (128x128 only) or 8 .. 11 (timing study)");
+    const bool x6_var = prec == 6 && ((var == 3 && (bm >= 128 && bn >= 128)) || (var == 5 && bm == 128 && bn == 128));
+    CWT_CHECK((var >= 0 && var <= 2) || (var == 4 && bm == 128 && bn == 128) || (var >= 8 && var <= 11) || x6_var,
+              "variant must be 0, 1, 2, 4 (128x128 only), 8 .. 11 (timing study), or for x6 3 (tiles >= 128x128) "
+              "and 5 (128x128)");
     if (var >= 8 && var <= 11) {  // the timing-study kernels have fixed tiles: the grid must be theirs
       bm = bn = var < 10 ? 64 : 128;
     }

@@ -132,13 +132,18 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
                     continue
                 tiles = -(-M // bm) * (Co // bn)
                 for var in variants:
-                    if var and bm == 256 and bn == 256:
+                    x6v = prec in (6, 7)
+                    if var == 3 and not (x6v and bm >= 128 and bn >= 128):
+                        continue   # x6 only: the WN = 128 wave layouts of the big tiles
+                    if var == 5 and not (x6v and (bm, bn) == (128, 128)):
+                        continue   # x6 only: 128x128 in 4x1 waves on a 2-stage ring
+                    if var in (1, 2) and bm == 256 and bn == 256:
                         continue   # no prefetch form of 256x256
                     if var == 4 and (bm, bn) != (128, 128):
                         continue   # two-workgroups-per-CU 128x128 form
                     if var >= 8 and (bm, bn) != ((64, 64) if var < 10 else (128, 128)):
                         continue   # timing-study kernels: fixed tiles
-                    if var >= 2 and (bm == 256 or bn == 256):
+                    if var == 2 and (bm == 256 or bn == 256):
                         continue   # 8-wave form only for the 128/64 tiles
                     for ns in (1, 2, 4, 8):
                         if ns > 1 and (prec == 7 or (K // (64 if prec == 1 else 32)) // ns < 4 or tiles * ns > 4096):
