@@ -144,7 +144,8 @@ __device__ __forceinline__ void split3_bf16(const f32x4& x0, const f32x4& x1, bf
 // the slot tile t occupied is refilled (tile t + NSTG) as soon as every wave has passed that
 // barrier, so the ring keeps NSTG - 1 tiles in flight either way.
 // PF bits: 1 fragment prefetch; 2 / 4 timing studies (no MFMAs / no operand DMA); 8 buffer
-// addressing of the operand DMA (every production instantiation sets it).
+// addressing of the operand DMA (every production instantiation sets it); 16 timing study of the
+// x6 WN = 128 forms without the A split (wrong numbers, same data movement and MFMAs).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF>
 __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   static_assert(PREC == 0 || PREC == 1 || PREC == 3 || PREC == 6,
@@ -380,7 +381,14 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       bf16x8 as[FM][3];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        split3_bf16(__builtin_bit_cast(f32x4, F.ah[i]), __builtin_bit_cast(f32x4, F.al[i]), as[i][0], as[i][1], as[i][2]);
+        if constexpr ((PF & 16) != 0) {  // timing study (x6 var 12, 13): no A split, the raw bits as the terms
+          as[i][0] = F.ah[i];
+          as[i][1] = F.al[i];
+          as[i][2] = F.ah[i];
+        } else {
+          split3_bf16(__builtin_bit_cast(f32x4, F.ah[i]), __builtin_bit_cast(f32x4, F.al[i]), as[i][0], as[i][1],
+                      as[i][2]);
+        }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const char* p = sb + (b_row0 + j * 16) * 128;
