@@ -31,13 +31,14 @@ def roof_of(name):
 
 def pmc_key(name):
     """'conv_igemm_x6w<256,256,6> ...' -> (kind, bm, bn, stage) to match rocprofv3's kernel names
-    'void cwt::conv_igemm_x6<256, 256, 2, 4, 2, 6, 0>(cwt::ConvSArgs)' (the Winograd GEMMs are
-    conv_igemm_x6 instantiations)."""
+    'void cwt::conv_igemm_x6<256, 256, 4, 2, 2, 7, 0>(cwt::ConvSArgs)' (the Winograd form's GEMMs
+    are the stage-7 conv_igemm_x6 instantiations; its transforms are separate kernels)."""
     m = re.match(r"conv_igemm_(\w+?)<(\d+),(\d+),(\d+)>", name)
     if not m:
         return None
-    kind = "x6" if m.group(1) == "x6w" else m.group(1)
-    return kind, m.group(2), m.group(3), m.group(4)
+    if m.group(1) == "x6w":
+        return "x6", m.group(2), m.group(3), "7"
+    return m.group(1), m.group(2), m.group(3), m.group(4)
 
 
 def pmc_lookup(pmc, key):
@@ -92,7 +93,12 @@ def main(path, pmc_path=None):
             key = pmc_key(k)
             hits = pmc_lookup(pmc, key) if key else []
             if hits:
-                e = hits[0]
+                # the wave-layout forms of one tile and stage are separate instantiations: their
+                # launch-weighted average
+                n_l = sum(h.get("launches", 1) for h in hits)
+                e = {c: sum(h.get(c, 0) * h.get("launches", 1) for h in hits) / n_l
+                     for c in set().union(*hits) if c != "launches"}
+                e["launches"] = n_l
                 tr = e.get("traffic_bytes")
                 mf = e.get("SQ_INSTS_MFMA") or 0
                 # MFMA busy share of the SIMD-cycles of the dispatch: GRBM_GUI_ACTIVE sums the 8 XCDs'
