@@ -630,6 +630,7 @@ constexpr int PA_R = 16;             // max replica rows of dW[1] (and arrival c
 constexpr int PA_R_DEFAULT = 8;      // rows used (CWT_ADAPT_PR: 2, 4, 8 or 16)
 constexpr int PA_NSLOT = 4;          // accumulator slots (step s adds into s % 4)
 constexpr int PA_EW = 4;             // episodes one workgroup's units may span
+constexpr bool PA_HIRES2 = true;     // the lockstep pair's hi-res passes interleaved (hires_pass2)
 #ifndef PA_CNT_STRIDE_WORDS
 #define PA_CNT_STRIDE_WORDS 32
 #endif
@@ -1166,6 +1167,70 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
         }
       }
     };
+    // The lockstep pair's two hi-res passes in ONE loop body (round 5): the per-pixel chain (bilinear
+    // z from LDS -> exp / rcp -> two DPP octet sums -> LDS) is latency-bound, and two independent
+    // units' chains interleave where two consecutive passes ran back to back (stamps, profiles/r5:
+    // 1.94 us for the pair against 0.95 for one unit).  The rare extra-row terms (the last row
+    // pair's row S - 1, e2 = 1) run for both units when either has them; a unit without them has
+    // labels 255 there, i.e. a zero gradient, as in the single pass.
+    auto hires_pass2 = [&](const PaUnit& qa, int ewa, unsigned ya, const float* zda, float (*P0a)[2][PA_NC + 1],
+                           float (*P1a)[2][PA_NC + 1], const PaUnit& qb, int ewb, unsigned yb, const float* zdb,
+                           float (*P0b)[2][PA_NC + 1], float (*P1b)[2][PA_NC + 1]) {
+      const bool extra = (qa.extra_row || qb.extra_row) && i_row == 0;
+      const float wf[2] = {wfg_l[ewa], wfg_l[ewb]};
+      int ln = lane;
+      asm volatile("" : "+v"(ln), "+v"(ya), "+v"(yb));
+      const unsigned yl[2] = {ya, yb};
+      const float* zdp[2] = {zda, zdb};
+      float (*P0p[2])[2][PA_NC + 1] = {P0a, P0b};
+      float (*P1p[2])[2][PA_NC + 1] = {P1a, P1b};
+      const int x0[2] = {qa.x0, qb.x0};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (k == 1 && a.uc < 16) break;
+        int slot_x[2], xi0[2], xi1[2];
+        float lx0[2], lx1[2], sa[2][2], sb[2][2];
+#pragma unroll
+        for (int uu = 0; uu < 2; ++uu) {
+          const int X = 8 * x0[uu] + 64 * (wv & 1) + 128 * k + ln;
+          slot_x[uu] = 8 * (wv & 1) + 16 * k + (ln >> 3);
+          const int ix = min(X >> 3, a.w - 1);
+          xi0[uu] = min(ix - x0[uu], PA_NC - 1);
+          xi1[uu] = (ix < a.w - 1) ? min(xi0[uu] + 1, PA_NC - 1) : xi0[uu];
+          lx1[uu] = (float)(X & 7) * 0.125f;
+          lx0[uu] = 1.f - lx1[uu];
+          sa[uu][1] = sb[uu][1] = 0.f;
+        }
+#pragma unroll
+        for (int e2 = 0; e2 < 2; ++e2) {
+          if (e2 == 1 && !extra) break;
+#pragma unroll
+          for (int uu = 0; uu < 2; ++uu) {
+            const float* zd_ = zdp[uu];
+            const int y = (int)((yl[uu] >> (8 * (2 * k + e2))) & 255u);
+            float gv = 0.f;
+            if (y != 255) {
+              const float dd = e2 ? (lx0[uu] * zd_[PA_NC + xi0[uu]] + lx1[uu] * zd_[PA_NC + xi1[uu]])
+                                  : ly0 * (lx0[uu] * zd_[xi0[uu]] + lx1[uu] * zd_[xi1[uu]]) +
+                                        ly1 * (lx0[uu] * zd_[PA_NC + xi0[uu]] + lx1[uu] * zd_[PA_NC + xi1[uu]]);
+              const float p1 = __builtin_amdgcn_rcpf(1.f + __expf(-dd));
+              gv = ((y == 1) ? wf[uu] : 1.f) * (p1 - (float)y);
+            }
+            sa[uu][e2] = octet_sum(lx0[uu] * gv);
+            sb[uu][e2] = octet_sum(lx1[uu] * gv);
+          }
+        }
+        if ((lane & 7) == 0) {
+#pragma unroll
+          for (int uu = 0; uu < 2; ++uu) {
+            P0p[uu][i_row][0][slot_x[uu]] = ly0 * sa[uu][0];
+            P1p[uu][i_row][0][slot_x[uu] + 1] = ly0 * sb[uu][0];
+            P0p[uu][i_row][1][slot_x[uu]] = ly1 * sa[uu][0] + sa[uu][1];
+            P1p[uu][i_row][1][slot_x[uu] + 1] = ly1 * sb[uu][0] + sb[uu][1];
+          }
+        }
+      }
+    };
     auto gs_of = [&](int tt, float (*P0p)[2][PA_NC + 1], float (*P1p)[2][PA_NC + 1]) {
       const int ri = tt >> 5, xi = tt & 31;
       float gsum = 0.f;
@@ -1210,8 +1275,13 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       }
       lds_barrier();
       stamp(1);
-      hires_pass(qa, ewa, pack_y(cur.y), zd_u[0], P0_u[0], P1_u[0]);
-      if (has_b) hires_pass(qb, ewb, y2p, zd_u[NU - 1], P0_u[NU - 1], P1_u[NU - 1]);
+      if (PA_HIRES2) {  // both units' passes interleaved (unit B absent: labels 255, zero gradient)
+        hires_pass2(qa, ewa, pack_y(cur.y), zd_u[0], P0_u[0], P1_u[0], qb, ewb, has_b ? y2p : 0xFFFFFFFFu,
+                    zd_u[NU - 1], P0_u[NU - 1], P1_u[NU - 1]);
+      } else {
+        hires_pass(qa, ewa, pack_y(cur.y), zd_u[0], P0_u[0], P1_u[0]);
+        if (has_b) hires_pass(qb, ewb, y2p, zd_u[NU - 1], P0_u[NU - 1], P1_u[NU - 1]);
+      }
       lds_barrier();
       if (t < 2 * PA_NPX) {
         const int uu = t >> 6, tt = t & 63;

@@ -30,6 +30,9 @@ ep = syn.make_episode(2021, 0, S, n)
 f = torch.from_numpy(syn.normal(2021, "f", (n, 512, h, h), 0.1)).abs().to(dev).contiguous(
     memory_format=torch.channels_last)
 lbl = torch.from_numpy(ep["s_label"][0]).to(dev)
+# CWT_STAMP_UNITS=2: the episode pipeline's adapt geometry (cwt_ctx_set_adapt_units; <5> at 1-shot 473^2)
+if os.environ.get("CWT_STAMP_UNITS"):
+    _lib.check(_lib.lib().cwt_ctx_set_adapt_units(_lib.ctx(0), int(os.environ["CWT_STAMP_UNITS"])), "units")
 W = torch.zeros(2, 512, device=dev)
 for _ in range(3):
     inner_adapt(f, lbl, W, 0.1, iters)
@@ -74,4 +77,5 @@ ph["clock GHz"] = round(clk / 10.0, 3)
 print(json.dumps(ph, indent=1))
 out = os.path.join(ROOT, "gpurun_out")
 if os.path.isdir(out):
-    json.dump(ph, open(os.path.join(out, f"persist_stamps_{n}shot_{S}.json"), "w"), indent=1)
+    json.dump(ph, open(os.path.join(out, f"persist_stamps_{n}shot_{S}_u{os.environ.get('CWT_STAMP_UNITS', 0)}.json"),
+                       "w"), indent=1)
