@@ -131,10 +131,13 @@ struct ConvLayer {
   float* w = nullptr;  // device, packed [Co][k][k][Ci] (stem conv1: [ci][ky][kx][co])
   __bf16* w_s = nullptr;   // S-layout [Co][K/32][hi 32 | lo 32] of the same split (conv_x3s.hip)
   __bf16* w_l = nullptr;   // x6: the third term w - hi - lo, [Co][K/32][32] (exact in bf16)
-  // x6 Winograd F(2x2,3x3) (stride-1 3x3, Ci >= 256; wino.hip): U = G g G^T per transformed
-  // position, [16][Co][Ci] split like w_s / w_l
+  // x6 Winograd forms (stride-1 3x3, Ci >= 256; wino.hip): U = G g G^T per transformed
+  // position, [P][Co][Ci] split like w_s / w_l; wino_s / wino_l F(2x2,3x3) (P = 16), wino4_s /
+  // wino4_l F(4x4,3x3) (P = 36)
   __bf16* wino_s = nullptr;
   __bf16* wino_l = nullptr;
+  __bf16* wino4_s = nullptr;
+  __bf16* wino4_l = nullptr;
   __bf16* w_b = nullptr;   // plain bf16 [Co][K], K in packed_k64 order (bf16 conv stack; Ci % 64 == 0)
   float* scale = nullptr;
   float* shift = nullptr;
@@ -483,21 +486,24 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
     // 16 thin GEMMs and the transforms measured slower than the direct conv: 35.9 vs 29.1 us,
     // profiles/r5/sweeps)
     if (k == 3 && stride == 1 && Ci >= 256 && Ci % 32 == 0) {
-      const size_t n = (size_t)16 * Co * Ci;
-      void *U = nullptr, *us = nullptr, *ul = nullptr;
-      CWT_HIP(hipMalloc(&us, n * 4));
-      bb->allocs.push_back(us);
-      CWT_HIP(hipMalloc(&ul, n * 2));
-      bb->allocs.push_back(ul);
-      CWT_HIP(hipMalloc(&U, n * 4));
-      rc = launch_wino_weights(L->w, Co, Ci, (float*)U, nullptr);
-      if (!rc) rc = launch_split_w3((const float*)U, 16L * Co, Ci, (__bf16*)us, (__bf16*)ul, nullptr);
-      const hipError_t e = hipDeviceSynchronize();
-      (void)hipFree(U);
-      if (rc) return rc;
-      if (e != hipSuccess) return fail((int)e, "winograd weight transform");
-      L->wino_s = (__bf16*)us;
-      L->wino_l = (__bf16*)ul;
+      for (const int m : {2, 4}) {
+        const int P = (m + 2) * (m + 2);
+        const size_t n = (size_t)P * Co * Ci;
+        void *U = nullptr, *us = nullptr, *ul = nullptr;
+        CWT_HIP(hipMalloc(&us, n * 4));
+        bb->allocs.push_back(us);
+        CWT_HIP(hipMalloc(&ul, n * 2));
+        bb->allocs.push_back(ul);
+        CWT_HIP(hipMalloc(&U, n * 4));
+        rc = launch_wino_weights(L->w, Co, Ci, (float*)U, nullptr, m);
+        if (!rc) rc = launch_split_w3((const float*)U, (long)P * Co, Ci, (__bf16*)us, (__bf16*)ul, nullptr);
+        const hipError_t e = hipDeviceSynchronize();
+        (void)hipFree(U);
+        if (rc) return rc;
+        if (e != hipSuccess) return fail((int)e, "winograd weight transform");
+        (m == 2 ? L->wino_s : L->wino4_s) = (__bf16*)us;
+        (m == 2 ? L->wino_l : L->wino4_l) = (__bf16*)ul;
+      }
     }
     if (Ci % 64 == 0) {  // plain bf16 operand of the bf16 conv stack, K in packed_k64 order
       std::vector<uint16_t> b16(packed.size());
@@ -677,20 +683,32 @@ static ConvArgs make_args(const ConvCall& c) {
   return a;
 }
 
-// One stride-1 3x3 conv (dilation d = padding) in the Winograd form on the x6 matrix-core
-// arithmetic (wino.hip): input transform -> 16 batched GEMMs (conv_igemm_x6, batch 16) -> output
-// transform with the conv's BN / residual / ReLU.  us / ul: the layer's wino_s / wino_l; bm > 0
-// overrides the GEMMs' tile (bm = 1000 * variant + rows, as cwt_debug_conv_s).
-static int run_wino_conv(cwt_ctx* ctx, const float* x, int N, int H, int W, int Ci, int Co, int d, const __bf16* us,
-                         const __bf16* ul, const float* scale, const float* shift, const float* res, int res_ld,
-                         int relu, float* y, int y_ld, int y_off, int stage, hipStream_t st, int bm = 0, int bn = 0) {
-  const WinoGeom g = wino_geom(N, H, W, d);
+// The Winograd output tile the x6 stack takes for a stride-1 3x3 conv (Ci >= 256) by default
+static int wino_tile_default(int Ci, int Co, int d, int Ho) {
+  (void)Ci;
+  (void)Co;
+  (void)d;
+  (void)Ho;
+  return 4;
+}
+
+// One stride-1 3x3 conv (dilation d = padding) in the Winograd form F(m x m, 3x3) on the x6
+// matrix-core arithmetic (wino.hip): input transform -> P = (m+2)^2 batched GEMMs
+// (conv_igemm_x6, batch P) -> output transform with the conv's BN / residual / ReLU.  us / ul: the
+// layer's wino_s / wino_l (m = 2) or wino4_s / wino4_l (m = 4); bm > 0 overrides the GEMMs' tile
+// (bm = 1000 * variant + rows, as cwt_debug_conv_s).
+static int run_wino_conv(cwt_ctx* ctx, const float* x, int N, int H, int W, int Ci, int Co, int d, int m,
+                         const __bf16* us, const __bf16* ul, const float* scale, const float* shift, const float* res,
+                         int res_ld, int relu, float* y, int y_ld, int y_off, int stage, hipStream_t st, int bm = 0,
+                         int bn = 0) {
+  if (m != 2 && m != 4) return fail(CWT_EARG, "winograd: output tile must be 2 or 4");
+  const WinoGeom g = wino_geom(N, H, W, d, m);
   if (g.T * Ci * 4 >= (1L << 31) || g.T * Co * 4 >= (1L << 31)) return fail(CWT_EARG, "winograd: plane too large");
   void *V, *Mb;
   const __bf16* zero = nullptr;
   int rc;
-  if ((rc = ensure_ws(ctx, "wino.V", (size_t)16 * g.T * Ci * 4, &V)) ||
-      (rc = ensure_ws(ctx, "wino.M", (size_t)16 * g.T * Co * 4, &Mb)) || (rc = zero_line(ctx, &zero)))
+  if ((rc = ensure_ws(ctx, "wino.V", (size_t)g.P * g.T * Ci * 4, &V)) ||
+      (rc = ensure_ws(ctx, "wino.M", (size_t)g.P * g.T * Co * 4, &Mb)) || (rc = zero_line(ctx, &zero)))
     return rc;
   if ((rc = launch_wino_in(x, g, Ci, (float*)V, st))) return rc;
   ConvSArgs a;
@@ -715,19 +733,21 @@ static int run_wino_conv(cwt_ctx* ctx, const float* x, int N, int H, int W, int 
   a.M = (int)g.T;
   a.K = Ci;
   a.part = (float*)Mb;
-  a.batch = 16;
+  a.batch = g.P;
   a.xs_bstride = g.T * Ci * 4;
   a.ws_bstride = (long)Co * Ci * 2;
   a.wl_bstride = (long)Co * Ci;
-  ConvPlan p = plan_conv_x6_batched(a.M, Co, Ci, 16);
+  ConvPlan p = plan_conv_x6_batched(a.M, Co, Ci, g.P);
   if (bm > 0) {
     p.var = bm / 1000;
     p.bm = bm % 1000;
     p.bn = bn;
     if (Co % p.bn) return fail(CWT_EARG, "winograd GEMM tile: Co % bn");
   }
-  (void)stage;  // the batched GEMMs are the stage-7 instantiations (their own rocprofv3 statistics)
-  if ((rc = launch_conv_x3s(a, p, 7, nullptr, 0, st, 6))) return rc;
+  // the batched GEMMs are the stage-7 (F(2x2)) / stage-8 (F(4x4)) instantiations: their own
+  // rocprofv3 statistics
+  (void)stage;
+  if ((rc = launch_conv_x3s(a, p, m == 4 ? 8 : 7, nullptr, 0, st, 6))) return rc;
   return launch_wino_out((const float*)Mb, g, Co, scale, shift, res, res_ld, relu, y, y_ld, y_off, st);
 }
 
@@ -905,7 +925,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   // the Winograd form: stride-1 3x3 layers whose transformed weights were built at load, on
   // images of a pixel stride equal to their channels
   auto c_wino = [&](const ConvCall& c) {
-    return c.L->wino_s && c.L->k == 3 && c.L->stride == 1 && c.L->pad == c.L->dil && c.x_ld == c.L->Ci;
+    return c.L->wino_s && c.L->wino4_s && c.L->k == 3 && c.L->stride == 1 && c.L->pad == c.L->dil && c.x_ld == c.L->Ci;
   };
   auto run_call = [&](size_t i) -> int {
     ConvArgs a = make_args(calls[i]);
@@ -918,11 +938,14 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
       a.relu = 0;
       if (!keep_res) a.res = nullptr;
     }
-    static const bool wino_env = !(getenv("CWT_WINO") && getenv("CWT_WINO")[0] == '0');  // A/B: 0 = direct
-    const bool wino = x6 && wino_env && c_wino(calls[i]);
+    // A/B: CWT_WINO=0 every conv direct, 2 / 4 every Winograd-eligible conv in F(2x2) / F(4x4)
+    static const int wino_env = getenv("CWT_WINO") ? atoi(getenv("CWT_WINO")) : -1;
+    const bool wino = x6 && wino_env != 0 && c_wino(calls[i]);
+    const int wm = !wino ? 0 : wino_env == 2 || wino_env == 4 ? wino_env : wino_tile_default(a.Ci, a.Co, a.dil, a.Ho);
     // the Winograd form's record names its batched GEMM's plan; its FLOPs stay the direct conv's
     // (algorithmic: the roofline prices the conv, not the form that computes it)
-    const ConvPlan pl = wino ? plan_conv_x6_batched((int)wino_geom(a.N, a.Hi, a.Wi, a.dil).T, a.Co, a.Ci, 16) : plans[i];
+    const WinoGeom wg = wino_geom(a.N, a.Hi, a.Wi, a.dil, wm ? wm : 2);
+    const ConvPlan pl = wino ? plan_conv_x6_batched((int)wg.T, a.Co, a.Ci, wg.P) : plans[i];
     const double flops = 2.0 * a.M * a.Co * a.K;
     // algorithmic bytes: every operand once; 4 B per element (fp32 or the bf16x3 S-layout),
     // 2 B for the bf16 stack's activations and weights (its fp32 bottleneck output: 4 B)
@@ -930,7 +953,7 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     const double bytes = eb * ((double)a.N * a.Hi * a.Wi * a.Ci + (double)a.Co * a.K) +
                          ob * ((double)a.M * a.Co + (a.res ? (double)a.M * a.Co : 0.0));
     Prof p(ctx, st,
-           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : wino ? "conv_igemm_x6w<"
+           std::string(b16 ? "conv_igemm_b16<" : conv_split ? "conv_igemm_x3s<" : wino ? (wm == 4 ? "conv_igemm_x6w4<" : "conv_igemm_x6w<")
                        : x6 ? "conv_igemm_x6<" : f32d ? "conv_igemm_f32d<" : "conv_igemm_f32<") +
                std::to_string(pl.bm) + "," +
                std::to_string(pl.bn) + "," +
@@ -942,8 +965,9 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
     int r;
     if (wino) {
       const ConvCall& c = calls[i];
-      r = run_wino_conv(ctx, c.x, a.N, a.Hi, a.Wi, a.Ci, a.Co, a.dil, c.L->wino_s, c.L->wino_l, a.scale, a.shift,
-                        a.res, c.res_ld, a.relu, c.y, c.y_ld, c.y_off, c.stage, st);
+      r = run_wino_conv(ctx, c.x, a.N, a.Hi, a.Wi, a.Ci, a.Co, a.dil, wm, wm == 4 ? c.L->wino4_s : c.L->wino_s,
+                        wm == 4 ? c.L->wino4_l : c.L->wino_l, a.scale, a.shift, a.res, c.res_ld, a.relu, c.y, c.y_ld,
+                        c.y_off, c.stage, st);
     } else if (dma) {
       ConvSArgs sa;
       memset(&sa, 0, sizeof(sa));
@@ -2617,9 +2641,10 @@ int cwt_debug_conv_x6w(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int 
                        const float* scale, const float* shift, int Co, int k, int stride, int pad, int dil,
                        const float* res, int res_ld, int relu, float* y, int y_ld, int y_off, int bm, int bn,
                        int nsplit, void* stream) {
-  (void)nsplit;
+  const int m = nsplit == 4 ? 4 : 2;  // nsplit selects the output tile: 4 = F(4x4,3x3), else F(2x2,3x3)
   if (!ctx) return fail(CWT_EARG, "ctx is NULL");
   CWT_CHECK(x && w_packed && scale && shift && y, "null buffer");
+  CWT_CHECK(nsplit == 0 || nsplit == 1 || nsplit == 2 || nsplit == 4, "nsplit (the Winograd tile) must be 0, 2 or 4");
   CWT_CHECK(k == 3 && stride == 1 && pad == dil && dil >= 1, "winograd form: 3x3, stride 1, padding = dilation");
   CWT_CHECK(Ci % 32 == 0 && Co % 64 == 0 && N >= 1 && Hi >= 1 && Wi >= 1, "need Ci % 32 == 0, Co % 64 == 0");
   CWT_CHECK(y_ld >= y_off + Co && y_ld % 4 == 0 && y_off % 4 == 0 && (!res || res_ld % 4 == 0), "bad strides");
@@ -2627,17 +2652,18 @@ int cwt_debug_conv_x6w(cwt_ctx* ctx, const float* x, int N, int Hi, int Wi, int 
             "bad tile");
   CWT_HIP(hipSetDevice(ctx->device));
   const hipStream_t st = (hipStream_t)stream;
-  const size_t n = (size_t)16 * Co * Ci;
+  const int P = (m + 2) * (m + 2);
+  const size_t n = (size_t)P * Co * Ci;
   void *U, *us, *ul;
   int rc;
   if ((rc = ensure_ws(ctx, "dbg.wU", n * 4, &U)) || (rc = ensure_ws(ctx, "dbg.wUs", n * 4, &us)) ||
       (rc = ensure_ws(ctx, "dbg.wUl", n * 2, &ul)))
     return rc;
-  if ((rc = launch_wino_weights(w_packed, Co, Ci, (float*)U, st)) ||
-      (rc = launch_split_w3((const float*)U, 16L * Co, Ci, (__bf16*)us, (__bf16*)ul, st)))
+  if ((rc = launch_wino_weights(w_packed, Co, Ci, (float*)U, st, m)) ||
+      (rc = launch_split_w3((const float*)U, (long)P * Co, Ci, (__bf16*)us, (__bf16*)ul, st)))
     return rc;
-  return run_wino_conv(ctx, x, N, Hi, Wi, Ci, Co, dil, (const __bf16*)us, (const __bf16*)ul, scale, shift, res, res_ld,
-                       relu, y, y_ld, y_off, 0, st, bm, bn);
+  return run_wino_conv(ctx, x, N, Hi, Wi, Ci, Co, dil, m, (const __bf16*)us, (const __bf16*)ul, scale, shift, res,
+                       res_ld, relu, y, y_ld, y_off, 0, st, bm, bn);
 }
 
 int cwt_debug_conv_b16(cwt_ctx* ctx, const void* xs, int N, int Hi, int Wi, int Ci, const void* ws, const float* scale,

@@ -99,8 +99,9 @@ static void launch_tiles_x6_stage(const ConvSArgs& a, const ConvPlan& p, dim3 gr
 #undef X6
 }
 
-// STAGE names the instantiation for rocprofv3 (0 stem .. 6 bottleneck as the other kernels; 7 the
-// Winograd form's batched GEMMs, so their counters are not averaged with the direct convs')
+// STAGE names the instantiation for rocprofv3 (0 stem .. 6 bottleneck as the other kernels; 7 / 8
+// the F(2x2) / F(4x4) Winograd forms' batched GEMMs, so their counters are not averaged with the
+// direct convs')
 void launch_tiles_x6(int stage, const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
   switch (stage) {
     case 0: launch_tiles_x6_stage<0>(a, p, grid, st); break;
@@ -110,24 +111,26 @@ void launch_tiles_x6(int stage, const ConvSArgs& a, const ConvPlan& p, dim3 grid
     case 4: launch_tiles_x6_stage<4>(a, p, grid, st); break;
     case 5: launch_tiles_x6_stage<5>(a, p, grid, st); break;
     case 6: launch_tiles_x6_stage<6>(a, p, grid, st); break;
-    default: launch_tiles_x6_stage<7>(a, p, grid, st); break;
+    case 7: launch_tiles_x6_stage<7>(a, p, grid, st); break;
+    default: launch_tiles_x6_stage<8>(a, p, grid, st); break;
   }
 }
 
+// batch: 0 for a direct conv's GEMM, else the Winograd form's GEMM count (16 or 36), M its tiles
 struct MeasuredPlanS6 {
-  int M, Co, K, bm, bn, nsplit, var;
+  int M, Co, K, bm, bn, nsplit, var, batch;
 };
 
 static const MeasuredPlanS6 kMeasuredPlansX6[] = {
 #include "conv_plans_x6.inc"
-    {0, 0, 0, 0, 0, 0, 0}};
+    {0, 0, 0, 0, 0, 0, 0, 0}};
 
 // fp32 width on the bf16 matrix cores (conv_igemm_x6): 32-deep K-tiles over f32d's operands; its
 // own measured table (conv_plans_x6.inc, tools/conv_s_sweep.py --prec 6), else the heuristic.
 ConvPlan plan_conv_x6(int M, int Co, int K) {
   const int ktiles = K / 32;
   for (const MeasuredPlanS6& e : kMeasuredPlansX6)
-    if (e.M == M && e.Co == Co && e.K == K && e.bn > 0 && Co % e.bn == 0) {
+    if (e.batch == 0 && e.M == M && e.Co == Co && e.K == K && e.bn > 0 && Co % e.bn == 0) {
       ConvPlan p;
       p.bm = e.bm;
       p.bn = e.bn;
@@ -139,13 +142,13 @@ ConvPlan plan_conv_x6(int M, int Co, int K) {
   return plan_heuristic_s(M, Co, ktiles);
 }
 
-// The Winograd path's 16 batched GEMMs [M = tiles][K = Ci] x [Ci][Co]: the measured table (keyed
-// like the direct convs; tile counts M never collide with them), else the largest tile giving
-// >= 200 workgroups over the whole batch, no split-K
+// The Winograd forms' batched GEMMs [M = tiles][K = Ci] x [Ci][Co] (batch 16 or 36): the
+// measured table (entries carrying the batch), else the largest tile giving >= 200 workgroups
+// over the whole batch, no split-K
 ConvPlan plan_conv_x6_batched(int M, int Co, int K, int batch) {
   const int ktiles = K / 32;
   for (const MeasuredPlanS6& e : kMeasuredPlansX6)
-    if (e.M == M && e.Co == Co && e.K == K && e.bn > 0 && Co % e.bn == 0 && e.nsplit == 1) {
+    if (e.batch == batch && e.M == M && e.Co == Co && e.K == K && e.bn > 0 && Co % e.bn == 0 && e.nsplit == 1) {
       ConvPlan p;
       p.bm = e.bm;
       p.bn = e.bn;

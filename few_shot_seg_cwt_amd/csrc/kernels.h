@@ -124,15 +124,17 @@ ConvPlan plan_conv_x3s(int M, int Co, int K);
 ConvPlan plan_conv_b16(int M, int Co, int K);
 ConvPlan plan_conv_f32d(int M, int Co, int K);
 ConvPlan plan_conv_x6(int M, int Co, int K);
-ConvPlan plan_conv_x6_batched(int M, int Co, int K, int batch);
-// Winograd F(2x2, 3x3) for the x6 path's stride-1 3x3 convs (wino.hip)
+ConvPlan plan_conv_x6_batched(int M, int Co, int K, int batch);  // the Winograd forms' GEMMs
+// Winograd F(2x2, 3x3) and F(4x4, 3x3) for the x6 path's stride-1 3x3 convs (wino.hip)
 struct WinoGeom {
   int N, H, W, d;  // image, dilation (= padding)
-  int TY, TX;      // 2x2 output tiles per dilation sub-grid
+  int m;           // output tile edge: 2 (F(2x2,3x3), 16 positions) or 4 (F(4x4,3x3), 36)
+  int P;           // transformed positions (m + 2)^2 = the batched GEMMs' count
+  int TY, TX;      // m x m output tiles per dilation sub-grid
   long T;          // N * d * d * TY * TX
 };
-WinoGeom wino_geom(int N, int H, int W, int d);
-int launch_wino_weights(const float* w_packed, int Co, int Ci, float* U, hipStream_t st);
+WinoGeom wino_geom(int N, int H, int W, int d, int m = 2);
+int launch_wino_weights(const float* w_packed, int Co, int Ci, float* U, hipStream_t st, int m = 2);
 int launch_wino_in(const float* x, const WinoGeom& g, int Ci, float* V, hipStream_t st);
 int launch_wino_out(const float* Mb, const WinoGeom& g, int Co, const float* scale, const float* shift, const float* res,
                     int res_ld, int relu, float* y, int y_ld, int y_off, hipStream_t st);

@@ -348,9 +348,10 @@ def test_conv_x6_channel_strided_out():
     assert float((y.double() - ref).abs().max() / ref.abs().max()) < TOL_X6
 
 
-# ---------------------------------------------------------------- x6 Winograd F(2x2, 3x3) (wino.hip)
-# the x6 stack's form for stride-1 3x3 convs: transforms in fp32 (+-1 coefficients; G g G^T in
-# double, rounded once), 16 batched x6 GEMMs; against float64 at the same bar as the direct x6
+# ------------------------------------------------ x6 Winograd F(2x2, 3x3) and F(4x4, 3x3) (wino.hip)
+# the x6 stack's forms for stride-1 3x3 convs: transforms in fp32 (small integer coefficients;
+# G g G^T in double, rounded once), 16 / 36 batched x6 GEMMs; against float64 at the same bar as
+# the direct x6 (wtile = the entry's nsplit argument: the output tile edge m)
 WINO_CASES = [  # N, Ci, Co, Hi, dil, residual
     (2, 64, 64, 37, 1, False),
     (2, 128, 128, 15, 1, True),
@@ -359,6 +360,8 @@ WINO_CASES = [  # N, Ci, Co, Hi, dil, residual
     (1, 512, 128, 13, 4, False),
     (1, 256, 64, 9, 4, True),       # sub-grids of 3 and 2 rows: half-empty edge tiles
     (1, 64, 512, 19, 1, True),
+    (1, 256, 128, 23, 1, True),     # 23 rows: the last 4x4 tile row three quarters empty
+    (2, 128, 64, 30, 2, False),     # sub-grids of 15 rows: F(4x4) tiles ragged, F(2x2) exact-ish
 ]
 WINO_TILES = [(0, 0), (256, 256), (256, 128), (128, 256), (128, 128), (128, 64), (64, 128), (64, 64), (4128, 128),
               (1064, 64), (2128, 128)]
@@ -366,7 +369,8 @@ WINO_TILES = [(0, 0), (256, 256), (256, 128), (128, 256), (128, 128), (128, 64),
 
 @pytest.mark.parametrize("case", WINO_CASES, ids=lambda c: "x".join(map(str, c)))
 @pytest.mark.parametrize("tile", WINO_TILES, ids=lambda p: f"{p[0]}x{p[1]}")
-def test_conv_x6_winograd(case, tile):
+@pytest.mark.parametrize("wtile", [2, 4], ids=lambda m: f"F{m}")
+def test_conv_x6_winograd(case, tile, wtile):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     N, Ci, Co, Hi, dil, has_res = case
@@ -379,18 +383,41 @@ def test_conv_x6_winograd(case, tile):
     scale = torch.from_numpy(syn.uniform(1, "s" + tag, (Co,), 0.5, 1.5))
     shift = torch.from_numpy(syn.normal(1, "b" + tag, (Co,), 0.1))
     res = torch.from_numpy(syn.normal(1, "r" + tag, (N, Co, Hi, Hi), 1.0)) if has_res else None
-    y = run_conv_f32d(x, w, scale, shift, 1, dil, dil, res, bm=bm, bn=bn, entry="cwt_debug_conv_x6w")
+    y = run_conv_f32d(x, w, scale, shift, 1, dil, dil, res, bm=bm, bn=bn, nsplit=wtile, entry="cwt_debug_conv_x6w")
     ref = ref_conv(x, w, scale, shift, 1, dil, dil, res, True)
     err = float((y.double() - ref).abs().max() / ref.abs().max())
     assert err < TOL_X6, err
 
 
-def test_conv_x6_winograd_channel_strided_out():
+@pytest.mark.parametrize("wtile", [2, 4], ids=lambda m: f"F{m}")
+def test_conv_x6_winograd_channel_strided_out(wtile):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     x = torch.from_numpy(syn.normal(2, "xw", (2, 128, 11, 11), 1.0))
     w = torch.from_numpy(syn.normal(2, "ww", (128, 128, 3, 3), 0.04))
     scale, shift = torch.ones(128), torch.zeros(128)
-    y = run_conv_f32d(x, w, scale, shift, 1, 2, 2, None, relu=False, y_pad=256, y_off=128, entry="cwt_debug_conv_x6w")
+    y = run_conv_f32d(x, w, scale, shift, 1, 2, 2, None, relu=False, y_pad=256, y_off=128, nsplit=wtile,
+                      entry="cwt_debug_conv_x6w")
     ref = ref_conv(x, w, scale, shift, 1, 2, 2, None, False)
     assert float((y.double() - ref).abs().max() / ref.abs().max()) < TOL_X6
+
+
+@pytest.mark.parametrize("wtile", [2, 4], ids=lambda m: f"F{m}")
+def test_conv_x6_winograd_error_vs_fp32_conv(wtile):
+    """Each Winograd form's error against float64 beside a plain fp32 conv's (torch on the CPU),
+    on a bottleneck-like conv (post-ReLU input, Ci = 512): the transforms' rounding stays within a
+    small multiple of the fp32 conv's own accumulation error."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    g = torch.Generator().manual_seed(11)
+    x = torch.relu(torch.randn((1, 512, 24, 24), generator=g))
+    w = torch.randn((128, 512, 3, 3), generator=g) * (2.0 / (512 * 9)) ** 0.5
+    one, zero = torch.ones(128), torch.zeros(128)
+    y = run_conv_f32d(x, w, one, zero, 1, 1, 1, None, relu=False, nsplit=wtile, entry="cwt_debug_conv_x6w")
+    ref = ref_conv(x, w, one, zero, 1, 1, 1, None, False)
+    y32 = F.conv2d(x, w, None, 1, 1, 1).double()
+    mx = float(ref.abs().max())
+    e_w = float((y.double() - ref).abs().max()) / mx
+    e_32 = float((y32 - ref).abs().max()) / mx
+    print(f"F({wtile}x{wtile},3x3) max err / max|y|: {e_w:.3g}   torch fp32 conv: {e_32:.3g}")
+    assert e_w < max(8 * e_32, 2e-6), (e_w, e_32)

@@ -78,7 +78,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
     for name, cnt, Ci, Co, Hi, k, stride, dil, has_res in shapes(layers, size, n_img):
         if only and name not in only:
             continue
-        if prec == 7 and (k != 3 or stride != 1 or Ci < 128):
+        if prec in (7, 8) and (k != 3 or stride != 1 or Ci < 128):
             continue   # the Winograd form's candidates: stride-1 3x3 layers with Ci >= 128 (used at >= 256)
         pad = dil if k == 3 else 0
         Ho = (Hi + 2 * pad - dil * (k - 1) - 1) // stride + 1
@@ -89,7 +89,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         if prec == 1:   # plain bf16 operands (K order inside a row does not matter for timing)
             xs = x.to(torch.bfloat16).contiguous()
             ws = w.reshape(Co, K).to(torch.bfloat16).contiguous()
-        elif prec in (0, 6, 7):  # exact fp32 (f32d) / bf16x6 (x6, x6 Winograd): fp32 NHWC and fp32 [Co][K]
+        elif prec in (0, 6, 7, 8):  # exact fp32 (f32d) / bf16x6 (x6, x6 Winograd): fp32 NHWC and fp32 [Co][K]
             xs = x
             ws = w.reshape(Co, K).contiguous()
         else:
@@ -101,7 +101,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         sh = torch.zeros(Co, device=dev)
         r = torch.randn(n_img, Ho, Ho, Co, device=dev) if has_res else None
         rs = None
-        if has_res and prec in (0, 6, 7):
+        if has_res and prec in (0, 6, 7, 8):
             rs = None
         elif has_res and prec == 1:
             rs = r.to(torch.bfloat16).contiguous()
@@ -115,8 +115,11 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
         conv_fn = lib.cwt_debug_conv_b16 if prec == 1 else lib.cwt_debug_conv_s
 
         def new(bm, bn, ns):
-            if prec in (0, 6, 7):
-                fn = {0: lib.cwt_debug_conv_f32d, 6: lib.cwt_debug_conv_x6, 7: lib.cwt_debug_conv_x6w}[prec]
+            if prec in (0, 6, 7, 8):
+                fn = {0: lib.cwt_debug_conv_f32d, 6: lib.cwt_debug_conv_x6, 7: lib.cwt_debug_conv_x6w,
+                      8: lib.cwt_debug_conv_x6w}[prec]
+                if prec in (7, 8):   # the Winograd entry's nsplit argument is its output tile
+                    ns = 4 if prec == 8 else 2
                 return lambda: _lib.check(fn(
                     ctx, _lib.ptr(xs), n_img, Hi, Hi, Ci, _lib.ptr(ws), _lib.ptr(sc), _lib.ptr(sh), Co, k, stride,
                     pad, dil, _lib.ptr(r), Co, 1, _lib.ptr(y), Co, 0, bm, bn, ns, sp))
@@ -132,7 +135,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
                     continue
                 tiles = -(-M // bm) * (Co // bn)
                 for var in variants:
-                    x6v = prec in (6, 7)
+                    x6v = prec in (6, 7, 8)
                     if var == 3 and not (x6v and bm >= 128 and bn >= 128):
                         continue   # x6 only: the WN = 128 wave layouts of the big tiles
                     if var == 5 and not (x6v and (bm, bn) == (128, 128)):
@@ -146,7 +149,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
                     if var == 2 and (bm == 256 or bn == 256):
                         continue   # 8-wave form only for the 128/64 tiles
                     for ns in (1, 2, 4, 8):
-                        if ns > 1 and (prec == 7 or (K // (64 if prec == 1 else 32)) // ns < 4 or tiles * ns > 4096):
+                        if ns > 1 and (prec in (7, 8) or (K // (64 if prec == 1 else 32)) // ns < 4 or tiles * ns > 4096):
                             continue
                         us = timed(new(1000 * var + bm, bn, ns), reps)
                         rows.append({"bm": bm, "bn": bn, "ns": ns, "var": var, "us": round(us, 2),
@@ -159,12 +162,13 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
               f"auto {t_auto:7.1f} ({flops / t_auto / 1e6:6.1f} TF)  best "
               f"{best['bm']}x{best['bn']}s{best['ns']}v{best['var']} {best['us']:7.1f} ({best['tflops']:6.1f} TF)",
               flush=True)
-        if prec == 7:   # the plan table keys the batched GEMMs by (tiles, Co, Ci)
-            d_ = dil
-            TY = (-(-Ho // d_) + 1) // 2
-            M, K = n_img * d_ * d_ * TY * TY, Ci
+        batch = 0
+        if prec in (7, 8):   # the plan table keys the batched GEMMs by (tiles, Co, Ci, batch)
+            d_, m_ = dil, (2 if prec == 7 else 4)
+            TY = (-(-Ho // d_) + m_ - 1) // m_
+            M, K, batch = n_img * d_ * d_ * TY * TY, Ci, (m_ + 2) ** 2
         res_all.append({"cfg": f"{layers}:{size}:{n_img}", "prec": prec, "name": name, "count": cnt, "Ci": Ci, "Co": Co, "k": k,
-                        "Ho": Ho, "M": M, "K": K, "stride": stride, "dil": dil, "res": has_res,
+                        "Ho": Ho, "M": M, "K": K, "batch": batch, "stride": stride, "dil": dil, "res": has_res,
                         "auto_us": round(t_auto, 2), "plans": rows})
         del x, w, wp, xs, ws, r, rs, y, ys
     print(f"sum over the stack: auto {tot_auto:.1f} us, best {tot_best:.1f} us", flush=True)
@@ -178,9 +182,10 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--quick", action="store_true", help="old vs new automatic plan only")
     ap.add_argument("--out", default="conv_s_sweep.json")
-    ap.add_argument("--prec", type=int, default=3, choices=[0, 1, 3, 6, 7],
+    ap.add_argument("--prec", type=int, default=3, choices=[0, 1, 3, 6, 7, 8],
                     help="3 = bf16x3 (x3s), 1 = plain bf16 (b16), 0 = exact fp32 on the LDS-DMA body (f32d), "
-                         "6 = fp32 width on bf16 MFMA (x6), 7 = x6 in the Winograd F(2x2,3x3) form (x6w)")
+                         "6 = fp32 width on bf16 MFMA (x6), 7 = x6 in the Winograd F(2x2,3x3) form (x6w), "
+                         "8 = x6 in the Winograd F(4x4,3x3) form (x6w4)")
     ap.add_argument("--vars", default="0,1,2,4", help="main-loop variants (0 base, 1 prefetch, 2 prefetch 8 waves, 4 128x128 two per CU; 8-11 timing study)")
     ap.add_argument("--only", default="", help="comma list of shape names (default: all)")
     args = ap.parse_args()

@@ -6,9 +6,9 @@ joined with the per-kernel PMC summary of the same build (tools/pmc.sh + tools/p
 Each launch of the per-launch episode (libcwt profile level 2: a hipEvent pair around every
 launch, so each time carries ~1-3 us of event overhead) is priced at
 max(algorithmic FLOPs / matrix roof, algorithmic bytes / 8 TB/s), the roof of its arithmetic:
-x6 / x6w (fp32 width as six bf16 products) 419.4 TF, f32d (v_mfma_f32) 157.3 TF, x3s (bf16x3)
-838.9 TF, b16 2516.6 TF.  The Winograd form (x6w) is priced on the direct conv's FLOPs (the
-algorithm's work; it executes 4/9 of them).  The footer gives the stack's roofline_frac (sum of
+x6 / x6w / x6w4 (fp32 width as six bf16 products) 419.4 TF, f32d (v_mfma_f32) 157.3 TF, x3s (bf16x3)
+838.9 TF, b16 2516.6 TF.  The Winograd forms (x6w F(2x2,3x3), x6w4 F(4x4,3x3)) are priced on the direct conv's
+FLOPs (the algorithm's work; they execute 4/9 and 1/4 of them).  The footer gives the stack's roofline_frac (sum of
 per-launch floors / sum of launch times; bench.py's conv_stack.roofline_frac), then one row per
 kernel instantiation with its PMC averages: HBM traffic per launch (FETCH_SIZE x 2 + WRITE_SIZE,
 gfx950-corrected) against the algorithmic bytes, MFMA busy share, VALU / MFMA / LDS instruction
@@ -20,7 +20,7 @@ import re
 import sys
 
 HBM = 8.0e12
-ROOFS = {"x6w": 2516.6e12 / 6, "x6": 2516.6e12 / 6, "f32d": 157.3e12, "f32": 157.3e12, "x3s": 2516.6e12 / 3,
+ROOFS = {"x6w": 2516.6e12 / 6, "x6w4": 2516.6e12 / 6, "x6": 2516.6e12 / 6, "f32d": 157.3e12, "f32": 157.3e12, "x3s": 2516.6e12 / 3,
          "b16": 2516.6e12}
 
 
@@ -36,8 +36,8 @@ def pmc_key(name):
     m = re.match(r"conv_igemm_(\w+?)<(\d+),(\d+),(\d+)>", name)
     if not m:
         return None
-    if m.group(1) == "x6w":
-        return "x6", m.group(2), m.group(3), "7"
+    if m.group(1) in ("x6w", "x6w4"):   # F(2x2) / F(4x4): stage 7 / 8
+        return "x6", m.group(2), m.group(3), "7" if m.group(1) == "x6w" else "8"
     return m.group(1), m.group(2), m.group(3), m.group(4)
 
 
