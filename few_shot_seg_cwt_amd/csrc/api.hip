@@ -485,8 +485,9 @@ static int load_conv(Backbone* bb, const HostParams& hp, const std::string& wnam
     // the Winograd form's transformed weights: stride-1 3x3 layers with Ci >= 256 (at Ci = 128 the
     // 16 thin GEMMs and the transforms measured slower than the direct conv: 35.9 vs 29.1 us,
     // profiles/r5/sweeps)
-    if (k == 3 && stride == 1 && Ci >= 256 && Ci % 32 == 0) {
+    if (k == 3 && stride == 1 && Ci >= 128 && Ci % 32 == 0) {
       for (const int m : {2, 4}) {
+        if (m == 2 && Ci < 256) continue;
         const int P = (m + 2) * (m + 2);
         const size_t n = (size_t)P * Co * Ci;
         void *U = nullptr, *us = nullptr, *ul = nullptr;
@@ -683,13 +684,13 @@ static ConvArgs make_args(const ConvCall& c) {
   return a;
 }
 
-// The Winograd output tile the x6 stack takes for a stride-1 3x3 conv (Ci >= 256) by default
+// The Winograd output tile the x6 stack takes for a stride-1 3x3 conv by default (0 = the direct
+// conv): F(4x4,3x3) for Ci >= 256, the direct conv below
 static int wino_tile_default(int Ci, int Co, int d, int Ho) {
-  (void)Ci;
   (void)Co;
   (void)d;
   (void)Ho;
-  return 4;
+  return Ci >= 256 ? 4 : 0;
 }
 
 // One stride-1 3x3 conv (dilation d = padding) in the Winograd form F(m x m, 3x3) on the x6
@@ -925,7 +926,8 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
   // the Winograd form: stride-1 3x3 layers whose transformed weights were built at load, on
   // images of a pixel stride equal to their channels
   auto c_wino = [&](const ConvCall& c) {
-    return c.L->wino_s && c.L->wino4_s && c.L->k == 3 && c.L->stride == 1 && c.L->pad == c.L->dil && c.x_ld == c.L->Ci;
+    return (c.L->wino_s || c.L->wino4_s) && c.L->k == 3 && c.L->stride == 1 && c.L->pad == c.L->dil &&
+           c.x_ld == c.L->Ci;
   };
   auto run_call = [&](size_t i) -> int {
     ConvArgs a = make_args(calls[i]);
@@ -939,9 +941,12 @@ static int run_extract(cwt_ctx* ctx, const Backbone* bb, const float* img, int N
       if (!keep_res) a.res = nullptr;
     }
     // A/B: CWT_WINO=0 every conv direct, 2 / 4 every Winograd-eligible conv in F(2x2) / F(4x4)
-    static const int wino_env = getenv("CWT_WINO") ? atoi(getenv("CWT_WINO")) : -1;
-    const bool wino = x6 && wino_env != 0 && c_wino(calls[i]);
-    const int wm = !wino ? 0 : wino_env == 2 || wino_env == 4 ? wino_env : wino_tile_default(a.Ci, a.Co, a.dil, a.Ho);
+    static const int wino_env = getenv("CWT_WINO") && getenv("CWT_WINO")[0] ? atoi(getenv("CWT_WINO")) : -1;
+    int wm = x6 && wino_env != 0 && c_wino(calls[i])
+                 ? (wino_env == 2 || wino_env == 4 ? wino_env : wino_tile_default(a.Ci, a.Co, a.dil, a.Ho))
+                 : 0;
+    if (wm && !(wm == 4 ? calls[i].L->wino4_s : calls[i].L->wino_s)) wm = 0;  // form not built for this layer
+    const bool wino = wm != 0;
     // the Winograd form's record names its batched GEMM's plan; its FLOPs stay the direct conv's
     // (algorithmic: the roofline prices the conv, not the form that computes it)
     const WinoGeom wg = wino_geom(a.N, a.Hi, a.Wi, a.dil, wm ? wm : 2);
