@@ -138,15 +138,6 @@ __device__ __forceinline__ void split3_bf16(const f32x4& x0, const f32x4& x1, bf
   }
 }
 
-// Compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
 // PF = 0: fragments of tile t are read after the barrier that publishes it, then its MFMAs.
 // PF = 1: fragments of tile t+1 are read (into a second register set) right after the barrier
 // that publishes it, BEFORE the MFMAs of tile t, so their LDS latency hides under the MFMAs;
@@ -154,10 +145,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 // barrier, so the ring keeps NSTG - 1 tiles in flight either way.
 // PF bits: 1 fragment prefetch; 2 / 4 timing studies (no MFMAs / no operand DMA); 8 buffer
 // addressing of the operand DMA (every production instantiation sets it); 16 timing study of the
-// x6 WN = 128 forms without the A split (wrong numbers, same data movement and MFMAs); 32 (PREC 6,
-// WN = 128 forms) A direct: each wave loads its own A fragments from global memory into a register
-// ring NSTG - 1 tiles ahead (buffer loads; out-of-image taps and rows past M read as zeros), so a
-// stage holds only the weights' planes (BN x 192 B) and the ring can be deeper.
+// x6 WN = 128 forms without the A split (wrong numbers, same data movement and MFMAs).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF>
 __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   static_assert(PREC == 0 || PREC == 1 || PREC == 3 || PREC == 6,
@@ -166,19 +154,16 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr bool ADIR = PREC == 6 && (PF & 32) != 0;     // A direct (see above)
-  constexpr int LA = ADIR ? 0 : BM / (8 * NW), LB = BN / (8 * NW);  // LDS-DMA pieces (8 rows x 128 B) per wave per tile
-  constexpr int LAX = LA > 0 ? LA : 1;
+  constexpr int LA = BM / (8 * NW), LB = BN / (8 * NW);  // LDS-DMA pieces (8 rows x 128 B) per wave per tile
   // PREC 6: the weights' lo plane, pieces of 16 rows x 64 B; with fewer pieces than waves the
   // surplus waves repeat one (identical bytes to the same LDS slot), so every wave issues the same
   // count per tile (the vmcnt accounting)
   constexpr int NLO = PREC == 6 ? BN / 16 : 0;
   constexpr int LBL = PREC == 6 ? (NLO + NW - 1) / NW : 0;
-  constexpr int LPT = LA + LB + LBL + (ADIR ? 2 * FM : 0);  // vector-memory ops per lane per tile
-  constexpr int A_BYTES = ADIR ? 0 : BM * 128;               // the A rows' place in a stage
-  constexpr int LO_OFF = A_BYTES + BN * 128;                 // the lo plane's place in a stage
-  constexpr int STG_BYTES = A_BYTES + BN * 128 + (PREC == 6 ? BN * 64 : 0);
-  static_assert((ADIR || LA * 8 * NW == BM) && LB * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
+  constexpr int LPT = LA + LB + LBL;
+  constexpr int LO_OFF = (BM + BN) * 128;  // the lo plane's place in a stage
+  constexpr int STG_BYTES = (BM + BN) * 128 + (PREC == 6 ? BN * 64 : 0);
+  static_assert(LA * 8 * NW == BM && LB * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
   static_assert(NSTG >= 2 && NSTG <= 6, "ring depth");
   constexpr int EP_ROWS = WM < 32 ? WM : 32;
   constexpr int EP_LD = WN + 4;  // floats per row of a wave's epilogue tile
@@ -208,7 +193,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   // ---- LDS-DMA source geometry (constant over K) ----
   const int lrow = lane >> 3, lslot = lane & 7;
   const int cblocks = a.Ci >> (PREC == 1 ? 6 : 5);  // 128-B lines per pixel
-  int a_ih0[LAX], a_iw0[LAX], a_pix0[LAX], a_ch[LAX];
+  int a_ih0[LA], a_iw0[LA], a_pix0[LA], a_ch[LA];
   const int HoWo = a.Ho * a.Wo;
 #pragma unroll
   for (int j = 0; j < LA; ++j) {
@@ -253,10 +238,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   // line, no 64-bit address math, no exec-masked branch per piece).  The weights' K offset goes in
   // the uniform soffset.
   __amdgpu_buffer_rsrc_t rsA, rsB, rsL;
-  int a_roff[LAX], b_voff[LB], l_voff[LBL > 0 ? LBL : 1];
-  // A direct: per A fragment i of this wave, the lane's row (lane & 15) and 32-B k piece (lane >> 4)
-  constexpr int FMD = ADIR ? FM : 1;
-  int d_ih0[FMD], d_iw0[FMD], d_roff[FMD];
+  int a_roff[LA], b_voff[LB], l_voff[LBL > 0 ? LBL : 1];
 #if defined(__HIP_DEVICE_COMPILE__)  // the buffer builtins exist for the device pass only
   if constexpr ((PF & 8) != 0) {
     const int cbl = a.Ci >> (PREC == 1 ? 6 : 5);
@@ -265,25 +247,6 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
     rsB = __builtin_amdgcn_make_buffer_rsrc((void*)ws_b, (short)0, (int)((long)a.Co * a.ktiles_total * 128), 0x00020000);
 #pragma unroll
     for (int j = 0; j < LA; ++j) a_roff[j] = (a_pix0[j] * cbl * 64 + a_ch[j]) * 2;
-    if constexpr (ADIR) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int m = m0 + wm * WM + i * 16 + (lane & 15);
-        if (m < a.M) {
-          const int n = m / HoWo;
-          const int rem = m - n * HoWo;
-          const int oh = rem / a.Wo;
-          const int ow = rem - oh * a.Wo;
-          d_ih0[i] = oh * a.stride - a.pad;
-          d_iw0[i] = ow * a.stride - a.pad;
-          d_roff[i] = ((n * a.Hi + d_ih0[i]) * a.Wi + d_iw0[i]) * cbl * 128 + (lane >> 4) * 32;
-        } else {
-          d_ih0[i] = -(1 << 28);
-          d_iw0[i] = 0;
-          d_roff[i] = 0;
-        }
-      }
-    }
 #pragma unroll
     for (int j = 0; j < LB; ++j) b_voff[j] = b_off[j] * 2;
     if constexpr (PREC == 6) {
@@ -300,13 +263,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
     }
   }
 #endif
-  // adst: A direct's register-ring slot for this tile's fragments (nullptr in the other forms);
-  // live = false (A direct only): a tile past the K range, issued as out-of-range buffer reads so
-  // every path through the main loop issues the same vector-memory ops (the compiler's own wait
-  // counts on the register ring then stay exact across the loop's back edge)
-  auto issue = [&](int stg, f32x4 (*adst)[2], bool live = true) {
-    (void)adst;
-    (void)live;
+  auto issue = [&](int stg) {
     if (PF & 4) return;  // timing study: no operand traffic
     char* sb = smem + stg * STG_BYTES;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -322,23 +279,13 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       }
 #pragma unroll
       for (int j = 0; j < LB; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (CWT_LDS void*)(sb + A_BYTES + (wv * LB + j) * 1024), 16,
-                                                 (ADIR && !live) ? (int)0x80000000 : b_voff[j], i_kt * 128, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (CWT_LDS void*)(sb + BM * 128 + (wv * LB + j) * 1024), 16,
+                                                 b_voff[j], i_kt * 128, 0, 0);
       if constexpr (PREC == 6) {
 #pragma unroll
         for (int j = 0; j < LBL; ++j)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsL, (CWT_LDS void*)(sb + LO_OFF + ((wv * LBL + j) % NLO) * 1024), 16,
-                                                   (ADIR && !live) ? (int)0x80000000 : l_voff[j], i_kt * 64, 0, 0);
-      }
-      if constexpr (ADIR) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int ih = d_ih0[i] + dy, iw = d_iw0[i] + dx;
-          const bool in = live && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;
-          const int off = in ? d_roff[i] + uni : (int)0x80000000;
-          adst[i][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off, 0, 0));
-          adst[i][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off + 16, 0, 0));
-        }
+                                                   l_voff[j], i_kt * 64, 0, 0);
       }
       ++i_kt;
       if (++i_kx == a.kw) {
@@ -361,7 +308,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       glds16(src, sb + (wv * LA + j) * 1024);
     }
 #pragma unroll
-    for (int j = 0; j < LB; ++j) glds16(a.ws + b_off[j] + i_kt * 64, sb + A_BYTES + (wv * LB + j) * 1024);
+    for (int j = 0; j < LB; ++j) glds16(a.ws + b_off[j] + i_kt * 64, sb + BM * 128 + (wv * LB + j) * 1024);
     ++i_kt;
     if (++i_kx == a.kw) {
       i_kx = 0;
@@ -390,7 +337,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   const int off_a0 = PREC == 6 ? fr * 128 + (((2 * fk) ^ swz) << 4) : off_hi;
   const int off_a1 = PREC == 6 ? fr * 128 + (((2 * fk + 1) ^ swz) << 4) : off_lo;
   const int off_l = fr * 64 + ((fk ^ ((fr >> 2) & 3)) << 4);
-  const int a_row0 = wm * WM, b_row0 = A_BYTES / 128 + wn * WN;
+  const int a_row0 = wm * WM, b_row0 = BM + wn * WN;
 
   // PREC 6 without fragment prefetch: the B fragments (three pre-split terms each) are read from the
   // stage inside the MFMA loop, one fragment column at a time, after all A fragments are split --
@@ -420,25 +367,6 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       for (int j = 0; j < FN; ++j) F.bo[j] = *(const bf16x8*)(sb + LO_OFF + (wn * WN + j * 16) * 64 + off_l);
     }
   };
-  // the LAZY_B MFMAs of one K-tile: the split A terms against one B column at a time from stage stg
-  auto mfma_lazy = [&](const bf16x8 (&as)[FM][3], int stg) {
-    const char* sb = smem + stg * STG_BYTES;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const char* p = sb + (b_row0 + j * 16) * 128;
-      const bf16x8 bh = *(const bf16x8*)(p + off_hi), bm = *(const bf16x8*)(p + off_lo);
-      const bf16x8 bl = *(const bf16x8*)(sb + LO_OFF + (wn * WN + j * 16) * 64 + off_l);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {  // smallest products first
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][1], bm, acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][2], bh, acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][0], bl, acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][1], bh, acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][0], bm, acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][0], bh, acc[i][j], 0, 0, 0);
-      }
-    }
-  };
   auto mfmas = [&](const Frags& F, int stg) {
     if (PF & 2) {  // timing study: no MFMAs (keep the fragments live)
 #pragma unroll
@@ -449,6 +377,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       return;
     }
     if constexpr (LAZY_B) {  // split every A fragment, then one B column at a time from the stage
+      const char* sb = smem + stg * STG_BYTES;
       bf16x8 as[FM][3];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -460,7 +389,21 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
           split3_bf16(__builtin_bit_cast(f32x4, F.ah[i]), __builtin_bit_cast(f32x4, F.al[i]), as[i][0], as[i][1],
                       as[i][2]);
         }
-      mfma_lazy(as, stg);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const char* p = sb + (b_row0 + j * 16) * 128;
+        const bf16x8 bh = *(const bf16x8*)(p + off_hi), bm = *(const bf16x8*)(p + off_lo);
+        const bf16x8 bl = *(const bf16x8*)(sb + LO_OFF + (wn * WN + j * 16) * 64 + off_l);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {  // smallest products first
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][1], bm, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][2], bh, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][0], bl, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][1], bh, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][0], bm, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as[i][0], bh, acc[i][j], 0, 0, 0);
+        }
+      }
     } else if constexpr (PREC == 6) {  // B: hi = bh, mid = bl, lo = bo (pre-split); A split here
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
@@ -503,42 +446,15 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
     }
   };
 
-  static_assert(!ADIR || LAZY_B, "A direct: the WN = 128 (LAZY_B) forms only");
-  if constexpr (ADIR) {
-    // A register ring of R = NSTG - 1 slots, indexed at compile time (the loop unrolled by R): tile
-    // t's fragments sit in slot t % R; once split, the slot takes tile t + R's loads
-    constexpr int R = NSTG - 1;
-    f32x4 ar[R][FM][2];
-    static_for<0, R>([&](auto s) { issue((int)s, ar[(int)s], (int)s < T); });
-    auto step = [&](int t, auto u) {
-      wait_tiles<LPT>(min(NSTG - 2, T - 1 - t));
-      block_sync_lds();
-      bf16x8 as[FM][3];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) split3_bf16(ar[(int)u][i][0], ar[(int)u][i][1], as[i][0], as[i][1], as[i][2]);
-      // the split terms exist before the slot's next loads are issued (a memory clobber the loads
-      // cannot cross): the loads then land in the slot's own registers, and no copy at the loop's
-      // back edge waits on loads in flight
-#pragma unroll
-      for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(as[i][0]), "v"(as[i][1]), "v"(as[i][2]) : "memory");
-      issue((t + NSTG - 1) % NSTG, ar[(int)u], t + NSTG - 1 < T);
-      mfma_lazy(as, t % NSTG);
-    };
-    int t0 = 0;
-    for (; t0 + R <= T; t0 += R)  // whole rounds: the same ops on every path
-      static_for<0, R>([&](auto u) { step(t0 + (int)u, u); });
-    static_for<0, R>([&](auto u) {  // the last T % R tiles
-      if (t0 + (int)u < T) step(t0 + (int)u, u);
-    });
-  } else if constexpr ((PF & 1) == 0) {
+  if constexpr ((PF & 1) == 0) {
 #pragma unroll
     for (int s = 0; s < NSTG - 1; ++s)
-      if (s < T) issue(s, nullptr);
+      if (s < T) issue(s);
 
     for (int t = 0; t < T; ++t) {
       wait_tiles<LPT>(min(NSTG - 2, T - 1 - t));
       block_sync_lds();
-      if (t + NSTG - 1 < T) issue((t + NSTG - 1) % NSTG, nullptr);
+      if (t + NSTG - 1 < T) issue((t + NSTG - 1) % NSTG);
       Frags F;
       read_frags(F, t % NSTG);
       mfmas(F, t % NSTG);
@@ -547,7 +463,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
     // prologue: tiles 0 .. NSTG-1 fill every slot; tile 0's fragments
 #pragma unroll
     for (int s = 0; s < NSTG; ++s)
-      if (s < T) issue(s, nullptr);
+      if (s < T) issue(s);
     Frags F0, F1;
     if (T > 0) {
       wait_tiles<LPT>(min(NSTG - 1, T - 1));
@@ -560,7 +476,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       if (t + 1 < T) {
         wait_tiles<LPT>(min(T - t - 2, NSTG - 2));
         block_sync_lds();
-        if (t + NSTG < T) issue(t % NSTG, nullptr);
+        if (t + NSTG < T) issue(t % NSTG);
         read_frags(nxt, (t + 1) % NSTG);
       }
       mfmas(cur, -1);

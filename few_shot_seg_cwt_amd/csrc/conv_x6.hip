@@ -9,7 +9,7 @@ namespace cwt {
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int STAGE, int PF = 0>
 __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_igemm_x6(ConvSArgs a) {
   // a stage also holds the weights' lo plane: rings that would overflow the 160 KB of LDS lose a stage
-  constexpr int STG = (PF & 32) ? BN * 192 : (BM + BN) * 128 + BN * 64;  // A direct: no A rows in LDS
+  constexpr int STG = (BM + BN) * 128 + BN * 64;
   constexpr int NS = NSTG * STG <= 163840 ? NSTG : 163840 / STG;
   static_assert(NS >= 2, "x6: a two-stage ring must fit in LDS");
   conv_s_body<BM, BN, WAVES_M, WAVES_N, NS, 6, (PF | 8)>(a);
@@ -51,9 +51,7 @@ int launch_split_w3(const float* w, long R, int K, __bf16* ws, __bf16* wl, hipSt
 //   2x4, 4 = 2x2 on a 2-stage ring, 3 = 4x1 (WN 128), 5 = 4x1 on a 2-stage ring (two per CU);
 //   128x64, 64x128, 64x64: 0, 1, 2 as the other kernels.  var 8-11: the timing-study kernels;
 //   12 / 13: var 5 (128x128) / var 3 (256x256) without the A split (timing study: wrong numbers);
-//   14 / 15: var 5 without operand DMA / without MFMAs (timing study: wrong numbers);
-//   16 - 20: A direct (conv_body.h PF & 32): 16 / 17 128x128 4x1 on a 3 / 5-stage weights ring,
-//   18 256x128 8x1, 19 256x256 4x2, 20 128x256 4x2.
+//   14 / 15: var 5 without operand DMA / without MFMAs (timing study: wrong numbers).
 template <int STAGE>
 static void launch_tiles_x6_stage(const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
   const int v = p.var;
@@ -63,11 +61,6 @@ static void launch_tiles_x6_stage(const ConvSArgs& a, const ConvPlan& p, dim3 gr
     if (v == 12) X6(128, 128, 4, 1, 2, 16);  // timing study: var 5 without the A split
     else if (v == 14) X6(128, 128, 4, 1, 2, 4);   // timing study: var 5 without operand DMA
     else if (v == 15) X6(128, 128, 4, 1, 2, 2);   // timing study: var 5 without MFMAs
-    else if (v == 16) X6(128, 128, 4, 1, 3, 32);  // A direct, 3-stage weights ring (72 KB: two per CU)
-    else if (v == 17) X6(128, 128, 4, 1, 5, 32);  // A direct, 5-stage weights ring
-    else if (v == 18) X6(256, 128, 8, 1, 4, 32);  // A direct
-    else if (v == 19) X6(256, 256, 4, 2, 3, 32);  // A direct
-    else if (v == 20) X6(128, 256, 4, 2, 3, 32);  // A direct
     else if (v == 13) X6(256, 256, 4, 2, 2, 16);  // timing study: 256x256 var 3 without the A split
     else if (v == 8) X6(64, 64, 2, 2, 4, 2);
     else if (v == 9) X6(64, 64, 2, 2, 4, 4);

@@ -146,9 +146,6 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
                         continue   # two-workgroups-per-CU 128x128 form
                     if 8 <= var < 16 and (bm, bn) != ((64, 64) if var < 10 else (128, 128)):
                         continue   # timing-study kernels: fixed tiles
-                    if var >= 16 and not (x6v and (bm, bn) == {16: (128, 128), 17: (128, 128), 18: (256, 128),
-                                                                19: (256, 256), 20: (128, 256)}[var]):
-                        continue   # x6 only: the A-direct forms (conv_x6.hip var 16 - 20)
                     if var == 2 and (bm == 256 or bn == 256):
                         continue   # 8-wave form only for the 128/64 tiles
                     for ns in (1, 2, 4, 8):
@@ -190,7 +187,7 @@ def main():
                          "6 = fp32 width on bf16 MFMA (x6), 7 = x6 in the Winograd F(2x2,3x3) form (x6w), "
                          "8 = x6 in the Winograd F(4x4,3x3) form (x6w4)")
     ap.add_argument("--vars", default="0,1,2,4", help="main-loop variants (0 base, 1 prefetch, 2 prefetch 8 waves, 4 128x128 two per CU; 8-15 timing "
-                         "studies; x6: 3 / 5 WN = 128 layouts, 16-20 A direct)")
+                         "studies; x6: 3 / 5 WN = 128 layouts)")
     ap.add_argument("--only", default="", help="comma list of shape names (default: all)")
     args = ap.parse_args()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
