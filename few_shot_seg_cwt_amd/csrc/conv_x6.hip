@@ -49,7 +49,8 @@ int launch_split_w3(const float* w, long R, int K, __bf16* ws, __bf16* wl, hipSt
 //   256x256: 0 = 2x4 waves, 3 = 4x2 (WN 128);  256x128: 0 = 4x2, 1 = prefetch, 3 = 8x1 (WN 128);
 //   128x256: 0 = 2x4, 1 = prefetch, 3 = 4x2 (WN 128);  128x128: 0 = 2x2, 1 = prefetch, 2 = prefetch
 //   2x4, 4 = 2x2 on a 2-stage ring, 3 = 4x1 (WN 128), 5 = 4x1 on a 2-stage ring (two per CU);
-//   128x64, 64x128, 64x64: 0, 1, 2 as the other kernels.  var 8-11: the timing-study kernels;
+//   128x64, 64x128, 64x64: 0, 1, 2 as the other kernels; 64x128 also 3 = 4x1 (WN 128), 5 = 4x1 on a
+//   2-stage ring.  var 8-11: the timing-study kernels;
 //   12 / 13: var 5 (128x128) / var 3 (256x256) without the A split (timing study: wrong numbers);
 //   14 / 15: var 5 without operand DMA / without MFMAs (timing study: wrong numbers).
 template <int STAGE>
@@ -91,7 +92,9 @@ static void launch_tiles_x6_stage(const ConvSArgs& a, const ConvPlan& p, dim3 gr
     else if (v) X6(128, 64, 2, 2, 3, 1);
     else X6(128, 64, 2, 2, 3, 0);
   } else if (p.bm == 64 && p.bn == 128) {
-    if (v == 2) X6(64, 128, 2, 4, 3, 1);
+    if (v == 3) X6(64, 128, 4, 1, 3, 0);  // WN = 128: one A fragment per wave, no split-K needed at Co = 256
+    else if (v == 5) X6(64, 128, 4, 1, 2, 0);
+    else if (v == 2) X6(64, 128, 2, 4, 3, 1);
     else if (v) X6(64, 128, 2, 2, 3, 1);
     else X6(64, 128, 2, 2, 3, 0);
   } else {
