@@ -19,7 +19,7 @@ LIB = os.path.join(HERE, "libcwt.so")
 SOURCES = ["api.hip", "conv.hip", "conv_x3s.hip", "backbone.hip", "adapt.hip", "cwt_attn.hip", "seg.hip",
            "bn_train.hip", "preprocess.hip", "heads.hip", "match.hip", "detr.hip", "pretrain_kernels.hip",
            "pretrain.hip", "tail.hip", "match_bwd.hip", "wino.hip", "conv_x6.hip"]
-HEADERS = ["common.h", "kernels.h", "pretrain.h", "conv_plans_x3s.inc", "conv_plans_b16.inc", "conv_plans_f32.inc", "conv_plans_f32d.inc", "conv_plans_x6.inc", "conv_body.h"]
+HEADERS = ["common.h", "kernels.h", "pretrain.h", "conv_plans_x3s.inc", "conv_plans_b16.inc", "conv_plans_f32.inc", "conv_plans_f32d.inc", "conv_plans_x6.inc", "conv_body.h", "tail_body.h"]
 PUBLIC_HEADERS = ["cwt.h", "cwt_debug.h"]
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
