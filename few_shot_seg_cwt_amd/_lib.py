@@ -53,6 +53,8 @@ SIGNATURES = {
     "cwt_classify_scaled": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "cwt_episode_tail": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P,
                               _P]),
+    "cwt_inner_adapt_tail": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P,
+                                  _P, _P, _P, _P, _P]),
     "cwt_seg_metrics": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
     "cwt_seg_metrics_pair": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "cwt_seg_ce_fwd_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),

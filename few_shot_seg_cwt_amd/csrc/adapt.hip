@@ -24,6 +24,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "tail_body.h"
 
 namespace cwt {
 
@@ -655,6 +656,7 @@ struct PersistArgs {
   int uc;      // lo-res columns owned per unit (15 or 31)
   long spin_limit;   // polls per barrier before the grid gives up (PA_SPIN_LIMIT by default)
   unsigned* status;  // the context's mapped host status word (cwt_ctx_status), or null
+  float* wq = nullptr;  // the fused tail: [G][2][512] per-workgroup copies of the adapted W
 };
 
 struct PaUnit {
@@ -848,8 +850,9 @@ struct PaScrAlias {
 // skipped, what is left is the per-step exchange); 3 SIDE, code identical to 0, launched for
 // bench.py's side legs (CWT_ADAPT_DBG & 128: the loop timed alone, the exact-fp32 leg) so that
 // they do not mix into the timed kernel's rocprof average.
-template <int NRES, int MODE = 0>
-__global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsigned long long* stamps = nullptr) {
+// The kernel's body: false when the grid gave up (barrier spin bound or another workgroup's abort).
+template <int NRES, int MODE>
+__device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigned long long* stamps) {
   constexpr bool STAMPS = MODE == 1;
   constexpr bool FLOOR = MODE == 2;
   constexpr int C = 512;
@@ -1500,7 +1503,7 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
     if (STAMPS && stp) stp[9] = __builtin_amdgcn_s_memrealtime();
     lds_barrier();
     stamp(6);
-    if (abort_flag) return;
+    if (abort_flag) return false;
     // ---- W of every spanned episode: W1 -= lr_eff * D, W0 += lr_eff * D (same order everywhere).
     // Each wave reads D of its own 32 channels only (its W slice): lanes L < 32 sum replica rows [0, nrep/2),
     // lanes L + 32 rows [nrep/2, nrep), and one v_permlane32_swap adds the halves (the same two
@@ -1545,6 +1548,48 @@ __global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsi
       wo[C + cw] = wlw[wv][ew][1][lane];
     }
   }
+  // the fused tail (one episode: every workgroup holds its W): this workgroup's own copy, read
+  // back by this workgroup only
+  if (a.wq && lane < 32) {
+    float* wq = a.wq + (long)g * 2 * C;
+    wq[cw] = wlw[wv][0][0][lane];
+    wq[C + cw] = wlw[wv][0][1][lane];
+  }
+  return true;
+}
+
+template <int NRES, int MODE = 0>
+__global__ __launch_bounds__(PA_T) void adapt_persist_kernel(PersistArgs a, unsigned long long* stamps = nullptr) {
+  (void)adapt_persist_body<NRES, MODE>(a, stamps);
+}
+
+// The inner loop with the post-loop episode tail fused behind its last step (one episode, one
+// query; EpisodePipeline's adapt context): the loop's workgroups, already resident, run the
+// tail's phases (episode_tail_body, tail_body.h) on their first TL_T threads -- the other waves
+// exit, and a workgroup barrier then waits for the remaining ones only -- instead of a separate
+// grid that must wait for CUs the extractor passes hold.  fst (optional): this launch's slot of
+// three realtime stamps, {min over workgroups of the start, max of the loop's end, max of the
+// tail's end} (the host pre-sets {~0, 0, 0}); the profile splits the launch into loop and tail
+// with them.
+template <int NRES>
+__global__ __launch_bounds__(PA_T) void adapt_persist_tail_kernel(PersistArgs a, TailArgs ta, unsigned long long* fst) {
+  __shared__ __attribute__((aligned(16))) char tail_smem[sizeof(TailTok)];
+  __shared__ int tail_abort, tail_last;
+  if (fst && threadIdx.x == 0)
+    __hip_atomic_fetch_min(fst, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  if (!adapt_persist_body<NRES, 0>(a, nullptr)) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's W copy is written
+  __syncthreads();
+  if (fst && threadIdx.x == 0)
+    __hip_atomic_fetch_max(fst + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x >= TL_T) return;
+  ta.q = a.wq + (long)blockIdx.x * 2 * 512;
+  episode_tail_body<false>(ta, blockIdx.x, tail_smem, tail_abort, tail_last);
+  if (fst && threadIdx.x == 0)
+    __hip_atomic_fetch_max(fst + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Host side of the persistent loop: G = min(units, CUs).  Returns 1 (not an error) when the
@@ -1619,7 +1664,7 @@ static int persist_geometry(int E, int n, int h, int w, int upw_pref, int* G_out
 static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const AdaptScalars* sc, float* acc3,
                                  unsigned* cnt, const AdaptDevArgs* dargs, int E, int n, int h, int w, int S,
                                  int iters, int G, int units, int ncb, int nres, int uc, unsigned* status,
-                                 long spin_limit, hipStream_t st) {
+                                 long spin_limit, hipStream_t st, const FusedTail* tail) {
   PersistArgs a;
   a.status = status;
   a.spin_limit = spin_limit > 0 ? spin_limit : PA_SPIN_LIMIT;
@@ -1648,6 +1693,14 @@ static int enqueue_adapt_persist(const float* f, const uint8_t* lbl_ws, const Ad
   const int dbgv = dbg ? atoi(dbg) : 0;
   // MODE: 1 stamps (timing study), 2 latency floor (& 64), 3 side leg (& 128), 0 product
   const int mode = (dbgv & 32) ? 1 : (dbgv & 64) ? 2 : (dbgv & 128) ? 3 : 0;
+  if (tail) {  // the fused tail: the product instantiation of the two-unit register form only
+    if (nres != 5 || mode != 0 || E != 1 || !tail->args || !tail->wq)
+      return fail(CWT_EARG, "fused tail: needs the two-unit persistent loop (nres 5), one episode, product mode");
+    a.wq = tail->wq;
+    hipLaunchKernelGGL((adapt_persist_tail_kernel<5>), dim3(G), dim3(PA_T), 0, st, a, *tail->args, tail->stamps);
+    CWT_LAUNCH_CHECK();
+    return 0;
+  }
   unsigned long long* stp = nullptr;
   if (mode == 1) {  // timing study (tools/persist_stamps.py)
     const long n_st = ((long)iters + 1) * G * 10;
@@ -1728,7 +1781,7 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
                  float* W, float* f_ws /*[E][n][h][w][512]*/, uint8_t* lbl_ws, AdaptScalars* sc /*[E] + partial counts*/,
                  float* acc3 /*[E][3][R][512]*/, float* wbuf /*[E][2][2][512]*/, AdaptDevArgs* dargs /*[E]*/,
                  AdaptGraphCache* cache, int upw, unsigned* status, long spin_limit, hipStream_t st,
-                 hipEvent_t ev_k0, hipEvent_t ev_k1) {
+                 hipEvent_t ev_k0, hipEvent_t ev_k1, const FusedTail* tail) {
   const long total = (long)n * S * S;  // labels per episode
   unsigned long long* part = (unsigned long long*)(sc + E);  // [E][PREP_MAXBLK][2] after the scalars
   const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
@@ -1745,11 +1798,12 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
                      (double*)nullptr,
                      persist ? cnt : (unsigned*)nullptr, persist ? PA_CNT_WORDS : 0);
   CWT_LAUNCH_CHECK();
-  if (iters <= 0) return 0;
+  if (iters <= 0) return tail ? fail(CWT_EARG, "fused tail: needs the persistent loop") : 0;
+  if (tail && !persist) return fail(CWT_EARG, "fused tail: needs the persistent loop");
   if (persist) {  // one launch for all steps, f read in place (no copy, no graph)
     if (ev_k0) CWT_HIP(hipEventRecord(ev_k0, st));  // profile bracket of the kernel alone (optional)
     const int r = enqueue_adapt_persist(f, lbl_ws, sc, acc3, cnt, dargs, E, n, h, w, S, iters, pG, punits, pncb, pnres,
-                                        puc, status, spin_limit, st);
+                                        puc, status, spin_limit, st, tail);
     if (ev_k1) CWT_HIP(hipEventRecord(ev_k1, st));
     return r;
   }

@@ -15,6 +15,7 @@
 #include "../../include/cwt_debug.h"
 #include "common.h"
 #include "kernels.h"
+#include "tail_body.h"
 
 namespace cwt {
 
@@ -31,7 +32,7 @@ struct AdaptDevArgs;
 int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int w, int S, float lr, int iters,
                  float* W, float* f_ws, uint8_t* lbl_ws, AdaptScalars* sc, float* acc3, float* wbuf,
                  AdaptDevArgs* dargs, AdaptGraphCache* cache, int upw, unsigned* status, long spin_limit,
-                 hipStream_t st, hipEvent_t ev_k0, hipEvent_t ev_k1);
+                 hipStream_t st, hipEvent_t ev_k0, hipEvent_t ev_k1, const FusedTail* tail = nullptr);
 const char* adapt_kernel_name(int E, int n, int h, int w, int iters, int upw);
 int adapt_persist_workgroups(int E, int n, int h, int w, int iters, int upw);
 extern unsigned long long* g_adapt_stamps;
@@ -185,7 +186,12 @@ struct cwt_ctx {
     std::string name;
     double flops, bytes;
     hipEvent_t e0, e1;
+    int fslot = -1;  // a fused loop + tail launch: its slot in fstamps, and which part (0 loop, 1 tail)
+    int fpart = 0;
   };
+  // the fused loop + tail launches' realtime stamps ({start, loop end, tail end} per slot, a ring)
+  unsigned long long* fstamps = nullptr;
+  int fstamp_next = 0;
   std::vector<Rec> recs;
   std::vector<hipEvent_t> evpool;
   size_t ev_used = 0;
@@ -1182,6 +1188,7 @@ int cwt_ctx_destroy(cwt_ctx* ctx) {
   for (auto& kv : ctx->ws)
     if (kv.second.p) (void)hipFree(kv.second.p);
   if (ctx->status_host) (void)hipHostFree(ctx->status_host);
+  if (ctx->fstamps) (void)hipFree(ctx->fstamps);
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
@@ -1196,7 +1203,9 @@ int cwt_ctx_status(cwt_ctx* ctx, uint32_t* status, int clear) {
   volatile unsigned* w = ctx->status_host;
   const unsigned w0 = w[0], w1 = w[1];
   *status = w0 | w1;
-  if (w1) ctx->tail_epoch = ~0u;  // the tail aborted: its counters are re-zeroed before the next tail
+  // the tail aborted, or the inner loop did (a fused tail then never ran its barriers): the tail's
+  // counters are re-zeroed before the next tail
+  if (w0 || w1) ctx->tail_epoch = ~0u;
   if (clear) {
     w[0] = 0u;
     w[1] = 0u;
@@ -1507,6 +1516,103 @@ int cwt_episode_tail(cwt_ctx* ctx, const float* q, const float* f, int B, int h,
   if (pk.ev1()) CWT_HIP(hipEventRecord(pk.ev1(), st));
   p.end();
   return rc;
+}
+
+int cwt_inner_adapt_tail(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int n, int h, int w, int C, int S,
+                         float lr, int iters, float* W_inout, const float* f_q, const int64_t* q_label,
+                         const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
+                         const float* ln_b, int64_t params_version, float* out, float* logits, float* logits0,
+                         float* iut, double* ce, float* iut0, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(f_s && s_label && W_inout && f_q && q_label && w_qkvs && fc_w && fc_b && ln_w && ln_b && out && logits &&
+                logits0 && iut && ce && iut0,
+            "null buffer");
+  CWT_CHECK(C == 512, "C must be 512");
+  CWT_CHECK(n >= 1 && h >= 2 && w >= 2 && iters >= 0 && h * w <= 512 * 32, "bad sizes");
+  CWT_CHECK(S - 1 == 8 * (h - 1) && S - 1 == 8 * (w - 1), "need S-1 == 8*(h-1) == 8*(w-1)");
+  CWT_HIP(hipSetDevice(ctx->device));
+  // fused where the loop runs as the two-unit register form (EpisodePipeline's adapt context) in
+  // its product instantiation; everything else (and CWT_FUSED_LOOP_TAIL=0) runs the two calls
+  const char* kname = adapt_kernel_name(1, n, h, w, iters, ctx->adapt_upw);
+  const char* dbg = getenv("CWT_ADAPT_DBG");
+  const char* fz = getenv("CWT_FUSED_LOOP_TAIL");
+  const char* tst = getenv("CWT_TAIL_STAMPS");
+  const bool fuse = strcmp(kname, "adapt_persist_kernel<5") == 0 && !(dbg && atoi(dbg) != 0) && !(fz && fz[0] == '0') &&
+                    !(tst && tst[0] == '1');
+  if (!fuse) {
+    int rc = cwt_inner_adapt(ctx, f_s, s_label, n, h, w, C, S, lr, iters, W_inout, stream);
+    if (rc) return rc;
+    return cwt_episode_tail(ctx, W_inout, f_q, 1, h, w, S, q_label, w_qkvs, fc_w, fc_b, ln_w, ln_b, params_version, out,
+                            logits, logits0, iut, ce, iut0, stream);
+  }
+  const hipStream_t st = (hipStream_t)stream;
+  constexpr int H = 4;
+  const int hw = h * w;
+  const int G = adapt_persist_workgroups(1, n, h, w, iters, ctx->adapt_upw);
+  CWT_CHECK(G >= 1 && G <= 512, "fused tail: loop geometry");
+  // the loop's workspaces (cwt_inner_adapt_batch)
+  void *fws, *lbl, *sc, *acc, *wb, *dargs;
+  size_t b_f, b_lbl, b_sc, b_acc, b_wb, b_args;
+  adapt_ws_sizes(1, n, h, w, S, &b_f, &b_lbl, &b_sc, &b_acc, &b_wb, &b_args);
+  int rc;
+  if ((rc = ensure_ws(ctx, "adapt.f", b_f, &fws)) || (rc = ensure_ws(ctx, "adapt.args", b_args, &dargs)) ||
+      (rc = ensure_ws(ctx, "adapt.lbl", b_lbl, &lbl)) || (rc = ensure_ws(ctx, "adapt.sc", b_sc, &sc)) ||
+      (rc = ensure_ws(ctx, "adapt.acc", b_acc, &acc)) || (rc = ensure_ws(ctx, "adapt.wbuf", b_wb, &wb)))
+    return rc;
+  // the tail's (cwt_episode_tail), over the loop's G workgroups
+  void *fold, *tws, *cnt, *wq;
+  if ((rc = ensure_ws(ctx, "attn.fold", attention_fold_floats(C, H) * 4, &fold)) ||
+      (rc = ensure_ws(ctx, "tail.ws", std::max(episode_tail_ws_floats(1, hw, G), (size_t)4 << 20) * 4, &tws)) ||
+      (rc = ensure_ws(ctx, "tail.cnt", episode_tail_cnt_words() * 4, &cnt)) ||
+      (rc = ensure_ws(ctx, "tail.wq", (size_t)G * 2 * C * 4, &wq)))
+    return rc;
+  if (ctx->fold_w != w_qkvs || ctx->fold_fc != fc_w || ctx->fold_ver != params_version || ctx->fold_H != H) {
+    if ((rc = attention_fold(w_qkvs, fc_w, C, H, (float*)fold, (float*)tws, (size_t)4 << 20, st))) return rc;
+    ctx->fold_w = w_qkvs;
+    ctx->fold_fc = fc_w;
+    ctx->fold_ver = params_version;
+    ctx->fold_H = H;
+  }
+  if (ctx->tail_epoch > episode_tail_max_epoch(G) || ctx->tail_G != G) {  // fresh, wrapped, aborted or re-sized
+    CWT_HIP(hipMemsetAsync(cnt, 0, episode_tail_cnt_words() * 4, st));
+    ctx->tail_epoch = 0;
+    ctx->tail_G = G;
+  }
+  // this launch's stamp slot: {start (min), loop end (max), tail end (max)}, pre-set {~0, 0, 0}
+  constexpr int kFSlots = 4096;
+  if (!ctx->fstamps) CWT_HIP(hipMalloc(&ctx->fstamps, (size_t)kFSlots * 3 * sizeof(unsigned long long)));
+  const int slot = ctx->fstamp_next;
+  ctx->fstamp_next = (ctx->fstamp_next + 1) % kFSlots;
+  unsigned long long* fst = ctx->fstamps + 3 * slot;
+  CWT_HIP(hipMemsetAsync(fst, 0xFF, sizeof(unsigned long long), st));
+  CWT_HIP(hipMemsetAsync(fst + 1, 0, 2 * sizeof(unsigned long long), st));
+  TailArgs ta;
+  if ((rc = fill_episode_tail_args(W_inout, f_q, 1, hw, h, w, S, q_label, (const float*)fold, fc_b, ln_w, ln_b, out,
+                                   logits, logits0, iut, ce, iut0, (float*)tws, (unsigned*)cnt, ctx->tail_epoch++, G,
+                                   ctx->adapt_spin_limit, ctx->status_dev + 1, nullptr, &ta)))
+    return rc;
+  const FusedTail ft{&ta, (float*)wq, fst};
+  const std::string kn = "adapt_persist_tail_kernel<5";
+  const double lfl = (double)iters * 2.0 * (4.0 * C * h * w * n), lby = (double)iters * ((double)n * h * w * C * 4 + (double)n * S * S);
+  const double tfl = 2.0 * 2.0 * hw * C * C * H + 2.0 * 2.0 * H * 2.0 * hw * C;
+  Prof p(ctx, st, "inner_adapt x" + std::to_string(iters) + " [" + kn + "]", lfl, lby, 1);
+  // the launch's loop part and tail part (its stamps; the events only order the read-back)
+  Prof pk(ctx, st, "inner_adapt_kernel [" + kn + "]", lfl, lby, 1, true);
+  if (pk.idx >= 0) ctx->recs[pk.idx].fslot = slot;
+  rc = launch_adapt(f_s, s_label, 1, n, h, w, S, lr, iters, W_inout, (float*)fws, (uint8_t*)lbl, (AdaptScalars*)sc,
+                    (float*)acc, (float*)wb, (AdaptDevArgs*)dargs, nullptr, ctx->adapt_upw, ctx->status_dev,
+                    ctx->adapt_spin_limit, st, pk.ev0(), pk.ev1(), &ft);
+  p.end();
+  if (rc) return rc;
+  for (const char* tn : {"post_loop_tail", "episode_tail_kernel"}) {
+    Prof pt(ctx, st, tn, tfl, 4.0 * ((double)hw * C * 2 + 2.0 * H * C * C) + 9.0 * S * S, 1);
+    pt.end();
+    if (pt.idx >= 0) {
+      ctx->recs[pt.idx].fslot = slot;
+      ctx->recs[pt.idx].fpart = 1;
+    }
+  }
+  return 0;
 }
 
 int cwt_classify_scaled(cwt_ctx* ctx, const float* W, const float* f, const float* inv_norm, int B, int P, int C,
@@ -2777,7 +2883,14 @@ int cwt_profile_record(cwt_ctx* ctx, int i, char* name, int name_len, double* fl
   if (bytes) *bytes = r.bytes;
   if (ms) {
     CWT_HIP(hipEventSynchronize(r.e1));
-    CWT_HIP(hipEventElapsedTime(ms, r.e0, r.e1));
+    if (r.fslot >= 0) {  // a fused loop + tail launch: its part from the kernel's realtime stamps (100 MHz)
+      unsigned long long v[3];
+      CWT_HIP(hipMemcpy(v, ctx->fstamps + 3 * r.fslot, sizeof(v), hipMemcpyDeviceToHost));
+      const unsigned long long t0 = r.fpart ? v[1] : v[0], t1 = r.fpart ? v[2] : v[1];
+      *ms = t1 > t0 ? (float)((double)(t1 - t0) * 1e-5) : 0.f;
+    } else {
+      CWT_HIP(hipEventElapsedTime(ms, r.e0, r.e1));
+    }
   }
   return 0;
 }

@@ -140,6 +140,14 @@ struct TailMet {  // P5
   double fd[2][TL_T];
 };
 
+// The inner loop's fused tail (adapt.hip adapt_persist_tail_kernel): its arguments (q is set per
+// workgroup in the kernel), the per-workgroup W copies [G][2][512] and an optional stamp slot
+struct FusedTail {
+  const TailArgs* args;
+  float* wq;
+  unsigned long long* stamps;
+};
+
 // Host: the arguments of one tail over G workgroups (launch_episode_tail's checks; tail.hip)
 int fill_episode_tail_args(const float* q, const float* f, int B, int hw, int h, int w, int S, const int64_t* target,
                            const float* fold, const float* fc_b, const float* ln_w, const float* ln_b, float* out,

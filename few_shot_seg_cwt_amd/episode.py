@@ -130,6 +130,8 @@ def cwt_tail(transformer, Wb: torch.Tensor, f_q: torch.Tensor):
 
 
 _FUSED_TAIL = os.environ.get("CWT_FUSED_TAIL", "1") != "0"   # 0: the module kernels (A/B)
+# 0: inner loop and tail as two library calls (the library also honours CWT_FUSED_LOOP_TAIL=0)
+_FUSED_LOOP_TAIL = os.environ.get("CWT_FUSED_LOOP_TAIL", "1") != "0"
 
 
 def fused_tail_ok(transformer, f_q: torch.Tensor, S: int) -> bool:
@@ -176,6 +178,45 @@ def tail_and_metrics(transformer, Wb: torch.Tensor, f_q: torch.Tensor, q_label: 
     W2, pred_q, pred_q0 = cwt_tail(transformer, Wb, f_q)
     iut, ce, iut0 = seg_metrics_pair(pred_q, pred_q0, q_label)
     return W2, pred_q, pred_q0, iut, ce, iut0
+
+
+def adapt_and_tail(transformer, f_s: torch.Tensor, s_label: torch.Tensor, W: torch.Tensor, lr: float, iters: int,
+                   f_q: torch.Tensor, q_label: torch.Tensor):
+    """inner_adapt(f_s, s_label, W) then tail_and_metrics(W, f_q, q_label) for one episode with
+    one query -- as ONE call (cwt_inner_adapt_tail) where the one-launch tail applies: on the
+    pipeline's adapt context the library fuses the tail behind the loop's last step in the same
+    launch.  Returns (W, (W', pred_q, pred_q0, iut, ce, iut0))."""
+    if f_q.shape[0] != 1 or not fused_tail_ok(transformer, f_q, q_label.shape[-1]) or not _FUSED_LOOP_TAIL:
+        W = inner_adapt(f_s, s_label, W, lr, iters)
+        return W, tail_and_metrics(transformer, W.view(1, 2, -1), f_q, q_label)
+    _lib.require(f_s, "f_s")
+    _lib.require(s_label, "s_label", torch.int64)
+    _lib.require(W, "W")
+    n, Cc, h, w = f_s.shape
+    if not f_s.is_contiguous(memory_format=torch.channels_last):
+        f_s = f_s.contiguous(memory_format=torch.channels_last)
+    if not f_q.is_contiguous(memory_format=torch.channels_last):
+        f_q = f_q.contiguous(memory_format=torch.channels_last)
+    if f_q.shape[2:] != f_s.shape[2:]:
+        raise ValueError("f_q and f_s must share h, w")
+    S = s_label.shape[-1]
+    lbl = s_label.reshape(n, S, S).contiguous()
+    tg = q_label.reshape(1, S, S).contiguous()
+    assert W.is_contiguous() and W.numel() == 2 * Cc
+    dev = f_q.device
+    out = torch.empty((1, 2, Cc), device=dev, dtype=torch.float32)
+    logits = torch.empty((1, 2, h, w), device=dev, dtype=torch.float32)
+    logits0 = torch.empty_like(logits)
+    iut = torch.empty((1, 3, 2), device=dev, dtype=torch.float32)
+    iut0 = torch.empty_like(iut)
+    ce = torch.empty((1, 2), device=dev, dtype=torch.float64)
+    t = transformer
+    wq, fw, fb, lw, lb = t._ptrs(t.flat)
+    _lib.check(_lib.lib().cwt_inner_adapt_tail(
+        _lib.ctx(dev.index), _lib.ptr(f_s), _lib.ptr(lbl), n, h, w, Cc, S, float(lr), int(iters), _lib.ptr(W),
+        _lib.ptr(f_q), _lib.ptr(tg), wq, fw, fb, lw, lb, t.params_version(), _lib.ptr(out), _lib.ptr(logits),
+        _lib.ptr(logits0), _lib.ptr(iut), _lib.ptr(ce), _lib.ptr(iut0), _lib.stream_ptr(dev)), "cwt_inner_adapt_tail")
+    return W, (out, logits, logits0, iut, ce, iut0)
 
 
 def classify_bwd(dlogits: torch.Tensor, f: torch.Tensor, dW: torch.Tensor):
@@ -373,9 +414,8 @@ class EpisodePipeline:
             for t in (f_all, imgs, s_label, q_label, W0):
                 t.record_stream(self.s_adapt)
             f_s, f_q = f_all[:shot], f_all[shot:]
-            W = inner_adapt(f_s, s_label, W0, eng.lr, eng.iters)
-            Wb = W.view(1, 2, -1)
-            W2, pred_q, pred_q0, iut, ce, iut0 = tail_and_metrics(eng.transformer, Wb, f_q, q_label)
+            W, (W2, pred_q, pred_q0, iut, ce, iut0) = adapt_and_tail(eng.transformer, f_s, s_label, W0, eng.lr,
+                                                                      eng.iters, f_q, q_label)
             done_all = torch.cuda.Event()
             done_all.record(self.s_adapt)
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, done=done_all)

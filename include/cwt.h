@@ -281,6 +281,24 @@ int cwt_episode_tail(cwt_ctx* ctx, const float* q, const float* f, int B, int h,
                      float* iut0, void* stream);
 
 /*
+ * One episode's inner loop and post-loop tail (test.py:164-224): cwt_inner_adapt on f_s /
+ * s_label / W_inout, then cwt_episode_tail with q = the adapted W and B = 1 query (f_q, q_label),
+ * with the same outputs.  Where the loop runs as the persistent two-unit form (the episode
+ * pipeline's adapt context: cwt_ctx_set_adapt_units 2) the tail is FUSED behind the loop's last
+ * step in the same launch: the loop's resident workgroups run the tail's phases instead of a
+ * second grid that waits for CUs.  Elsewhere (and with CWT_FUSED_LOOP_TAIL=0) it makes the two
+ * calls.  The profile splits a fused launch into its loop part ("inner_adapt_kernel [...]") and
+ * its tail part ("episode_tail_kernel", "post_loop_tail") by in-kernel realtime stamps.
+ * Status: a loop barrier that cannot complete sets CWT_STATUS_ADAPT_BARRIER (the tail is then
+ * skipped), a tail barrier CWT_STATUS_TAIL_BARRIER.
+ */
+int cwt_inner_adapt_tail(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int n, int h, int w, int C, int S,
+                         float lr, int iters, float* W_inout, const float* f_q, const int64_t* q_label,
+                         const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
+                         const float* ln_b, int64_t params_version, float* out, float* logits, float* logits0,
+                         float* iut, double* ce, float* iut0, void* stream);
+
+/*
  * Segmentation metrics of low-res logits against a full-res label:
  * bilinear(align_corners=True) upsample [B,2,h,w] -> [B,2,S,S], argmax over classes,
  * preds[target==255] = 255, histc intersection / union / target over 2 classes

@@ -182,3 +182,77 @@ def test_episode_tail_barrier_timeout_is_raised(dev):
     _lib.check_status()
     W2r, pqr, _ = cwt_tail(t, W, f)
     assert rel(W2, W2r) < TOL and rel(pq, pqr) < TOL
+
+
+# ---------------------------------------------------------------- the tail fused behind the inner loop
+def _episode_inputs(dev, shot, h, tag):
+    S = 8 * (h - 1) + 1
+    f_s = torch.from_numpy(syn.normal(11, "fs" + tag, (shot, 512, h, h), 1.0)).abs().to(dev)
+    f_s = f_s.contiguous(memory_format=torch.channels_last)
+    f_q = torch.from_numpy(syn.normal(12, "fq" + tag, (1, 512, h, h), 1.0)).abs().to(dev)
+    f_q = f_q.contiguous(memory_format=torch.channels_last)
+    s_lab = _labels(shot, S, "s" + tag).to(dev)
+    q_lab = _labels(1, S, "q" + tag).to(dev)
+    W0 = torch.from_numpy(syn.normal(13, "w0" + tag, (2, 512), 0.05)).to(dev)
+    return f_s, f_q, s_lab, q_lab, W0
+
+
+@pytest.mark.parametrize("shot,h", [(1, 60), (1, 33), (2, 60)])
+def test_loop_tail_fused_equals_two_calls(dev, shot, h):
+    """cwt_inner_adapt_tail on a context set for the pipeline's two-unit loop (the fused launch:
+    the loop's workgroups run the tail behind its last step) against inner_adapt + episode_tail
+    on the same context: the same loop code, so W bit-identical; the tail's arithmetic does not
+    depend on its grid (the loop's G instead of 64) except the CE partials' grouping -- W',
+    pred_q, pred_q0 and the counts identical, the CE sum to double rounding.  Twice, so the
+    second launch runs on the counters the first advanced; the status word stays clear."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib
+    from few_shot_seg_cwt_amd.episode import adapt_and_tail, episode_tail, inner_adapt
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    t.eval()
+    f_s, f_q, s_lab, q_lab, W0 = _episode_inputs(dev, shot, h, f"{shot}_{h}")
+    c = _lib.new_ctx(dev.index)
+    _lib.check(_lib.lib().cwt_ctx_set_adapt_units(c, 2), "adapt units")
+    with _lib.using_ctx(c):
+        for rep in range(2):
+            Wf, (W2f, pqf, pq0f, iutf, cef, iut0f) = adapt_and_tail(t, f_s, s_lab, W0.clone(), 0.1, 50, f_q, q_lab)
+            Wr = inner_adapt(f_s, s_lab, W0.clone(), 0.1, 50)
+            W2r, pqr, pq0r, iutr, cer, iut0r = episode_tail(t, Wr.view(1, 2, -1), f_q, q_lab)
+            torch.cuda.synchronize()
+            _lib.check_status()
+            assert torch.equal(Wf, Wr), rep
+            errs = dict(W2=rel(W2f, W2r), pred_q=rel(pqf, pqr), pred_q0=rel(pq0f, pq0r))
+            print(f"loop+tail fused shot={shot} h={h} rep={rep}: {errs}")
+            assert max(errs.values()) == 0.0, errs
+            assert torch.equal(iutf, iutr) and torch.equal(iut0f, iut0r)
+            assert float(cef[:, 1].sub(cer[:, 1]).abs().max()) == 0.0
+            assert float(((cef[:, 0] - cer[:, 0]).abs() / cer[:, 0].abs().clamp_min(1e-30)).max()) < 1e-12
+
+
+def test_loop_tail_fused_profile_split(dev):
+    """The profile of a fused launch: a loop part and a tail part from the kernel's stamps, both
+    positive and together within the launch's own event bracket."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib
+    from few_shot_seg_cwt_amd.episode import adapt_and_tail
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    t.eval()
+    f_s, f_q, s_lab, q_lab, W0 = _episode_inputs(dev, 1, 60, "prof")
+    c = _lib.new_ctx(dev.index)
+    _lib.check(_lib.lib().cwt_ctx_set_adapt_units(c, 2), "adapt units")
+    with _lib.using_ctx(c):
+        adapt_and_tail(t, f_s, s_lab, W0.clone(), 0.1, 200, f_q, q_lab)
+        torch.cuda.synchronize()
+        _lib.profile_enable(1)
+        adapt_and_tail(t, f_s, s_lab, W0.clone(), 0.1, 200, f_q, q_lab)
+        torch.cuda.synchronize()
+        recs = _lib.profile_records()
+        _lib.profile_enable(0)
+    names = [r[0] for r in recs]
+    print(recs)
+    loop = [r for r in recs if r[0].startswith("inner_adapt_kernel [adapt_persist_tail_kernel<5")]
+    tail = [r for r in recs if r[0] == "episode_tail_kernel"]
+    brk = [r for r in recs if r[0].startswith("inner_adapt x")]
+    assert len(loop) == 1 and len(tail) == 1 and len(brk) == 1, names
+    assert loop[0][3] > 0.1 and 0.0 < tail[0][3] < 1.0
+    assert loop[0][3] + tail[0][3] <= brk[0][3] * 1.05 + 0.05
