@@ -733,7 +733,7 @@ def main():
     # same G with every unit's arithmetic and atomics skipped (CWT_ADAPT_DBG & 64) -- the per-step
     # exchange alone (slot zeroing, arrival, poll, replica reads, W update) x adapt_iter ----
     latency_floor = None
-    if not args.train and E == 1 and ad_kernel.startswith("adapt_persist_kernel"):
+    if not args.train and E == 1 and ad_kernel.startswith("adapt_persist"):   # (also the fused loop + tail)
         imgs0, sl0, ql0 = pool[0]
         with torch.no_grad():
             f_s0 = model.extract_features(imgs0)[0][:shot]
@@ -791,21 +791,30 @@ def main():
         hw_ = h_feat * h_feat
         exec_fl = E * (2.0 * 2 * 4 * hw_ * 512 * 2 + 2.0 * 2 * hw_ * 512 * 2)   # scores + A.f per head, 2 classifiers
         ref_fl = reference_cwt_flops(hw_) * E
-        tk_traffic, tk_traffic_src = pmc_traffic("episode_tail_kernel")
+        fused_tail = "tail_kernel" in ad_kernel   # the tail fused behind the loop (cwt_inner_adapt_tail)
+        tk_traffic, tk_traffic_src = pmc_traffic("episode_tail_kernel") if not fused_tail else (None, None)
         tail_roofline = {
-            "bound": "hbm", "kernel": "episode_tail_kernel (cwt_episode_tail, one launch per episode)",
+            "bound": "hbm",
+            "kernel": ("the tail part of adapt_persist_tail_kernel<5> (cwt_inner_adapt_tail: the episode tail fused "
+                       "behind the inner loop's last step; its time from in-kernel realtime stamps, the last "
+                       "workgroup's loop end to the last workgroup's tail end)" if fused_tail else
+                       "episode_tail_kernel (cwt_episode_tail, one launch per episode)"),
             "avg_launch_ms": round(tk_launch_ms, 4), "launches": len(tk_sel),
             "algorithmic_bytes_per_launch": round(tk_bytes),
             "achieved": round(tk_bytes / (tk_launch_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
             "frac": round(tk_bytes / (tk_launch_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
-            "traffic": tk_traffic, "traffic_unit": "bytes/launch", "traffic_source": tk_traffic_src,
+            "traffic": tk_traffic, "traffic_unit": "bytes/launch",
+            "traffic_source": tk_traffic_src if not fused_tail else
+            "none: the fused launch's PMC counts the loop and the tail together",
             "executed_flops_per_launch": exec_fl,
             "reference_formulation_flops_per_launch": ref_fl,
             "reference_formulation_tflops": round(ref_fl / (tk_launch_ms * 1e-3) / 1e12, 2),
             "reference_formulation_frac_of_fp32_mfma": round(ref_fl / (tk_launch_ms * 1e-3) / 1e12
                                                              / PEAK_FP32_MFMA_TFLOPS, 4),
-            "measured_in": "the timed region (pipelined: launched on the adapt stream while the next episodes' "
-                           "extractor passes hold most CUs)",
+            "measured_in": ("the timed region (pipelined: run by the inner loop's resident workgroups behind its "
+                            "last grid barrier, no launch and no wait for CUs)" if fused_tail else
+                            "the timed region (pipelined: launched on the adapt stream while the next episodes' "
+                            "extractor passes hold most CUs)"),
             "note": "the CWT runs re-associated (DESIGN.md §3): scores = f . (W_k^T q') and W_v (sum_j a_j f_j) -- "
                     "token work of ~59 MFLOP instead of projecting every token (15.1 GFLOP as written); the kernel "
                     "is latency-bound (grid barriers between its phases), so both fractions are small"}

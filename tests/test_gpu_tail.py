@@ -201,10 +201,11 @@ def _episode_inputs(dev, shot, h, tag):
 def test_loop_tail_fused_equals_two_calls(dev, shot, h):
     """cwt_inner_adapt_tail on a context set for the pipeline's two-unit loop (the fused launch:
     the loop's workgroups run the tail behind its last step) against inner_adapt + episode_tail
-    on the same context: the same loop code, so W bit-identical; the tail's arithmetic does not
-    depend on its grid (the loop's G instead of 64) except the CE partials' grouping -- W',
-    pred_q, pred_q0 and the counts identical, the CE sum to double rounding.  Twice, so the
-    second launch runs on the counters the first advanced; the status word stays clear."""
+    on the same context.  The loop's replica sums are float atomics (their order varies from run
+    to run), so W agrees to fp32 rounding, not bitwise, and the tail's outputs follow it: W', pred_q,
+    pred_q0 at the module bar, counts within 2 pixels (near-tie flips), the valid-pixel counts
+    equal, the CE sum at 1e-5.  Twice, so the second launch runs on the counters the first
+    advanced; the status word stays clear."""
     from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib
     from few_shot_seg_cwt_amd.episode import adapt_and_tail, episode_tail, inner_adapt
     t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
@@ -220,13 +221,12 @@ def test_loop_tail_fused_equals_two_calls(dev, shot, h):
             W2r, pqr, pq0r, iutr, cer, iut0r = episode_tail(t, Wr.view(1, 2, -1), f_q, q_lab)
             torch.cuda.synchronize()
             _lib.check_status()
-            assert torch.equal(Wf, Wr), rep
-            errs = dict(W2=rel(W2f, W2r), pred_q=rel(pqf, pqr), pred_q0=rel(pq0f, pq0r))
+            errs = dict(W=rel(Wf, Wr), W2=rel(W2f, W2r), pred_q=rel(pqf, pqr), pred_q0=rel(pq0f, pq0r))
             print(f"loop+tail fused shot={shot} h={h} rep={rep}: {errs}")
-            assert max(errs.values()) == 0.0, errs
-            assert torch.equal(iutf, iutr) and torch.equal(iut0f, iut0r)
+            assert max(errs.values()) < TOL, errs
+            assert float((iutf - iutr).abs().max()) <= 2 and float((iut0f - iut0r).abs().max()) <= 2
             assert float(cef[:, 1].sub(cer[:, 1]).abs().max()) == 0.0
-            assert float(((cef[:, 0] - cer[:, 0]).abs() / cer[:, 0].abs().clamp_min(1e-30)).max()) < 1e-12
+            assert float(((cef[:, 0] - cer[:, 0]).abs() / cer[:, 0].abs().clamp_min(1e-30)).max()) < 1e-5
 
 
 def test_loop_tail_fused_profile_split(dev):
@@ -243,11 +243,12 @@ def test_loop_tail_fused_profile_split(dev):
     with _lib.using_ctx(c):
         adapt_and_tail(t, f_s, s_lab, W0.clone(), 0.1, 200, f_q, q_lab)
         torch.cuda.synchronize()
-        _lib.profile_enable(1)
+    _lib.profile_enable(1)   # (outside using_ctx: all_ctx lists the default context and the extra ones)
+    with _lib.using_ctx(c):
         adapt_and_tail(t, f_s, s_lab, W0.clone(), 0.1, 200, f_q, q_lab)
         torch.cuda.synchronize()
-        recs = _lib.profile_records()
-        _lib.profile_enable(0)
+    recs = _lib.profile_records()
+    _lib.profile_enable(0)
     names = [r[0] for r in recs]
     print(recs)
     loop = [r for r in recs if r[0].startswith("inner_adapt_kernel [adapt_persist_tail_kernel<5")]
