@@ -257,3 +257,37 @@ def test_loop_tail_fused_profile_split(dev):
     assert len(loop) == 1 and len(tail) == 1 and len(brk) == 1, names
     assert loop[0][3] > 0.1 and 0.0 < tail[0][3] < 1.0
     assert loop[0][3] + tail[0][3] <= brk[0][3] * 1.05 + 0.05
+
+
+def test_loop_tail_fused_barrier_timeout_is_raised(dev):
+    """A fused launch whose loop barrier gives up (spin bound 1) skips the tail, reports
+    CWT_STATUS_ADAPT_BARRIER and the host raises at its next check; the check re-arms the tail's
+    counters too (the skipped tail never arrived on them), after which the same call is clean and
+    equals the two separate calls."""
+    from few_shot_seg_cwt_amd import MultiHeadAttentionOne, _lib
+    from few_shot_seg_cwt_amd.episode import adapt_and_tail, episode_tail, inner_adapt
+    t = MultiHeadAttentionOne(4, 512, 512, 512, dropout=0.5)
+    t.load_state_dict(syn.make_transformer_state(4, 512, SEED))
+    t.eval()
+    f_s, f_q, s_lab, q_lab, W0 = _episode_inputs(dev, 1, 60, "to")
+    c = _lib.new_ctx(dev.index)
+    _lib.check(_lib.lib().cwt_ctx_set_adapt_units(c, 2), "adapt units")
+    with _lib.using_ctx(c):
+        adapt_and_tail(t, f_s, s_lab, W0.clone(), 0.1, 20, f_q, q_lab)   # the counters advanced once
+        torch.cuda.synchronize()
+        _lib.check_status()
+        _lib.check(_lib.lib().cwt_debug_adapt_spin_limit(c, 1), "spin limit")
+        try:
+            adapt_and_tail(t, f_s, s_lab, W0.clone(), 0.1, 20, f_q, q_lab)
+            torch.cuda.synchronize()
+            with pytest.raises(_lib.CwtError, match="barrier timed out"):
+                _lib.check_status()
+        finally:
+            _lib.check(_lib.lib().cwt_debug_adapt_spin_limit(c, 0), "spin limit")
+        Wf, (W2f, pqf, _, _, _, _) = adapt_and_tail(t, f_s, s_lab, W0.clone(), 0.1, 20, f_q, q_lab)
+        torch.cuda.synchronize()
+        _lib.check_status()
+        Wr = inner_adapt(f_s, s_lab, W0.clone(), 0.1, 20)
+        W2r, pqr, _, _, _, _ = episode_tail(t, Wr.view(1, 2, -1), f_q, q_lab)
+        torch.cuda.synchronize()
+    assert rel(Wf, Wr) < TOL and rel(W2f, W2r) < TOL and rel(pqf, pqr) < TOL
