@@ -124,6 +124,18 @@ int launch_wino_weights(const float* w_packed, int Co, int Ci, float* U, hipStre
   return 0;
 }
 
+// The input transforms' thread index with the blocks remapped XCD-contiguous: the dispatcher
+// deals blocks round-robin over the 8 XCDs (block b on XCD b % 8, MI355X_MICROARCH.md), so
+// logically consecutive blocks -- neighbouring tiles, whose input patches overlap by half -- would
+// each fetch the shared rows into a different XCD's L2; remapped, one XCD takes one contiguous run
+// of tiles and the overlap hits its L2
+__device__ __forceinline__ long wino_xcd_index() {
+  const unsigned nb = gridDim.x, b = blockIdx.x;
+  const unsigned q = nb >> 3, r = nb & 7, xcd = b & 7, slot = b >> 3;
+  const unsigned L = xcd < r ? xcd * (q + 1) + slot : r * (q + 1) + (xcd - r) * q + slot;
+  return (long)L * blockDim.x + threadIdx.x;
+}
+
 __device__ __forceinline__ void wino_tile(long t, const WinoGeom& g, int& n, int& py, int& px, int& ti, int& tj) {
   tj = (int)(t % g.TX);
   long r = t / g.TX;
@@ -140,7 +152,7 @@ __device__ __forceinline__ void wino_tile(long t, const WinoGeom& g, int& n, int
 __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ x, WinoGeom g, int Ci,
                                                       float* __restrict__ V) {
   const int q4 = Ci >> 2;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long idx = wino_xcd_index();
   if (idx >= g.T * q4) return;
   const long t = idx / q4;
   const int c = (int)(idx - t * q4) * 4;
@@ -191,7 +203,7 @@ __device__ __forceinline__ void wino4_bt(const f32x4 d[6], f32x4 r[6]) {
 __global__ __launch_bounds__(256) void wino4_in_kernel(const float* __restrict__ x, WinoGeom g, int Ci,
                                                        float* __restrict__ V) {
   const int q4 = Ci >> 2;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long idx = wino_xcd_index();
   if (idx >= g.T * q4) return;
   const long t = idx / q4;
   const int c = (int)(idx - t * q4) * 4;
