@@ -146,14 +146,19 @@ __global__ __launch_bounds__(256) void stem_conv1_s_kernel(const float* __restri
 // shuffle.  A lane's weights (28), BN scale / shift (16 + 16) stay in registers while the wave
 // walks its 16-pixel groups; the image reads are 4-B gathers from L2 (2.7 MB image per episode).
 // The VALU form above gave every (pixel, 8 channels) thread 216 FMAs behind 54 LDS weight reads
-// and ran at 26-33 us for 2 x 237^2 pixels, 6x its byte floor.
-template <bool BF16>
+// and ran at 26-33 us for 2 x 237^2 pixels, 6x its byte floor.  OUT: 0 the S-layout, 1 plain
+// bf16 NHWC, 2 fp32 NHWC (the fp32-width stacks, round 5: the lane's 16 channels as four 16-B
+// stores; the one-pixel-per-thread VALU kernel's 64-channel rows took 32 us alone, its stores
+// scattered 16 B per 256-B row across the wave)
+template <int OUT>
 __global__ __launch_bounds__(256) void stem_conv1_mfma_kernel(const float* __restrict__ img, int N, int S,
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ scale,
                                                               const float* __restrict__ shift,
-                                                              __bf16* __restrict__ out, int Ho, float floor_,
+                                                              void* __restrict__ out_, int Ho, float floor_,
                                                               int ngroups) {
+  constexpr bool BF16 = OUT == 1;
+  __bf16* out = (__bf16*)out_;
   const int lane = threadIdx.x & 63, j = lane >> 4, c16 = lane & 15;
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
@@ -213,6 +218,21 @@ __global__ __launch_bounds__(256) void stem_conv1_mfma_kernel(const float* __res
     }
     if (pix >= total) continue;
     // channel block pair h = 0: channels 8j..8j+7 (nb 0, 1); h = 1: 32 + 8j .. (nb 2, 3)
+    if constexpr (OUT == 2) {
+      float* of = (float*)out_ + pix * 64;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 r0, r1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          r0[i] = fmaxf(fmaf(acc[2 * h][i], sc[2 * h][i], sh[2 * h][i]), floor_);
+          r1[i] = fmaxf(fmaf(acc[2 * h + 1][i], sc[2 * h + 1][i], sh[2 * h + 1][i]), floor_);
+        }
+        *(f32x4*)(of + 32 * h + 8 * j) = r0;
+        *(f32x4*)(of + 32 * h + 8 * j + 4) = r1;
+      }
+      continue;
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       bf16x8 hi, lo;
@@ -242,11 +262,14 @@ int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const
   const int ngroups = (int)cdiv(total, 16);
   const int grid = (int)std::min<long>(cdiv(ngroups, 4 * 4), 2048);  // ~4 groups per wave, 4 waves per block
   if (layout == ACT_SPLIT && !valu)
-    hipLaunchKernelGGL(stem_conv1_mfma_kernel<false>, dim3(grid), dim3(256), 0, st, img, N, S, w27x64, scale, shift,
-                       (__bf16*)out, Ho, floor_, ngroups);
+    hipLaunchKernelGGL(stem_conv1_mfma_kernel<0>, dim3(grid), dim3(256), 0, st, img, N, S, w27x64, scale, shift,
+                       (void*)out, Ho, floor_, ngroups);
   else if (layout == ACT_BF16 && !valu)
-    hipLaunchKernelGGL(stem_conv1_mfma_kernel<true>, dim3(grid), dim3(256), 0, st, img, N, S, w27x64, scale, shift,
-                       (__bf16*)out, Ho, floor_, ngroups);
+    hipLaunchKernelGGL(stem_conv1_mfma_kernel<1>, dim3(grid), dim3(256), 0, st, img, N, S, w27x64, scale, shift,
+                       (void*)out, Ho, floor_, ngroups);
+  else if (!valu && layout != ACT_SPLIT && layout != ACT_BF16)  // fp32 NHWC: the exact f32 MFMA form
+    hipLaunchKernelGGL(stem_conv1_mfma_kernel<2>, dim3(grid), dim3(256), 0, st, img, N, S, w27x64, scale, shift,
+                       (void*)out, Ho, floor_, ngroups);
   else if (layout == ACT_SPLIT)
     hipLaunchKernelGGL(stem_conv1_s_kernel<false>, dim3(cdiv(total * 8, 256)), dim3(256), 0, st, img, N, S, w27x64,
                        scale, shift, (__bf16*)out, Ho, floor_);
