@@ -260,7 +260,9 @@ int launch_stem_conv1(const float* img, int N, int S, const float* w27x64, const
   const float floor_ = relu ? 0.f : -INFINITY;  // relu = 0: raw conv (training-mode BN follows)
   static const bool valu = getenv("CWT_STEM_VALU") && atoi(getenv("CWT_STEM_VALU"));  // A/B switch
   const int ngroups = (int)cdiv(total, 16);
-  const int grid = (int)std::min<long>(cdiv(ngroups, 4 * 4), 2048);  // ~4 groups per wave, 4 waves per block
+  // ~gpw groups of 16 pixels per wave (4 waves per block); CWT_STEM_GPW for A/B
+  static const int gpw = getenv("CWT_STEM_GPW") ? std::max(1, atoi(getenv("CWT_STEM_GPW"))) : 4;
+  const int grid = (int)std::min<long>(cdiv(ngroups, 4 * gpw), 8192);
   if (layout == ACT_SPLIT && !valu)
     hipLaunchKernelGGL(stem_conv1_mfma_kernel<0>, dim3(grid), dim3(256), 0, st, img, N, S, w27x64, scale, shift,
                        (void*)out, Ho, floor_, ngroups);
