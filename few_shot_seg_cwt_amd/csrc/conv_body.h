@@ -145,11 +145,7 @@ __device__ __forceinline__ void split3_bf16(const f32x4& x0, const f32x4& x1, bf
 // barrier, so the ring keeps NSTG - 1 tiles in flight either way.
 // PF bits: 1 fragment prefetch; 2 / 4 timing studies (no MFMAs / no operand DMA); 8 buffer
 // addressing of the operand DMA (every production instantiation sets it); 16 timing study of the
-// x6 WN = 128 forms without the A split (wrong numbers, same data movement and MFMAs); 32 (x6,
-// WN = 128, one wave column: every wave's A rows are its own LDS-DMA pieces) early split: tile
-// t+1's A fragments are read and split in the middle of tile t's MFMA stream, as soon as the
-// wave's own pieces of it have landed (its vmcnt, no barrier), instead of in a VALU burst after
-// tile t+1's barrier that every wave of the workgroup reaches at once.
+// x6 WN = 128 forms without the A split (wrong numbers, same data movement and MFMAs).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF>
 __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   static_assert(PREC == 0 || PREC == 1 || PREC == 3 || PREC == 6,
@@ -450,68 +446,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
     }
   };
 
-  constexpr bool ES = PREC == 6 && (PF & 32) != 0;
-  static_assert(!ES || (LAZY_B && WAVES_N == 1 && LA * 8 == WM), "early split: WN = 128 forms, one wave column");
-  if constexpr (ES) {
-#pragma unroll
-    for (int s = 0; s < NSTG - 1; ++s)
-      if (s < T) issue(s);
-    // this wave's A fragments of the tile in stage stg, split (its own rows: no barrier needed)
-    auto read_split_a = [&](bf16x8 (&as)[FM][3], int stg) {
-      const char* sb = smem + stg * STG_BYTES;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const char* pa = sb + (a_row0 + i * 16) * 128;
-        const bf16x8 x0 = *(const bf16x8*)(pa + off_a0), x1 = *(const bf16x8*)(pa + off_a1);
-        split3_bf16(__builtin_bit_cast(f32x4, x0), __builtin_bit_cast(f32x4, x1), as[i][0], as[i][1], as[i][2]);
-      }
-    };
-    // vector-memory ops issued after a tile's A pieces by the time its early split waits, in the
-    // steady state (the tile's own B / lo pieces and the NSTG - 2 tiles issued after it); near the
-    // end fewer are in flight and the wait takes them all
-    constexpr int NSTEADY = LB + LBL + LPT * (NSTG - 2);
-    bf16x8 asc[FM][3];
-    if (T > 0) {
-      wait_tiles<LPT>(min(NSTG - 2, T - 1));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      read_split_a(asc, 0);
-    }
-    for (int t = 0; t < T; ++t) {
-      wait_tiles<LPT>(min(NSTG - 2, T - 1 - t));
-      block_sync_lds();
-      const bool more = t + NSTG - 1 < T;
-      if (more) issue((t + NSTG - 1) % NSTG);
-      bf16x8 asn[FM][3];
-      const char* sb = smem + (t % NSTG) * STG_BYTES;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        if (j == FN / 2 && t + 1 < T) {  // tile t+1's A: wait for this wave's pieces, read, split
-          if (more || NSTG > 2) {
-            if (t + NSTG - 1 < T) wait_vmcnt<NSTEADY>(); else wait_vmcnt<0>();
-          } else {
-            wait_vmcnt<0>();
-          }
-          read_split_a(asn, (t + 1) % NSTG);
-        }
-        const char* p = sb + (b_row0 + j * 16) * 128;
-        const bf16x8 bh = *(const bf16x8*)(p + off_hi), bm = *(const bf16x8*)(p + off_lo);
-        const bf16x8 bl = *(const bf16x8*)(sb + LO_OFF + (wn * WN + j * 16) * 64 + off_l);
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {  // smallest products first
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asc[i][1], bm, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asc[i][2], bh, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asc[i][0], bl, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asc[i][1], bh, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asc[i][0], bm, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(asc[i][0], bh, acc[i][j], 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) asc[i][k] = asn[i][k];
-    }
-  } else if constexpr ((PF & 1) == 0) {
+  if constexpr ((PF & 1) == 0) {
 #pragma unroll
     for (int s = 0; s < NSTG - 1; ++s)
       if (s < T) issue(s);
