@@ -2697,8 +2697,7 @@ static int debug_conv_s(cwt_ctx* ctx, int prec, const void* xs, int N, int Hi, i
               "tile must be one of 256x256, 256x128, 128x256, 128x128, 128x64, 64x128, 64x64");
     const bool x6_var = prec == 6 && ((var == 3 && (bm >= 128 && bn >= 128)) || (var == 5 && bm == 128 && bn == 128) ||
                                       ((var == 3 || var == 5) && bm == 64 && bn == 128) ||
-                                      ((var == 12 || var == 14 || var == 15 || var == 16) && bm == 128 && bn == 128) ||
-                                      (var == 17 && bm == 256 && bn == 128) ||
+                                      ((var == 12 || var == 14 || var == 15) && bm == 128 && bn == 128) ||
                                       (var == 13 && bm == 256 && bn == 256));
     CWT_CHECK((var >= 0 && var <= 2) || (var == 4 && bm == 128 && bn == 128) || (var >= 8 && var <= 11) || x6_var,
               "variant must be 0, 1, 2, 4 (128x128 only), 8 .. 11 (timing study), or for x6 3 (tiles >= 128x128) "

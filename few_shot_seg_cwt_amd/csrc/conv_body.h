@@ -145,10 +145,7 @@ __device__ __forceinline__ void split3_bf16(const f32x4& x0, const f32x4& x1, bf
 // barrier, so the ring keeps NSTG - 1 tiles in flight either way.
 // PF bits: 1 fragment prefetch; 2 / 4 timing studies (no MFMAs / no operand DMA); 8 buffer
 // addressing of the operand DMA (every production instantiation sets it); 16 timing study of the
-// x6 WN = 128 forms without the A split (wrong numbers, same data movement and MFMAs); 128 (x6,
-// WN = 128, WM = 32) the products on v_mfma_f32_32x32x16_bf16 (one 32x32 block per B column block
-// and 16-deep K-step: half the MFMA instructions, each holding the SIMD's vector issue for 8 of
-// its 32 cycles instead of 8 of 16).
+// x6 WN = 128 forms without the A split (wrong numbers, same data movement and MFMAs).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF>
 __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   static_assert(PREC == 0 || PREC == 1 || PREC == 3 || PREC == 6,
@@ -327,14 +324,6 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr bool M32 = PREC == 6 && (PF & 128) != 0;
-  static_assert(!M32 || (WM == 32 && WN % 32 == 0 && (PF & 3) == 0), "32x32 products: WM = 32 forms");
-  constexpr int FN32 = WN / 32;
-  f32x16 acc32[M32 ? FN32 : 1];
-#pragma unroll
-  for (int j = 0; j < (M32 ? FN32 : 1); ++j)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc32[j][q] = 0.f;
 
   // fragment read geometry: lane -> row (lane & 15) of a 16-row block, k-chunk (lane >> 4)
   const int fr = lane & 15, fk = lane >> 4;
@@ -368,7 +357,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
       F.bl[j] = *(const bf16x8*)(p + off_lo);
     }
 #pragma unroll
-    for (int i = 0; i < (M32 ? 0 : FM); ++i) {
+    for (int i = 0; i < FM; ++i) {
       const char* p = sb + (a_row0 + i * 16) * 128;
       F.ah[i] = *(const bf16x8*)(p + off_a0);
       F.al[i] = *(const bf16x8*)(p + off_a1);
@@ -387,38 +376,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
         asm volatile("" ::"v"(F.bh[j]), "v"(F.bl[j]), "v"(F.bo[j < (PREC == 6 && !LAZY_B ? FN : 1) ? j : 0]));
       return;
     }
-    if constexpr (M32) {  // 32x32x16: two 16-deep K-steps per tile; lane: row / column lane & 31, k 8 (lane >> 5)
-      const char* sb = smem + stg * STG_BYTES;
-      const int r32 = lane & 31, h32 = lane >> 5;
-      const int swA = (r32 >> 1) & 7;  // a_row0 and the block offsets are multiples of 32
-      bf16x8 as2[2][3];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int c = 4 * ks + 2 * h32;
-        const char* pa = sb + (a_row0 + r32) * 128;
-        const f32x4 x0 = *(const f32x4*)(pa + ((c ^ swA) << 4)), x1 = *(const f32x4*)(pa + (((c + 1) ^ swA) << 4));
-        split3_bf16(x0, x1, as2[ks][0], as2[ks][1], as2[ks][2]);
-      }
-#pragma unroll
-      for (int jb = 0; jb < FN32; ++jb) {
-        const int rb = wn * WN + jb * 32 + r32;  // the row of the B tile (and of its lo plane)
-        const char* pb = sb + (BM + rb) * 128;
-        const int swL = (rb >> 2) & 3;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int ch = 2 * ks + h32;
-          const bf16x8 bh = *(const bf16x8*)(pb + ((ch ^ swA) << 4));
-          const bf16x8 bm = *(const bf16x8*)(pb + (((4 + ch) ^ swA) << 4));
-          const bf16x8 bl = *(const bf16x8*)(sb + LO_OFF + rb * 64 + ((ch ^ swL) << 4));
-          acc32[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as2[ks][1], bm, acc32[jb], 0, 0, 0);
-          acc32[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as2[ks][2], bh, acc32[jb], 0, 0, 0);
-          acc32[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as2[ks][0], bl, acc32[jb], 0, 0, 0);
-          acc32[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as2[ks][1], bh, acc32[jb], 0, 0, 0);
-          acc32[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as2[ks][0], bm, acc32[jb], 0, 0, 0);
-          acc32[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as2[ks][0], bh, acc32[jb], 0, 0, 0);
-        }
-      }
-    } else if constexpr (LAZY_B) {  // split every A fragment, then one B column at a time from the stage
+    if constexpr (LAZY_B) {  // split every A fragment, then one B column at a time from the stage
       const char* sb = smem + stg * STG_BYTES;
       bf16x8 as[FM][3];
 #pragma unroll
@@ -560,15 +518,7 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if constexpr (!M32) ep[(fi * 16 + fq * 4 + q) * EP_LD + j * 16 + fr] = acc[pass * (EP_ROWS / 16) + fi][j][q];
-    if constexpr (M32) {  // 32x32 D layout: column lane & 31, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-#pragma unroll
-      for (int jb = 0; jb < FN32; ++jb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          ep[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * EP_LD + jb * 32 + (lane & 31)] = acc32[jb][r];
-    }
+        for (int q = 0; q < 4; ++q) ep[(fi * 16 + fq * 4 + q) * EP_LD + j * 16 + fr] = acc[pass * (EP_ROWS / 16) + fi][j][q];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     f32x4 v0[RR], v1[RR];
 #pragma unroll

@@ -62,8 +62,6 @@ static void launch_tiles_x6_stage(const ConvSArgs& a, const ConvPlan& p, dim3 gr
     if (v == 12) X6(128, 128, 4, 1, 2, 16);  // timing study: var 5 without the A split
     else if (v == 14) X6(128, 128, 4, 1, 2, 4);   // timing study: var 5 without operand DMA
     else if (v == 15) X6(128, 128, 4, 1, 2, 2);   // timing study: var 5 without MFMAs
-    else if (v == 16) X6(128, 128, 4, 1, 2, 128);  // var 5 on the 32x32x16 MFMA
-    else if (v == 17) X6(256, 128, 8, 1, 2, 128);  // 256x128 var 3 on the 32x32x16 MFMA
     else if (v == 13) X6(256, 256, 4, 2, 2, 16);  // timing study: 256x256 var 3 without the A split
     else if (v == 8) X6(64, 64, 2, 2, 4, 2);
     else if (v == 9) X6(64, 64, 2, 2, 4, 4);

@@ -291,8 +291,7 @@ TOL_X6 = 1e-5
 # the x6-only forms (bm = 1000 * variant + rows): 3 the WN = 128 wave layouts, 5 128x128 4x1 on a
 # 2-stage ring (two workgroups per CU)
 X6_FORMS = [(3256, 256, 1), (3256, 128, 1), (3128, 256, 1), (3128, 128, 1), (3128, 128, 2), (5128, 128, 1),
-            (5128, 128, 4), (3064, 128, 1), (5064, 128, 1), (5064, 128, 2), (16128, 128, 1), (16128, 128, 2),
-            (17256, 128, 1)]
+            (5128, 128, 4), (3064, 128, 1), (5064, 128, 1), (5064, 128, 2)]
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))

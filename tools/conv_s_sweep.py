@@ -146,8 +146,6 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
                         continue   # two-workgroups-per-CU 128x128 form
                     if 8 <= var < 16 and (bm, bn) != ((64, 64) if var < 10 else (128, 128)):
                         continue   # timing-study kernels: fixed tiles
-                    if var >= 16 and not (x6v and (bm, bn) == {16: (128, 128), 17: (256, 128)}[var]):
-                        continue   # x6 only: the 32x32x16 forms (conv_x6.hip var 16, 17)
                     if var == 2 and (bm == 256 or bn == 256):
                         continue   # 8-wave form only for the 128/64 tiles
                     for ns in (1, 2, 4, 8):
