@@ -131,18 +131,6 @@ static const MeasuredPlanS6 kMeasuredPlansX6[] = {
 #include "conv_plans_x6.inc"
     {0, 0, 0, 0, 0, 0, 0, 0}};
 
-// A/B (CWT_X6_NO256=1): a table plan on 256x256 tiles (one workgroup holds a CU's whole LDS)
-// becomes 128x128 var 5 (two per CU) -- in the episode pipeline the inner loop holds 59 CUs
-static ConvPlan no256(ConvPlan p) {
-  static const bool on = getenv("CWT_X6_NO256") && getenv("CWT_X6_NO256")[0] == '1';
-  if (on && p.bm == 256 && p.bn == 256) {
-    p.bm = 128;
-    p.bn = 128;
-    p.var = 5;
-  }
-  return p;
-}
-
 // fp32 width on the bf16 matrix cores (conv_igemm_x6): 32-deep K-tiles over f32d's operands; its
 // own measured table (conv_plans_x6.inc, tools/conv_s_sweep.py --prec 6), else the heuristic.
 ConvPlan plan_conv_x6(int M, int Co, int K) {
@@ -155,7 +143,7 @@ ConvPlan plan_conv_x6(int M, int Co, int K) {
       p.var = e.var;
       p.kt_per_split = cdiv(ktiles, e.nsplit);
       p.nsplit = cdiv(ktiles, p.kt_per_split);
-      return no256(p);
+      return p;
     }
   return plan_heuristic_s(M, Co, ktiles);
 }
@@ -173,7 +161,7 @@ ConvPlan plan_conv_x6_batched(int M, int Co, int K, int batch) {
       p.var = e.var;
       p.kt_per_split = ktiles;
       p.nsplit = 1;
-      return no256(p);
+      return p;
     }
   static const int cand[7][2] = {{256, 256}, {256, 128}, {128, 256}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
   ConvPlan best;
