@@ -138,8 +138,8 @@ def pmc_traffic(dom_name: str):
             if mt:
                 # kernel names carry <BM, BN, WAVES_M, WAVES_N, NSTG, STAGE, PF>
                 kind, bm, bn, stage = mt.group(1), mt.group(2), mt.group(3), mt.group(4)
-                if kind in ("x6w", "x6w4"):   # the Winograd forms: their batched GEMM (stage 7 / 8)
-                    kind, stage = "x6", ("7" if kind == "x6w" else "8")
+                if kind in ("x6w", "x6w4"):   # the Winograd forms: their batched GEMM (stage 7 / 8; the bottleneck 6)
+                    kind, stage = "x6", ("8" if kind == "x6w4" else "6" if stage == "6" else "7")
                 targs = k.split(">(")[0].split("<", 1)[-1].split(", ")
                 hit = (f"conv_igemm_{kind}<" in k and len(targs) >= 6 and targs[0] == bm and targs[1] == bn
                        and targs[5] == stage)

@@ -757,10 +757,9 @@ static int run_wino_conv(cwt_ctx* ctx, const float* x, int N, int H, int W, int 
     p.bn = bn;
     if (Co % p.bn) return fail(CWT_EARG, "winograd GEMM tile: Co % bn");
   }
-  // the batched GEMMs are the stage-7 (F(2x2)) / stage-8 (F(4x4)) instantiations: their own
-  // rocprofv3 statistics
-  (void)stage;
-  if ((rc = launch_conv_x3s(a, p, m == 4 ? 8 : 7, nullptr, 0, st, 6))) return rc;
+  // the batched GEMMs are the stage-7 (F(2x2)) / stage-8 (F(4x4)) instantiations, the
+  // bottleneck's (stage 6) its own: their own rocprofv3 statistics
+  if ((rc = launch_conv_x3s(a, p, m == 4 ? 8 : stage == 6 ? 6 : 7, nullptr, 0, st, 6))) return rc;
   return launch_wino_out((const float*)Mb, g, Co, scale, shift, res, res_ld, relu, y, y_ld, y_off, st);
 }
 

@@ -36,8 +36,8 @@ def pmc_key(name):
     m = re.match(r"conv_igemm_(\w+?)<(\d+),(\d+),(\d+)>", name)
     if not m:
         return None
-    if m.group(1) in ("x6w", "x6w4"):   # F(2x2) / F(4x4): stage 7 / 8
-        return "x6", m.group(2), m.group(3), "7" if m.group(1) == "x6w" else "8"
+    if m.group(1) in ("x6w", "x6w4"):   # F(2x2) / F(4x4): stage 7 / 8 (the bottleneck's F(2x2): its own 6)
+        return "x6", m.group(2), m.group(3), ("8" if m.group(1) == "x6w4" else "6" if m.group(4) == "6" else "7")
     return m.group(1), m.group(2), m.group(3), m.group(4)
 
 
