@@ -204,6 +204,37 @@ def conv_roofline(fine, peak_tflops):
                               "summed over the stack's conv launches (one episode, per-launch events)"}
 
 
+def wino_executed(recs, dn, dms, peak):
+    """The Winograd bottleneck priced on the work it executes (SURVEY §8(d):
+    algebraic shortcuts reported separately from the reference-formulation figure).  The conv's
+    record (conv_igemm_x6w...) brackets the input transform, the batched GEMMs and the output
+    transform; the library's sub-records (wino_in / wino_gemm / wino_out, api.hip run_wino_conv,
+    the same profile level) carry the GEMMs' executed FLOPs (2 x P x tiles x Ci x Co: 4/9 of the
+    direct conv at F(2x2,3x3)) and the transforms' algorithmic bytes."""
+    sub = {k: [r for r in recs if r[0].startswith(k + " ")] for k in ("wino_in", "wino_gemm", "wino_out")}
+    if not dn or not all(sub.values()):
+        return {}
+    n = len(sub["wino_gemm"])
+    ms = {k: sum(r[3] for r in v) / len(v) for k, v in sub.items()}
+    by = {k: sum(r[2] for r in v) / len(v) for k, v in sub.items()}
+    fl_ex = sum(r[1] for r in sub["wino_gemm"]) / n
+    launch_ms = dms / dn
+    return {"winograd": {
+        "form": "F(2x2,3x3): input transform -> 16 batched x6 GEMMs -> output transform (DESIGN.md §3)",
+        "flops_executed_per_launch": fl_ex,
+        "frac_executed": round(fl_ex / (launch_ms * 1e-3) / 1e12 / peak, 4),
+        "frac_executed_note": "the GEMMs' executed FLOPs / the whole conv bracket (transforms included) / the x6 roof",
+        "gemm_ms": round(ms["wino_gemm"], 4),
+        "gemm_tflops_executed": round(fl_ex / (ms["wino_gemm"] * 1e-3) / 1e12, 2),
+        "gemm_frac_executed": round(fl_ex / (ms["wino_gemm"] * 1e-3) / 1e12 / peak, 4),
+        "input_transform_ms": round(ms["wino_in"], 4), "input_transform_bytes": round(by["wino_in"]),
+        "output_transform_ms": round(ms["wino_out"], 4), "output_transform_bytes": round(by["wino_out"]),
+        "transforms_GBps": round((by["wino_in"] + by["wino_out"]) / ((ms["wino_in"] + ms["wino_out"]) * 1e-3) / 1e9, 1),
+        "gemm_bytes": round(by["wino_gemm"]),
+        "bytes_executed_per_launch": round(by["wino_in"] + by["wino_gemm"] + by["wino_out"]),
+        "records": n}}
+
+
 class adapt_leg:
     """Launch the inner loops of a side leg (timing studies, the exact-fp32 leg) as their own
     instantiation of the persistent kernel (CWT_ADAPT_DBG: 128 = the SIDE instantiation, code
@@ -964,7 +995,8 @@ def main():
                           "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                           "traffic_source": traffic_src,
                           "peak_basis": peak_basis, "launches_per_step": dn // args.steps,
-                          "flops_per_launch": dfl / dn, "avg_launch_ms": round(dms / dn, 4)},
+                          "flops_per_launch": dfl / dn, "avg_launch_ms": round(dms / dn, 4),
+                          **wino_executed(recs, dn, dms, peak)},
         "conv_stack": {"tflops": round(ex_fl / (ex_ms * 1e-3) / 1e12, 2),
                        "frac": round(ex_fl / (ex_ms * 1e-3) / 1e12 / peak, 4),
                        "gflop_per_step": round(ex_fl / args.steps / 1e9, 1),

@@ -102,6 +102,7 @@ SIGNATURES = {
     "cwt_pretrain_num_params": (_I, [_P, C.POINTER(_I64), C.POINTER(_I64)]),
     "cwt_cu_count": (_I, [_P, _P]),
     "cwt_adapt_workgroups": (_I, [_P, _I, _I, _I, _I, _I, _P]),
+    "cwt_adapt_fuses_tail": (_I, [_P, _I, _I, _I, _I, _P]),
     "cwt_stream_create_masked": (_I, [_P, _P, _I, _P]),
     "cwt_stream_destroy": (_I, [_P]),
     "cwt_debug_conv": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I,

@@ -723,7 +723,15 @@ static int run_wino_conv(cwt_ctx* ctx, const float* x, int N, int H, int W, int 
   if ((rc = ensure_ws(ctx, "wino.V", (size_t)g.P * g.T * Ci * 4, &V)) ||
       (rc = ensure_ws(ctx, "wino.M", (size_t)g.P * g.T * Co * 4, &Mb)) || (rc = zero_line(ctx, &zero)))
     return rc;
-  if ((rc = launch_wino_in(x, g, Ci, (float*)V, st))) return rc;
+  // sub-records (the executed work of the form): the transforms' algorithmic bytes
+  // and the batched GEMMs' executed FLOPs, at the conv record's own profile level
+  const int plev = stage == 6 ? 1 : 2;
+  const double vb = 4.0 * g.P * g.T * Ci, mb = 4.0 * g.P * g.T * Co;
+  Prof pin(ctx, st, "wino_in " + std::to_string(Ci) + "@" + std::to_string(H), 0.0,
+           4.0 * N * H * W * Ci + vb, plev);
+  rc = launch_wino_in(x, g, Ci, (float*)V, st);
+  pin.end();
+  if (rc) return rc;
   ConvSArgs a;
   memset(&a, 0, sizeof(a));
   a.xs = (const __bf16*)V;
@@ -759,8 +767,16 @@ static int run_wino_conv(cwt_ctx* ctx, const float* x, int N, int H, int W, int 
   }
   // the batched GEMMs are the stage-7 (F(2x2)) / stage-8 (F(4x4)) instantiations, the
   // bottleneck's (stage 6) its own: their own rocprofv3 statistics
-  if ((rc = launch_conv_x3s(a, p, m == 4 ? 8 : stage == 6 ? 6 : 7, nullptr, 0, st, 6))) return rc;
-  return launch_wino_out((const float*)Mb, g, Co, scale, shift, res, res_ld, relu, y, y_ld, y_off, st);
+  Prof pg(ctx, st, "wino_gemm " + std::to_string(Ci) + "x" + std::to_string(Co) + "@" + std::to_string(H),
+          2.0 * g.P * g.T * Ci * Co, vb + 6.0 * g.P * Co * Ci + mb, plev);
+  rc = launch_conv_x3s(a, p, m == 4 ? 8 : stage == 6 ? 6 : 7, nullptr, 0, st, 6);
+  pg.end();
+  if (rc) return rc;
+  const double ob = 4.0 * N * H * W * Co * (res ? 2.0 : 1.0);
+  Prof pout(ctx, st, "wino_out " + std::to_string(Co) + "@" + std::to_string(H), 0.0, mb + ob, plev);
+  rc = launch_wino_out((const float*)Mb, g, Co, scale, shift, res, res_ld, relu, y, y_ld, y_off, st);
+  pout.end();
+  return rc;
 }
 
 // Training-mode BN of one extraction (cwt_extract_features_train_bn; bn_train.hip)
@@ -1517,6 +1533,17 @@ int cwt_episode_tail(cwt_ctx* ctx, const float* q, const float* f, int B, int h,
   return rc;
 }
 
+// cwt_inner_adapt_tail fuses the tail into the loop's launch where the loop runs as the two-unit
+// register form (EpisodePipeline's adapt context) in its product instantiation
+static bool fused_tail_applies(cwt_ctx* ctx, int n, int h, int w, int iters) {
+  const char* kname = adapt_kernel_name(1, n, h, w, iters, ctx->adapt_upw);
+  const char* dbg = getenv("CWT_ADAPT_DBG");
+  const char* fz = getenv("CWT_FUSED_LOOP_TAIL");
+  const char* tst = getenv("CWT_TAIL_STAMPS");
+  return strcmp(kname, "adapt_persist_kernel<5") == 0 && !(dbg && atoi(dbg) != 0) && !(fz && fz[0] == '0') &&
+         !(tst && tst[0] == '1');
+}
+
 int cwt_inner_adapt_tail(cwt_ctx* ctx, const float* f_s, const int64_t* s_label, int n, int h, int w, int C, int S,
                          float lr, int iters, float* W_inout, const float* f_q, const int64_t* q_label,
                          const float* w_qkvs, const float* fc_w, const float* fc_b, const float* ln_w,
@@ -1532,13 +1559,7 @@ int cwt_inner_adapt_tail(cwt_ctx* ctx, const float* f_s, const int64_t* s_label,
   CWT_HIP(hipSetDevice(ctx->device));
   // fused where the loop runs as the two-unit register form (EpisodePipeline's adapt context) in
   // its product instantiation; everything else (and CWT_FUSED_LOOP_TAIL=0) runs the two calls
-  const char* kname = adapt_kernel_name(1, n, h, w, iters, ctx->adapt_upw);
-  const char* dbg = getenv("CWT_ADAPT_DBG");
-  const char* fz = getenv("CWT_FUSED_LOOP_TAIL");
-  const char* tst = getenv("CWT_TAIL_STAMPS");
-  const bool fuse = strcmp(kname, "adapt_persist_kernel<5") == 0 && !(dbg && atoi(dbg) != 0) && !(fz && fz[0] == '0') &&
-                    !(tst && tst[0] == '1');
-  if (!fuse) {
+  if (!fused_tail_applies(ctx, n, h, w, iters)) {
     int rc = cwt_inner_adapt(ctx, f_s, s_label, n, h, w, C, S, lr, iters, W_inout, stream);
     if (rc) return rc;
     return cwt_episode_tail(ctx, W_inout, f_q, 1, h, w, S, q_label, w_qkvs, fc_w, fc_b, ln_w, ln_b, params_version, out,
@@ -1577,14 +1598,20 @@ int cwt_inner_adapt_tail(cwt_ctx* ctx, const float* f_s, const int64_t* s_label,
     ctx->tail_epoch = 0;
     ctx->tail_G = G;
   }
-  // this launch's stamp slot: {start (min), loop end (max), tail end (max)}, pre-set {~0, 0, 0}
+  // this launch's stamp slot: {start (min), loop end (max), tail end (max)}, pre-set {~0, 0, 0}; only
+  // when the profile records it (otherwise no memsets on the adapt stream and no stamp atomics: the
+  // kernel guards every use of a null slot)
   constexpr int kFSlots = 4096;
-  if (!ctx->fstamps) CWT_HIP(hipMalloc(&ctx->fstamps, (size_t)kFSlots * 3 * sizeof(unsigned long long)));
-  const int slot = ctx->fstamp_next;
-  ctx->fstamp_next = (ctx->fstamp_next + 1) % kFSlots;
-  unsigned long long* fst = ctx->fstamps + 3 * slot;
-  CWT_HIP(hipMemsetAsync(fst, 0xFF, sizeof(unsigned long long), st));
-  CWT_HIP(hipMemsetAsync(fst + 1, 0, 2 * sizeof(unsigned long long), st));
+  int slot = -1;
+  unsigned long long* fst = nullptr;
+  if (ctx->prof_level >= 1) {
+    if (!ctx->fstamps) CWT_HIP(hipMalloc(&ctx->fstamps, (size_t)kFSlots * 3 * sizeof(unsigned long long)));
+    slot = ctx->fstamp_next;
+    ctx->fstamp_next = (ctx->fstamp_next + 1) % kFSlots;
+    fst = ctx->fstamps + 3 * slot;
+    CWT_HIP(hipMemsetAsync(fst, 0xFF, sizeof(unsigned long long), st));
+    CWT_HIP(hipMemsetAsync(fst + 1, 0, 2 * sizeof(unsigned long long), st));
+  }
   TailArgs ta;
   if ((rc = fill_episode_tail_args(W_inout, f_q, 1, hw, h, w, S, q_label, (const float*)fold, fc_b, ln_w, ln_b, out,
                                    logits, logits0, iut, ce, iut0, (float*)tws, (unsigned*)cnt, ctx->tail_epoch++, G,
@@ -2898,6 +2925,13 @@ int cwt_adapt_workgroups(cwt_ctx* ctx, int E, int n, int h, int w, int iters, in
   if (!ctx || !G || E < 1 || n < 1 || h < 2 || w < 2) return fail(CWT_EARG, "bad arguments");
   CWT_HIP(hipSetDevice(ctx->device));
   *G = adapt_persist_workgroups(E, n, h, w, iters, ctx->adapt_upw);
+  return 0;
+}
+
+int cwt_adapt_fuses_tail(cwt_ctx* ctx, int n, int h, int w, int iters, int* fused) {
+  if (!ctx || !fused || n < 1 || h < 2 || w < 2 || iters < 0) return fail(CWT_EARG, "bad arguments");
+  CWT_HIP(hipSetDevice(ctx->device));
+  *fused = fused_tail_applies(ctx, n, h, w, iters) ? 1 : 0;
   return 0;
 }
 

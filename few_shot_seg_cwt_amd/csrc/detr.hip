@@ -151,8 +151,10 @@ int launch_deform_attn(const float* value, const float* offsets, const float* lo
 //   deform_attn_dv_finish_kernel converts it back.
 __global__ void absmax_bits_kernel(const float* __restrict__ x, long n, unsigned* __restrict__ out) {
   float m = 0.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(x[i]));
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = fabsf(x[i]);
+    if (v <= 3.4028235e38f) m = fmaxf(m, v);  // finite values only (NaN / Inf take the float path below)
+  }
   for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // order-free: deterministic
 }
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(256) void deform_attn_bwd_kernel(const float* __res
                                                               const float* __restrict__ logits, int B, int H, int W,
                                                               int M, int P, int D, const float* __restrict__ d_out,
                                                               unsigned long long* dv64, const unsigned* gmax_bits,
-                                                              int headroom, float* __restrict__ d_offsets,
+                                                              int headroom, float* d_value, float* __restrict__ d_offsets,
                                                               float* __restrict__ d_logits) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
@@ -191,6 +193,7 @@ __global__ __launch_bounds__(256) void deform_attn_bwd_kernel(const float* __res
   const long vs = (long)M * D;
   const float* vb = value + (long)b * L * vs + m * D + lane;
   unsigned long long* dvb = dv64 + (long)b * L * vs + m * D + lane;
+  float* dvf = d_value + (long)b * L * vs + m * D + lane;
   const double S = dv_scale(gmax_bits, headroom);
   const bool act = lane < D;
   const float g = act ? d_out[bq * vs + m * D + lane] : 0.f;
@@ -223,11 +226,19 @@ __global__ __launch_bounds__(256) void deform_attn_bwd_kernel(const float* __res
     ap[p] = a;
     sad += a * da[p];
     const float gv = a * g;
-    auto fx64 = [&](float c) { return (unsigned long long)(long long)rint((double)c * S); };
-    if (i00) atomicAdd(&dvb[((long)y0 * W + x0) * vs], fx64(w00 * gv));
-    if (i01) atomicAdd(&dvb[((long)y0 * W + x1) * vs], fx64(w01 * gv));
-    if (i10) atomicAdd(&dvb[((long)y1 * W + x0) * vs], fx64(w10 * gv));
-    if (i11) atomicAdd(&dvb[((long)y1 * W + x1) * vs], fx64(w11 * gv));
+    // a non-finite contribution (NaN / Inf in d_out or the logits) goes to d_value itself as a float
+    // atomic, as the reference's CUDA op adds it, so it propagates to exactly the positions it reaches;
+    // the finish kernel adds the fixed-point sum to it (0 elsewhere)
+    auto add = [&](long pos, float c) {
+      if (fabsf(c) <= 3.4028235e38f)
+        atomicAdd(&dvb[pos], (unsigned long long)(long long)rint((double)c * S));
+      else
+        atomicAdd(&dvf[pos], c);
+    };
+    if (i00) add(((long)y0 * W + x0) * vs, w00 * gv);
+    if (i01) add(((long)y0 * W + x1) * vs, w01 * gv);
+    if (i10) add(((long)y1 * W + x0) * vs, w10 * gv);
+    if (i11) add(((long)y1 * W + x1) * vs, w11 * gv);
   }
   if (lane == 0) {
     float* dl = d_logits + (bq * M + m) * P;
@@ -245,7 +256,7 @@ __global__ void deform_attn_dv_finish_kernel(const unsigned long long* __restric
                                              float* __restrict__ d_value) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  d_value[i] = (float)((double)(long long)dv64[i] / dv_scale(gmax_bits, headroom));
+  d_value[i] += (float)((double)(long long)dv64[i] / dv_scale(gmax_bits, headroom));  // + the non-finite part
 }
 
 size_t deform_attn_bwd_ws_bytes(int B, int H, int W, int M, int D) { return 256 + (size_t)B * H * W * M * D * 8; }
@@ -261,12 +272,14 @@ int launch_deform_attn_bwd(const float* value, const float* offsets, const float
   unsigned long long* dv64 = (unsigned long long*)((char*)ws + 256);
   int headroom = 1;  // bits for the number of contributions per position (<= H W P) and the sign
   while ((1L << headroom) < (long)H * W * P * 2) ++headroom;
-  if (hipMemsetAsync(ws, 0, 256 + (size_t)n * 8, st) != hipSuccess) return fail(CWT_ESTATE, "deform_attn_bwd: memset");
+  if (hipMemsetAsync(ws, 0, 256 + (size_t)n * 8, st) != hipSuccess ||
+      hipMemsetAsync(d_value, 0, (size_t)n * 4, st) != hipSuccess)
+    return fail(CWT_ESTATE, "deform_attn_bwd: memset");
   hipLaunchKernelGGL(absmax_bits_kernel, dim3((unsigned)std::min<long>(1024, cdiv(n, 256))), dim3(256), 0, st, d_out, n,
                      gmax);
   CWT_LAUNCH_CHECK();
   hipLaunchKernelGGL(deform_attn_bwd_kernel, dim3((unsigned)cdiv(nw, 4)), dim3(256), 0, st, value, offsets, logits, B, H,
-                     W, M, P, D, d_out, dv64, (const unsigned*)gmax, headroom, d_offsets, d_logits);
+                     W, M, P, D, d_out, dv64, (const unsigned*)gmax, headroom, d_value, d_offsets, d_logits);
   CWT_LAUNCH_CHECK();
   hipLaunchKernelGGL(deform_attn_dv_finish_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st,
                      (const unsigned long long*)dv64, n, (const unsigned*)gmax, headroom, d_value);

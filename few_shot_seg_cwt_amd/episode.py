@@ -355,9 +355,13 @@ class EpisodePipeline:
                 _lib.check(_lib.lib().cwt_adapt_workgroups(c, 1, shot, h, w, iters, ctypes.byref(g)),
                            "cwt_adapt_workgroups")
                 gs.append(g.value)
-            # the adapt context's fused tail (a 64-workgroup co-resident grid, cwt_episode_tail on a
-            # context with cwt_ctx_set_adapt_units >= 2) may run beside the drain loop as well
-            tail_g = min(64, _lib.cu_count(self.device))
+            # the previous episode's tail may run beside the drain loop as well: nothing extra where
+            # the adapt context fuses it into its loop's own workgroups (cwt_inner_adapt_tail), else a
+            # 64-workgroup co-resident grid (cwt_episode_tail)
+            fz = ctypes.c_int(0)
+            _lib.check(_lib.lib().cwt_adapt_fuses_tail(self.c_adapt, shot, h, w, iters, ctypes.byref(fz)),
+                       "cwt_adapt_fuses_tail")
+            tail_g = 0 if fz.value else min(64, _lib.cu_count(self.device))
             self._fits[key] = min(gs) > 0 and sum(gs) + tail_g <= _lib.cu_count(self.device)
         return self._fits[key]
 

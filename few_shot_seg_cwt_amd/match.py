@@ -46,6 +46,7 @@ import torch.nn.functional as F
 from . import _lib
 from .heads import get_corr
 from .transformer import as_tokens
+from .util import dropout_seed
 
 
 def MutualMatching(corr4d: torch.Tensor) -> torch.Tensor:
@@ -451,10 +452,11 @@ class MatchNet(torch.nn.Module):
             return (wv, corr2d.reshape(B, h, w, h, w)) if ret_corr else wv
         if cyc_on and s_mask is None:   # run_cyc returns None and the reference fails on it
             raise ValueError("the cycle mask needs s_mask")
-        # train mode: run_cyc's ass_drop = nn.Dropout(0.1) on the mask (match.py:97,181), one draw per
-        # call from torch's generator (the reference's own draw cannot be reproduced: its RNG stream)
+        # train mode: run_cyc's ass_drop = nn.Dropout(0.1) on the mask (match.py:97,181), one counter
+        # draw per call.  The reference's nn.Dropout on a CUDA tensor draws from the CUDA generator and
+        # never moves the host RNG stream (the W0 draws), so the seed comes from util.dropout_seed
         drop_p = 0.1 if (cyc_on and self.training) else 0.0
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0 else 0
+        seed = dropout_seed() if drop_p > 0 else 0
         dev = corr.device
         ig = None
         if ig_mask is not None:

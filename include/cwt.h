@@ -468,6 +468,11 @@ int cwt_mmn_blend(cwt_ctx* ctx, const float* f_q, const float* att_fq, int B, in
  * burst's last two loops side by side only when the two grids fit on the chip together. */
 int cwt_adapt_workgroups(cwt_ctx* ctx, int E, int n, int h, int w, int iters, int* G);
 
+/* 1 if cwt_inner_adapt_tail on this context runs the episode tail inside the inner loop's own
+ * launch (the two-unit persistent form, EpisodePipeline's adapt context), else 0 (it then launches
+ * the tail as a grid of its own, which needs CUs beside the loop). */
+int cwt_adapt_fuses_tail(cwt_ctx* ctx, int n, int h, int w, int iters, int* fused);
+
 /* Floats of the activations cwt_match_corr_forward_train keeps for the backward (CenterPivotConv4d
  * layers): the MutualMatching output, each branch's three ReLU outputs, their sum and, with
  * readout != 0, the attention [B][h*w][ld] (ld = h*w rounded up to 32). */

@@ -92,6 +92,36 @@ def test_deform_att_backward(dev, h, w):
     assert max(errs.values()) < TOL, errs
 
 
+def test_deform_att_backward_nonfinite(dev):
+    """A NaN / Inf in the upstream gradient reaches d_value as it does through the reference's float
+    atomics (the fixed-point scatter used to turn it into large finite garbage): every
+    position whose oracle gradient is non-finite is non-finite here, and the finite rest still
+    matches float64 autograd."""
+    from few_shot_seg_cwt_amd.detr import DeformAtt
+    from oracle import detr_oracle as D
+    h, w = 9, 11
+    mod = DeformAtt(embed_dims=512, n_heads=8, n_points=9, device=dev)
+    _deform_params(mod, 11)
+    fq0, v0 = _rand((1, 512, h, w), 12, 0.0, 1.0).double(), _rand((1, 512, h, w), 13).double()
+    G = _rand((1, 512, h, w), 14).double()
+    G[0, 5, 4, 6] = float("nan")
+    G[0, 7, 2, 3] = float("inf")
+    fq = fq0.float().to(dev).requires_grad_(True)
+    v = v0.float().to(dev).requires_grad_(True)
+    (mod(fq, v) * G.float().to(dev)).sum().backward()
+    p = {k[len("self_trans."):]: t.detach().double().cpu().requires_grad_(True) for k, t in mod.state_dict().items()
+         if k.startswith("self_trans.")}
+    vo = v0.clone().requires_grad_(True)
+    (D.deform_att(fq0.clone(), vo, p) * G).sum().backward()
+    hip, ref = v.grad.detach().cpu().double(), vo.grad
+    bad_ref = ~torch.isfinite(ref)
+    print(f"non-finite d_v entries: oracle {int(bad_ref.sum())}, HIP {int((~torch.isfinite(hip)).sum())}")
+    assert bad_ref.any()
+    assert not torch.isfinite(hip[bad_ref]).any()
+    ok = torch.isfinite(hip) & ~bad_ref
+    assert float((hip[ok] - ref[ok]).abs().max()) <= TOL * float(ref[ok].abs().max())
+
+
 @pytest.mark.parametrize("cs,sf", [(True, False), (True, True)])
 def test_detr_backward(dev, cs, sf):
     """DeTr.forward (detr.py:36-47) as train_trans.py trains it: gradients of a linear functional of

@@ -250,8 +250,12 @@ def test_forward_masks_backward(dev, use_ig, use_cyc, train):
     sm = (torch.rand(B, h, w, generator=g) < 0.4).long() if use_cyc else None
     G1, G2 = _rand((B, Cv, h, w), 43, -1, 1), _rand((B, h * w, h * w), 44, -1, 1)
     v = v0.float().to(dev).requires_grad_(True)
+    host_rng = torch.get_rng_state()
     out = net(fq0.float().to(dev), fs0.float().to(dev), v, s_mask=sm.to(dev) if use_cyc else None,
               ig_mask=ig.to(dev) if use_ig else None, ret_corr=True, use_cyc=use_cyc, ret_cyc=use_cyc)
+    # the train-mode Dropout draw leaves the host RNG stream (the W0 draws) untouched, as the
+    # reference's nn.Dropout on a CUDA tensor does
+    assert torch.equal(torch.get_rng_state(), host_rng)
     wv, corr = out[0], out[1]
     ((wv * G1.float().to(dev)).sum() + (corr.reshape(B, h * w, h * w) * G2.float().to(dev)).sum()).backward()
     names = [f"NeighConsensus.conv.{i}.{c}.{p}" for i in (0, 2, 4) for c in ("conv1", "conv2") for p in ("weight", "bias")]

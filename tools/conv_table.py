@@ -80,6 +80,36 @@ def main(path, pmc_path=None):
                    f"{roof / 1e12:.1f} | {floor:.1f} | {floor / us if us else 0:.2f} |")
     out.append("")
     out.append(f"Stack: {tot_t:.0f} us of launches, floor {tot_floor:.0f} us, roofline_frac {tot_floor / tot_t:.3f}")
+    # the Winograd forms on the work they execute: each x6w record is followed by
+    # its wino_in / wino_gemm / wino_out sub-records (api.hip run_wino_conv)
+    wrows = []
+    for i, r in enumerate(rows):
+        name, fl, by, ms = (r if isinstance(r, list) else (r["name"], r["flops"], r["bytes"], r["ms"]))
+        if not name.startswith("conv_igemm_x6w"):
+            continue
+        sub = {}
+        for q in rows[i + 1:i + 4]:
+            qn = q[0] if isinstance(q, list) else q["name"]
+            for k in ("wino_in", "wino_gemm", "wino_out"):
+                if qn.startswith(k + " "):
+                    sub[k] = q if isinstance(q, list) else (q["name"], q["flops"], q["bytes"], q["ms"])
+        if len(sub) < 3:
+            continue
+        roof = roof_of(name)
+        fx, gms = sub["wino_gemm"][1], sub["wino_gemm"][3]
+        tms = sub["wino_in"][3] + sub["wino_out"][3]
+        tby = sub["wino_in"][2] + sub["wino_out"][2]
+        wrows.append(f"| {i} | `{name.split(' ')[0]}` {name.split(' ')[1]} | {fl / 1e9:.2f} | {fx / 1e9:.2f} | "
+                     f"{ms * 1e3:.1f} | {fx / ms / 1e9 / (roof / 1e12):.2f} | {gms * 1e3:.1f} | "
+                     f"{fx / gms / 1e9:.1f} | {fx / gms / 1e9 / (roof / 1e12):.2f} | {sub['wino_gemm'][2] / 1e6:.1f} | "
+                     f"{sub['wino_in'][3] * 1e3:.1f} | {sub['wino_out'][3] * 1e3:.1f} | {tby / 1e6:.1f} | "
+                     f"{tby / tms / 1e9:.0f} | {(sub['wino_in'][2] + sub['wino_gemm'][2] + sub['wino_out'][2]) / 1e6:.1f} |")
+    if wrows:
+        out += ["", "Winograd forms on their executed work (the GEMMs' FLOPs; the transforms' and GEMMs' algorithmic bytes):", "",
+                "| # | conv | direct GFLOP | executed GFLOP | bracket us | frac executed (bracket) | GEMM us | GEMM TF/s "
+                "| GEMM frac executed | GEMM MB | in-transform us | out-transform us | transforms MB | transforms GB/s "
+                "| executed MB total |",
+                "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"] + wrows
     out.append("")
     hdr = "| record (kernel, tile, stage) | launches | us | floor us | frac |"
     sep = "|---|---|---|---|---|"
