@@ -32,17 +32,44 @@ struct AdaptScalars {
   unsigned long long nbg, nfg;  // label counts (class 0 / class 1)
   float wfg;                    // CE class weight of class 1
   float lr_eff;                 // lr / sum_p w_{y_p}
+  // the persistent loop's dW[1] exchange in 64-bit fixed point (exact, order-free integer sums:
+  // deterministic): value = integer * fx_inv, integer = rint(partial * fx_scale), fx_scale = 2^k
+  // with every sum below 2^58: |dW[1]_c| <= max|f| * sum_p |g_p| <= max|f| * sum_p w_{y_p} (the
+  // loop's per-pixel CE gradients are w_y (p - onehot), unnormalised, and the bilinear adjoint
+  // keeps the L1 norm); the quantum 2^-k is ~2^-57 of that bound.  A non-finite f gives
+  // fx_scale 0 and fx_inv NaN: W becomes NaN, as the reference's would
+  double fx_scale, fx_inv;
 };
 
 // int64 labels -> u8 (0, 1, 255 for anything else) plus per-block label counts (no atomics,
 // so nothing has to be zeroed first; adapt_setup_kernel sums the blocks in fixed order).
 constexpr int PREP_MAXBLK = 256;
 // Episode e = blockIdx.y owns lbl[e*total, (e+1)*total) and part[e][PREP_MAXBLK][2].
+// f (optional, [E][fcount]): per-block max of |f| as float bits (an unsigned max: NaN and Inf
+// above every finite value) into fpart[e][block], for the fixed-point scale of AdaptScalars.
 __global__ void adapt_prep_kernel(const int64_t* __restrict__ lbl, long total, uint8_t* __restrict__ out,
-                                  unsigned long long* __restrict__ part) {
+                                  unsigned long long* __restrict__ part, const float* __restrict__ f = nullptr,
+                                  long fcount = 0, unsigned* __restrict__ fpart = nullptr) {
   lbl += (long)blockIdx.y * total;
   out += (long)blockIdx.y * total;
   part += (long)blockIdx.y * 2 * PREP_MAXBLK;
+  if (f) {
+    const float* fe = f + (long)blockIdx.y * fcount;
+    unsigned mb = 0u;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < fcount / 4; i += (long)gridDim.x * blockDim.x) {
+      const f32x4 v = ((const f32x4*)fe)[i];
+      mb = max(max(mb, __float_as_uint(fabsf(v[0]))), __float_as_uint(fabsf(v[1])));
+      mb = max(max(mb, __float_as_uint(fabsf(v[2]))), __float_as_uint(fabsf(v[3])));
+    }
+    for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o, 64));
+    __shared__ unsigned fred[16];
+    if ((threadIdx.x & 63) == 0) fred[threadIdx.x >> 6] = mb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int i = 0; i < (int)(blockDim.x >> 6); ++i) mb = max(mb, fred[i]);
+      fpart[(long)blockIdx.y * PREP_MAXBLK + blockIdx.x] = mb;
+    }
+  }
   unsigned long long nb = 0, nf = 0;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int64_t v = lbl[i];
@@ -106,8 +133,10 @@ struct AdaptDevArgs {
 __global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, int nblk, AdaptScalars* sc, float lr,
                                    int mode, AdaptDevArgs* dargs, const float* f, long f_stride, const float* w_in,
                                    float* w_out, int w_stride, float* zero, long zero_stride, int nzero,
-                                   double* zero_d, unsigned* zero_u = nullptr, int nzero_u = 0) {
+                                   double* zero_d, unsigned* zero_u = nullptr, int nzero_u = 0,
+                                   const unsigned* fpart = nullptr) {
   __shared__ unsigned long long red[2][PREP_MAXBLK];
+  __shared__ unsigned fred[PREP_MAXBLK];
   const int t = threadIdx.x;
   const int e = blockIdx.x;
   part += (long)e * 2 * PREP_MAXBLK;
@@ -115,11 +144,13 @@ __global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, 
   if (zero) zero += (long)e * zero_stride;
   red[0][t] = t < nblk ? part[2 * t] : 0ull;
   red[1][t] = t < nblk ? part[2 * t + 1] : 0ull;
+  fred[t] = (fpart && t < nblk) ? fpart[(long)e * PREP_MAXBLK + t] : 0u;
   __syncthreads();
-  for (int o = PREP_MAXBLK / 2; o > 0; o >>= 1) {  // integer sums: order-independent
+  for (int o = PREP_MAXBLK / 2; o > 0; o >>= 1) {  // integer sums / maxima: order-independent
     if (t < o) {
       red[0][t] += red[0][t + o];
       red[1][t] += red[1][t + o];
+      fred[t] = max(fred[t], fred[t + o]);
     }
     __syncthreads();
   }
@@ -133,6 +164,19 @@ __global__ void adapt_setup_kernel(const unsigned long long* __restrict__ part, 
     sc->wfg = wfg;
     const double sumw = nb + nf * (double)wfg;
     sc->lr_eff = (float)((double)lr / sumw);
+    // fixed-point scale of the dW exchange: every sum below 2^58 (see AdaptScalars).  The loop's
+    // per-pixel gradients are unnormalised (the 1 / sum_p w_{y_p} rides in lr_eff), so
+    // |dW[1]_c| <= max|f| * sumw
+    const unsigned mb = fred[0];
+    if (mb >= 0x7f800000u) {  // NaN / Inf in f
+      sc->fx_scale = 0.0;
+      sc->fx_inv = __builtin_nan("");
+    } else {
+      const double bound = (double)__uint_as_float(mb) * (sumw > 1.0 ? sumw : 1.0);
+      const int k = bound > 0.0 ? 57 - ilogb(bound) : 0;  // bound < 2^(ilogb + 1)
+      sc->fx_scale = ldexp(1.0, k);
+      sc->fx_inv = ldexp(1.0, -k);
+    }
     if (dargs) {
       dargs[e].f = f + e * f_stride;
       dargs[e].w_in = w_in + (long)e * w_stride;
@@ -659,6 +703,17 @@ struct PersistArgs {
   float* wq = nullptr;  // the fused tail: [G][2][512] per-workgroup copies of the adapted W
 };
 
+// Episode e's accumulator slot k of the persistent loop as 64-bit fixed-point replica rows
+// [PA_R][512] (the same bytes as ADAPT_SLOT floats)
+__device__ __forceinline__ unsigned long long* pa_fx_slot(const PersistArgs& a, int e, int k) {
+  return (unsigned long long*)(a.acc + (long)e * ADAPT_ESTRIDE + (long)k * ADAPT_SLOT);
+}
+// rint(v * scale) as a two's-complement 64-bit integer (scale = 2^k: the product is exact in double)
+__device__ __forceinline__ unsigned long long pa_fx(float v, double scale) {
+  return (unsigned long long)(long long)__builtin_rint((double)v * scale);
+}
+static_assert(PA_R * 512 * 8 <= ADAPT_SLOT * 4, "a fixed-point slot must fit an accumulator slot");
+
 struct PaUnit {
   int e, img, r, x0, ncol, x_end;
   bool extra_row;  // this unit's row pair is the last: it also owns hi-res row S-1
@@ -885,6 +940,7 @@ __device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigne
   auto& P0 = P0_u[0];
   auto& P1 = P1_u[0];
   __shared__ float wfg_l[EWK], lr_l[EWK];
+  __shared__ double fxs_l[EWK], fxi_l[EWK];  // the episodes' fixed-point scales (AdaptScalars)
   __shared__ int abort_flag;
   const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);  // wv: SGPR
   const int g = blockIdx.x, G = a.G;
@@ -920,6 +976,8 @@ __device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigne
   if (t < new_) {
     wfg_l[t] = a.sc[e_lo + t].wfg;
     lr_l[t] = a.sc[e_lo + t].lr_eff;
+    fxs_l[t] = a.sc[e_lo + t].fx_scale;
+    fxi_l[t] = a.sc[e_lo + t].fx_inv;
   }
   PaTile cur;
   PaUnit q = pa_unit(a, u0);
@@ -1005,8 +1063,7 @@ __device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigne
         const int tot = a.nep * nrep * C, per = (tot + G - 1) / G;
         for (int i = g * per + t; i < min(tot, (g + 1) * per); i += PA_T) {
           const int e = i / (nrep * C), k = i - e * (nrep * C);
-          __hip_atomic_store(a.acc + (long)e * ADAPT_ESTRIDE + (long)zs * ADAPT_SLOT + k, 0.f, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(pa_fx_slot(a, e, zs) + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     };
@@ -1014,13 +1071,17 @@ __device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigne
     // NRES 3: each unit's dW is reduced over the wave by the butterfly as usual, and the one
     // value a lane then holds (channel lane >> 1) is summed over the step's units of one episode
     // in a register; one atomic per episode and step (none in flight at the next unit's DMA wait)
+    // dW[1] partial v of channel 32 wv + (lane >> 1) of episode e into replica row rep of the step's
+    // slot: one no-return 64-bit fixed-point atomic (integer adds: exact and order-free, so every
+    // workgroup reads the same sums whatever the arrival order -- a deterministic loop)
+    auto add_dw = [&](int e, float v) {
+      __hip_atomic_fetch_add(pa_fx_slot(a, e, slot) + rep * C + wv * PA_CPW + (lane >> 1), pa_fx(v, fxs_l[e - e_lo]),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     float dsum3 = 0.f;
     int dsum3_e = e_lo;
     auto flush3 = [&]() {
-      if ((lane & 1) == 0)
-        __hip_atomic_fetch_add(a.acc + (long)dsum3_e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
-                                   wv * PA_CPW + (lane >> 1),
-                               dsum3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((lane & 1) == 0) add_dw(dsum3_e, dsum3);
       dsum3 = 0.f;
     };
     // one unit's z / hi-res / dW passes; fget(j): f of lane p's pixel, channel 32*wv + j
@@ -1121,9 +1182,7 @@ __device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigne
           }
           dsum3 += accd[0];
         } else if ((lane & 1) == 0) {
-          __hip_atomic_fetch_add(a.acc + (long)q.e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
-                                     wv * PA_CPW + (lane >> 1),
-                                 accd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          add_dw(q.e, accd[0]);
         }
       }
     };
@@ -1302,10 +1361,7 @@ __device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigne
           if (pass && qb.e == qa.e) break;
           const float ma = qa.e == e ? ga : 0.f, mb = qb.e == e ? gb : 0.f;
           const float dsum = pa_butterfly_fn([&](int j) { return fmaf(mb, cur2.fr[j], ma * cur.fr[j]); }, lane);
-          if ((lane & 1) == 0)
-            __hip_atomic_fetch_add(a.acc + (long)e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C + wv * PA_CPW +
-                                       (lane >> 1),
-                                   dsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((lane & 1) == 0) add_dw(e, dsum);
         }
       } else {
         float accd[PA_CPW];
@@ -1323,10 +1379,7 @@ __device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigne
             if (!BREG) asm volatile("" ::: "memory");
           }
           pa_butterfly(accd, lane);
-          if ((lane & 1) == 0)
-            __hip_atomic_fetch_add(a.acc + (long)qa.e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
-                                       wv * PA_CPW + (lane >> 1),
-                                   accd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((lane & 1) == 0) add_dw(qa.e, accd[0]);
         } else {
 #pragma unroll
           for (int uu = 0; uu < 2; ++uu) {
@@ -1334,10 +1387,7 @@ __device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigne
 #pragma unroll
             for (int j = 0; j < PA_CPW; ++j) accd[j] = uu ? gb * (BREG ? cur2.fr[j] : fl2[wv][j][lane]) : ga * cur.fr[j];
             pa_butterfly(accd, lane);
-            if ((lane & 1) == 0)
-              __hip_atomic_fetch_add(a.acc + (long)q.e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C +
-                                         wv * PA_CPW + (lane >> 1),
-                                     accd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((lane & 1) == 0) add_dw(q.e, accd[0]);
           }
         }
       }
@@ -1400,10 +1450,7 @@ __device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigne
         const float ma = qa.e == e ? ga : 0.f, mb = qb.e == e ? gb : 0.f, mc = qc.e == e ? gc : 0.f;
         const float dsum = pa_butterfly_fn(
             [&](int j) { return fmaf(mc, cur2.fr[j], fmaf(mb, fl2[wv][j][lane], ma * cur.fr[j])); }, lane);
-        if ((lane & 1) == 0)
-          __hip_atomic_fetch_add(a.acc + (long)e * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + rep * C + wv * PA_CPW +
-                                     (lane >> 1),
-                                 dsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((lane & 1) == 0) add_dw(e, dsum);
       }
     };
     if constexpr (FLOOR) {
@@ -1513,16 +1560,20 @@ __device__ __forceinline__ bool adapt_persist_body(const PersistArgs& a, unsigne
 #pragma unroll
       for (int ew = 0; ew < EWK; ++ew) {
         if (ew >= new_) break;
-        const float* ap = a.acc + (long)(e_lo + ew) * ADAPT_ESTRIDE + (long)slot * ADAPT_SLOT + (long)hh * nh * C + cw;
-        float v[PA_R / 2];
+        const unsigned long long* ap = pa_fx_slot(a, e_lo + ew, slot) + (long)hh * nh * C + cw;
+        unsigned long long v[PA_R / 2];
 #pragma unroll
         for (int r = 0; r < PA_R / 2; ++r)
-          v[r] = r < nh ? __hip_atomic_load(ap + r * C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-        float D = 0.f;
+          v[r] = r < nh ? __hip_atomic_load(ap + r * C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        unsigned long long Di = 0ull;
 #pragma unroll
-        for (int r = 0; r < PA_R / 2; ++r) D += v[r];
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(D), __float_as_uint(D), false, false);
-        D = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);  // rows [0,nh) + rows [nh,nrep) in every lane
+        for (int r = 0; r < PA_R / 2; ++r) Di += v[r];
+        // rows [0,nh) + rows [nh,nrep) in every lane (integers: the sum is exact), then one rounding
+        const auto slo = __builtin_amdgcn_permlane32_swap((unsigned)Di, (unsigned)Di, false, false);
+        const auto shi = __builtin_amdgcn_permlane32_swap((unsigned)(Di >> 32), (unsigned)(Di >> 32), false, false);
+        const unsigned long long Do = ((unsigned long long)(lane < 32 ? shi[1] : shi[0]) << 32) |
+                                      (unsigned long long)(lane < 32 ? slo[1] : slo[0]);
+        const float D = (float)((double)(long long)(Di + Do) * fxi_l[ew]);
         if (lane < 32) {
           const float lr = lr_l[ew];
           const float w1 = wlw[wv][ew][1][lane] - lr * D, w0 = wlw[wv][ew][0][lane] + lr * D;
@@ -1745,7 +1796,8 @@ size_t adapt_ws_sizes(int E, int n, int h, int w, int S, size_t* fws, size_t* lb
                       size_t* wbuf, size_t* dargs) {
   *fws = (size_t)E * n * h * w * 512 * sizeof(float);
   *lbl = (size_t)E * n * S * S;
-  *sc = (size_t)E * (sizeof(AdaptScalars) + 2 * PREP_MAXBLK * sizeof(unsigned long long)) + 64;
+  *sc = (size_t)E * (sizeof(AdaptScalars) + 2 * PREP_MAXBLK * sizeof(unsigned long long) + PREP_MAXBLK * sizeof(unsigned)) +
+        64;
   *acc = (size_t)E * ADAPT_ESTRIDE * sizeof(float) + PA_CNT_WORDS * sizeof(unsigned);  // + persistent-loop counters
   *wbuf = (size_t)E * ADAPT_WSTRIDE * sizeof(float);
   *dargs = (size_t)E * sizeof(AdaptDevArgs);
@@ -1784,8 +1836,11 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
                  hipEvent_t ev_k0, hipEvent_t ev_k1, const FusedTail* tail) {
   const long total = (long)n * S * S;  // labels per episode
   unsigned long long* part = (unsigned long long*)(sc + E);  // [E][PREP_MAXBLK][2] after the scalars
+  unsigned* fpart = (unsigned*)(part + (long)E * 2 * PREP_MAXBLK);  // [E][PREP_MAXBLK] max |f| bits
   const int pblocks = (int)std::min<long>(PREP_MAXBLK, cdiv(total, 1024));
-  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks, E), dim3(1024), 0, st, lbl64, total, lbl_ws, part);
+  const long fcount = (long)n * h * w * 512;
+  hipLaunchKernelGGL(adapt_prep_kernel, dim3(pblocks, E), dim3(1024), 0, st, lbl64, total, lbl_ws, part, f, fcount,
+                     fpart);
   CWT_LAUNCH_CHECK();
   int pG = 0, punits = 0, pncb = 0, pnres = 0, puc = 0;
   const char* pe = getenv("CWT_ADAPT_PERSIST");
@@ -1796,7 +1851,7 @@ int launch_adapt(const float* f, const int64_t* lbl64, int E, int n, int h, int 
                      sc, lr, 0, dargs, f, (long)n * h * w * 512, (const float*)W, W, 1024,
                      iters > 0 ? acc3 : (float*)nullptr, ADAPT_ESTRIDE, persist ? 2 * ADAPT_SLOT : ADAPT_SLOT,
                      (double*)nullptr,
-                     persist ? cnt : (unsigned*)nullptr, persist ? PA_CNT_WORDS : 0);
+                     persist ? cnt : (unsigned*)nullptr, persist ? PA_CNT_WORDS : 0, (const unsigned*)fpart);
   CWT_LAUNCH_CHECK();
   if (iters <= 0) return tail ? fail(CWT_EARG, "fused tail: needs the persistent loop") : 0;
   if (tail && !persist) return fail(CWT_EARG, "fused tail: needs the persistent loop");

@@ -145,7 +145,8 @@ __device__ __forceinline__ void split3_bf16(const f32x4& x0, const f32x4& x1, bf
 // barrier, so the ring keeps NSTG - 1 tiles in flight either way.
 // PF bits: 1 fragment prefetch; 2 / 4 timing studies (no MFMAs / no operand DMA); 8 buffer
 // addressing of the operand DMA (every production instantiation sets it); 16 timing study of the
-// x6 WN = 128 forms without the A split (wrong numbers, same data movement and MFMAs).
+// x6 WN = 128 forms without the A split (wrong numbers, same data movement and MFMAs); 32 timing
+// study without the epilogue.
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF>
 __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   static_assert(PREC == 0 || PREC == 1 || PREC == 3 || PREC == 6,
@@ -489,6 +490,13 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
 
   // ---- epilogue through a per-wave LDS tile ----
   wait_vmcnt<0>();
+  if constexpr ((PF & 32) != 0) {  // timing study (x6 var 17): no epilogue (the accumulators kept live)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   block_sync_lds();
   float* ep = (float*)smem + wv * (EP_ROWS * EP_LD);
   constexpr int LPR = WN / 8;    // lanes per output row (8 channels each)

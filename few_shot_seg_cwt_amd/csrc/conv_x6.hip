@@ -52,7 +52,8 @@ int launch_split_w3(const float* w, long R, int K, __bf16* ws, __bf16* wl, hipSt
 //   128x64, 64x128, 64x64: 0, 1, 2 as the other kernels; 64x128 also 3 = 4x1 (WN 128), 5 = 4x1 on a
 //   2-stage ring.  var 8-11: the timing-study kernels;
 //   12 / 13: var 5 (128x128) / var 3 (256x256) without the A split (timing study: wrong numbers);
-//   14 / 15: var 5 without operand DMA / without MFMAs (timing study: wrong numbers).
+//   14 / 15: var 5 without operand DMA / without MFMAs (timing study: wrong numbers); 16 without
+//   both, 17 without both and without the epilogue (the launch, prologue and barriers alone).
 template <int STAGE>
 static void launch_tiles_x6_stage(const ConvSArgs& a, const ConvPlan& p, dim3 grid, hipStream_t st) {
   const int v = p.var;
@@ -62,6 +63,8 @@ static void launch_tiles_x6_stage(const ConvSArgs& a, const ConvPlan& p, dim3 gr
     if (v == 12) X6(128, 128, 4, 1, 2, 16);  // timing study: var 5 without the A split
     else if (v == 14) X6(128, 128, 4, 1, 2, 4);   // timing study: var 5 without operand DMA
     else if (v == 15) X6(128, 128, 4, 1, 2, 2);   // timing study: var 5 without MFMAs
+    else if (v == 16) X6(128, 128, 4, 1, 2, 6);   // timing study: var 5 without operand DMA and MFMAs
+    else if (v == 17) X6(128, 128, 4, 1, 2, 38);  // timing study: ... and without the epilogue
     else if (v == 13) X6(256, 256, 4, 2, 2, 16);  // timing study: 256x256 var 3 without the A split
     else if (v == 8) X6(64, 64, 2, 2, 4, 2);
     else if (v == 9) X6(64, 64, 2, 2, 4, 4);

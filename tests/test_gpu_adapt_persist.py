@@ -1,7 +1,8 @@
 """The persistent inner loop (adapt_persist_kernel: all 200 SGD steps in one launch, in-kernel
 grid barrier) against the per-step launches it replaces (CWT_ADAPT_PERSIST=0) on the same
 inputs, at the BASELINE shapes and in batched / multi-unit-per-workgroup geometries.  Both
-are fp32 with atomic (order-free) gradient sums, so they agree to rounding; the oracle and
+are fp32; the step launches sum the gradient with float atomics and the persistent loop with
+64-bit fixed-point atomics (exact), so they agree to rounding; the oracle and
 reference fixtures pin the absolute result (test_gpu_parity.py, test_gpu_shapes.py)."""
 import os
 
@@ -145,3 +146,42 @@ def test_barrier_timeout_is_raised(dev, upw):
     _lib.check_status()
     Wr = _run("0", f, lbl, W0, 200)
     assert rel(W, Wr) < 1e-4
+
+
+@pytest.mark.parametrize("E,n,S,iters,upw,stream", [
+    (1, 1, 473, 200, "1", None),    # config #2 sequential geometry (adapt_persist_kernel<1>)
+    (1, 1, 473, 200, "2", None),    # the pipeline's two-unit register form (<5>)
+    (1, 1, 473, 50, "2lds", None),  # <2>
+    (1, 5, 473, 50, None, None),    # config #3: three units in lockstep (<4>)
+    (1, 5, 641, 20, None, "1"),     # the LDS-streamed form (<3>)
+    (4, 1, 129, 20, None, None),    # workgroups spanning two episodes
+])
+def test_persist_loop_is_deterministic(dev, E, n, S, iters, upw, stream):
+    """The persistent loop's dW exchange sums 64-bit fixed-point integers (exact, order-free:
+    AdaptScalars.fx_scale), so the same call twice gives bitwise the same W whatever order the
+    workgroups' atomics land in -- as the reference's CPU path is bitwise deterministic (SURVEY
+    §0).  Five repeats, every geometry form."""
+    h = (S - 1) // 8 + 1
+    f = torch.from_numpy(syn.normal(9, f"fd{E}{n}{S}", (E * n, 512, h, h), 0.1)).to(dev)
+    f = f.contiguous(memory_format=torch.channels_last)
+    lbl = torch.stack([torch.from_numpy(syn.make_episode(SEED, 40 + e, S, n)["s_label"][0]) for e in range(E)]).to(dev)
+    W0 = torch.from_numpy(syn.normal(10, f"wd{E}{n}{S}", (E, 2, 512), 0.04)).to(dev)
+    W1 = _run("2", f, lbl, W0, iters, upw=upw, stream=stream)
+    for _ in range(4):
+        assert torch.equal(_run("2", f, lbl, W0, iters, upw=upw, stream=stream), W1)
+    Ws = _run("0", f, lbl, W0, iters)   # and still the float-atomic step launches' result to rounding
+    assert max(rel(W1[e], Ws[e]) for e in range(E)) < 1e-4
+
+
+def test_persist_loop_nonfinite_features(dev):
+    """A NaN in the support features makes the adapted W NaN (the fixed-point scale cannot be
+    formed: fx_inv NaN), as the reference's float sums would, instead of garbage integers."""
+    S, n = 129, 1
+    h = (S - 1) // 8 + 1
+    f = torch.from_numpy(syn.normal(11, "fnan", (n, 512, h, h), 0.1)).to(dev)
+    f[0, 7, 3, 4] = float("nan")
+    f = f.contiguous(memory_format=torch.channels_last)
+    lbl = torch.from_numpy(syn.make_episode(SEED, 12, S, n)["s_label"][0]).to(dev)[None]
+    W0 = torch.from_numpy(syn.normal(12, "wnan", (1, 2, 512), 0.04)).to(dev)
+    W = _run("2", f, lbl, W0, 5, upw="1")
+    assert torch.isnan(W).all()

@@ -355,17 +355,67 @@ def test_episode_exact_fp32_vs_reference(dev, golden_dir, name, layers, S, shot,
     assert hard == 0
 
 
+def _check_episode_outputs(r, g, e, S, tag):
+    """One episode of the product path (validate_transformer's episodes_out: the pipelined, fused
+    loop + tail on the adapt context, or the drain's whole-chip loop for a run's last episode)
+    against the reference's fixture: W, W', pred_q, pred_q0 (1e-3), IoU counts of both logits
+    within the low-margin pixel count, no argmax flip above the margin (test.py:164-219)."""
+    errs = dict(W=rel(r["W"], g[f"e{e}_W"]), W2=rel(r["W2"][0], g[f"e{e}_W2"]),
+                pred_q=rel(r["pred_q"][0], g[f"e{e}_pred_q"]), pred_q0=rel(r["pred_q0"][0], g[f"e{e}_pred_q0"]))
+    print(f"{tag} e{e}: " + ", ".join(f"{k} {v:.1e}" for k, v in errs.items()))
+    assert max(errs.values()) < TOL, errs
+    for key, iu_key in (("pred_q", "iut"), ("pred_q0", "iut0")):
+        low = _low_margin(g[f"e{e}_{key}"], S)
+        iu = r[iu_key][0].numpy()
+        ref = g[f"e{e}_iu" if key == "pred_q" else f"e{e}_iu0"]
+        assert np.abs(iu - ref).max() <= low, (key, iu, ref, low)
+        _, hard = flip_report(r[key][0], g[f"e{e}_{key}"], S, f"{tag}:e{e}:{key}")
+        assert hard == 0
+
+
 def test_validate_transformer_vs_reference(dev, golden_dir):
-    from few_shot_seg_cwt_amd.episode import SyntheticEpisodes, validate_transformer
+    """validate_transformer (test.py:103-254) through the episode pipeline, against the
+    reference's own run: run-level mIoU and loss, and per episode the product path's W, W',
+    pred_q, pred_q0 and IoU counts.  Episodes 0 and 1 run the fused loop + tail on the pipeline's
+    adapt context, episode 2 (the run's last) the drain's whole-chip loop."""
+    from few_shot_seg_cwt_amd import _lib
+    from few_shot_seg_cwt_amd.episode import EpisodeEngine, EpisodePipeline, SyntheticEpisodes, validate_transformer
+    import ctypes
     g = dict(np.load(os.path.join(golden_dir, "episode_pascal_r50_1shot.npz")))
     cfg = syn.cfg_defaults(test_num=3, n_runs=1)
     torch.manual_seed(SEED)
     eps = []
-    miou, loss = validate_transformer(cfg, SyntheticEpisodes(3), model(50), transformer(4), episodes_out=eps)
+    m, t = model(50), transformer(4)
+    miou, loss = validate_transformer(cfg, SyntheticEpisodes(3), m, t, episodes_out=eps)
     assert abs(miou - float(g["mIoU"])) < 2e-3
     assert abs(loss - float(g["loss"])) < 1e-3 * abs(float(g["loss"]))
+    pipe = EpisodePipeline.shared(EpisodeEngine(m, t, cfg), extract_streams=2)
+    fz = ctypes.c_int(0)
+    _lib.check(_lib.lib().cwt_adapt_fuses_tail(pipe.c_adapt, 1, 60, 60, 200, ctypes.byref(fz)), "cwt_adapt_fuses_tail")
+    assert fz.value == 1   # the product path under test is the fused one
     for e in range(3):   # W0 drawn from the torch RNG exactly as the reference draws it
-        assert rel(eps[e]["W"], g[f"e{e}_W"]) < TOL
+        _check_episode_outputs(eps[e], g, e, 473, "validate_transformer pascal 1-shot")
+
+
+@pytest.mark.parametrize("name,layers,S,shot", [
+    ("episode_pascal_r50_5shot.npz", 50, 473, 5),
+    ("episode_coco_r101_1shot.npz", 101, 641, 1),
+])
+def test_validate_transformer_pipelined_vs_reference(dev, golden_dir, name, layers, S, shot):
+    """BASELINE configs #3 / #4's shapes through validate_transformer's pipeline: the fixture holds
+    one episode (the reference's run of test_num 1), so the run here has two and episode 0 -- the
+    one with the fixture's W0, the first torch draw after manual_seed -- runs on the pipeline's adapt
+    context (not the drain): its W, W', pred_q, pred_q0 and IoU counts against the fixture."""
+    from few_shot_seg_cwt_amd.episode import SyntheticEpisodes, validate_transformer
+    g = dict(np.load(os.path.join(golden_dir, name)))
+    cfg = syn.cfg_defaults(layers=layers, image_size=S, shot=shot, test_num=2, n_runs=1)
+    classes = syn.coco_val_classes(0) if layers == 101 else None
+    torch.manual_seed(SEED)
+    eps = []
+    validate_transformer(cfg, SyntheticEpisodes(2, S=S, shot=shot, classes=classes), model(layers), transformer(4),
+                         episodes_out=eps)
+    assert len(eps) == 2
+    _check_episode_outputs(eps[0], g, 0, S, f"validate_transformer {name}")
 
 
 @pytest.mark.parametrize("name", ["train_pascal_r50_1shot.npz", "train_coco_r101_1shot.npz"])

@@ -11,6 +11,10 @@ import sys
 
 import torch
 
+# the debug conv entries split / transform the weights per call unless asked to cache them: the
+# timed calls are then the conv alone (as the extractor runs it, on weights split at load)
+os.environ.setdefault("CWT_DBG_W3_CACHE", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -144,7 +148,7 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
                         continue   # no prefetch form of 256x256
                     if var == 4 and (bm, bn) != (128, 128):
                         continue   # two-workgroups-per-CU 128x128 form
-                    if 8 <= var < 16 and (bm, bn) != ((64, 64) if var < 10 else (128, 128)):
+                    if 8 <= var < 18 and (bm, bn) != ((64, 64) if var < 10 else (128, 128)):
                         continue   # timing-study kernels: fixed tiles
                     if var == 2 and (bm == 256 or bn == 256):
                         continue   # 8-wave form only for the 128/64 tiles
