@@ -724,8 +724,10 @@ static int run_wino_conv(cwt_ctx* ctx, const float* x, int N, int H, int W, int 
       (rc = ensure_ws(ctx, "wino.M", (size_t)g.P * g.T * Co * 4, &Mb)) || (rc = zero_line(ctx, &zero)))
     return rc;
   // sub-records (the executed work of the form): the transforms' algorithmic bytes
-  // and the batched GEMMs' executed FLOPs, at the conv record's own profile level
-  const int plev = stage == 6 ? 1 : 2;
+  // and the batched GEMMs' executed FLOPs, at profile level 3 only (their event pairs would add
+  // ~10 us of gaps to each Winograd conv's own bracket at levels 1 and 2)
+  const int plev = 3;
+  (void)stage;
   const double vb = 4.0 * g.P * g.T * Ci, mb = 4.0 * g.P * g.T * Co;
   Prof pin(ctx, st, "wino_in " + std::to_string(Ci) + "@" + std::to_string(H), 0.0,
            4.0 * N * H * W * Ci + vb, plev);
@@ -2723,7 +2725,8 @@ static int debug_conv_s(cwt_ctx* ctx, int prec, const void* xs, int N, int Hi, i
               "tile must be one of 256x256, 256x128, 128x256, 128x128, 128x64, 64x128, 64x64");
     const bool x6_var = prec == 6 && ((var == 3 && (bm >= 128 && bn >= 128)) || (var == 5 && bm == 128 && bn == 128) ||
                                       ((var == 3 || var == 5) && bm == 64 && bn == 128) ||
-                                      ((var == 12 || (var >= 14 && var <= 17)) && bm == 128 && bn == 128) ||
+                                      ((var == 3 || var == 5) && bm == 128 && bn == 64) || (var == 3 && bm == 64 && bn == 64) ||
+                                      ((var == 12 || (var >= 14 && var <= 18)) && bm == 128 && bn == 128) ||
                                       (var == 13 && bm == 256 && bn == 256));
     CWT_CHECK((var >= 0 && var <= 2) || (var == 4 && bm == 128 && bn == 128) || (var >= 8 && var <= 11) || x6_var,
               "variant must be 0, 1, 2, 4 (128x128 only), 8 .. 11 (timing study), or for x6 3 (tiles >= 128x128) "

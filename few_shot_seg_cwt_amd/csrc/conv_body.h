@@ -146,7 +146,7 @@ __device__ __forceinline__ void split3_bf16(const f32x4& x0, const f32x4& x1, bf
 // PF bits: 1 fragment prefetch; 2 / 4 timing studies (no MFMAs / no operand DMA); 8 buffer
 // addressing of the operand DMA (every production instantiation sets it); 16 timing study of the
 // x6 WN = 128 forms without the A split (wrong numbers, same data movement and MFMAs); 32 timing
-// study without the epilogue.
+// study without the epilogue; 64 timing study: every workgroup returns at once (the launch alone).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTG, int PREC, int PF>
 __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   static_assert(PREC == 0 || PREC == 1 || PREC == 3 || PREC == 6,
@@ -190,6 +190,11 @@ __device__ __forceinline__ void conv_s_body(const ConvSArgs& a) {
   const int kt_begin = ks * a.kt_per_split;
   const int kt_end = min(a.ktiles, kt_begin + a.kt_per_split);
   const int T = kt_end - kt_begin;
+  if constexpr ((PF & 64) != 0) {  // timing study (x6 var 18): the launch alone (every workgroup returns here)
+    asm volatile("" ::"s"(T));
+    return;
+  }
+
 
   // ---- LDS-DMA source geometry (constant over K) ----
   const int lrow = lane >> 3, lslot = lane & 7;

@@ -50,7 +50,9 @@ int launch_split_w3(const float* w, long R, int K, __bf16* ws, __bf16* wl, hipSt
 //   128x256: 0 = 2x4, 1 = prefetch, 3 = 4x2 (WN 128);  128x128: 0 = 2x2, 1 = prefetch, 2 = prefetch
 //   2x4, 4 = 2x2 on a 2-stage ring, 3 = 4x1 (WN 128), 5 = 4x1 on a 2-stage ring (two per CU);
 //   128x64, 64x128, 64x64: 0, 1, 2 as the other kernels; 64x128 also 3 = 4x1 (WN 128), 5 = 4x1 on a
-//   2-stage ring.  var 8-11: the timing-study kernels;
+//   2-stage ring; round 6, for the Co = 64 layers (stem conv2, layer1 conv1 / conv2), where the 2x2
+//   forms split every A fragment twice: 128x64 3 = 4x1 (WN 64), 5 = the same on a 2-stage ring, 64x64
+//   3 = 4x1 (WN 64).  var 8-11: the timing-study kernels;
 //   12 / 13: var 5 (128x128) / var 3 (256x256) without the A split (timing study: wrong numbers);
 //   14 / 15: var 5 without operand DMA / without MFMAs (timing study: wrong numbers); 16 without
 //   both, 17 without both and without the epilogue (the launch, prologue and barriers alone).
@@ -65,6 +67,7 @@ static void launch_tiles_x6_stage(const ConvSArgs& a, const ConvPlan& p, dim3 gr
     else if (v == 15) X6(128, 128, 4, 1, 2, 2);   // timing study: var 5 without MFMAs
     else if (v == 16) X6(128, 128, 4, 1, 2, 6);   // timing study: var 5 without operand DMA and MFMAs
     else if (v == 17) X6(128, 128, 4, 1, 2, 38);  // timing study: ... and without the epilogue
+    else if (v == 18) X6(128, 128, 4, 1, 2, 64);  // timing study: the launch alone (every workgroup returns)
     else if (v == 13) X6(256, 256, 4, 2, 2, 16);  // timing study: 256x256 var 3 without the A split
     else if (v == 8) X6(64, 64, 2, 2, 4, 2);
     else if (v == 9) X6(64, 64, 2, 2, 4, 4);
@@ -91,7 +94,9 @@ static void launch_tiles_x6_stage(const ConvSArgs& a, const ConvPlan& p, dim3 gr
     else if (v) X6(128, 128, 2, 2, 3, 1);
     else X6(128, 128, 2, 2, 3, 0);
   } else if (p.bm == 128 && p.bn == 64) {
-    if (v == 2) X6(128, 64, 4, 2, 3, 1);
+    if (v == 3) X6(128, 64, 4, 1, 3, 0);       // WN = 64: the A split once per row block (Co = 64 layers)
+    else if (v == 5) X6(128, 64, 4, 1, 2, 0);  // ... on a two-stage ring
+    else if (v == 2) X6(128, 64, 4, 2, 3, 1);
     else if (v) X6(128, 64, 2, 2, 3, 1);
     else X6(128, 64, 2, 2, 3, 0);
   } else if (p.bm == 64 && p.bn == 128) {
@@ -101,7 +106,8 @@ static void launch_tiles_x6_stage(const ConvSArgs& a, const ConvPlan& p, dim3 gr
     else if (v) X6(64, 128, 2, 2, 3, 1);
     else X6(64, 128, 2, 2, 3, 0);
   } else {
-    if (v == 2) X6(64, 64, 2, 4, 4, 1);
+    if (v == 3) X6(64, 64, 4, 1, 4, 0);  // WN = 64
+    else if (v == 2) X6(64, 64, 2, 4, 4, 1);
     else if (v) X6(64, 64, 2, 2, 4, 1);
     else X6(64, 64, 2, 2, 4, 0);
   }

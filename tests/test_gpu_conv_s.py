@@ -289,9 +289,11 @@ def test_conv_f32d_channel_strided_out():
 # total < 2^-23 |a||b| per product (one fp32 rounding): the same bar as the exact-fp32 kernel
 TOL_X6 = 1e-5
 # the x6-only forms (bm = 1000 * variant + rows): 3 the WN = 128 wave layouts, 5 128x128 4x1 on a
-# 2-stage ring (two workgroups per CU)
+# 2-stage ring (two workgroups per CU); round 6: the WN = 64 4x1 forms of the Co = 64 layers (128x64
+# var 3 / 5, 64x64 var 3)
 X6_FORMS = [(3256, 256, 1), (3256, 128, 1), (3128, 256, 1), (3128, 128, 1), (3128, 128, 2), (5128, 128, 1),
-            (5128, 128, 4), (3064, 128, 1), (5064, 128, 1), (5064, 128, 2)]
+            (5128, 128, 4), (3064, 128, 1), (5064, 128, 1), (5064, 128, 2),
+            (3128, 64, 1), (5128, 64, 1), (5128, 64, 2), (3064, 64, 1), (3064, 64, 2)]
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))

@@ -140,10 +140,10 @@ def sweep(layers, size, n_img, reps, quick, prec=3, variants=(0,), only=None):
                 tiles = -(-M // bm) * (Co // bn)
                 for var in variants:
                     x6v = prec in (6, 7, 8)
-                    if var == 3 and not (x6v and ((bm >= 128 and bn >= 128) or (bm, bn) == (64, 128))):
-                        continue   # x6 only: the WN = 128 wave layouts
-                    if var == 5 and not (x6v and (bm, bn) in ((128, 128), (64, 128))):
-                        continue   # x6 only: 128x128 in 4x1 waves on a 2-stage ring
+                    if var == 3 and not (x6v and ((bm >= 128 and bn >= 128) or (bm, bn) in ((64, 128), (128, 64), (64, 64)))):
+                        continue   # x6 only: the 4x1 / WN = 128 wave layouts
+                    if var == 5 and not (x6v and (bm, bn) in ((128, 128), (64, 128), (128, 64))):
+                        continue   # x6 only: 4x1 waves on a 2-stage ring
                     if var in (1, 2) and bm == 256 and bn == 256:
                         continue   # no prefetch form of 256x256
                     if var == 4 and (bm, bn) != (128, 128):

@@ -83,12 +83,13 @@ def main(path, pmc_path=None):
     # the Winograd forms on the work they execute: each x6w record is followed by
     # its wino_in / wino_gemm / wino_out sub-records (api.hip run_wino_conv)
     wrows = []
-    for i, r in enumerate(rows):
+    prows = d.get("winograd_parts", rows)   # bench.py's level-3 extraction (the parts' own events)
+    for i, r in enumerate(prows):
         name, fl, by, ms = (r if isinstance(r, list) else (r["name"], r["flops"], r["bytes"], r["ms"]))
         if not name.startswith("conv_igemm_x6w"):
             continue
         sub = {}
-        for q in rows[i + 1:i + 4]:
+        for q in prows[i + 1:i + 4]:
             qn = q[0] if isinstance(q, list) else q["name"]
             for k in ("wino_in", "wino_gemm", "wino_out"):
                 if qn.startswith(k + " "):
