@@ -6,3 +6,5 @@ echo "pytest rc=$rc"
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --profile-json gpurun_out/r6f/prof.json > gpurun_out/r6f/bench.json 2> gpurun_out/r6f/bench.err
 echo "bench rc=$?"
+timeout -k 10 300 python -u tools/graph_extract.py > gpurun_out/r6f/graph_extract.log 2>&1
+echo "graph rc=$?"
