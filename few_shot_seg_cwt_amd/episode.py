@@ -345,13 +345,6 @@ class EpisodePipeline:
         self.drain_overlap = os.environ.get("CWT_PIPE_DRAIN_OVERLAP", "0") == "1"
         self.s_drain = None
         self._fits = {}
-        # Round 6, the drain split (CWT_PIPE_DRAIN_SPLIT=0 turns it off): the last episode's support
-        # images and its query image run as two extractor passes on the two extractor streams, so its
-        # inner loop -- which reads only the supports -- starts when the support pass ends and runs
-        # beside the query pass instead of after both; the tail then waits for the query.  Eval-mode
-        # BN makes each image's features independent of its batch; only the conv plans' split-K
-        # grouping (chosen per GEMM size M) can differ, at fp32 rounding
-        self.drain_split = os.environ.get("CWT_PIPE_DRAIN_SPLIT", "1") != "0" and len(self.s_ext) >= 2
 
     def _drain_fits(self, shot: int, h: int, w: int, iters: int) -> bool:
         key = (shot, h, w, iters)
@@ -380,8 +373,6 @@ class EpisodePipeline:
         eng = self.eng
         cur = torch.cuda.current_stream()
         shot = imgs.shape[0] - 1
-        if last and self.drain and self.drain_split and not self.drain_overlap:
-            return self._submit_split(imgs, s_label, q_label, W0)
         i = self.k % len(self.s_ext)
         self.k += 1
         s_ex = self.s_ext[i]
@@ -429,52 +420,6 @@ class EpisodePipeline:
             f_s, f_q = f_all[:shot], f_all[shot:]
             W, (W2, pred_q, pred_q0, iut, ce, iut0) = adapt_and_tail(eng.transformer, f_s, s_label, W0, eng.lr,
                                                                       eng.iters, f_q, q_label)
-            done_all = torch.cuda.Event()
-            done_all.record(self.s_adapt)
-        return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, done=done_all)
-
-    def _extract_into(self, j: int, x: torch.Tensor, out: torch.Tensor) -> torch.cuda.Event:
-        """One extractor pass of x into out on extractor stream j (its context); returns its event."""
-        s = self.s_ext[j]
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for t in (x, out):
-                t.record_stream(s)
-            if self.c_ext[j] is None:
-                self.eng.model.extract_features(x, out=out)
-            else:
-                with _lib.using_ctx(self.c_ext[j]):
-                    self.eng.model.extract_features(x, out=out)
-            ev = torch.cuda.Event()
-            ev.record(s)
-        return ev
-
-    def _submit_split(self, imgs, s_label, q_label, W0) -> dict:
-        """The last episode of a burst (the drain split, __init__): the support pass on the next
-        extractor stream, the query pass on the one after it; the inner loop on the whole-chip
-        context as soon as the supports are extracted, the tail after the query."""
-        eng = self.eng
-        cur = torch.cuda.current_stream()
-        shot = imgs.shape[0] - 1
-        S = imgs.shape[2]
-        h = feature_side(S)
-        f_all = torch.empty((shot + 1, 512, h, h), device=imgs.device, dtype=torch.float32,
-                            memory_format=torch.channels_last)
-        i = self.k % len(self.s_ext)
-        self.k += 1
-        done_s = self._extract_into(i, imgs[:shot], f_all[:shot])
-        done_q = self._extract_into((i + 1) % len(self.s_ext), imgs[shot:], f_all[shot:])
-        if self.c_solo is None:
-            self.c_solo = _lib.new_ctx()   # automatic geometry (cwt_ctx_set_adapt_units 0)
-        self.s_adapt.wait_stream(cur)
-        with torch.cuda.stream(self.s_adapt), _lib.using_ctx(self.c_solo):
-            for t in (f_all, imgs, s_label, q_label, W0):
-                t.record_stream(self.s_adapt)
-            self.s_adapt.wait_event(done_s)
-            W = inner_adapt(f_all[:shot], s_label, W0, eng.lr, eng.iters)
-            self.s_adapt.wait_event(done_q)
-            W2, pred_q, pred_q0, iut, ce, iut0 = tail_and_metrics(eng.transformer, W.view(1, 2, -1), f_all[shot:],
-                                                                  q_label)
             done_all = torch.cuda.Event()
             done_all.record(self.s_adapt)
         return dict(W=W, W2=W2, pred_q=pred_q, pred_q0=pred_q0, iut=iut, iut0=iut0, ce=ce, done=done_all)

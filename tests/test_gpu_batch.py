@@ -75,9 +75,7 @@ def test_pipeline_equals_run(dev, streams, overlap):
     """EpisodePipeline (extractor of episode i+1 on one stream beside episode i's inner loop and
     CWT on another) gives every episode what EpisodeEngine.run gives it alone -- the burst's last
     episode through the drain (its loop on the whole-chip context; overlap: on a stream of its own
-    beside the previous episode's loop and tail; with two extractor streams and no overlap, the drain
-    split: its support and query images as two passes, whose conv plans may group split-K partials
-    differently, so its baseline counts agree within the near-tie pixels)."""
+    beside the previous episode's loop and tail)."""
     from few_shot_seg_cwt_amd import MultiHeadAttentionOne, get_model
     from few_shot_seg_cwt_amd.episode import EpisodeEngine, EpisodePipeline
     S, shot, n = 129, 1, 4
@@ -104,10 +102,7 @@ def test_pipeline_equals_run(dev, streams, overlap):
         torch.cuda.synchronize()
         assert rel(outs[e]["W"], r["W"]) < TOL, e
         assert rel(outs[e]["pred_q"], r["pred_q"]) < TOL_RUN, e
-        if e == n - 1 and pipe.drain_split and not overlap:
-            assert float((outs[e]["iut0"] - r["iut0"]).abs().max()) <= 2, e
-        else:
-            assert torch.equal(outs[e]["iut0"], r["iut0"]), e
+        assert torch.equal(outs[e]["iut0"], r["iut0"]), e
     pipe.close()
 
 
