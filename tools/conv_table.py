@@ -104,7 +104,7 @@ def main(path, pmc_path=None):
                      f"{ms * 1e3:.1f} | {fx / ms / 1e9 / (roof / 1e12):.2f} | {gms * 1e3:.1f} | "
                      f"{fx / gms / 1e9:.1f} | {fx / gms / 1e9 / (roof / 1e12):.2f} | {sub['wino_gemm'][2] / 1e6:.1f} | "
                      f"{sub['wino_in'][3] * 1e3:.1f} | {sub['wino_out'][3] * 1e3:.1f} | {tby / 1e6:.1f} | "
-                     f"{tby / tms / 1e9:.0f} | {(sub['wino_in'][2] + sub['wino_gemm'][2] + sub['wino_out'][2]) / 1e6:.1f} |")
+                     f"{tby / tms / 1e6:.0f} | {(sub['wino_in'][2] + sub['wino_gemm'][2] + sub['wino_out'][2]) / 1e6:.1f} |")
     if wrows:
         out += ["", "Winograd forms on their executed work (the GEMMs' FLOPs; the transforms' and GEMMs' algorithmic bytes):", "",
                 "| # | conv | direct GFLOP | executed GFLOP | bracket us | frac executed (bracket) | GEMM us | GEMM TF/s "
