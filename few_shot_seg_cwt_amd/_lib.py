@@ -123,6 +123,7 @@ SIGNATURES = {
                                 _I, _I, _P]),
     "cwt_debug_census": (_I, [_P, _I, _P, _P]),
     "cwt_debug_tail_stamps": (_I, [_P, _P, _I64, _P]),
+    "cwt_debug_occupy": (_I, [_P, _I, _I, _P]),
     "cwt_debug_pretrain_op": (_I, [_P, _I, C.POINTER(_P), C.POINTER(_I64), C.POINTER(_F), _P]),
     "cwt_debug_adapt_stamps": (_I, [_P, _P, _I64, C.POINTER(_I64)]),
     "cwt_ctx_set_adapt_units": (_I, [_P, _I]),

@@ -2853,6 +2853,13 @@ int cwt_debug_cp4d_layer(cwt_ctx* ctx, const float* x, int B, int hA, int wA, in
   return launch_cp4d_layer_variant(x, B, hA, wA, hB, wB, cin, cout, Wa, ba, Wb, bb, y, variant, (hipStream_t)stream);
 }
 
+int cwt_debug_occupy(cwt_ctx* ctx, int nwg, int us, void* stream) {
+  if (!ctx) return fail(CWT_EARG, "ctx is NULL");
+  CWT_CHECK(nwg >= 1 && nwg <= 256 && us >= 1 && us <= 100000, "occupy: 1 <= nwg <= 256, 1 <= us <= 100000");
+  CWT_HIP(hipSetDevice(ctx->device));
+  return launch_occupy(nwg, us, (hipStream_t)stream);
+}
+
 int cwt_debug_tail_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t max_count, int64_t* count) {
   if (!ctx || !count) return fail(CWT_EARG, "null argument");
   CWT_HIP(hipSetDevice(ctx->device));

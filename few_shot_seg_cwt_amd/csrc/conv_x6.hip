@@ -41,6 +41,26 @@ int launch_split_w3(const float* w, long R, int K, __bf16* ws, __bf16* wl, hipSt
   return 0;
 }
 
+// Timing study (cwt_debug_occupy): each workgroup holds a whole CU -- 1024 threads and all 160 KB of
+// its LDS -- and sleeps on the 100 MHz realtime clock for `ticks`, so a conv timed meanwhile on
+// another stream gets the CUs the pipeline's resident inner loop leaves it.  Bounded by `ticks`.
+__global__ __launch_bounds__(1024) void occupy_kernel(long ticks) {
+  extern __shared__ char occ_lds[];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) occ_lds[0] = 0;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+int launch_occupy(int nwg, int us, hipStream_t st) {
+  constexpr int kLds = 160 * 1024;
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void*)occupy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+  if (attr != hipSuccess) return fail(CWT_ESTATE, "occupy: 160 KB of dynamic LDS refused");
+  hipLaunchKernelGGL(occupy_kernel, dim3(nwg), dim3(1024), kLds, st, (long)us * 100);
+  CWT_LAUNCH_CHECK();
+  return 0;
+}
+
 // Tile and wave-layout forms (plan.var).  The main loop's VALU is the A split (~44 instructions per
 // 8 fp32 values, per A fragment per K-tile) against 6 MFMAs per fragment pair, so a wave that holds
 // more output columns (larger WN) amortises each split over more MFMAs: var 3 lays the waves out

@@ -146,6 +146,7 @@ int launch_conv_x3s(ConvSArgs a, const ConvPlan& p, int stage, float* part_ws, s
                     hipStream_t st, int prec = 3);
 int launch_split_act(const float* x, long P, int C, int ld, __bf16* out, hipStream_t st);
 int launch_split_w3(const float* w, long R, int K, __bf16* ws, __bf16* wl, hipStream_t st);
+int launch_occupy(int nwg, int us, hipStream_t st);  // timing study (cwt_debug_occupy)
 int launch_unsplit_act(const __bf16* s, long P, int C, float* out, int ld, hipStream_t st);
 
 // inner loop (adapt.hip): cache of instantiated graphs of the 200-step launch sequence

@@ -94,6 +94,12 @@ int cwt_debug_cp4d_layer(cwt_ctx* ctx, const float* x, int B, int hA, int wA, in
  * the last stamped launch's values to host_out; *count = G * 16 (0 if none). */
 int cwt_debug_tail_stamps(cwt_ctx* ctx, unsigned long long* host_out, int64_t max_count, int64_t* count);
 
+/* Timing-study hook: hold nwg CUs for about `us` microseconds (nwg workgroups of 1024 threads, each
+ * taking a whole CU's LDS, spinning on the realtime clock with s_sleep, bounded), so a kernel timed
+ * on another stream meanwhile sees the CUs the pipeline's resident inner loop leaves it.  nwg <= 256,
+ * us <= 100000. */
+int cwt_debug_occupy(cwt_ctx* ctx, int nwg, int us, void* stream);
+
 /* Timing-study hook of the inner loop: with CWT_ADAPT_DBG=32 in the environment, the inner
  * loop runs a separately compiled instantiation that records clock stamps per step and
  * workgroup (persistent loop: tools/persist_stamps.py; per-step launches with

@@ -62,15 +62,41 @@ def shapes(layers, S, N):
 TILES = [(256, 256), (256, 128), (128, 256), (128, 128), (128, 64), (64, 128), (64, 64)]
 
 
+OCCUPY = 0   # --occupy: CUs held by cwt_debug_occupy on a side stream while each plan is timed
+_SIDE = []   # that side stream, created once (a new stream per timing can land on the timed stream's
+             # hardware queue, which serialises the blocker before the timed calls)
+
+
 def timed(fn, reps):
     fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if OCCUPY:
+        # the pipeline's condition: the resident inner loop holds OCCUPY whole CUs (its 133 KB of LDS
+        # leave no room for a conv workgroup); a blocker holds them for longer than the timed calls
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        us = int(min(100000, e0.elapsed_time(e1) * 1e3 * reps * 10 + 3000))
+        if not _SIDE:
+            _SIDE.append(torch.cuda.Stream())
+        side = _SIDE[0]
+        eb = torch.cuda.Event(enable_timing=True)
+        _lib.check(_lib.lib().cwt_debug_occupy(_lib.ctx(0), OCCUPY, us, side.cuda_stream))
+        eb.record(side)
+        # ~1 ms on this stream: the blocker's workgroups land, and every timed call is queued before
+        # the first one runs (the timing is the GPU's, not the host's submission rate)
+        torch.cuda._sleep(2000000)
     e0.record()
     for _ in range(reps):
         fn()
     e1.record()
     torch.cuda.synchronize()
+    if OCCUPY and e0.elapsed_time(eb) <= e0.elapsed_time(e1):
+        print(f"  (blocker ended before the timed calls: {e0.elapsed_time(eb):.3f} vs {e0.elapsed_time(e1):.3f} ms; "
+              "plan not counted)", flush=True)
+        return float("inf")
     return e0.elapsed_time(e1) / reps * 1e3
 
 
@@ -193,7 +219,11 @@ def main():
     ap.add_argument("--vars", default="0,1,2,4", help="main-loop variants (0 base, 1 prefetch, 2 prefetch 8 waves, 4 128x128 two per CU; 8-15 timing "
                          "studies; x6: 3 / 5 WN = 128 layouts)")
     ap.add_argument("--only", default="", help="comma list of shape names (default: all)")
+    ap.add_argument("--occupy", type=int, default=0,
+                    help="time every plan while this many CUs are held (the pipeline's resident inner loop: 59)")
     args = ap.parse_args()
+    global OCCUPY
+    OCCUPY = args.occupy
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     res_all = []
     for cfg in args.configs.split(","):
