@@ -558,13 +558,21 @@ __device__ __forceinline__ void episode_tail_body(const TailArgs& a, const int g
         const int64_t tg = a.target[(long)b * npix + i];
         if (tg == 255) continue;
         const int pred = (l1 > l0) ? 1 : 0, pred0 = (k1 > k0) ? 1 : 0;  // torch.argmax: first index on ties
-        c[2 + pred]++;
-        c[6 + 2 + pred0]++;
+        // every counter by a constant index (a dynamic index would put c[] in scratch, which the
+        // compiler then promotes to 48 KB of LDS per 1024-thread workgroup)
+        c[2] += pred == 0;
+        c[3] += pred == 1;
+        c[8] += pred0 == 0;
+        c[9] += pred0 == 1;
         if (tg == 0 || tg == 1) {
-          c[4 + (int)tg]++;
-          c[6 + 4 + (int)tg]++;
-          if (pred == tg) c[pred]++;
-          if (pred0 == tg) c[6 + pred0]++;
+          c[4] += tg == 0;
+          c[5] += tg == 1;
+          c[10] += tg == 0;
+          c[11] += tg == 1;
+          c[0] += pred == tg && pred == 0;
+          c[1] += pred == tg && pred == 1;
+          c[6] += pred0 == tg && pred0 == 0;
+          c[7] += pred0 == tg && pred0 == 1;
           const float m = fmaxf(l0, l1);
           const float lse = m + logf(expf(l0 - m) + expf(l1 - m));
           nll += (double)(lse - (tg == 1 ? l1 : l0));
