@@ -646,9 +646,9 @@ static int enqueue_adapt_steps(const AdaptDevArgs* dargs, const float* f_ws, con
 //     each octet writes its two adjoint terms to slots of its own (no LDS atomics; the 16
 //     slots of a lo-res pixel are summed in fixed order).
 //   * dW[1] = sum_p g_p f_p: 32 FMAs per lane per unit, then a 64-lane butterfly
-//     (pa_butterfly) leaves lane 2c+{0,1} holding channel 32v+c; 32 no-return float atomics
-//     per wave into replica row (g % nrep) of the step's slot (they execute at the memory side,
-//     MI355X_MICROARCH.md Global float atomics).
+//     (pa_butterfly) leaves lane 2c+{0,1} holding channel 32v+c; 32 no-return 64-bit
+//     fixed-point integer atomics per wave into replica row (g % nrep) of the step's slot (round 6:
+//     exact and order-free, so the loop is deterministic; they execute at the memory side).
 //   * grid barrier: every wave waits for its atomics (vmcnt(0)), workgroup barrier, one lane
 //     adds 1 to arrival counter (g % nrep) (agent scope); wave 0 polls the counters with sc1
 //     loads until they sum to G*(s+1) (MI355X_MICROARCH.md hand-off table, counter row); every

@@ -289,7 +289,8 @@ class EpisodePipeline:
     runs while episode i's inner loop (one persistent launch on ~118 of the 256 CUs, the rest
     idle) and its CWT / classifier / metrics run.  Every episode executes exactly the kernels
     ``EpisodeEngine.run`` launches, with the same inputs, so its outputs are the same (up to the
-    order of the inner loop's fp32 atomic adds); only their placement in time changes.  Each
+    fp32 rounding of the inner loop's per-workgroup partial sums, which depends on how many units a
+    workgroup holds; the exchange itself is exact); only their placement in time changes.  Each
     episode is still processed alone (batch_size_val = 1): nothing is batched across episodes.
 
     Stream use: the extractor's workspaces are only touched by the extract stream, the inner

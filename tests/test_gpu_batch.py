@@ -1,7 +1,7 @@
 """Episodes in flight (cwt_inner_adapt_batch, EpisodeEngine.run_batch): E independent
 episodes sharing the backbone pass and the inner loop's step launches give each episode the
-result it gets alone.  Only the inner loop's fp32 atomic accumulation order differs between
-the two runs, so the bar is 1e-5 relative, and IoU counts may differ only on pixels whose
+result it gets alone.  Only the fp32 rounding of the inner loop's per-workgroup partial sums
+differs between the two runs (their workgroup geometries differ), so the bar is 1e-5 relative, and IoU counts may differ only on pixels whose
 logit margin is at that rounding level."""
 import numpy as np
 import pytest
