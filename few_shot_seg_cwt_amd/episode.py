@@ -320,9 +320,11 @@ class EpisodePipeline:
         self.s_ext = [torch.cuda.Stream() for _ in range(max(1, int(extract_streams)))]
         self.c_ext = [None] + [_lib.new_ctx() for _ in range(len(self.s_ext) - 1)]
         self.s_extract = self.s_ext[0]
-        # (a high-priority adapt stream measured no different in round 2; CWT_PIPE_ADAPT_PRIO=1
-        # re-measures it with the one-launch tail, whose workgroups wait for CUs beside the passes)
-        prio = -1 if os.environ.get("CWT_PIPE_ADAPT_PRIO", "0") == "1" else 0
+        # the adapt stream at high priority: its loop's grid is dispatched ahead of the extractor
+        # pass's pending workgroups.  Rounds 2 and 5 measured no difference; round 6 (the fused
+        # tail) 5 of 6 interleaved pairs higher, +0.9 % on average (profiles/r6/studies/adapt_prio/).
+        # CWT_PIPE_ADAPT_PRIO=0 turns it off (A/B)
+        prio = -1 if os.environ.get("CWT_PIPE_ADAPT_PRIO", "1") == "1" else 0
         self.s_adapt = torch.cuda.Stream(priority=prio)
         # the adapt stream's own context: its persistent inner loop holds two units per
         # workgroup (59 instead of 118 CUs at 1-shot 473^2), leaving the rest to the extractor
